@@ -1,0 +1,247 @@
+// bvh8.cpp -- host BVH8 builder: binned-SAH BVH2, greedy collapse to 8-wide nodes
+// (expand the child with the largest surface area), octant-ordered child slots
+// (so that a ray visits slot k ^ (octant ^ 7) first, front to back), conservative
+// 8-bit quantisation of child boxes.  See bvh8.h for the node format.
+#include "bvh8.h"
+
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <cstring>
+
+namespace mpt {
+namespace {
+
+struct AABB {
+    float lo[3], hi[3];
+    AABB() { for (int i = 0; i < 3; i++) { lo[i] = FLT_MAX; hi[i] = -FLT_MAX; } }
+    void grow(const AABB& b) { for (int i = 0; i < 3; i++) { lo[i] = std::min(lo[i], b.lo[i]); hi[i] = std::max(hi[i], b.hi[i]); } }
+    void grow(const float* p) { for (int i = 0; i < 3; i++) { lo[i] = std::min(lo[i], p[i]); hi[i] = std::max(hi[i], p[i]); } }
+    float area() const {
+        float d0 = std::max(0.0f, hi[0] - lo[0]), d1 = std::max(0.0f, hi[1] - lo[1]), d2 = std::max(0.0f, hi[2] - lo[2]);
+        return 2.0f * (d0 * d1 + d1 * d2 + d2 * d0);
+    }
+    bool valid() const { return lo[0] <= hi[0]; }
+};
+
+struct N2 { AABB box; int left = -1, right = -1, first = 0, count = 0; };
+
+struct Builder {
+    const float* v;
+    const int32_t* idx;
+    int n;
+    int max_leaf;
+    std::vector<AABB> tbox;
+    std::vector<float> cen;
+    std::vector<int> order;
+    std::vector<N2> nodes;
+
+    int build2(int begin, int end, int depth) {
+        int id = (int)nodes.size();
+        nodes.emplace_back();
+        AABB b, cb;
+        for (int i = begin; i < end; i++) { b.grow(tbox[order[i]]); cb.grow(&cen[3 * (size_t)order[i]]); }
+        nodes[id].box = b;
+        int cnt = end - begin;
+        if (cnt <= max_leaf) { nodes[id].first = begin; nodes[id].count = cnt; return id; }
+        const int NB = 32;
+        int best_axis = -1, best_split = 0;
+        float best_cost = FLT_MAX;
+        // past depth 40 only balanced splits, so the tree depth stays below 64 (traversal stack)
+        for (int ax = 0; ax < 3 && depth < 40; ax++) {
+            float ext = cb.hi[ax] - cb.lo[ax];
+            if (!(ext > 0.0f)) continue;
+            AABB bb[NB];
+            int bc[NB] = {0};
+            float k = NB / ext;
+            for (int i = begin; i < end; i++) {
+                int t = order[i];
+                int bi = std::min(NB - 1, (int)((cen[3 * (size_t)t + ax] - cb.lo[ax]) * k));
+                bb[bi].grow(tbox[t]);
+                bc[bi]++;
+            }
+            float la[NB];
+            int lc[NB];
+            AABB acc;
+            int ac = 0;
+            for (int i = 0; i < NB; i++) { acc.grow(bb[i]); ac += bc[i]; la[i] = acc.valid() ? acc.area() : 0.0f; lc[i] = ac; }
+            acc = AABB();
+            ac = 0;
+            for (int i = NB - 1; i > 0; i--) {
+                acc.grow(bb[i]);
+                ac += bc[i];
+                if (lc[i - 1] == 0 || ac == 0) continue;
+                float cost = la[i - 1] * lc[i - 1] + acc.area() * ac;
+                if (cost < best_cost) { best_cost = cost; best_axis = ax; best_split = i; }
+            }
+        }
+        int mid;
+        if (best_axis >= 0) {
+            float ext = cb.hi[best_axis] - cb.lo[best_axis];
+            float k = NB / ext;
+            int* m = std::partition(order.data() + begin, order.data() + end, [&](int t) {
+                return std::min(NB - 1, (int)((cen[3 * (size_t)t + best_axis] - cb.lo[best_axis]) * k)) < best_split;
+            });
+            mid = (int)(m - order.data());
+        } else {
+            mid = (begin + end) / 2;   // all centroids equal: split by count
+        }
+        if (mid == begin || mid == end) mid = (begin + end) / 2;
+        int l = build2(begin, mid, depth + 1);
+        int r = build2(mid, end, depth + 1);
+        nodes[id].left = l;
+        nodes[id].right = r;
+        return id;
+    }
+};
+
+inline uint8_t quant_exp(float ext) {
+    // smallest e with 255 * 2^e >= ext, clamped to normal floats
+    int e = -126;
+    if (ext > 0.0f) {
+        e = (int)std::ceil(std::log2((double)ext / 255.0));
+        while (std::ldexp(255.0, e) < (double)ext) e++;
+        e = std::max(-126, std::min(127, e));
+    }
+    return (uint8_t)(e + 127);
+}
+
+}  // namespace
+
+void build_bvh8(const float* vertices, const int32_t* indices, int32_t num_triangles, BVH8& out, int max_leaf) {
+    out.nodes.clear();
+    out.tris.clear();
+    if (num_triangles <= 0) return;
+    max_leaf = std::max(1, std::min(4, max_leaf));
+    Builder b;
+    b.v = vertices;
+    b.idx = indices;
+    b.n = num_triangles;
+    b.max_leaf = max_leaf;
+    b.tbox.resize(num_triangles);
+    b.cen.resize(3 * (size_t)num_triangles);
+    b.order.resize(num_triangles);
+    for (int t = 0; t < num_triangles; t++) {
+        for (int k = 0; k < 3; k++) b.tbox[t].grow(vertices + 3 * (size_t)indices[3 * (size_t)t + k]);
+        for (int i = 0; i < 3; i++) b.cen[3 * (size_t)t + i] = 0.5f * (b.tbox[t].lo[i] + b.tbox[t].hi[i]);
+        b.order[t] = t;
+    }
+    b.nodes.reserve(2 * (size_t)num_triangles);
+    int root = b.build2(0, num_triangles, 0);
+
+    // BFS over BVH8 nodes; each entry names the BVH2 node it collapses
+    struct Item { int n2; int n8; int depth; };
+    std::vector<Item> queue;
+    out.nodes.emplace_back();
+    queue.push_back({root, 0, 1});
+    size_t qi = 0;
+    int max_depth = 1;
+    while (qi < queue.size()) {
+        Item it = queue[qi++];
+        max_depth = std::max(max_depth, it.depth);
+        // gather up to 8 children
+        std::vector<int> ch;
+        const N2& r2 = b.nodes[it.n2];
+        if (r2.count > 0) ch.push_back(it.n2);
+        else { ch.push_back(r2.left); ch.push_back(r2.right); }
+        while (ch.size() < 8) {
+            int best = -1;
+            float ba = -1.0f;
+            for (int i = 0; i < (int)ch.size(); i++) {
+                const N2& c = b.nodes[ch[i]];
+                if (c.count == 0 && c.box.area() > ba) { ba = c.box.area(); best = i; }
+            }
+            if (best < 0) break;
+            int nb = ch[best];
+            ch[best] = b.nodes[nb].left;
+            ch.push_back(b.nodes[nb].right);
+        }
+        // node box and slot assignment (octant heuristic)
+        AABB nb;
+        for (int c : ch) nb.grow(b.nodes[c].box);
+        float pc[3] = {0.5f * (nb.lo[0] + nb.hi[0]), 0.5f * (nb.lo[1] + nb.hi[1]), 0.5f * (nb.lo[2] + nb.hi[2])};
+        int slot_of[8];
+        int child_in_slot[8];
+        for (int s = 0; s < 8; s++) child_in_slot[s] = -1;
+        bool used[8] = {false};
+        for (int round = 0; round < (int)ch.size(); round++) {
+            float best = FLT_MAX;
+            int bi = -1, bs = -1;
+            for (int i = 0; i < (int)ch.size(); i++) {
+                if (used[i]) continue;
+                const AABB& cb = b.nodes[ch[i]].box;
+                float v[3];
+                for (int a = 0; a < 3; a++) v[a] = 0.5f * (cb.lo[a] + cb.hi[a]) - pc[a];
+                for (int s = 0; s < 8; s++) {
+                    if (child_in_slot[s] >= 0) continue;
+                    float cost = -((s & 1 ? v[0] : -v[0]) + (s & 2 ? v[1] : -v[1]) + (s & 4 ? v[2] : -v[2]));
+                    if (cost < best) { best = cost; bi = i; bs = s; }
+                }
+            }
+            used[bi] = true;
+            child_in_slot[bs] = bi;
+            slot_of[bi] = bs;
+        }
+        (void)slot_of;
+        Node8 nd;
+        std::memset(&nd, 0, sizeof(nd));
+        nd.px = nb.lo[0];
+        nd.py = nb.lo[1];
+        nd.pz = nb.lo[2];
+        uint8_t e[3];
+        for (int a = 0; a < 3; a++) e[a] = quant_exp(nb.hi[a] - nb.lo[a]);
+        nd.ex = e[0];
+        nd.ey = e[1];
+        nd.ez = e[2];
+        nd.child_base = (uint32_t)out.nodes.size();
+        nd.tri_base = (uint32_t)out.tris.size();
+        int internal_rank = 0;
+        double p[3] = {nd.px, nd.py, nd.pz};
+        for (int s = 0; s < 8; s++) {
+            int ci = child_in_slot[s];
+            if (ci < 0) continue;
+            const N2& c = b.nodes[ch[ci]];
+            uint8_t qlo[3], qhi[3];
+            for (int a = 0; a < 3; a++) {
+                double sc = std::ldexp(1.0, (int)e[a] - 127);
+                double lo = std::floor(((double)c.box.lo[a] - p[a]) / sc);
+                double hi = std::ceil(((double)c.box.hi[a] - p[a]) / sc);
+                while (lo > 0 && p[a] + lo * sc > (double)c.box.lo[a]) lo -= 1;
+                while (hi < 255 && p[a] + hi * sc < (double)c.box.hi[a]) hi += 1;
+                lo = std::max(0.0, std::min(255.0, lo));
+                hi = std::max(0.0, std::min(255.0, hi));
+                qlo[a] = (uint8_t)lo;
+                qhi[a] = (uint8_t)hi;
+            }
+            nd.qlox[s] = qlo[0]; nd.qloy[s] = qlo[1]; nd.qloz[s] = qlo[2];
+            nd.qhix[s] = qhi[0]; nd.qhiy[s] = qhi[1]; nd.qhiz[s] = qhi[2];
+            if (c.count == 0) {
+                nd.imask |= (uint8_t)(1u << s);
+                nd.meta[s] = (uint8_t)internal_rank++;
+                out.nodes.emplace_back();
+                queue.push_back({ch[ci], (int)out.nodes.size() - 1, it.depth + 1});
+            } else {
+                int off = (int)out.tris.size() - (int)nd.tri_base;
+                nd.meta[s] = (uint8_t)((c.count << 5) | off);
+                for (int k = 0; k < c.count; k++) {
+                    int t = b.order[c.first + k];
+                    const float* A = vertices + 3 * (size_t)indices[3 * (size_t)t + 0];
+                    const float* B = vertices + 3 * (size_t)indices[3 * (size_t)t + 1];
+                    const float* C = vertices + 3 * (size_t)indices[3 * (size_t)t + 2];
+                    TriRec tr;
+                    std::memset(&tr, 0, sizeof(tr));
+                    tr.ax = A[0]; tr.ay = A[1]; tr.az = A[2];
+                    int32_t pb = t;
+                    std::memcpy(&tr.prim_bits, &pb, 4);
+                    tr.e1x = B[0] - A[0]; tr.e1y = B[1] - A[1]; tr.e1z = B[2] - A[2];
+                    tr.e2x = C[0] - A[0]; tr.e2y = C[1] - A[1]; tr.e2z = C[2] - A[2];
+                    out.tris.push_back(tr);
+                }
+            }
+        }
+        out.nodes[it.n8] = nd;
+    }
+    out.depth = max_depth;
+}
+
+}  // namespace mpt

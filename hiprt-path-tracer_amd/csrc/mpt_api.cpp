@@ -1,0 +1,628 @@
+// mpt_api.cpp -- the C ABI of libmpt (include/mpt.h).  Owns all device memory of a
+// context (one per GPU), builds the BVH8 on scene upload, stages per-frame settings
+// and launches the wavefront frame (mpt_kernels.hip).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <deque>
+#include <string>
+#include <vector>
+
+#include "bvh8.h"
+#include "mpt.h"
+#include "mpt_internal.h"
+
+using namespace mpt;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIPCHK(expr)                                                                                  \
+    do {                                                                                              \
+        hipError_t e_ = (expr);                                                                       \
+        if (e_ != hipSuccess) return fail(MPT_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+template <typename T>
+struct DBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    void release() { if (p) (void)hipFree(p); p = nullptr; n = 0; }
+    hipError_t alloc(size_t count) {
+        if (count == n && p) return hipSuccess;
+        release();
+        if (count == 0) return hipSuccess;
+        hipError_t e = hipMalloc(&p, count * sizeof(T));
+        if (e == hipSuccess) n = count;
+        return e;
+    }
+    hipError_t upload(const T* h, size_t count, hipStream_t s) {
+        hipError_t e = alloc(count);
+        if (e != hipSuccess || count == 0) return e;
+        return hipMemcpyAsync(p, h, count * sizeof(T), hipMemcpyHostToDevice, s);
+    }
+};
+
+constexpr int FRAME_RING = 64;
+constexpr int EV_POOL = 256;
+constexpr int SPILL_WORDS = 2 * TRAV_SPILL_DEPTH;
+constexpr int MAX_STACK = TRAV_LDS_STACK + TRAV_SPILL_DEPTH;
+
+}  // namespace
+
+struct MptContext {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    int num_cus = 256;
+    int grid = 1024;
+    // scene
+    bool has_scene = false;
+    BVH8 bvh;
+    DBuf<Node8> nodes;
+    DBuf<TriRec> tris;
+    DBuf<int32_t> idx, mat_idx, mat_prio, emissive, tex_dims;
+    DBuf<float> pos, nrm, uv;
+    DBuf<uint8_t> has_n, tex;
+    DBuf<uint64_t> tex_off;
+    DBuf<MptMaterial> mats;
+    std::vector<MptMaterial> h_mats;
+    int n_tex = 0;
+    // luts / envmap
+    DBuf<float> lut_conductor, lut_glossy, lut_glass, lut_glass_inv, lut_thin, lut_sheen;
+    DBuf<float4> env;
+    DBuf<float> alias_p;
+    DBuf<int32_t> alias_i;
+    int env_w = 0, env_h = 0;
+    float env_sum = 0.0f;
+    // paths
+    int res_x = 0, res_y = 0, band_h = 1, band_i = 0, band_c = 1, n_slots = 0;
+    DBuf<float4> ray_o, ray_d, hit, thr, col, alb, nrmv, nq_o, nq_d, nhit;
+    DBuf<uint8_t> hit_inside, occ;
+    DBuf<uint32_t> rng, spill;
+    DBuf<uint4> vsA, vsB;
+    DBuf<int32_t> q0, q1, counters, nq_tgt, fetch_raw;
+    DBuf<NeeRec> nee;
+    DBuf<float> fb_color, fb_albedo, fb_normal;
+    DBuf<uint64_t> stats;
+    // frames
+    MptFrame* h_frames = nullptr;   // pinned ring
+    MptFrame* d_frames = nullptr;
+    int frame_slot = 0;
+    // stats
+    bool timing = false;
+    bool instrumented = false;
+    hipEvent_t ev[EV_POOL];
+    hipEvent_t ev_frame[2];
+    int ev_used = 0;
+    uint32_t last_launches = 0;
+    // raw traces
+    DBuf<float4> raw_o, raw_d, raw_hit;
+    DBuf<uint8_t> raw_occ;
+};
+
+namespace {
+
+DevScene dev_scene(MptContext* c) {
+    DevScene S{};
+    S.nodes = c->nodes.p;
+    S.tris = c->tris.p;
+    S.idx = c->idx.p;
+    S.pos = c->pos.p;
+    S.nrm = c->nrm.p;
+    S.has_n = c->has_n.p;
+    S.uv = c->uv.p;
+    S.mat_idx = c->mat_idx.p;
+    S.mats = c->mats.p;
+    S.mat_prio = c->mat_prio.p;
+    S.emissive = c->emissive.p;
+    S.n_emissive = (int32_t)c->emissive.n;
+    S.n_tris = (int32_t)c->mat_idx.n;
+    S.tex = c->tex.p;
+    S.tex_off = c->tex_off.p;
+    S.tex_dims = c->tex_dims.p;
+    S.n_tex = c->n_tex;
+    S.lut_conductor = c->lut_conductor.p;
+    S.lut_glossy = c->lut_glossy.p;
+    S.lut_glass = c->lut_glass.p;
+    S.lut_glass_inv = c->lut_glass_inv.p;
+    S.lut_thin_glass = c->lut_thin.p;
+    S.lut_sheen = c->lut_sheen.p;
+    S.env = c->env.p;
+    S.alias_p = c->alias_p.p;
+    S.alias_i = c->alias_i.p;
+    S.env_w = c->env_w;
+    S.env_h = c->env_h;
+    S.env_sum = c->env_sum;
+    return S;
+}
+
+DevPaths dev_paths(MptContext* c) {
+    DevPaths P{};
+    P.n = c->n_slots;
+    P.res_x = c->res_x;
+    P.ray_o = c->ray_o.p;
+    P.ray_d = c->ray_d.p;
+    P.hit = c->hit.p;
+    P.hit_inside = c->hit_inside.p;
+    P.rng = c->rng.p;
+    P.thr = c->thr.p;
+    P.col = c->col.p;
+    P.vsA = c->vsA.p;
+    P.vsB = c->vsB.p;
+    P.alb = c->alb.p;
+    P.nrm = c->nrmv.p;
+    P.q0 = c->q0.p;
+    P.q1 = c->q1.p;
+    P.counters = c->counters.p;
+    P.nee = c->nee.p;
+    P.nq_o = c->nq_o.p;
+    P.nq_d = c->nq_d.p;
+    P.nq_tgt = c->nq_tgt.p;
+    P.occ = c->occ.p;
+    P.nhit = c->nhit.p;
+    P.fb_color = c->fb_color.p;
+    P.fb_albedo = c->fb_albedo.p;
+    P.fb_normal = c->fb_normal.p;
+    P.stack_spill = c->spill.p;
+    P.stats = c->stats.p;
+    return P;
+}
+
+int rows_of(int res_y, int bh, int bi, int bc) {
+    int r = 0;
+    for (int y = 0; y < res_y; y++)
+        if ((y / bh) % bc == bi) r++;
+    return r;
+}
+
+int ensure_paths(MptContext* c, int rx, int ry, int bh, int bi, int bc) {
+    int rows = rows_of(ry, bh, bi, bc);
+    int n = rows * rx;
+    bool same = c->res_x == rx && c->res_y == ry && c->band_h == bh && c->band_i == bi && c->band_c == bc && c->n_slots == n && c->ray_o.p;
+    if (same) return MPT_OK;
+    c->res_x = rx; c->res_y = ry; c->band_h = bh; c->band_i = bi; c->band_c = bc; c->n_slots = n;
+    size_t N = (size_t)std::max(n, 1);
+    HIPCHK(c->ray_o.alloc(N)); HIPCHK(c->ray_d.alloc(N)); HIPCHK(c->hit.alloc(N)); HIPCHK(c->hit_inside.alloc(N));
+    HIPCHK(c->rng.alloc(N)); HIPCHK(c->thr.alloc(N)); HIPCHK(c->col.alloc(N)); HIPCHK(c->vsA.alloc(N)); HIPCHK(c->vsB.alloc(N));
+    HIPCHK(c->alb.alloc(N)); HIPCHK(c->nrmv.alloc(N)); HIPCHK(c->q0.alloc(N)); HIPCHK(c->q1.alloc(N));
+    HIPCHK(c->nee.alloc(N)); HIPCHK(c->nq_o.alloc(4 * N)); HIPCHK(c->nq_d.alloc(4 * N)); HIPCHK(c->nq_tgt.alloc(4 * N));
+    HIPCHK(c->occ.alloc(3 * N)); HIPCHK(c->nhit.alloc(N));
+    HIPCHK(c->fb_color.alloc(3 * N)); HIPCHK(c->fb_albedo.alloc(3 * N)); HIPCHK(c->fb_normal.alloc(3 * N));
+    HIPCHK(hipMemsetAsync(c->fb_color.p, 0, 3 * N * sizeof(float), c->stream));
+    HIPCHK(hipMemsetAsync(c->fb_albedo.p, 0, 3 * N * sizeof(float), c->stream));
+    HIPCHK(hipMemsetAsync(c->fb_normal.p, 0, 3 * N * sizeof(float), c->stream));
+    return MPT_OK;
+}
+
+int validate_frame(const MptFrame* f) {
+    const MptRenderSettings& rs = f->render_settings;
+    if (f->res_x <= 0 || f->res_y <= 0) return fail(MPT_ERR_INVALID_ARGUMENT, "resolution must be positive");
+    if (f->band_height <= 0 || f->band_count <= 0 || f->band_index < 0 || f->band_index >= f->band_count)
+        return fail(MPT_ERR_INVALID_ARGUMENT, "invalid row partition");
+    if (rs.nb_bounces < 0 || rs.nb_bounces > 64) return fail(MPT_ERR_INVALID_ARGUMENT, "nb_bounces out of range");
+    if (rs.accumulate && (rs.enable_adaptive_sampling || rs.stop_pixel_noise_threshold > 0.0f))
+        return fail(MPT_ERR_UNSUPPORTED, "adaptive sampling / stop-noise threshold not implemented yet (SURVEY §8f #3)");
+    if (rs.wants_render_low_resolution && rs.allow_render_low_resolution && rs.accumulate)
+        return fail(MPT_ERR_UNSUPPORTED, "low-resolution interactive mode not implemented");
+    if (rs.do_alpha_testing)
+        return fail(MPT_ERR_UNSUPPORTED, "alpha testing not implemented yet (do_alpha_testing must be false)");
+    if (rs.number_of_light_samples != 1) return fail(MPT_ERR_UNSUPPORTED, "number_of_light_samples must be 1");
+    if (rs.ris_number_of_bsdf_candidates < 0 || rs.ris_number_of_bsdf_candidates > 1)
+        return fail(MPT_ERR_UNSUPPORTED, "ris_number_of_bsdf_candidates must be 0 or 1");
+    if (rs.ris_number_of_light_candidates < 0) return fail(MPT_ERR_INVALID_ARGUMENT, "negative RIS light candidates");
+    int lss = f->options.direct_light_sampling;
+    if (lss < 0 || lss > MPT_LSS_RESTIR_DI) return fail(MPT_ERR_INVALID_ARGUMENT, "bad direct_light_sampling");
+    if (lss == MPT_LSS_RESTIR_DI) return fail(MPT_ERR_UNSUPPORTED, "ReSTIR DI not implemented yet");
+    if (f->options.envmap_sampling == MPT_ESS_BINARY_SEARCH) return fail(MPT_ERR_UNSUPPORTED, "ESS_BINARY_SEARCH not implemented");
+    if (f->options.bsdf_override != MPT_BSDF_NONE && f->options.bsdf_override != MPT_BSDF_LAMBERTIAN)
+        return fail(MPT_ERR_UNSUPPORTED, "only BSDF_NONE (Principled) and BSDF_LAMBERTIAN are implemented");
+    if (f->options.ris_use_visibility) return fail(MPT_ERR_UNSUPPORTED, "RISUseVisiblityTargetFunction not implemented");
+    return MPT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* mpt_last_error(void) { return g_err.c_str(); }
+int mpt_version(void) { return 1; }
+
+int mpt_abi_sizes(int32_t* out, int n) {
+    int32_t s[6] = {(int32_t)sizeof(MptMaterial), (int32_t)sizeof(MptRenderSettings), (int32_t)sizeof(MptWorldSettings),
+                    (int32_t)sizeof(MptCamera), (int32_t)sizeof(MptFrame), (int32_t)sizeof(MptScene)};
+    for (int i = 0; i < n && i < 6; i++) out[i] = s[i];
+    return MPT_OK;
+}
+
+static_assert(sizeof(MptMaterial) == 332, "RendererMaterial mirror");
+static_assert(sizeof(MptRenderSettings) == 304, "HIPRTRenderSettings mirror");
+static_assert(sizeof(MptWorldSettings) == 200, "WorldSettings mirror");
+static_assert(sizeof(MptCamera) == 196, "HIPRTCamera mirror");
+
+int mpt_partition_rows(int32_t res_y, int32_t bh, int32_t bi, int32_t bc) {
+    if (bh <= 0 || bc <= 0) return 0;
+    return rows_of(res_y, bh, bi, bc);
+}
+
+int mpt_create(int device, void* hip_stream, MptContext** out) {
+    if (!out) return fail(MPT_ERR_INVALID_ARGUMENT, "out_ctx is NULL");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(MPT_ERR_HIP, "no HIP device available");
+    if (device < 0 || device >= ndev) return fail(MPT_ERR_INVALID_ARGUMENT, "device index out of range");
+    MptContext* c = new MptContext();
+    c->device = device;
+    HIPCHK(hipSetDevice(device));
+    hipDeviceProp_t prop;
+    HIPCHK(hipGetDeviceProperties(&prop, device));
+    c->num_cus = prop.multiProcessorCount;
+    c->grid = c->num_cus * 4;
+    if (hip_stream) c->stream = (hipStream_t)hip_stream;
+    else { HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)); c->own_stream = true; }
+    HIPCHK(hipHostMalloc((void**)&c->h_frames, sizeof(MptFrame) * FRAME_RING));
+    HIPCHK(hipMalloc((void**)&c->d_frames, sizeof(MptFrame) * FRAME_RING));
+    HIPCHK(c->counters.alloc(CTR_COUNT));
+    HIPCHK(hipMemsetAsync(c->counters.p, 0, CTR_COUNT * sizeof(int32_t), c->stream));
+    HIPCHK(c->fetch_raw.alloc(4));
+    HIPCHK(c->stats.alloc(4));
+    HIPCHK(hipMemsetAsync(c->stats.p, 0, 4 * sizeof(uint64_t), c->stream));
+    HIPCHK(c->spill.alloc((size_t)c->grid * TRAV_BLOCK * SPILL_WORDS));
+    for (int i = 0; i < EV_POOL; i++) HIPCHK(hipEventCreate(&c->ev[i]));
+    HIPCHK(hipEventCreate(&c->ev_frame[0]));
+    HIPCHK(hipEventCreate(&c->ev_frame[1]));
+    *out = c;
+    return MPT_OK;
+}
+
+int mpt_destroy(MptContext* c) {
+    if (!c) return MPT_OK;
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    for (int i = 0; i < EV_POOL; i++) (void)hipEventDestroy(c->ev[i]);
+    (void)hipEventDestroy(c->ev_frame[0]);
+    (void)hipEventDestroy(c->ev_frame[1]);
+    c->nodes.release(); c->tris.release(); c->idx.release(); c->mat_idx.release(); c->mat_prio.release();
+    c->emissive.release(); c->tex_dims.release(); c->pos.release(); c->nrm.release(); c->uv.release();
+    c->has_n.release(); c->tex.release(); c->tex_off.release(); c->mats.release();
+    c->lut_conductor.release(); c->lut_glossy.release(); c->lut_glass.release(); c->lut_glass_inv.release();
+    c->lut_thin.release(); c->lut_sheen.release(); c->env.release(); c->alias_p.release(); c->alias_i.release();
+    c->ray_o.release(); c->ray_d.release(); c->hit.release(); c->thr.release(); c->col.release(); c->alb.release();
+    c->nrmv.release(); c->nq_o.release(); c->nq_d.release(); c->nhit.release(); c->hit_inside.release(); c->occ.release();
+    c->rng.release(); c->spill.release(); c->vsA.release(); c->vsB.release(); c->q0.release(); c->q1.release();
+    c->counters.release(); c->nq_tgt.release(); c->fetch_raw.release(); c->nee.release(); c->fb_color.release();
+    c->fb_albedo.release(); c->fb_normal.release(); c->stats.release();
+    c->raw_o.release(); c->raw_d.release(); c->raw_hit.release(); c->raw_occ.release();
+    if (c->h_frames) (void)hipHostFree(c->h_frames);
+    if (c->d_frames) (void)hipFree(c->d_frames);
+    if (c->own_stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+    return MPT_OK;
+}
+
+int mpt_upload_scene(MptContext* c, const MptScene* s) {
+    if (!c || !s) return fail(MPT_ERR_INVALID_ARGUMENT, "NULL argument");
+    if (s->num_triangles <= 0 || s->num_vertices <= 0 || !s->triangle_indices || !s->vertices || !s->material_indices ||
+        !s->materials || s->num_materials <= 0)
+        return fail(MPT_ERR_INVALID_ARGUMENT, "scene has no geometry or materials");
+    for (int64_t i = 0; i < 3 * (int64_t)s->num_triangles; i++)
+        if (s->triangle_indices[i] < 0 || s->triangle_indices[i] >= s->num_vertices)
+            return fail(MPT_ERR_INVALID_ARGUMENT, "triangle index out of range");
+    for (int64_t i = 0; i < s->num_triangles; i++)
+        if (s->material_indices[i] < 0 || s->material_indices[i] >= s->num_materials)
+            return fail(MPT_ERR_INVALID_ARGUMENT, "material index out of range");
+    for (int i = 0; i < s->num_emissive_triangles; i++)
+        if (s->emissive_triangle_indices[i] < 0 || s->emissive_triangle_indices[i] >= s->num_triangles)
+            return fail(MPT_ERR_INVALID_ARGUMENT, "emissive triangle index out of range");
+    HIPCHK(hipSetDevice(c->device));
+    build_bvh8(s->vertices, s->triangle_indices, s->num_triangles, c->bvh, 3);
+    if (c->bvh.depth > MAX_STACK) return fail(MPT_ERR_UNSUPPORTED, "BVH8 deeper than the traversal stack");
+    hipStream_t st = c->stream;
+    HIPCHK(c->nodes.upload(c->bvh.nodes.data(), c->bvh.nodes.size(), st));
+    HIPCHK(c->tris.upload(c->bvh.tris.data(), c->bvh.tris.size(), st));
+    HIPCHK(c->idx.upload(s->triangle_indices, 3 * (size_t)s->num_triangles, st));
+    HIPCHK(c->pos.upload(s->vertices, 3 * (size_t)s->num_vertices, st));
+    std::vector<float> zeros3, zeros2;
+    std::vector<uint8_t> zerosb;
+    const float* nrm = s->vertex_normals;
+    if (!nrm) { zeros3.assign(3 * (size_t)s->num_vertices, 0.0f); nrm = zeros3.data(); }
+    const float* uv = s->texcoords;
+    if (!uv) { zeros2.assign(2 * (size_t)s->num_vertices, 0.0f); uv = zeros2.data(); }
+    const uint8_t* hn = s->has_vertex_normals;
+    if (!hn) { zerosb.assign((size_t)s->num_vertices, 0); hn = zerosb.data(); }
+    HIPCHK(c->nrm.upload(nrm, 3 * (size_t)s->num_vertices, st));
+    HIPCHK(c->uv.upload(uv, 2 * (size_t)s->num_vertices, st));
+    HIPCHK(c->has_n.upload(hn, (size_t)s->num_vertices, st));
+    HIPCHK(c->mat_idx.upload(s->material_indices, (size_t)s->num_triangles, st));
+    c->h_mats.assign(s->materials, s->materials + s->num_materials);
+    HIPCHK(c->mats.upload(c->h_mats.data(), c->h_mats.size(), st));
+    std::vector<int32_t> prio(s->num_materials);
+    for (int i = 0; i < s->num_materials; i++) prio[i] = s->materials[i].dielectric_priority;
+    HIPCHK(c->mat_prio.upload(prio.data(), prio.size(), st));
+    if (s->num_emissive_triangles > 0) HIPCHK(c->emissive.upload(s->emissive_triangle_indices, (size_t)s->num_emissive_triangles, st));
+    else { c->emissive.release(); }
+    c->n_tex = s->num_textures;
+    if (s->num_textures > 0) {
+        std::vector<uint64_t> off(s->num_textures);
+        uint64_t total = 0;
+        for (int i = 0; i < s->num_textures; i++) {
+            off[i] = total;
+            total += (uint64_t)s->texture_dims[2 * i] * s->texture_dims[2 * i + 1] * 4;
+        }
+        std::vector<uint8_t> all(total);
+        for (int i = 0; i < s->num_textures; i++)
+            std::memcpy(all.data() + off[i], s->texture_data[i], (size_t)s->texture_dims[2 * i] * s->texture_dims[2 * i + 1] * 4);
+        HIPCHK(c->tex.upload(all.data(), all.size(), st));
+        HIPCHK(c->tex_off.upload(off.data(), off.size(), st));
+        HIPCHK(c->tex_dims.upload(s->texture_dims, 2 * (size_t)s->num_textures, st));
+        HIPCHK(hipStreamSynchronize(st));
+    } else HIPCHK(hipStreamSynchronize(st));
+    c->has_scene = true;
+    return MPT_OK;
+}
+
+int mpt_update_materials(MptContext* c, const MptMaterial* m, int32_t count) {
+    if (!c || !m) return fail(MPT_ERR_INVALID_ARGUMENT, "NULL argument");
+    if (!c->has_scene) return fail(MPT_ERR_NO_SCENE, "no scene uploaded");
+    if (count != (int32_t)c->h_mats.size()) return fail(MPT_ERR_INVALID_ARGUMENT, "material count differs from the scene's");
+    HIPCHK(hipSetDevice(c->device));
+    c->h_mats.assign(m, m + count);
+    HIPCHK(c->mats.upload(c->h_mats.data(), c->h_mats.size(), c->stream));
+    std::vector<int32_t> prio(count);
+    for (int i = 0; i < count; i++) prio[i] = m[i].dielectric_priority;
+    HIPCHK(c->mat_prio.upload(prio.data(), prio.size(), c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return MPT_OK;
+}
+
+int mpt_build_alias_table(const float* rgba, int32_t w, int32_t h, float* out_p, int32_t* out_a, float* out_sum) {
+    // Image32Bit::compute_alias_table (Image/Image.cpp:579-659): Vose in double precision
+    if (!rgba || w <= 0 || h <= 0 || !out_p || !out_a) return fail(MPT_ERR_INVALID_ARGUMENT, "bad alias-table arguments");
+    size_t n = (size_t)w * h;
+    std::vector<double> L(n);
+    double sum = 0.0f;
+    const float wts[3] = {0.3086f, 0.6094f, 0.0820f};
+    for (int y = 0; y < h; y++)
+        for (int x = 0; x < w; x++) {
+            size_t i = (size_t)y * w + x;
+            float l = 0.0f;
+            for (int c = 0; c < 3; c++) l += rgba[i * 4 + c] * wts[c];
+            L[i] = (double)l;
+            sum += L[i];
+        }
+    if (out_sum) *out_sum = (float)sum;
+    for (double& v : L) { v /= sum; v *= (double)(w * h); }
+    std::deque<int> small, large;
+    for (size_t i = 0; i < n; i++) (L[i] < 1.0 ? small : large).push_back((int)i);
+    while (!small.empty() && !large.empty()) {
+        int s = small.front(), l = large.front();
+        small.pop_front();
+        large.pop_front();
+        out_p[s] = (float)L[s];
+        out_a[s] = l;
+        L[l] = (L[l] + L[s]) - 1.0;
+        (L[l] > 1.0 ? large : small).push_back(l);
+    }
+    while (!large.empty()) { out_p[large.front()] = 1.0f; large.pop_front(); }
+    while (!small.empty()) { out_p[small.front()] = 1.0f; small.pop_front(); }
+    return MPT_OK;
+}
+
+int mpt_set_envmap(MptContext* c, const float* rgba, int32_t w, int32_t h, const float* probas, const int32_t* alias, float lsum) {
+    if (!c) return fail(MPT_ERR_INVALID_ARGUMENT, "NULL context");
+    HIPCHK(hipSetDevice(c->device));
+    if (!rgba || w <= 0 || h <= 0) {
+        c->env.release(); c->alias_p.release(); c->alias_i.release();
+        c->env_w = c->env_h = 0;
+        return MPT_OK;
+    }
+    if (!probas || !alias) return fail(MPT_ERR_INVALID_ARGUMENT, "alias table required (ESS_ALIAS_TABLE)");
+    size_t n = (size_t)w * h;
+    for (size_t i = 0; i < n; i++)
+        if (alias[i] < 0 || (size_t)alias[i] >= n) {
+            // entries never reached by Vose's loop keep probability 1 and are never aliased
+            if (probas[i] < 1.0f) return fail(MPT_ERR_INVALID_ARGUMENT, "alias index out of range");
+        }
+    std::vector<int32_t> al(alias, alias + n);
+    for (size_t i = 0; i < n; i++) if (al[i] < 0 || (size_t)al[i] >= n) al[i] = (int32_t)i;
+    HIPCHK(c->env.upload(reinterpret_cast<const float4*>(rgba), n, c->stream));
+    HIPCHK(c->alias_p.upload(probas, n, c->stream));
+    HIPCHK(c->alias_i.upload(al.data(), n, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    c->env_w = w;
+    c->env_h = h;
+    c->env_sum = lsum;
+    return MPT_OK;
+}
+
+int mpt_set_luts(MptContext* c, const MptLuts* L) {
+    if (!c || !L || !L->ggx_conductor_ess || !L->glossy_dielectric_ess || !L->ggx_glass_ess || !L->ggx_glass_inverse_ess ||
+        !L->ggx_thin_glass_ess || !L->sheen_ltc_params)
+        return fail(MPT_ERR_INVALID_ARGUMENT, "all six LUTs are required");
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(c->lut_conductor.upload(L->ggx_conductor_ess, 128 * 128, c->stream));
+    HIPCHK(c->lut_glossy.upload(L->glossy_dielectric_ess, 128 * 64 * 128, c->stream));
+    HIPCHK(c->lut_glass.upload(L->ggx_glass_ess, 256 * 16 * 128, c->stream));
+    HIPCHK(c->lut_glass_inv.upload(L->ggx_glass_inverse_ess, 256 * 16 * 128, c->stream));
+    HIPCHK(c->lut_thin.upload(L->ggx_thin_glass_ess, 32 * 32 * 96, c->stream));
+    HIPCHK(c->lut_sheen.upload(L->sheen_ltc_params, 32 * 32 * 3, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return MPT_OK;
+}
+
+int mpt_resize(MptContext* c, int32_t w, int32_t h) {
+    if (!c || w <= 0 || h <= 0) return fail(MPT_ERR_INVALID_ARGUMENT, "bad resolution");
+    HIPCHK(hipSetDevice(c->device));
+    return ensure_paths(c, w, h, c->band_h, c->band_i, c->band_c);
+}
+
+int mpt_render_frame(MptContext* c, const MptFrame* f) {
+    if (!c || !f) return fail(MPT_ERR_INVALID_ARGUMENT, "NULL argument");
+    if (!c->has_scene) return fail(MPT_ERR_NO_SCENE, "no scene uploaded");
+    if (!c->lut_conductor.p && f->options.bsdf_override == MPT_BSDF_NONE) return fail(MPT_ERR_INVALID_ARGUMENT, "Principled BSDF needs mpt_set_luts");
+    int v = validate_frame(f);
+    if (v != MPT_OK) return v;
+    if (f->world_settings.ambient_light_type == MPT_AMBIENT_ENVMAP && !c->env.p)
+        return fail(MPT_ERR_INVALID_ARGUMENT, "ENVMAP ambient light without mpt_set_envmap");
+    HIPCHK(hipSetDevice(c->device));
+    int r = ensure_paths(c, f->res_x, f->res_y, f->band_height, f->band_index, f->band_count);
+    if (r != MPT_OK) return r;
+    // stage the frame constants through a pinned ring (the previous use of the slot
+    // has completed once 64 frames later are enqueued; synchronise defensively)
+    int slot = c->frame_slot;
+    c->frame_slot = (c->frame_slot + 1) % FRAME_RING;
+    if (slot == 0) HIPCHK(hipStreamSynchronize(c->stream));
+    c->h_frames[slot] = *f;
+    HIPCHK(hipMemcpyAsync(c->d_frames + slot, c->h_frames + slot, sizeof(MptFrame), hipMemcpyHostToDevice, c->stream));
+    LaunchCfg cfg{};
+    cfg.grid_persistent = c->grid;
+    cfg.stats = c->instrumented ? 1 : 0;
+    cfg.ev_pool = c->timing ? c->ev : nullptr;
+    cfg.ev_cap = EV_POOL;
+    cfg.ev_used = 0;
+    if (c->instrumented) HIPCHK(hipMemsetAsync(c->stats.p, 0, 4 * sizeof(uint64_t), c->stream));
+    if (c->timing) HIPCHK(hipEventRecord(c->ev_frame[0], c->stream));
+    hipError_t e = launch_frame(dev_scene(c), dev_paths(c), c->d_frames + slot, *f, cfg, c->stream);
+    if (e != hipSuccess) return fail(MPT_ERR_HIP, std::string("kernel launch: ") + hipGetErrorString(e));
+    if (c->timing) HIPCHK(hipEventRecord(c->ev_frame[1], c->stream));
+    c->ev_used = cfg.ev_used;
+    c->last_launches = cfg.launches;
+    return MPT_OK;
+}
+
+int mpt_synchronize(MptContext* c) {
+    if (!c) return fail(MPT_ERR_INVALID_ARGUMENT, "NULL context");
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return MPT_OK;
+}
+
+int mpt_query_done(MptContext* c, int* done) {
+    if (!c || !done) return fail(MPT_ERR_INVALID_ARGUMENT, "NULL argument");
+    hipError_t e = hipStreamQuery(c->stream);
+    if (e == hipSuccess) *done = 1;
+    else if (e == hipErrorNotReady) *done = 0;
+    else return fail(MPT_ERR_HIP, hipGetErrorString(e));
+    return MPT_OK;
+}
+
+int mpt_get_framebuffer(MptContext* c, int kind, float* dst, int dst_is_device) {
+    if (!c || !dst) return fail(MPT_ERR_INVALID_ARGUMENT, "NULL argument");
+    const float* src = kind == MPT_FB_COLOR ? c->fb_color.p : kind == MPT_FB_ALBEDO ? c->fb_albedo.p : kind == MPT_FB_NORMALS ? c->fb_normal.p : nullptr;
+    if (!src) return fail(MPT_ERR_INVALID_ARGUMENT, "bad framebuffer kind or no frame rendered");
+    HIPCHK(hipSetDevice(c->device));
+    size_t bytes = 3 * (size_t)c->n_slots * sizeof(float);
+    HIPCHK(hipMemcpyAsync(dst, src, bytes, dst_is_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return MPT_OK;
+}
+
+int mpt_enable_stats(MptContext* c, int enable, int instrumented) {
+    if (!c) return fail(MPT_ERR_INVALID_ARGUMENT, "NULL context");
+    c->timing = enable != 0;
+    c->instrumented = instrumented != 0;
+    return MPT_OK;
+}
+
+int mpt_get_stats(MptContext* c, MptStats* out) {
+    if (!c || !out) return fail(MPT_ERR_INVALID_ARGUMENT, "NULL argument");
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    std::memset(out, 0, sizeof(*out));
+    uint64_t s[4];
+    HIPCHK(hipMemcpy(s, c->stats.p, sizeof(s), hipMemcpyDeviceToHost));
+    out->rays_closest = s[0];
+    out->rays_any = s[1];
+    out->node_visits = s[2];
+    out->triangle_tests = s[3];
+    out->trace_launches = c->last_launches;
+    if (c->timing) {
+        float total = 0.0f;
+        for (int i = 0; i + 1 < c->ev_used; i += 2) {
+            float ms = 0.0f;
+            HIPCHK(hipEventElapsedTime(&ms, c->ev[i], c->ev[i + 1]));
+            total += ms;
+        }
+        out->trace_ms = total;
+        float fms = 0.0f;
+        HIPCHK(hipEventElapsedTime(&fms, c->ev_frame[0], c->ev_frame[1]));
+        out->frame_ms = fms;
+    }
+    return MPT_OK;
+}
+
+static int raw_trace(MptContext* c, const float* rays, const int32_t* last_hit, int32_t n, bool any, int32_t* prim,
+                     float* t, float* u, float* v, uint8_t* occ, int dev) {
+    if (!c || !rays || n < 0) return fail(MPT_ERR_INVALID_ARGUMENT, "bad ray-query arguments");
+    if (!c->has_scene) return fail(MPT_ERR_NO_SCENE, "no scene uploaded");
+    if (n == 0) return MPT_OK;
+    HIPCHK(hipSetDevice(c->device));
+    // pack (o, last_hit) / (d, tmax)
+    std::vector<float4> ho(n), hd(n);
+    std::vector<float> hr;
+    std::vector<int32_t> hl;
+    const float* R = rays;
+    const int32_t* LH = last_hit;
+    if (dev) {
+        hr.resize(8 * (size_t)n);
+        HIPCHK(hipMemcpy(hr.data(), rays, hr.size() * sizeof(float), hipMemcpyDeviceToHost));
+        R = hr.data();
+        if (last_hit) {
+            hl.resize(n);
+            HIPCHK(hipMemcpy(hl.data(), last_hit, n * sizeof(int32_t), hipMemcpyDeviceToHost));
+            LH = hl.data();
+        }
+    }
+    for (int i = 0; i < n; i++) {
+        int32_t lh = LH ? LH[i] : -1;
+        float lhf;
+        std::memcpy(&lhf, &lh, 4);
+        ho[i] = make_float4(R[8 * i], R[8 * i + 1], R[8 * i + 2], lhf);
+        hd[i] = make_float4(R[8 * i + 4], R[8 * i + 5], R[8 * i + 6], R[8 * i + 7]);
+    }
+    HIPCHK(c->raw_o.upload(ho.data(), n, c->stream));
+    HIPCHK(c->raw_d.upload(hd.data(), n, c->stream));
+    HIPCHK(c->raw_hit.alloc(n));
+    HIPCHK(c->raw_occ.alloc(n));
+    hipError_t e = launch_trace_raw(dev_scene(c), c->raw_o.p, c->raw_d.p, n, any, c->raw_hit.p, c->raw_occ.p, c->fetch_raw.p,
+                                    c->spill.p, c->grid, c->stream);
+    if (e != hipSuccess) return fail(MPT_ERR_HIP, std::string("trace launch: ") + hipGetErrorString(e));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (any) {
+        if (occ) HIPCHK(hipMemcpy(occ, c->raw_occ.p, n, dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost));
+        return MPT_OK;
+    }
+    std::vector<float4> hh(n);
+    HIPCHK(hipMemcpy(hh.data(), c->raw_hit.p, n * sizeof(float4), hipMemcpyDeviceToHost));
+    std::vector<int32_t> P(n);
+    std::vector<float> T(n), U(n), V(n);
+    for (int i = 0; i < n; i++) {
+        int32_t p;
+        std::memcpy(&p, &hh[i].w, 4);
+        P[i] = p; T[i] = hh[i].x; U[i] = hh[i].y; V[i] = hh[i].z;
+    }
+    hipMemcpyKind k = dev ? hipMemcpyHostToDevice : hipMemcpyHostToHost;
+    if (prim) HIPCHK(hipMemcpy(prim, P.data(), n * sizeof(int32_t), k));
+    if (t) HIPCHK(hipMemcpy(t, T.data(), n * sizeof(float), k));
+    if (u) HIPCHK(hipMemcpy(u, U.data(), n * sizeof(float), k));
+    if (v) HIPCHK(hipMemcpy(v, V.data(), n * sizeof(float), k));
+    return MPT_OK;
+}
+
+int mpt_trace_closest(MptContext* c, const float* rays, const int32_t* last_hit, int32_t n, int32_t* prim, float* t, float* u,
+                      float* v, int dev) {
+    return raw_trace(c, rays, last_hit, n, false, prim, t, u, v, nullptr, dev);
+}
+
+int mpt_trace_any(MptContext* c, const float* rays, const int32_t* last_hit, int32_t n, uint8_t* occ, int dev) {
+    return raw_trace(c, rays, last_hit, n, true, nullptr, nullptr, nullptr, nullptr, occ, dev);
+}
+
+}  // extern "C"

@@ -1,0 +1,131 @@
+// mpt_internal.h -- device-side data layout shared by the C ABI (mpt_api.cpp) and the
+// kernels (mpt_kernels.hip).  All buffers are SoA in HBM, indexed by "slot" = the
+// index of a pixel inside the context's row partition.
+#ifndef MPT_INTERNAL_H
+#define MPT_INTERNAL_H
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "bvh8.h"
+#include "mpt.h"
+
+namespace mpt {
+
+// traversal stack: LDS part + per-thread global spill (entries of 2 words)
+constexpr int TRAV_BLOCK = 256;
+constexpr int TRAV_LDS_STACK = 12;
+constexpr int TRAV_SPILL_DEPTH = 52;
+
+struct DevScene {
+    const Node8* nodes;
+    const TriRec* tris;
+    const int32_t* idx;          // 3 per triangle
+    const float* pos;            // 3 per vertex
+    const float* nrm;            // 3 per vertex
+    const uint8_t* has_n;
+    const float* uv;             // 2 per vertex
+    const int32_t* mat_idx;      // per triangle
+    const MptMaterial* mats;
+    const int32_t* mat_prio;     // dielectric_priority per material (nested-dielectric push)
+    const int32_t* emissive;
+    int32_t n_emissive;
+    int32_t n_tris;
+    const uint8_t* tex;          // all textures, RGBA8, concatenated
+    const uint64_t* tex_off;     // byte offset per texture
+    const int32_t* tex_dims;     // w, h per texture
+    int32_t n_tex;
+    // LUTs
+    const float* lut_conductor;
+    const float* lut_glossy;
+    const float* lut_glass;
+    const float* lut_glass_inv;
+    const float* lut_thin_glass;
+    const float* lut_sheen;
+    // envmap
+    const float4* env;
+    const float* alias_p;
+    const int32_t* alias_i;
+    int32_t env_w, env_h;
+    float env_sum;
+};
+
+// NEE record written by the shade stage and consumed by the resolve stage (128 B / slot)
+struct alignas(16) NeeRec {
+    float thr[3]; uint32_t flags;
+    float a[3]; float a_cos;        // light sample: MIS/uniform pending radiance, RIS winner bsdf*; cos
+    float b[3]; float b_pdf;        // BSDF sample / candidate: bsdf colour, pdf
+    float dir[3]; float b_cos;      // BSDF sample direction, cosine
+    float e1[3]; float ris_wsum;    // envmap light-sampled contribution; RIS weight sum of light candidates
+    float e2[3]; float ris_target;  // envmap BSDF-sampled contribution; RIS target of the light winner
+    float r_add; int32_t ris_tri; float imm[3];   // RIS random of the BSDF candidate; light winner triangle; immediate light term
+    float pad[3];
+};
+static_assert(sizeof(NeeRec) == 128, "NeeRec is 128 bytes");
+
+enum : uint32_t {
+    NF_SHADED = 1u << 0,     // the path had a hit at this bounce -> resolve adds NEE
+    NF_A = 1u << 1,          // light-sample contribution pending occlusion slot 0
+    NF_B = 1u << 2,          // BSDF ray pending in the closest-hit slot
+    NF_B_REFR = 1u << 3,
+    NF_E1 = 1u << 4,         // env light-sample contribution pending occlusion slot 1
+    NF_E2 = 1u << 5,         // env BSDF-sample contribution pending occlusion slot 2
+    NF_RIS_W = 1u << 6,      // RIS light winner exists
+    NF_IMM = 1u << 7,        // immediate light term (emissive textured material)
+    NF_NOADD = 1u << 8,      // LSS_NO_DIRECT_LIGHT_SAMPLING: nothing to add at resolve
+    NF_L = 1u << 9,          // the light-sampling strategy ran at this vertex
+};
+
+struct DevPaths {
+    int32_t n;                // slots
+    int32_t res_x;
+    float4* ray_o;            // xyz + last_hit bits
+    float4* ray_d;            // xyz + tmax
+    float4* hit;              // t, u, v, prim bits
+    uint8_t* hit_inside;      // "inside a volume" before the last stack push (trace_ray normal flip)
+    uint32_t* rng;
+    float4* thr;
+    float4* col;
+    uint4* vsA;
+    uint4* vsB;
+    float4* alb;
+    float4* nrm;
+    int32_t* q0;
+    int32_t* q1;
+    int32_t* counters;        // see CTR_*
+    NeeRec* nee;
+    float4* nq_o;             // NEE query rays: [0, n*3) any-hit area, [n*3, n*4) closest area
+    float4* nq_d;
+    int32_t* nq_tgt;          // target: slot*4 + kind
+    uint8_t* occ;             // 3 per slot
+    float4* nhit;             // closest NEE result per slot
+    float* fb_color;          // 3 per slot (sum)
+    float* fb_albedo;
+    float* fb_normal;
+    uint32_t* stack_spill;    // global spill area of the traversal stacks
+    uint64_t* stats;          // 4 counters
+};
+
+enum {
+    CTR_Q0 = 0, CTR_Q1 = 1, CTR_ANY = 2, CTR_CL = 3, CTR_FETCH = 4,
+    CTR_COUNT = 16
+};
+
+// launch glue (mpt_kernels.hip)
+struct LaunchCfg {
+    int grid_persistent;      // blocks of the persistent traversal kernels
+    int stats;                // instrumented traversal
+    hipEvent_t* ev_pool;      // optional: one event pair per traversal launch
+    int ev_cap;
+    int ev_used;
+    uint32_t launches;
+};
+
+hipError_t launch_frame(const DevScene& S, const DevPaths& P, const MptFrame* d_frame, const MptFrame& h_frame,
+                        LaunchCfg& cfg, hipStream_t st);
+hipError_t launch_trace_raw(const DevScene& S, const float4* o, const float4* d, int n, bool any, float4* out_hit,
+                            uint8_t* out_occ, int32_t* fetch_ctr, uint32_t* spill, int grid, hipStream_t st);
+
+}  // namespace mpt
+
+#endif

@@ -1,0 +1,1129 @@
+// mpt_kernels.hip -- the MI355X wavefront path tracer (hot path).
+//
+// One frame = one sample per pixel of the context's row partition:
+//
+//   k_camera ............ CameraRays ray generation (Device/kernels/CameraRays.h:45-142)
+//   for bounce in 0..nb_bounces:                        (FullPathTracer.h:155-290)
+//     k_trace<closest, volume-aware> over the active-path queue: BVH8 traversal +
+//                       nested-dielectric boundary skipping (Intersect.h:114-206)
+//     k_shade ........... hit processing, emission, every RNG draw of the vertex in the
+//                       reference order (light sampling Lights.h / RIS.h, envmap
+//                       Envmap.h, BSDF continuation, Russian roulette), appends the
+//                       vertex's NEE queries (shadow any-hit + BSDF closest-hit) and the
+//                       continuation ray with wave64 ballot compaction
+//     k_trace<any> / k_trace<closest> over the NEE queues
+//     k_resolve ......... finishes RIS / MIS / envmap-MIS with the trace results, clamps
+//                       and adds to the path radiance (FullPathTracer.h:196-214)
+//   k_accumulate ........ sanity check + running-sum framebuffer / AOVs (FullPathTracer.h:292-327)
+//
+// RNG: each path owns one Xorshift32 stream seeded exactly as the reference
+// (wang_hash((pixel+1)*(sample+1)*random_seed), FullPathTracer.h:124-129); every draw
+// happens in k_shade in the reference's order, and the trace results only decide how
+// the already-drawn values are used, so the stream is identical to the megakernel's.
+//
+// BVH8 traversal: one ray per lane, 64 rays fetched per wave from a global counter
+// (persistent waves), node groups (child base, internal mask, remaining-hit mask)
+// on a 12-deep LDS stack per lane with a global spill area, octant-ordered children
+// (near-to-far without sorting), leaves tested as soon as their node is opened.
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+
+#include "dev_bsdf.h"
+#include "mpt_internal.h"
+
+namespace mpt {
+
+constexpr int TB = TRAV_BLOCK;
+constexpr int LDS_STACK = TRAV_LDS_STACK;
+constexpr int SPILL_DEPTH = TRAV_SPILL_DEPTH;
+
+// ----------------------------------------------------------------------------------
+// wave64 helpers
+// ----------------------------------------------------------------------------------
+DEV int lane_id() { return __lane_id(); }
+DEV int wave_append(int32_t* counter, bool pred) {
+    unsigned long long m = __ballot(pred);
+    unsigned long long act = __ballot(1);
+    int leader = __ffsll((long long)act) - 1;
+    int cnt = __popcll(m);
+    int base = 0;
+    if (lane_id() == leader && cnt) base = atomicAdd(counter, cnt);
+    base = __shfl(base, leader);
+    unsigned long long lower = m & ((1ull << lane_id()) - 1ull);
+    return base + __popcll(lower);
+}
+
+// ----------------------------------------------------------------------------------
+// BVH8 traversal
+// ----------------------------------------------------------------------------------
+struct THit { int prim; float t, u, v; };
+
+DEV uint32_t qbyte(uint32_t w0, uint32_t w1, int s) { return ((s < 4 ? w0 : w1) >> ((s & 3) * 8)) & 0xffu; }
+
+template <bool ANY, bool STATS>
+DEV bool traverse(const DevScene& S, v3 o, v3 d, int last_hit, float tmax, THit& out, uint2* lds, uint32_t* spill,
+                  uint32_t& n_nodes, uint32_t& n_tris) {
+    const float4* nodes = reinterpret_cast<const float4*>(S.nodes);
+    const float4* tris = reinterpret_cast<const float4*>(S.tris);
+    float ix = 1.0f / (fabsf(d.x) > 1e-30f ? d.x : copysignf(1e-30f, d.x));
+    float iy = 1.0f / (fabsf(d.y) > 1e-30f ? d.y : copysignf(1e-30f, d.y));
+    float iz = 1.0f / (fabsf(d.z) > 1e-30f ? d.z : copysignf(1e-30f, d.z));
+    int oct = (d.x > 0.0f ? 1 : 0) | (d.y > 0.0f ? 2 : 0) | (d.z > 0.0f ? 4 : 0);
+    int xr = oct ^ 7;
+    float best = ANY ? tmax : INFINITY;
+    int bprim = -1;
+    float bu = 0.0f, bv = 0.0f;
+    uint32_t gbase = 0, gimask = 1u, gk = 1u << (0 ^ xr);
+    int sp = 0;
+    const int tid = threadIdx.x;
+    while (true) {
+        if (gk == 0) {
+            if (sp == 0) break;
+            --sp;
+            uint2 e;
+            if (sp < LDS_STACK) e = lds[sp * TB + tid];
+            else { e.x = spill[2 * (sp - LDS_STACK)]; e.y = spill[2 * (sp - LDS_STACK) + 1]; }
+            gbase = e.x; gimask = e.y & 0xffu; gk = e.y >> 8;
+        }
+        int k = __builtin_ctz(gk);
+        gk &= gk - 1u;
+        int s = k ^ xr;
+        uint32_t ni = gbase + (uint32_t)__builtin_popcount(gimask & ((1u << s) - 1u));
+        if (gk) {
+            uint2 e = make_uint2(gbase, gimask | (gk << 8));
+            if (sp < LDS_STACK) lds[sp * TB + tid] = e;
+            else { spill[2 * (sp - LDS_STACK)] = e.x; spill[2 * (sp - LDS_STACK) + 1] = e.y; }
+            ++sp;
+        }
+        if (STATS) n_nodes++;
+        const float4 n0 = nodes[5 * (size_t)ni + 0];
+        const float4 n1 = nodes[5 * (size_t)ni + 1];
+        const float4 n2 = nodes[5 * (size_t)ni + 2];
+        const float4 n3 = nodes[5 * (size_t)ni + 3];
+        const float4 n4 = nodes[5 * (size_t)ni + 4];
+        uint32_t eb = __float_as_uint(n0.w);
+        float sx = __uint_as_float((eb & 0xffu) << 23), sy = __uint_as_float(((eb >> 8) & 0xffu) << 23),
+              sz = __uint_as_float(((eb >> 16) & 0xffu) << 23);
+        uint32_t imask = eb >> 24;
+        float ax = (n0.x - o.x) * ix, ay = (n0.y - o.y) * iy, az = (n0.z - o.z) * iz;
+        float cx = sx * ix, cy = sy * iy, cz = sz * iz;
+        uint32_t lox0 = __float_as_uint(n2.x), lox1 = __float_as_uint(n2.y);
+        uint32_t loy0 = __float_as_uint(n2.z), loy1 = __float_as_uint(n2.w);
+        uint32_t loz0 = __float_as_uint(n3.x), loz1 = __float_as_uint(n3.y);
+        uint32_t hix0 = __float_as_uint(n3.z), hix1 = __float_as_uint(n3.w);
+        uint32_t hiy0 = __float_as_uint(n4.x), hiy1 = __float_as_uint(n4.y);
+        uint32_t hiz0 = __float_as_uint(n4.z), hiz1 = __float_as_uint(n4.w);
+        // near / far planes by direction sign
+        uint32_t nx0 = ix >= 0.0f ? lox0 : hix0, nx1 = ix >= 0.0f ? lox1 : hix1;
+        uint32_t fx0 = ix >= 0.0f ? hix0 : lox0, fx1 = ix >= 0.0f ? hix1 : lox1;
+        uint32_t ny0 = iy >= 0.0f ? loy0 : hiy0, ny1 = iy >= 0.0f ? loy1 : hiy1;
+        uint32_t fy0 = iy >= 0.0f ? hiy0 : loy0, fy1 = iy >= 0.0f ? hiy1 : loy1;
+        uint32_t nz0 = iz >= 0.0f ? loz0 : hiz0, nz1 = iz >= 0.0f ? loz1 : hiz1;
+        uint32_t fz0 = iz >= 0.0f ? hiz0 : loz0, fz1 = iz >= 0.0f ? hiz1 : loz1;
+        uint32_t meta0 = __float_as_uint(n1.z), meta1 = __float_as_uint(n1.w);
+        uint32_t child_base = __float_as_uint(n1.x), tri_base = __float_as_uint(n1.y);
+        uint32_t hit_internal = 0u;   // k-ordered
+        uint32_t hit_leaf = 0u;       // slot-ordered
+#pragma unroll
+        for (int c = 0; c < 8; c++) {
+            float tnx = fmaf((float)qbyte(nx0, nx1, c), cx, ax), tfx = fmaf((float)qbyte(fx0, fx1, c), cx, ax);
+            float tny = fmaf((float)qbyte(ny0, ny1, c), cy, ay), tfy = fmaf((float)qbyte(fy0, fy1, c), cy, ay);
+            float tnz = fmaf((float)qbyte(nz0, nz1, c), cz, az), tfz = fmaf((float)qbyte(fz0, fz1, c), cz, az);
+            float tn = fmaxf(fmaxf(tnx, tny), fmaxf(tnz, 0.0f));
+            float tf = fminf(fminf(tfx, tfy), fminf(tfz, best)) * 1.0000009f;
+            bool h = tn <= tf;
+            uint32_t meta = qbyte(meta0, meta1, c);
+            bool internal = (imask >> c) & 1u;
+            if (h && internal) hit_internal |= 1u << (c ^ xr);
+            if (h && !internal && (meta >> 5)) hit_leaf |= 1u << c;
+        }
+        while (hit_leaf) {
+            int c = __builtin_ctz(hit_leaf);
+            hit_leaf &= hit_leaf - 1u;
+            uint32_t meta = qbyte(meta0, meta1, c);
+            uint32_t first = tri_base + (meta & 31u), cnt = meta >> 5;
+            for (uint32_t j = 0; j < cnt; j++) {
+                if (STATS) n_tris++;
+                const float4 t0 = tris[3 * (size_t)(first + j) + 0];
+                const float4 t1 = tris[3 * (size_t)(first + j) + 1];
+                const float4 t2 = tris[3 * (size_t)(first + j) + 2];
+                int prim = (int)__float_as_uint(t0.w);
+                // Moller-Trumbore exactly as Renderer/Triangle.h:20-62 (no contraction)
+                v3 e1 = mk3(t1.x, t1.y, t1.z), e2 = mk3(t2.x, t2.y, t2.z);
+                v3 h = cross(d, e2);
+                float a = dot(e1, h);
+                if (a > -0.0000001f && a < 0.0000001f) continue;
+                float f = 1.0f / a;
+                v3 sv = o - mk3(t0.x, t0.y, t0.z);
+                float u = f * dot(sv, h);
+                if (u < 0.0f || u > 1.0f) continue;
+                v3 q = cross(sv, e1);
+                float v = f * dot(d, q);
+                if (v < 0.0f || u + v > 1.0f) continue;
+                float t = f * dot(e2, q);
+                if (!(t > 0.0000001f)) continue;
+                if (prim == last_hit) continue;
+                if (ANY) {
+                    if (t < tmax) { out.prim = prim; out.t = t; out.u = u; out.v = v; return true; }
+                } else if (t < best || (t == best && prim < bprim)) {
+                    best = t; bprim = prim; bu = u; bv = v;
+                }
+            }
+        }
+        gbase = child_base;
+        gimask = imask;
+        gk = hit_internal;
+    }
+    out.prim = bprim;
+    out.t = best;
+    out.u = bu;
+    out.v = bv;
+    return bprim >= 0;
+}
+
+// Ray sources of the persistent traversal kernel
+enum TraceMode { TM_PATH = 0, TM_NEE_ANY = 1, TM_NEE_CLOSEST = 2, TM_RAW_CLOSEST = 3, TM_RAW_ANY = 4 };
+
+struct TraceArgs {
+    DevScene S;
+    DevPaths P;
+    const int32_t* queue;      // TM_PATH: slot list
+    const int32_t* count_ptr;  // device count (TM_PATH / NEE)
+    int count_const;           // RAW
+    int32_t* fetch;            // work counter (zeroed before the launch)
+    const float4* raw_o;
+    const float4* raw_d;
+    float4* raw_hit;
+    uint8_t* raw_occ;
+};
+
+template <int MODE, bool STATS>
+__global__ __launch_bounds__(TB) void k_trace(TraceArgs A) {
+    __shared__ uint2 lds[LDS_STACK * TB];
+    const DevScene& S = A.S;
+    const DevPaths& P = A.P;
+    const int count = (MODE == TM_RAW_CLOSEST || MODE == TM_RAW_ANY) ? A.count_const : *A.count_ptr;
+    uint32_t* spill = P.stack_spill + ((size_t)blockIdx.x * TB + threadIdx.x) * (2 * SPILL_DEPTH);
+    uint32_t n_nodes = 0, n_tris = 0, n_rays = 0;
+    const bool any = (MODE == TM_NEE_ANY || MODE == TM_RAW_ANY);
+    while (true) {
+        int base = 0;
+        if (lane_id() == 0) base = atomicAdd(A.fetch, 64);
+        base = __shfl(base, 0);
+        if (base >= count) break;
+        int i = base + lane_id();
+        if (i >= count) continue;
+        float4 ro, rd;
+        int slot = 0;
+        if (MODE == TM_PATH) { slot = A.queue[i]; ro = P.ray_o[slot]; rd = P.ray_d[slot]; }
+        else if (MODE == TM_NEE_ANY) { ro = P.nq_o[i]; rd = P.nq_d[i]; }
+        else if (MODE == TM_NEE_CLOSEST) { ro = P.nq_o[(size_t)P.n * 3 + i]; rd = P.nq_d[(size_t)P.n * 3 + i]; }
+        else { ro = A.raw_o[i]; rd = A.raw_d[i]; }
+        v3 o = mk3(ro.x, ro.y, ro.z), d = mk3(rd.x, rd.y, rd.z);
+        int last_hit = (int)__float_as_uint(ro.w);
+        THit h;
+        if (MODE == TM_PATH) {
+            // trace_ray's boundary-skipping loop (Intersect.h:117-206)
+            VState vs = vs_load(P.vsA, P.vsB, slot);
+            bool was_inside = false;
+            bool found;
+            while (true) {
+                n_rays++;
+                found = traverse<false, STATS>(S, o, d, last_hit, INFINITY, h, lds, spill, n_nodes, n_tris);
+                if (!found) break;
+                was_inside = vs.pos > 0;
+                if (was_inside) vs.dist += h.t;
+                int mi = S.mat_idx[h.prim];
+                bool skip = vs_push(vs, mi, S.mat_prio[mi]);
+                if (!skip) break;
+                o = o + h.t * d;
+                vs.dist += h.t;
+            }
+            vs_store(P.vsA, P.vsB, slot, vs);
+            P.ray_o[slot] = make_float4(o.x, o.y, o.z, ro.w);
+            P.hit[slot] = make_float4(h.t, h.u, h.v, __uint_as_float((uint32_t)(found ? h.prim : -1)));
+            P.hit_inside[slot] = was_inside ? 1 : 0;
+        } else {
+            n_rays++;
+            bool found = any ? traverse<true, STATS>(S, o, d, last_hit, rd.w, h, lds, spill, n_nodes, n_tris)
+                             : traverse<false, STATS>(S, o, d, last_hit, INFINITY, h, lds, spill, n_nodes, n_tris);
+            if (MODE == TM_NEE_ANY) {
+                int tgt = P.nq_tgt[i];
+                P.occ[(tgt >> 2) * 3 + (tgt & 3)] = found ? 1 : 0;
+            } else if (MODE == TM_NEE_CLOSEST) {
+                int tgt = P.nq_tgt[(size_t)P.n * 3 + i];
+                // evaluate_shadow_light_ray: a hit counts only below t_max - 1e-4 (Intersect.h:337-343)
+                bool ok = found && h.t < rd.w;
+                P.nhit[tgt >> 2] = make_float4(h.t, h.u, h.v, __uint_as_float((uint32_t)(ok ? h.prim : -1)));
+            } else if (MODE == TM_RAW_ANY) {
+                A.raw_occ[i] = found ? 1 : 0;
+            } else {
+                A.raw_hit[i] = make_float4(h.t, h.u, h.v, __uint_as_float((uint32_t)(found ? h.prim : -1)));
+            }
+        }
+    }
+    if (STATS) {
+        // wave-aggregated counters
+        for (int off = 32; off > 0; off >>= 1) {
+            n_nodes += __shfl_xor(n_nodes, off);
+            n_tris += __shfl_xor(n_tris, off);
+            n_rays += __shfl_xor(n_rays, off);
+        }
+        if (lane_id() == 0) {
+            atomicAdd((unsigned long long*)&P.stats[any ? 1 : 0], (unsigned long long)n_rays);
+            atomicAdd((unsigned long long*)&P.stats[2], (unsigned long long)n_nodes);
+            atomicAdd((unsigned long long*)&P.stats[3], (unsigned long long)n_tris);
+        }
+    }
+}
+
+// ----------------------------------------------------------------------------------
+// Scene access helpers (Intersect.h:30-83, Material.h:47-159, Texture.h:31-222)
+// ----------------------------------------------------------------------------------
+DEV v3 ld3(const float* p, int i) { return mk3(p[3 * (size_t)i], p[3 * (size_t)i + 1], p[3 * (size_t)i + 2]); }
+DEV v2 ld2(const float* p, int i) { return mk2(p[2 * (size_t)i], p[2 * (size_t)i + 1]); }
+DEV int3 tri_idx(const DevScene& S, int p) { return make_int3(S.idx[3 * (size_t)p], S.idx[3 * (size_t)p + 1], S.idx[3 * (size_t)p + 2]); }
+DEV v3 uv_interp3(const float* data, int3 t, v2 uv) { return ld3(data, t.y) * uv.x + ld3(data, t.z) * uv.y + ld3(data, t.x) * (1.0f - uv.x - uv.y); }
+DEV v2 uv_interp2(const float* data, int3 t, v2 uv) { return ld2(data, t.y) * uv.x + ld2(data, t.z) * uv.y + ld2(data, t.x) * (1.0f - uv.x - uv.y); }
+DEV v3 tri_normal(const DevScene& S, int p) {
+    const float4* tr = reinterpret_cast<const float4*>(S.tris);
+    (void)tr;
+    int3 t = tri_idx(S, p);
+    v3 A = ld3(S.pos, t.x), B = ld3(S.pos, t.y), C = ld3(S.pos, t.z);
+    return normalize(cross(B - A, C - A));
+}
+DEV void tex_rgba(const DevScene& S, int ti, bool srgb, v2 uv, float out[4]) {
+    int w = S.tex_dims[2 * ti], h = S.tex_dims[2 * ti + 1];
+    float u = wrap01(uv.x), v = 1.0f - wrap01(uv.y);
+    int x = (int)(u * (float)(w - 1)), y = (int)(v * (float)(h - 1));
+    const uint8_t* p = S.tex + S.tex_off[ti] + (size_t)(x + y * w) * 4;
+    uchar4 c = *reinterpret_cast<const uchar4*>(p);
+    out[0] = (float)c.x / 255.0f; out[1] = (float)c.y / 255.0f; out[2] = (float)c.z / 255.0f; out[3] = (float)c.w / 255.0f;
+    if (srgb) for (int i = 0; i < 4; i++) out[i] = ppow(out[i], 2.2f);
+}
+DEV bool has_tex(int ti) { return ti != MPT_NO_TEXTURE && ti != MPT_CONSTANT_EMISSIVE_TEXTURE; }
+DEV void prop_f(const DevScene& S, float& v, v2 uv, int ti) { if (has_tex(ti)) { float r[4]; tex_rgba(S, ti, false, uv, r); v = r[0]; } }
+DEV void prop_c(const DevScene& S, MptColor& v, v2 uv, int ti) { if (has_tex(ti)) { float r[4]; tex_rgba(S, ti, false, uv, r); v.r = r[0]; v.g = r[1]; v.b = r[2]; } }
+
+DEV Col emission_of(const Mat& m) { return C3(m.emission) * m.emission_strength; }
+DEV bool is_emissive(const Mat& m) {
+    float k = m.emission_strength;
+    return !is_zero(m.emission.r * k) || !is_zero(m.emission.g * k) || !is_zero(m.emission.b * k) || m.emissive_texture_used;
+}
+
+DEV Mat intersection_material(const DevScene& S, int mi, v2 uv, bool white_furnace) {
+    Mat m = S.mats[mi];
+    MptColor e;
+    e.r = m.emission.r * m.emission_strength / m.emission_strength;
+    e.g = m.emission.g * m.emission_strength / m.emission_strength;
+    e.b = m.emission.b * m.emission_strength / m.emission_strength;
+    if (S.n_tex > 0) prop_c(S, e, uv, m.emission_texture_index);
+    m.emission = e;
+    if (white_furnace) { m.base_color.r = 1.0f; m.base_color.g = 1.0f; m.base_color.b = 1.0f; }
+    else if (S.n_tex > 0 && has_tex(m.base_color_texture_index)) {
+        float r[4];
+        tex_rgba(S, m.base_color_texture_index, true, uv, r);
+        m.base_color.r = r[0]; m.base_color.g = r[1]; m.base_color.b = r[2];
+    }
+    if (S.n_tex > 0) {
+        if (m.roughness_metallic_texture_index != MPT_NO_TEXTURE) {
+            float r[4];
+            tex_rgba(S, m.roughness_metallic_texture_index, false, uv, r);
+            m.roughness = r[1];
+            m.metallic = r[2];
+        } else {
+            prop_f(S, m.metallic, uv, m.metallic_texture_index);
+            prop_f(S, m.roughness, uv, m.roughness_texture_index);
+        }
+        prop_f(S, m.oren_nayar_sigma, uv, m.oren_sigma_texture_index);
+        prop_f(S, m.specular, uv, m.specular_texture_index);
+        prop_f(S, m.specular_tint, uv, m.specular_tint_texture_index);
+        prop_c(S, m.specular_color, uv, m.specular_color_texture_index);
+        prop_f(S, m.anisotropy, uv, m.anisotropic_texture_index);
+        prop_f(S, m.anisotropy_rotation, uv, m.anisotropic_rotation_texture_index);
+        prop_f(S, m.coat, uv, m.coat_texture_index);
+        prop_f(S, m.coat_roughness, uv, m.coat_roughness_texture_index);
+        prop_f(S, m.coat_ior, uv, m.coat_ior_texture_index);
+        prop_f(S, m.sheen, uv, m.sheen_texture_index);
+        prop_f(S, m.sheen_roughness, uv, m.sheen_roughness_texture_index);
+        prop_c(S, m.sheen_color, uv, m.sheen_color_texture_index);
+        prop_f(S, m.specular_transmission, uv, m.specular_transmission_texture_index);
+    }
+    float coat = m.coat;
+    m.emissive_texture_used = m.emission_texture_index > 0;
+    float tbr = sqrtf(sqrtf(minr(1.0f, pow4(m.roughness) + 2.0f * pow4(m.coat_roughness))));
+    m.roughness = lerpr(m.roughness, lerpr(m.roughness, tbr, coat), m.coat_roughening);
+    float tsr = sqrtf(sqrtf(minr(1.0f, pow4(m.second_roughness) + 2.0f * pow4(m.coat_roughness))));
+    m.second_roughness = lerpr(m.second_roughness, lerpr(m.second_roughness, tsr, coat), m.coat_roughening);
+    return m;
+}
+
+DEV v3 shading_normal_of(const DevScene& S, v3 gn, int p, v2 uv, v2 tc) {
+    int3 t = tri_idx(S, p);
+    const Mat& m = S.mats[S.mat_idx[p]];
+    v3 n = S.has_n[t.x] ? normalize(uv_interp3(S.nrm, t, uv)) : gn;
+    if (S.n_tex > 0 && m.normal_map_texture_index != MPT_NO_TEXTURE) {
+        v2 d1 = ld2(S.uv, t.y) - ld2(S.uv, t.x), d2 = ld2(S.uv, t.z) - ld2(S.uv, t.x);
+        v3 e1 = ld3(S.pos, t.y) - ld3(S.pos, t.x), e2 = ld3(S.pos, t.z) - ld3(S.pos, t.x);
+        float di = 1.0f / (d1.x * d2.y - d1.y * d2.x);
+        v3 T = (e1 * d2.y - e2 * d1.y) * di;
+        v3 B = (e2 * d1.x - e1 * d2.x) * di;
+        float r[4];
+        tex_rgba(S, m.normal_map_texture_index, false, tc, r);
+        v3 ts = normalize(mk3(r[0] - 0.5f, r[1] - 0.5f, r[2] - 0.5f));
+        n = to_world(normalize(T), normalize(B), n, ts);
+    }
+    return n;
+}
+
+// slot -> pixel of the band partition (rows y with (y / bh) % bc == bi, increasing y)
+DEV uint32_t slot_pixel(const MptFrame& F, int slot, int& x, int& y) {
+    int r = slot / F.res_x;
+    x = slot - r * F.res_x;
+    int bh = F.band_height;
+    y = ((r / bh) * F.band_count + F.band_index) * bh + (r % bh);
+    return (uint32_t)x + (uint32_t)y * (uint32_t)F.res_x;
+}
+DEV uint32_t pixel_seed(const MptFrame& F, uint32_t pix) {
+    const MptRenderSettings& rs = F.render_settings;
+    return rs.freeze_random ? wang_hash(pix + 1u) : wang_hash((pix + 1u) * (uint32_t)(rs.sample_number + 1) * F.random_seed);
+}
+
+// ----------------------------------------------------------------------------------
+// k_camera: CameraRays ray generation (CameraRays.h:127-142, HIPRTCamera.h:27-47)
+// ----------------------------------------------------------------------------------
+__global__ __launch_bounds__(TB) void k_camera(DevPaths P, const MptFrame* __restrict__ Fp) {
+    const MptFrame& F = *Fp;
+    int slot = blockIdx.x * TB + threadIdx.x;
+    if (slot >= P.n) return;
+    int x, y;
+    uint32_t pix = slot_pixel(F, slot, x, y);
+    Rng rng = make_rng(pixel_seed(F, pix));
+    float xd = (float)x + 0.5f, yd = (float)y + 0.5f;
+    if (F.current_camera.do_jittering) { xd += rng() - 0.5f; yd += rng() - 0.5f; }
+    float xn = xd / (float)F.res_x * 2.0f - 1.0f;
+    float yn = yd / (float)F.res_y * 2.0f - 1.0f;
+    v3 o = mat_x_point(F.current_camera.inverse_view.m, mk3(0.0f, 0.0f, 0.0f));
+    v3 pvs = mat_x_point(F.current_camera.inverse_projection.m, mk3(xn, yn, -1.0f));
+    v3 pws = mat_x_point(F.current_camera.inverse_view.m, pvs);
+    v3 d = normalize(pws - o);
+    P.ray_o[slot] = make_float4(o.x, o.y, o.z, __uint_as_float(0xffffffffu));
+    P.ray_d[slot] = make_float4(d.x, d.y, d.z, INFINITY);
+    P.rng[slot] = rng.s;   // camera stream after the jitter draws (trace_ray's wavelength draw)
+    vs_store(P.vsA, P.vsB, slot, vs_default());
+    P.thr[slot] = make_float4(1.0f, 1.0f, 1.0f, 0.0f);
+    P.col[slot] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    P.alb[slot] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    P.nrm[slot] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    P.q0[slot] = slot;
+}
+
+// ----------------------------------------------------------------------------------
+// light sampling helpers (LightUtils.h)
+// ----------------------------------------------------------------------------------
+struct LightInfo { int tri; v3 normal; float area; Col emission; };
+DEV v3 sample_emissive_triangle(const DevScene& S, Rng& rng, float& pdf, LightInfo& li) {
+    int ri = rng.random_index(S.n_emissive);
+    int t = S.emissive[ri];
+    int3 ti = tri_idx(S, t);
+    v3 A = ld3(S.pos, ti.x), B = ld3(S.pos, ti.y), C = ld3(S.pos, ti.z);
+    float r1 = rng(), r2 = rng();
+    float sr1 = sqrtf(r1);
+    float u = 1.0f - sr1, v = (1.0f - r2) * sr1;
+    v3 AB = B - A, AC = C - A;
+    v3 pt = A + AB * u + AC * v;
+    v3 n = cross(AB, AC);
+    float ln = length(n);
+    li.tri = -1; li.normal = mk3(0.0f, 1.0f, 0.0f); li.area = 1.0f; li.emission = col(0.0f);
+    if (ln <= 1.0e-6f) { pdf = 0.0f; return mk3(0.0f, 0.0f, 0.0f); }
+    li.tri = t;
+    li.normal = n / ln;
+    li.area = ln * 0.5f;
+    li.emission = emission_of(S.mats[S.mat_idx[t]]);
+    pdf = 1.0f / li.area;
+    pdf /= (float)S.n_emissive;
+    return pt;
+}
+DEV bool min_contrib(float mn, Col c) { return mn > 0.0f ? !(c.r < mn && c.g < mn && c.b < mn) : true; }
+DEV Col clamp_contrib(Col c, float mx, bool cond) { return (!has_nan(c) && mx > 0.0f && cond) ? clampc(c, -mx, mx) : c; }
+
+// envmap (Envmap.h)
+DEV Col env_tex(const DevScene& S, const MptFrame& F, v2 uv) {
+    float u = wrap01(uv.x), v = 1.0f - wrap01(uv.y);
+    int x = (int)(u * (float)(S.env_w - 1)), y = (int)(v * (float)(S.env_h - 1));
+    float4 p = S.env[x + (size_t)y * S.env_w];
+    return col(p.x, p.y, p.z) * F.world_settings.envmap_intensity;
+}
+DEV Col eval_env_no_pdf(const DevScene& S, const MptFrame& F, v3 d) {
+    v3 r = mat_x_vec(F.world_settings.world_to_envmap_matrix.m, d);
+    float u = 0.5f + patan2(r.z, r.x) * INV_2_PI;
+    float v = 0.5f + pasin(r.y) * INV_PI;
+    return env_tex(S, F, mk2(u, 1.0f - v));
+}
+DEV Col env_sample(const DevScene& S, const MptFrame& F, v3& dir, float& pdf, Rng& rng) {
+    int ri = rng.random_index(S.env_h * S.env_w);
+    float prob = S.alias_p[ri];
+    if (rng() > prob) ri = S.alias_i[ri];
+    int y = (int)((unsigned)ri / (unsigned)S.env_w);
+    int x = ri - y * S.env_w;
+    float u = (float)x / (float)(unsigned)S.env_w, v = (float)y / (float)(unsigned)S.env_h;
+    float phi = u * TWO_PI;
+    float theta = maxr(1.0e-5f, v * PI);
+    float ct = pcos(theta), st = psin(theta);
+    dir = mat_x_vec(F.world_settings.envmap_to_world_matrix.m, mk3(-st * pcos(phi), -ct, -st * psin(phi)));
+    Col rad = env_tex(S, F, mk2(u, 1.0f - v));
+    pdf = lum(rad) / (S.env_sum * F.world_settings.envmap_intensity);
+    pdf *= (float)((unsigned)S.env_w * (unsigned)S.env_h);
+    pdf /= (TWO_PIPI * st);
+    return rad;
+}
+DEV Col env_eval(const DevScene& S, const MptFrame& F, v3 d, float& pdf) {
+    Col rad = eval_env_no_pdf(S, F, d);
+    float st = psin(pacos(-d.y));
+    pdf = lum(rad) / (S.env_sum * F.world_settings.envmap_intensity);
+    pdf *= (float)((unsigned)S.env_w * (unsigned)S.env_h);
+    pdf /= (TWO_PIPI * st);
+    return rad;
+}
+
+// NEE query emission: any-hit area [0, 3n), closest area [3n, 4n)
+DEV void emit_query(const DevPaths& P, int area_closest, int idx, v3 o, int last_hit, v3 d, float tmax, int tgt) {
+    size_t base = area_closest ? (size_t)P.n * 3 : 0;
+    P.nq_o[base + idx] = make_float4(o.x, o.y, o.z, __uint_as_float((uint32_t)last_hit));
+    P.nq_d[base + idx] = make_float4(d.x, d.y, d.z, tmax);
+    P.nq_tgt[base + idx] = tgt;
+}
+
+DEV void store3(float* p, Col c) { p[0] = c.r; p[1] = c.g; p[2] = c.b; }
+DEV void store3(float* p, v3 c) { p[0] = c.x; p[1] = c.y; p[2] = c.z; }
+DEV Col load3c(const float* p) { return col(p[0], p[1], p[2]); }
+DEV v3 load3v(const float* p) { return mk3(p[0], p[1], p[2]); }
+
+// ----------------------------------------------------------------------------------
+// k_shade: one path vertex up to (not including) the NEE trace results
+// ----------------------------------------------------------------------------------
+struct ShadeArgs {
+    DevScene S;
+    DevPaths P;
+    const MptFrame* F;
+    int bounce;
+    int last_bounce;
+    const int32_t* q_cur;
+    const int32_t* count_cur;
+    int32_t* q_next;
+    int32_t* count_next;
+};
+
+template <int OVR>
+__global__ __launch_bounds__(TB) void k_shade(ShadeArgs A) {
+    const DevScene& S = A.S;
+    const DevPaths& P = A.P;
+    const MptFrame& F = *A.F;
+    const MptRenderSettings& rs = F.render_settings;
+    const int bounce = A.bounce;
+    int i = blockIdx.x * TB + threadIdx.x;
+    bool valid = i < *A.count_cur;
+    int slot = valid ? A.q_cur[i] : 0;
+
+    BCtx bc;
+    bc.mats = S.mats;
+    bc.luts = DevLuts{S.lut_conductor, S.lut_glossy, S.lut_glass, S.lut_glass_inv, S.lut_thin_glass, S.lut_sheen};
+    bc.clearcoat_comp = F.bsdf_flags.clearcoat_compensation_approximation;
+    bc.masking = F.bsdf_flags.ggx_masking_shadowing;
+
+    bool cont = false;   // continuation ray emitted
+    bool want_any[3] = {false, false, false};
+    bool want_cl = false;
+    v3 q_o[4], q_d[4];
+    float q_t[4];
+    int last_prim = -1;
+    if (valid) {
+        float4 ro = P.ray_o[slot], rdv = P.ray_d[slot], hv = P.hit[slot];
+        v3 o = mk3(ro.x, ro.y, ro.z), d = mk3(rdv.x, rdv.y, rdv.z);
+        int prim = (int)__float_as_uint(hv.w);
+        bool found = prim >= 0;
+        VState vs = vs_load(P.vsA, P.vsB, slot);
+        Rng rng = make_rng(P.rng[slot]);
+        Col thr = col(P.thr[slot].x, P.thr[slot].y, P.thr[slot].z);
+        float4 cv = P.col[slot];
+        Col rcol = col(cv.x, cv.y, cv.z);
+        v3 ip = mk3(0, 0, 0), gn = mk3(0, 0, 0), sn = mk3(0, 0, 0);
+        Mat m;
+        if (found) {
+            // trace_ray hit processing (Intersect.h:154-216)
+            float t = hv.x;
+            v2 uv = mk2(hv.y, hv.z);
+            int3 ti = tri_idx(S, prim);
+            ip = o + t * d;
+            v2 tc = uv_interp2(S.uv, ti, uv);
+            gn = normalize(tri_normal(S, prim));
+            sn = shading_normal_of(S, gn, prim, uv, tc);
+            m = intersection_material(S, S.mat_idx[prim], tc, F.bsdf_flags.white_furnace_mode);
+            bool was_inside = P.hit_inside[slot] != 0;
+            if ((!was_inside || m.specular_transmission == 0.0f) && !m.thin_walled) {
+                gn *= dot(gn, -d) < 0.0f ? -1.0f : 1.0f;
+                sn *= dot(sn, gn) < 0.0f ? -1.0f : 1.0f;
+                float NoV = dot(sn, -d);
+                sn += (2.0f * clampr(0.0f, 1.0f, -NoV)) * -d;
+            }
+            if (m.dispersion_scale > 0.0f && m.specular_transmission > 0.0f && vs.wl == 0.0f)
+                vs.wl = -(rng() * (float)(830 - 360) + (float)360);
+        }
+        if (bounce == 0) {
+            // CameraRays G-buffer hand-off (CameraRays.h:147-166) and FullPathTracer's
+            // re-read of it (FullPathTracer.h:131-150): emissive flip, normalise, restart RNG
+            if (found && is_emissive(m) && dot(-d, gn) < 0) { gn = -gn; sn = -sn; }
+            gn = normalize(gn);
+            sn = normalize(sn);
+            d = normalize(d);
+            int x, y;
+            rng = make_rng(pixel_seed(F, slot_pixel(F, slot, x, y)));
+        }
+        NeeRec nr;
+        uint32_t fl = 0;
+        if (found) {
+            if (bounce == 0) {
+                float4 a = P.alb[slot], n4 = P.nrm[slot];
+                P.alb[slot] = make_float4(a.x + m.base_color.r, a.y + m.base_color.g, a.z + m.base_color.b, 0.0f);
+                P.nrm[slot] = make_float4(n4.x + sn.x, n4.y + sn.y, n4.z + sn.z, 0.0f);
+            }
+            if (is_emissive(m) && dot(-d, gn) < 0) { gn = -gn; sn = -sn; }
+            v3 view = -d;
+            last_prim = prim;
+            fl |= NF_SHADED;
+            const int lss = F.options.direct_light_sampling;
+            // ---------------- direct light (Lights.h:277-321) ----------------
+            bool do_light = S.n_emissive != 0 && !(F.bsdf_flags.white_furnace_mode && F.bsdf_flags.white_furnace_mode_turn_off_emissives);
+            if (do_light && is_emissive(m)) {
+                do_light = false;
+                if (m.emissive_texture_used && bounce > 0) { fl |= NF_IMM; store3(nr.imm, emission_of(m)); }
+            }
+            if (do_light && lss != MPT_LSS_NO_DIRECT_LIGHT_SAMPLING) {
+                fl |= NF_L;
+                bool inside = dot(view, gn) < 0;
+                float ism = inside ? -1.0f : 1.0f;
+                if (lss == MPT_LSS_RIS_BSDF_AND_LIGHT) {
+                    // sample_bsdf_and_lights_RIS_reservoir (RIS.h:82-289)
+                    v3 ep = ip + sn * 1.0e-4f * ism;
+                    int nl = rs.ris_number_of_light_candidates, nbc = rs.ris_number_of_bsdf_candidates;
+                    float wsum = 0.0f, targetW = 0.0f;
+                    v3 pointW = mk3(0, 0, 0);
+                    int triW = -1;
+                    bool hasW = false;
+                    for (int c = 0; c < nl; c++) {
+                        float lpdf;
+                        LightInfo li;
+                        float target = 0.0f, cw = 0.0f;
+                        v3 lp = sample_emissive_triangle(S, rng, lpdf, li);
+                        if (lpdf > 0.0f) {
+                            v3 tl = lp - ep;
+                            float dist = length(tl);
+                            tl = tl / dist;
+                            float cl = absr(dot(li.normal, -tl));
+                            float ce = maxr(0.0f, dot(sn * ism, tl));
+                            if (ce > 0.0f && cl > 1.0e-6f) {
+                                lpdf *= dist * dist;
+                                lpdf /= cl;
+                                float bp = 0.0f;
+                                if (!min_contrib(rs.minimum_light_contribution, li.emission / lpdf)) target = 0.0f;
+                                else {
+                                    VState tv = vs;
+                                    Col bcol = bsdf_eval<OVR>(bc, m, tv, view, sn, tl, bp);
+                                    Col lc = bcol * li.emission * ce;
+                                    target = min_contrib(rs.minimum_light_contribution, lc / bp / lpdf) ? lum(lc) : 0.0f;
+                                }
+                                cw = balance(lpdf, (float)nl, bp, (float)nbc) * target / lpdf;
+                            }
+                        }
+                        wsum += cw;
+                        if (rng() < cw / wsum) { hasW = true; targetW = target; pointW = lp; triW = li.tri; }
+                    }
+                    nr.ris_wsum = wsum;
+                    if (nbc > 0) {
+                        // the BSDF candidate (nb = 1; validated on the host)
+                        float bpdf = 0.0f;
+                        v3 dir;
+                        VState tv = vs;
+                        Col bcol = bsdf_sample<OVR>(bc, m, tv, view, sn, gn, dir, bpdf, rng);
+                        bool refr = dot(dir, sn * ism) < 0;
+                        v3 so = refr ? ip + sn * 1.0e-4f * ism * -1.0f : ep;
+                        if (bpdf > 0.0f) {
+                            fl |= NF_B | (refr ? NF_B_REFR : 0u);
+                            want_cl = true;
+                            q_o[3] = so; q_d[3] = dir; q_t[3] = 1.0e35f - 1.0e-4f;
+                            store3(nr.b, bcol);
+                            nr.b_pdf = bpdf;
+                            store3(nr.dir, dir);
+                            nr.b_cos = absr(dot(sn, dir));
+                        }
+                        nr.r_add = rng();
+                    }
+                    if (hasW) {
+                        // evaluate_reservoir_sample for the light winner (RIS.h:18-80), speculatively
+                        fl |= NF_RIS_W;
+                        v3 ep2 = ip + sn * 1.0e-4f;
+                        v3 sd = pointW - ep2;
+                        float dist = length(sd);
+                        v3 sdn = sd / dist;
+                        want_any[0] = true;
+                        q_o[0] = ep2; q_d[0] = sdn; q_t[0] = dist - 1.0e-4f;
+                        float bp;
+                        VState tv = vs;
+                        Col bcol = bsdf_eval<OVR>(bc, m, tv, view, sn, sdn, bp);
+                        store3(nr.a, bcol);
+                        nr.a_cos = maxr(0.0f, dot(sn, sdn));
+                        nr.ris_target = targetW;
+                        nr.ris_tri = triW;
+                    }
+                } else if (lss == MPT_LSS_MIS_LIGHT_BSDF) {
+                    // sample_one_light_MIS (Lights.h:115-220)
+                    v3 ep = ip + sn * 1.0e-4f * ism;
+                    float lpdf;
+                    LightInfo li;
+                    v3 lp = sample_emissive_triangle(S, rng, lpdf, li);
+                    if (lpdf > 0.0f) {
+                        v3 sd = lp - ep;
+                        float dist = length(sd);
+                        v3 sdn = sd / dist;
+                        float dl = absr(dot(li.normal, -sdn));
+                        if (dl > 0.0f) {
+                            float bp;
+                            VState tv = vs;
+                            Col bcol = bsdf_eval<OVR>(bc, m, tv, view, sn, sdn, bp);
+                            if (bp != 0.0f) {
+                                float lp2 = lpdf;
+                                lp2 *= dist * dist;
+                                lp2 /= dl;
+                                float w = balance(lp2, bp);
+                                float cosv = maxr(dot(sn, sdn), 0.0f);
+                                store3(nr.a, bcol * cosv * li.emission * w / lp2);
+                                fl |= NF_A;
+                                want_any[0] = true;
+                                q_o[0] = ep; q_d[0] = sdn; q_t[0] = dist - 1.0e-4f;
+                            }
+                        }
+                        float dpdf;
+                        v3 dir;
+                        VState tv = vs;
+                        Col bcol = bsdf_sample<OVR>(bc, m, tv, view, sn, gn, dir, dpdf, rng);
+                        bool refr = dot(dir, sn * ism) < 0;
+                        v3 bo = refr ? ip + sn * 1.0e-4f * ism * -1.0f : ep;
+                        if (dpdf > 0) {
+                            fl |= NF_B;
+                            want_cl = true;
+                            q_o[3] = bo; q_d[3] = dir; q_t[3] = 1.0e35f - 1.0e-4f;
+                            store3(nr.b, bcol);
+                            nr.b_pdf = dpdf;
+                            store3(nr.dir, dir);
+                            nr.b_cos = absr(dot(sn, dir));
+                        }
+                    }
+                } else if (lss == MPT_LSS_UNIFORM_ONE_LIGHT) {
+                    // sample_one_light_no_MIS (Lights.h:22-65)
+                    float lpdf;
+                    LightInfo li;
+                    v3 lp = sample_emissive_triangle(S, rng, lpdf, li);
+                    if (lpdf > 0.0f) {
+                        v3 so = ip + sn * 1.0e-4f;
+                        v3 sd = lp - so;
+                        float dist = length(sd);
+                        v3 sdn = sd / dist;
+                        float dl = absr(dot(li.normal, -sdn));
+                        if (dl > 0.0f) {
+                            float bp;
+                            VState tv = vs;
+                            Col bcol = bsdf_eval<OVR>(bc, m, tv, view, sn, sdn, bp);
+                            if (bp != 0.0f) {
+                                float lp2 = lpdf;
+                                lp2 *= dist * dist;
+                                lp2 /= dl;
+                                float cosv = maxr(dot(sn, sdn), 0.0f);
+                                store3(nr.a, li.emission * cosv * bcol / lp2);
+                                fl |= NF_A;
+                                want_any[0] = true;
+                                q_o[0] = so; q_d[0] = sdn; q_t[0] = dist - 1.0e-4f;
+                            }
+                        }
+                    }
+                } else if (lss == MPT_LSS_BSDF) {
+                    // sample_one_light_bsdf (Lights.h:67-113)
+                    float dpdf;
+                    v3 dir;
+                    VState tv = vs;
+                    Col bcol = bsdf_sample<OVR>(bc, m, tv, view, sn, gn, dir, dpdf, rng);
+                    bool refr = dot(dir, sn * ism) < 0;
+                    if (dpdf > 0.0f) {
+                        v3 no = refr ? ip + sn * 1.0e-4f * ism * -1.0f : ip + sn * 1.0e-4f;
+                        fl |= NF_B;
+                        want_cl = true;
+                        q_o[3] = no; q_d[3] = dir; q_t[3] = 1.0e35f - 1.0e-4f;
+                        store3(nr.b, bcol);
+                        nr.b_pdf = dpdf;
+                        store3(nr.dir, dir);
+                        nr.b_cos = maxr(0.0f, dot(sn, dir));
+                    }
+                }
+            }
+            // ---------------- envmap (Envmap.h:151-246) ----------------
+            const MptWorldSettings& ws = F.world_settings;
+            if (ws.ambient_light_type == MPT_AMBIENT_ENVMAP && !F.bsdf_flags.white_furnace_mode && !is_emissive(m) &&
+                ws.envmap_intensity > 0.0f && F.options.envmap_sampling != MPT_ESS_NO_SAMPLING) {
+                bool use = lss != MPT_LSS_NO_DIRECT_LIGHT_SAMPLING;
+                float epdf;
+                v3 sdir;
+                Col ec = env_sample(S, F, sdir, epdf, rng);
+                float cosv = dot(sn, sdir);
+                if (epdf > 0.0f && cosv > 0.0f) {
+                    float bp;
+                    VState tv = vs;
+                    Col bcol = bsdf_eval<OVR>(bc, m, tv, view, sn, sdir, bp);
+                    float mw = F.options.envmap_bsdf_mis ? balance(epdf, bp) : 1.0f;
+                    store3(nr.e1, bcol * cosv * mw * ec / epdf);
+                    if (use) {
+                        fl |= NF_E1;
+                        want_any[1] = true;
+                        q_o[1] = ip; q_d[1] = sdir; q_t[1] = 1.0e35f - 1.0e-4f;
+                    }
+                }
+                if (F.options.envmap_bsdf_mis) {
+                    float bpdf;
+                    v3 bd;
+                    VState tv = vs;
+                    Col bcol = bsdf_sample<OVR>(bc, m, tv, view, sn, gn, bd, bpdf, rng);
+                    float c2 = absr(dot(sn, bd));
+                    if (bpdf > 0.0f) {
+                        float ep;
+                        Col er = env_eval(S, F, bd, ep);
+                        if (ep > 0.0f && use) {
+                            float mw = balance(bpdf, ep);
+                            store3(nr.e2, er * mw * c2 * bcol / bpdf);
+                            fl |= NF_E2;
+                            want_any[2] = true;
+                            q_o[2] = ip; q_d[2] = bd; q_t[2] = 1.0e35f - 1.0e-4f;
+                        }
+                    }
+                }
+            }
+            // emission (FullPathTracer.h:192-214)
+            if (lss == MPT_LSS_NO_DIRECT_LIGHT_SAMPLING) {
+                Col he = clamp_contrib(emission_of(m), rs.indirect_contribution_clamp, bounce > 0);
+                rcol += he * thr;
+                fl &= ~(NF_A | NF_B | NF_E1 | NF_E2 | NF_RIS_W | NF_IMM | NF_L);
+                fl |= NF_NOADD;
+                want_any[0] = want_any[1] = want_any[2] = false;
+                want_cl = false;
+            } else if (bounce == 0) {
+                rcol += emission_of(m);
+            }
+            store3(nr.thr, thr);
+            // ---------------- continuation (FullPathTracer.h:221-247) ----------------
+            if (bounce < A.last_bounce) {
+                float bpdf;
+                v3 bd;
+                Col bcol = bsdf_sample<OVR>(bc, m, vs, view, sn, gn, bd, bpdf, rng);
+                Col att = bcol * absr(dot(bd, sn)) / bpdf;
+                if (bpdf > 0.0f) {
+                    bool alive = true;
+                    if (bounce >= rs.russian_roulette_min_depth && rs.use_russian_roulette) {
+                        float sp;
+                        if (rs.path_russian_roulette_method == 0) sp = maxc(thr);
+                        else sp = sqrtf(maxc(thr * att) / maxc(thr));
+                        sp = minr(sp, 1.0f);
+                        if (rng() > sp) alive = false;
+                        else {
+                            float inc = 1.0f / sp;
+                            if (rs.russian_roulette_throughput_clamp > 0.0f) inc = minr(inc, rs.russian_roulette_throughput_clamp);
+                            thr *= inc;
+                        }
+                    }
+                    if (alive) {
+                        thr *= dispersion_ray_color(vs.wl, m.dispersion_scale);
+                        thr *= att;
+                        P.ray_o[slot] = make_float4(ip.x, ip.y, ip.z, __uint_as_float((uint32_t)prim));
+                        P.ray_d[slot] = make_float4(bd.x, bd.y, bd.z, INFINITY);
+                        cont = true;
+                    }
+                }
+            }
+        } else {
+            // miss (FullPathTracer.h:250-284)
+            const MptWorldSettings& ws = F.world_settings;
+            Col sky = col(0.0f);
+            if (ws.ambient_light_type == MPT_AMBIENT_UNIFORM || F.bsdf_flags.white_furnace_mode) sky = C3(ws.uniform_light_color);
+            else if (ws.ambient_light_type == MPT_AMBIENT_ENVMAP) {
+                bool sampled = F.options.envmap_sampling != MPT_ESS_NO_SAMPLING;
+                if (!sampled || bounce == 0) {
+                    sky = eval_env_no_pdf(S, F, d);
+                    bool unscale = sampled ? !ws.envmap_scale_background_intensity : (!ws.envmap_scale_background_intensity && bounce == 0);
+                    if (unscale) sky /= ws.envmap_intensity;
+                }
+            }
+            sky = clamp_contrib(sky, rs.envmap_contribution_clamp, true);
+            rcol += clamp_contrib(sky * thr, rs.indirect_contribution_clamp, bounce > 0);
+        }
+        nr.flags = fl;
+        if (fl & NF_SHADED) P.nee[slot] = nr;
+        else P.nee[slot].flags = 0;
+        P.rng[slot] = rng.s;
+        P.thr[slot] = make_float4(thr.r, thr.g, thr.b, 0.0f);
+        P.col[slot] = make_float4(rcol.r, rcol.g, rcol.b, 0.0f);
+        vs_store(P.vsA, P.vsB, slot, vs);
+    }
+    // queue appends (every lane of the wave takes part in the ballots)
+    int qi = wave_append(A.count_next, valid && cont);
+    if (valid && cont) A.q_next[qi] = slot;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        bool w = valid && want_any[k];
+        int ai = wave_append(&P.counters[CTR_ANY], w);
+        if (w) emit_query(P, 0, ai, q_o[k], last_prim, q_d[k], q_t[k], slot * 4 + k);
+    }
+    bool wc = valid && want_cl;
+    int ci = wave_append(&P.counters[CTR_CL], wc);
+    if (wc) emit_query(P, 1, ci, q_o[3], last_prim, q_d[3], q_t[3], slot * 4 + 3);
+}
+
+// ----------------------------------------------------------------------------------
+// k_resolve: finish the vertex's direct lighting with the NEE trace results
+// ----------------------------------------------------------------------------------
+struct ShadowLightHit { int prim; float dist; v3 sn; Col em; };
+DEV bool shadow_light_hit(const DevScene& S, float4 h, ShadowLightHit& out) {
+    int prim = (int)__float_as_uint(h.w);
+    if (prim < 0) return false;
+    const Mat& m = S.mats[S.mat_idx[prim]];
+    int3 ti = tri_idx(S, prim);
+    v2 uv = mk2(h.y, h.z);
+    v2 tc = uv_interp2(S.uv, ti, uv);
+    if (m.emission_texture_index != MPT_NO_TEXTURE) {
+        MptColor e; e.r = 0.0f; e.g = 0.0f; e.b = 0.0f;
+        if (S.n_tex > 0) prop_c(S, e, tc, m.emission_texture_index);
+        out.em = C3(e);
+    } else out.em = emission_of(m);
+    out.sn = shading_normal_of(S, normalize(tri_normal(S, prim)), prim, uv, tc);
+    out.prim = prim;
+    out.dist = h.x;
+    return true;
+}
+DEV float pdf_emissive_hit(const DevScene& S, const ShadowLightHit& h, v3 d) {
+    int3 ti = tri_idx(S, h.prim);
+    v3 A = ld3(S.pos, ti.x), B = ld3(S.pos, ti.y), C = ld3(S.pos, ti.z);
+    float area = length(cross(B - A, C - A)) * 0.5f;
+    float pdf = 1.0f / area;
+    pdf /= (float)S.n_emissive;
+    float cl = absr(dot(h.sn, -d));
+    pdf *= h.dist * h.dist;
+    pdf /= cl;
+    return pdf;
+}
+
+__global__ __launch_bounds__(TB) void k_resolve(DevScene S, DevPaths P, const MptFrame* __restrict__ Fp, int bounce,
+                                                const int32_t* q_cur, const int32_t* count_cur) {
+    const MptFrame& F = *Fp;
+    const MptRenderSettings& rs = F.render_settings;
+    int i = blockIdx.x * TB + threadIdx.x;
+    if (i >= *count_cur) return;
+    int slot = q_cur[i];
+    const NeeRec& nr = P.nee[slot];
+    uint32_t fl = nr.flags;
+    if (!(fl & NF_SHADED) || (fl & NF_NOADD)) return;
+    const int lss = F.options.direct_light_sampling;
+    Col ld = col(0.0f), ed = col(0.0f);
+    const uint8_t* occ = P.occ + (size_t)slot * 3;
+    if (fl & NF_IMM) ld = load3c(nr.imm);
+    else if (!(fl & NF_L)) ld = col(0.0f);
+    else if (lss == MPT_LSS_RIS_BSDF_AND_LIGHT) {
+        float wsum = nr.ris_wsum;
+        float cwb = 0.0f, targetb = 0.0f;
+        int trib = -1;
+        if (fl & NF_B) {
+            ShadowLightHit sh;
+            v3 dir = load3v(nr.dir);
+            if (shadow_light_hit(S, P.nhit[slot], sh) && !is_black(sh.em)) {
+                Col lc = load3c(nr.b) * sh.em * nr.b_cos;
+                targetb = lum(lc);
+                float lpdf = pdf_emissive_hit(S, sh, dir);
+                lpdf *= (fl & NF_B_REFR) ? 0.0f : 1.0f;
+                if (!min_contrib(rs.minimum_light_contribution, lc / lpdf / nr.b_pdf)) targetb = 0.0f;
+                float w = balance(nr.b_pdf, (float)rs.ris_number_of_bsdf_candidates, lpdf, (float)rs.ris_number_of_light_candidates);
+                cwb = w * targetb / nr.b_pdf;
+                trib = sh.prim;
+            }
+        }
+        bool bsdf_wins = false;
+        if (rs.ris_number_of_bsdf_candidates > 0) {
+            wsum += cwb;
+            bsdf_wins = nr.r_add < cwb / wsum;
+        }
+        // RISReservoir::end (RIS_Reservoir.h:45-51); wsum > 0 implies a winner exists
+        float target = bsdf_wins ? targetb : ((fl & NF_RIS_W) ? nr.ris_target : 0.0f);
+        float ucw = wsum == 0.0f ? 0.0f : 1.0f / target * wsum;
+        if (ucw > 0.0f) {
+            if (bsdf_wins) {
+                float c = nr.b_cos;
+                if (c > 0.0f) ld = load3c(nr.b) * ucw * emission_of(S.mats[S.mat_idx[trib]]) * c;
+            } else if (!occ[0]) {
+                float c = nr.a_cos;
+                if (c > 0.0f) ld = load3c(nr.a) * ucw * emission_of(S.mats[S.mat_idx[nr.ris_tri]]) * c;
+            }
+        }
+    } else if (lss == MPT_LSS_MIS_LIGHT_BSDF) {
+        Col lrad = col(0.0f), brad = col(0.0f);
+        if ((fl & NF_A) && !occ[0]) lrad = load3c(nr.a);
+        if (fl & NF_B) {
+            ShadowLightHit sh;
+            v3 dir = load3v(nr.dir);
+            if (shadow_light_hit(S, P.nhit[slot], sh) && !is_black(sh.em)) {
+                float lp2 = pdf_emissive_hit(S, sh, dir);
+                float w = balance(nr.b_pdf, lp2);
+                brad = load3c(nr.b) * nr.b_cos * sh.em * w / nr.b_pdf;
+            }
+        }
+        ld = lrad + brad;
+    } else if (lss == MPT_LSS_UNIFORM_ONE_LIGHT) {
+        if ((fl & NF_A) && !occ[0]) ld = load3c(nr.a);
+    } else if (lss == MPT_LSS_BSDF) {
+        if (fl & NF_B) {
+            ShadowLightHit sh;
+            if (shadow_light_hit(S, P.nhit[slot], sh) && !is_black(sh.em))
+                ld = load3c(nr.b) * nr.b_cos * sh.em / nr.b_pdf;
+        }
+    }
+    // sample_many_lights: / number_of_light_samples (= 1, validated on the host)
+    if ((fl & NF_L) && !(fl & NF_IMM)) ld = ld / (float)rs.number_of_light_samples;
+    {
+        Col e2 = col(0.0f), e1 = col(0.0f);
+        if ((fl & NF_E2) && !occ[2]) e2 = load3c(nr.e2);
+        if ((fl & NF_E1) && !occ[1]) e1 = load3c(nr.e1);
+        ed = e2 + e1;
+    }
+    ld = clamp_contrib(ld, rs.direct_contribution_clamp, bounce == 0);
+    ed = clamp_contrib(ed, rs.envmap_contribution_clamp, bounce == 0);
+    Col ind = (ld + ed) * load3c(nr.thr);
+    float4 cv = P.col[slot];
+    Col rc = col(cv.x, cv.y, cv.z) + clamp_contrib(ind, rs.indirect_contribution_clamp, bounce > 0);
+    P.col[slot] = make_float4(rc.r, rc.g, rc.b, 0.0f);
+}
+
+// ----------------------------------------------------------------------------------
+// k_accumulate (FullPathTracer.h:292-327)
+// ----------------------------------------------------------------------------------
+__global__ __launch_bounds__(TB) void k_accumulate(DevPaths P, const MptFrame* __restrict__ Fp) {
+    const MptFrame& F = *Fp;
+    const MptRenderSettings& rs = F.render_settings;
+    int slot = blockIdx.x * TB + threadIdx.x;
+    if (slot >= P.n) return;
+    float4 cv = P.col[slot];
+    Col c = col(cv.x, cv.y, cv.z);
+    float wl = __uint_as_float(P.vsB[slot].w);
+    bool invalid = false;
+    if (wl == 0.0f) invalid |= (c.r < 0 || c.g < 0 || c.b < 0);
+    invalid |= has_nan(c);
+    float* fb = P.fb_color + 3 * (size_t)slot;
+    if (invalid) {
+        if (rs.display_NaNs) {
+            Col dc = col(1.0e30f, 0.0f, 1.0e30f);
+            if (rs.sample_number != 0) dc = dc * (float)rs.sample_number;
+            fb[0] = dc.r; fb[1] = dc.g; fb[2] = dc.b;
+        }
+        return;
+    }
+    if (rs.sample_number == 0) { fb[0] = c.r; fb[1] = c.g; fb[2] = c.b; }
+    else { fb[0] += c.r; fb[1] += c.g; fb[2] += c.b; }
+    float cnt = (float)rs.denoiser_AOV_accumulation_counter;
+    float4 a = P.alb[slot], n = P.nrm[slot];
+    float* fa = P.fb_albedo + 3 * (size_t)slot;
+    float* fn = P.fb_normal + 3 * (size_t)slot;
+    if (rs.sample_number == 0) {
+        fa[0] = a.x; fa[1] = a.y; fa[2] = a.z;
+        fn[0] = n.x; fn[1] = n.y; fn[2] = n.z;
+    } else {
+        fa[0] = (fa[0] * cnt + a.x) / (cnt + 1.0f);
+        fa[1] = (fa[1] * cnt + a.y) / (cnt + 1.0f);
+        fa[2] = (fa[2] * cnt + a.z) / (cnt + 1.0f);
+        v3 acc = (mk3(fn[0], fn[1], fn[2]) * cnt + mk3(n.x, n.y, n.z)) / (cnt + 1.0f);
+        float len = length(acc);
+        if (!is_zero(len)) { acc = acc / len; fn[0] = acc.x; fn[1] = acc.y; fn[2] = acc.z; }
+    }
+}
+
+// ----------------------------------------------------------------------------------
+// host launch glue
+// ----------------------------------------------------------------------------------
+static int blocks_for(int n) { return (n + TB - 1) / TB; }
+
+template <int MODE>
+static void launch_trace_mode(const TraceArgs& a, int grid, bool stats, hipStream_t st) {
+    if (stats) hipLaunchKernelGGL((k_trace<MODE, true>), dim3(grid), dim3(TB), 0, st, a);
+    else hipLaunchKernelGGL((k_trace<MODE, false>), dim3(grid), dim3(TB), 0, st, a);
+}
+
+template <int MODE>
+static void timed_trace(const TraceArgs& a, LaunchCfg& cfg, hipStream_t st) {
+    bool timed = cfg.ev_pool && cfg.ev_used + 2 <= cfg.ev_cap;
+    if (timed) hipEventRecord(cfg.ev_pool[cfg.ev_used], st);
+    launch_trace_mode<MODE>(a, cfg.grid_persistent, cfg.stats, st);
+    if (timed) { hipEventRecord(cfg.ev_pool[cfg.ev_used + 1], st); cfg.ev_used += 2; }
+    cfg.launches++;
+}
+
+hipError_t launch_frame(const DevScene& S, const DevPaths& P, const MptFrame* d_frame, const MptFrame& hf, LaunchCfg& cfg,
+                        hipStream_t st) {
+    const int n = P.n;
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_camera, dim3(blocks_for(n)), dim3(TB), 0, st, P, d_frame);
+    hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(&P.counters[CTR_Q0]), n, 1, st);
+    int32_t* q_cur = P.q0;
+    int32_t* q_next = P.q1;
+    int c_cur = CTR_Q0, c_next = CTR_Q1;
+    const int nb = hf.render_settings.nb_bounces;
+    for (int b = 0; b <= nb; b++) {
+        // continuation / camera rays
+        hipMemsetAsync(&P.counters[CTR_FETCH], 0, sizeof(int32_t), st);
+        TraceArgs ta{};
+        ta.S = S; ta.P = P; ta.queue = q_cur; ta.count_ptr = &P.counters[c_cur]; ta.fetch = &P.counters[CTR_FETCH];
+        timed_trace<TM_PATH>(ta, cfg, st);
+        hipMemsetAsync(&P.counters[c_next], 0, sizeof(int32_t), st);
+        hipMemsetAsync(&P.counters[CTR_ANY], 0, 2 * sizeof(int32_t), st);
+        ShadeArgs sa;
+        sa.S = S; sa.P = P; sa.F = d_frame; sa.bounce = b; sa.last_bounce = nb;
+        sa.q_cur = q_cur; sa.count_cur = &P.counters[c_cur]; sa.q_next = q_next; sa.count_next = &P.counters[c_next];
+        if (hf.options.bsdf_override == MPT_BSDF_LAMBERTIAN)
+            hipLaunchKernelGGL((k_shade<MPT_BSDF_LAMBERTIAN>), dim3(blocks_for(n)), dim3(TB), 0, st, sa);
+        else
+            hipLaunchKernelGGL((k_shade<MPT_BSDF_NONE>), dim3(blocks_for(n)), dim3(TB), 0, st, sa);
+        // NEE queries
+        hipMemsetAsync(&P.counters[CTR_FETCH], 0, sizeof(int32_t), st);
+        TraceArgs tn{};
+        tn.S = S; tn.P = P; tn.count_ptr = &P.counters[CTR_ANY]; tn.fetch = &P.counters[CTR_FETCH];
+        timed_trace<TM_NEE_ANY>(tn, cfg, st);
+        hipMemsetAsync(&P.counters[CTR_FETCH], 0, sizeof(int32_t), st);
+        tn.count_ptr = &P.counters[CTR_CL];
+        timed_trace<TM_NEE_CLOSEST>(tn, cfg, st);
+        hipLaunchKernelGGL(k_resolve, dim3(blocks_for(n)), dim3(TB), 0, st, S, P, d_frame, b, q_cur, &P.counters[c_cur]);
+        // swap queues
+        int32_t* tq = q_cur; q_cur = q_next; q_next = tq;
+        int tc = c_cur; c_cur = c_next; c_next = tc;
+    }
+    hipLaunchKernelGGL(k_accumulate, dim3(blocks_for(n)), dim3(TB), 0, st, P, d_frame);
+    return hipGetLastError();
+}
+
+hipError_t launch_trace_raw(const DevScene& S, const float4* o, const float4* d, int n, bool any, float4* out_hit,
+                            uint8_t* out_occ, int32_t* fetch_ctr, uint32_t* spill, int grid, hipStream_t st) {
+    TraceArgs a{};
+    a.S = S;
+    a.P.stack_spill = spill;
+    a.count_const = n;
+    a.fetch = fetch_ctr;
+    a.raw_o = o;
+    a.raw_d = d;
+    a.raw_hit = out_hit;
+    a.raw_occ = out_occ;
+    hipMemsetAsync(fetch_ctr, 0, sizeof(int32_t), st);
+    if (any) hipLaunchKernelGGL((k_trace<TM_RAW_ANY, false>), dim3(grid), dim3(TB), 0, st, a);
+    else hipLaunchKernelGGL((k_trace<TM_RAW_CLOSEST, false>), dim3(grid), dim3(TB), 0, st, a);
+    return hipGetLastError();
+}
+
+}  // namespace mpt

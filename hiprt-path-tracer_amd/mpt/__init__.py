@@ -1,0 +1,216 @@
+"""mpt -- MI355X path tracer: Python binding of libmpt.so (include/mpt.h).
+
+``GPURenderer`` mirrors the launch surface of the reference's
+``GPURenderer`` (src/Renderer/GPURenderer.h:69-260): a scene is uploaded once, the
+envmap / LUTs are set, and every ``render()`` call enqueues one sample per pixel on the
+context's HIP stream (``GPURenderer::render``, GPURenderer.cpp:245-271), accumulating
+into the 'pixels' sum buffer and the denoiser AOVs.
+
+There is no CPU fallback: if libmpt.so is missing or no HIP device exists, the
+constructor raises.  Build the library with ``python -m mpt._build`` or
+``__graft_entry__.build()``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import abi
+from . import scene
+from ._build import LIB_PATH
+
+__all__ = ["abi", "scene", "lib", "GPURenderer", "MptError", "build_envmap", "partition_rows"]
+
+SYMBOLS = [
+    "mpt_last_error", "mpt_version", "mpt_abi_sizes", "mpt_create", "mpt_destroy", "mpt_upload_scene",
+    "mpt_update_materials", "mpt_set_envmap", "mpt_build_alias_table", "mpt_set_luts", "mpt_resize",
+    "mpt_render_frame", "mpt_synchronize", "mpt_query_done", "mpt_get_framebuffer", "mpt_partition_rows",
+    "mpt_enable_stats", "mpt_get_stats", "mpt_trace_closest", "mpt_trace_any",
+]
+
+
+class MptError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"mpt error {code}: {msg}")
+        self.code = code
+
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    """Loads the in-tree libmpt.so (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"libmpt.so not found at {LIB_PATH}; run __graft_entry__.build() (no CPU fallback)")
+    L = C.CDLL(str(LIB_PATH))
+    vp, i32, f32 = C.c_void_p, C.c_int32, C.c_float
+    L.mpt_last_error.restype = C.c_char_p
+    L.mpt_abi_sizes.argtypes = [vp, C.c_int]
+    L.mpt_create.argtypes = [C.c_int, vp, C.POINTER(vp)]
+    L.mpt_destroy.argtypes = [vp]
+    L.mpt_upload_scene.argtypes = [vp, C.POINTER(abi.Scene)]
+    L.mpt_update_materials.argtypes = [vp, vp, i32]
+    L.mpt_set_envmap.argtypes = [vp, vp, i32, i32, vp, vp, f32]
+    L.mpt_build_alias_table.argtypes = [vp, i32, i32, vp, vp, vp]
+    L.mpt_set_luts.argtypes = [vp, C.POINTER(abi.Luts)]
+    L.mpt_resize.argtypes = [vp, i32, i32]
+    L.mpt_render_frame.argtypes = [vp, C.POINTER(abi.Frame)]
+    L.mpt_synchronize.argtypes = [vp]
+    L.mpt_query_done.argtypes = [vp, C.POINTER(C.c_int)]
+    L.mpt_get_framebuffer.argtypes = [vp, C.c_int, vp, C.c_int]
+    L.mpt_partition_rows.argtypes = [i32, i32, i32, i32]
+    L.mpt_enable_stats.argtypes = [vp, C.c_int, C.c_int]
+    L.mpt_get_stats.argtypes = [vp, C.POINTER(abi.Stats)]
+    L.mpt_trace_closest.argtypes = [vp, vp, vp, i32, vp, vp, vp, vp, C.c_int]
+    L.mpt_trace_any.argtypes = [vp, vp, vp, i32, vp, C.c_int]
+    _lib = L
+    return L
+
+
+def _check(rc):
+    if rc != 0:
+        raise MptError(rc, lib().mpt_last_error().decode(errors="replace"))
+
+
+def _p(a):
+    return None if a is None else C.c_void_p(a.ctypes.data)
+
+
+def abi_sizes():
+    out = np.zeros(6, np.int32)
+    _check(lib().mpt_abi_sizes(_p(out), 6))
+    return dict(zip(["Material", "RenderSettings", "WorldSettings", "Camera", "Frame", "Scene"], out.tolist()))
+
+
+def partition_rows(res_y, band_height, band_index, band_count):
+    return lib().mpt_partition_rows(res_y, band_height, band_index, band_count)
+
+
+def build_envmap(rgba):
+    """float32 [H, W, 4] (already flipped as the reference's loader does) -> envmap dict
+    with the alias table of Image32Bit::compute_alias_table (Image.cpp:579-659)."""
+    rgba = np.ascontiguousarray(rgba, np.float32)
+    h, w = rgba.shape[:2]
+    probas = np.zeros(h * w, np.float32)
+    alias = np.full(h * w, -1, np.int32)
+    s = np.zeros(1, np.float32)
+    _check(lib().mpt_build_alias_table(_p(rgba), w, h, _p(probas), _p(alias), _p(s)))
+    alias = np.where(alias < 0, np.arange(h * w, dtype=np.int32), alias).astype(np.int32)
+    return {"rgba": rgba, "probas": probas, "alias": alias, "width": w, "height": h, "sum": float(s[0])}
+
+
+class GPURenderer:
+    """One renderer context on one GPU (GPURenderer.h:69)."""
+
+    def __init__(self, device: int = 0, stream: int | None = None):
+        L = lib()
+        h = C.c_void_p()
+        _check(L.mpt_create(device, C.c_void_p(stream) if stream else None, C.byref(h)))
+        self.h = h
+        self.device = device
+        self.frame = None
+        self._n_mats = 0
+
+    # --- scene / resources -----------------------------------------------------
+    def set_scene(self, sd: "scene.SceneData"):
+        """GPURenderer::set_scene (GPURenderer.cpp:1052-1130)."""
+        s = sd.to_abi()
+        _check(lib().mpt_upload_scene(self.h, C.byref(s)))
+        self._n_mats = len(sd.materials)
+
+    def update_materials(self, materials):
+        arr = (abi.Material * len(materials))(*materials)
+        _check(lib().mpt_update_materials(self.h, C.cast(arr, C.c_void_p), len(materials)))
+
+    def set_envmap(self, env):
+        """GPURenderer::set_envmap (GPURenderer.cpp:1136-1174); env from build_envmap() or None."""
+        if env is None:
+            _check(lib().mpt_set_envmap(self.h, None, 0, 0, None, None, 0.0))
+            return
+        self._env = env
+        _check(lib().mpt_set_envmap(self.h, _p(env["rgba"]), env["width"], env["height"], _p(env["probas"]),
+                                    _p(env["alias"]), env["sum"]))
+
+    def set_luts(self, luts=None):
+        luts = luts if luts is not None else scene.load_luts()
+        L = scene.luts_to_abi(luts)
+        _check(lib().mpt_set_luts(self.h, C.byref(L)))
+
+    def resize(self, w, h):
+        _check(lib().mpt_resize(self.h, w, h))
+
+    # --- frames --------------------------------------------------------------------
+    def render(self, frame: "abi.Frame"):
+        """Enqueues one sample per pixel (asynchronous)."""
+        _check(lib().mpt_render_frame(self.h, C.byref(frame)))
+        self.frame = frame
+
+    def synchronize_kernel(self):
+        _check(lib().mpt_synchronize(self.h))
+
+    def frame_render_done(self) -> bool:
+        d = C.c_int()
+        _check(lib().mpt_query_done(self.h, C.byref(d)))
+        return bool(d.value)
+
+    def rows(self):
+        f = self.frame
+        return partition_rows(f.res_y, f.band_height, f.band_index, f.band_count)
+
+    def framebuffer(self, kind=abi.FB_COLOR):
+        """Copies the partition's rows (band-major, increasing y) -> float32 [rows, W, 3]."""
+        f = self.frame
+        out = np.zeros((self.rows(), f.res_x, 3), np.float32)
+        _check(lib().mpt_get_framebuffer(self.h, kind, _p(out), 0))
+        return out
+
+    def framebuffer_to_device(self, kind, dev_ptr: int):
+        _check(lib().mpt_get_framebuffer(self.h, kind, C.c_void_p(dev_ptr), 1))
+
+    # --- stats / queries -------------------------------------------------------
+    def enable_stats(self, timing=True, instrumented=False):
+        _check(lib().mpt_enable_stats(self.h, int(timing), int(instrumented)))
+
+    def stats(self) -> "abi.Stats":
+        s = abi.Stats()
+        _check(lib().mpt_get_stats(self.h, C.byref(s)))
+        return s
+
+    def trace_closest(self, rays, last_hit=None):
+        rays = np.ascontiguousarray(rays, np.float32).reshape(-1, 8)
+        n = len(rays)
+        prim = np.empty(n, np.int32)
+        t, u, v = (np.empty(n, np.float32) for _ in range(3))
+        lh = None if last_hit is None else np.ascontiguousarray(last_hit, np.int32)
+        _check(lib().mpt_trace_closest(self.h, _p(rays), _p(lh), n, _p(prim), _p(t), _p(u), _p(v), 0))
+        return prim, t, u, v
+
+    def trace_any(self, rays, last_hit=None):
+        rays = np.ascontiguousarray(rays, np.float32).reshape(-1, 8)
+        n = len(rays)
+        occ = np.empty(n, np.uint8)
+        lh = None if last_hit is None else np.ascontiguousarray(last_hit, np.int32)
+        _check(lib().mpt_trace_any(self.h, _p(rays), _p(lh), n, _p(occ), 0))
+        return occ.astype(bool)
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().mpt_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()

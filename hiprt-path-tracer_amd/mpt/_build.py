@@ -1,0 +1,73 @@
+"""Builds libmpt.so (the HIP path tracer + C ABI) in-tree for gfx950.
+
+Plain hipcc invocations, compiled in parallel, relinked only when a source or
+header is newer than the library.  Used by ``__graft_entry__.build()`` and by the
+test-suite; never invoked implicitly by the product path (``mpt.lib()`` fails
+loudly when the library is missing).
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+PKG_DIR = Path(__file__).resolve().parent
+ROOT = PKG_DIR.parent
+CSRC = ROOT / "csrc"
+INCLUDE = ROOT.parent / "include"
+LIB_PATH = PKG_DIR / "libmpt.so"
+OBJ_DIR = CSRC / "build"
+
+SOURCES = ["bvh8.cpp", "mpt_kernels.hip", "mpt_api.cpp"]
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = "gfx950"
+CXXFLAGS = [
+    f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
+    "-Wno-unused-result", "-Wno-unused-value", f"-I{INCLUDE}", f"-I{CSRC}",
+]
+
+
+def _deps() -> list[Path]:
+    return [CSRC / s for s in SOURCES] + sorted(CSRC.glob("*.h")) + sorted(INCLUDE.glob("*.h"))
+
+
+def up_to_date() -> bool:
+    if not LIB_PATH.exists():
+        return False
+    t = LIB_PATH.stat().st_mtime
+    return all(p.stat().st_mtime <= t for p in _deps())
+
+
+def build(force: bool = False, verbose: bool = True) -> Path:
+    if not force and up_to_date():
+        return LIB_PATH
+    OBJ_DIR.mkdir(exist_ok=True)
+    procs = []
+    objs = []
+    for s in SOURCES:
+        obj = OBJ_DIR / (Path(s).stem + ".o")
+        objs.append(obj)
+        cmd = [HIPCC, *CXXFLAGS, "-c", str(CSRC / s), "-o", str(obj)]
+        if verbose:
+            print("[mpt build]", " ".join(cmd), file=sys.stderr)
+        procs.append((s, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))
+    errors = []
+    for s, p in procs:
+        out, _ = p.communicate()
+        if p.returncode != 0:
+            errors.append(f"{s}:\n{out.decode(errors='replace')}")
+    if errors:
+        raise RuntimeError("libmpt build failed:\n" + "\n".join(errors))
+    tmp = LIB_PATH.with_suffix(".so.tmp")
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp), *map(str, objs)]
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+    if r.returncode != 0:
+        raise RuntimeError("libmpt link failed:\n" + r.stdout.decode(errors="replace"))
+    os.replace(tmp, LIB_PATH)
+    return LIB_PATH
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv)
+    print(LIB_PATH)

@@ -1,0 +1,431 @@
+"""Host-side scene preparation: glTF -> the flat arrays of the reference's ``Scene``.
+
+The reference ingests scenes with ASSIMP (``SceneParser::parse_scene_file``,
+src/Scene/SceneParser.cpp:22-220, flags PreTransformVertices | Triangulate) and
+produces flat SoA arrays (``Scene``, SceneParser.h:80-131).  ASSIMP is an empty
+submodule in the reference snapshot, so this module restates the parts of its glTF2
+importer that the reference consumes:
+
+* one output mesh per (material) in material order (PreTransformVertices joins the
+  node-transformed primitives sharing a material);
+* material parameters read as ``SceneParser::read_material_properties``
+  (SceneParser.cpp:366-407) reads them from ASSIMP's glTF2 material keys, then
+  ``make_safe`` + ``precompute_properties`` (HostDeviceCommon/Material.h:44-71);
+* the emissive triangle list of ``ThreadFunctions::load_scene_parse_emissive_triangles``
+  (Threads/ThreadFunctions.cpp:116-143);
+* the camera of ``SceneParser::parse_camera`` (SceneParser.cpp:222-276) and
+  ``Camera::to_hiprt`` / ``get_view_matrix`` (Scene/Camera.cpp:9-45), including the
+  reference's '+0.425 rad' vertical-FOV term and its matrix conventions.
+
+ASSIMP's own conversions (glTF yfov -> mHorizontalFOV = yfov * aspect, default
+material values) are assumptions of this restatement; they only
+decide which scene is rendered, not the renderer's parity, since the oracle and the
+HIP path consume the same arrays.
+"""
+import json
+import math
+import os
+
+import numpy as np
+
+from . import abi
+
+_COMP = {5120: np.int8, 5121: np.uint8, 5122: np.int16, 5123: np.uint16, 5125: np.uint32, 5126: np.float32}
+_NCOMP = {"SCALAR": 1, "VEC2": 2, "VEC3": 3, "VEC4": 4, "MAT4": 16}
+
+DATA_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))), "data")
+
+
+class SceneData:
+    """Flat arrays + materials, i.e. what ``mpt_upload_scene`` receives."""
+
+    def __init__(self):
+        self.triangle_indices = None  # int32 [T*3]
+        self.vertices = None          # float32 [V,3]
+        self.normals = None           # float32 [V,3]
+        self.has_normals = None       # uint8 [V]
+        self.texcoords = None         # float32 [V,2]
+        self.material_indices = None  # int32 [T]
+        self.materials = []           # list[abi.Material]
+        self.emissive = None          # int32 [E]
+        self.textures = []            # list of uint8 [h, w, 4]
+        self.camera_info = None       # dict for make_camera
+        self.name = ""
+
+    @property
+    def num_triangles(self):
+        return len(self.material_indices)
+
+    def finalize(self):
+        self.emissive = np.array([i for i, m in enumerate(self.material_indices)
+                                  if _is_emissive(self.materials[m])], np.int32)
+        return self
+
+    def to_abi(self):
+        """Builds an abi.Scene (keeps references to the numpy arrays alive on self)."""
+        C = abi.C
+        s = abi.Scene()
+        self._keep = []
+
+        def ptr(a, t):
+            a = np.ascontiguousarray(a)
+            self._keep.append(a)
+            return a.ctypes.data_as(C.POINTER(t))
+
+        s.triangle_indices = ptr(self.triangle_indices.astype(np.int32), abi.i32)
+        s.num_triangles = self.num_triangles
+        s.vertices = ptr(self.vertices.astype(np.float32), abi.f32)
+        s.vertex_normals = ptr(self.normals.astype(np.float32), abi.f32)
+        s.has_vertex_normals = ptr(self.has_normals.astype(np.uint8), C.c_uint8)
+        s.texcoords = ptr(self.texcoords.astype(np.float32), abi.f32)
+        s.num_vertices = len(self.vertices)
+        s.material_indices = ptr(self.material_indices.astype(np.int32), abi.i32)
+        mats = (abi.Material * len(self.materials))(*self.materials)
+        self._keep.append(mats)
+        s.materials = C.cast(mats, C.POINTER(abi.Material))
+        s.num_materials = len(self.materials)
+        s.emissive_triangle_indices = ptr(self.emissive.astype(np.int32) if len(self.emissive) else np.zeros(1, np.int32), abi.i32)
+        s.num_emissive_triangles = len(self.emissive)
+        s.num_textures = len(self.textures)
+        if self.textures:
+            texs = [np.ascontiguousarray(t, dtype=np.uint8) for t in self.textures]
+            self._keep.extend(texs)
+            arr = (C.POINTER(C.c_uint8) * len(texs))(*[t.ctypes.data_as(C.POINTER(C.c_uint8)) for t in texs])
+            self._keep.append(arr)
+            s.texture_data = C.cast(arr, C.POINTER(C.POINTER(C.c_uint8)))
+            dims = np.array([[t.shape[1], t.shape[0]] for t in texs], np.int32).ravel()
+            s.texture_dims = ptr(dims, abi.i32)
+        return s
+
+
+def _is_emissive(m):
+    """SimplifiedRendererMaterial::is_emissive (Material.h:35-41) && !emissive_texture_used."""
+    f = np.float32
+    e, k = m.emission, f(m.emission_strength)
+    nz = lambda v: not (f(v) * k < f(1e-10) and f(v) * k > f(-1e-10))
+    return (nz(e.r) or nz(e.g) or nz(e.b) or m.emissive_texture_used) and not m.emissive_texture_used
+
+
+def _quat_to_mat(q):
+    x, y, z, w = q
+    return np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - z * w), 2 * (x * z + y * w)],
+                     [2 * (x * y + z * w), 1 - 2 * (x * x + z * z), 2 * (y * z - x * w)],
+                     [2 * (x * z - y * w), 2 * (y * z + x * w), 1 - 2 * (x * x + y * y)]], np.float64)
+
+
+def _node_matrix(n):
+    if "matrix" in n:
+        return np.array(n["matrix"], np.float64).reshape(4, 4).T
+    m = np.eye(4)
+    t = n.get("translation", [0, 0, 0])
+    r = n.get("rotation", [0, 0, 0, 1])
+    s = n.get("scale", [1, 1, 1])
+    m[:3, :3] = _quat_to_mat(r) @ np.diag(s)
+    m[:3, 3] = t
+    return m
+
+
+def _accessor(g, bins, idx):
+    a = g["accessors"][idx]
+    bv = g["bufferViews"][a["bufferView"]]
+    dt = np.dtype(_COMP[a["componentType"]])
+    n = _NCOMP[a["type"]]
+    off = bv.get("byteOffset", 0) + a.get("byteOffset", 0)
+    stride = bv.get("byteStride", 0)
+    buf = bins[bv["buffer"]]
+    cnt = a["count"]
+    if stride and stride != n * dt.itemsize:
+        arr = np.ndarray((cnt, n), dt, buf, off, (stride, dt.itemsize))
+    else:
+        arr = np.frombuffer(buf, dt, cnt * n, off).reshape(cnt, n)
+    return np.array(arr)
+
+
+def _material_from_gltf(gm):
+    """SceneParser::read_material_properties on ASSIMP's glTF2 material keys."""
+    m = abi.Material.default()
+    pbr = gm.get("pbrMetallicRoughness", {})
+    bc = pbr.get("baseColorFactor", [1.0, 1.0, 1.0, 1.0])
+    m.base_color = abi.Color(*bc[:3])
+    ext = gm.get("extensions", {})
+    if m.emission_texture_index == -1:
+        m.emission = abi.Color(*gm.get("emissiveFactor", [0.0, 0.0, 0.0]))
+    if "KHR_materials_emissive_strength" in ext:
+        m.emission_strength = ext["KHR_materials_emissive_strength"].get("emissiveStrength", 1.0)
+    m.metallic = pbr.get("metallicFactor", 1.0)
+    m.roughness = pbr.get("roughnessFactor", 1.0)
+    if "KHR_materials_anisotropy" in ext:
+        m.anisotropy = ext["KHR_materials_anisotropy"].get("anisotropyStrength", 0.0)
+    if "KHR_materials_sheen" in ext:
+        sh = ext["KHR_materials_sheen"]
+        m.sheen_color = abi.Color(*sh.get("sheenColorFactor", [0.0, 0.0, 0.0]))
+        m.sheen_roughness = sh.get("sheenRoughnessFactor", 0.0)
+        m.sheen = 1.0
+    if "KHR_materials_specular" in ext:
+        m.specular = ext["KHR_materials_specular"].get("specularFactor", 1.0)
+        m.specular_tint = 1.0
+        m.specular_color = abi.Color(1.0)
+    if "KHR_materials_clearcoat" in ext:
+        cc = ext["KHR_materials_clearcoat"]
+        m.coat = cc.get("clearcoatFactor", 0.0)
+        m.coat_roughness = cc.get("clearcoatRoughnessFactor", 0.0)
+    if "KHR_materials_ior" in ext:
+        m.ior = ext["KHR_materials_ior"].get("ior", 1.5)
+    if "KHR_materials_transmission" in ext:
+        m.specular_transmission = ext["KHR_materials_transmission"].get("transmissionFactor", 0.0)
+    if "KHR_materials_volume" in ext:
+        v = ext["KHR_materials_volume"]
+        if "attenuationColor" in v:
+            m.absorption_color = abi.Color(*v["attenuationColor"])
+        if "attenuationDistance" in v:
+            m.absorption_at_distance = v["attenuationDistance"]
+    if gm.get("alphaMode", "OPAQUE") != "OPAQUE":
+        m.alpha_opacity = bc[3]
+    m.make_safe()
+    m.precompute_properties()
+    return m
+
+
+def load_gltf(path, aspect_override=None):
+    """Loads a .gltf (+ .bin) into SceneData."""
+    with open(path) as f:
+        g = json.load(f)
+    base = os.path.dirname(path)
+    bins = []
+    for b in g.get("buffers", []):
+        with open(os.path.join(base, b["uri"]), "rb") as f:
+            bins.append(f.read())
+
+    # world transforms
+    world = {}
+
+    def visit(ni, parent):
+        n = g["nodes"][ni]
+        m = parent @ _node_matrix(n)
+        world[ni] = m
+        for c in n.get("children", []):
+            visit(c, m)
+
+    scene_idx = g.get("scene", 0)
+    roots = g["scenes"][scene_idx]["nodes"] if "scenes" in g else list(range(len(g["nodes"])))
+    for r in roots:
+        visit(r, np.eye(4))
+
+    materials_json = g.get("materials", [])
+    n_mat = len(materials_json)
+    # instances: (material, positions, normals or None, texcoords or None, indices)
+    inst = []
+    need_default = False
+    for ni, n in enumerate(g["nodes"]):
+        if "mesh" not in n or ni not in world:
+            continue
+        M = world[ni]
+        R = M[:3, :3]
+        RIT = np.linalg.inv(R).T
+        for prim in g["meshes"][n["mesh"]]["primitives"]:
+            if prim.get("mode", 4) != 4:
+                continue
+            att = prim["attributes"]
+            pos = _accessor(g, bins, att["POSITION"]).astype(np.float64)
+            pos = (pos @ R.T + M[:3, 3]).astype(np.float32)
+            nrm = None
+            if "NORMAL" in att:
+                nrm = _accessor(g, bins, att["NORMAL"]).astype(np.float64) @ RIT.T
+                nrm /= np.maximum(np.linalg.norm(nrm, axis=1, keepdims=True), 1e-30)
+                nrm = nrm.astype(np.float32)
+            uv = _accessor(g, bins, att["TEXCOORD_0"]).astype(np.float32) if "TEXCOORD_0" in att else None
+            if "indices" in prim:
+                idx = _accessor(g, bins, prim["indices"]).astype(np.int64).ravel()
+            else:
+                idx = np.arange(len(pos), dtype=np.int64)
+            mi = prim.get("material")
+            if mi is None:
+                need_default = True
+                mi = n_mat
+            inst.append((mi, pos, nrm, uv, idx.reshape(-1, 3)))
+
+    total_mats = n_mat + (1 if need_default else 0)
+    mats = [_material_from_gltf(gm) for gm in materials_json]
+    if need_default:
+        mats.append(_material_from_gltf({}))
+
+    sd = SceneData()
+    sd.name = os.path.splitext(os.path.basename(path))[0]
+    tri, verts, nrms, hasn, uvs, mids = [], [], [], [], [], []
+    voff = 0
+    # PreTransformVertices: output meshes ordered by material index
+    for mi in range(total_mats):
+        for (m, pos, nrm, uv, idx) in inst:
+            if m != mi:
+                continue
+            tri.append(idx + voff)
+            verts.append(pos)
+            nrms.append(nrm if nrm is not None else np.zeros_like(pos))
+            hasn.append(np.full(len(pos), 1 if nrm is not None else 0, np.uint8))
+            # texcoords only kept when the material has textures (SceneParser.cpp:136-141)
+            uvs.append(np.zeros((len(pos), 2), np.float32))
+            mids.append(np.full(len(idx), mi, np.int32))
+            voff += len(pos)
+    sd.triangle_indices = np.concatenate(tri).astype(np.int32).ravel()
+    sd.vertices = np.concatenate(verts).astype(np.float32)
+    sd.normals = np.concatenate(nrms).astype(np.float32)
+    sd.has_normals = np.concatenate(hasn)
+    sd.texcoords = np.concatenate(uvs)
+    sd.material_indices = np.concatenate(mids)
+    sd.materials = mats
+
+    cams = [(ni, n) for ni, n in enumerate(g["nodes"]) if "camera" in n and ni in world]
+    if cams:
+        ni, n = cams[0]
+        cam = g["cameras"][n["camera"]]
+        p = cam.get("perspective", {})
+        aspect = p.get("aspectRatio", 16.0 / 9.0)
+        M = world[ni]
+        sd.camera_info = dict(position=M[:3, 3].copy(), lookat=M[:3, :3] @ np.array([0.0, 0.0, -1.0]),
+                              up=M[:3, :3] @ np.array([0.0, 1.0, 0.0]),
+                              hfov=p.get("yfov", 0.7) * (aspect if aspect != 0 else 1.0),
+                              aspect=aspect, znear=p.get("znear", 0.1), zfar=p.get("zfar", 100.0))
+    return sd.finalize()
+
+
+def load_scene(name):
+    """Loads a scene shipped in data/scenes (copied from the reference's data/GLTFs)."""
+    return load_gltf(os.path.join(DATA_DIR, "scenes", name + ".gltf"))
+
+
+# ----------------------------------------------------------------------------------
+# Camera: SceneParser::parse_camera + Camera::to_hiprt (float32, glm conventions)
+# ----------------------------------------------------------------------------------
+def _lookat(eye, center, up):
+    f = center - eye
+    f = f / np.linalg.norm(f)
+    s = np.cross(f, up)
+    s = s / np.linalg.norm(s)
+    u = np.cross(s, f)
+    V = np.eye(4)
+    V[0, :3], V[1, :3], V[2, :3] = s, u, -f
+    V[0, 3], V[1, 3], V[2, 3] = -s @ eye, -u @ eye, f @ eye
+    return V
+
+
+def _perspective(fovy, aspect, n, f):
+    t = math.tan(fovy / 2.0)
+    P = np.zeros((4, 4))
+    P[0, 0] = 1.0 / (aspect * t)
+    P[1, 1] = 1.0 / t
+    P[2, 2] = -(f + n) / (f - n)
+    P[3, 2] = -1.0
+    P[2, 3] = -(2.0 * f * n) / (f - n)
+    return P
+
+
+def make_camera(camera_info, width, height, jitter=True):
+    """Returns abi.Camera for the scene camera at the given resolution.
+
+    parse_camera: inverse(lookAt(position, lookat, up)) decomposed into translation +
+    rotation, vertical_fov = 2 atan(tan(hfov/2) * aspect) + 0.425 with aspect = W/H
+    (main.cpp:43), glm::perspective.  to_hiprt stores, row-major, the inverse of the
+    (transposed-for-row-major) view matrix and glm's column-major inverse projection
+    reinterpreted as row-major (Camera.cpp:9-26, 37-45).
+    """
+    if camera_info is None:
+        camera_info = dict(position=np.zeros(3), lookat=np.array([0.0, 0.0, -1.0]), up=np.array([0.0, 1.0, 0.0]),
+                           hfov=40.0 / 180 * math.pi, aspect=1280 / 720, znear=0.1, zfar=100.0)
+    aspect = width / height
+    eye = np.asarray(camera_info["position"], np.float64)
+    V = _lookat(eye, np.asarray(camera_info["lookat"], np.float64), np.asarray(camera_info["up"], np.float64))
+    cam_to_world = np.linalg.inv(V)
+    vfov = 2.0 * math.atan(math.tan(camera_info["hfov"] * 0.5) * aspect) + 0.425
+    P = _perspective(vfov, aspect, camera_info["znear"], camera_info["zfar"])
+    # row-major view (world->view) and its inverse
+    view = np.linalg.inv(cam_to_world)
+    inv_view_rowmajor = np.linalg.inv(view)
+    # glm stores P column-major; inverse(P) reinterpreted row-major == inverse(P)^T
+    inv_proj_reinterpreted = np.linalg.inv(P).T
+    view_proj = (view.T @ P.T)  # glm view_matrix * projection_matrix, column-major storage
+    cam = abi.Camera()
+    for i in range(4):
+        for j in range(4):
+            cam.inverse_view.m[i][j] = float(np.float32(inv_view_rowmajor[i, j]))
+            cam.inverse_projection.m[i][j] = float(np.float32(inv_proj_reinterpreted[i, j]))
+            cam.view_projection.m[i][j] = float(np.float32(view_proj[i, j]))
+    cam.do_jittering = bool(jitter)
+    return cam
+
+
+# ----------------------------------------------------------------------------------
+# LUTs
+# ----------------------------------------------------------------------------------
+def load_luts():
+    """The reference's energy-compensation LUTs (see tools/make_data.py)."""
+    d = np.load(os.path.join(DATA_DIR, "luts.npz"))
+    return {k: np.ascontiguousarray(d[k], np.float32) for k in d.files}
+
+
+def luts_to_abi(luts):
+    C = abi.C
+    L = abi.Luts()
+    keep = []
+
+    def p(a):
+        a = np.ascontiguousarray(a, np.float32)
+        keep.append(a)
+        return a.ctypes.data_as(C.POINTER(abi.f32))
+
+    L.ggx_conductor_ess = p(luts["ggx_conductor"])
+    L.glossy_dielectric_ess = p(luts["glossy_dielectric"])
+    L.ggx_glass_ess = p(luts["ggx_glass"])
+    L.ggx_glass_inverse_ess = p(luts["ggx_glass_inverse"])
+    L.ggx_thin_glass_ess = p(luts["ggx_thin_glass"])
+    L.sheen_ltc_params = p(luts["sheen_ltc"])
+    L._keep = keep
+    return L
+
+
+# ----------------------------------------------------------------------------------
+# Frame / seed schedule
+# ----------------------------------------------------------------------------------
+def cpu_seed_schedule(nframes, first_sample=0):
+    """(sample_number, random_seed) per frame as CPURenderer::render does
+    (Renderer/CPURenderer.cpp:90, 271-287): random_seed starts at 42 and after each
+    frame becomes m_rng.xorshift32() with m_rng seeded 42."""
+    out = []
+    seed = 42
+    rng = 42
+    for f in range(nframes):
+        out.append((first_sample + f, seed))
+        x = rng
+        x ^= (x << 13) & 0xFFFFFFFF
+        x ^= x >> 17
+        x ^= (x << 5) & 0xFFFFFFFF
+        rng = x & 0xFFFFFFFF
+        seed = rng
+    return out
+
+
+def make_frame(camera, width, height, options=None, settings=None, world=None, flags=None,
+               sample_number=0, random_seed=42, band=(1, 0, 1)):
+    fr = abi.Frame()
+    fr.render_settings = settings if settings is not None else parity_settings()
+    fr.render_settings.sample_number = sample_number
+    fr.world_settings = world if world is not None else abi.WorldSettings.default()
+    fr.current_camera = camera
+    fr.prev_camera = camera
+    fr.options = options if options is not None else abi.KernelOptions.default()
+    fr.bsdf_flags = flags if flags is not None else abi.BSDFFlags.default()
+    fr.random_seed = random_seed
+    fr.res_x, fr.res_y = width, height
+    fr.band_height, fr.band_index, fr.band_count = band
+    return fr
+
+
+def parity_settings(nb_bounces=3):
+    """Reference defaults with the parity pins of BASELINE.md §2: adaptive sampling
+    off, alpha testing off (scenes without alpha textures), freeze_random off."""
+    s = abi.RenderSettings.default()
+    s.enable_adaptive_sampling = False
+    s.enable_pixel_stop_noise_threshold = False
+    s.stop_pixel_noise_threshold = 0.0
+    s.do_alpha_testing = False
+    s.nb_bounces = nb_bounces
+    return s

@@ -1,0 +1,408 @@
+/*
+ * mpt.h -- C ABI of the MI355X-native path-tracing hot path ("libmpt").
+ *
+ * This is the drop-in boundary described in SURVEY.md §8(b).  Every entry point
+ * replaces one piece of the reference's GPU launch API (wuyakuma/HIPRT-Path-Tracer,
+ * src/Renderer/GPURenderer.h) or of the HIPRT/Orochi glue it sits on:
+ *
+ *   mpt_create / mpt_destroy      <- GPURenderer::GPURenderer (GPURenderer.h:75,
+ *                                    GPURenderer.cpp:48-86) + HIPRTOrochiCtx (HIPRTOrochiCtx.h:20-66)
+ *   mpt_upload_scene              <- GPURenderer::set_scene -> set_hiprt_scene_from_scene
+ *                                    (GPURenderer.h:220, GPURenderer.cpp:1041-1134) and
+ *                                    HIPRTGeometry::build_bvh (HIPRTScene.h:60-87)
+ *   mpt_update_materials          <- GPURenderer::update_materials (GPURenderer.h:228)
+ *   mpt_set_envmap                <- GPURenderer::set_envmap (GPURenderer.h:222, .cpp:1136-1174)
+ *   mpt_set_luts                  <- GPURenderer::setup_brdfs_data (GPURenderer.h:76, .cpp:88-175)
+ *   mpt_resize                    <- GPURenderer::resize (GPURenderer.h:172)
+ *   mpt_render_frame              <- GPURenderer::render -> launch_camera_rays +
+ *                                    launch_path_tracing (GPURenderer.h:139-143,
+ *                                    .cpp:408-486), i.e. the CameraRays and FullPathTracer
+ *                                    kernels (Device/kernels/CameraRays.h:45,
+ *                                    Device/kernels/FullPathTracer.h:99)
+ *   mpt_synchronize / mpt_query_done <- GPURenderer::synchronize_kernel / frame_render_done
+ *                                    (GPURenderer.h:149-156)
+ *   mpt_get_framebuffer           <- the 'pixels' / denoiser AOV interop buffers
+ *                                    (GPURenderer.h:193-197, RenderData.h:32-36)
+ *   mpt_trace_closest / mpt_trace_any <- hiprtGeomTraversalClosest/AnyHit as called by
+ *                                    trace_ray / evaluate_shadow_ray (Device/includes/Intersect.h:114-286)
+ *
+ * Conventions: every function returns MPT_OK (0) or a negative error code; the
+ * message of the last error of the calling thread is in mpt_last_error().  The
+ * library never exits the process (the reference logs and calls exit(),
+ * HIPRT-Orochi/HIPRTOrochiUtils.cpp:15-47).  All device memory is owned by the
+ * context; host arrays passed in are copied before the call returns.  Calls on one
+ * context must be externally serialised.  All GPU work of a context is enqueued on
+ * the stream given to mpt_create (or the context's own stream).
+ *
+ * The POD structs below are byte-identical mirrors of the reference's
+ * HostDeviceCommon structs (sizes are static_assert-ed in the implementation):
+ *   MptMaterial       == RendererMaterial        (HostDeviceCommon/Material.h:29-268), 332 B
+ *   MptRenderSettings == HIPRTRenderSettings     (HostDeviceCommon/RenderSettings.h:26-252), 304 B
+ *   MptWorldSettings  == WorldSettings           (HostDeviceCommon/WorldSettings.h:18-52), 200 B
+ *   MptCamera         == HIPRTCamera             (HostDeviceCommon/HIPRTCamera.h:16-49), 196 B
+ */
+#ifndef MPT_H
+#define MPT_H
+
+#include <stddef.h>
+#include <stdint.h>
+#include <stdbool.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ------------------------------------------------------------------------- */
+/* Status codes                                                               */
+/* ------------------------------------------------------------------------- */
+#define MPT_OK 0
+#define MPT_ERR_INVALID_ARGUMENT (-1)
+#define MPT_ERR_HIP (-2)
+#define MPT_ERR_NO_SCENE (-3)
+#define MPT_ERR_UNSUPPORTED (-4)
+#define MPT_ERR_OUT_OF_MEMORY (-5)
+
+/* ------------------------------------------------------------------------- */
+/* Compile-time kernel options of the reference (HostDeviceCommon/KernelOptions.h) */
+/* become runtime selections of pre-instantiated kernel variants.             */
+/* ------------------------------------------------------------------------- */
+#define MPT_BSDF_NONE 0        /* BSDF_NONE: Principled BSDF  (KernelOptions.h:21) */
+#define MPT_BSDF_LAMBERTIAN 1  /* BSDF_LAMBERTIAN                                   */
+
+#define MPT_LSS_NO_DIRECT_LIGHT_SAMPLING 0 /* KernelOptions.h:50-56 */
+#define MPT_LSS_UNIFORM_ONE_LIGHT 1
+#define MPT_LSS_BSDF 2
+#define MPT_LSS_MIS_LIGHT_BSDF 3
+#define MPT_LSS_RIS_BSDF_AND_LIGHT 4
+#define MPT_LSS_RESTIR_DI 5
+
+#define MPT_ESS_NO_SAMPLING 0 /* KernelOptions.h:58-60 */
+#define MPT_ESS_BINARY_SEARCH 1
+#define MPT_ESS_ALIAS_TABLE 2
+
+#define MPT_AMBIENT_NONE 0 /* WorldSettings.h:11-16 */
+#define MPT_AMBIENT_UNIFORM 1
+#define MPT_AMBIENT_ENVMAP 2
+
+#define MPT_NO_TEXTURE (-1)
+#define MPT_CONSTANT_EMISSIVE_TEXTURE (-2)
+
+/* ------------------------------------------------------------------------- */
+/* Byte-identical mirrors of the reference PODs                               */
+/* ------------------------------------------------------------------------- */
+typedef struct MptColor { float r, g, b; } MptColor;           /* ColorRGB32F, Color.h:61 */
+typedef struct MptFloat4x4 { float m[4][4]; } MptFloat4x4;      /* float4x4, Math.h:43 */
+
+/* RendererMaterial (HostDeviceCommon/Material.h:29-268).  Field order is the
+ * reference's; 'emission' is the (private) last field of SimplifiedRendererMaterial. */
+typedef struct MptMaterial {
+    bool emissive_texture_used;
+    float emission_strength;
+    MptColor base_color;
+    float roughness;
+    float oren_nayar_sigma;
+    float metallic;
+    float metallic_F90_falloff_exponent;
+    MptColor metallic_F82;
+    MptColor metallic_F90;
+    float anisotropy;
+    float anisotropy_rotation;
+    float second_roughness_weight;
+    float second_roughness;
+    float specular;
+    float specular_tint;
+    MptColor specular_color;
+    float specular_darkening;
+    float coat;
+    MptColor coat_medium_absorption;
+    float coat_medium_thickness;
+    float coat_roughness;
+    float coat_roughening;
+    float coat_darkening;
+    float coat_anisotropy;
+    float coat_anisotropy_rotation;
+    float coat_ior;
+    float sheen;
+    float sheen_roughness;
+    MptColor sheen_color;
+    float ior;
+    float specular_transmission;
+    float absorption_at_distance;
+    MptColor absorption_color;
+    float dispersion_scale;
+    float dispersion_abbe_number;
+    bool thin_walled;
+    float thin_film;
+    float thin_film_ior;
+    float thin_film_thickness;
+    float thin_film_kappa_3;
+    float thin_film_hue_shift_degrees;
+    float thin_film_base_ior_override;
+    bool thin_film_do_ior_override;
+    bool srgb;
+    float alpha_opacity;
+    int32_t dielectric_priority;
+    int32_t energy_preservation_monte_carlo_samples;
+    bool enforce_strong_energy_conservation;
+    MptColor emission;
+    /* RendererMaterial texture indices (Material.h:217-266) */
+    int32_t normal_map_texture_index;
+    int32_t emission_texture_index;
+    int32_t base_color_texture_index;
+    int32_t roughness_metallic_texture_index;
+    int32_t roughness_texture_index;
+    int32_t oren_sigma_texture_index;
+    int32_t metallic_texture_index;
+    int32_t specular_texture_index;
+    int32_t specular_tint_texture_index;
+    int32_t specular_color_texture_index;
+    int32_t anisotropic_texture_index;
+    int32_t anisotropic_rotation_texture_index;
+    int32_t coat_texture_index;
+    int32_t coat_roughness_texture_index;
+    int32_t coat_ior_texture_index;
+    int32_t sheen_texture_index;
+    int32_t sheen_roughness_texture_index;
+    int32_t sheen_color_texture_index;
+    int32_t specular_transmission_texture_index;
+} MptMaterial;
+
+/* ReSTIRDISettings (HostDeviceCommon/ReSTIRDISettings.h:12-195) */
+typedef struct MptReSTIRDISettings {
+    /* InitialCandidatesSettings */
+    int32_t number_of_initial_light_candidates;
+    int32_t number_of_initial_bsdf_candidates;
+    float envmap_candidate_probability;
+    void* ic_output_reservoirs;
+    /* TemporalPassSettings */
+    bool do_temporal_reuse_pass;
+    bool use_permutation_sampling;
+    int32_t permutation_sampling_random_bits;
+    int32_t max_neighbor_search_count;
+    int32_t neighbor_search_radius;
+    bool temporal_buffer_clear_requested;
+    void* tp_input_reservoirs;
+    void* tp_output_reservoirs;
+    /* SpatialPassSettings */
+    bool do_spatial_reuse_pass;
+    int32_t spatial_pass_index;
+    int32_t number_of_passes;
+    int32_t reuse_radius;
+    int32_t reuse_neighbor_count;
+    bool do_disocclusion_reuse_boost;
+    int32_t disocclusion_reuse_count;
+    bool debug_neighbor_location;
+    bool do_neighbor_rotation;
+    bool allow_converged_neighbors_reuse;
+    float converged_neighbor_reuse_probability;
+    bool do_visibility_only_last_pass;
+    int32_t neighbor_visibility_count;
+    void* sp_input_reservoirs;
+    void* sp_output_reservoirs;
+    /* LightPresamplingSettings */
+    int32_t number_of_subsets;
+    int32_t subset_size;
+    int32_t tile_size;
+    void* light_samples;
+    /* ReSTIRDISettings */
+    bool do_fused_spatiotemporal;
+    int32_t m_cap;
+    bool use_confidence_weights;
+    bool use_normal_similarity_heuristic;
+    float normal_similarity_angle_degrees;
+    float normal_similarity_angle_precomp;
+    bool use_plane_distance_heuristic;
+    float plane_distance_threshold;
+    bool use_roughness_similarity_heuristic;
+    float roughness_similarity_threshold;
+    bool do_final_shading_visibility;
+    void* restir_output_reservoirs;
+} MptReSTIRDISettings;
+
+/* HIPRTRenderSettings (HostDeviceCommon/RenderSettings.h:26-252) */
+typedef struct MptRenderSettings {
+    bool need_to_reset;
+    bool do_update_status_buffers;
+    bool accumulate;
+    int32_t denoiser_AOV_accumulation_counter;
+    int32_t sample_number;
+    int32_t samples_per_frame;
+    int32_t nb_bounces;
+    bool use_russian_roulette;
+    int32_t russian_roulette_min_depth;
+    float russian_roulette_throughput_clamp;
+    int32_t path_russian_roulette_method; /* PathRussianRoulette: 0 MAX_THROUGHPUT, 1 ARNOLD_2014 */
+    int32_t freeze_random;
+    bool display_NaNs;
+    bool allow_render_low_resolution;
+    bool wants_render_low_resolution;
+    int32_t render_low_resolution_scaling;
+    bool enable_adaptive_sampling;
+    int32_t adaptive_sampling_min_samples;
+    float adaptive_sampling_noise_threshold;
+    bool enable_pixel_stop_noise_threshold;
+    float stop_pixel_percentage_converged;
+    float stop_pixel_noise_threshold;
+    float direct_contribution_clamp;
+    float envmap_contribution_clamp;
+    float indirect_contribution_clamp;
+    float minimum_light_contribution;
+    int32_t number_of_light_samples;
+    bool do_alpha_testing;
+    int32_t ris_number_of_light_candidates; /* RISSettings (RenderSettings.h:17-24) */
+    int32_t ris_number_of_bsdf_candidates;
+    MptReSTIRDISettings restir_di_settings;
+} MptRenderSettings;
+
+/* WorldSettings (HostDeviceCommon/WorldSettings.h:18-52).  The pointer fields are
+ * ignored by mpt_render_frame: the envmap lives in the context (mpt_set_envmap). */
+typedef struct MptWorldSettings {
+    int32_t ambient_light_type;
+    MptColor uniform_light_color;
+    uint32_t envmap_width, envmap_height;
+    float envmap_intensity;
+    int32_t envmap_scale_background_intensity;
+    void* envmap;
+    float envmap_total_sum;
+    float* envmap_cdf;
+    int32_t* alias_table_alias;
+    float* alias_table_probas;
+    MptFloat4x4 envmap_to_world_matrix;
+    MptFloat4x4 world_to_envmap_matrix;
+} MptWorldSettings;
+
+/* HIPRTCamera (HostDeviceCommon/HIPRTCamera.h:16-49) */
+typedef struct MptCamera {
+    MptFloat4x4 inverse_view;
+    MptFloat4x4 inverse_projection;
+    MptFloat4x4 view_projection;
+    bool do_jittering;
+} MptCamera;
+
+/* The compile-time options of KernelOptions.h that select code paths on the hot
+ * path.  Defaults of the reference: bsdf_override NONE, light_sampling RIS,
+ * envmap_sampling ALIAS_TABLE, envmap_bsdf_mis 1, ggx multiple scattering 1. */
+typedef struct MptKernelOptions {
+    int32_t bsdf_override;                 /* BSDFOverride (KernelOptions.h:116) */
+    int32_t direct_light_sampling;         /* DirectLightSamplingStrategy (KernelOptions.h:218) */
+    int32_t envmap_sampling;               /* EnvmapSamplingStrategy (KernelOptions.h:231) */
+    int32_t envmap_bsdf_mis;               /* EnvmapSamplingDoBSDFMIS (KernelOptions.h:242) */
+    int32_t ris_use_visibility;            /* RISUseVisiblityTargetFunction (KernelOptions.h:252) */
+} MptKernelOptions;
+
+/* BRDFsData flags (HostDeviceCommon/BSDFsData.h:24-62), the LUTs themselves are
+ * uploaded once with mpt_set_luts. */
+typedef struct MptBSDFFlags {
+    bool white_furnace_mode;
+    bool white_furnace_mode_turn_off_emissives;
+    bool clearcoat_compensation_approximation;
+    int32_t ggx_masking_shadowing; /* 0 HeightCorrelated, 1 HeightUncorrelated */
+} MptBSDFFlags;
+
+/* Everything one sample-per-pixel pass needs (the by-value HIPRTRenderData of
+ * the reference, minus device pointers which the library owns). */
+typedef struct MptFrame {
+    MptRenderSettings render_settings;
+    MptWorldSettings world_settings;
+    MptCamera current_camera;
+    MptCamera prev_camera;
+    MptKernelOptions options;
+    MptBSDFFlags bsdf_flags;
+    uint32_t random_seed;   /* HIPRTRenderData::random_seed (RenderData.h:146) */
+    int32_t res_x, res_y;   /* int2 res kernel argument */
+    /* Framebuffer row partition for multi-GPU tiling: this context renders the
+     * rows y with (y / band_height) % band_count == band_index.  (1, 0, 1) renders
+     * the whole frame.  Per-pixel RNG seeds use the global pixel index so a
+     * partitioned render is bit-identical to a single-device one. */
+    int32_t band_height, band_index, band_count;
+} MptFrame;
+
+/* Scene arrays as produced by the reference's SceneParser (Scene/SceneParser.h:80-131). */
+typedef struct MptScene {
+    const int32_t* triangle_indices;   /* 3 * num_triangles */
+    int32_t num_triangles;
+    const float* vertices;             /* 3 * num_vertices  (float3) */
+    const float* vertex_normals;       /* 3 * num_vertices */
+    const uint8_t* has_vertex_normals; /* num_vertices */
+    const float* texcoords;            /* 2 * num_vertices  (float2) */
+    int32_t num_vertices;
+    const int32_t* material_indices;   /* num_triangles */
+    const MptMaterial* materials;
+    int32_t num_materials;
+    const int32_t* emissive_triangle_indices;
+    int32_t num_emissive_triangles;
+    /* 8-bit textures, tightly packed one after the other, RGBA8 per texel */
+    int32_t num_textures;
+    const uint8_t* const* texture_data; /* num_textures pointers, RGBA8 (4 channels) */
+    const int32_t* texture_dims;        /* 2 * num_textures (width, height) */
+} MptScene;
+
+/* Energy-compensation LUTs (data/BRDFsData, GPUBakerConstants.h:15-32), float32,
+ * x fastest (cos_theta_o), then y (roughness), then z (ior / layer); already flipped
+ * vertically as Image32Bit::read_image_hdr(..., flipY=true) does (CPURenderer.cpp:93-132). */
+typedef struct MptLuts {
+    const float* ggx_conductor_ess;        /* 128 x 128 */
+    const float* glossy_dielectric_ess;    /* 128 x 64 x 128 */
+    const float* ggx_glass_ess;            /* 256 x 16 x 128 */
+    const float* ggx_glass_inverse_ess;    /* 256 x 16 x 128 */
+    const float* ggx_thin_glass_ess;       /* 32 x 32 x 96 */
+    const float* sheen_ltc_params;         /* 32 x 32 x 3 */
+} MptLuts;
+
+/* Counters and timings of the last mpt_render_frame (when enabled). */
+typedef struct MptStats {
+    uint64_t rays_closest;      /* closest-hit queries traced */
+    uint64_t rays_any;          /* any-hit (shadow) queries traced */
+    uint64_t node_visits;       /* BVH8 nodes fetched (instrumented build only) */
+    uint64_t triangle_tests;    /* triangle records fetched (instrumented build only) */
+    uint32_t trace_launches;    /* traversal kernel launches */
+    float trace_ms;             /* summed traversal kernel time (hipEvents) */
+    float frame_ms;             /* whole pass time (hipEvents) */
+} MptStats;
+
+#define MPT_FB_COLOR 0        /* 'pixels': running SUM of samples (RenderData.h:34-36) */
+#define MPT_FB_ALBEDO 1       /* denoiser_albedo */
+#define MPT_FB_NORMALS 2      /* denoiser_normals */
+
+typedef struct MptContext MptContext;
+
+const char* mpt_last_error(void);
+int mpt_version(void);
+/* sizes of the mirrored structs as compiled into the library (ABI check) */
+int mpt_abi_sizes(int32_t* out_sizes, int n);
+
+int mpt_create(int device, void* hip_stream, MptContext** out_ctx);
+int mpt_destroy(MptContext* ctx);
+int mpt_upload_scene(MptContext* ctx, const MptScene* scene);
+int mpt_update_materials(MptContext* ctx, const MptMaterial* materials, int32_t count);
+int mpt_set_envmap(MptContext* ctx, const float* rgba, int32_t width, int32_t height,
+                   const float* alias_probas, const int32_t* alias_indices, float luminance_total_sum);
+/* Vose alias table in double precision, Image32Bit::compute_alias_table (Image/Image.cpp:579-659) */
+int mpt_build_alias_table(const float* rgba, int32_t width, int32_t height,
+                          float* out_probas, int32_t* out_alias, float* out_luminance_sum);
+int mpt_set_luts(MptContext* ctx, const MptLuts* luts);
+int mpt_resize(MptContext* ctx, int32_t width, int32_t height);
+/* Renders one sample per pixel of the context's partition, accumulating into the
+ * sum framebuffer (assign when render_settings.sample_number == 0). Asynchronous. */
+int mpt_render_frame(MptContext* ctx, const MptFrame* frame);
+int mpt_synchronize(MptContext* ctx);
+int mpt_query_done(MptContext* ctx, int* out_done);
+/* Copies the partition's rows of a framebuffer (band-major compact layout: the
+ * rows owned by this context in increasing y) to dst; dst may be host or device. */
+int mpt_get_framebuffer(MptContext* ctx, int kind, float* dst, int dst_is_device);
+int mpt_partition_rows(int32_t res_y, int32_t band_height, int32_t band_index, int32_t band_count);
+int mpt_enable_stats(MptContext* ctx, int enable, int instrumented);
+int mpt_get_stats(MptContext* ctx, MptStats* out);
+/* Raw ray queries against the uploaded BVH8 (parity / microbenchmarks).
+ * rays: n * 8 floats (ox, oy, oz, tmin_unused, dx, dy, dz, tmax); last_hit: n ints (-1 = none).
+ * Outputs (may be NULL): prim (n ints, -1 on miss), t, u, v (n floats).  Host or device pointers. */
+int mpt_trace_closest(MptContext* ctx, const float* rays, const int32_t* last_hit, int32_t n,
+                      int32_t* out_prim, float* out_t, float* out_u, float* out_v, int pointers_are_device);
+int mpt_trace_any(MptContext* ctx, const float* rays, const int32_t* last_hit, int32_t n,
+                  uint8_t* out_occluded, int pointers_are_device);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MPT_H */

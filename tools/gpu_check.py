@@ -1,0 +1,90 @@
+"""Development check on a GPU box: GPU traversal + small renders vs the CPU oracle.
+
+Prints agreement statistics (exact-match fraction, max abs diff) instead of asserting,
+so a first run reports everything at once.  The pass/fail gates live in tests/.
+"""
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "hiprt-path-tracer_amd"))
+sys.path.insert(0, ROOT)
+
+import mpt  # noqa: E402
+from mpt import abi, scene  # noqa: E402
+from oracle import oracle as orc  # noqa: E402
+
+
+def random_rays(sd, n, seed=1):
+    rng = np.random.default_rng(seed)
+    v = sd.vertices
+    lo, hi = v.min(0), v.max(0)
+    o = lo + (hi - lo) * rng.random((n, 3))
+    d = rng.normal(size=(n, 3))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    r = np.zeros((n, 8), np.float32)
+    r[:, 0:3] = o
+    r[:, 4:7] = d
+    r[:, 7] = 1e30
+    return r
+
+
+def cmp(name, a, b):
+    a = np.asarray(a)
+    b = np.asarray(b)
+    eq = (a == b) | (np.isnan(a) & np.isnan(b))
+    d = np.abs(a.astype(np.float64) - b.astype(np.float64))
+    d = d[np.isfinite(d)]
+    print(f"{name}: exact {eq.mean():.6f}  max|diff| {d.max() if d.size else 0:.3e}  mean|a| {np.abs(a).mean():.4f}", flush=True)
+
+
+def main():
+    sd = scene.load_scene("cornell_pbr")
+    luts = scene.load_luts()
+    r = mpt.GPURenderer(0)
+    r.set_scene(sd)
+    r.set_luts(luts)
+    o = orc.Oracle(sd, luts)
+    rays = random_rays(sd, 200000)
+    t0 = time.time()
+    gp, gt, gu, gv = r.trace_closest(rays)
+    print("gpu trace", time.time() - t0)
+    op, ot, ou, ov = o.trace_closest(rays)
+    cmp("prim", gp, op)
+    cmp("t", gt, ot)
+    cmp("u", gu, ou)
+    occ = r.trace_any(rays)
+    print("any-hit consistent with closest:", np.mean(occ == (op >= 0)))
+
+    W, H = 64, 48
+    for name, ovr, lss in [("lambert_ris", abi.BSDF_LAMBERTIAN, abi.LSS_RIS_BSDF_AND_LIGHT),
+                           ("principled_mis", abi.BSDF_NONE, abi.LSS_MIS_LIGHT_BSDF),
+                           ("principled_ris", abi.BSDF_NONE, abi.LSS_RIS_BSDF_AND_LIGHT),
+                           ("principled_uniform", abi.BSDF_NONE, abi.LSS_UNIFORM_ONE_LIGHT),
+                           ("principled_bsdf", abi.BSDF_NONE, abi.LSS_BSDF)]:
+        cam = scene.make_camera(sd.camera_info, W, H)
+        opt = abi.KernelOptions.default()
+        opt.bsdf_override = ovr
+        opt.direct_light_sampling = lss
+        frames = [scene.make_frame(cam, W, H, options=opt, sample_number=s, random_seed=seed)
+                  for s, seed in scene.cpu_seed_schedule(4)]
+        for f in frames:
+            r.render(f)
+        r.synchronize_kernel()
+        g = r.framebuffer(abi.FB_COLOR)
+        ga = r.framebuffer(abi.FB_ALBEDO)
+        gn = r.framebuffer(abi.FB_NORMALS)
+        oc, oa, on = o.render(frames, aov=True)
+        cmp(name + " color", g, oc)
+        cmp(name + " albedo", ga, oa)
+        cmp(name + " normal", gn, on)
+        bad = np.argwhere(np.any(g != oc, axis=-1))
+        if len(bad):
+            print("   first differing pixels:", bad[:5].tolist())
+
+
+if __name__ == "__main__":
+    main()
