@@ -1,0 +1,217 @@
+"""Benchmark of the MI355X path tracer (libmpt) -- one JSON line on rank 0.
+
+Workload (BASELINE.json configs[1], "C2"): the Cornell box glTF at 1920x1080, full
+layered Principled BSDF with NEE + MIS (LSS_MIS_LIGHT_BSDF), 3 bounces, reference
+defaults otherwise (adaptive sampling off).  One *step* = one sample
+per pixel over the frame (one mpt_render_frame); the default K = 64 steps is the
+config's 64 spp.  Multi-GPU: one process per GPU, the framebuffer is split into
+interleaved 8-row bands (each rank renders every N-th band), and the per-rank sum
+buffers are gathered with RCCL (all_gather over xGMI) inside the timed region.
+
+value = whole-job Mray/s (every closest + any-hit query: camera, continuation, NEE
+shadow, MIS BSDF ray) = rays of all ranks / max-over-ranks wall time.
+roofline: the dominant traversal stage's algorithmic bytes (SURVEY.md §8d,
+B_ray = 32 + 16 + 80 N_node + 48 N_tri, N counted by an instrumented calibration
+pass) over its HIP-event-timed launches in the timed region.
+cpu_baseline: the CPU oracle (a port, test infrastructure) on a bounded band sample.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "hiprt-path-tracer_amd"))
+
+import mpt  # noqa: E402
+from mpt import abi, scene  # noqa: E402
+
+METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
+HBM_PEAK_GBS = 8000.0
+S_NODE, S_TRI = 80, 48
+BAND_H = 8
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=64)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--scene", default="cornell_pbr")
+    ap.add_argument("--strategy", default="mis", choices=["mis", "ris", "uniform", "bsdf"])
+    ap.add_argument("--bounces", type=int, default=3)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+LSS = {"mis": abi.LSS_MIS_LIGHT_BSDF, "ris": abi.LSS_RIS_BSDF_AND_LIGHT, "uniform": abi.LSS_UNIFORM_ONE_LIGHT,
+       "bsdf": abi.LSS_BSDF}
+
+
+def frames_for(cam, W, H, opt, band, n, first=0, bounces=3):
+    out = []
+    for s, seed in scene.cpu_seed_schedule(n):
+        st = scene.parity_settings(bounces)
+        out.append(scene.make_frame(cam, W, H, options=opt, settings=st, sample_number=s + first, random_seed=seed,
+                                    band=band))
+    return out
+
+
+def cpu_baseline(sd, luts, cam, W, H, opt, bounces, target_s):
+    """Oracle (CPU port) timed on a bounded sample of the same frame: a subset of the
+    8-row bands at 1 spp, or the whole frame at several spp, sized to ~target_s."""
+    sys.path.insert(0, ROOT)
+    from oracle import oracle as orc
+    cores = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    o = orc.Oracle(sd, luts)
+    bc = 64
+    t0 = time.perf_counter()
+    o.render(frames_for(cam, W, H, opt, (BAND_H, 0, bc), 1, bounces=bounces), nthreads=cores)
+    dt = max(time.perf_counter() - t0, 1e-3)
+    scale = target_s / dt                       # multiples of the probe's work
+    if scale >= bc:                             # whole frame, several spp
+        bc2, spp = 1, max(1, int(round(scale / bc)))
+    else:
+        bc2, spp = max(1, int(round(bc / scale))), 1
+    t0 = time.perf_counter()
+    o.render(frames_for(cam, W, H, opt, (BAND_H, 0, bc2), spp, bounces=bounces), nthreads=cores)
+    dt = time.perf_counter() - t0
+    rows = orc.mpt_rows(H, BAND_H, 0, bc2)
+    rays = o.last_rays[0] + o.last_rays[1]
+    o.close()
+    return {"value": round(rays / dt / 1e6, 4), "unit": "Mray/s", "cores": cores, "kind": "port",
+            "msample_per_s": round(rows * W * spp / dt / 1e6, 5),
+            "sample": f"oracle (C++ CPU port, OpenMP, {cores} threads): {spp} spp over {rows} of {H} rows "
+                      f"({BAND_H}-row bands, 1 of every {bc2}) of the same {W}x{H} frame, {dt:.1f} s"}
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    W, H, K = a.width, a.height, a.steps
+    sd = scene.load_scene(a.scene)
+    luts = scene.load_luts()
+    cam = scene.make_camera(sd.camera_info, W, H)
+    opt = abi.KernelOptions.default()
+    opt.bsdf_override = abi.BSDF_NONE
+    opt.direct_light_sampling = LSS[a.strategy]
+    band = (BAND_H, rank, world)
+
+    r = mpt.GPURenderer(local)
+    r.set_scene(sd)
+    r.set_luts(luts)
+
+    # calibration: instrumented traversal -> nodes / triangles per query per stage
+    r.enable_stats(timing=False, instrumented=True)
+    for f in frames_for(cam, W, H, opt, band, 2, first=0, bounces=a.bounces):
+        r.render(f)
+    cal = r.stats()
+    # warmup (untimed), then the timed K-frame accumulation restarting at sample 0
+    r.enable_stats(timing=False, instrumented=False)
+    for f in frames_for(cam, W, H, opt, band, a.warmup, bounces=a.bounces):
+        r.render(f)
+    frames = frames_for(cam, W, H, opt, band, K, bounces=a.bounces)
+    r.synchronize_kernel()
+    r.enable_stats(timing=True, instrumented=False)
+
+    rows = mpt.partition_rows(H, BAND_H, rank, world)
+    if dist is not None:
+        import torch
+        from mpt import partition
+        local_fb = torch.zeros((rows, W, 3), dtype=torch.float32, device="cuda")
+        dist.barrier()
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for f in frames:
+        r.render(f)
+    r.synchronize_kernel()
+    if dist is not None:
+        r.framebuffer_to_device(abi.FB_COLOR, local_fb.data_ptr())
+        frame = partition.gather_frame(local_fb, H, BAND_H, dist)
+        torch.cuda.synchronize()
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    st = r.stats()
+
+    rays_local = st.rays_closest + st.rays_any
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        n = torch.tensor([rays_local], dtype=torch.float64, device="cuda")
+        dist.all_reduce(n, op=dist.ReduceOp.SUM)
+        rays_total = float(n.item())
+    else:
+        rays_total = float(rays_local)
+
+    # roofline of the dominant traversal stage
+    stage = int(np.argmax([st.stage_ms[m] for m in range(3)]))
+    names = ["k_trace<TM_PATH> (camera/continuation, closest hit)", "k_trace<TM_NEE_ANY> (NEE shadow, any hit)",
+             "k_trace<TM_NEE_CLOSEST> (NEE BSDF/light ray, closest hit)"]
+    q_cal = max(1, cal.stage_rays[stage])
+    n_node = cal.stage_nodes[stage] / q_cal
+    n_tri = cal.stage_tris[stage] / q_cal
+    b_ray = 32 + 16 + S_NODE * n_node + S_TRI * n_tri
+    launches = max(1, st.stage_launches[stage])
+    avg_ms = st.stage_ms[stage] / launches
+    bytes_per_launch = st.stage_rays[stage] * b_ray / launches
+    achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        try:
+            cpu = cpu_baseline(sd, luts, cam, W, H, opt, a.bounces, a.cpu_seconds)
+        except Exception as e:  # the baseline is reported, never the product path
+            cpu = {"value": None, "unit": "Mray/s", "cores": 0, "kind": "port", "sample": f"failed: {e}"}
+
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": round(rays_total / elapsed / 1e6, 3),
+            "unit": "Mray/s",
+            "n_gpus": world,
+            "steps": K,
+            "warmup": a.warmup,
+            "ms_per_step": round(elapsed * 1e3 / K, 4),
+            "higher_is_better": True,
+            "scaling": "strong",   # fixed frame split over the ranks
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (reference Cornell glTF, seeded CPU seed schedule)",
+            "msample_per_s": round(W * H * K / elapsed / 1e6, 3),
+            "rays_per_sample": round(rays_total / (W * H * K), 4),
+            "config": {"workload": f"C2: {a.scene} {W}x{H}, {K} spp, layered Principled BSDF + NEE "
+                                   f"({a.strategy.upper()}), {a.bounces} bounces, 1 step = 1 spp",
+                       "scene": a.scene, "width": W, "height": H, "spp": K, "strategy": a.strategy,
+                       "partition": f"interleaved {BAND_H}-row bands over {world} rank(s), RCCL all_gather"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                         "kernel": names[stage], "avg_launch_ms": round(avg_ms, 5),
+                         "bytes_per_ray": round(b_ray, 2), "nodes_per_ray": round(n_node, 3),
+                         "tris_per_ray": round(n_tri, 3), "rays_per_launch": round(st.stage_rays[stage] / launches, 1),
+                         "stage_ms": [round(st.stage_ms[m], 3) for m in range(3)],
+                         "frame_ms_gpu": round(st.frame_ms / max(1, st.frames), 4)},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    r.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

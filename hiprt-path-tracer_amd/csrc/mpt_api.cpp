@@ -93,6 +93,7 @@ struct MptContext {
     DBuf<NeeRec> nee;
     DBuf<float> fb_color, fb_albedo, fb_normal;
     DBuf<uint64_t> stats;
+    DBuf<uint64_t> ray_counts;
     // frames
     MptFrame* h_frames = nullptr;   // pinned ring
     MptFrame* d_frames = nullptr;
@@ -100,10 +101,19 @@ struct MptContext {
     // stats
     bool timing = false;
     bool instrumented = false;
-    hipEvent_t ev[EV_POOL];
-    hipEvent_t ev_frame[2];
-    int ev_used = 0;
-    uint32_t last_launches = 0;
+    // two event pools used by alternate frames: a pool is read back when it is
+    // reused two frames later, so collecting timings never stalls the stream
+    hipEvent_t ev[2][EV_POOL];
+    int ev_mode[2][EV_POOL / 2];
+    hipEvent_t ev_frame[2][2];
+    int ev_used[2] = {0, 0};
+    bool ev_pending[2] = {false, false};
+    uint32_t frames_submitted = 0;
+    uint32_t trace_launches = 0;
+    uint32_t frames = 0;
+    double stage_ms[3] = {0, 0, 0};
+    uint32_t stage_launches[3] = {0, 0, 0};
+    double frame_ms = 0.0;
     // raw traces
     DBuf<float4> raw_o, raw_d, raw_hit;
     DBuf<uint8_t> raw_occ;
@@ -174,6 +184,7 @@ DevPaths dev_paths(MptContext* c) {
     P.fb_normal = c->fb_normal.p;
     P.stack_spill = c->spill.p;
     P.stats = c->stats.p;
+    P.ray_counts = c->ray_counts.p;
     return P;
 }
 
@@ -229,6 +240,22 @@ int validate_frame(const MptFrame* f) {
     return MPT_OK;
 }
 
+int collect_pool(MptContext* c, int p) {
+    if (!c->ev_pending[p]) return MPT_OK;
+    HIPCHK(hipEventSynchronize(c->ev_frame[p][1]));
+    for (int i = 0; i + 1 < c->ev_used[p]; i += 2) {
+        float ms = 0.0f;
+        HIPCHK(hipEventElapsedTime(&ms, c->ev[p][i], c->ev[p][i + 1]));
+        int m = c->ev_mode[p][i / 2];
+        if (m >= 0 && m < 3) { c->stage_ms[m] += ms; c->stage_launches[m]++; }
+    }
+    float fms = 0.0f;
+    HIPCHK(hipEventElapsedTime(&fms, c->ev_frame[p][0], c->ev_frame[p][1]));
+    c->frame_ms += fms;
+    c->ev_pending[p] = false;
+    return MPT_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -272,12 +299,16 @@ int mpt_create(int device, void* hip_stream, MptContext** out) {
     HIPCHK(c->counters.alloc(CTR_COUNT));
     HIPCHK(hipMemsetAsync(c->counters.p, 0, CTR_COUNT * sizeof(int32_t), c->stream));
     HIPCHK(c->fetch_raw.alloc(4));
-    HIPCHK(c->stats.alloc(4));
-    HIPCHK(hipMemsetAsync(c->stats.p, 0, 4 * sizeof(uint64_t), c->stream));
+    HIPCHK(c->stats.alloc(N_STATS));
+    HIPCHK(hipMemsetAsync(c->stats.p, 0, N_STATS * sizeof(uint64_t), c->stream));
+    HIPCHK(c->ray_counts.alloc(4));
+    HIPCHK(hipMemsetAsync(c->ray_counts.p, 0, 4 * sizeof(uint64_t), c->stream));
     HIPCHK(c->spill.alloc((size_t)c->grid * TRAV_BLOCK * SPILL_WORDS));
-    for (int i = 0; i < EV_POOL; i++) HIPCHK(hipEventCreate(&c->ev[i]));
-    HIPCHK(hipEventCreate(&c->ev_frame[0]));
-    HIPCHK(hipEventCreate(&c->ev_frame[1]));
+    for (int p = 0; p < 2; p++) {
+        for (int i = 0; i < EV_POOL; i++) HIPCHK(hipEventCreate(&c->ev[p][i]));
+        HIPCHK(hipEventCreate(&c->ev_frame[p][0]));
+        HIPCHK(hipEventCreate(&c->ev_frame[p][1]));
+    }
     *out = c;
     return MPT_OK;
 }
@@ -286,9 +317,11 @@ int mpt_destroy(MptContext* c) {
     if (!c) return MPT_OK;
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
-    for (int i = 0; i < EV_POOL; i++) (void)hipEventDestroy(c->ev[i]);
-    (void)hipEventDestroy(c->ev_frame[0]);
-    (void)hipEventDestroy(c->ev_frame[1]);
+    for (int p = 0; p < 2; p++) {
+        for (int i = 0; i < EV_POOL; i++) (void)hipEventDestroy(c->ev[p][i]);
+        (void)hipEventDestroy(c->ev_frame[p][0]);
+        (void)hipEventDestroy(c->ev_frame[p][1]);
+    }
     c->nodes.release(); c->tris.release(); c->idx.release(); c->mat_idx.release(); c->mat_prio.release();
     c->emissive.release(); c->tex_dims.release(); c->pos.release(); c->nrm.release(); c->uv.release();
     c->has_n.release(); c->tex.release(); c->tex_off.release(); c->mats.release();
@@ -298,7 +331,7 @@ int mpt_destroy(MptContext* c) {
     c->nrmv.release(); c->nq_o.release(); c->nq_d.release(); c->nhit.release(); c->hit_inside.release(); c->occ.release();
     c->rng.release(); c->spill.release(); c->vsA.release(); c->vsB.release(); c->q0.release(); c->q1.release();
     c->counters.release(); c->nq_tgt.release(); c->fetch_raw.release(); c->nee.release(); c->fb_color.release();
-    c->fb_albedo.release(); c->fb_normal.release(); c->stats.release();
+    c->fb_albedo.release(); c->fb_normal.release(); c->stats.release(); c->ray_counts.release();
     c->raw_o.release(); c->raw_d.release(); c->raw_hit.release(); c->raw_occ.release();
     if (c->h_frames) (void)hipHostFree(c->h_frames);
     if (c->d_frames) (void)hipFree(c->d_frames);
@@ -481,19 +514,29 @@ int mpt_render_frame(MptContext* c, const MptFrame* f) {
     if (slot == 0) HIPCHK(hipStreamSynchronize(c->stream));
     c->h_frames[slot] = *f;
     HIPCHK(hipMemcpyAsync(c->d_frames + slot, c->h_frames + slot, sizeof(MptFrame), hipMemcpyHostToDevice, c->stream));
+    int pool = (int)(c->frames_submitted & 1u);
+    if (c->timing) {
+        int rc = collect_pool(c, pool);
+        if (rc != MPT_OK) return rc;
+    }
     LaunchCfg cfg{};
     cfg.grid_persistent = c->grid;
     cfg.stats = c->instrumented ? 1 : 0;
-    cfg.ev_pool = c->timing ? c->ev : nullptr;
+    cfg.ev_pool = c->timing ? c->ev[pool] : nullptr;
+    cfg.ev_mode = c->ev_mode[pool];
     cfg.ev_cap = EV_POOL;
     cfg.ev_used = 0;
-    if (c->instrumented) HIPCHK(hipMemsetAsync(c->stats.p, 0, 4 * sizeof(uint64_t), c->stream));
-    if (c->timing) HIPCHK(hipEventRecord(c->ev_frame[0], c->stream));
+    if (c->timing) HIPCHK(hipEventRecord(c->ev_frame[pool][0], c->stream));
     hipError_t e = launch_frame(dev_scene(c), dev_paths(c), c->d_frames + slot, *f, cfg, c->stream);
     if (e != hipSuccess) return fail(MPT_ERR_HIP, std::string("kernel launch: ") + hipGetErrorString(e));
-    if (c->timing) HIPCHK(hipEventRecord(c->ev_frame[1], c->stream));
-    c->ev_used = cfg.ev_used;
-    c->last_launches = cfg.launches;
+    if (c->timing) {
+        HIPCHK(hipEventRecord(c->ev_frame[pool][1], c->stream));
+        c->ev_used[pool] = cfg.ev_used;
+        c->ev_pending[pool] = true;
+    }
+    c->frames_submitted++;
+    c->frames++;
+    c->trace_launches += cfg.launches;
     return MPT_OK;
 }
 
@@ -526,8 +569,18 @@ int mpt_get_framebuffer(MptContext* c, int kind, float* dst, int dst_is_device) 
 
 int mpt_enable_stats(MptContext* c, int enable, int instrumented) {
     if (!c) return fail(MPT_ERR_INVALID_ARGUMENT, "NULL context");
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipStreamSynchronize(c->stream));
     c->timing = enable != 0;
     c->instrumented = instrumented != 0;
+    c->ev_pending[0] = c->ev_pending[1] = false;
+    c->trace_launches = 0;
+    c->frames = 0;
+    c->frame_ms = 0.0;
+    for (int m = 0; m < 3; m++) { c->stage_ms[m] = 0.0; c->stage_launches[m] = 0; }
+    HIPCHK(hipMemsetAsync(c->stats.p, 0, N_STATS * sizeof(uint64_t), c->stream));
+    HIPCHK(hipMemsetAsync(c->ray_counts.p, 0, 4 * sizeof(uint64_t), c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
     return MPT_OK;
 }
 
@@ -535,26 +588,31 @@ int mpt_get_stats(MptContext* c, MptStats* out) {
     if (!c || !out) return fail(MPT_ERR_INVALID_ARGUMENT, "NULL argument");
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipStreamSynchronize(c->stream));
-    std::memset(out, 0, sizeof(*out));
-    uint64_t s[4];
-    HIPCHK(hipMemcpy(s, c->stats.p, sizeof(s), hipMemcpyDeviceToHost));
-    out->rays_closest = s[0];
-    out->rays_any = s[1];
-    out->node_visits = s[2];
-    out->triangle_tests = s[3];
-    out->trace_launches = c->last_launches;
-    if (c->timing) {
-        float total = 0.0f;
-        for (int i = 0; i + 1 < c->ev_used; i += 2) {
-            float ms = 0.0f;
-            HIPCHK(hipEventElapsedTime(&ms, c->ev[i], c->ev[i + 1]));
-            total += ms;
-        }
-        out->trace_ms = total;
-        float fms = 0.0f;
-        HIPCHK(hipEventElapsedTime(&fms, c->ev_frame[0], c->ev_frame[1]));
-        out->frame_ms = fms;
+    for (int p = 0; p < 2; p++) {
+        int rc = collect_pool(c, p);
+        if (rc != MPT_OK) return rc;
     }
+    std::memset(out, 0, sizeof(*out));
+    uint64_t s[N_STATS];
+    HIPCHK(hipMemcpy(s, c->stats.p, sizeof(s), hipMemcpyDeviceToHost));
+    uint64_t rc[4];
+    HIPCHK(hipMemcpy(rc, c->ray_counts.p, sizeof(rc), hipMemcpyDeviceToHost));
+    out->rays_closest = rc[0] + rc[2];
+    out->rays_any = rc[1];
+    for (int m = 0; m < 3; m++) {
+        out->stage_rays[m] = rc[m];
+        out->stage_traversals[m] = s[m * 4 + 0];
+        out->stage_nodes[m] = s[m * 4 + 1];
+        out->stage_tris[m] = s[m * 4 + 2];
+        out->node_visits += s[m * 4 + 1];
+        out->triangle_tests += s[m * 4 + 2];
+        out->stage_ms[m] = c->stage_ms[m];
+        out->stage_launches[m] = c->stage_launches[m];
+        out->trace_ms += c->stage_ms[m];
+    }
+    out->trace_launches = c->trace_launches;
+    out->frames = c->frames;
+    out->frame_ms = c->frame_ms;
     return MPT_OK;
 }
 

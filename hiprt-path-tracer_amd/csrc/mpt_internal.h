@@ -103,8 +103,12 @@ struct DevPaths {
     float* fb_albedo;
     float* fb_normal;
     uint32_t* stack_spill;    // global spill area of the traversal stacks
-    uint64_t* stats;          // 4 counters
+    uint64_t* stats;          // [trace mode][rays, nodes, tris, -] (instrumented traversal)
+    uint64_t* ray_counts;     // path rays, NEE any-hit rays, NEE closest rays (always on)
 };
+
+constexpr int N_TRACE_MODES = 5;
+constexpr int N_STATS = N_TRACE_MODES * 4;
 
 enum {
     CTR_Q0 = 0, CTR_Q1 = 1, CTR_ANY = 2, CTR_CL = 3, CTR_FETCH = 4,
@@ -116,6 +120,7 @@ struct LaunchCfg {
     int grid_persistent;      // blocks of the persistent traversal kernels
     int stats;                // instrumented traversal
     hipEvent_t* ev_pool;      // optional: one event pair per traversal launch
+    int* ev_mode;             // trace mode of each event pair
     int ev_cap;
     int ev_used;
     uint32_t launches;

@@ -271,9 +271,9 @@ __global__ __launch_bounds__(TB) void k_trace(TraceArgs A) {
             n_rays += __shfl_xor(n_rays, off);
         }
         if (lane_id() == 0) {
-            atomicAdd((unsigned long long*)&P.stats[any ? 1 : 0], (unsigned long long)n_rays);
-            atomicAdd((unsigned long long*)&P.stats[2], (unsigned long long)n_nodes);
-            atomicAdd((unsigned long long*)&P.stats[3], (unsigned long long)n_tris);
+            atomicAdd((unsigned long long*)&P.stats[MODE * 4 + 0], (unsigned long long)n_rays);
+            atomicAdd((unsigned long long*)&P.stats[MODE * 4 + 1], (unsigned long long)n_nodes);
+            atomicAdd((unsigned long long*)&P.stats[MODE * 4 + 2], (unsigned long long)n_tris);
         }
     }
 }
@@ -922,6 +922,12 @@ __global__ __launch_bounds__(TB) void k_resolve(DevScene S, DevPaths P, const Mp
     const MptFrame& F = *Fp;
     const MptRenderSettings& rs = F.render_settings;
     int i = blockIdx.x * TB + threadIdx.x;
+    if (i == 0) {
+        // always-on ray accounting: path rays + NEE any-hit + NEE closest of this bounce
+        P.ray_counts[0] += (uint64_t)*count_cur;
+        P.ray_counts[1] += (uint64_t)P.counters[CTR_ANY];
+        P.ray_counts[2] += (uint64_t)P.counters[CTR_CL];
+    }
     if (i >= *count_cur) return;
     int slot = q_cur[i];
     const NeeRec& nr = P.nee[slot];
@@ -1061,7 +1067,7 @@ static void launch_trace_mode(const TraceArgs& a, int grid, bool stats, hipStrea
 template <int MODE>
 static void timed_trace(const TraceArgs& a, LaunchCfg& cfg, hipStream_t st) {
     bool timed = cfg.ev_pool && cfg.ev_used + 2 <= cfg.ev_cap;
-    if (timed) hipEventRecord(cfg.ev_pool[cfg.ev_used], st);
+    if (timed) { cfg.ev_mode[cfg.ev_used / 2] = MODE; hipEventRecord(cfg.ev_pool[cfg.ev_used], st); }
     launch_trace_mode<MODE>(a, cfg.grid_persistent, cfg.stats, st);
     if (timed) { hipEventRecord(cfg.ev_pool[cfg.ev_used + 1], st); cfg.ev_used += 2; }
     cfg.launches++;

@@ -345,8 +345,11 @@ class Luts(C.Structure):
 
 class Stats(C.Structure):
     _fields_ = [("rays_closest", C.c_uint64), ("rays_any", C.c_uint64), ("node_visits", C.c_uint64),
-                ("triangle_tests", C.c_uint64), ("trace_launches", u32), ("trace_ms", f32),
-                ("frame_ms", f32)]
+                ("triangle_tests", C.c_uint64), ("trace_launches", u32), ("frames", u32),
+                ("trace_ms", C.c_double), ("frame_ms", C.c_double),
+                ("stage_rays", C.c_uint64 * 3), ("stage_traversals", C.c_uint64 * 3), ("stage_nodes", C.c_uint64 * 3),
+                ("stage_tris", C.c_uint64 * 3), ("stage_ms", C.c_double * 3),
+                ("stage_launches", u32 * 3), ("reserved", u32)]
 
 
 BSDF_NONE, BSDF_LAMBERTIAN = 0, 1

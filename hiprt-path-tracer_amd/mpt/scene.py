@@ -429,3 +429,42 @@ def parity_settings(nb_bounces=3):
     s.do_alpha_testing = False
     s.nb_bounces = nb_bounces
     return s
+
+
+# ----------------------------------------------------------------------------------
+# Synthetic assets (SURVEY.md §8d stand-ins for inputs not shipped in the container)
+# ----------------------------------------------------------------------------------
+def procedural_sky(width=2048, height=1024, seed=7, sun_dir=(0.3, 0.8, 0.5), sun_radiance=2000.0):
+    """Seeded HDR sky, RGBA32F [height, width, 4] in the reference's equirectangular
+    layout (row 0 = bottom after the loader's vertical flip): a vertical gradient, a
+    small bright sun lobe and low-amplitude seeded noise, so the alias table is far
+    from uniform (stand-in for the Bistro HDR)."""
+    rng = np.random.default_rng(seed)
+    v = (np.arange(height) + 0.5) / height           # 0 bottom .. 1 top
+    u = (np.arange(width) + 0.5) / width
+    theta = (1.0 - v) * math.pi                       # polar angle from +Y
+    phi = u * 2.0 * math.pi
+    st = np.sin(theta)[:, None]
+    d = np.stack([st * np.cos(phi)[None, :], np.repeat(np.cos(theta)[:, None], width, 1),
+                  st * np.sin(phi)[None, :]], -1)
+    up = np.clip(d[..., 1], -1.0, 1.0)
+    horizon = np.array([0.9, 0.85, 0.8])
+    zenith = np.array([0.25, 0.45, 0.9])
+    ground = np.array([0.18, 0.16, 0.14])
+    t = np.clip(up, 0.0, 1.0)[..., None]
+    col = np.where(up[..., None] >= 0.0, horizon * (1 - t) + zenith * t, ground)
+    s = np.asarray(sun_dir, np.float64)
+    s = s / np.linalg.norm(s)
+    cosang = np.clip(d @ s, -1.0, 1.0)
+    sun = np.exp((cosang - 1.0) * 4000.0) * sun_radiance
+    col = col + sun[..., None] * np.array([1.0, 0.95, 0.85])
+    col = col * (1.0 + 0.05 * rng.standard_normal((height, width, 1)))
+    rgba = np.concatenate([np.maximum(col, 0.0), np.ones((height, width, 1))], -1)
+    return np.ascontiguousarray(rgba, np.float32)
+
+
+def envmap_world(intensity=1.0):
+    w = abi.WorldSettings.default()
+    w.ambient_light_type = abi.AMBIENT_ENVMAP
+    w.envmap_intensity = intensity
+    return w

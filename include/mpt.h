@@ -349,15 +349,28 @@ typedef struct MptLuts {
     const float* sheen_ltc_params;         /* 32 x 32 x 3 */
 } MptLuts;
 
-/* Counters and timings of the last mpt_render_frame (when enabled). */
+/* Counters and timings, cumulative since the last mpt_enable_stats call.
+ * Ray counts are always collected; node/triangle counts only with the instrumented
+ * traversal; times only when timing is enabled (hipEvents around every traversal launch
+ * and around every frame, read back without stalling the stream). */
 typedef struct MptStats {
-    uint64_t rays_closest;      /* closest-hit queries traced */
-    uint64_t rays_any;          /* any-hit (shadow) queries traced */
-    uint64_t node_visits;       /* BVH8 nodes fetched (instrumented build only) */
-    uint64_t triangle_tests;    /* triangle records fetched (instrumented build only) */
+    uint64_t rays_closest;      /* closest-hit queries (camera/continuation + NEE BSDF/light rays) */
+    uint64_t rays_any;          /* any-hit (shadow) queries */
+    uint64_t node_visits;       /* BVH8 node fetches, all stages (instrumented) */
+    uint64_t triangle_tests;    /* triangle record fetches, all stages (instrumented) */
     uint32_t trace_launches;    /* traversal kernel launches */
-    float trace_ms;             /* summed traversal kernel time (hipEvents) */
-    float frame_ms;             /* whole pass time (hipEvents) */
+    uint32_t frames;            /* mpt_render_frame calls */
+    double trace_ms;            /* summed traversal kernel time */
+    double frame_ms;            /* summed whole-frame time */
+    /* per traversal stage: 0 = path rays (camera / continuation, closest hit),
+     * 1 = NEE shadow rays (any hit), 2 = NEE BSDF / light rays (closest hit) */
+    uint64_t stage_rays[3];         /* queries, always counted */
+    uint64_t stage_traversals[3];   /* BVH traversals (instrumented; >= queries: boundary skips retrace) */
+    uint64_t stage_nodes[3];
+    uint64_t stage_tris[3];
+    double stage_ms[3];
+    uint32_t stage_launches[3];
+    uint32_t reserved;
 } MptStats;
 
 #define MPT_FB_COLOR 0        /* 'pixels': running SUM of samples (RenderData.h:34-36) */

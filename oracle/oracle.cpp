@@ -1122,6 +1122,37 @@ int oracle_bsdf_sample(const MptMaterial* mat, const MptMaterial* all_mats, cons
     return 0;
 }
 
+// Monte Carlo directional albedo E(wo) = mean(f * |cos| / pdf) of bsdf_sample, for the
+// white-furnace pinning of the BSDF restatement against the reference's baked LUTs.
+int oracle_directional_albedo(const MptMaterial* mat, const MptMaterial* all_mats, const MptLuts* luts, int override_,
+                              float cos_theta_o, int n, uint32_t seed, float* out_rgb) {
+    BsdfCtx c;
+    c.materials = all_mats;
+    c.luts = Luts{luts->ggx_conductor_ess, luts->glossy_dielectric_ess, luts->ggx_glass_ess, luts->ggx_glass_inverse_ess,
+                  luts->ggx_thin_glass_ess, luts->sheen_ltc_params};
+    c.clearcoat_compensation = true;
+    c.ggx_masking = 0;
+    c.white_furnace = false;
+    float st = std::sqrt(std::max(0.0f, 1.0f - cos_theta_o * cos_theta_o));
+    f3 v = mk3(st, 0.0f, cos_theta_o);
+    f3 nn = mk3(0.0f, 0.0f, 1.0f);
+    double acc[3] = {0, 0, 0};
+    Rng rng(seed);
+    for (int i = 0; i < n; i++) {
+        VolumeState vs;
+        vs.incident_mat_index = MAX_MATERIAL_INDEX;
+        vs.outgoing_mat_index = 0;
+        float pdf;
+        f3 d;
+        Col r = bsdf_sample(c, override_, *mat, vs, v, nn, nn, d, pdf, rng);
+        if (!(pdf > 0.0f)) continue;
+        float w = std::fabs(d.z) / pdf;
+        acc[0] += r.r * w; acc[1] += r.g * w; acc[2] += r.b * w;
+    }
+    for (int k = 0; k < 3; k++) out_rgb[k] = (float)(acc[k] / n);
+    return 0;
+}
+
 uint32_t oracle_wang_hash(uint32_t s) { return wang_hash(s); }
 void oracle_xorshift(uint32_t seed, int n, uint32_t* out_u, float* out_f) {
     Rng a(seed), b(seed);

@@ -20,7 +20,10 @@ LIB_PATH = os.path.join(HERE, "liboracle.so")
 
 
 def build(force=False):
-    if force or not os.path.exists(LIB_PATH):
+    srcs = [os.path.join(HERE, f) for f in ("oracle.cpp", "oracle_math.h", "oracle_bsdf.h", "Makefile")]
+    stale = os.path.exists(LIB_PATH) and any(os.path.getmtime(f) > os.path.getmtime(LIB_PATH) for f in srcs
+                                             if os.path.exists(f))
+    if force or stale or not os.path.exists(LIB_PATH):
         subprocess.check_call(["make", "-s", "-C", HERE])
     return LIB_PATH
 
@@ -46,6 +49,8 @@ def lib():
         L.oracle_bsdf_sample.argtypes = [C.POINTER(abi.Material), C.POINTER(abi.Material), C.POINTER(abi.Luts),
                                          C.c_int, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p,
                                          C.c_void_p]
+        L.oracle_directional_albedo.argtypes = [C.POINTER(abi.Material), C.POINTER(abi.Material), C.POINTER(abi.Luts),
+                                                C.c_int, C.c_float, C.c_int, C.c_uint32, C.c_void_p]
         L.oracle_wang_hash.restype = C.c_uint32
         L.oracle_wang_hash.argtypes = [C.c_uint32]
         L.oracle_xorshift.argtypes = [C.c_uint32, C.c_int, C.c_void_p, C.c_void_p]
@@ -128,6 +133,13 @@ def bsdf_eval(mat, all_mats, luts_abi, override, view, normal, light):
     arr = (abi.Material * len(all_mats))(*all_mats)
     lib().oracle_bsdf_eval(C.byref(mat), arr, C.byref(luts_abi), override, _p(v), _p(n), _p(l), _p(out), _p(pdf))
     return out, float(pdf[0])
+
+
+def directional_albedo(mat, luts_abi, cos_theta_o, n, seed=1, override=0):
+    out = np.zeros(3, np.float32)
+    arr = (abi.Material * 1)(mat)
+    lib().oracle_directional_albedo(C.byref(mat), arr, C.byref(luts_abi), override, cos_theta_o, n, seed, _p(out))
+    return out
 
 
 def xorshift(seed, n):

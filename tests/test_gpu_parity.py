@@ -1,0 +1,234 @@
+"""GPU parity: the HIP path (through the C ABI, libmpt.so) against the CPU oracle.
+
+Bar: bit-exact.  Traversal results (prim, t, u, v) and rendered sums / AOVs must equal
+the oracle's float32 values exactly -- the device code is compiled without
+contraction, transcendentals are rounded from double on both sides and the RNG stream
+of every path is consumed in the reference's order (DESIGN.md "Parity").
+At the bench size (1920x1080) the properties checked are size-independent: run-to-run
+determinism, partition invariance and finite output.
+"""
+import numpy as np
+import pytest
+
+import mpt
+from mpt import abi, partition, scene
+
+pytestmark = pytest.mark.gpu
+
+STRATEGIES = {"none": abi.LSS_NO_DIRECT_LIGHT_SAMPLING, "uniform": abi.LSS_UNIFORM_ONE_LIGHT, "bsdf": abi.LSS_BSDF,
+              "mis": abi.LSS_MIS_LIGHT_BSDF, "ris": abi.LSS_RIS_BSDF_AND_LIGHT}
+
+
+@pytest.fixture(scope="module")
+def scenes():
+    return {n: scene.load_scene(n) for n in ("cornell_pbr", "nested-dielectrics", "nested-dielectrics-complex",
+                                              "multi-dispersion")}
+
+
+@pytest.fixture(scope="module")
+def sky():
+    return mpt.build_envmap(scene.procedural_sky(256, 128, seed=7))
+
+
+_cache = {}
+
+
+def renderer(sd, luts, env=None):
+    key = (sd.name, id(sd), env is not None)
+    if key not in _cache:
+        r = mpt.GPURenderer(0)
+        r.set_scene(sd)
+        r.set_luts(luts)
+        if env is not None:
+            r.set_envmap(env)
+        _cache[key] = r
+    return _cache[key]
+
+
+_oracles = {}
+
+
+def oracle_for(sd, luts, env=None):
+    from oracle import oracle as orc
+    key = (id(sd), env is not None)
+    if key not in _oracles:
+        _oracles[key] = orc.Oracle(sd, luts, envmap=env)
+    return _oracles[key]
+
+
+def frames(sd, W, H, n, ovr=abi.BSDF_NONE, lss=abi.LSS_MIS_LIGHT_BSDF, band=(1, 0, 1), bounces=3, world=None,
+           env_mis=1, ess=abi.ESS_ALIAS_TABLE, first=0):
+    cam = scene.make_camera(sd.camera_info, W, H)
+    opt = abi.KernelOptions.default()
+    opt.bsdf_override, opt.direct_light_sampling = ovr, lss
+    opt.envmap_bsdf_mis, opt.envmap_sampling = env_mis, ess
+    return [scene.make_frame(cam, W, H, options=opt, settings=scene.parity_settings(bounces), world=world,
+                             sample_number=s + first, random_seed=seed, band=band)
+            for s, seed in scene.cpu_seed_schedule(n)]
+
+
+def gpu_render(r, frs):
+    for f in frs:
+        r.render(f)
+    r.synchronize_kernel()
+    return r.framebuffer(abi.FB_COLOR), r.framebuffer(abi.FB_ALBEDO), r.framebuffer(abi.FB_NORMALS)
+
+
+def assert_same(a, b, what):
+    a, b = np.asarray(a), np.asarray(b)
+    assert a.shape == b.shape, what
+    diff = np.argwhere(~((a == b) | (np.isnan(a) & np.isnan(b))))
+    assert len(diff) == 0, f"{what}: {len(diff)} values differ, first at {diff[:3].tolist()}: " \
+                           f"{a[tuple(diff[0])]} vs {b[tuple(diff[0])]}"
+
+
+# ------------------------------------------------------------------------------------
+# Traversal
+# ------------------------------------------------------------------------------------
+def random_rays(sd, n, seed, spread=1.5):
+    rng = np.random.default_rng(seed)
+    lo, hi = sd.vertices.min(0), sd.vertices.max(0)
+    c, e = (lo + hi) / 2, (hi - lo) / 2 * spread
+    o = c + e * (2 * rng.random((n, 3)) - 1)
+    d = rng.normal(size=(n, 3))
+    d[: n // 8, 0] = 0.0          # axis-parallel components (box-test reciprocal edge cases)
+    d[n // 8: n // 4, 1:] = 0.0
+    d /= np.maximum(np.linalg.norm(d, axis=1, keepdims=True), 1e-12)
+    r = np.zeros((n, 8), np.float32)
+    r[:, 0:3], r[:, 4:7], r[:, 7] = o, d, 1e30
+    return r
+
+
+@pytest.mark.parametrize("name", ["cornell_pbr", "nested-dielectrics-complex", "multi-dispersion"])
+def test_traversal_closest_bit_exact(scenes, luts, name):
+    sd = scenes[name]
+    r = renderer(sd, luts)
+    o = oracle_for(sd, luts)
+    rays = random_rays(sd, 200000, 5)
+    gp, gt, gu, gv = r.trace_closest(rays)
+    op, ot, ou, ov = o.trace_closest(rays)
+    assert_same(gp, op, "prim")
+    hit = op >= 0
+    assert hit.mean() > 0.05
+    assert_same(gt[hit], ot[hit], "t")
+    assert_same(gu[hit], ou[hit], "u")
+    assert_same(gv[hit], ov[hit], "v")
+    # re-trace from the hit point excluding the hit primitive (filter function of Intersect.h)
+    o2 = rays.copy()
+    o2[hit, 0:3] = rays[hit, 0:3] + ot[hit, None] * rays[hit, 4:7]
+    lh = np.where(hit, op, -1).astype(np.int32)
+    gp2, gt2, _, _ = r.trace_closest(o2, lh)
+    op2, ot2, _, _ = o.trace_closest(o2, lh)
+    assert_same(gp2, op2, "prim after last-hit filter")
+    assert_same(gt2[op2 >= 0], ot2[op2 >= 0], "t after last-hit filter")
+
+
+def test_traversal_any_hit_consistent(scenes, luts):
+    sd = scenes["cornell_pbr"]
+    r = renderer(sd, luts)
+    o = oracle_for(sd, luts)
+    rays = random_rays(sd, 100000, 9)
+    rng = np.random.default_rng(2)
+    rays[:, 7] = rng.random(len(rays)).astype(np.float32) * 3.0
+    occ = r.trace_any(rays)
+    op, ot, _, _ = o.trace_closest(rays)
+    expect = (op >= 0) & (ot < rays[:, 7])
+    assert_same(occ, expect, "occluded")
+
+
+def test_empty_and_single_ray_queries(scenes, luts):
+    r = renderer(scenes["cornell_pbr"], luts)
+    p, t, u, v = r.trace_closest(np.zeros((0, 8), np.float32))
+    assert len(p) == 0
+    one = random_rays(scenes["cornell_pbr"], 1, 1)
+    assert len(r.trace_closest(one)[0]) == 1
+
+
+# ------------------------------------------------------------------------------------
+# Rendering
+# ------------------------------------------------------------------------------------
+@pytest.mark.parametrize("ovr", [abi.BSDF_NONE, abi.BSDF_LAMBERTIAN], ids=["principled", "lambert"])
+@pytest.mark.parametrize("strategy", list(STRATEGIES))
+def test_render_cornell_bit_exact(scenes, luts, ovr, strategy):
+    sd = scenes["cornell_pbr"]
+    W, H = 48, 32
+    frs = frames(sd, W, H, 3, ovr=ovr, lss=STRATEGIES[strategy])
+    g = gpu_render(renderer(sd, luts), frs)
+    c = oracle_for(sd, luts).render(frs, aov=True)
+    for k, name in enumerate(["color", "albedo", "normals"]):
+        assert_same(g[k], c[k], f"{strategy} {name}")
+    assert np.isfinite(g[0]).all() and g[0].mean() > 0
+
+
+@pytest.mark.parametrize("name,bounces", [("nested-dielectrics", 8), ("nested-dielectrics-complex", 8),
+                                          ("multi-dispersion", 8)])
+@pytest.mark.parametrize("strategy", ["mis", "ris"])
+def test_render_dielectric_scenes_bit_exact(scenes, luts, name, bounces, strategy):
+    sd = scenes[name]
+    W, H = 40, 30
+    frs = frames(sd, W, H, 2, lss=STRATEGIES[strategy], bounces=bounces)
+    g = gpu_render(renderer(sd, luts), frs)
+    c = oracle_for(sd, luts).render(frs, aov=True)
+    for k, what in enumerate(["color", "albedo", "normals"]):
+        assert_same(g[k], c[k], f"{name} {strategy} {what}")
+
+
+@pytest.mark.parametrize("strategy,env_mis,ess", [("mis", 1, abi.ESS_ALIAS_TABLE), ("ris", 1, abi.ESS_ALIAS_TABLE),
+                                                  ("mis", 0, abi.ESS_ALIAS_TABLE), ("mis", 1, abi.ESS_NO_SAMPLING)])
+def test_render_envmap_bit_exact(scenes, luts, sky, strategy, env_mis, ess):
+    sd = scenes["nested-dielectrics"]
+    W, H = 40, 30
+    frs = frames(sd, W, H, 2, lss=STRATEGIES[strategy], world=scene.envmap_world(0.5), env_mis=env_mis, ess=ess)
+    g = gpu_render(renderer(sd, luts, sky), frs)
+    c = oracle_for(sd, luts, sky).render(frs, aov=True)
+    for k, what in enumerate(["color", "albedo", "normals"]):
+        assert_same(g[k], c[k], f"envmap {strategy} {what}")
+
+
+@pytest.mark.parametrize("band", [(4, 0, 3), (4, 2, 3), (8, 1, 2), (1, 5, 7)])
+def test_partition_bit_exact(scenes, luts, band):
+    sd = scenes["cornell_pbr"]
+    W, H = 40, 36
+    r = renderer(sd, luts)
+    full = gpu_render(r, frames(sd, W, H, 2))[0]
+    part = gpu_render(r, frames(sd, W, H, 2, band=band))[0]
+    assert_same(part, full[partition.rows_of(H, *band)], f"band {band}")
+
+
+def test_accumulation_restarts_at_sample_zero(scenes, luts):
+    sd = scenes["cornell_pbr"]
+    r = renderer(sd, luts)
+    a = gpu_render(r, frames(sd, 32, 16, 2))[0]
+    b = gpu_render(r, frames(sd, 32, 16, 2))[0]       # sample_number 0 again: assign, not add
+    assert_same(a, b, "re-render")
+
+
+def test_unsupported_options_fail_loudly(scenes, luts):
+    sd = scenes["cornell_pbr"]
+    r = renderer(sd, luts)
+    f = frames(sd, 16, 16, 1)[0]
+    f.render_settings.enable_adaptive_sampling = True
+    with pytest.raises(mpt.MptError) as e:
+        r.render(f)
+    assert e.value.code == -4
+    f = frames(sd, 16, 16, 1, lss=abi.LSS_RESTIR_DI)[0]
+    with pytest.raises(mpt.MptError):
+        r.render(f)
+
+
+def test_full_size_properties(scenes, luts):
+    """Bench configuration (1920x1080, Principled + MIS): determinism, partition
+    invariance, finite output and the oracle on a band subset."""
+    sd = scenes["cornell_pbr"]
+    W, H = 1920, 1080
+    r = renderer(sd, luts)
+    a = gpu_render(r, frames(sd, W, H, 2))[0]
+    b = gpu_render(r, frames(sd, W, H, 2))[0]
+    assert_same(a, b, "determinism")
+    assert np.isfinite(a).all()
+    band = (8, 3, 64)
+    p = gpu_render(r, frames(sd, W, H, 2, band=band))[0]
+    ys = partition.rows_of(H, *band)
+    assert_same(p, a[ys], "partition at full size")
+    c = oracle_for(sd, luts).render(frames(sd, W, H, 2, band=band))
+    assert_same(p, c, "oracle on a band subset of the full frame")
