@@ -45,6 +45,7 @@ def parse():
     ap.add_argument("--scene", default="cornell_pbr")
     ap.add_argument("--strategy", default="mis", choices=["mis", "ris", "uniform", "bsdf"])
     ap.add_argument("--bounces", type=int, default=3)
+    ap.add_argument("--bsdf", default="principled", choices=["principled", "lambert"])
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
@@ -107,7 +108,7 @@ def main():
     luts = scene.load_luts()
     cam = scene.make_camera(sd.camera_info, W, H)
     opt = abi.KernelOptions.default()
-    opt.bsdf_override = abi.BSDF_NONE
+    opt.bsdf_override = abi.BSDF_NONE if a.bsdf == "principled" else abi.BSDF_LAMBERTIAN
     opt.direct_light_sampling = LSS[a.strategy]
     band = (BAND_H, rank, world)
 
@@ -158,18 +159,39 @@ def main():
     else:
         rays_total = float(rays_local)
 
-    # roofline of the dominant traversal stage
-    stage = int(np.argmax([st.stage_ms[m] for m in range(3)]))
-    names = ["k_trace<TM_PATH> (camera/continuation, closest hit)", "k_trace<TM_NEE_ANY> (NEE shadow, any hit)",
-             "k_trace<TM_NEE_CLOSEST> (NEE BSDF/light ray, closest hit)"]
-    q_cal = max(1, cal.stage_rays[stage])
-    n_node = cal.stage_nodes[stage] / q_cal
-    n_tri = cal.stage_tris[stage] / q_cal
-    b_ray = 32 + 16 + S_NODE * n_node + S_TRI * n_tri
-    launches = max(1, st.stage_launches[stage])
-    avg_ms = st.stage_ms[stage] / launches
-    bytes_per_launch = st.stage_rays[stage] * b_ray / launches
-    achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+    # rooflines (SURVEY.md §8d algorithmic bytes): every traversal stage and the shade
+    # kernel; "roofline" is the one with the largest summed time in the timed region
+    names = ["k_trace<TM_PATH> (camera/continuation rays, closest hit)", "k_trace<TM_NEE_ANY> (NEE shadow rays, any hit)",
+             "k_trace<TM_NEE_CLOSEST> (NEE BSDF/light rays, closest hit)"]
+    lines = []
+    for m in range(3):
+        q_cal = max(1, cal.stage_rays[m])
+        n_node, n_tri = cal.stage_nodes[m] / q_cal, cal.stage_tris[m] / q_cal
+        b_ray = 32 + 16 + S_NODE * n_node + S_TRI * n_tri
+        launches = max(1, st.stage_launches[m])
+        avg_ms = st.stage_ms[m] / launches
+        ach = st.stage_rays[m] * b_ray / launches / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+        lines.append({"kernel": names[m], "total_ms": st.stage_ms[m], "achieved": ach, "avg_launch_ms": avg_ms,
+                      "bytes_per_unit": b_ray, "unit_of_work": "ray", "nodes_per_ray": n_node, "tris_per_ray": n_tri,
+                      "units_per_launch": st.stage_rays[m] / launches})
+    # shade: per path vertex = material 256 + vertex gathers 12+36+36+24 + path state 2x96 (§8d)
+    b_vtx = 256 + 12 + 36 + 36 + 24 + 2 * 96
+    sl = max(1, st.shade_launches)
+    s_avg = st.shade_ms / sl
+    lines.append({"kernel": "k_shade<BSDF_NONE> (path vertex: hit, NEE sampling, BSDF sampling, RR)",
+                  "total_ms": st.shade_ms, "avg_launch_ms": s_avg, "bytes_per_unit": b_vtx, "unit_of_work": "path vertex",
+                  "units_per_launch": st.stage_rays[0] / sl,
+                  "achieved": st.stage_rays[0] * b_vtx / sl / (s_avg * 1e-3) / 1e9 if s_avg > 0 else 0.0})
+    dom = max(lines, key=lambda x: x["total_ms"])
+
+    def roof(x):
+        r = {"bound": "hbm", "achieved": round(x["achieved"], 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+             "frac": round(x["achieved"] / HBM_PEAK_GBS, 5), "traffic": None, "kernel": x["kernel"],
+             "avg_launch_ms": round(x["avg_launch_ms"], 5), "bytes_per_unit": round(x["bytes_per_unit"], 2),
+             "unit_of_work": x["unit_of_work"], "units_per_launch": round(x["units_per_launch"], 1)}
+        if "nodes_per_ray" in x:
+            r.update(nodes_per_ray=round(x["nodes_per_ray"], 3), tris_per_ray=round(x["tris_per_ray"], 3))
+        return r
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
@@ -194,17 +216,19 @@ def main():
             "data": "synthetic (reference Cornell glTF, seeded CPU seed schedule)",
             "msample_per_s": round(W * H * K / elapsed / 1e6, 3),
             "rays_per_sample": round(rays_total / (W * H * K), 4),
-            "config": {"workload": f"C2: {a.scene} {W}x{H}, {K} spp, layered Principled BSDF + NEE "
+            "config": {"workload": f"C2: {a.scene} {W}x{H}, {K} spp, "
+                                   f"{'layered Principled' if a.bsdf == 'principled' else 'Lambert-override'} BSDF + NEE "
                                    f"({a.strategy.upper()}), {a.bounces} bounces, 1 step = 1 spp",
                        "scene": a.scene, "width": W, "height": H, "spp": K, "strategy": a.strategy,
                        "partition": f"interleaved {BAND_H}-row bands over {world} rank(s), RCCL all_gather"},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
-                         "kernel": names[stage], "avg_launch_ms": round(avg_ms, 5),
-                         "bytes_per_ray": round(b_ray, 2), "nodes_per_ray": round(n_node, 3),
-                         "tris_per_ray": round(n_tri, 3), "rays_per_launch": round(st.stage_rays[stage] / launches, 1),
-                         "stage_ms": [round(st.stage_ms[m], 3) for m in range(3)],
-                         "frame_ms_gpu": round(st.frame_ms / max(1, st.frames), 4)},
+            "roofline": roof(dom),
+            "roofline_traversal": roof(max(lines[:3], key=lambda x: x["total_ms"])),
+            "kernel_ms_per_step": {"trace_path": round(st.stage_ms[0] / K, 4), "trace_nee_any": round(st.stage_ms[1] / K, 4),
+                                   "trace_nee_closest": round(st.stage_ms[2] / K, 4), "shade": round(st.shade_ms / K, 4),
+                                   "resolve": round(st.resolve_ms / K, 4), "camera": round(st.camera_ms / K, 4),
+                                   "accumulate": round(st.accumulate_ms / K, 4),
+                                   "compact": round(st.compact_ms / K, 4),
+                                   "frame_gpu": round(st.frame_ms / max(1, st.frames), 4)},
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

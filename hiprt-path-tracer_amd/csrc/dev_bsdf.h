@@ -727,8 +727,10 @@ DEV Col principled_eval(const BCtx& c, const Mat& m, VState& vs, v3 view, v3 n, 
     return fc;
 }
 
-DEV Col principled_sample(const BCtx& c, const Mat& m, VState& vs, v3 view, v3 sn, v3 gn, v3& out, float& pdf, Rng& rng) {
-    pdf = 0.0f;
+// Direction half of PrincipledBSDF sampling (Principled.h:1050-1120): picks a lobe, samples
+// it, updates the nested-dielectric state.  Returns false where the reference returns a
+// zero BSDF without evaluating it (direction below the surface for a non-glass lobe).
+DEV bool principled_sample_dir(const BCtx& c, const Mat& m, VState& vs, v3 view, v3 sn, v3 gn, v3& out, Rng& rng) {
     v3 n = sn;
     bool outside = dot(view, n) > 0 || m.thin_walled;
     float gw = (1.0f - m.metallic) * m.specular_transmission;
@@ -757,18 +759,21 @@ DEV Col principled_sample(const BCtx& c, const Mat& m, VState& vs, v3 view, v3 s
         v3 T, B;
         build_onb(n, T, B);
         out = to_world(T, B, n, sheen_sample(c, m, to_local(T, B, n, view), rng));
-    } else if (r1 < c2) {
-        out = to_world(TR, BR, n, ggx_sample_reflection(m.roughness, m.anisotropy, lvr, rng));
-    } else if (r1 < c3) {
-        out = to_world(TR, BR, n, ggx_sample_reflection(m.second_roughness, m.anisotropy, lvr, rng));
     } else if (r1 < c4) {
-        out = to_world(TR, BR, n, ggx_sample_reflection(m.roughness, m.anisotropy, lvr, rng));
+        // metal (first / second roughness) and specular lobes share the GGX reflection sampler
+        float r = (r1 >= c2 && r1 < c3) ? m.second_roughness : m.roughness;
+        out = to_world(TR, BR, n, ggx_sample_reflection(r, m.anisotropy, lvr, rng));
     } else if (r1 < c5) {
         out = cosine_sample_around(n, rng);
     } else {
         out = to_world(TR, BR, n, glass_sample(c, m, vs, lvr, rng));
     }
-    if (dot(out, sn) < 0 && !glass) return col(0.0f);
+    return !(dot(out, sn) < 0 && !glass);
+}
+
+DEV Col principled_sample(const BCtx& c, const Mat& m, VState& vs, v3 view, v3 sn, v3 gn, v3& out, float& pdf, Rng& rng) {
+    pdf = 0.0f;
+    if (!principled_sample_dir(c, m, vs, view, sn, gn, out, rng)) return col(0.0f);
     return principled_eval(c, m, vs, view, sn, out, pdf);
 }
 
@@ -777,10 +782,17 @@ DEV Col bsdf_eval(const BCtx& c, const Mat& m, VState& vs, v3 view, v3 sn, v3 L,
     if (OVERRIDE == MPT_BSDF_LAMBERTIAN) return lambert_eval(m, dot(L, sn), pdf);
     return principled_eval(c, m, vs, view, sn, L, pdf);
 }
+// sample = sample_dir + bsdf_eval on the updated state (eval skipped when sample_dir is false)
+template <int OVERRIDE>
+DEV bool bsdf_sample_dir(const BCtx& c, const Mat& m, VState& vs, v3 view, v3 sn, v3 gn, v3& dir, Rng& rng) {
+    if (OVERRIDE == MPT_BSDF_LAMBERTIAN) { dir = cosine_sample_around(sn, rng); return true; }
+    return principled_sample_dir(c, m, vs, view, sn, gn, dir, rng);
+}
 template <int OVERRIDE>
 DEV Col bsdf_sample(const BCtx& c, const Mat& m, VState& vs, v3 view, v3 sn, v3 gn, v3& dir, float& pdf, Rng& rng) {
-    if (OVERRIDE == MPT_BSDF_LAMBERTIAN) return lambert_sample(m, sn, dir, pdf, rng);
-    return principled_sample(c, m, vs, view, sn, gn, dir, pdf, rng);
+    pdf = 0.0f;
+    if (!bsdf_sample_dir<OVERRIDE>(c, m, vs, view, sn, gn, dir, rng)) return col(0.0f);
+    return bsdf_eval<OVERRIDE>(c, m, vs, view, sn, dir, pdf);
 }
 
 }  // namespace mpt

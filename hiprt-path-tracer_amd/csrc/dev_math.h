@@ -124,7 +124,8 @@ DEV void build_onb(v3 n, v3& t, v3& b) {
 DEV void build_rotated_onb(v3 n, v3& t, v3& b, float rot) {
     v3 up = absr(n.z) < 0.9999999f ? mk3(0.0f, 0.0f, 1.0f) : mk3(1.0f, 0.0f, 0.0f);
     t = normalize(cross(up, n));
-    float c = pcos(rot), s = psin(rot);
+    // rot == +-0 (no anisotropy rotation, the common case): cos = 1, sin = rot exactly
+    float c = rot == 0.0f ? 1.0f : pcos(rot), s = rot == 0.0f ? rot : psin(rot);
     t = t * c + cross(n, t) * s + n * dot(n, t) * (1.0f - c);
     b = cross(n, t);
 }

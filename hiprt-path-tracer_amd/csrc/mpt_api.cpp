@@ -74,6 +74,9 @@ struct MptContext {
     DBuf<uint8_t> has_n, tex;
     DBuf<uint64_t> tex_off;
     DBuf<MptMaterial> mats;
+    DBuf<MptMaterial> mats_res;   // untextured intersection-time resolution per material
+    DBuf<int32_t> mat_tex;
+    bool any_tex = false;
     std::vector<MptMaterial> h_mats;
     int n_tex = 0;
     // luts / envmap
@@ -86,12 +89,13 @@ struct MptContext {
     // paths
     int res_x = 0, res_y = 0, band_h = 1, band_i = 0, band_c = 1, n_slots = 0;
     DBuf<float4> ray_o, ray_d, hit, thr, col, alb, nrmv, nq_o, nq_d, nhit;
-    DBuf<uint8_t> hit_inside, occ;
+    DBuf<uint8_t> hit_inside, occ, qmask;
     DBuf<uint32_t> rng, spill;
     DBuf<uint4> vsA, vsB;
     DBuf<int32_t> q0, q1, counters, nq_tgt, fetch_raw;
     DBuf<NeeRec> nee;
     DBuf<float> fb_color, fb_albedo, fb_normal;
+    DBuf<MptMaterial> mat_slot;
     DBuf<uint64_t> stats;
     DBuf<uint64_t> ray_counts;
     // frames
@@ -111,8 +115,8 @@ struct MptContext {
     uint32_t frames_submitted = 0;
     uint32_t trace_launches = 0;
     uint32_t frames = 0;
-    double stage_ms[3] = {0, 0, 0};
-    uint32_t stage_launches[3] = {0, 0, 0};
+    double stage_ms[KT_COUNT] = {};
+    uint32_t stage_launches[KT_COUNT] = {};
     double frame_ms = 0.0;
     // raw traces
     DBuf<float4> raw_o, raw_d, raw_hit;
@@ -132,6 +136,8 @@ DevScene dev_scene(MptContext* c) {
     S.uv = c->uv.p;
     S.mat_idx = c->mat_idx.p;
     S.mats = c->mats.p;
+    S.mats_res = c->mats_res.p;
+    S.mat_tex = c->mat_tex.p;
     S.mat_prio = c->mat_prio.p;
     S.emissive = c->emissive.p;
     S.n_emissive = (int32_t)c->emissive.n;
@@ -178,7 +184,9 @@ DevPaths dev_paths(MptContext* c) {
     P.nq_d = c->nq_d.p;
     P.nq_tgt = c->nq_tgt.p;
     P.occ = c->occ.p;
+    P.qmask = c->qmask.p;
     P.nhit = c->nhit.p;
+    P.mat_slot = c->mat_slot.p;
     P.fb_color = c->fb_color.p;
     P.fb_albedo = c->fb_albedo.p;
     P.fb_normal = c->fb_normal.p;
@@ -206,11 +214,24 @@ int ensure_paths(MptContext* c, int rx, int ry, int bh, int bi, int bc) {
     HIPCHK(c->rng.alloc(N)); HIPCHK(c->thr.alloc(N)); HIPCHK(c->col.alloc(N)); HIPCHK(c->vsA.alloc(N)); HIPCHK(c->vsB.alloc(N));
     HIPCHK(c->alb.alloc(N)); HIPCHK(c->nrmv.alloc(N)); HIPCHK(c->q0.alloc(N)); HIPCHK(c->q1.alloc(N));
     HIPCHK(c->nee.alloc(N)); HIPCHK(c->nq_o.alloc(4 * N)); HIPCHK(c->nq_d.alloc(4 * N)); HIPCHK(c->nq_tgt.alloc(4 * N));
-    HIPCHK(c->occ.alloc(3 * N)); HIPCHK(c->nhit.alloc(N));
+    HIPCHK(c->occ.alloc(4 * N)); HIPCHK(c->nhit.alloc(N)); HIPCHK(c->qmask.alloc(N));
     HIPCHK(c->fb_color.alloc(3 * N)); HIPCHK(c->fb_albedo.alloc(3 * N)); HIPCHK(c->fb_normal.alloc(3 * N));
     HIPCHK(hipMemsetAsync(c->fb_color.p, 0, 3 * N * sizeof(float), c->stream));
     HIPCHK(hipMemsetAsync(c->fb_albedo.p, 0, 3 * N * sizeof(float), c->stream));
     HIPCHK(hipMemsetAsync(c->fb_normal.p, 0, 3 * N * sizeof(float), c->stream));
+    return MPT_OK;
+}
+
+int resolve_materials(MptContext* c) {
+    size_t n = c->h_mats.size();
+    HIPCHK(c->mats_res.alloc(n));
+    HIPCHK(c->mat_tex.alloc(n));
+    HIPCHK(launch_resolve_materials(dev_scene(c), c->mats_res.p, c->mat_tex.p, (int)n, c->stream));
+    std::vector<int32_t> t(n);
+    HIPCHK(hipMemcpyAsync(t.data(), c->mat_tex.p, n * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    c->any_tex = false;
+    for (int32_t v : t) c->any_tex |= v != 0;
     return MPT_OK;
 }
 
@@ -247,7 +268,7 @@ int collect_pool(MptContext* c, int p) {
         float ms = 0.0f;
         HIPCHK(hipEventElapsedTime(&ms, c->ev[p][i], c->ev[p][i + 1]));
         int m = c->ev_mode[p][i / 2];
-        if (m >= 0 && m < 3) { c->stage_ms[m] += ms; c->stage_launches[m]++; }
+        if (m >= 0 && m < KT_COUNT) { c->stage_ms[m] += ms; c->stage_launches[m]++; }
     }
     float fms = 0.0f;
     HIPCHK(hipEventElapsedTime(&fms, c->ev_frame[p][0], c->ev_frame[p][1]));
@@ -325,10 +346,11 @@ int mpt_destroy(MptContext* c) {
     c->nodes.release(); c->tris.release(); c->idx.release(); c->mat_idx.release(); c->mat_prio.release();
     c->emissive.release(); c->tex_dims.release(); c->pos.release(); c->nrm.release(); c->uv.release();
     c->has_n.release(); c->tex.release(); c->tex_off.release(); c->mats.release();
+    c->mats_res.release(); c->mat_tex.release(); c->mat_slot.release();
     c->lut_conductor.release(); c->lut_glossy.release(); c->lut_glass.release(); c->lut_glass_inv.release();
     c->lut_thin.release(); c->lut_sheen.release(); c->env.release(); c->alias_p.release(); c->alias_i.release();
     c->ray_o.release(); c->ray_d.release(); c->hit.release(); c->thr.release(); c->col.release(); c->alb.release();
-    c->nrmv.release(); c->nq_o.release(); c->nq_d.release(); c->nhit.release(); c->hit_inside.release(); c->occ.release();
+    c->nrmv.release(); c->nq_o.release(); c->nq_d.release(); c->nhit.release(); c->hit_inside.release(); c->occ.release(); c->qmask.release();
     c->rng.release(); c->spill.release(); c->vsA.release(); c->vsB.release(); c->q0.release(); c->q1.release();
     c->counters.release(); c->nq_tgt.release(); c->fetch_raw.release(); c->nee.release(); c->fb_color.release();
     c->fb_albedo.release(); c->fb_normal.release(); c->stats.release(); c->ray_counts.release();
@@ -397,6 +419,8 @@ int mpt_upload_scene(MptContext* c, const MptScene* s) {
         HIPCHK(c->tex_dims.upload(s->texture_dims, 2 * (size_t)s->num_textures, st));
         HIPCHK(hipStreamSynchronize(st));
     } else HIPCHK(hipStreamSynchronize(st));
+    int rr = resolve_materials(c);
+    if (rr != MPT_OK) return rr;
     c->has_scene = true;
     return MPT_OK;
 }
@@ -412,7 +436,7 @@ int mpt_update_materials(MptContext* c, const MptMaterial* m, int32_t count) {
     for (int i = 0; i < count; i++) prio[i] = m[i].dielectric_priority;
     HIPCHK(c->mat_prio.upload(prio.data(), prio.size(), c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
-    return MPT_OK;
+    return resolve_materials(c);
 }
 
 int mpt_build_alias_table(const float* rgba, int32_t w, int32_t h, float* out_p, int32_t* out_a, float* out_sum) {
@@ -507,6 +531,10 @@ int mpt_render_frame(MptContext* c, const MptFrame* f) {
     HIPCHK(hipSetDevice(c->device));
     int r = ensure_paths(c, f->res_x, f->res_y, f->band_height, f->band_index, f->band_count);
     if (r != MPT_OK) return r;
+    if ((c->any_tex || f->bsdf_flags.white_furnace_mode) && c->mat_slot.n < (size_t)std::max(c->n_slots, 1)) {
+        HIPCHK(hipStreamSynchronize(c->stream));
+        HIPCHK(c->mat_slot.alloc((size_t)std::max(c->n_slots, 1)));
+    }
     // stage the frame constants through a pinned ring (the previous use of the slot
     // has completed once 64 frames later are enqueued; synchronise defensively)
     int slot = c->frame_slot;
@@ -577,7 +605,7 @@ int mpt_enable_stats(MptContext* c, int enable, int instrumented) {
     c->trace_launches = 0;
     c->frames = 0;
     c->frame_ms = 0.0;
-    for (int m = 0; m < 3; m++) { c->stage_ms[m] = 0.0; c->stage_launches[m] = 0; }
+    for (int m = 0; m < KT_COUNT; m++) { c->stage_ms[m] = 0.0; c->stage_launches[m] = 0; }
     HIPCHK(hipMemsetAsync(c->stats.p, 0, N_STATS * sizeof(uint64_t), c->stream));
     HIPCHK(hipMemsetAsync(c->ray_counts.p, 0, 4 * sizeof(uint64_t), c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
@@ -610,6 +638,12 @@ int mpt_get_stats(MptContext* c, MptStats* out) {
         out->stage_launches[m] = c->stage_launches[m];
         out->trace_ms += c->stage_ms[m];
     }
+    out->camera_ms = c->stage_ms[KT_CAMERA];
+    out->shade_ms = c->stage_ms[KT_SHADE];
+    out->resolve_ms = c->stage_ms[KT_RESOLVE];
+    out->accumulate_ms = c->stage_ms[KT_ACCUMULATE];
+    out->compact_ms = c->stage_ms[KT_COMPACT];
+    out->shade_launches = c->stage_launches[KT_SHADE];
     out->trace_launches = c->trace_launches;
     out->frames = c->frames;
     out->frame_ms = c->frame_ms;

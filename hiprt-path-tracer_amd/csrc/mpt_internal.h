@@ -27,6 +27,8 @@ struct DevScene {
     const float* uv;             // 2 per vertex
     const int32_t* mat_idx;      // per triangle
     const MptMaterial* mats;
+    const MptMaterial* mats_res;  // per material: intersection-time resolution without textures
+    const int32_t* mat_tex;       // per material: 1 if any texture feeds the resolved material
     const int32_t* mat_prio;     // dielectric_priority per material (nested-dielectric push)
     const int32_t* emissive;
     int32_t n_emissive;
@@ -94,11 +96,13 @@ struct DevPaths {
     int32_t* q1;
     int32_t* counters;        // see CTR_*
     NeeRec* nee;
-    float4* nq_o;             // NEE query rays: [0, n*3) any-hit area, [n*3, n*4) closest area
+    float4* nq_o;             // staged NEE query rays, slot * 4 + kind (kinds 0..2 any hit, 3 closest)
     float4* nq_d;
-    int32_t* nq_tgt;          // target: slot*4 + kind
-    uint8_t* occ;             // 3 per slot
+    int32_t* nq_tgt;          // compacted query lists: [0, 3n) any hit, [3n, 4n) closest; entries slot * 4 + kind
+    uint8_t* qmask;           // per slot: staged queries (bits 0..3), continuation (QM_CONT)
+    uint8_t* occ;             // any-hit results, slot * 4 + kind
     float4* nhit;             // closest NEE result per slot
+    MptMaterial* mat_slot;    // per-slot resolved material (textured materials, white furnace)
     float* fb_color;          // 3 per slot (sum)
     float* fb_albedo;
     float* fb_normal;
@@ -108,6 +112,9 @@ struct DevPaths {
 };
 
 constexpr int N_TRACE_MODES = 5;
+// timed kernel kinds: 0..2 = traversal stages (trace modes), then the others
+enum { KT_CAMERA = 3, KT_SHADE = 4, KT_RESOLVE = 5, KT_ACCUMULATE = 6, KT_COMPACT = 7, KT_COUNT = 8 };
+constexpr uint32_t QM_CONT = 16u;
 constexpr int N_STATS = N_TRACE_MODES * 4;
 
 enum {
@@ -128,6 +135,7 @@ struct LaunchCfg {
 
 hipError_t launch_frame(const DevScene& S, const DevPaths& P, const MptFrame* d_frame, const MptFrame& h_frame,
                         LaunchCfg& cfg, hipStream_t st);
+hipError_t launch_resolve_materials(const DevScene& S, MptMaterial* out_res, int32_t* out_tex, int n, hipStream_t st);
 hipError_t launch_trace_raw(const DevScene& S, const float4* o, const float4* d, int n, bool any, float4* out_hit,
                             uint8_t* out_occ, int32_t* fetch_ctr, uint32_t* spill, int grid, hipStream_t st);
 

@@ -35,6 +35,11 @@
 namespace mpt {
 
 constexpr int TB = TRAV_BLOCK;
+constexpr int MAX_BOUNDARY_SKIPS = 16;   // trace_ray's volume-boundary skip loop bound
+#ifndef MPT_TRACE_FETCH
+#define MPT_TRACE_FETCH 64
+#endif
+constexpr int TRACE_FETCH = MPT_TRACE_FETCH;   // rays claimed per wave and atomic
 constexpr int LDS_STACK = TRAV_LDS_STACK;
 constexpr int SPILL_DEPTH = TRAV_SPILL_DEPTH;
 
@@ -208,17 +213,22 @@ __global__ __launch_bounds__(TB) void k_trace(TraceArgs A) {
     uint32_t n_nodes = 0, n_tris = 0, n_rays = 0;
     const bool any = (MODE == TM_NEE_ANY || MODE == TM_RAW_ANY);
     while (true) {
+        // one atomic per TRACE_FETCH rays (same-address atomics serialise in L2)
         int base = 0;
-        if (lane_id() == 0) base = atomicAdd(A.fetch, 64);
+        if (lane_id() == 0) base = atomicAdd(A.fetch, TRACE_FETCH);
         base = __shfl(base, 0);
         if (base >= count) break;
-        int i = base + lane_id();
-        if (i >= count) continue;
+        for (int sub = 0; sub < TRACE_FETCH / 64; sub++) {
+        int i = base + sub * 64 + lane_id();
+        if (i >= count) break;
         float4 ro, rd;
         int slot = 0;
         if (MODE == TM_PATH) { slot = A.queue[i]; ro = P.ray_o[slot]; rd = P.ray_d[slot]; }
-        else if (MODE == TM_NEE_ANY) { ro = P.nq_o[i]; rd = P.nq_d[i]; }
-        else if (MODE == TM_NEE_CLOSEST) { ro = P.nq_o[(size_t)P.n * 3 + i]; rd = P.nq_d[(size_t)P.n * 3 + i]; }
+        else if (MODE == TM_NEE_ANY || MODE == TM_NEE_CLOSEST) {
+            // compacted list of staged queries (entry = slot * 4 + kind), see k_compact
+            slot = P.nq_tgt[MODE == TM_NEE_ANY ? (size_t)i : (size_t)P.n * 3 + i];
+            ro = P.nq_o[slot]; rd = P.nq_d[slot];
+        }
         else { ro = A.raw_o[i]; rd = A.raw_d[i]; }
         v3 o = mk3(ro.x, ro.y, ro.z), d = mk3(rd.x, rd.y, rd.z);
         int last_hit = (int)__float_as_uint(ro.w);
@@ -228,6 +238,7 @@ __global__ __launch_bounds__(TB) void k_trace(TraceArgs A) {
             VState vs = vs_load(P.vsA, P.vsB, slot);
             bool was_inside = false;
             bool found;
+            int skips = 0;
             while (true) {
                 n_rays++;
                 found = traverse<false, STATS>(S, o, d, last_hit, INFINITY, h, lds, spill, n_nodes, n_tris);
@@ -237,6 +248,9 @@ __global__ __launch_bounds__(TB) void k_trace(TraceArgs A) {
                 int mi = S.mat_idx[h.prim];
                 bool skip = vs_push(vs, mi, S.mat_prio[mi]);
                 if (!skip) break;
+                // bounded like the oracle: a re-traced ray can keep re-hitting the triangle
+                // it sits on (only the original last hit is filtered), see DESIGN.md
+                if (++skips >= MAX_BOUNDARY_SKIPS) break;
                 o = o + h.t * d;
                 vs.dist += h.t;
             }
@@ -249,10 +263,9 @@ __global__ __launch_bounds__(TB) void k_trace(TraceArgs A) {
             bool found = any ? traverse<true, STATS>(S, o, d, last_hit, rd.w, h, lds, spill, n_nodes, n_tris)
                              : traverse<false, STATS>(S, o, d, last_hit, INFINITY, h, lds, spill, n_nodes, n_tris);
             if (MODE == TM_NEE_ANY) {
-                int tgt = P.nq_tgt[i];
-                P.occ[(tgt >> 2) * 3 + (tgt & 3)] = found ? 1 : 0;
+                P.occ[slot] = found ? 1 : 0;
             } else if (MODE == TM_NEE_CLOSEST) {
-                int tgt = P.nq_tgt[(size_t)P.n * 3 + i];
+                int tgt = slot;
                 // evaluate_shadow_light_ray: a hit counts only below t_max - 1e-4 (Intersect.h:337-343)
                 bool ok = found && h.t < rd.w;
                 P.nhit[tgt >> 2] = make_float4(h.t, h.u, h.v, __uint_as_float((uint32_t)(ok ? h.prim : -1)));
@@ -261,6 +274,7 @@ __global__ __launch_bounds__(TB) void k_trace(TraceArgs A) {
             } else {
                 A.raw_hit[i] = make_float4(h.t, h.u, h.v, __uint_as_float((uint32_t)(found ? h.prim : -1)));
             }
+        }
         }
     }
     if (STATS) {
@@ -488,11 +502,15 @@ DEV Col env_eval(const DevScene& S, const MptFrame& F, v3 d, float& pdf) {
 }
 
 // NEE query emission: any-hit area [0, 3n), closest area [3n, 4n)
-DEV void emit_query(const DevPaths& P, int area_closest, int idx, v3 o, int last_hit, v3 d, float tmax, int tgt) {
-    size_t base = area_closest ? (size_t)P.n * 3 : 0;
-    P.nq_o[base + idx] = make_float4(o.x, o.y, o.z, __uint_as_float((uint32_t)last_hit));
-    P.nq_d[base + idx] = make_float4(d.x, d.y, d.z, tmax);
-    P.nq_tgt[base + idx] = tgt;
+// NEE queries are staged at a fixed place per path (slot * 4 + kind; kinds 0..2 any hit,
+// 3 closest hit) and the bit is set in the path's query mask; k_compact builds the
+// compacted lists afterwards, so k_shade itself issues no atomics (an atomic with a
+// return value would wait for all of the lane's outstanding stores).
+DEV void stage_query(const DevPaths& P, int slot, int kind, uint32_t& qm, v3 o, int last_hit, v3 d, float tmax) {
+    size_t e = (size_t)slot * 4 + kind;
+    P.nq_o[e] = make_float4(o.x, o.y, o.z, __uint_as_float((uint32_t)last_hit));
+    P.nq_d[e] = make_float4(d.x, d.y, d.z, tmax);
+    qm |= 1u << kind;
 }
 
 DEV void store3(float* p, Col c) { p[0] = c.r; p[1] = c.g; p[2] = c.b; }
@@ -503,6 +521,25 @@ DEV v3 load3v(const float* p) { return mk3(p[0], p[1], p[2]); }
 // ----------------------------------------------------------------------------------
 // k_shade: one path vertex up to (not including) the NEE trace results
 // ----------------------------------------------------------------------------------
+// Development instrumentation (-DMPT_SECTION_TIMING): shader-clock cycles per k_shade
+// section (0 hit processing, 1 op pre, 2 BSDF eval, 3 op post, 4 finish), summed over
+// lanes into g_sect; read with mpt_debug_sections.
+#ifdef MPT_SECTION_TIMING
+__device__ unsigned long long g_sect[8];
+#define SECT_BEGIN() uint64_t sect_[5] = {0, 0, 0, 0, 0}; uint64_t tprev_ = __builtin_amdgcn_s_memtime()
+#define SECT(k) do { uint64_t now_ = __builtin_amdgcn_s_memtime(); sect_[k] += now_ - tprev_; tprev_ = now_; } while (0)
+#define SECT_END() do { for (int k_ = 0; k_ < 5; k_++) atomicAdd(&g_sect[k_], (unsigned long long)sect_[k_]); } while (0)
+#else
+#define SECT_BEGIN() do {} while (0)
+#define SECT(k) do {} while (0)
+#define SECT_END() do {} while (0)
+#endif
+
+enum ShadeOp {
+    OP_DONE = 0, OP_RIS_LIGHT, OP_RIS_BSDF, OP_RIS_WIN, OP_MIS_LIGHT, OP_MIS_BSDF, OP_UNI_LIGHT, OP_BSDF_LIGHT,
+    OP_ENV_LIGHT, OP_ENV_BSDF, OP_CONT
+};
+
 struct ShadeArgs {
     DevScene S;
     DevPaths P;
@@ -515,8 +552,11 @@ struct ShadeArgs {
     int32_t* count_next;
 };
 
+#ifndef MPT_SHADE_WAVES
+#define MPT_SHADE_WAVES 1
+#endif
 template <int OVR>
-__global__ __launch_bounds__(TB) void k_shade(ShadeArgs A) {
+__global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MPT_SHADE_WAVES))) void k_shade(ShadeArgs A) {
     const DevScene& S = A.S;
     const DevPaths& P = A.P;
     const MptFrame& F = *A.F;
@@ -533,11 +573,7 @@ __global__ __launch_bounds__(TB) void k_shade(ShadeArgs A) {
     bc.masking = F.bsdf_flags.ggx_masking_shadowing;
 
     bool cont = false;   // continuation ray emitted
-    bool want_any[3] = {false, false, false};
-    bool want_cl = false;
-    v3 q_o[4], q_d[4];
-    float q_t[4];
-    int last_prim = -1;
+    SECT_BEGIN();
     if (valid) {
         float4 ro = P.ray_o[slot], rdv = P.ray_d[slot], hv = P.hit[slot];
         v3 o = mk3(ro.x, ro.y, ro.z), d = mk3(rdv.x, rdv.y, rdv.z);
@@ -549,7 +585,10 @@ __global__ __launch_bounds__(TB) void k_shade(ShadeArgs A) {
         float4 cv = P.col[slot];
         Col rcol = col(cv.x, cv.y, cv.z);
         v3 ip = mk3(0, 0, 0), gn = mk3(0, 0, 0), sn = mk3(0, 0, 0);
-        Mat m;
+        // The material is read through a pointer (L1/L2-resident) instead of being held in
+        // registers: untextured materials use the per-material resolved copy, textured ones
+        // (and white-furnace mode) a per-slot resolved copy written here.
+        const Mat* mp = S.mats_res;
         if (found) {
             // trace_ray hit processing (Intersect.h:154-216)
             float t = hv.x;
@@ -559,7 +598,14 @@ __global__ __launch_bounds__(TB) void k_shade(ShadeArgs A) {
             v2 tc = uv_interp2(S.uv, ti, uv);
             gn = normalize(tri_normal(S, prim));
             sn = shading_normal_of(S, gn, prim, uv, tc);
-            m = intersection_material(S, S.mat_idx[prim], tc, F.bsdf_flags.white_furnace_mode);
+            const int mi = S.mat_idx[prim];
+            if (F.bsdf_flags.white_furnace_mode || S.mat_tex[mi]) {
+                P.mat_slot[slot] = intersection_material(S, mi, tc, F.bsdf_flags.white_furnace_mode);
+                mp = &P.mat_slot[slot];
+            } else {
+                mp = &S.mats_res[mi];
+            }
+            const Mat& m = *mp;
             bool was_inside = P.hit_inside[slot] != 0;
             if ((!was_inside || m.specular_transmission == 0.0f) && !m.thin_walled) {
                 gn *= dot(gn, -d) < 0.0f ? -1.0f : 1.0f;
@@ -570,6 +616,7 @@ __global__ __launch_bounds__(TB) void k_shade(ShadeArgs A) {
             if (m.dispersion_scale > 0.0f && m.specular_transmission > 0.0f && vs.wl == 0.0f)
                 vs.wl = -(rng() * (float)(830 - 360) + (float)360);
         }
+        const Mat& m = *mp;
         if (bounce == 0) {
             // CameraRays G-buffer hand-off (CameraRays.h:147-166) and FullPathTracer's
             // re-read of it (FullPathTracer.h:131-150): emissive flip, normalise, restart RNG
@@ -580,8 +627,9 @@ __global__ __launch_bounds__(TB) void k_shade(ShadeArgs A) {
             int x, y;
             rng = make_rng(pixel_seed(F, slot_pixel(F, slot, x, y)));
         }
-        NeeRec nr;
+        NeeRec& nr = P.nee[slot];   // written field by field, straight to HBM
         uint32_t fl = 0;
+        uint32_t qm = 0;            // staged NEE queries (bits 0..3) + continuation (bit 4)
         if (found) {
             if (bounce == 0) {
                 float4 a = P.alb[slot], n4 = P.nrm[slot];
@@ -590,262 +638,252 @@ __global__ __launch_bounds__(TB) void k_shade(ShadeArgs A) {
             }
             if (is_emissive(m) && dot(-d, gn) < 0) { gn = -gn; sn = -sn; }
             v3 view = -d;
-            last_prim = prim;
             fl |= NF_SHADED;
             const int lss = F.options.direct_light_sampling;
-            // ---------------- direct light (Lights.h:277-321) ----------------
+            const MptWorldSettings& ws = F.world_settings;
+            // ---------------- which BSDF operations this vertex runs, in RNG order ----------------
             bool do_light = S.n_emissive != 0 && !(F.bsdf_flags.white_furnace_mode && F.bsdf_flags.white_furnace_mode_turn_off_emissives);
             if (do_light && is_emissive(m)) {
                 do_light = false;
                 if (m.emissive_texture_used && bounce > 0) { fl |= NF_IMM; store3(nr.imm, emission_of(m)); }
             }
-            if (do_light && lss != MPT_LSS_NO_DIRECT_LIGHT_SAMPLING) {
-                fl |= NF_L;
-                bool inside = dot(view, gn) < 0;
-                float ism = inside ? -1.0f : 1.0f;
-                if (lss == MPT_LSS_RIS_BSDF_AND_LIGHT) {
-                    // sample_bsdf_and_lights_RIS_reservoir (RIS.h:82-289)
-                    v3 ep = ip + sn * 1.0e-4f * ism;
-                    int nl = rs.ris_number_of_light_candidates, nbc = rs.ris_number_of_bsdf_candidates;
-                    float wsum = 0.0f, targetW = 0.0f;
-                    v3 pointW = mk3(0, 0, 0);
-                    int triW = -1;
-                    bool hasW = false;
-                    for (int c = 0; c < nl; c++) {
-                        float lpdf;
-                        LightInfo li;
-                        float target = 0.0f, cw = 0.0f;
-                        v3 lp = sample_emissive_triangle(S, rng, lpdf, li);
-                        if (lpdf > 0.0f) {
-                            v3 tl = lp - ep;
-                            float dist = length(tl);
-                            tl = tl / dist;
-                            float cl = absr(dot(li.normal, -tl));
-                            float ce = maxr(0.0f, dot(sn * ism, tl));
-                            if (ce > 0.0f && cl > 1.0e-6f) {
-                                lpdf *= dist * dist;
-                                lpdf /= cl;
-                                float bp = 0.0f;
-                                if (!min_contrib(rs.minimum_light_contribution, li.emission / lpdf)) target = 0.0f;
-                                else {
-                                    VState tv = vs;
-                                    Col bcol = bsdf_eval<OVR>(bc, m, tv, view, sn, tl, bp);
-                                    Col lc = bcol * li.emission * ce;
-                                    target = min_contrib(rs.minimum_light_contribution, lc / bp / lpdf) ? lum(lc) : 0.0f;
-                                }
-                                cw = balance(lpdf, (float)nl, bp, (float)nbc) * target / lpdf;
-                            }
+            do_light = do_light && lss != MPT_LSS_NO_DIRECT_LIGHT_SAMPLING;
+            if (do_light) fl |= NF_L;
+            const bool do_env = ws.ambient_light_type == MPT_AMBIENT_ENVMAP && !F.bsdf_flags.white_furnace_mode &&
+                                !is_emissive(m) && ws.envmap_intensity > 0.0f && F.options.envmap_sampling != MPT_ESS_NO_SAMPLING;
+            const bool env_use = lss != MPT_LSS_NO_DIRECT_LIGHT_SAMPLING;
+            const bool do_cont = bounce < A.last_bounce;
+            const float ism = dot(view, gn) < 0 ? -1.0f : 1.0f;
+            const v3 ep = ip + sn * 1.0e-4f * ism;              // NEE origin (Lights.h / RIS.h)
+            const int nl = rs.ris_number_of_light_candidates, nbc = rs.ris_number_of_bsdf_candidates;
+            int op = OP_DONE;
+            if (do_light) {
+                if (lss == MPT_LSS_RIS_BSDF_AND_LIGHT) op = nl > 0 ? OP_RIS_LIGHT : (nbc > 0 ? OP_RIS_BSDF : OP_RIS_WIN);
+                else if (lss == MPT_LSS_MIS_LIGHT_BSDF) op = OP_MIS_LIGHT;
+                else if (lss == MPT_LSS_UNIFORM_ONE_LIGHT) op = OP_UNI_LIGHT;
+                else if (lss == MPT_LSS_BSDF) op = OP_BSDF_LIGHT;
+            }
+            if (op == OP_DONE) op = do_env ? OP_ENV_LIGHT : (do_cont ? OP_CONT : OP_DONE);
+            // RIS reservoir (sample_bsdf_and_lights_RIS_reservoir, RIS.h:82-289)
+            float wsum = 0.0f, targetW = 0.0f;
+            v3 pointW = mk3(0, 0, 0);
+            int triW = -1, ris_c = 0;
+            bool hasW = false;
+            const Col thr_vertex = thr;
+            // One BSDF evaluation site for every operation of the vertex: each iteration
+            // prepares a direction (light / envmap sample, or a BSDF lobe sample), evaluates
+            // the BSDF once, and consumes the result.  All lanes of a wave meet at the same
+            // evaluation whatever operation they are on.
+            SECT(0);
+            while (op != OP_DONE) {
+                VState tv = vs;
+                v3 L = mk3(0.0f, 0.0f, 0.0f);
+                bool do_eval = false;
+                float lpdf = 0.0f, dist = 0.0f, geo = 0.0f;
+                LightInfo li;
+                li.tri = -1; li.emission = col(0.0f);
+                v3 lp = mk3(0.0f, 0.0f, 0.0f);
+                Col ec = col(0.0f);
+                bool inner = false;
+                if (op == OP_RIS_BSDF || op == OP_MIS_BSDF || op == OP_BSDF_LIGHT || op == OP_ENV_BSDF || op == OP_CONT) {
+                    do_eval = bsdf_sample_dir<OVR>(bc, m, tv, view, sn, gn, L, rng);
+                } else if (op == OP_RIS_LIGHT) {
+                    lp = sample_emissive_triangle(S, rng, lpdf, li);
+                    if (lpdf > 0.0f) {
+                        v3 tl = lp - ep;
+                        dist = length(tl);
+                        tl = tl / dist;
+                        float cl = absr(dot(li.normal, -tl));
+                        geo = maxr(0.0f, dot(sn * ism, tl));
+                        if (geo > 0.0f && cl > 1.0e-6f) {
+                            inner = true;
+                            lpdf *= dist * dist;
+                            lpdf /= cl;
+                            if (min_contrib(rs.minimum_light_contribution, li.emission / lpdf)) { L = tl; do_eval = true; }
                         }
-                        wsum += cw;
-                        if (rng() < cw / wsum) { hasW = true; targetW = target; pointW = lp; triW = li.tri; }
                     }
+                } else if (op == OP_RIS_WIN) {
+                    // evaluate_reservoir_sample for the light winner (RIS.h:18-80), speculatively
+                    v3 ep2 = ip + sn * 1.0e-4f;
+                    v3 sd = pointW - ep2;
+                    dist = length(sd);
+                    L = sd / dist;
+                    lp = ep2;
+                    do_eval = hasW;
+                } else if (op == OP_MIS_LIGHT || op == OP_UNI_LIGHT) {
+                    // sample_one_light_MIS (Lights.h:115-220) / _no_MIS (Lights.h:22-65)
+                    lp = sample_emissive_triangle(S, rng, lpdf, li);
+                    if (lpdf > 0.0f) {
+                        v3 so = op == OP_MIS_LIGHT ? ep : ip + sn * 1.0e-4f;
+                        v3 sd = lp - so;
+                        dist = length(sd);
+                        L = sd / dist;
+                        geo = absr(dot(li.normal, -L));
+                        lp = so;
+                        do_eval = geo > 0.0f;
+                    }
+                } else if (op == OP_ENV_LIGHT) {
+                    ec = env_sample(S, F, L, lpdf, rng);
+                    geo = dot(sn, L);
+                    do_eval = lpdf > 0.0f && geo > 0.0f;
+                }
+                float pdf = 0.0f;
+                Col f = col(0.0f);
+                SECT(1);
+                if (do_eval) f = bsdf_eval<OVR>(bc, m, tv, view, sn, L, pdf);
+                SECT(2);
+                int next = OP_DONE;
+                if (op == OP_RIS_LIGHT) {
+                    float target = 0.0f, cw = 0.0f;
+                    if (inner) {
+                        float bp = 0.0f;
+                        if (do_eval) {
+                            bp = pdf;
+                            Col lc = f * li.emission * geo;
+                            target = min_contrib(rs.minimum_light_contribution, lc / bp / lpdf) ? lum(lc) : 0.0f;
+                        }
+                        cw = balance(lpdf, (float)nl, bp, (float)nbc) * target / lpdf;
+                    }
+                    wsum += cw;
+                    if (rng() < cw / wsum) { hasW = true; targetW = target; pointW = lp; triW = li.tri; }
+                    ris_c++;
+                    next = ris_c < nl ? OP_RIS_LIGHT : (nbc > 0 ? OP_RIS_BSDF : OP_RIS_WIN);
+                } else if (op == OP_RIS_BSDF) {
+                    bool refr = dot(L, sn * ism) < 0;
+                    v3 so = refr ? ip + sn * 1.0e-4f * ism * -1.0f : ep;
+                    if (pdf > 0.0f) {
+                        fl |= NF_B | (refr ? NF_B_REFR : 0u);
+                        stage_query(P, slot, 3, qm, so, prim, L, 1.0e35f - 1.0e-4f);
+                        store3(nr.b, f);
+                        nr.b_pdf = pdf;
+                        store3(nr.dir, L);
+                        nr.b_cos = absr(dot(sn, L));
+                    }
+                    nr.r_add = rng();
+                    next = OP_RIS_WIN;
+                } else if (op == OP_RIS_WIN) {
                     nr.ris_wsum = wsum;
-                    if (nbc > 0) {
-                        // the BSDF candidate (nb = 1; validated on the host)
-                        float bpdf = 0.0f;
-                        v3 dir;
-                        VState tv = vs;
-                        Col bcol = bsdf_sample<OVR>(bc, m, tv, view, sn, gn, dir, bpdf, rng);
-                        bool refr = dot(dir, sn * ism) < 0;
-                        v3 so = refr ? ip + sn * 1.0e-4f * ism * -1.0f : ep;
-                        if (bpdf > 0.0f) {
-                            fl |= NF_B | (refr ? NF_B_REFR : 0u);
-                            want_cl = true;
-                            q_o[3] = so; q_d[3] = dir; q_t[3] = 1.0e35f - 1.0e-4f;
-                            store3(nr.b, bcol);
-                            nr.b_pdf = bpdf;
-                            store3(nr.dir, dir);
-                            nr.b_cos = absr(dot(sn, dir));
-                        }
-                        nr.r_add = rng();
-                    }
                     if (hasW) {
-                        // evaluate_reservoir_sample for the light winner (RIS.h:18-80), speculatively
                         fl |= NF_RIS_W;
-                        v3 ep2 = ip + sn * 1.0e-4f;
-                        v3 sd = pointW - ep2;
-                        float dist = length(sd);
-                        v3 sdn = sd / dist;
-                        want_any[0] = true;
-                        q_o[0] = ep2; q_d[0] = sdn; q_t[0] = dist - 1.0e-4f;
-                        float bp;
-                        VState tv = vs;
-                        Col bcol = bsdf_eval<OVR>(bc, m, tv, view, sn, sdn, bp);
-                        store3(nr.a, bcol);
-                        nr.a_cos = maxr(0.0f, dot(sn, sdn));
+                        stage_query(P, slot, 0, qm, lp, prim, L, dist - 1.0e-4f);
+                        store3(nr.a, f);
+                        nr.a_cos = maxr(0.0f, dot(sn, L));
                         nr.ris_target = targetW;
                         nr.ris_tri = triW;
                     }
-                } else if (lss == MPT_LSS_MIS_LIGHT_BSDF) {
-                    // sample_one_light_MIS (Lights.h:115-220)
-                    v3 ep = ip + sn * 1.0e-4f * ism;
-                    float lpdf;
-                    LightInfo li;
-                    v3 lp = sample_emissive_triangle(S, rng, lpdf, li);
-                    if (lpdf > 0.0f) {
-                        v3 sd = lp - ep;
-                        float dist = length(sd);
-                        v3 sdn = sd / dist;
-                        float dl = absr(dot(li.normal, -sdn));
-                        if (dl > 0.0f) {
-                            float bp;
-                            VState tv = vs;
-                            Col bcol = bsdf_eval<OVR>(bc, m, tv, view, sn, sdn, bp);
-                            if (bp != 0.0f) {
-                                float lp2 = lpdf;
-                                lp2 *= dist * dist;
-                                lp2 /= dl;
-                                float w = balance(lp2, bp);
-                                float cosv = maxr(dot(sn, sdn), 0.0f);
-                                store3(nr.a, bcol * cosv * li.emission * w / lp2);
-                                fl |= NF_A;
-                                want_any[0] = true;
-                                q_o[0] = ep; q_d[0] = sdn; q_t[0] = dist - 1.0e-4f;
-                            }
-                        }
-                        float dpdf;
-                        v3 dir;
-                        VState tv = vs;
-                        Col bcol = bsdf_sample<OVR>(bc, m, tv, view, sn, gn, dir, dpdf, rng);
-                        bool refr = dot(dir, sn * ism) < 0;
-                        v3 bo = refr ? ip + sn * 1.0e-4f * ism * -1.0f : ep;
-                        if (dpdf > 0) {
-                            fl |= NF_B;
-                            want_cl = true;
-                            q_o[3] = bo; q_d[3] = dir; q_t[3] = 1.0e35f - 1.0e-4f;
-                            store3(nr.b, bcol);
-                            nr.b_pdf = dpdf;
-                            store3(nr.dir, dir);
-                            nr.b_cos = absr(dot(sn, dir));
-                        }
+                    next = OP_DONE;
+                } else if (op == OP_MIS_LIGHT) {
+                    if (do_eval && pdf != 0.0f) {
+                        float lp2 = lpdf;
+                        lp2 *= dist * dist;
+                        lp2 /= geo;
+                        float w = balance(lp2, pdf);
+                        float cosv = maxr(dot(sn, L), 0.0f);
+                        store3(nr.a, f * cosv * li.emission * w / lp2);
+                        fl |= NF_A;
+                        stage_query(P, slot, 0, qm, lp, prim, L, dist - 1.0e-4f);
                     }
-                } else if (lss == MPT_LSS_UNIFORM_ONE_LIGHT) {
-                    // sample_one_light_no_MIS (Lights.h:22-65)
-                    float lpdf;
-                    LightInfo li;
-                    v3 lp = sample_emissive_triangle(S, rng, lpdf, li);
-                    if (lpdf > 0.0f) {
-                        v3 so = ip + sn * 1.0e-4f;
-                        v3 sd = lp - so;
-                        float dist = length(sd);
-                        v3 sdn = sd / dist;
-                        float dl = absr(dot(li.normal, -sdn));
-                        if (dl > 0.0f) {
-                            float bp;
-                            VState tv = vs;
-                            Col bcol = bsdf_eval<OVR>(bc, m, tv, view, sn, sdn, bp);
-                            if (bp != 0.0f) {
-                                float lp2 = lpdf;
-                                lp2 *= dist * dist;
-                                lp2 /= dl;
-                                float cosv = maxr(dot(sn, sdn), 0.0f);
-                                store3(nr.a, li.emission * cosv * bcol / lp2);
-                                fl |= NF_A;
-                                want_any[0] = true;
-                                q_o[0] = so; q_d[0] = sdn; q_t[0] = dist - 1.0e-4f;
-                            }
-                        }
+                    next = lpdf > 0.0f ? OP_MIS_BSDF : OP_DONE;
+                } else if (op == OP_MIS_BSDF) {
+                    bool refr = dot(L, sn * ism) < 0;
+                    v3 bo = refr ? ip + sn * 1.0e-4f * ism * -1.0f : ep;
+                    if (pdf > 0) {
+                        fl |= NF_B;
+                        stage_query(P, slot, 3, qm, bo, prim, L, 1.0e35f - 1.0e-4f);
+                        store3(nr.b, f);
+                        nr.b_pdf = pdf;
+                        store3(nr.dir, L);
+                        nr.b_cos = absr(dot(sn, L));
                     }
-                } else if (lss == MPT_LSS_BSDF) {
+                } else if (op == OP_UNI_LIGHT) {
+                    if (do_eval && pdf != 0.0f) {
+                        float lp2 = lpdf;
+                        lp2 *= dist * dist;
+                        lp2 /= geo;
+                        float cosv = maxr(dot(sn, L), 0.0f);
+                        store3(nr.a, li.emission * cosv * f / lp2);
+                        fl |= NF_A;
+                        stage_query(P, slot, 0, qm, lp, prim, L, dist - 1.0e-4f);
+                    }
+                } else if (op == OP_BSDF_LIGHT) {
                     // sample_one_light_bsdf (Lights.h:67-113)
-                    float dpdf;
-                    v3 dir;
-                    VState tv = vs;
-                    Col bcol = bsdf_sample<OVR>(bc, m, tv, view, sn, gn, dir, dpdf, rng);
-                    bool refr = dot(dir, sn * ism) < 0;
-                    if (dpdf > 0.0f) {
+                    bool refr = dot(L, sn * ism) < 0;
+                    if (pdf > 0.0f) {
                         v3 no = refr ? ip + sn * 1.0e-4f * ism * -1.0f : ip + sn * 1.0e-4f;
                         fl |= NF_B;
-                        want_cl = true;
-                        q_o[3] = no; q_d[3] = dir; q_t[3] = 1.0e35f - 1.0e-4f;
-                        store3(nr.b, bcol);
-                        nr.b_pdf = dpdf;
-                        store3(nr.dir, dir);
-                        nr.b_cos = maxr(0.0f, dot(sn, dir));
+                        stage_query(P, slot, 3, qm, no, prim, L, 1.0e35f - 1.0e-4f);
+                        store3(nr.b, f);
+                        nr.b_pdf = pdf;
+                        store3(nr.dir, L);
+                        nr.b_cos = maxr(0.0f, dot(sn, L));
                     }
-                }
-            }
-            // ---------------- envmap (Envmap.h:151-246) ----------------
-            const MptWorldSettings& ws = F.world_settings;
-            if (ws.ambient_light_type == MPT_AMBIENT_ENVMAP && !F.bsdf_flags.white_furnace_mode && !is_emissive(m) &&
-                ws.envmap_intensity > 0.0f && F.options.envmap_sampling != MPT_ESS_NO_SAMPLING) {
-                bool use = lss != MPT_LSS_NO_DIRECT_LIGHT_SAMPLING;
-                float epdf;
-                v3 sdir;
-                Col ec = env_sample(S, F, sdir, epdf, rng);
-                float cosv = dot(sn, sdir);
-                if (epdf > 0.0f && cosv > 0.0f) {
-                    float bp;
-                    VState tv = vs;
-                    Col bcol = bsdf_eval<OVR>(bc, m, tv, view, sn, sdir, bp);
-                    float mw = F.options.envmap_bsdf_mis ? balance(epdf, bp) : 1.0f;
-                    store3(nr.e1, bcol * cosv * mw * ec / epdf);
-                    if (use) {
-                        fl |= NF_E1;
-                        want_any[1] = true;
-                        q_o[1] = ip; q_d[1] = sdir; q_t[1] = 1.0e35f - 1.0e-4f;
-                    }
-                }
-                if (F.options.envmap_bsdf_mis) {
-                    float bpdf;
-                    v3 bd;
-                    VState tv = vs;
-                    Col bcol = bsdf_sample<OVR>(bc, m, tv, view, sn, gn, bd, bpdf, rng);
-                    float c2 = absr(dot(sn, bd));
-                    if (bpdf > 0.0f) {
-                        float ep;
-                        Col er = env_eval(S, F, bd, ep);
-                        if (ep > 0.0f && use) {
-                            float mw = balance(bpdf, ep);
-                            store3(nr.e2, er * mw * c2 * bcol / bpdf);
-                            fl |= NF_E2;
-                            want_any[2] = true;
-                            q_o[2] = ip; q_d[2] = bd; q_t[2] = 1.0e35f - 1.0e-4f;
+                } else if (op == OP_ENV_LIGHT) {
+                    // Envmap.h:151-246
+                    if (do_eval) {
+                        float mw = F.options.envmap_bsdf_mis ? balance(lpdf, pdf) : 1.0f;
+                        store3(nr.e1, f * geo * mw * ec / lpdf);
+                        if (env_use) {
+                            fl |= NF_E1;
+                            stage_query(P, slot, 1, qm, ip, prim, L, 1.0e35f - 1.0e-4f);
                         }
                     }
+                    next = F.options.envmap_bsdf_mis ? OP_ENV_BSDF : OP_DONE;
+                } else if (op == OP_ENV_BSDF) {
+                    float c2 = absr(dot(sn, L));
+                    if (pdf > 0.0f) {
+                        float epdf;
+                        Col er = env_eval(S, F, L, epdf);
+                        if (epdf > 0.0f && env_use) {
+                            float mw = balance(pdf, epdf);
+                            store3(nr.e2, er * mw * c2 * f / pdf);
+                            fl |= NF_E2;
+                            stage_query(P, slot, 2, qm, ip, prim, L, 1.0e35f - 1.0e-4f);
+                        }
+                    }
+                } else if (op == OP_CONT) {
+                    // continuation (FullPathTracer.h:221-247)
+                    vs = tv;
+                    Col att = f * absr(dot(L, sn)) / pdf;
+                    if (pdf > 0.0f) {
+                        bool alive = true;
+                        if (bounce >= rs.russian_roulette_min_depth && rs.use_russian_roulette) {
+                            float sp;
+                            if (rs.path_russian_roulette_method == 0) sp = maxc(thr);
+                            else sp = sqrtf(maxc(thr * att) / maxc(thr));
+                            sp = minr(sp, 1.0f);
+                            if (rng() > sp) alive = false;
+                            else {
+                                float inc = 1.0f / sp;
+                                if (rs.russian_roulette_throughput_clamp > 0.0f) inc = minr(inc, rs.russian_roulette_throughput_clamp);
+                                thr *= inc;
+                            }
+                        }
+                        if (alive) {
+                            thr *= dispersion_ray_color(vs.wl, m.dispersion_scale);
+                            thr *= att;
+                            P.ray_o[slot] = make_float4(ip.x, ip.y, ip.z, __uint_as_float((uint32_t)prim));
+                            P.ray_d[slot] = make_float4(L.x, L.y, L.z, INFINITY);
+                            cont = true;
+                        }
+                    }
+                    next = -1;
                 }
+                // after the light strategy: envmap, then the continuation
+                if (next == OP_DONE && op != OP_ENV_LIGHT && op != OP_ENV_BSDF && do_env) next = OP_ENV_LIGHT;
+                else if (next == OP_DONE && do_cont) next = OP_CONT;
+                op = next < 0 ? OP_DONE : next;
+                SECT(3);
             }
             // emission (FullPathTracer.h:192-214)
             if (lss == MPT_LSS_NO_DIRECT_LIGHT_SAMPLING) {
                 Col he = clamp_contrib(emission_of(m), rs.indirect_contribution_clamp, bounce > 0);
-                rcol += he * thr;
+                rcol += he * thr_vertex;
                 fl &= ~(NF_A | NF_B | NF_E1 | NF_E2 | NF_RIS_W | NF_IMM | NF_L);
                 fl |= NF_NOADD;
-                want_any[0] = want_any[1] = want_any[2] = false;
-                want_cl = false;
             } else if (bounce == 0) {
                 rcol += emission_of(m);
             }
-            store3(nr.thr, thr);
-            // ---------------- continuation (FullPathTracer.h:221-247) ----------------
-            if (bounce < A.last_bounce) {
-                float bpdf;
-                v3 bd;
-                Col bcol = bsdf_sample<OVR>(bc, m, vs, view, sn, gn, bd, bpdf, rng);
-                Col att = bcol * absr(dot(bd, sn)) / bpdf;
-                if (bpdf > 0.0f) {
-                    bool alive = true;
-                    if (bounce >= rs.russian_roulette_min_depth && rs.use_russian_roulette) {
-                        float sp;
-                        if (rs.path_russian_roulette_method == 0) sp = maxc(thr);
-                        else sp = sqrtf(maxc(thr * att) / maxc(thr));
-                        sp = minr(sp, 1.0f);
-                        if (rng() > sp) alive = false;
-                        else {
-                            float inc = 1.0f / sp;
-                            if (rs.russian_roulette_throughput_clamp > 0.0f) inc = minr(inc, rs.russian_roulette_throughput_clamp);
-                            thr *= inc;
-                        }
-                    }
-                    if (alive) {
-                        thr *= dispersion_ray_color(vs.wl, m.dispersion_scale);
-                        thr *= att;
-                        P.ray_o[slot] = make_float4(ip.x, ip.y, ip.z, __uint_as_float((uint32_t)prim));
-                        P.ray_d[slot] = make_float4(bd.x, bd.y, bd.z, INFINITY);
-                        cont = true;
-                    }
-                }
-            }
+            store3(nr.thr, thr_vertex);
         } else {
             // miss (FullPathTracer.h:250-284)
             const MptWorldSettings& ws = F.world_settings;
@@ -863,25 +901,103 @@ __global__ __launch_bounds__(TB) void k_shade(ShadeArgs A) {
             rcol += clamp_contrib(sky * thr, rs.indirect_contribution_clamp, bounce > 0);
         }
         nr.flags = fl;
-        if (fl & NF_SHADED) P.nee[slot] = nr;
-        else P.nee[slot].flags = 0;
+        P.qmask[slot] = (uint8_t)(qm | (cont ? QM_CONT : 0u));
         P.rng[slot] = rng.s;
         P.thr[slot] = make_float4(thr.r, thr.g, thr.b, 0.0f);
         P.col[slot] = make_float4(rcol.r, rcol.g, rcol.b, 0.0f);
         vs_store(P.vsA, P.vsB, slot, vs);
     }
     // queue appends (every lane of the wave takes part in the ballots)
-    int qi = wave_append(A.count_next, valid && cont);
-    if (valid && cont) A.q_next[qi] = slot;
+    SECT(4);
+    SECT_END();
+}
+
+// ----------------------------------------------------------------------------------
+// k_compact: next path queue + NEE query lists from the per-path masks (wave64 ballot,
+// one atomic per wave and list; all atomics before any store)
+// ----------------------------------------------------------------------------------
+constexpr int CP_NT = 1024;        // threads per k_compact block
+constexpr int CP_ITEMS = 8;        // queue entries per thread -> 8192 per block, 5 atomics per block
+
+// exclusive block-wide scan of one int per thread (wave64 shuffles + LDS across waves)
+DEV int block_scan_excl(int v, int* tmp, int& total) {
+    const int lane = lane_id(), wid = threadIdx.x >> 6;
+    constexpr int NW = CP_NT / 64;
+    int x = v;
 #pragma unroll
-    for (int k = 0; k < 3; k++) {
-        bool w = valid && want_any[k];
-        int ai = wave_append(&P.counters[CTR_ANY], w);
-        if (w) emit_query(P, 0, ai, q_o[k], last_prim, q_d[k], q_t[k], slot * 4 + k);
+    for (int o = 1; o < 64; o <<= 1) {
+        int y = __shfl_up(x, o);
+        if (lane >= o) x += y;
     }
-    bool wc = valid && want_cl;
-    int ci = wave_append(&P.counters[CTR_CL], wc);
-    if (wc) emit_query(P, 1, ci, q_o[3], last_prim, q_d[3], q_t[3], slot * 4 + 3);
+    if (lane == 63) tmp[wid] = x;
+    __syncthreads();
+    if (wid == 0) {
+        int w = lane < NW ? tmp[lane] : 0;
+        int xs = w;
+#pragma unroll
+        for (int o = 1; o < NW; o <<= 1) {
+            int y = __shfl_up(xs, o);
+            if (lane >= o) xs += y;
+        }
+        if (lane < NW) tmp[lane] = xs - w;
+        if (lane == NW - 1) tmp[NW] = xs;
+    }
+    __syncthreads();
+    int excl = x - v + tmp[wid];
+    total = tmp[NW];
+    __syncthreads();
+    return excl;
+}
+
+__global__ __launch_bounds__(CP_NT) void k_compact(DevPaths P, const int32_t* q_cur, const int32_t* count_cur,
+                                                   int32_t* q_next, int32_t* count_next) {
+    __shared__ int tmp[CP_NT / 64 + 1];
+    __shared__ int base[5];
+    const int count = *count_cur;
+    const int b0 = blockIdx.x * CP_NT * CP_ITEMS;
+    if (b0 >= count) return;                       // whole block beyond the queue
+    uint8_t m[CP_ITEMS];
+    int slots[CP_ITEMS];
+    int c[5] = {0, 0, 0, 0, 0};
+#pragma unroll
+    for (int j = 0; j < CP_ITEMS; j++) {
+        int i = b0 + j * CP_NT + threadIdx.x;      // coalesced
+        slots[j] = i < count ? q_cur[i] : 0;
+        m[j] = i < count ? P.qmask[slots[j]] : 0;
+        c[0] += (m[j] & QM_CONT) ? 1 : 0;
+        c[1] += m[j] & 1u;
+        c[2] += (m[j] >> 1) & 1u;
+        c[3] += (m[j] >> 2) & 1u;
+        c[4] += (m[j] >> 3) & 1u;
+    }
+    int off[5];
+    int32_t* ctr[5] = {count_next, &P.counters[CTR_ANY], &P.counters[CTR_ANY], &P.counters[CTR_ANY], &P.counters[CTR_CL]};
+    // one reservation per list; the three any-hit kinds share one list and one atomic
+    int tot[5];
+#pragma unroll
+    for (int k = 0; k < 5; k++) off[k] = block_scan_excl(c[k], tmp, tot[k]);
+    if (threadIdx.x == 0) {
+        base[0] = tot[0] ? atomicAdd(ctr[0], tot[0]) : 0;
+        int a = tot[1] + tot[2] + tot[3];
+        int ab = a ? atomicAdd(ctr[1], a) : 0;
+        base[1] = ab;
+        base[2] = ab + tot[1];
+        base[3] = ab + tot[1] + tot[2];
+        base[4] = tot[4] ? atomicAdd(ctr[4], tot[4]) : 0;
+    }
+    __syncthreads();
+    int32_t* any = P.nq_tgt;
+    int32_t* cl = P.nq_tgt + (size_t)P.n * 3;
+    int o0 = base[0] + off[0], o1 = base[1] + off[1], o2 = base[2] + off[2], o3 = base[3] + off[3], o4 = base[4] + off[4];
+#pragma unroll
+    for (int j = 0; j < CP_ITEMS; j++) {
+        int sl = slots[j];
+        if (m[j] & QM_CONT) q_next[o0++] = sl;
+        if (m[j] & 1u) any[o1++] = sl * 4 + 0;
+        if (m[j] & 2u) any[o2++] = sl * 4 + 1;
+        if (m[j] & 4u) any[o3++] = sl * 4 + 2;
+        if (m[j] & 8u) cl[o4++] = sl * 4 + 3;
+    }
 }
 
 // ----------------------------------------------------------------------------------
@@ -935,7 +1051,7 @@ __global__ __launch_bounds__(TB) void k_resolve(DevScene S, DevPaths P, const Mp
     if (!(fl & NF_SHADED) || (fl & NF_NOADD)) return;
     const int lss = F.options.direct_light_sampling;
     Col ld = col(0.0f), ed = col(0.0f);
-    const uint8_t* occ = P.occ + (size_t)slot * 3;
+    const uint8_t* occ = P.occ + (size_t)slot * 4;
     if (fl & NF_IMM) ld = load3c(nr.imm);
     else if (!(fl & NF_L)) ld = col(0.0f);
     else if (lss == MPT_LSS_RIS_BSDF_AND_LIGHT) {
@@ -1064,6 +1180,19 @@ static void launch_trace_mode(const TraceArgs& a, int grid, bool stats, hipStrea
     else hipLaunchKernelGGL((k_trace<MODE, false>), dim3(grid), dim3(TB), 0, st, a);
 }
 
+// event pair around a non-traversal kernel (KT_* id), when timing is enabled
+struct TimedScope {
+    LaunchCfg& cfg;
+    hipStream_t st;
+    bool on;
+    TimedScope(LaunchCfg& c, hipStream_t s, int kind) : cfg(c), st(s), on(c.ev_pool && c.ev_used + 2 <= c.ev_cap) {
+        if (on) { cfg.ev_mode[cfg.ev_used / 2] = kind; hipEventRecord(cfg.ev_pool[cfg.ev_used], st); }
+    }
+    ~TimedScope() {
+        if (on) { hipEventRecord(cfg.ev_pool[cfg.ev_used + 1], st); cfg.ev_used += 2; }
+    }
+};
+
 template <int MODE>
 static void timed_trace(const TraceArgs& a, LaunchCfg& cfg, hipStream_t st) {
     bool timed = cfg.ev_pool && cfg.ev_used + 2 <= cfg.ev_cap;
@@ -1077,7 +1206,10 @@ hipError_t launch_frame(const DevScene& S, const DevPaths& P, const MptFrame* d_
                         hipStream_t st) {
     const int n = P.n;
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_camera, dim3(blocks_for(n)), dim3(TB), 0, st, P, d_frame);
+    {
+        TimedScope ts(cfg, st, KT_CAMERA);
+        hipLaunchKernelGGL(k_camera, dim3(blocks_for(n)), dim3(TB), 0, st, P, d_frame);
+    }
     hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(&P.counters[CTR_Q0]), n, 1, st);
     int32_t* q_cur = P.q0;
     int32_t* q_next = P.q1;
@@ -1094,10 +1226,18 @@ hipError_t launch_frame(const DevScene& S, const DevPaths& P, const MptFrame* d_
         ShadeArgs sa;
         sa.S = S; sa.P = P; sa.F = d_frame; sa.bounce = b; sa.last_bounce = nb;
         sa.q_cur = q_cur; sa.count_cur = &P.counters[c_cur]; sa.q_next = q_next; sa.count_next = &P.counters[c_next];
-        if (hf.options.bsdf_override == MPT_BSDF_LAMBERTIAN)
-            hipLaunchKernelGGL((k_shade<MPT_BSDF_LAMBERTIAN>), dim3(blocks_for(n)), dim3(TB), 0, st, sa);
-        else
-            hipLaunchKernelGGL((k_shade<MPT_BSDF_NONE>), dim3(blocks_for(n)), dim3(TB), 0, st, sa);
+        {
+            TimedScope ts(cfg, st, KT_SHADE);
+            if (hf.options.bsdf_override == MPT_BSDF_LAMBERTIAN)
+                hipLaunchKernelGGL((k_shade<MPT_BSDF_LAMBERTIAN>), dim3(blocks_for(n)), dim3(TB), 0, st, sa);
+            else
+                hipLaunchKernelGGL((k_shade<MPT_BSDF_NONE>), dim3(blocks_for(n)), dim3(TB), 0, st, sa);
+        }
+        {
+            TimedScope ts(cfg, st, KT_COMPACT);
+            hipLaunchKernelGGL(k_compact, dim3((n + CP_NT * CP_ITEMS - 1) / (CP_NT * CP_ITEMS)), dim3(CP_NT), 0, st, P, q_cur,
+                               &P.counters[c_cur], q_next, &P.counters[c_next]);
+        }
         // NEE queries
         hipMemsetAsync(&P.counters[CTR_FETCH], 0, sizeof(int32_t), st);
         TraceArgs tn{};
@@ -1106,12 +1246,48 @@ hipError_t launch_frame(const DevScene& S, const DevPaths& P, const MptFrame* d_
         hipMemsetAsync(&P.counters[CTR_FETCH], 0, sizeof(int32_t), st);
         tn.count_ptr = &P.counters[CTR_CL];
         timed_trace<TM_NEE_CLOSEST>(tn, cfg, st);
-        hipLaunchKernelGGL(k_resolve, dim3(blocks_for(n)), dim3(TB), 0, st, S, P, d_frame, b, q_cur, &P.counters[c_cur]);
+        {
+            TimedScope ts(cfg, st, KT_RESOLVE);
+            hipLaunchKernelGGL(k_resolve, dim3(blocks_for(n)), dim3(TB), 0, st, S, P, d_frame, b, q_cur, &P.counters[c_cur]);
+        }
         // swap queues
         int32_t* tq = q_cur; q_cur = q_next; q_next = tq;
         int tc = c_cur; c_cur = c_next; c_next = tc;
     }
-    hipLaunchKernelGGL(k_accumulate, dim3(blocks_for(n)), dim3(TB), 0, st, P, d_frame);
+    {
+        TimedScope ts(cfg, st, KT_ACCUMULATE);
+        hipLaunchKernelGGL(k_accumulate, dim3(blocks_for(n)), dim3(TB), 0, st, P, d_frame);
+    }
+    return hipGetLastError();
+}
+
+// per-material resolution of the intersection-time material edits for untextured
+// materials (the texture-independent part of intersection_material)
+__global__ void k_resolve_materials(DevScene S, MptMaterial* out, int32_t* tex, int n) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const Mat& m = S.mats[i];
+    int textured = 0;
+    if (S.n_tex > 0) {
+        const int32_t* ti = &m.emission_texture_index;
+        for (int k = 0; k < 18; k++) textured |= ti[k] != MPT_NO_TEXTURE;
+    }
+    tex[i] = textured;
+    DevScene S0 = S;
+    S0.n_tex = 0;
+    out[i] = intersection_material(S0, i, mk2(0.0f, 0.0f), false);
+}
+
+#ifdef MPT_SECTION_TIMING
+extern "C" int mpt_debug_sections(unsigned long long* out, int reset) {
+    hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sect), sizeof(unsigned long long) * 8);
+    if (reset) { unsigned long long z[8] = {0}; hipMemcpyToSymbol(HIP_SYMBOL(g_sect), z, sizeof(z)); }
+    return 0;
+}
+#endif
+
+hipError_t launch_resolve_materials(const DevScene& S, MptMaterial* out_res, int32_t* out_tex, int n, hipStream_t st) {
+    hipLaunchKernelGGL(k_resolve_materials, dim3((n + 63) / 64), dim3(64), 0, st, S, out_res, out_tex, n);
     return hipGetLastError();
 }
 

@@ -45,9 +45,10 @@ def lib() -> C.CDLL:
     global _lib
     if _lib is not None:
         return _lib
-    if not os.path.exists(LIB_PATH):
-        raise ImportError(f"libmpt.so not found at {LIB_PATH}; run __graft_entry__.build() (no CPU fallback)")
-    L = C.CDLL(str(LIB_PATH))
+    path = os.environ.get("MPT_LIB_PATH", str(LIB_PATH))   # development variants
+    if not os.path.exists(path):
+        raise ImportError(f"libmpt.so not found at {path}; run __graft_entry__.build() (no CPU fallback)")
+    L = C.CDLL(path)
     vp, i32, f32 = C.c_void_p, C.c_int32, C.c_float
     L.mpt_last_error.restype = C.c_char_p
     L.mpt_abi_sizes.argtypes = [vp, C.c_int]

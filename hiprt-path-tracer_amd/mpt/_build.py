@@ -39,16 +39,19 @@ def up_to_date() -> bool:
     return all(p.stat().st_mtime <= t for p in _deps())
 
 
-def build(force: bool = False, verbose: bool = True) -> Path:
-    if not force and up_to_date():
+def build(force: bool = False, verbose: bool = True, defines=(), out: Path | None = None) -> Path:
+    """defines/out: development variants (e.g. -DMPT_SHADE_WAVES=2 into another path)."""
+    lib_path = Path(out) if out else LIB_PATH
+    if not force and not defines and out is None and up_to_date():
         return LIB_PATH
-    OBJ_DIR.mkdir(exist_ok=True)
+    obj_dir = OBJ_DIR if out is None else lib_path.parent / "obj"
+    obj_dir.mkdir(parents=True, exist_ok=True)
     procs = []
     objs = []
     for s in SOURCES:
-        obj = OBJ_DIR / (Path(s).stem + ".o")
+        obj = obj_dir / (Path(s).stem + ".o")
         objs.append(obj)
-        cmd = [HIPCC, *CXXFLAGS, "-c", str(CSRC / s), "-o", str(obj)]
+        cmd = [HIPCC, *CXXFLAGS, *defines, "-c", str(CSRC / s), "-o", str(obj)]
         if verbose:
             print("[mpt build]", " ".join(cmd), file=sys.stderr)
         procs.append((s, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))
@@ -59,15 +62,17 @@ def build(force: bool = False, verbose: bool = True) -> Path:
             errors.append(f"{s}:\n{out.decode(errors='replace')}")
     if errors:
         raise RuntimeError("libmpt build failed:\n" + "\n".join(errors))
-    tmp = LIB_PATH.with_suffix(".so.tmp")
+    tmp = lib_path.with_suffix(".so.tmp")
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp), *map(str, objs)]
     r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
     if r.returncode != 0:
         raise RuntimeError("libmpt link failed:\n" + r.stdout.decode(errors="replace"))
-    os.replace(tmp, LIB_PATH)
-    return LIB_PATH
+    os.replace(tmp, lib_path)
+    return lib_path
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv)
-    print(LIB_PATH)
+    args = sys.argv[1:]
+    defs = [a for a in args if a.startswith("-D")]
+    outs = [a[len("--out="):] for a in args if a.startswith("--out=")]
+    print(build(force="--force" in args, defines=defs, out=Path(outs[0]) if outs else None))

@@ -349,7 +349,9 @@ class Stats(C.Structure):
                 ("trace_ms", C.c_double), ("frame_ms", C.c_double),
                 ("stage_rays", C.c_uint64 * 3), ("stage_traversals", C.c_uint64 * 3), ("stage_nodes", C.c_uint64 * 3),
                 ("stage_tris", C.c_uint64 * 3), ("stage_ms", C.c_double * 3),
-                ("stage_launches", u32 * 3), ("reserved", u32)]
+                ("stage_launches", u32 * 3), ("shade_launches", u32), ("camera_ms", C.c_double),
+                ("shade_ms", C.c_double), ("resolve_ms", C.c_double), ("accumulate_ms", C.c_double),
+                ("compact_ms", C.c_double)]
 
 
 BSDF_NONE, BSDF_LAMBERTIAN = 0, 1

@@ -370,7 +370,13 @@ typedef struct MptStats {
     uint64_t stage_tris[3];
     double stage_ms[3];
     uint32_t stage_launches[3];
-    uint32_t reserved;
+    uint32_t shade_launches;
+    /* summed time of the other kernels (timing enabled) */
+    double camera_ms;
+    double shade_ms;
+    double resolve_ms;
+    double accumulate_ms;
+    double compact_ms;
 } MptStats;
 
 #define MPT_FB_COLOR 0        /* 'pixels': running SUM of samples (RenderData.h:34-36) */

@@ -372,11 +372,14 @@ f3 shading_normal_of(const Ctx& c, f3 gn, int p, f2 uv, f2 tc) {
 
 inline f3 tri_normal(const OScene& s, int p) { return normalize(cross(s.tris[p].e1, s.tris[p].e2)); }
 
+constexpr int MAX_BOUNDARY_SKIPS = 16;
+
 // trace_ray (Intersect.h:114-219), CPU branch
 bool trace_ray(Ctx& c, f3 o, f3 d, Payload& pl, HitInfo& out, int last_hit, Rng& rng) {
     const OScene& s = *c.s;
     Hit h;
     bool skipping;
+    int skips = 0;
     do {
         c.rays_closest++;
         h = closest(s, o, d, last_hit);
@@ -399,6 +402,10 @@ bool trace_ray(Ctx& c, f3 o, f3 d, Payload& pl, HitInfo& out, int last_hit, Rng&
             out.shading_normal += (2.0f * clampf(0.0f, 1.0f, -NoV)) * -d;
         }
         skipping = pl.vs.interior_stack.push(pl.vs.incident_mat_index, pl.vs.outgoing_mat_index, pl.vs.inside_material, mi, pl.material.dielectric_priority);
+        // Bounded: the reference loops until the boundary is not skipped, which never ends
+        // when a re-traced ray keeps re-hitting the triangle it sits on (the filter only
+        // excludes the ray's original last hit).  Same bound as the HIP path.
+        if (skipping && ++skips >= MAX_BOUNDARY_SKIPS) break;
         if (skipping) { o = out.inter_point; pl.vs.distance_in_volume += h.t; }
     } while (skipping);
     if (pl.material.dispersion_scale > 0.0f && pl.material.specular_transmission > 0.0f && pl.vs.sampled_wavelength == 0.0f)
