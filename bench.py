@@ -1,10 +1,14 @@
 """Benchmark of the MI355X path tracer (libmpt) -- one JSON line on rank 0.
 
-Workload (BASELINE.json configs[1], "C2"): the Cornell box glTF at 1920x1080, full
-layered Principled BSDF with NEE + MIS (LSS_MIS_LIGHT_BSDF), 3 bounces, reference
-defaults otherwise (adaptive sampling off).  One *step* = one sample
-per pixel over the frame (one mpt_render_frame); the default K = 64 steps is the
-config's 64 spp.  Multi-GPU: one process per GPU, the framebuffer is split into
+Workloads (BASELINE.json configs):
+* c3 (default; the configuration the metric is quoted on): the Bistro-exterior
+  stand-in -- a seeded procedural city of 2.84 M triangles (mpt/synthetic.py, seed
+  1234) under a seeded procedural HDR sky (2048x1024, alias-table sampling + BSDF MIS),
+  1920x1080, layered Principled BSDF, reference-default RIS light sampling; K = 256.
+* c2: the Cornell box glTF at 1920x1080, Principled + NEE/MIS (LSS_MIS_LIGHT_BSDF); K = 64.
+Both: 3 bounces, reference defaults otherwise (adaptive sampling and alpha testing off,
+see DESIGN.md).  One *step* = one sample per pixel over the frame (one
+mpt_render_frame); K steps = the config's spp.  Multi-GPU: one process per GPU, the framebuffer is split into
 interleaved 8-row bands (each rank renders every N-th band), and the per-rank sum
 buffers are gathered with RCCL (all_gather over xGMI) inside the timed region.
 
@@ -38,12 +42,14 @@ BAND_H = 8
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=64)
+    ap.add_argument("--workload", default="c3", choices=["c2", "c3"])
+    ap.add_argument("--steps", type=int, default=None, help="default: the workload's spp (c3 256, c2 64)")
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
-    ap.add_argument("--scene", default="cornell_pbr")
-    ap.add_argument("--strategy", default="mis", choices=["mis", "ris", "uniform", "bsdf"])
+    ap.add_argument("--scene", default=None, help="c2: a glTF of data/scenes (default cornell_pbr)")
+    ap.add_argument("--strategy", default=None, choices=["mis", "ris", "uniform", "bsdf"],
+                    help="default: c3 ris (reference default), c2 mis")
     ap.add_argument("--bounces", type=int, default=3)
     ap.add_argument("--bsdf", default="principled", choices=["principled", "lambert"])
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration")
@@ -55,25 +61,25 @@ LSS = {"mis": abi.LSS_MIS_LIGHT_BSDF, "ris": abi.LSS_RIS_BSDF_AND_LIGHT, "unifor
        "bsdf": abi.LSS_BSDF}
 
 
-def frames_for(cam, W, H, opt, band, n, first=0, bounces=3):
+def frames_for(cam, W, H, opt, band, n, first=0, bounces=3, world=None):
     out = []
     for s, seed in scene.cpu_seed_schedule(n):
         st = scene.parity_settings(bounces)
-        out.append(scene.make_frame(cam, W, H, options=opt, settings=st, sample_number=s + first, random_seed=seed,
-                                    band=band))
+        out.append(scene.make_frame(cam, W, H, options=opt, settings=st, world=world, sample_number=s + first,
+                                    random_seed=seed, band=band))
     return out
 
 
-def cpu_baseline(sd, luts, cam, W, H, opt, bounces, target_s):
+def cpu_baseline(sd, luts, cam, W, H, opt, bounces, target_s, env=None, world=None):
     """Oracle (CPU port) timed on a bounded sample of the same frame: a subset of the
     8-row bands at 1 spp, or the whole frame at several spp, sized to ~target_s."""
     sys.path.insert(0, ROOT)
     from oracle import oracle as orc
     cores = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
-    o = orc.Oracle(sd, luts)
+    o = orc.Oracle(sd, luts, envmap=env)
     bc = 64
     t0 = time.perf_counter()
-    o.render(frames_for(cam, W, H, opt, (BAND_H, 0, bc), 1, bounces=bounces), nthreads=cores)
+    o.render(frames_for(cam, W, H, opt, (BAND_H, 0, bc), 1, bounces=bounces, world=world), nthreads=cores)
     dt = max(time.perf_counter() - t0, 1e-3)
     scale = target_s / dt                       # multiples of the probe's work
     if scale >= bc:                             # whole frame, several spp
@@ -81,7 +87,7 @@ def cpu_baseline(sd, luts, cam, W, H, opt, bounces, target_s):
     else:
         bc2, spp = max(1, int(round(bc / scale))), 1
     t0 = time.perf_counter()
-    o.render(frames_for(cam, W, H, opt, (BAND_H, 0, bc2), spp, bounces=bounces), nthreads=cores)
+    o.render(frames_for(cam, W, H, opt, (BAND_H, 0, bc2), spp, bounces=bounces, world=world), nthreads=cores)
     dt = time.perf_counter() - t0
     rows = orc.mpt_rows(H, BAND_H, 0, bc2)
     rays = o.last_rays[0] + o.last_rays[1]
@@ -103,29 +109,45 @@ def main():
         import torch.distributed as dist
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    W, H, K = a.width, a.height, a.steps
-    sd = scene.load_scene(a.scene)
+    W, H = a.width, a.height
+    if a.workload == "c3":
+        from mpt import synthetic
+        sd = synthetic.procedural_city(1234)
+        env = mpt.build_envmap(scene.procedural_sky(2048, 1024, seed=7))
+        wset = scene.envmap_world(1.0)
+        strategy = a.strategy or "ris"
+        K = a.steps or 256
+        desc = "C3 stand-in: procedural city (2.84 M tris, seed 1234) + procedural HDR sky 2048x1024"
+    else:
+        sd = scene.load_scene(a.scene or "cornell_pbr")
+        env, wset = None, None
+        strategy = a.strategy or "mis"
+        K = a.steps or 64
+        desc = f"C2: {sd.name or a.scene or 'cornell_pbr'}"
     luts = scene.load_luts()
     cam = scene.make_camera(sd.camera_info, W, H)
     opt = abi.KernelOptions.default()
     opt.bsdf_override = abi.BSDF_NONE if a.bsdf == "principled" else abi.BSDF_LAMBERTIAN
-    opt.direct_light_sampling = LSS[a.strategy]
+    opt.direct_light_sampling = LSS[strategy]
+
     band = (BAND_H, rank, world)
 
     r = mpt.GPURenderer(local)
     r.set_scene(sd)
     r.set_luts(luts)
+    if env is not None:
+        r.set_envmap(env)
 
     # calibration: instrumented traversal -> nodes / triangles per query per stage
     r.enable_stats(timing=False, instrumented=True)
-    for f in frames_for(cam, W, H, opt, band, 2, first=0, bounces=a.bounces):
+    for f in frames_for(cam, W, H, opt, band, 2, first=0, bounces=a.bounces, world=wset):
         r.render(f)
     cal = r.stats()
     # warmup (untimed), then the timed K-frame accumulation restarting at sample 0
     r.enable_stats(timing=False, instrumented=False)
-    for f in frames_for(cam, W, H, opt, band, a.warmup, bounces=a.bounces):
+    for f in frames_for(cam, W, H, opt, band, a.warmup, bounces=a.bounces, world=wset):
         r.render(f)
-    frames = frames_for(cam, W, H, opt, band, K, bounces=a.bounces)
+    frames = frames_for(cam, W, H, opt, band, K, bounces=a.bounces, world=wset)
     r.synchronize_kernel()
     r.enable_stats(timing=True, instrumented=False)
 
@@ -196,7 +218,7 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         try:
-            cpu = cpu_baseline(sd, luts, cam, W, H, opt, a.bounces, a.cpu_seconds)
+            cpu = cpu_baseline(sd, luts, cam, W, H, opt, a.bounces, a.cpu_seconds, env=env, world=wset)
         except Exception as e:  # the baseline is reported, never the product path
             cpu = {"value": None, "unit": "Mray/s", "cores": 0, "kind": "port", "sample": f"failed: {e}"}
 
@@ -213,13 +235,15 @@ def main():
             "scaling": "strong",   # fixed frame split over the ranks
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (reference Cornell glTF, seeded CPU seed schedule)",
+            "data": ("synthetic (seeded procedural city + sky standing in for Bistro + its HDR, CPU seed schedule)"
+                     if a.workload == "c3" else "synthetic (reference Cornell glTF, seeded CPU seed schedule)"),
             "msample_per_s": round(W * H * K / elapsed / 1e6, 3),
             "rays_per_sample": round(rays_total / (W * H * K), 4),
-            "config": {"workload": f"C2: {a.scene} {W}x{H}, {K} spp, "
+            "config": {"workload": f"{desc}, {W}x{H}, {K} spp, "
                                    f"{'layered Principled' if a.bsdf == 'principled' else 'Lambert-override'} BSDF + NEE "
-                                   f"({a.strategy.upper()}), {a.bounces} bounces, 1 step = 1 spp",
-                       "scene": a.scene, "width": W, "height": H, "spp": K, "strategy": a.strategy,
+                                   f"({strategy.upper()}), {a.bounces} bounces, 1 step = 1 spp",
+                       "scene": sd.name, "triangles": int(sd.num_triangles), "width": W, "height": H, "spp": K,
+                       "strategy": strategy,
                        "partition": f"interleaved {BAND_H}-row bands over {world} rank(s), RCCL all_gather"},
             "roofline": roof(dom),
             "roofline_traversal": roof(max(lines[:3], key=lambda x: x["total_ms"])),

@@ -609,65 +609,113 @@ DEV void lobe_probas(const float w[7], float p[7]) {
     for (int i = 0; i < 7; i++) p[i] = w[i] * nf;
 }
 
-DEV Col principled_eval(const BCtx& c, const Mat& m, VState& vs, v3 view, v3 n, v3 L, float& pdf) {
-    pdf = 0.0f;
-    bool outside = dot(view, n) > 0 || m.thin_walled;
-    bool refracting = dot(n, L) < 0.0f && outside;
-    if (dot(view, n) < 0.0f) n = -n;
-    v3 T, B;
-    build_onb(n, T, B);
-    v3 lv = to_local(T, B, n, view), ll = to_local(T, B, n, L);
-    v3 lh = normalize(lv + ll);
-    v3 TR, BR;
-    build_rotated_onb(n, TR, BR, m.anisotropy_rotation * PI);
-    v3 lvr = to_local(TR, BR, n, view), llr = to_local(TR, BR, n, L);
-    v3 lhr = normalize(lvr + llr);
+// Principled BSDF evaluation (Principled.h:430-790), split into the part that depends
+// only on the path vertex (normal frame, view direction in both frames, lobe weights,
+// incident IOR, the view-side Fresnel / darkening terms and the LUT energy
+// compensation) and the part that depends on the light direction.  A vertex evaluates
+// the BSDF up to ~9 times (RIS candidates, MIS, envmap, continuation); the vertex part
+// is computed once.  Same operations in the same order as a monolithic evaluation, so
+// the results are bit-identical to it.
+struct PEval {
+    v3 n, T, B, lv, TR, BR, lvr;
+    bool outside;
     float w[7], p[7];
-    lobe_weights(m, outside, w);
-    float inc = ior_or_air(c, vs.incident);
-    lobe_probas(w, p);
+    float inc;
+    float coat_vdf, coat_oa;
+    Col coat_dark;
+    float rel;
+    bool spec_ok;
+    Col spec_tint, spec_vdf, spec_dark;
+    float gbc, ccc;
+};
+
+DEV void principled_eval_pre(const BCtx& c, const Mat& m, const VState& vs, v3 view, v3 sn, PEval& e) {
+    v3 n = sn;
+    e.outside = dot(view, n) > 0 || m.thin_walled;
+    if (dot(view, n) < 0.0f) n = -n;
+    e.n = n;
+    build_onb(n, e.T, e.B);
+    e.lv = to_local(e.T, e.B, n, view);
+    build_rotated_onb(n, e.TR, e.BR, m.anisotropy_rotation * PI);
+    e.lvr = to_local(e.TR, e.BR, n, view);
+    lobe_weights(m, e.outside, e.w);
+    e.inc = ior_or_air(c, vs.incident);
+    lobe_probas(e.w, e.p);
+    // coat, view side (entered when the coat has weight or the light refracts, which
+    // needs 'outside')
+    e.coat_vdf = 0.0f; e.coat_oa = 0.0f; e.coat_dark = col(1.0f);
+    if (e.w[0] > 0.0f || e.outside) {
+        e.coat_vdf = fresnel_dielectric(absr(e.lv.z), e.inc, m.coat_ior);
+        if (!is_white(C3(m.coat_medium_absorption)))
+            e.coat_oa = maxr(1.0e-6f, sqrtf(1.0f - (1.0f - e.lv.z * e.lv.z) / (m.coat_ior * m.coat_ior)));
+        e.coat_dark = coat_darkening(m, m.coat_ior / e.inc, e.coat_vdf);
+    }
+    // specular layer, view side
+    e.rel = 1.0f; e.spec_ok = false;
+    e.spec_tint = col(1.0f); e.spec_vdf = col(0.0f); e.spec_dark = col(1.0f);
+    if (e.w[4] > 0.0f) {
+        e.rel = spec_rel_ior(m, e.inc);
+        e.spec_ok = absr(e.rel - 1.0f) > 1.0e-3f;
+        if (e.spec_ok) {
+            e.spec_tint = lerpc(col(1.0f), m.specular_tint * C3(m.specular_color), m.specular);
+            e.spec_vdf = spec_fresnel(m, e.rel, e.lvr.z);
+            e.spec_dark = spec_darkening(m, e.rel);
+        }
+    }
+    e.gbc = glossy_base_comp(c, m, e.inc, e.lv.z);
+    e.ccc = c.clearcoat_comp ? clearcoat_comp(c, m, e.inc, e.lv.z) : 1.0f;
+}
+
+DEV Col principled_eval_post(const BCtx& c, const Mat& m, VState& vs, const PEval& e, v3 sn, v3 L, float& pdf) {
+    pdf = 0.0f;
+    const bool refracting = dot(sn, L) < 0.0f && e.outside;
+    const v3 n = e.n;
+    v3 ll = to_local(e.T, e.B, n, L);
+    v3 lh = normalize(e.lv + ll);
+    v3 llr = to_local(e.TR, e.BR, n, L);
+    v3 lhr = normalize(e.lvr + llr);
+    const v3 lv = e.lv, lvr = e.lvr;
+    const float inc = e.inc;
     Col thr = col(1.0f), fc = col(0.0f);
     float nr = refracting ? 0.0f : 1.0f;
     // coat (Principled.h:493-593)
-    if (w[0] > 0.0f || refracting) {
+    if (e.w[0] > 0.0f || refracting) {
         float cp = 0.0f;
         Col ct = col(0.0f);
         if (!refracting) {
             float HoL = clampr(1.0e-8f, 1.0f, dot(lh, ll));
             ct = ts_ggx1(c, m.coat_roughness, m.coat_anisotropy, col(fresnel_dielectric(HoL, inc, m.coat_ior)), lv, ll, lh, cp);
-            ct *= w[0];
+            ct *= e.w[0];
             ct *= thr;
         }
-        pdf += cp * p[0];
+        pdf += cp * e.p[0];
         Col att = col(1.0f);
         att *= 1.0f - fresnel_dielectric(absr(ll.z), inc, m.coat_ior);
-        float vdf = fresnel_dielectric(absr(lv.z), inc, m.coat_ior);
-        att *= 1.0f - vdf;
+        att *= 1.0f - e.coat_vdf;
         if (!is_white(C3(m.coat_medium_absorption))) {
             float ia = maxr(1.0e-6f, sqrtf(1.0f - (1.0f - ll.z * ll.z) / (m.coat_ior * m.coat_ior)));
-            float oa = maxr(1.0e-6f, sqrtf(1.0f - (1.0f - lv.z * lv.z) / (m.coat_ior * m.coat_ior)));
-            float tda = 1.0f / ia + 1.0f / oa;
+            float tda = 1.0f / ia + 1.0f / e.coat_oa;
             att *= cexp(-(col(1.0f) - cpow(csqrt(C3(m.coat_medium_absorption)), tda)) * m.coat_medium_thickness);
         }
-        att *= coat_darkening(m, m.coat_ior / inc, vdf);
+        att *= e.coat_dark;
         att = lerpc(col(1.0f), att, m.coat);
         thr *= att;
         fc += ct;
     }
     // sheen
-    if (w[1] > 0.0f) {
+    if (e.w[1] > 0.0f) {
         float refl, sp;
         Col ct = sheen_eval(c, m, ll, lv, sp, refl);
-        ct *= w[1];
+        ct *= e.w[1];
         ct *= thr;
-        pdf += sp * p[1];
+        pdf += sp * e.p[1];
         thr *= 1.0f - m.sheen * refl;
         fc += ct;
     }
     // metal x2
 #pragma unroll
     for (int k = 0; k < 2; k++) {
-        float wk = w[2 + k] * nr;
+        float wk = e.w[2 + k] * nr;
         if (wk > 0.0f) {
             float mp;
             float HoL = clampr(1.0e-8f, 1.0f, dot(lhr, llr));
@@ -676,55 +724,59 @@ DEV Col principled_eval(const BCtx& c, const Mat& m, VState& vs, v3 view, v3 n, 
             Col ct = ts_ggx1(c, k == 0 ? m.roughness : m.second_roughness, m.anisotropy, lerpc(Fm, Ft, m.thin_film), lvr, llr, lhr, mp);
             ct *= wk;
             ct *= thr;
-            pdf += mp * p[2 + k];
+            pdf += mp * e.p[2 + k];
             fc += ct;
         }
     }
     // glass
-    if (w[6] > 0.0f) {
+    if (e.w[6] > 0.0f) {
         float gp;
         Col ct = glass_eval(c, m, vs, lvr, llr, gp);
-        ct *= w[6];
+        ct *= e.w[6];
         ct *= thr;
-        pdf += gp * p[6];
+        pdf += gp * e.p[6];
         fc += ct;
     }
     // glossy base = specular + diffuse
     {
         Col g = col(0.0f);
-        float ws = w[4] * nr;
+        float ws = e.w[4] * nr;
         if (ws > 0.0f) {
-            float rel = spec_rel_ior(m, inc);
             float sp;
-            Col ct = ts_ggx0(c, m.roughness, m.anisotropy, spec_fresnel(m, rel, dot(llr, lhr)), lvr, llr, lhr, sp);
-            if (absr(rel - 1.0f) > 1.0e-3f) {
-                ct *= lerpc(col(1.0f), m.specular_tint * C3(m.specular_color), m.specular);
+            Col ct = ts_ggx0(c, m.roughness, m.anisotropy, spec_fresnel(m, e.rel, dot(llr, lhr)), lvr, llr, lhr, sp);
+            if (e.spec_ok) {
+                ct *= e.spec_tint;
                 ct *= ws;
                 ct *= thr;
                 Col att = col(1.0f);
-                att *= col(1.0f) - spec_fresnel(m, rel, llr.z);
-                Col vdf = spec_fresnel(m, rel, lvr.z);
-                att *= col(1.0f) - vdf;
-                att *= spec_darkening(m, rel);
+                att *= col(1.0f) - spec_fresnel(m, e.rel, llr.z);
+                att *= col(1.0f) - e.spec_vdf;
+                att *= e.spec_dark;
                 att = lerpc(col(1.0f), att, m.specular);
                 thr *= att;
             }
-            pdf += sp * p[4];
+            pdf += sp * e.p[4];
             g += ct;
         }
-        float wd = w[5] * nr;
+        float wd = e.w[5] * nr;
         if (wd > 0.0f) {
             float dp;
             Col ct = lambert_eval(m, ll.z, dp);
             ct *= wd;
             ct *= thr;
-            pdf += dp * p[5];
+            pdf += dp * e.p[5];
             g += ct;
         }
-        fc += g / glossy_base_comp(c, m, inc, lv.z);
+        fc += g / e.gbc;
     }
-    if (c.clearcoat_comp) fc /= clearcoat_comp(c, m, inc, lv.z);
+    if (c.clearcoat_comp) fc /= e.ccc;
     return fc;
+}
+
+DEV Col principled_eval(const BCtx& c, const Mat& m, VState& vs, v3 view, v3 n, v3 L, float& pdf) {
+    PEval e;
+    principled_eval_pre(c, m, vs, view, n, e);
+    return principled_eval_post(c, m, vs, e, n, L, pdf);
 }
 
 // Direction half of PrincipledBSDF sampling (Principled.h:1050-1120): picks a lobe, samples
@@ -781,6 +833,16 @@ template <int OVERRIDE>
 DEV Col bsdf_eval(const BCtx& c, const Mat& m, VState& vs, v3 view, v3 sn, v3 L, float& pdf) {
     if (OVERRIDE == MPT_BSDF_LAMBERTIAN) return lambert_eval(m, dot(L, sn), pdf);
     return principled_eval(c, m, vs, view, sn, L, pdf);
+}
+// evaluation split into a per-vertex part and a per-light-direction part (see PEval)
+template <int OVERRIDE>
+DEV void bsdf_eval_pre(const BCtx& c, const Mat& m, const VState& vs, v3 view, v3 sn, PEval& e) {
+    if (OVERRIDE != MPT_BSDF_LAMBERTIAN) principled_eval_pre(c, m, vs, view, sn, e);
+}
+template <int OVERRIDE>
+DEV Col bsdf_eval_post(const BCtx& c, const Mat& m, VState& vs, const PEval& e, v3 sn, v3 L, float& pdf) {
+    if (OVERRIDE == MPT_BSDF_LAMBERTIAN) return lambert_eval(m, dot(L, sn), pdf);
+    return principled_eval_post(c, m, vs, e, sn, L, pdf);
 }
 // sample = sample_dir + bsdf_eval on the updated state (eval skipped when sample_dir is false)
 template <int OVERRIDE>

@@ -670,6 +670,10 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MPT_SHADE_WA
             int triW = -1, ris_c = 0;
             bool hasW = false;
             const Col thr_vertex = thr;
+            PEval pe;                          // per-vertex half of every BSDF evaluation below
+            bsdf_eval_pre<OVR>(bc, m, vs, view, sn, pe);
+            Col fW = col(0.0f);                // BSDF value / pdf at the RIS light winner
+            float pdfW = 0.0f;
             // One BSDF evaluation site for every operation of the vertex: each iteration
             // prepares a direction (light / envmap sample, or a BSDF lobe sample), evaluates
             // the BSDF once, and consumes the result.  All lanes of a wave meet at the same
@@ -709,7 +713,9 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MPT_SHADE_WA
                     dist = length(sd);
                     L = sd / dist;
                     lp = ep2;
-                    do_eval = hasW;
+                    // outside the surface the winner's direction is bit-identical to its
+                    // candidate's (same origin), and so is the evaluation: reuse it
+                    do_eval = hasW && ism != 1.0f;
                 } else if (op == OP_MIS_LIGHT || op == OP_UNI_LIGHT) {
                     // sample_one_light_MIS (Lights.h:115-220) / _no_MIS (Lights.h:22-65)
                     lp = sample_emissive_triangle(S, rng, lpdf, li);
@@ -730,7 +736,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MPT_SHADE_WA
                 float pdf = 0.0f;
                 Col f = col(0.0f);
                 SECT(1);
-                if (do_eval) f = bsdf_eval<OVR>(bc, m, tv, view, sn, L, pdf);
+                if (do_eval) f = bsdf_eval_post<OVR>(bc, m, tv, pe, sn, L, pdf);
                 SECT(2);
                 int next = OP_DONE;
                 if (op == OP_RIS_LIGHT) {
@@ -745,7 +751,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MPT_SHADE_WA
                         cw = balance(lpdf, (float)nl, bp, (float)nbc) * target / lpdf;
                     }
                     wsum += cw;
-                    if (rng() < cw / wsum) { hasW = true; targetW = target; pointW = lp; triW = li.tri; }
+                    if (rng() < cw / wsum) { hasW = true; targetW = target; pointW = lp; triW = li.tri; fW = f; pdfW = pdf; }
                     ris_c++;
                     next = ris_c < nl ? OP_RIS_LIGHT : (nbc > 0 ? OP_RIS_BSDF : OP_RIS_WIN);
                 } else if (op == OP_RIS_BSDF) {
@@ -762,6 +768,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MPT_SHADE_WA
                     nr.r_add = rng();
                     next = OP_RIS_WIN;
                 } else if (op == OP_RIS_WIN) {
+                    if (!do_eval) { f = fW; pdf = pdfW; }
                     nr.ris_wsum = wsum;
                     if (hasW) {
                         fl |= NF_RIS_W;

@@ -1,0 +1,220 @@
+"""Seeded procedural stand-in for the Bistro exterior.
+
+The Bistro glTF is not in the container, so the C3/C4 workloads run on a procedural
+city of the same scale: a street grid of buildings whose facades are tessellated into
+recessed windows (18 triangles per window cell), roofs, sidewalks, street lamps (the
+emissive triangles NEE samples) and trees (smooth-shaded icospheres), ≈2.6 M triangles
+for the default seed.  Everything is generated with numpy from ``seed`` (default 1234),
+so the scene is identical on every machine without shipping a file.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+
+from . import abi
+from .scene import SceneData
+
+
+def _mat(base, rough=0.8, metallic=0.0, specular=0.5, emission=None, strength=1.0):
+    m = abi.Material.default()
+    m.base_color = abi.Color(*base)
+    m.roughness = rough
+    m.metallic = metallic
+    m.specular = specular
+    if emission is not None:
+        m.emission = abi.Color(*emission)
+        m.emission_strength = strength
+    m.make_safe()
+    m.precompute_properties()
+    return m
+
+
+class _Builder:
+    def __init__(self):
+        self.v, self.n, self.hn, self.idx, self.mi = [], [], [], [], []
+        self.nv = 0
+
+    def quads(self, p00, p10, p11, p01, mat):
+        """Batch of quads (arrays [K,3] of corners, counter-clockwise) -> 2 flat triangles each."""
+        k = len(p00)
+        if k == 0:
+            return
+        V = np.stack([p00, p10, p11, p01], 1).reshape(-1, 3)
+        base = self.nv + 4 * np.arange(k)[:, None]
+        I = np.concatenate([base + np.array([0, 1, 2]), base + np.array([0, 2, 3])], 1).reshape(-1, 3)
+        self.v.append(V)
+        self.n.append(np.zeros_like(V))
+        self.hn.append(np.zeros(len(V), np.uint8))
+        self.idx.append(I)
+        self.mi.append(np.broadcast_to(np.asarray(mat, np.int32), (k,)).repeat(2) if np.ndim(mat) == 0
+                       else np.repeat(np.asarray(mat, np.int32), 2))
+        self.nv += len(V)
+
+    def mesh(self, V, N, I, mat):
+        self.v.append(V)
+        self.n.append(N)
+        self.hn.append(np.ones(len(V), np.uint8))
+        self.idx.append(I + self.nv)
+        self.mi.append(np.full(len(I), mat, np.int32))
+        self.nv += len(V)
+
+
+def _icosphere(sub=2):
+    t = (1.0 + 5 ** 0.5) / 2.0
+    V = [(-1, t, 0), (1, t, 0), (-1, -t, 0), (1, -t, 0), (0, -1, t), (0, 1, t), (0, -1, -t), (0, 1, -t),
+         (t, 0, -1), (t, 0, 1), (-t, 0, -1), (-t, 0, 1)]
+    F = [(0, 11, 5), (0, 5, 1), (0, 1, 7), (0, 7, 10), (0, 10, 11), (1, 5, 9), (5, 11, 4), (11, 10, 2), (10, 7, 6),
+         (7, 1, 8), (3, 9, 4), (3, 4, 2), (3, 2, 6), (3, 6, 8), (3, 8, 9), (4, 9, 5), (2, 4, 11), (6, 2, 10), (8, 6, 7),
+         (9, 8, 1)]
+    V = [np.array(v, float) / np.linalg.norm(v) for v in V]
+    for _ in range(sub):
+        cache, F2 = {}, []
+
+        def mid(a, b):
+            key = (min(a, b), max(a, b))
+            if key not in cache:
+                m = V[a] + V[b]
+                V.append(m / np.linalg.norm(m))
+                cache[key] = len(V) - 1
+            return cache[key]
+        for a, b, c in F:
+            ab, bc, ca = mid(a, b), mid(b, c), mid(c, a)
+            F2 += [(a, ab, ca), (b, bc, ab), (c, ca, bc), (ab, bc, ca)]
+        F = F2
+    return np.array(V), np.array(F, np.int64)
+
+
+def procedural_city(seed: int = 1234, blocks: int = 17) -> SceneData:
+    rng = np.random.default_rng(seed)
+    B = _Builder()
+    mats = [
+        _mat((0.08, 0.08, 0.085), rough=0.9, specular=0.3),            # 0 asphalt
+        _mat((0.45, 0.44, 0.42), rough=0.85, specular=0.4),            # 1 sidewalk
+        _mat((0.62, 0.55, 0.45), rough=0.8),                           # 2 wall beige
+        _mat((0.55, 0.25, 0.2), rough=0.8),                            # 3 wall brick
+        _mat((0.7, 0.7, 0.72), rough=0.7),                             # 4 wall white
+        _mat((0.3, 0.35, 0.4), rough=0.6),                             # 5 wall slate
+        _mat((0.05, 0.07, 0.08), rough=0.05, specular=1.0),            # 6 window glass (glossy dark)
+        _mat((0.2, 0.2, 0.22), rough=0.9),                             # 7 roof
+        _mat((0.12, 0.3, 0.08), rough=0.95, specular=0.2),             # 8 foliage
+        _mat((0.8, 0.8, 0.82), rough=0.3, metallic=1.0),               # 9 lamp metal
+        _mat((1.0, 0.9, 0.7), emission=(1.0, 0.85, 0.6), strength=40.0),  # 10 lamp light
+    ]
+    blk, street = 40.0, 12.0
+    pitch = blk + street
+    half = blocks * pitch / 2.0
+    # ground: asphalt streets as one big quad grid (coarse) + raised sidewalks per block
+    g = np.linspace(-half, half, 33)
+    gx, gz = np.meshgrid(g[:-1], g[:-1], indexing="ij")
+    gx, gz = gx.ravel(), gz.ravel()
+    d = g[1] - g[0]
+    z0 = np.zeros_like(gx)
+    B.quads(np.stack([gx, z0, gz], 1), np.stack([gx, z0, gz + d], 1), np.stack([gx + d, z0, gz + d], 1),
+            np.stack([gx + d, z0, gz], 1), 0)
+    bx, bz = np.meshgrid(np.arange(blocks), np.arange(blocks), indexing="ij")
+    bx = -half + street / 2 + bx.ravel() * pitch
+    bz = -half + street / 2 + bz.ravel() * pitch
+    h0 = np.full_like(bx, 0.15)
+    # sidewalk tops
+    B.quads(np.stack([bx, h0, bz], 1), np.stack([bx, h0, bz + blk], 1), np.stack([bx + blk, h0, bz + blk], 1),
+            np.stack([bx + blk, h0, bz], 1), 1)
+    # buildings: 2x2 per block with jittered footprints
+    lots = []
+    for i in range(2):
+        for j in range(2):
+            w = rng.uniform(12.0, 17.0, len(bx))
+            dd = rng.uniform(12.0, 17.0, len(bx))
+            x0 = bx + 2.0 + i * 19.0 + rng.uniform(0.0, 17.0 - w + 0.01)
+            zz0 = bz + 2.0 + j * 19.0 + rng.uniform(0.0, 17.0 - dd + 0.01)
+            h = np.clip(rng.lognormal(math.log(22.0), 0.45, len(bx)), 9.0, 90.0)
+            lots.append(np.stack([x0, zz0, w, dd, h], 1))
+    lots = np.concatenate(lots, 0)
+    wall_mat = rng.integers(2, 6, len(lots))
+    # roofs
+    x0, zz, w, dd, h = lots.T
+    B.quads(np.stack([x0, h, zz], 1), np.stack([x0, h, zz + dd], 1), np.stack([x0 + w, h, zz + dd], 1),
+            np.stack([x0 + w, h, zz], 1), wall_mat * 0 + 7)
+    # facades: (origin, right, normal) per side; cells of ~3.2 m x 3.5 m with a recessed window
+    for side in range(4):
+        if side == 0:   # -z facade, right = +x
+            O = np.stack([x0, np.zeros_like(x0), zz], 1); R = np.array([1.0, 0, 0]); N = np.array([0, 0, -1.0]); L = w
+        elif side == 1:  # +x facade, right = +z
+            O = np.stack([x0 + w, np.zeros_like(x0), zz], 1); R = np.array([0, 0, 1.0]); N = np.array([1.0, 0, 0]); L = dd
+        elif side == 2:  # +z facade, right = -x
+            O = np.stack([x0 + w, np.zeros_like(x0), zz + dd], 1); R = np.array([-1.0, 0, 0]); N = np.array([0, 0, 1.0]); L = w
+        else:            # -x facade, right = -z
+            O = np.stack([x0, np.zeros_like(x0), zz + dd], 1); R = np.array([0, 0, -1.0]); N = np.array([-1.0, 0, 0]); L = dd
+        cols = np.maximum(1, np.round(L / 3.2)).astype(int)
+        floors = np.maximum(1, np.round(h / 3.5)).astype(int)
+        cw, ch = L / cols, h / floors
+        ncell = cols * floors
+        bi = np.repeat(np.arange(len(lots)), ncell)
+        # cell (c, f) indices per building
+        starts = np.concatenate([[0], np.cumsum(ncell)[:-1]])
+        k = np.arange(ncell.sum()) - np.repeat(starts, ncell)
+        c = k % cols[bi]
+        f = k // cols[bi]
+        U = np.array([0.0, 1.0, 0.0])
+        o = O[bi] + (c * cw[bi])[:, None] * R + (f * ch[bi])[:, None] * U
+        cwv, chv = cw[bi][:, None], ch[bi][:, None]
+        mx, my = 0.22 * cwv, 0.25 * chv                      # wall margins around the window
+        depth = rng.uniform(0.15, 0.4, len(bi))[:, None]
+        Ru, Uu = R[None, :], U[None, :]
+
+        def P(a, b, dep=0.0):
+            return o + a * Ru + b * Uu - dep * N[None, :]
+        wm = wall_mat[bi]
+        # wall strips: bottom, top, left, right (outward facing => counter-clockwise seen from N)
+        B.quads(P(0, 0), P(cwv, 0), P(cwv, my), P(0, my), wm)
+        B.quads(P(0, chv - my), P(cwv, chv - my), P(cwv, chv), P(0, chv), wm)
+        B.quads(P(0, my), P(mx, my), P(mx, chv - my), P(0, chv - my), wm)
+        B.quads(P(cwv - mx, my), P(cwv, my), P(cwv, chv - my), P(cwv - mx, chv - my), wm)
+        # reveals (window recess sides)
+        B.quads(P(mx, my), P(mx, my, depth), P(cwv - mx, my, depth), P(cwv - mx, my), wm)
+        B.quads(P(mx, chv - my), P(cwv - mx, chv - my), P(cwv - mx, chv - my, depth), P(mx, chv - my, depth), wm)
+        B.quads(P(mx, my), P(mx, chv - my), P(mx, chv - my, depth), P(mx, my, depth), wm)
+        B.quads(P(cwv - mx, my), P(cwv - mx, my, depth), P(cwv - mx, chv - my, depth), P(cwv - mx, chv - my), wm)
+        # glass
+        B.quads(P(mx, my, depth), P(cwv - mx, my, depth), P(cwv - mx, chv - my, depth), P(mx, chv - my, depth), 6)
+    # street lamps along the streets: post (thin box, 4 quads) + emissive panel facing down
+    lx = np.concatenate([bx + 5.0, bx + 25.0, bx - 1.5, bx - 1.5])
+    lz = np.concatenate([bz - 1.5, bz - 1.5, bz + 5.0, bz + 25.0])
+    keep = rng.random(len(lx)) < 0.6
+    lx, lz = lx[keep], lz[keep]
+    t = 0.08
+    for (ax, az, bxo, bzo) in [(-t, -t, t, -t), (t, -t, t, t), (t, t, -t, t), (-t, t, -t, -t)]:
+        y0 = np.zeros_like(lx)
+        y1 = np.full_like(lx, 5.0)
+        B.quads(np.stack([lx + ax, y0, lz + az], 1), np.stack([lx + bxo, y0, lz + bzo], 1),
+                np.stack([lx + bxo, y1, lz + bzo], 1), np.stack([lx + ax, y1, lz + az], 1), 9)
+    s = 0.35
+    y = np.full_like(lx, 4.95)
+    B.quads(np.stack([lx - s, y, lz - s], 1), np.stack([lx + s, y, lz - s], 1), np.stack([lx + s, y, lz + s], 1),
+            np.stack([lx - s, y, lz + s], 1), 10)
+    # trees: smooth icospheres on the sidewalks
+    SV, SF = _icosphere(2)
+    tx = np.concatenate([bx + rng.uniform(1, 39, len(bx)), bx + rng.uniform(1, 39, len(bx))])
+    tz = np.concatenate([bz + 0.8 + 0 * bx, bz + 39.2 + 0 * bx])
+    tr = rng.uniform(1.2, 2.2, len(tx))
+    ctr = np.stack([tx, 3.0 + tr, tz], 1)
+    V = (SV[None, :, :] * tr[:, None, None] + ctr[:, None, :]).reshape(-1, 3)
+    Nn = np.broadcast_to(SV[None], (len(tx),) + SV.shape).reshape(-1, 3)
+    F = (SF[None, :, :] + (len(SV) * np.arange(len(tx)))[:, None, None]).reshape(-1, 3)
+    B.mesh(V, Nn.copy(), F, 8)
+    sd = SceneData()
+    sd.vertices = np.concatenate(B.v).astype(np.float32)
+    sd.normals = np.concatenate(B.n).astype(np.float32)
+    sd.has_normals = np.concatenate(B.hn).astype(np.uint8)
+    sd.texcoords = np.zeros((len(sd.vertices), 2), np.float32)
+    sd.triangle_indices = np.concatenate(B.idx).astype(np.int32).ravel()
+    sd.material_indices = np.concatenate(B.mi).astype(np.int32)
+    sd.materials = mats
+    sd.textures = []
+    sd.name = f"procedural_city_{seed}"
+    # street-level camera at an intersection looking down a street, slightly up
+    cx = -half + street / 2 + (blocks // 2) * pitch - street / 2
+    sd.camera_info = dict(position=np.array([cx, 1.7, half - 8.0]), lookat=np.array([cx + 0.8, 4.0, half - 60.0]),
+                          up=np.array([0.0, 1.0, 0.0]), hfov=1.0, aspect=16 / 9, znear=0.1, zfar=1000.0)
+    return sd.finalize()
