@@ -95,6 +95,13 @@ struct Builder {
     }
 };
 
+inline float scene_box_pad(const float* vertices, int num_triangles, const int32_t* indices) {
+    float m = 0.0f;
+    for (size_t k = 0; k < 3 * (size_t)num_triangles; k++)
+        for (int i = 0; i < 3; i++) m = std::max(m, std::fabs(vertices[3 * (size_t)indices[k] + i]));
+    return std::ldexp(std::max(m, 1.0f), -20);
+}
+
 inline uint8_t quant_exp(float ext) {
     // smallest e with 255 * 2^e >= ext, clamped to normal floats
     int e = -126;
@@ -126,6 +133,14 @@ void build_bvh8(const float* vertices, const int32_t* indices, int32_t num_trian
         for (int i = 0; i < 3; i++) b.cen[3 * (size_t)t + i] = 0.5f * (b.tbox[t].lo[i] + b.tbox[t].hi[i]);
         b.order[t] = t;
     }
+    // Pad every triangle box by 2^-20 of the scene's largest coordinate magnitude.  The
+    // Moller-Trumbore test accepts hits a rounding error outside the exact triangle (a
+    // ray grazing along a wall that holds an edge of the triangle), so unpadded boxes can
+    // cull a triangle the test would accept.  With the pad, box culling never changes a
+    // result: traversal equals brute force (the oracle pads its boxes the same way).
+    const float pad = scene_box_pad(vertices, num_triangles, indices);
+    for (int t = 0; t < num_triangles; t++)
+        for (int i = 0; i < 3; i++) { b.tbox[t].lo[i] -= pad; b.tbox[t].hi[i] += pad; }
     b.nodes.reserve(2 * (size_t)num_triangles);
     int root = b.build2(0, num_triangles, 0);
 

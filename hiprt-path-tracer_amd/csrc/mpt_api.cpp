@@ -76,6 +76,7 @@ struct MptContext {
     DBuf<MptMaterial> mats;
     DBuf<MptMaterial> mats_res;   // untextured intersection-time resolution per material
     DBuf<int32_t> mat_tex;
+    DBuf<float4> em_tab;
     bool any_tex = false;
     std::vector<MptMaterial> h_mats;
     int n_tex = 0;
@@ -140,6 +141,7 @@ DevScene dev_scene(MptContext* c) {
     S.mat_tex = c->mat_tex.p;
     S.mat_prio = c->mat_prio.p;
     S.emissive = c->emissive.p;
+    S.em_tab = c->em_tab.p;
     S.n_emissive = (int32_t)c->emissive.n;
     S.n_tris = (int32_t)c->mat_idx.n;
     S.tex = c->tex.p;
@@ -226,7 +228,8 @@ int resolve_materials(MptContext* c) {
     size_t n = c->h_mats.size();
     HIPCHK(c->mats_res.alloc(n));
     HIPCHK(c->mat_tex.alloc(n));
-    HIPCHK(launch_resolve_materials(dev_scene(c), c->mats_res.p, c->mat_tex.p, (int)n, c->stream));
+    HIPCHK(c->em_tab.alloc(5 * std::max<size_t>(c->emissive.n, 1)));
+    HIPCHK(launch_resolve_materials(dev_scene(c), c->mats_res.p, c->mat_tex.p, (int)n, c->em_tab.p, c->stream));
     std::vector<int32_t> t(n);
     HIPCHK(hipMemcpyAsync(t.data(), c->mat_tex.p, n * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
@@ -346,7 +349,7 @@ int mpt_destroy(MptContext* c) {
     c->nodes.release(); c->tris.release(); c->idx.release(); c->mat_idx.release(); c->mat_prio.release();
     c->emissive.release(); c->tex_dims.release(); c->pos.release(); c->nrm.release(); c->uv.release();
     c->has_n.release(); c->tex.release(); c->tex_off.release(); c->mats.release();
-    c->mats_res.release(); c->mat_tex.release(); c->mat_slot.release();
+    c->mats_res.release(); c->mat_tex.release(); c->mat_slot.release(); c->em_tab.release();
     c->lut_conductor.release(); c->lut_glossy.release(); c->lut_glass.release(); c->lut_glass_inv.release();
     c->lut_thin.release(); c->lut_sheen.release(); c->env.release(); c->alias_p.release(); c->alias_i.release();
     c->ray_o.release(); c->ray_d.release(); c->hit.release(); c->thr.release(); c->col.release(); c->alb.release();

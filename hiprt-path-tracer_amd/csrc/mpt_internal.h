@@ -31,6 +31,7 @@ struct DevScene {
     const int32_t* mat_tex;       // per material: 1 if any texture feeds the resolved material
     const int32_t* mat_prio;     // dielectric_priority per material (nested-dielectric push)
     const int32_t* emissive;
+    const float4* em_tab;         // 5 float4 per emissive triangle (k_emissive_table)
     int32_t n_emissive;
     int32_t n_tris;
     const uint8_t* tex;          // all textures, RGBA8, concatenated
@@ -135,7 +136,8 @@ struct LaunchCfg {
 
 hipError_t launch_frame(const DevScene& S, const DevPaths& P, const MptFrame* d_frame, const MptFrame& h_frame,
                         LaunchCfg& cfg, hipStream_t st);
-hipError_t launch_resolve_materials(const DevScene& S, MptMaterial* out_res, int32_t* out_tex, int n, hipStream_t st);
+hipError_t launch_resolve_materials(const DevScene& S, MptMaterial* out_res, int32_t* out_tex, int n, float4* em_tab,
+                                   hipStream_t st);
 hipError_t launch_trace_raw(const DevScene& S, const float4* o, const float4* d, int n, bool any, float4* out_hit,
                             uint8_t* out_occ, int32_t* fetch_ctr, uint32_t* spill, int grid, hipStream_t st);
 

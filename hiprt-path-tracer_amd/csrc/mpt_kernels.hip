@@ -437,24 +437,45 @@ __global__ __launch_bounds__(TB) void k_camera(DevPaths P, const MptFrame* __res
 // light sampling helpers (LightUtils.h)
 // ----------------------------------------------------------------------------------
 struct LightInfo { int tri; v3 normal; float area; Col emission; };
-DEV v3 sample_emissive_triangle(const DevScene& S, Rng& rng, float& pdf, LightInfo& li) {
-    int ri = rng.random_index(S.n_emissive);
-    int t = S.emissive[ri];
+// Emissive-triangle table (built once per scene / material update by k_emissive_table):
+// per light 5 float4 {A, prim}, {B - A, area}, {C - A, |cross|}, {normal, valid}, {emission}
+// -- the values uniform_sample_one_emissive_triangle (LightUtils.h:15-58) derives from
+// the triangle's vertices and material, computed with the same operations, so a sample
+// costs one dependent 80-byte load instead of a chain of index / vertex / material loads.
+__global__ void k_emissive_table(DevScene S, float4* tab) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= S.n_emissive) return;
+    int t = S.emissive[i];
     int3 ti = tri_idx(S, t);
     v3 A = ld3(S.pos, ti.x), B = ld3(S.pos, ti.y), C = ld3(S.pos, ti.z);
+    v3 AB = B - A, AC = C - A;
+    v3 n = cross(AB, AC);
+    float ln = length(n);
+    bool ok = !(ln <= 1.0e-6f);
+    v3 nn = ok ? n / ln : mk3(0.0f, 1.0f, 0.0f);
+    Col e = emission_of(S.mats[S.mat_idx[t]]);
+    tab[5 * i + 0] = make_float4(A.x, A.y, A.z, __int_as_float(t));
+    tab[5 * i + 1] = make_float4(AB.x, AB.y, AB.z, ln * 0.5f);
+    tab[5 * i + 2] = make_float4(AC.x, AC.y, AC.z, ln);
+    tab[5 * i + 3] = make_float4(nn.x, nn.y, nn.z, ok ? 1.0f : 0.0f);
+    tab[5 * i + 4] = make_float4(e.r, e.g, e.b, 0.0f);
+}
+
+DEV v3 sample_emissive_triangle(const DevScene& S, Rng& rng, float& pdf, LightInfo& li) {
+    int ri = rng.random_index(S.n_emissive);
+    const float4* e = S.em_tab + 5 * (size_t)ri;
+    float4 e0 = e[0], e1 = e[1], e2 = e[2], e3 = e[3], e4 = e[4];
     float r1 = rng(), r2 = rng();
     float sr1 = sqrtf(r1);
     float u = 1.0f - sr1, v = (1.0f - r2) * sr1;
-    v3 AB = B - A, AC = C - A;
+    v3 A = mk3(e0.x, e0.y, e0.z), AB = mk3(e1.x, e1.y, e1.z), AC = mk3(e2.x, e2.y, e2.z);
     v3 pt = A + AB * u + AC * v;
-    v3 n = cross(AB, AC);
-    float ln = length(n);
     li.tri = -1; li.normal = mk3(0.0f, 1.0f, 0.0f); li.area = 1.0f; li.emission = col(0.0f);
-    if (ln <= 1.0e-6f) { pdf = 0.0f; return mk3(0.0f, 0.0f, 0.0f); }
-    li.tri = t;
-    li.normal = n / ln;
-    li.area = ln * 0.5f;
-    li.emission = emission_of(S.mats[S.mat_idx[t]]);
+    if (e3.w == 0.0f) { pdf = 0.0f; return mk3(0.0f, 0.0f, 0.0f); }
+    li.tri = __float_as_int(e0.w);
+    li.normal = mk3(e3.x, e3.y, e3.z);
+    li.area = e1.w;
+    li.emission = col(e4.x, e4.y, e4.z);
     pdf = 1.0f / li.area;
     pdf /= (float)S.n_emissive;
     return pt;
@@ -526,9 +547,9 @@ DEV v3 load3v(const float* p) { return mk3(p[0], p[1], p[2]); }
 // lanes into g_sect; read with mpt_debug_sections.
 #ifdef MPT_SECTION_TIMING
 __device__ unsigned long long g_sect[8];
-#define SECT_BEGIN() uint64_t sect_[5] = {0, 0, 0, 0, 0}; uint64_t tprev_ = __builtin_amdgcn_s_memtime()
+#define SECT_BEGIN() uint64_t sect_[6] = {0, 0, 0, 0, 0, 0}; uint64_t tprev_ = __builtin_amdgcn_s_memtime()
 #define SECT(k) do { uint64_t now_ = __builtin_amdgcn_s_memtime(); sect_[k] += now_ - tprev_; tprev_ = now_; } while (0)
-#define SECT_END() do { for (int k_ = 0; k_ < 5; k_++) atomicAdd(&g_sect[k_], (unsigned long long)sect_[k_]); } while (0)
+#define SECT_END() do { if (sect_[1]) for (int k_ = 0; k_ < 6; k_++) atomicAdd(&g_sect[k_], (unsigned long long)sect_[k_]); atomicAdd(&g_sect[7], 1ull); } while (0)
 #else
 #define SECT_BEGIN() do {} while (0)
 #define SECT(k) do {} while (0)
@@ -671,14 +692,15 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MPT_SHADE_WA
             bool hasW = false;
             const Col thr_vertex = thr;
             PEval pe;                          // per-vertex half of every BSDF evaluation below
+            SECT(0);
             bsdf_eval_pre<OVR>(bc, m, vs, view, sn, pe);
+            SECT(5);
             Col fW = col(0.0f);                // BSDF value / pdf at the RIS light winner
             float pdfW = 0.0f;
             // One BSDF evaluation site for every operation of the vertex: each iteration
             // prepares a direction (light / envmap sample, or a BSDF lobe sample), evaluates
             // the BSDF once, and consumes the result.  All lanes of a wave meet at the same
             // evaluation whatever operation they are on.
-            SECT(0);
             while (op != OP_DONE) {
                 VState tv = vs;
                 v3 L = mk3(0.0f, 0.0f, 0.0f);
@@ -732,6 +754,9 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MPT_SHADE_WA
                     ec = env_sample(S, F, L, lpdf, rng);
                     geo = dot(sn, L);
                     do_eval = lpdf > 0.0f && geo > 0.0f;
+#ifdef MPT_DEBUG_SLOT
+                    if (slot == MPT_DEBUG_SLOT) printf("GPU env ec %a %a %a pdf %a dir %a %a %a cos %a ip %a %a %a prim %d\n", ec.r, ec.g, ec.b, lpdf, L.x, L.y, L.z, geo, ip.x, ip.y, ip.z, prim);
+#endif
                 }
                 float pdf = 0.0f;
                 Col f = col(0.0f);
@@ -829,6 +854,9 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MPT_SHADE_WA
                     if (do_eval) {
                         float mw = F.options.envmap_bsdf_mis ? balance(lpdf, pdf) : 1.0f;
                         store3(nr.e1, f * geo * mw * ec / lpdf);
+#ifdef MPT_DEBUG_SLOT
+                        if (slot == MPT_DEBUG_SLOT) { Col e1_ = f * geo * mw * ec / lpdf; printf("GPU env f %a %a %a bp %a mw %a e1 %a %a %a\n", f.r, f.g, f.b, pdf, mw, e1_.r, e1_.g, e1_.b); }
+#endif
                         if (env_use) {
                             fl |= NF_E1;
                             stage_query(P, slot, 1, qm, ip, prim, L, 1.0e35f - 1.0e-4f);
@@ -906,6 +934,9 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MPT_SHADE_WA
             }
             sky = clamp_contrib(sky, rs.envmap_contribution_clamp, true);
             rcol += clamp_contrib(sky * thr, rs.indirect_contribution_clamp, bounce > 0);
+#ifdef MPT_DEBUG_SLOT
+            if (slot == MPT_DEBUG_SLOT) printf("GPU b%d miss sky %a %a %a rc %a %a %a\n", bounce, sky.r, sky.g, sky.b, rcol.r, rcol.g, rcol.b);
+#endif
         }
         nr.flags = fl;
         P.qmask[slot] = (uint8_t)(qm | (cont ? QM_CONT : 0u));
@@ -1124,6 +1155,9 @@ __global__ __launch_bounds__(TB) void k_resolve(DevScene S, DevPaths P, const Mp
         Col e2 = col(0.0f), e1 = col(0.0f);
         if ((fl & NF_E2) && !occ[2]) e2 = load3c(nr.e2);
         if ((fl & NF_E1) && !occ[1]) e1 = load3c(nr.e1);
+#ifdef MPT_DEBUG_SLOT
+        if (slot == MPT_DEBUG_SLOT) printf("GPU resolve fl %x occ %d %d %d\n", fl, occ[0], occ[1], occ[2]);
+#endif
         ed = e2 + e1;
     }
     ld = clamp_contrib(ld, rs.direct_contribution_clamp, bounce == 0);
@@ -1132,6 +1166,9 @@ __global__ __launch_bounds__(TB) void k_resolve(DevScene S, DevPaths P, const Mp
     float4 cv = P.col[slot];
     Col rc = col(cv.x, cv.y, cv.z) + clamp_contrib(ind, rs.indirect_contribution_clamp, bounce > 0);
     P.col[slot] = make_float4(rc.r, rc.g, rc.b, 0.0f);
+#ifdef MPT_DEBUG_SLOT
+    if (slot == MPT_DEBUG_SLOT) { Col t_ = load3c(nr.thr); printf("GPU b%d ld %a %a %a ed %a %a %a thr %a %a %a rc %a %a %a\n", bounce, ld.r, ld.g, ld.b, ed.r, ed.g, ed.b, t_.r, t_.g, t_.b, rc.r, rc.g, rc.b); }
+#endif
 }
 
 // ----------------------------------------------------------------------------------
@@ -1293,8 +1330,40 @@ extern "C" int mpt_debug_sections(unsigned long long* out, int reset) {
 }
 #endif
 
-hipError_t launch_resolve_materials(const DevScene& S, MptMaterial* out_res, int32_t* out_tex, int n, hipStream_t st) {
+// Development check of the transcendental layer (fn: 0 sin 1 cos 2 exp 3 log 4 pow
+// 5 atan2 6 asin 7 acos); host pointers, synchronous.
+__global__ void k_debug_math(int fn, const float* a, const float* b, float* out, int n) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    float x = a[i], y = b[i], r = 0.0f;
+    switch (fn) {
+        case 0: r = psin(x); break;
+        case 1: r = pcos(x); break;
+        case 2: r = pexp(x); break;
+        case 3: r = plog(x); break;
+        case 4: r = ppow(x, y); break;
+        case 5: r = patan2(x, y); break;
+        case 6: r = pasin(x); break;
+        default: r = pacos(x); break;
+    }
+    out[i] = r;
+}
+extern "C" int mpt_debug_math(int fn, const float* a, const float* b, float* out, int n) {
+    float *da, *db, *dout;
+    hipMalloc(&da, n * 4); hipMalloc(&db, n * 4); hipMalloc(&dout, n * 4);
+    hipMemcpy(da, a, n * 4, hipMemcpyHostToDevice);
+    hipMemcpy(db, b, n * 4, hipMemcpyHostToDevice);
+    hipLaunchKernelGGL(k_debug_math, dim3((n + 255) / 256), dim3(256), 0, 0, fn, da, db, dout, n);
+    hipMemcpy(out, dout, n * 4, hipMemcpyDeviceToHost);
+    hipFree(da); hipFree(db); hipFree(dout);
+    return 0;
+}
+
+hipError_t launch_resolve_materials(const DevScene& S, MptMaterial* out_res, int32_t* out_tex, int n, float4* em_tab,
+                                   hipStream_t st) {
     hipLaunchKernelGGL(k_resolve_materials, dim3((n + 63) / 64), dim3(64), 0, st, S, out_res, out_tex, n);
+    if (S.n_emissive > 0)
+        hipLaunchKernelGGL(k_emissive_table, dim3((S.n_emissive + 63) / 64), dim3(64), 0, st, S, em_tab);
     return hipGetLastError();
 }
 

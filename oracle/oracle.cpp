@@ -95,6 +95,15 @@ void build_bvh(OScene& s) {
         for (int k = 0; k < 3; k++) { f3 p = s.pos[s.idx[3 * t + k]]; float q[3] = {p.x, p.y, p.z}; tb[t].grow(q); }
         for (int i = 0; i < 3; i++) cen[3 * t + i] = 0.5f * (tb[t].lo[i] + tb[t].hi[i]);
     }
+    // Conservative boxes: pad by 2^-20 of the largest coordinate magnitude, so box culling
+    // never rejects a triangle that Moller-Trumbore accepts (grazing rays along a wall that
+    // holds a triangle edge).  Traversal = brute force; libmpt's builder pads the same way.
+    float m = 1.0f;
+    for (int t = 0; t < n; t++)
+        for (int k = 0; k < 3; k++) { f3 p = s.pos[s.idx[3 * t + k]]; m = std::max({m, std::fabs(p.x), std::fabs(p.y), std::fabs(p.z)}); }
+    const float pad = std::ldexp(m, -20);
+    for (int t = 0; t < n; t++)
+        for (int i = 0; i < 3; i++) { tb[t].lo[i] -= pad; tb[t].hi[i] += pad; }
     s.order.resize(n);
     for (int i = 0; i < n; i++) s.order[i] = i;
     s.nodes.clear();
@@ -264,6 +273,7 @@ struct Payload {
 };
 struct ShadowLightHit { int prim = 0; float dist = 0; f3 shading_normal{0, 0, 0}; Col emission; };
 
+static thread_local int g_dbg = 0;
 struct Ctx {
     const OScene* s;
     const MptFrame* f;
@@ -800,6 +810,7 @@ Col sample_environment_map(Ctx& c, const Payload& pl, const HitInfo& hi, f3 view
     Col ec = envmap_sample(c, sdir, epdf, rng);
     Col emis;
     float cosv = dot(hi.shading_normal, sdir);
+    if (g_dbg) printf("CPU env ec %a %a %a pdf %a dir %a %a %a cos %a ip %a %a %a prim %d occ %d\n", ec.r, ec.g, ec.b, epdf, sdir.x, sdir.y, sdir.z, cosv, hi.inter_point.x, hi.inter_point.y, hi.inter_point.z, hi.prim, (int)shadow_ray(c, hi.inter_point, sdir, 1.0e35f, hi.prim));
     if (epdf > 0.0f && cosv > 0.0f) {
         if (!shadow_ray(c, hi.inter_point, sdir, 1.0e35f, hi.prim)) {
             float bp;
@@ -807,6 +818,7 @@ Col sample_environment_map(Ctx& c, const Payload& pl, const HitInfo& hi, f3 view
             Col bc = bsdf_eval(c.bc, c.override_, pl.material, tv, view, hi.shading_normal, hi.geometric_normal, sdir, bp);
             float mw = c.f->options.envmap_bsdf_mis ? balance_heuristic(epdf, bp) : 1.0f;
             emis = bc * cosv * mw * ec / epdf;
+            if (g_dbg) printf("CPU env f %a %a %a bp %a mw %a e1 %a %a %a\n", bc.r, bc.g, bc.b, bp, mw, emis.r, emis.g, emis.b);
         }
     }
     if (!c.f->options.envmap_bsdf_mis) return emis;
@@ -862,6 +874,8 @@ struct PixelOut { Col color; Col albedo; f3 normal; bool valid; };
 // CameraRays (CameraRays.h:45-179) followed by FullPathTracer (FullPathTracer.h:99-327)
 PixelOut render_pixel(Ctx& c, int x, int y, GB& gb) {
     const MptFrame& f = *c.f;
+    { static int dbg_pix = getenv("ORACLE_DBG_PIX") ? atoi(getenv("ORACLE_DBG_PIX")) : -1;
+      g_dbg = (int)((uint32_t)x + (uint32_t)y * (uint32_t)f.res_x) == dbg_pix; }
     const MptRenderSettings& rs = f.render_settings;
     uint32_t pix = (uint32_t)x + (uint32_t)y * (uint32_t)f.res_x;
     uint32_t seed = rs.freeze_random ? wang_hash(pix + 1u) : wang_hash((pix + 1u) * (uint32_t)(rs.sample_number + 1) * f.random_seed);
@@ -919,6 +933,7 @@ PixelOut render_pixel(Ctx& c, int x, int y, GB& gb) {
                 Col ind = (ld + ed) * pl.throughput;
                 pl.ray_color += clamp_contrib(ind, rs.indirect_contribution_clamp, bounce > 0);
             }
+            if (g_dbg) printf("CPU b%d ld %a %a %a ed %a %a %a thr %a %a %a rc %a %a %a\n", bounce, ld.r, ld.g, ld.b, ed.r, ed.g, ed.b, pl.throughput.r, pl.throughput.g, pl.throughput.b, pl.ray_color.r, pl.ray_color.g, pl.ray_color.b);
             float bpdf;
             f3 bd;
             Col bc = bsdf_sample(c.bc, c.override_, pl.material, pl.vs, -rd, hi.shading_normal, hi.geometric_normal, bd, bpdf, rng);
@@ -943,6 +958,7 @@ PixelOut render_pixel(Ctx& c, int x, int y, GB& gb) {
             sky = clamp_contrib(sky, rs.envmap_contribution_clamp, true);
             Col ind = sky * pl.throughput;
             pl.ray_color += clamp_contrib(ind, rs.indirect_contribution_clamp, bounce > 0);
+            if (g_dbg) printf("CPU b%d miss sky %a %a %a rc %a %a %a\n", bounce, sky.r, sky.g, sky.b, pl.ray_color.r, pl.ray_color.g, pl.ray_color.b);
             pl.missed = true;
         }
     }

@@ -120,6 +120,25 @@ def test_oracle_traversal_matches_brute_force(cornell, luts, oracle_lib):
     o.close()
 
 
+@pytest.fixture(scope="module")
+def city():
+    from mpt import synthetic
+    return synthetic.procedural_city(1234)
+
+
+def test_oracle_grazing_rays_match_brute_force(city, luts, oracle_lib):
+    """Conservative box culling: rays running inside a wall's plane (the city stand-in's
+    envmap shadow rays) hit coplanar neighbours exactly as brute force says."""
+    from raygen import grazing_rays
+    rays, lh = grazing_rays(city, 24, 11)
+    o = oracle_lib.Oracle(city, luts)
+    prim, t, _, _ = o.trace_closest(rays, lh)
+    bf = brute_force_closest(city, rays, lh)
+    assert [p for p, _ in bf] == prim.tolist()
+    assert any(p >= 0 for p, _ in bf)
+    o.close()
+
+
 def _mat(**kw):
     m = abi.Material.default()
     for k, v in kw.items():
