@@ -98,6 +98,22 @@ def cpu_baseline(sd, luts, cam, W, H, opt, bounces, target_s, env=None, world=No
                       f"({BAND_H}-row bands, 1 of every {bc2}) of the same {W}x{H} frame, {dt:.1f} s"}
 
 
+def load_traffic(workload, W, H):
+    """HBM bytes per launch from the newest committed PMC summary of this workload
+    (profiles/r*_<workload>_pmc_traffic.json, made by tools/profile_round.sh +
+    tools/pmc_traffic.py from separate rocprofv3 --pmc passes of this same command).
+    PMC counters need rocprofv3 around the process, so they cannot be read live here."""
+    import glob
+    if (W, H) != (1920, 1080):
+        return None
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{workload}_pmc_traffic.json")))
+    if not files:
+        return None
+    d = json.load(open(files[-1]))
+    d["file"] = os.path.relpath(files[-1], ROOT)
+    return d
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -193,7 +209,7 @@ def main():
         launches = max(1, st.stage_launches[m])
         avg_ms = st.stage_ms[m] / launches
         ach = st.stage_rays[m] * b_ray / launches / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
-        lines.append({"kernel": names[m], "total_ms": st.stage_ms[m], "achieved": ach, "avg_launch_ms": avg_ms,
+        lines.append({"kernel": names[m], "symbol": f"void mpt::k_trace<{m}, false>(mpt::TraceArgs)", "total_ms": st.stage_ms[m], "achieved": ach, "avg_launch_ms": avg_ms,
                       "bytes_per_unit": b_ray, "unit_of_work": "ray", "nodes_per_ray": n_node, "tris_per_ray": n_tri,
                       "units_per_launch": st.stage_rays[m] / launches})
     # shade: per path vertex = material 256 + vertex gathers 12+36+36+24 + path state 2x96 (§8d)
@@ -201,16 +217,27 @@ def main():
     sl = max(1, st.shade_launches)
     s_avg = st.shade_ms / sl
     lines.append({"kernel": "k_shade<BSDF_NONE> (path vertex: hit, NEE sampling, BSDF sampling, RR)",
+                  "symbol": "void mpt::k_shade<0>(mpt::ShadeArgs)",
                   "total_ms": st.shade_ms, "avg_launch_ms": s_avg, "bytes_per_unit": b_vtx, "unit_of_work": "path vertex",
                   "units_per_launch": st.stage_rays[0] / sl,
                   "achieved": st.stage_rays[0] * b_vtx / sl / (s_avg * 1e-3) / 1e9 if s_avg > 0 else 0.0})
     dom = max(lines, key=lambda x: x["total_ms"])
 
+    default_cfg = a.strategy is None and a.bounces == 3 and a.bsdf == "principled" and a.scene is None
+    pmc = load_traffic(a.workload, W, H) if default_cfg else None
+
     def roof(x):
+        tr = pmc["kernels"].get(x["symbol"], {}) if pmc else {}
         r = {"bound": "hbm", "achieved": round(x["achieved"], 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-             "frac": round(x["achieved"] / HBM_PEAK_GBS, 5), "traffic": None, "kernel": x["kernel"],
+             "frac": round(x["achieved"] / HBM_PEAK_GBS, 5),
+             "traffic": round(tr["traffic_bytes"]) if tr.get("traffic_bytes") else None,
+             "kernel": x["kernel"],
              "avg_launch_ms": round(x["avg_launch_ms"], 5), "bytes_per_unit": round(x["bytes_per_unit"], 2),
              "unit_of_work": x["unit_of_work"], "units_per_launch": round(x["units_per_launch"], 1)}
+        if r["traffic"]:
+            r.update(traffic_read=round(tr["read_bytes"]), traffic_write=round(tr["write_bytes"]),
+                     traffic_per_unit=round(tr["traffic_bytes"] / max(1.0, x["units_per_launch"]), 1),
+                     traffic_source=pmc["file"])
         if "nodes_per_ray" in x:
             r.update(nodes_per_ray=round(x["nodes_per_ray"], 3), tris_per_ray=round(x["tris_per_ray"], 3))
         return r
