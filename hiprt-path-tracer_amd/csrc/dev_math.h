@@ -52,15 +52,21 @@ DEV float pow3(float x) { return x * x * x; }
 DEV float pow4(float x) { float x2 = x * x; return x2 * x2; }
 DEV float pow6(float x) { float x2 = x * x; float x4 = x2 * x2; return x4 * x2; }
 
-// transcendentals: double ocml, rounded once
-DEV float psin(float x) { return (float)::sin((double)x); }
-DEV float pcos(float x) { return (float)::cos((double)x); }
-DEV float pexp(float x) { return (float)::exp((double)x); }
-DEV float plog(float x) { return (float)::log((double)x); }
-DEV float ppow(float x, float y) { return (float)::pow((double)x, (double)y); }
-DEV float patan2(float y, float x) { return (float)::atan2((double)y, (double)x); }
-DEV float pasin(float x) { return (float)::asin((double)x); }
-DEV float pacos(float x) { return (float)::acos((double)x); }
+// transcendentals: double ocml, rounded once.  Out of line (one copy each): inlined,
+// the f64 ocml bodies made k_shade 282 KB of code, far beyond the instruction cache.
+#ifdef MPT_TRANS_INLINE
+#define TRANS DEV
+#else
+#define TRANS static __device__ __attribute__((noinline))
+#endif
+TRANS float psin(float x) { return (float)::sin((double)x); }
+TRANS float pcos(float x) { return (float)::cos((double)x); }
+TRANS float pexp(float x) { return (float)::exp((double)x); }
+TRANS float plog(float x) { return (float)::log((double)x); }
+TRANS float ppow(float x, float y) { return (float)::pow((double)x, (double)y); }
+TRANS float patan2(float y, float x) { return (float)::atan2((double)y, (double)x); }
+TRANS float pasin(float x) { return (float)::asin((double)x); }
+TRANS float pacos(float x) { return (float)::acos((double)x); }
 
 constexpr float PI = 3.14159265358979323846f;
 constexpr float TWO_PI = 6.28318530717958647693f;

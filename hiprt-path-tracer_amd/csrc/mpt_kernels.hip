@@ -574,7 +574,7 @@ struct ShadeArgs {
 };
 
 #ifndef MPT_SHADE_WAVES
-#define MPT_SHADE_WAVES 1
+#define MPT_SHADE_WAVES 2
 #endif
 template <int OVR>
 __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MPT_SHADE_WAVES))) void k_shade(ShadeArgs A) {
