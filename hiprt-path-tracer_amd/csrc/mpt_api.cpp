@@ -96,6 +96,10 @@ struct MptContext {
     DBuf<int32_t> q0, q1, counters, nq_tgt, fetch_raw;
     DBuf<NeeRec> nee;
     DBuf<float> fb_color, fb_albedo, fb_normal;
+    DBuf<int32_t> as_count, as_conv;
+    DBuf<float> as_sqlum;
+    DBuf<uint8_t> active;
+    DBuf<uint32_t> status;
     DBuf<MptMaterial> mat_slot;
     DBuf<uint64_t> stats;
     DBuf<uint64_t> ray_counts;
@@ -195,6 +199,11 @@ DevPaths dev_paths(MptContext* c) {
     P.stack_spill = c->spill.p;
     P.stats = c->stats.p;
     P.ray_counts = c->ray_counts.p;
+    P.as_count = c->as_count.p;
+    P.as_sqlum = c->as_sqlum.p;
+    P.as_conv = c->as_conv.p;
+    P.active = c->active.p;
+    P.status = c->status.p;
     return P;
 }
 
@@ -221,6 +230,11 @@ int ensure_paths(MptContext* c, int rx, int ry, int bh, int bi, int bc) {
     HIPCHK(hipMemsetAsync(c->fb_color.p, 0, 3 * N * sizeof(float), c->stream));
     HIPCHK(hipMemsetAsync(c->fb_albedo.p, 0, 3 * N * sizeof(float), c->stream));
     HIPCHK(hipMemsetAsync(c->fb_normal.p, 0, 3 * N * sizeof(float), c->stream));
+    HIPCHK(c->as_count.alloc(N)); HIPCHK(c->as_sqlum.alloc(N)); HIPCHK(c->as_conv.alloc(N)); HIPCHK(c->active.alloc(N));
+    HIPCHK(hipMemsetAsync(c->as_count.p, 0, N * sizeof(int32_t), c->stream));
+    HIPCHK(hipMemsetAsync(c->as_sqlum.p, 0, N * sizeof(float), c->stream));
+    HIPCHK(hipMemsetAsync(c->as_conv.p, 0xff, N * sizeof(int32_t), c->stream));
+    HIPCHK(hipMemsetAsync(c->active.p, 0, N, c->stream));
     return MPT_OK;
 }
 
@@ -244,8 +258,6 @@ int validate_frame(const MptFrame* f) {
     if (f->band_height <= 0 || f->band_count <= 0 || f->band_index < 0 || f->band_index >= f->band_count)
         return fail(MPT_ERR_INVALID_ARGUMENT, "invalid row partition");
     if (rs.nb_bounces < 0 || rs.nb_bounces > 64) return fail(MPT_ERR_INVALID_ARGUMENT, "nb_bounces out of range");
-    if (rs.accumulate && (rs.enable_adaptive_sampling || rs.stop_pixel_noise_threshold > 0.0f))
-        return fail(MPT_ERR_UNSUPPORTED, "adaptive sampling / stop-noise threshold not implemented yet (SURVEY §8f #3)");
     if (rs.wants_render_low_resolution && rs.allow_render_low_resolution && rs.accumulate)
         return fail(MPT_ERR_UNSUPPORTED, "low-resolution interactive mode not implemented");
     if (rs.do_alpha_testing)
@@ -326,6 +338,8 @@ int mpt_create(int device, void* hip_stream, MptContext** out) {
     HIPCHK(c->stats.alloc(N_STATS));
     HIPCHK(hipMemsetAsync(c->stats.p, 0, N_STATS * sizeof(uint64_t), c->stream));
     HIPCHK(c->ray_counts.alloc(4));
+    HIPCHK(c->status.alloc(4));
+    HIPCHK(hipMemsetAsync(c->status.p, 0, 4 * sizeof(uint32_t), c->stream));
     HIPCHK(hipMemsetAsync(c->ray_counts.p, 0, 4 * sizeof(uint64_t), c->stream));
     HIPCHK(c->spill.alloc((size_t)c->grid * TRAV_BLOCK * SPILL_WORDS));
     for (int p = 0; p < 2; p++) {
@@ -349,7 +363,8 @@ int mpt_destroy(MptContext* c) {
     c->nodes.release(); c->tris.release(); c->idx.release(); c->mat_idx.release(); c->mat_prio.release();
     c->emissive.release(); c->tex_dims.release(); c->pos.release(); c->nrm.release(); c->uv.release();
     c->has_n.release(); c->tex.release(); c->tex_off.release(); c->mats.release();
-    c->mats_res.release(); c->mat_tex.release(); c->mat_slot.release(); c->em_tab.release();
+    c->mats_res.release(); c->mat_tex.release(); c->as_count.release(); c->as_sqlum.release(); c->as_conv.release();
+    c->active.release(); c->status.release(); c->mat_slot.release(); c->em_tab.release();
     c->lut_conductor.release(); c->lut_glossy.release(); c->lut_glass.release(); c->lut_glass_inv.release();
     c->lut_thin.release(); c->lut_sheen.release(); c->env.release(); c->alias_p.release(); c->alias_i.release();
     c->ray_o.release(); c->ray_d.release(); c->hit.release(); c->thr.release(); c->col.release(); c->alb.release();
@@ -594,6 +609,37 @@ int mpt_get_framebuffer(MptContext* c, int kind, float* dst, int dst_is_device) 
     HIPCHK(hipSetDevice(c->device));
     size_t bytes = 3 * (size_t)c->n_slots * sizeof(float);
     HIPCHK(hipMemcpyAsync(dst, src, bytes, dst_is_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return MPT_OK;
+}
+
+int mpt_clear_status(MptContext* c) {
+    if (!c) return fail(MPT_ERR_INVALID_ARGUMENT, "NULL context");
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipMemsetAsync(c->status.p, 0, 4 * sizeof(uint32_t), c->stream));
+    return MPT_OK;
+}
+
+int mpt_query_status(MptContext* c, MptStatus* out) {
+    if (!c || !out) return fail(MPT_ERR_INVALID_ARGUMENT, "NULL argument");
+    HIPCHK(hipSetDevice(c->device));
+    uint32_t v[4];
+    HIPCHK(hipMemcpyAsync(v, c->status.p, sizeof(v), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    out->one_ray_active = v[1] != 0;
+    out->pixel_converged_count = v[0];
+    return MPT_OK;
+}
+
+int mpt_get_aux_buffer(MptContext* c, int kind, void* dst, int dst_is_device) {
+    if (!c || !dst) return fail(MPT_ERR_INVALID_ARGUMENT, "NULL argument");
+    const void* src = kind == MPT_AUX_SAMPLE_COUNT ? (const void*)c->as_count.p
+                    : kind == MPT_AUX_CONVERGED_SAMPLE_COUNT ? (const void*)c->as_conv.p
+                    : kind == MPT_AUX_SQUARED_LUMINANCE ? (const void*)c->as_sqlum.p : nullptr;
+    if (!src) return fail(MPT_ERR_INVALID_ARGUMENT, "bad aux buffer kind or no frame rendered");
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipMemcpyAsync(dst, src, (size_t)c->n_slots * 4, dst_is_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost,
+                          c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     return MPT_OK;
 }

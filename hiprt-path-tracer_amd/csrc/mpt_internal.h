@@ -110,6 +110,12 @@ struct DevPaths {
     uint32_t* stack_spill;    // global spill area of the traversal stacks
     uint64_t* stats;          // [trace mode][rays, nodes, tris, -] (instrumented traversal)
     uint64_t* ray_counts;     // path rays, NEE any-hit rays, NEE closest rays (always on)
+    // adaptive sampling / stop-noise threshold (AuxiliaryBuffers, RenderData.h:62-84)
+    int32_t* as_count;        // pixel_sample_count
+    float* as_sqlum;          // pixel_squared_luminance
+    int32_t* as_conv;         // pixel_converged_sample_count (-1 = not converged)
+    uint8_t* active;          // pixel_active
+    uint32_t* status;         // [0] stop_noise_threshold_converged_count, [1] still_one_ray_active
 };
 
 constexpr int N_TRACE_MODES = 5;

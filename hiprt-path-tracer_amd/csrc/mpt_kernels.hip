@@ -407,10 +407,88 @@ DEV uint32_t pixel_seed(const MptFrame& F, uint32_t pix) {
 // ----------------------------------------------------------------------------------
 // k_camera: CameraRays ray generation (CameraRays.h:127-142, HIPRTCamera.h:27-47)
 // ----------------------------------------------------------------------------------
+DEV bool has_adaptive_buffers(const MptRenderSettings& rs) {   // RenderSettings.h:207-218
+    return (rs.stop_pixel_noise_threshold > 0.0f || rs.enable_adaptive_sampling) && rs.accumulate;
+}
+// get_pixel_confidence_interval (AdaptiveSampling.h:11-20)
+DEV float pixel_confidence(const DevPaths& P, int slot, int count, float& avg) {
+    const float* px = P.fb_color + 3 * (size_t)slot;
+    float l = lum(col(px[0], px[1], px[2]));
+    avg = l / (float)(count + 1);
+    float var = (P.as_sqlum[slot] - l * avg) / (float)(count + 1);
+    return 1.96f * sqrtf(var) / sqrtf((float)(count + 1));
+}
+// adaptive_sampling (AdaptiveSampling.h:30-104): true if the pixel needs this sample
+DEV bool adaptive_sampling(const DevPaths& P, const MptRenderSettings& rs, int slot, bool& converged) {
+    if (!has_adaptive_buffers(rs)) return true;
+    if (rs.enable_adaptive_sampling) {
+        if (P.as_conv[slot] != -1) return false;
+        int cnt = P.as_count[slot];
+        if (cnt > rs.adaptive_sampling_min_samples) {
+            float avg;
+            float ci = pixel_confidence(P, slot, cnt, avg);
+            if (!(ci > rs.adaptive_sampling_noise_threshold * avg)) {
+                if (P.as_conv[slot] == -1) P.as_conv[slot] = cnt;
+                return false;
+            }
+        }
+        return true;
+    } else if (rs.stop_pixel_noise_threshold > 0.0f && rs.enable_pixel_stop_noise_threshold) {
+        int cnt = P.as_count[slot];
+        float avg;
+        float ci = pixel_confidence(P, slot, cnt, avg);
+        converged = (ci <= rs.stop_pixel_noise_threshold * avg) && (rs.sample_number > 1);
+        int cur = P.as_conv[slot];
+        if (converged && cur == -1) P.as_conv[slot] = cnt;
+        else if (!converged) P.as_conv[slot] = -1;
+    }
+    return true;
+}
+
 __global__ __launch_bounds__(TB) void k_camera(DevPaths P, const MptFrame* __restrict__ Fp) {
     const MptFrame& F = *Fp;
+    const MptRenderSettings& rs = F.render_settings;
     int slot = blockIdx.x * TB + threadIdx.x;
-    if (slot >= P.n) return;
+    const bool as = has_adaptive_buffers(rs);
+    bool act = slot < P.n;
+    if (act) {
+        // reset_render + adaptive gate (CameraRays.h:19-43, 88-125)
+        if (as && (rs.sample_number == 0 || rs.need_to_reset)) {
+            P.as_count[slot] = 0;
+            P.as_sqlum[slot] = 0.0f;
+            P.as_conv[slot] = -1;
+        }
+        bool converged = false;
+        bool needed = adaptive_sampling(P, rs, slot, converged);
+        if ((converged || !needed) && rs.do_update_status_buffers) atomicAdd(&P.status[0], 1u);
+        if (as) {
+            if (!needed) {
+                float* px = P.fb_color + 3 * (size_t)slot;
+                Col c = col(px[0], px[1], px[2]) / (float)rs.sample_number * (float)(rs.sample_number + 1);
+                px[0] = c.r; px[1] = c.g; px[2] = c.b;
+                act = false;
+            } else {
+                P.as_count[slot]++;
+            }
+        }
+        P.active[slot] = act ? 1 : 0;
+    }
+    if (as) {
+        // camera-ray queue of the active pixels (wave64 ballot, one atomic per wave)
+        uint64_t m = __ballot(act);
+        int lane = threadIdx.x & 63;
+        int base = 0;
+        if (m) {
+            int first = __ffsll((unsigned long long)m) - 1;
+            if (lane == first) base = atomicAdd(&P.counters[CTR_Q0], __popcll(m));
+            base = __shfl(base, first);
+        }
+        if (act) P.q0[base + __popcll(m & ((1ull << lane) - 1ull))] = slot;
+    } else if (act) {
+        P.q0[slot] = slot;
+    }
+    if (!act) return;
+    if (rs.do_update_status_buffers) P.status[1] = 1u;
     int x, y;
     uint32_t pix = slot_pixel(F, slot, x, y);
     Rng rng = make_rng(pixel_seed(F, pix));
@@ -430,7 +508,6 @@ __global__ __launch_bounds__(TB) void k_camera(DevPaths P, const MptFrame* __res
     P.col[slot] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     P.alb[slot] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     P.nrm[slot] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    P.q0[slot] = slot;
 }
 
 // ----------------------------------------------------------------------------------
@@ -1179,6 +1256,7 @@ __global__ __launch_bounds__(TB) void k_accumulate(DevPaths P, const MptFrame* _
     const MptRenderSettings& rs = F.render_settings;
     int slot = blockIdx.x * TB + threadIdx.x;
     if (slot >= P.n) return;
+    if (!P.active[slot]) return;          // FullPathTracer.h:114-115
     float4 cv = P.col[slot];
     Col c = col(cv.x, cv.y, cv.z);
     float wl = __uint_as_float(P.vsB[slot].w);
@@ -1193,6 +1271,11 @@ __global__ __launch_bounds__(TB) void k_accumulate(DevPaths P, const MptFrame* _
             fb[0] = dc.r; fb[1] = dc.g; fb[2] = dc.b;
         }
         return;
+    }
+    P.status[1] = 1u;                     // still_one_ray_active (FullPathTracer.h:299)
+    if (has_adaptive_buffers(rs)) {
+        float l = lum(c);
+        P.as_sqlum[slot] += l * l;
     }
     if (rs.sample_number == 0) { fb[0] = c.r; fb[1] = c.g; fb[2] = c.b; }
     else { fb[0] += c.r; fb[1] += c.g; fb[2] += c.b; }
@@ -1250,11 +1333,14 @@ hipError_t launch_frame(const DevScene& S, const DevPaths& P, const MptFrame* d_
                         hipStream_t st) {
     const int n = P.n;
     if (n == 0) return hipSuccess;
+    const MptRenderSettings& hrs = hf.render_settings;
+    const bool as = (hrs.stop_pixel_noise_threshold > 0.0f || hrs.enable_adaptive_sampling) && hrs.accumulate;
+    // all pixels start a path, unless adaptive sampling compacts the camera queue
+    hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(&P.counters[CTR_Q0]), as ? 0 : n, 1, st);
     {
         TimedScope ts(cfg, st, KT_CAMERA);
         hipLaunchKernelGGL(k_camera, dim3(blocks_for(n)), dim3(TB), 0, st, P, d_frame);
     }
-    hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(&P.counters[CTR_Q0]), n, 1, st);
     int32_t* q_cur = P.q0;
     int32_t* q_next = P.q1;
     int c_cur = CTR_Q0, c_next = CTR_Q1;

@@ -27,7 +27,8 @@ SYMBOLS = [
     "mpt_last_error", "mpt_version", "mpt_abi_sizes", "mpt_create", "mpt_destroy", "mpt_upload_scene",
     "mpt_update_materials", "mpt_set_envmap", "mpt_build_alias_table", "mpt_set_luts", "mpt_resize",
     "mpt_render_frame", "mpt_synchronize", "mpt_query_done", "mpt_get_framebuffer", "mpt_partition_rows",
-    "mpt_enable_stats", "mpt_get_stats", "mpt_trace_closest", "mpt_trace_any",
+    "mpt_enable_stats", "mpt_get_stats", "mpt_trace_closest", "mpt_trace_any", "mpt_clear_status",
+    "mpt_query_status", "mpt_get_aux_buffer",
 ]
 
 
@@ -69,6 +70,9 @@ def lib() -> C.CDLL:
     L.mpt_get_stats.argtypes = [vp, C.POINTER(abi.Stats)]
     L.mpt_trace_closest.argtypes = [vp, vp, vp, i32, vp, vp, vp, vp, C.c_int]
     L.mpt_trace_any.argtypes = [vp, vp, vp, i32, vp, C.c_int]
+    L.mpt_clear_status.argtypes = [vp]
+    L.mpt_query_status.argtypes = [vp, C.POINTER(abi.Status)]
+    L.mpt_get_aux_buffer.argtypes = [vp, C.c_int, vp, C.c_int]
     _lib = L
     return L
 
@@ -172,6 +176,24 @@ class GPURenderer:
 
     def framebuffer_to_device(self, kind, dev_ptr: int):
         _check(lib().mpt_get_framebuffer(self.h, kind, C.c_void_p(dev_ptr), 1))
+
+    # --- status buffers / adaptive sampling (GPURenderer.cpp:269-283) ---------------
+    def clear_status_buffers(self):
+        """internal_update_clear_device_status_buffers: once per displayed frame."""
+        _check(lib().mpt_clear_status(self.h))
+
+    def get_status_buffer_values(self) -> dict:
+        """copy_status_buffers + get_status_buffer_values (StatusBuffersValues)."""
+        st = abi.Status()
+        _check(lib().mpt_query_status(self.h, C.byref(st)))
+        return {"one_ray_active": bool(st.one_ray_active), "pixel_converged_count": int(st.pixel_converged_count)}
+
+    def aux_buffer(self, kind):
+        """MPT_AUX_* buffer of the partition -> [rows, W] (int32, or float32 for squared luminance)."""
+        f = self.frame
+        out = np.zeros((self.rows(), f.res_x), np.float32 if kind == abi.AUX_SQUARED_LUMINANCE else np.int32)
+        _check(lib().mpt_get_aux_buffer(self.h, kind, _p(out), 0))
+        return out
 
     # --- stats / queries -------------------------------------------------------
     def enable_stats(self, timing=True, instrumented=False):

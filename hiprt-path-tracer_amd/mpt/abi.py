@@ -360,6 +360,12 @@ BSDF_NONE, BSDF_LAMBERTIAN = 0, 1
 ESS_NO_SAMPLING, ESS_BINARY_SEARCH, ESS_ALIAS_TABLE = range(3)
 AMBIENT_NONE, AMBIENT_UNIFORM, AMBIENT_ENVMAP = range(3)
 FB_COLOR, FB_ALBEDO, FB_NORMALS = range(3)
+AUX_SAMPLE_COUNT, AUX_CONVERGED_SAMPLE_COUNT, AUX_SQUARED_LUMINANCE = range(3)
+
+
+class Status(C.Structure):
+    """MptStatus == StatusBuffersValues (Renderer/StatusBuffersValues.h:9-21)."""
+    _fields_ = [("one_ray_active", C.c_bool), ("pixel_converged_count", C.c_uint32)]
 
 ABI_SIZES = {"Material": 332, "RenderSettings": 304, "WorldSettings": 200, "Camera": 196}
 

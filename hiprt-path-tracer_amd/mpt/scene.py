@@ -408,6 +408,8 @@ def make_frame(camera, width, height, options=None, settings=None, world=None, f
     fr = abi.Frame()
     fr.render_settings = settings if settings is not None else parity_settings()
     fr.render_settings.sample_number = sample_number
+    # GPURenderer::render clears need_to_reset after the first launch (GPURenderer.cpp:446)
+    fr.render_settings.need_to_reset = sample_number == 0
     fr.world_settings = world if world is not None else abi.WorldSettings.default()
     fr.current_camera = camera
     fr.prev_camera = camera

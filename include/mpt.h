@@ -383,6 +383,17 @@ typedef struct MptStats {
 #define MPT_FB_ALBEDO 1       /* denoiser_albedo */
 #define MPT_FB_NORMALS 2      /* denoiser_normals */
 
+/* Adaptive-sampling buffers (AuxiliaryBuffers, RenderData.h:62-84), 4 bytes per pixel */
+#define MPT_AUX_SAMPLE_COUNT 0            /* pixel_sample_count (int32) */
+#define MPT_AUX_CONVERGED_SAMPLE_COUNT 1  /* pixel_converged_sample_count (int32, -1 = not converged) */
+#define MPT_AUX_SQUARED_LUMINANCE 2       /* pixel_squared_luminance (float) */
+
+/* StatusBuffersValues (Renderer/StatusBuffersValues.h:9-21) */
+typedef struct MptStatus {
+    bool one_ray_active;              /* at least one pixel still sampled in the last frame */
+    uint32_t pixel_converged_count;   /* pixels converged (adaptive sampling / stop noise threshold) */
+} MptStatus;
+
 typedef struct MptContext MptContext;
 
 const char* mpt_last_error(void);
@@ -410,6 +421,13 @@ int mpt_query_done(MptContext* ctx, int* out_done);
  * rows owned by this context in increasing y) to dst; dst may be host or device. */
 int mpt_get_framebuffer(MptContext* ctx, int kind, float* dst, int dst_is_device);
 int mpt_partition_rows(int32_t res_y, int32_t band_height, int32_t band_index, int32_t band_count);
+/* Status buffers: mpt_clear_status <- GPURenderer::internal_update_clear_device_status_buffers
+ * (GPURenderer.cpp:275-283, once per displayed frame); the last sample of the frame sets
+ * render_settings.do_update_status_buffers; mpt_query_status <- copy_status_buffers (.cpp:269-273). */
+int mpt_clear_status(MptContext* ctx);
+int mpt_query_status(MptContext* ctx, MptStatus* out);
+/* Copies an MPT_AUX_* buffer of the partition (n_slots * 4 bytes) to dst (host or device). */
+int mpt_get_aux_buffer(MptContext* ctx, int kind, void* dst, int dst_is_device);
 int mpt_enable_stats(MptContext* ctx, int enable, int instrumented);
 int mpt_get_stats(MptContext* ctx, MptStats* out);
 /* Raw ray queries against the uploaded BVH8 (parity / microbenchmarks).

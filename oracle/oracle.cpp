@@ -1035,12 +1035,51 @@ int oracle_trace_closest(OracleScene* sc, const float* rays, const int32_t* last
  * numbers / seeds) into the running sums.  sum_rgb/albedo/normals are res_x*res_y*3
  * floats over the frame's row partition in band-major compact layout, like
  * mpt_get_framebuffer.  Returns counted closest/any rays in rays[2]. */
+// has_access_to_adaptive_sampling_buffers (RenderSettings.h:207-218)
+inline bool has_adaptive_buffers(const MptRenderSettings& rs) {
+    return (rs.stop_pixel_noise_threshold > 0.0f || rs.enable_adaptive_sampling) && rs.accumulate;
+}
+// get_pixel_confidence_interval (AdaptiveSampling.h:11-20)
+inline float pixel_confidence(const float* px, float sqlum, int count, float& avg) {
+    float l = Col(px[0], px[1], px[2]).luminance();
+    avg = l / (float)(count + 1);
+    float var = (sqlum - l * avg) / (float)(count + 1);
+    return 1.96f * std::sqrt(var) / std::sqrt((float)(count + 1));
+}
+// adaptive_sampling (AdaptiveSampling.h:30-104)
+inline bool adaptive_sampling(const MptRenderSettings& rs, const float* px, float sqlum, int32_t& count, int32_t& conv,
+                              bool& converged) {
+    if (!has_adaptive_buffers(rs)) return true;
+    if (rs.enable_adaptive_sampling) {
+        if (conv != -1) return false;
+        if (count > rs.adaptive_sampling_min_samples) {
+            float avg;
+            float ci = pixel_confidence(px, sqlum, count, avg);
+            if (!(ci > rs.adaptive_sampling_noise_threshold * avg)) {
+                if (conv == -1) conv = count;
+                return false;
+            }
+        }
+        return true;
+    } else if (rs.stop_pixel_noise_threshold > 0.0f && rs.enable_pixel_stop_noise_threshold) {
+        float avg;
+        float ci = pixel_confidence(px, sqlum, count, avg);
+        converged = (ci <= rs.stop_pixel_noise_threshold * avg) && (rs.sample_number > 1);
+        if (converged && conv == -1) conv = count;
+        else if (!converged) conv = -1;
+    }
+    return true;
+}
+
+/* as_count / as_sqlum / as_conv: the adaptive-sampling buffers (one per pixel of the
+ * partition, kept by the caller across calls); status[0] converged count, status[1]
+ * one ray active.  All four may be NULL when adaptive sampling is off. */
 int oracle_render(OracleScene* sc, const MptFrame* frames, int nframes, float* sum_rgb, float* albedo, float* normals,
-                  uint64_t* rays, int nthreads) {
+                  uint64_t* rays, int nthreads, int32_t* as_count, float* as_sqlum, int32_t* as_conv, uint32_t* status) {
     OScene& s = *reinterpret_cast<OScene*>(sc);
     if (nframes <= 0) return 0;
     const MptFrame& f0 = frames[0];
-    if (f0.render_settings.enable_adaptive_sampling || (f0.render_settings.stop_pixel_noise_threshold > 0.0f && f0.render_settings.accumulate) ||
+    if ((has_adaptive_buffers(f0.render_settings) && !(as_count && as_sqlum && as_conv && status)) ||
         f0.render_settings.do_alpha_testing || f0.render_settings.wants_render_low_resolution ||
         f0.options.direct_light_sampling == MPT_LSS_RESTIR_DI || f0.options.envmap_sampling == MPT_ESS_BINARY_SEARCH)
         return -4;
@@ -1066,11 +1105,31 @@ int oracle_render(OracleScene* sc, const MptFrame* frames, int nframes, float* s
             c.override_ = f.options.bsdf_override;
             c.lss = f.options.direct_light_sampling;
             int y = rows[r];
+            const MptRenderSettings& rs = f.render_settings;
+            const bool as = has_adaptive_buffers(rs);
             for (int x = 0; x < W; x++) {
                 size_t o = (size_t)r * W + x;
+                float* p = sum_rgb + 3 * o;
+                if (as) {
+                    // CameraRays: reset_render + adaptive gate (CameraRays.h:19-43, 88-125)
+                    if (rs.sample_number == 0 || rs.need_to_reset) { as_count[o] = 0; as_sqlum[o] = 0.0f; as_conv[o] = -1; }
+                    bool converged = false;
+                    bool needed = adaptive_sampling(rs, p, as_sqlum[o], as_count[o], as_conv[o], converged);
+                    if ((converged || !needed) && rs.do_update_status_buffers) {
+#pragma omp atomic
+                        status[0]++;
+                    }
+                    if (!needed) {
+                        Col cc = Col(p[0], p[1], p[2]) / (float)rs.sample_number * (float)(rs.sample_number + 1);
+                        p[0] = cc.r; p[1] = cc.g; p[2] = cc.b;
+                        continue;
+                    }
+                    as_count[o]++;
+                }
                 PixelOut po = render_pixel(c, x, y, gbuf[o]);
                 if (!po.valid) continue;   // sanity_check fails -> no buffer write (FullPathTracer.h:293-294)
-                float* p = sum_rgb + 3 * o;
+                if (status) status[1] = 1u;
+                if (as) { float l = po.color.luminance(); as_sqlum[o] += l * l; }
                 if (f.render_settings.sample_number == 0) { p[0] = po.color.r; p[1] = po.color.g; p[2] = po.color.b; }
                 else { p[0] += po.color.r; p[1] += po.color.g; p[2] += po.color.b; }
                 float cnt = (float)f.render_settings.denoiser_AOV_accumulation_counter;

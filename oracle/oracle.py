@@ -43,7 +43,7 @@ def lib():
         L.oracle_trace_closest.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p,
                                            C.c_void_p, C.c_void_p]
         L.oracle_render.argtypes = [C.c_void_p, C.POINTER(abi.Frame), C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
-                                    C.c_void_p, C.c_int]
+                                    C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
         L.oracle_bsdf_eval.argtypes = [C.POINTER(abi.Material), C.POINTER(abi.Material), C.POINTER(abi.Luts), C.c_int,
                                        C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
         L.oracle_bsdf_sample.argtypes = [C.POINTER(abi.Material), C.POINTER(abi.Material), C.POINTER(abi.Luts),
@@ -112,10 +112,20 @@ class Oracle:
         nrm = np.zeros((n, 3), np.float32) if aov else None
         arr = (abi.Frame * len(frames))(*frames)
         rays = np.zeros(2, np.uint64)
-        rc = lib().oracle_render(self.h, arr, len(frames), _p(out), _p(alb), _p(nrm), _p(rays), nthreads)
+        # adaptive-sampling buffers and status values (AuxiliaryBuffers / StatusBuffersValues),
+        # reported in last_aux after the call
+        cnt = np.zeros(n, np.int32)
+        sql = np.zeros(n, np.float32)
+        conv = np.full(n, -1, np.int32)
+        status = np.zeros(4, np.uint32)
+        rc = lib().oracle_render(self.h, arr, len(frames), _p(out), _p(alb), _p(nrm), _p(rays), nthreads,
+                                 _p(cnt), _p(sql), _p(conv), _p(status))
         if rc != 0:
             raise RuntimeError("oracle_render failed: %d (unsupported option)" % rc)
         self.last_rays = (int(rays[0]), int(rays[1]))
+        self.last_aux = {"sample_count": cnt.reshape(rows, f0.res_x), "squared_luminance": sql.reshape(rows, f0.res_x),
+                         "converged_sample_count": conv.reshape(rows, f0.res_x),
+                         "one_ray_active": bool(status[1]), "pixel_converged_count": int(status[0])}
         out = out.reshape(rows, f0.res_x, 3)
         if aov:
             return out, alb.reshape(rows, f0.res_x, 3), nrm.reshape(rows, f0.res_x, 3)

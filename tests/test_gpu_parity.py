@@ -207,7 +207,8 @@ def test_unsupported_options_fail_loudly(scenes, luts):
     sd = scenes["cornell_pbr"]
     r = renderer(sd, luts)
     f = frames(sd, 16, 16, 1)[0]
-    f.render_settings.enable_adaptive_sampling = True
+    f.render_settings.wants_render_low_resolution = True
+    f.render_settings.allow_render_low_resolution = True
     with pytest.raises(mpt.MptError) as e:
         r.render(f)
     assert e.value.code == -4
