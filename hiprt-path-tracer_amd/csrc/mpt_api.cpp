@@ -79,6 +79,8 @@ struct MptContext {
     DBuf<float4> em_tab;
     bool any_tex = false;
     std::vector<MptMaterial> h_mats;
+    std::vector<int32_t> h_mat_idx;       // per triangle (alpha flags of the triangle records)
+    std::vector<uint8_t> h_tex_alpha;     // per texture: some texel has alpha < 255
     int n_tex = 0;
     // luts / envmap
     DBuf<float> lut_conductor, lut_glossy, lut_glass, lut_glass_inv, lut_thin, lut_sheen;
@@ -238,6 +240,33 @@ int ensure_paths(MptContext* c, int rx, int ry, int bh, int bi, int bc) {
     return MPT_OK;
 }
 
+// Alpha-test flag of every triangle record (TriRec::pad0): the filter function's test
+// (FilterFunction.h:19-48) can only reject a hit when alpha_opacity < 1 or the base
+// colour texture has a texel with alpha < 255; all other triangles skip it for free.
+int upload_alpha_flags(MptContext* c) {
+    std::vector<uint8_t> mflag(c->h_mats.size());
+    for (size_t i = 0; i < c->h_mats.size(); i++) {
+        const MptMaterial& m = c->h_mats[i];
+        int bt = m.base_color_texture_index;
+        bool tex_alpha = bt >= 0 && bt < (int)c->h_tex_alpha.size() && c->h_tex_alpha[bt];
+        mflag[i] = (m.alpha_opacity < 1.0f || tex_alpha) ? 1 : 0;
+    }
+    bool changed = false;
+    for (TriRec& tr : c->bvh.tris) {
+        int32_t prim;
+        std::memcpy(&prim, &tr.prim_bits, 4);
+        uint32_t f = mflag[c->h_mat_idx[prim]];
+        uint32_t old;
+        std::memcpy(&old, &tr.pad0, 4);
+        if (old != f) { std::memcpy(&tr.pad0, &f, 4); changed = true; }
+    }
+    if (changed) {
+        HIPCHK(c->tris.upload(c->bvh.tris.data(), c->bvh.tris.size(), c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+    }
+    return MPT_OK;
+}
+
 int resolve_materials(MptContext* c) {
     size_t n = c->h_mats.size();
     HIPCHK(c->mats_res.alloc(n));
@@ -260,8 +289,6 @@ int validate_frame(const MptFrame* f) {
     if (rs.nb_bounces < 0 || rs.nb_bounces > 64) return fail(MPT_ERR_INVALID_ARGUMENT, "nb_bounces out of range");
     if (rs.wants_render_low_resolution && rs.allow_render_low_resolution && rs.accumulate)
         return fail(MPT_ERR_UNSUPPORTED, "low-resolution interactive mode not implemented");
-    if (rs.do_alpha_testing)
-        return fail(MPT_ERR_UNSUPPORTED, "alpha testing not implemented yet (do_alpha_testing must be false)");
     if (rs.number_of_light_samples != 1) return fail(MPT_ERR_UNSUPPORTED, "number_of_light_samples must be 1");
     if (rs.ris_number_of_bsdf_candidates < 0 || rs.ris_number_of_bsdf_candidates > 1)
         return fail(MPT_ERR_UNSUPPORTED, "ris_number_of_bsdf_candidates must be 0 or 1");
@@ -414,6 +441,7 @@ int mpt_upload_scene(MptContext* c, const MptScene* s) {
     HIPCHK(c->uv.upload(uv, 2 * (size_t)s->num_vertices, st));
     HIPCHK(c->has_n.upload(hn, (size_t)s->num_vertices, st));
     HIPCHK(c->mat_idx.upload(s->material_indices, (size_t)s->num_triangles, st));
+    c->h_mat_idx.assign(s->material_indices, s->material_indices + s->num_triangles);
     c->h_mats.assign(s->materials, s->materials + s->num_materials);
     HIPCHK(c->mats.upload(c->h_mats.data(), c->h_mats.size(), st));
     std::vector<int32_t> prio(s->num_materials);
@@ -430,14 +458,23 @@ int mpt_upload_scene(MptContext* c, const MptScene* s) {
             total += (uint64_t)s->texture_dims[2 * i] * s->texture_dims[2 * i + 1] * 4;
         }
         std::vector<uint8_t> all(total);
-        for (int i = 0; i < s->num_textures; i++)
-            std::memcpy(all.data() + off[i], s->texture_data[i], (size_t)s->texture_dims[2 * i] * s->texture_dims[2 * i + 1] * 4);
+        c->h_tex_alpha.assign(s->num_textures, 0);
+        for (int i = 0; i < s->num_textures; i++) {
+            size_t texels = (size_t)s->texture_dims[2 * i] * s->texture_dims[2 * i + 1];
+            std::memcpy(all.data() + off[i], s->texture_data[i], texels * 4);
+            for (size_t k = 0; k < texels && !c->h_tex_alpha[i]; k++) c->h_tex_alpha[i] = s->texture_data[i][4 * k + 3] < 255;
+        }
         HIPCHK(c->tex.upload(all.data(), all.size(), st));
         HIPCHK(c->tex_off.upload(off.data(), off.size(), st));
         HIPCHK(c->tex_dims.upload(s->texture_dims, 2 * (size_t)s->num_textures, st));
         HIPCHK(hipStreamSynchronize(st));
-    } else HIPCHK(hipStreamSynchronize(st));
-    int rr = resolve_materials(c);
+    } else {
+        c->h_tex_alpha.clear();
+        HIPCHK(hipStreamSynchronize(st));
+    }
+    int rr = upload_alpha_flags(c);
+    if (rr != MPT_OK) return rr;
+    rr = resolve_materials(c);
     if (rr != MPT_OK) return rr;
     c->has_scene = true;
     return MPT_OK;
@@ -454,6 +491,8 @@ int mpt_update_materials(MptContext* c, const MptMaterial* m, int32_t count) {
     for (int i = 0; i < count; i++) prio[i] = m[i].dielectric_priority;
     HIPCHK(c->mat_prio.upload(prio.data(), prio.size(), c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
+    int rr = upload_alpha_flags(c);
+    if (rr != MPT_OK) return rr;
     return resolve_materials(c);
 }
 

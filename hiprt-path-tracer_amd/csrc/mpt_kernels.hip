@@ -64,11 +64,28 @@ DEV int wave_append(int32_t* counter, bool pred) {
 // ----------------------------------------------------------------------------------
 struct THit { int prim; float t, u, v; };
 
+// Alpha testing (filter_function, FilterFunction.h:19-48).  The reference draws one
+// path RNG number per candidate hit inside HIPRT's traversal, so its RNG stream depends
+// on the traversal order of a particular BVH.  Here the candidate's uniform is a hash of
+// (query key, primitive): the accept probability per candidate is the same
+// (alpha_opacity * base-colour alpha), so the expected image is the reference's, and
+// the result no longer depends on the traversal order (the oracle reproduces it bit
+// for bit).  The key is positional: pixel seed, bounce, query kind, boundary-skip pass.
+DEV uint32_t alpha_key(uint32_t pixel_seed, int bounce, int kind, int iter) {
+    return wang_hash(pixel_seed ^ wang_hash((uint32_t)(bounce * 8 + kind) * 0x85EBCA77u + (uint32_t)iter * 0xC2B2AE3Du + 1u));
+}
+DEV float alpha_uniform(uint32_t key, int prim) {
+    uint32_t h = wang_hash(key ^ ((uint32_t)prim * 0x9E3779B1u));
+    h = wang_hash(h + 0x7F4A7C15u);
+    return (float)(h >> 8) * (1.0f / 16777216.0f);
+}
+DEV bool alpha_rejects(const DevScene& S, int prim, float u, float v, uint32_t key);
+
 DEV uint32_t qbyte(uint32_t w0, uint32_t w1, int s) { return ((s < 4 ? w0 : w1) >> ((s & 3) * 8)) & 0xffu; }
 
 template <bool ANY, bool STATS>
 DEV bool traverse(const DevScene& S, v3 o, v3 d, int last_hit, float tmax, THit& out, uint2* lds, uint32_t* spill,
-                  uint32_t& n_nodes, uint32_t& n_tris) {
+                  uint32_t& n_nodes, uint32_t& n_tris, bool alpha_on = false, uint32_t akey = 0u) {
     const float4* nodes = reinterpret_cast<const float4*>(S.nodes);
     const float4* tris = reinterpret_cast<const float4*>(S.tris);
     float ix = 1.0f / (fabsf(d.x) > 1e-30f ? d.x : copysignf(1e-30f, d.x));
@@ -169,6 +186,10 @@ DEV bool traverse(const DevScene& S, v3 o, v3 d, int last_hit, float tmax, THit&
                 float t = f * dot(e2, q);
                 if (!(t > 0.0000001f)) continue;
                 if (prim == last_hit) continue;
+                // alpha-tested triangle (flag in the record): only when it would be kept
+                if (alpha_on && __float_as_uint(t1.w) != 0u &&
+                    (ANY ? t < tmax : (t < best || (t == best && prim < bprim))) && alpha_rejects(S, prim, u, v, akey))
+                    continue;
                 if (ANY) {
                     if (t < tmax) { out.prim = prim; out.t = t; out.u = u; out.v = v; return true; }
                 } else if (t < best || (t == best && prim < bprim)) {
@@ -201,7 +222,12 @@ struct TraceArgs {
     const float4* raw_d;
     float4* raw_hit;
     uint8_t* raw_occ;
+    const MptFrame* F;         // frame constants (alpha keys); NULL for raw queries
+    int bounce;
+    int alpha;                 // render_settings.do_alpha_testing
 };
+DEV uint32_t slot_pixel(const MptFrame& F, int slot, int& x, int& y);
+DEV uint32_t pixel_seed(const MptFrame& F, uint32_t pix);
 
 template <int MODE, bool STATS>
 __global__ __launch_bounds__(TB) void k_trace(TraceArgs A) {
@@ -239,9 +265,12 @@ __global__ __launch_bounds__(TB) void k_trace(TraceArgs A) {
             bool was_inside = false;
             bool found;
             int skips = 0;
+            uint32_t pseed = 0u;
+            if (A.alpha) { int px, py; pseed = pixel_seed(*A.F, slot_pixel(*A.F, slot, px, py)); }
             while (true) {
                 n_rays++;
-                found = traverse<false, STATS>(S, o, d, last_hit, INFINITY, h, lds, spill, n_nodes, n_tris);
+                found = traverse<false, STATS>(S, o, d, last_hit, INFINITY, h, lds, spill, n_nodes, n_tris, A.alpha != 0,
+                                               A.alpha ? alpha_key(pseed, A.bounce, 0, skips) : 0u);
                 if (!found) break;
                 was_inside = vs.pos > 0;
                 if (was_inside) vs.dist += h.t;
@@ -260,8 +289,11 @@ __global__ __launch_bounds__(TB) void k_trace(TraceArgs A) {
             P.hit_inside[slot] = was_inside ? 1 : 0;
         } else {
             n_rays++;
-            bool found = any ? traverse<true, STATS>(S, o, d, last_hit, rd.w, h, lds, spill, n_nodes, n_tris)
-                             : traverse<false, STATS>(S, o, d, last_hit, INFINITY, h, lds, spill, n_nodes, n_tris);
+            uint32_t akey = 0u;
+            bool al = (MODE == TM_NEE_ANY || MODE == TM_NEE_CLOSEST) && A.alpha;
+            if (al) { int px, py; akey = alpha_key(pixel_seed(*A.F, slot_pixel(*A.F, slot >> 2, px, py)), A.bounce, (slot & 3) + 1, 0); }
+            bool found = any ? traverse<true, STATS>(S, o, d, last_hit, rd.w, h, lds, spill, n_nodes, n_tris, al, akey)
+                             : traverse<false, STATS>(S, o, d, last_hit, INFINITY, h, lds, spill, n_nodes, n_tris, al, akey);
             if (MODE == TM_NEE_ANY) {
                 P.occ[slot] = found ? 1 : 0;
             } else if (MODE == TM_NEE_CLOSEST) {
@@ -317,6 +349,21 @@ DEV void tex_rgba(const DevScene& S, int ti, bool srgb, v2 uv, float out[4]) {
     if (srgb) for (int i = 0; i < 4; i++) out[i] = ppow(out[i], 2.2f);
 }
 DEV bool has_tex(int ti) { return ti != MPT_NO_TEXTURE && ti != MPT_CONSTANT_EMISSIVE_TEXTURE; }
+// filter_function's test: keep the candidate iff u < alpha_opacity * base-colour alpha
+// (get_hit_base_color_alpha, Material.h:23-37; the sRGB pow(2.2) of Texture.h:72-75 also
+// applies to the alpha channel)
+DEV bool alpha_rejects(const DevScene& S, int prim, float u, float v, uint32_t key) {
+    const Mat& m = S.mats[S.mat_idx[prim]];
+    float a = 1.0f;
+    if (S.n_tex > 0 && has_tex(m.base_color_texture_index)) {
+        v2 tc = uv_interp2(S.uv, tri_idx(S, prim), mk2(u, v));
+        float r[4];
+        tex_rgba(S, m.base_color_texture_index, true, tc, r);
+        a = r[3];
+    }
+    float comp = m.alpha_opacity * a;
+    return !(alpha_uniform(key, prim) < comp);
+}
 DEV void prop_f(const DevScene& S, float& v, v2 uv, int ti) { if (has_tex(ti)) { float r[4]; tex_rgba(S, ti, false, uv, r); v = r[0]; } }
 DEV void prop_c(const DevScene& S, MptColor& v, v2 uv, int ti) { if (has_tex(ti)) { float r[4]; tex_rgba(S, ti, false, uv, r); v.r = r[0]; v.g = r[1]; v.b = r[2]; } }
 
@@ -1350,6 +1397,7 @@ hipError_t launch_frame(const DevScene& S, const DevPaths& P, const MptFrame* d_
         hipMemsetAsync(&P.counters[CTR_FETCH], 0, sizeof(int32_t), st);
         TraceArgs ta{};
         ta.S = S; ta.P = P; ta.queue = q_cur; ta.count_ptr = &P.counters[c_cur]; ta.fetch = &P.counters[CTR_FETCH];
+        ta.F = d_frame; ta.bounce = b; ta.alpha = hf.render_settings.do_alpha_testing ? 1 : 0;
         timed_trace<TM_PATH>(ta, cfg, st);
         hipMemsetAsync(&P.counters[c_next], 0, sizeof(int32_t), st);
         hipMemsetAsync(&P.counters[CTR_ANY], 0, 2 * sizeof(int32_t), st);
@@ -1372,6 +1420,7 @@ hipError_t launch_frame(const DevScene& S, const DevPaths& P, const MptFrame* d_
         hipMemsetAsync(&P.counters[CTR_FETCH], 0, sizeof(int32_t), st);
         TraceArgs tn{};
         tn.S = S; tn.P = P; tn.count_ptr = &P.counters[CTR_ANY]; tn.fetch = &P.counters[CTR_FETCH];
+        tn.F = d_frame; tn.bounce = b; tn.alpha = ta.alpha;
         timed_trace<TM_NEE_ANY>(tn, cfg, st);
         hipMemsetAsync(&P.counters[CTR_FETCH], 0, sizeof(int32_t), st);
         tn.count_ptr = &P.counters[CTR_CL];

@@ -218,3 +218,44 @@ def procedural_city(seed: int = 1234, blocks: int = 17) -> SceneData:
     sd.camera_info = dict(position=np.array([cx, 1.7, half - 8.0]), lookat=np.array([cx + 0.8, 4.0, half - 60.0]),
                           up=np.array([0.0, 1.0, 0.0]), hfov=1.0, aspect=16 / 9, znear=0.1, zfar=1000.0)
     return sd.finalize()
+
+
+def with_alpha_cards(sd: SceneData, opacity: float = 0.5, tex_size: int = 16, alpha_levels=(0, 100, 255)) -> SceneData:
+    """Adds two alpha-tested cards to a scene (for do_alpha_testing, FilterFunction.h:19-48):
+    a textured card whose base-colour texture is a checkerboard of alpha levels (RGBA8),
+    and an untextured card with material alpha_opacity = ``opacity``.  Both stand
+    across the Cornell box's opening, so camera, NEE and envmap rays cross them."""
+    out = SceneData()
+    lo, hi = sd.vertices.min(0), sd.vertices.max(0)
+    c = (lo + hi) / 2
+    ext = (hi - lo) / 2
+    z1, z2 = hi[2] + 0.2 * ext[2], c[2] + 0.3 * ext[2]
+    x0, x1 = lo[0] + 0.1 * ext[0], hi[0] - 0.1 * ext[0]
+    y0, y1 = lo[1] + 0.1 * ext[1], hi[1] - 0.1 * ext[1]
+    cards_v = np.array([[x0, y0, z1], [c[0], y0, z1], [c[0], y1, z1], [x0, y1, z1],      # textured (left half)
+                        [c[0], y0, z2], [x1, y0, z2], [x1, y1, z2], [c[0], y1, z2]],     # opacity card (right half)
+                       np.float32)
+    cards_uv = np.array([[0, 0], [1, 0], [1, 1], [0, 1]] * 2, np.float32)
+    nv = len(sd.vertices)
+    cards_i = np.array([[0, 1, 2], [0, 2, 3], [4, 5, 6], [4, 6, 7]], np.int32) + nv
+    nm = len(sd.materials)
+    tm = abi.Material.from_buffer_copy(_mat((0.8, 0.3, 0.2), rough=0.5))
+    tm.base_color_texture_index = len(sd.textures)
+    om = abi.Material.from_buffer_copy(_mat((0.2, 0.4, 0.8), rough=0.3))
+    om.alpha_opacity = opacity
+    rng = np.random.default_rng(5)
+    tex = np.zeros((tex_size, tex_size, 4), np.uint8)
+    tex[..., :3] = rng.integers(64, 256, (tex_size, tex_size, 3))
+    yy, xx = np.meshgrid(np.arange(tex_size), np.arange(tex_size), indexing="ij")
+    tex[..., 3] = np.asarray(alpha_levels, np.uint8)[((yy // 4) + (xx // 4)) % len(alpha_levels)]
+    out.triangle_indices = np.concatenate([sd.triangle_indices.reshape(-1), cards_i.reshape(-1)]).astype(np.int32)
+    out.vertices = np.concatenate([sd.vertices, cards_v]).astype(np.float32)
+    out.normals = np.concatenate([sd.normals, np.zeros((8, 3), np.float32)]).astype(np.float32)
+    out.has_normals = np.concatenate([sd.has_normals, np.zeros(8, np.uint8)]).astype(np.uint8)
+    out.texcoords = np.concatenate([sd.texcoords, cards_uv]).astype(np.float32)
+    out.material_indices = np.concatenate([sd.material_indices, np.array([nm, nm, nm + 1, nm + 1], np.int32)])
+    out.materials = list(sd.materials) + [tm, om]
+    out.textures = list(sd.textures) + [tex]
+    out.camera_info = sd.camera_info
+    out.name = sd.name + "+alpha_cards"
+    return out.finalize()

@@ -225,8 +225,24 @@ inline bool box_hit(const BNode& n, const float o[3], const float inv[3], float 
     return t0 <= t1 && t1 >= 0.0f && t0 <= tbest;
 }
 
-// closest hit over the whole ray, skipping 'last_hit' (filter_function), ties -> lower prim
-Hit closest(const OScene& s, f3 o, f3 d, int last_hit) {
+// Alpha testing (filter_function, FilterFunction.h:19-48) with libmpt's order-independent
+// candidate uniforms: u = hash(query key, primitive), keep iff u < alpha_opacity *
+// base-colour alpha.  Same accept probability per candidate as the reference's RNG draw
+// inside HIPRT's traversal (whose stream depends on the traversal order, so no
+// implementation can reproduce it); see mpt_kernels.hip alpha_key / alpha_uniform.
+inline uint32_t alpha_key(uint32_t pixel_seed, int bounce, int kind, int iter) {
+    return wang_hash(pixel_seed ^ wang_hash((uint32_t)(bounce * 8 + kind) * 0x85EBCA77u + (uint32_t)iter * 0xC2B2AE3Du + 1u));
+}
+inline float alpha_uniform(uint32_t key, int prim) {
+    uint32_t h = wang_hash(key ^ ((uint32_t)prim * 0x9E3779B1u));
+    h = wang_hash(h + 0x7F4A7C15u);
+    return (float)(h >> 8) * (1.0f / 16777216.0f);
+}
+bool alpha_rejects(const OScene& s, int prim, float u, float v, uint32_t key);
+
+// closest hit over the whole ray, skipping 'last_hit' (filter_function), ties -> lower prim;
+// akey != NULL: alpha testing with that query key
+Hit closest(const OScene& s, f3 o, f3 d, int last_hit, const uint32_t* akey = nullptr) {
     Hit h;
     float best = FLT_MAX;
     float oo[3] = {o.x, o.y, o.z}, dd[3] = {d.x, d.y, d.z}, inv[3];
@@ -244,7 +260,10 @@ Hit closest(const OScene& s, f3 o, f3 d, int last_hit) {
                 float t, u, v;
                 if (!tri_intersect(s.tris[p], o, d, t, u, v)) continue;
                 if (p == last_hit) continue;
-                if (t < best || (t == best && p < h.prim)) { best = t; h.prim = p; h.t = t; h.u = u; h.v = v; }
+                if (t < best || (t == best && p < h.prim)) {
+                    if (akey && alpha_rejects(s, p, u, v, *akey)) continue;
+                    best = t; h.prim = p; h.t = t; h.u = u; h.v = v;
+                }
             }
         } else {
             float ta, tb;
@@ -274,6 +293,7 @@ struct Payload {
 struct ShadowLightHit { int prim = 0; float dist = 0; f3 shading_normal{0, 0, 0}; Col emission; };
 
 static thread_local int g_dbg = 0;
+inline uint32_t alpha_key(uint32_t pixel_seed, int bounce, int kind, int iter);
 struct Ctx {
     const OScene* s;
     const MptFrame* f;
@@ -281,6 +301,11 @@ struct Ctx {
     int override_;
     int lss;
     uint64_t rays_closest = 0, rays_any = 0;
+    // alpha testing: query keys are (pixel seed, bounce, kind, boundary-skip pass)
+    bool alpha = false;
+    uint32_t pseed = 0;
+    int bounce = 0;
+    uint32_t akey(int kind, int iter = 0) const { return alpha_key(pseed, bounce, kind, iter); }
 };
 
 inline Col emission_of(const Material& m) { return Col(m.emission.r, m.emission.g, m.emission.b) * m.emission_strength; }
@@ -300,6 +325,21 @@ template <>
 inline f3 uv_interp(const f3* d, const int32_t* idx, int p, f2 uv) {
     f3 A = d[idx[3 * p]], B = d[idx[3 * p + 1]], C = d[idx[3 * p + 2]];
     return B * uv.x + C * uv.y + A * (1.0f - uv.x - uv.y);
+}
+
+// get_hit_base_color_alpha (Material.h:23-37): the sRGB pow(2.2) also applies to alpha
+bool alpha_rejects(const OScene& s, int prim, float u, float v, uint32_t key) {
+    const Material& m = s.mats[s.mat_idx[prim]];
+    float a = 1.0f;
+    int ti = m.base_color_texture_index;
+    if (ti != MPT_NO_TEXTURE && ti != MPT_CONSTANT_EMISSIVE_TEXTURE) {
+        f2 tc = uv_interp(s.uv, s.idx, prim, mk2(u, v));
+        float r[4];
+        sample_texture_rgba(s.tex, ti, true, tc, r);
+        a = r[3];
+    }
+    float comp = m.alpha_opacity * a;
+    return !(alpha_uniform(key, prim) < comp);
 }
 
 // get_material_property (Device/includes/Material.h:140-159)
@@ -392,7 +432,8 @@ bool trace_ray(Ctx& c, f3 o, f3 d, Payload& pl, HitInfo& out, int last_hit, Rng&
     int skips = 0;
     do {
         c.rays_closest++;
-        h = closest(s, o, d, last_hit);
+        uint32_t ak = c.alpha ? c.akey(0, skips) : 0u;
+        h = closest(s, o, d, last_hit, c.alpha ? &ak : nullptr);
         if (h.prim < 0) return false;
         out.inter_point = o + h.t * d;
         out.prim = h.prim;
@@ -424,9 +465,11 @@ bool trace_ray(Ctx& c, f3 o, f3 d, Payload& pl, HitInfo& out, int last_hit, Rng&
 }
 
 // evaluate_shadow_ray (Intersect.h:224-286), CPU branch, alpha testing off
-bool shadow_ray(Ctx& c, f3 o, f3 d, float t_max, int last_hit) {
+// kind: 1 light sample, 2 envmap sample, 3 envmap BSDF sample (libmpt's staged query kinds + 1)
+bool shadow_ray(Ctx& c, f3 o, f3 d, float t_max, int last_hit, int kind) {
     c.rays_any++;
-    Hit h = closest(*c.s, o, d, last_hit);
+    uint32_t ak = c.alpha ? c.akey(kind) : 0u;
+    Hit h = closest(*c.s, o, d, last_hit, c.alpha ? &ak : nullptr);
     if (h.prim < 0) return false;
     return h.t < t_max - 1.0e-4f;
 }
@@ -435,7 +478,8 @@ bool shadow_ray(Ctx& c, f3 o, f3 d, float t_max, int last_hit) {
 bool shadow_light_ray(Ctx& c, f3 o, f3 d, float t_max, ShadowLightHit& out, int last_hit) {
     const OScene& s = *c.s;
     c.rays_closest++;
-    Hit h = closest(s, o, d, last_hit);
+    uint32_t ak = c.alpha ? c.akey(4) : 0u;
+    Hit h = closest(s, o, d, last_hit, c.alpha ? &ak : nullptr);
     if (h.prim < 0) return false;
     if (!(h.t < t_max - 1.0e-4f)) return false;
     const Material& m = s.mats[s.mat_idx[h.prim]];
@@ -508,7 +552,7 @@ Col sample_one_light_no_mis(Ctx& c, const Payload& pl, const HitInfo& hi, f3 vie
     f3 sdn = sd / dist;
     float dl = absf(dot(li.normal, -sdn));
     if (dl > 0.0f) {
-        if (!shadow_ray(c, so, sdn, dist, hi.prim)) {
+        if (!shadow_ray(c, so, sdn, dist, hi.prim, 1)) {
             float bp;
             VolumeState tv = pl.vs;
             Col bc = bsdf_eval(c.bc, c.override_, pl.material, tv, view, hi.shading_normal, hi.geometric_normal, sdn, bp);
@@ -559,7 +603,7 @@ Col sample_one_light_mis(Ctx& c, const Payload& pl, const HitInfo& hi, f3 view, 
     f3 sdn = sd / dist;
     float dl = absf(dot(li.normal, -sdn));
     if (dl > 0.0f) {
-        if (!shadow_ray(c, ep, sdn, dist, hi.prim)) {
+        if (!shadow_ray(c, ep, sdn, dist, hi.prim, 1)) {
             float bp;
             VolumeState tv = pl.vs;
             Col bc = bsdf_eval(c.bc, c.override_, pl.material, tv, view, hi.shading_normal, hi.geometric_normal, sdn, bp);
@@ -637,7 +681,7 @@ Col sample_lights_ris(Ctx& c, const Payload& pl, const HitInfo& hi, f3 view, Rng
                     target = enough ? lc.luminance() : 0.0f;
                 }
                 if (c.f->options.ris_use_visibility && target > 0.0f) {
-                    bool vis = !shadow_ray(c, ep, tl, dist, hi.prim);
+                    bool vis = !shadow_ray(c, ep, tl, dist, hi.prim, 1);
                     target *= vis ? 1.0f : 0.0f;
                 }
                 float w = balance_heuristic(lpdf, (float)nl, bp, (float)nb);
@@ -695,7 +739,7 @@ Col sample_lights_ris(Ctx& c, const Payload& pl, const HitInfo& hi, f3 view, Rng
     f3 sdn = sd / dist;
     bool shadowed;
     if (smp.is_bsdf) shadowed = false;
-    else shadowed = shadow_ray(c, ep2, sdn, dist, hi.prim);
+    else shadowed = shadow_ray(c, ep2, sdn, dist, hi.prim, 1);
     if (!shadowed) {
         float bp, ce;
         Col bc;
@@ -810,9 +854,9 @@ Col sample_environment_map(Ctx& c, const Payload& pl, const HitInfo& hi, f3 view
     Col ec = envmap_sample(c, sdir, epdf, rng);
     Col emis;
     float cosv = dot(hi.shading_normal, sdir);
-    if (g_dbg) printf("CPU env ec %a %a %a pdf %a dir %a %a %a cos %a ip %a %a %a prim %d occ %d\n", ec.r, ec.g, ec.b, epdf, sdir.x, sdir.y, sdir.z, cosv, hi.inter_point.x, hi.inter_point.y, hi.inter_point.z, hi.prim, (int)shadow_ray(c, hi.inter_point, sdir, 1.0e35f, hi.prim));
+    if (g_dbg) printf("CPU env ec %a %a %a pdf %a dir %a %a %a cos %a\n", ec.r, ec.g, ec.b, epdf, sdir.x, sdir.y, sdir.z, cosv);
     if (epdf > 0.0f && cosv > 0.0f) {
-        if (!shadow_ray(c, hi.inter_point, sdir, 1.0e35f, hi.prim)) {
+        if (!shadow_ray(c, hi.inter_point, sdir, 1.0e35f, hi.prim, 2)) {
             float bp;
             VolumeState tv = pl.vs;
             Col bc = bsdf_eval(c.bc, c.override_, pl.material, tv, view, hi.shading_normal, hi.geometric_normal, sdir, bp);
@@ -829,7 +873,7 @@ Col sample_environment_map(Ctx& c, const Payload& pl, const HitInfo& hi, f3 view
     Col bmis;
     cosv = absf(dot(hi.shading_normal, bd));
     if (bpdf > 0.0f) {
-        if (!shadow_ray(c, hi.inter_point, bd, 1.0e35f, hi.prim)) {
+        if (!shadow_ray(c, hi.inter_point, bd, 1.0e35f, hi.prim, 3)) {
             float ep;
             Col er = envmap_eval(c, bd, ep);
             if (ep > 0.0f) {
@@ -879,6 +923,9 @@ PixelOut render_pixel(Ctx& c, int x, int y, GB& gb) {
     const MptRenderSettings& rs = f.render_settings;
     uint32_t pix = (uint32_t)x + (uint32_t)y * (uint32_t)f.res_x;
     uint32_t seed = rs.freeze_random ? wang_hash(pix + 1u) : wang_hash((pix + 1u) * (uint32_t)(rs.sample_number + 1) * f.random_seed);
+    c.alpha = rs.do_alpha_testing;
+    c.pseed = seed;
+    c.bounce = 0;
     {   // ---- CameraRays
         Rng rng(seed);
         float xd = (float)x + 0.5f, yd = (float)y + 0.5f;
@@ -917,6 +964,7 @@ PixelOut render_pixel(Ctx& c, int x, int y, GB& gb) {
     const MptWorldSettings& w = f.world_settings;
     for (int bounce = 0; bounce < rs.nb_bounces + 1; bounce++) {
         if (pl.missed) break;
+        c.bounce = bounce;
         if (bounce > 0) found = trace_ray(c, ro, rd, pl, hi, hi.prim, rng);
         if (found) {
             if (bounce == 0) { dn += hi.shading_normal; albedo += C3(pl.material.base_color); }
@@ -1080,7 +1128,7 @@ int oracle_render(OracleScene* sc, const MptFrame* frames, int nframes, float* s
     if (nframes <= 0) return 0;
     const MptFrame& f0 = frames[0];
     if ((has_adaptive_buffers(f0.render_settings) && !(as_count && as_sqlum && as_conv && status)) ||
-        f0.render_settings.do_alpha_testing || f0.render_settings.wants_render_low_resolution ||
+        f0.render_settings.wants_render_low_resolution ||
         f0.options.direct_light_sampling == MPT_LSS_RESTIR_DI || f0.options.envmap_sampling == MPT_ESS_BINARY_SEARCH)
         return -4;
     std::vector<int> rows;
