@@ -2,12 +2,13 @@
 
 Workloads (BASELINE.json configs):
 * c3 (default; the configuration the metric is quoted on): the Bistro-exterior
-  stand-in -- a seeded procedural city of 2.84 M triangles (mpt/synthetic.py, seed
-  1234) under a seeded procedural HDR sky (2048x1024, alias-table sampling + BSDF MIS),
-  1920x1080, layered Principled BSDF, reference-default RIS light sampling; K = 256.
+  stand-in -- a seeded procedural city of 2.86 M triangles with alpha-tested leaf cards
+  (mpt/synthetic.py, seed 1234) under a seeded procedural HDR sky (2048x1024, alias-table
+  sampling + BSDF MIS), 1920x1080, layered Principled BSDF, reference-default RIS light
+  sampling, alpha testing on (C3 pins it for the foliage); K = 256.
 * c2: the Cornell box glTF at 1920x1080, Principled + NEE/MIS (LSS_MIS_LIGHT_BSDF); K = 64.
-Both: 3 bounces, reference defaults otherwise (adaptive sampling and alpha testing off,
-see DESIGN.md).  One *step* = one sample per pixel over the frame (one
+Both: 3 bounces, reference defaults otherwise (adaptive sampling off so that every step
+samples every pixel).  One *step* = one sample per pixel over the frame (one
 mpt_render_frame); K steps = the config's spp.  Multi-GPU: one process per GPU, the framebuffer is split into
 interleaved 8-row bands (each rank renders every N-th band), and the per-rank sum
 buffers are gathered with RCCL (all_gather over xGMI) inside the timed region.
@@ -52,7 +53,7 @@ def parse():
                     help="default: c3 ris (reference default), c2 mis")
     ap.add_argument("--bounces", type=int, default=3)
     ap.add_argument("--bsdf", default="principled", choices=["principled", "lambert"])
-    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration")
+    ap.add_argument("--cpu-seconds", type=float, default=20.0, help="target CPU-baseline sample duration")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
 
@@ -61,16 +62,17 @@ LSS = {"mis": abi.LSS_MIS_LIGHT_BSDF, "ris": abi.LSS_RIS_BSDF_AND_LIGHT, "unifor
        "bsdf": abi.LSS_BSDF}
 
 
-def frames_for(cam, W, H, opt, band, n, first=0, bounces=3, world=None):
+def frames_for(cam, W, H, opt, band, n, first=0, bounces=3, world=None, alpha=False):
     out = []
     for s, seed in scene.cpu_seed_schedule(n):
         st = scene.parity_settings(bounces)
+        st.do_alpha_testing = alpha
         out.append(scene.make_frame(cam, W, H, options=opt, settings=st, world=world, sample_number=s + first,
                                     random_seed=seed, band=band))
     return out
 
 
-def cpu_baseline(sd, luts, cam, W, H, opt, bounces, target_s, env=None, world=None):
+def cpu_baseline(sd, luts, cam, W, H, opt, bounces, target_s, env=None, world=None, alpha=False):
     """Oracle (CPU port) timed on a bounded sample of the same frame: a subset of the
     8-row bands at 1 spp, or the whole frame at several spp, sized to ~target_s."""
     sys.path.insert(0, ROOT)
@@ -79,7 +81,7 @@ def cpu_baseline(sd, luts, cam, W, H, opt, bounces, target_s, env=None, world=No
     o = orc.Oracle(sd, luts, envmap=env)
     bc = 64
     t0 = time.perf_counter()
-    o.render(frames_for(cam, W, H, opt, (BAND_H, 0, bc), 1, bounces=bounces, world=world), nthreads=cores)
+    o.render(frames_for(cam, W, H, opt, (BAND_H, 0, bc), 1, bounces=bounces, world=world, alpha=alpha), nthreads=cores)
     dt = max(time.perf_counter() - t0, 1e-3)
     scale = target_s / dt                       # multiples of the probe's work
     if scale >= bc:                             # whole frame, several spp
@@ -87,7 +89,8 @@ def cpu_baseline(sd, luts, cam, W, H, opt, bounces, target_s, env=None, world=No
     else:
         bc2, spp = max(1, int(round(bc / scale))), 1
     t0 = time.perf_counter()
-    o.render(frames_for(cam, W, H, opt, (BAND_H, 0, bc2), spp, bounces=bounces, world=world), nthreads=cores)
+    o.render(frames_for(cam, W, H, opt, (BAND_H, 0, bc2), spp, bounces=bounces, world=world, alpha=alpha),
+             nthreads=cores)
     dt = time.perf_counter() - t0
     rows = orc.mpt_rows(H, BAND_H, 0, bc2)
     rays = o.last_rays[0] + o.last_rays[1]
@@ -133,12 +136,15 @@ def main():
         wset = scene.envmap_world(1.0)
         strategy = a.strategy or "ris"
         K = a.steps or 256
-        desc = "C3 stand-in: procedural city (2.84 M tris, seed 1234) + procedural HDR sky 2048x1024"
+        alpha = True      # C3 pins do_alpha_testing = true (the Bistro's foliage)
+        desc = ("C3 stand-in: procedural city (2.86 M tris incl. alpha-tested leaf cards, seed 1234) + procedural "
+                "HDR sky 2048x1024, alpha testing on")
     else:
         sd = scene.load_scene(a.scene or "cornell_pbr")
         env, wset = None, None
         strategy = a.strategy or "mis"
         K = a.steps or 64
+        alpha = False
         desc = f"C2: {sd.name or a.scene or 'cornell_pbr'}"
     luts = scene.load_luts()
     cam = scene.make_camera(sd.camera_info, W, H)
@@ -156,14 +162,14 @@ def main():
 
     # calibration: instrumented traversal -> nodes / triangles per query per stage
     r.enable_stats(timing=False, instrumented=True)
-    for f in frames_for(cam, W, H, opt, band, 2, first=0, bounces=a.bounces, world=wset):
+    for f in frames_for(cam, W, H, opt, band, 2, first=0, bounces=a.bounces, world=wset, alpha=alpha):
         r.render(f)
     cal = r.stats()
     # warmup (untimed), then the timed K-frame accumulation restarting at sample 0
     r.enable_stats(timing=False, instrumented=False)
-    for f in frames_for(cam, W, H, opt, band, a.warmup, bounces=a.bounces, world=wset):
+    for f in frames_for(cam, W, H, opt, band, a.warmup, bounces=a.bounces, world=wset, alpha=alpha):
         r.render(f)
-    frames = frames_for(cam, W, H, opt, band, K, bounces=a.bounces, world=wset)
+    frames = frames_for(cam, W, H, opt, band, K, bounces=a.bounces, world=wset, alpha=alpha)
     r.synchronize_kernel()
     r.enable_stats(timing=True, instrumented=False)
 
@@ -245,7 +251,7 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         try:
-            cpu = cpu_baseline(sd, luts, cam, W, H, opt, a.bounces, a.cpu_seconds, env=env, world=wset)
+            cpu = cpu_baseline(sd, luts, cam, W, H, opt, a.bounces, a.cpu_seconds, env=env, world=wset, alpha=alpha)
         except Exception as e:  # the baseline is reported, never the product path
             cpu = {"value": None, "unit": "Mray/s", "cores": 0, "kind": "port", "sample": f"failed: {e}"}
 

@@ -86,7 +86,24 @@ def _icosphere(sub=2):
     return np.array(V), np.array(F, np.int64)
 
 
-def procedural_city(seed: int = 1234, blocks: int = 17) -> SceneData:
+def _leaf_texture(seed: int, size: int = 64) -> np.ndarray:
+    """RGBA8 leaf cluster: green shades, alpha 255 inside ~45 % of the texels (seeded
+    discs), 0 elsewhere -- the alpha-tested foliage of the Bistro (do_alpha_testing)."""
+    rng = np.random.default_rng(seed)
+    yy, xx = np.meshgrid(np.arange(size) + 0.5, np.arange(size) + 0.5, indexing="ij")
+    cover = np.zeros((size, size), bool)
+    for _ in range(14):
+        cx, cy, r = rng.uniform(0, size, 2).tolist() + [rng.uniform(0.08, 0.2) * size]
+        cover |= (xx - cx) ** 2 + (yy - cy) ** 2 < r * r
+    tex = np.zeros((size, size, 4), np.uint8)
+    tex[..., 0] = rng.integers(30, 70, (size, size))
+    tex[..., 1] = rng.integers(90, 160, (size, size))
+    tex[..., 2] = rng.integers(20, 50, (size, size))
+    tex[..., 3] = np.where(cover, 255, 0)
+    return tex
+
+
+def procedural_city(seed: int = 1234, blocks: int = 17, leaf_cards: int = 16) -> SceneData:
     rng = np.random.default_rng(seed)
     B = _Builder()
     mats = [
@@ -101,7 +118,9 @@ def procedural_city(seed: int = 1234, blocks: int = 17) -> SceneData:
         _mat((0.12, 0.3, 0.08), rough=0.95, specular=0.2),             # 8 foliage
         _mat((0.8, 0.8, 0.82), rough=0.3, metallic=1.0),               # 9 lamp metal
         _mat((1.0, 0.9, 0.7), emission=(1.0, 0.85, 0.6), strength=40.0),  # 10 lamp light
+        _mat((1.0, 1.0, 1.0), rough=0.9, specular=0.3),                # 11 leaf cards (alpha-tested texture 0)
     ]
+    mats[11].base_color_texture_index = 0
     blk, street = 40.0, 12.0
     pitch = blk + street
     half = blocks * pitch / 2.0
@@ -203,15 +222,32 @@ def procedural_city(seed: int = 1234, blocks: int = 17) -> SceneData:
     Nn = np.broadcast_to(SV[None], (len(tx),) + SV.shape).reshape(-1, 3)
     F = (SF[None, :, :] + (len(SV) * np.arange(len(tx)))[:, None, None]).reshape(-1, 3)
     B.mesh(V, Nn.copy(), F, 8)
+    # alpha-tested leaf cards around each crown (random orientation, uv 0..1 per card)
+    first_card_vertex = B.nv
+    if leaf_cards > 0:
+        nt, k = len(tx), leaf_cards
+        dirs = rng.normal(size=(nt, k, 3))
+        dirs /= np.linalg.norm(dirs, axis=-1, keepdims=True)
+        cc = ctr[:, None, :] + dirs * (tr[:, None, None] * rng.uniform(0.6, 1.2, (nt, k, 1)))
+        nrm = rng.normal(size=(nt, k, 3))
+        nrm /= np.linalg.norm(nrm, axis=-1, keepdims=True)
+        a = np.cross(nrm, np.array([0.0, 1.0, 0.0]))
+        a /= np.maximum(np.linalg.norm(a, axis=-1, keepdims=True), 1e-6)
+        b = np.cross(nrm, a)
+        hs = 0.6
+        c4 = [cc - hs * a - hs * b, cc + hs * a - hs * b, cc + hs * a + hs * b, cc - hs * a + hs * b]
+        B.quads(*[q.reshape(-1, 3) for q in c4], 11)
     sd = SceneData()
     sd.vertices = np.concatenate(B.v).astype(np.float32)
     sd.normals = np.concatenate(B.n).astype(np.float32)
     sd.has_normals = np.concatenate(B.hn).astype(np.uint8)
     sd.texcoords = np.zeros((len(sd.vertices), 2), np.float32)
+    ncard_v = len(sd.vertices) - first_card_vertex
+    sd.texcoords[first_card_vertex:] = np.tile(np.array([[0, 0], [1, 0], [1, 1], [0, 1]], np.float32), (ncard_v // 4, 1))
     sd.triangle_indices = np.concatenate(B.idx).astype(np.int32).ravel()
     sd.material_indices = np.concatenate(B.mi).astype(np.int32)
     sd.materials = mats
-    sd.textures = []
+    sd.textures = [_leaf_texture(seed)]
     sd.name = f"procedural_city_{seed}"
     # street-level camera at an intersection looking down a street, slightly up
     cx = -half + street / 2 + (blocks // 2) * pitch - street / 2

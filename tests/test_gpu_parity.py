@@ -241,13 +241,15 @@ def city():
     return synthetic.procedural_city(1234)
 
 
-@pytest.mark.parametrize("strategy", ["ris", "mis"])
+@pytest.mark.parametrize("strategy", ["ris", "ris_alpha", "mis"])
 def test_render_city_stand_in_bit_exact(city, luts, strategy):
-    """The bench workload (C3 stand-in: 2.84 M triangles, HDR sky with alias-table
-    sampling + BSDF MIS) on a band subset of the 1920x1080 frame."""
+    """The bench workload (C3 stand-in: 2.86 M triangles, alpha-tested leaf cards, HDR
+    sky with alias-table sampling + BSDF MIS) on a band subset of the 1920x1080 frame."""
     env = mpt.build_envmap(scene.procedural_sky(512, 256, seed=7))
     band = (8, 5, 48)
-    frs = frames(city, 1920, 1080, 2, lss=STRATEGIES[strategy], world=scene.envmap_world(1.0), band=band)
+    frs = frames(city, 1920, 1080, 2, lss=STRATEGIES[strategy.split("_")[0]], world=scene.envmap_world(1.0), band=band)
+    for f in frs:
+        f.render_settings.do_alpha_testing = strategy.endswith("alpha")
     g = gpu_render(renderer(city, luts, env), frs)
     c = oracle_for(city, luts, env).render(frs, aov=True)
     for k, what in enumerate(["color", "albedo", "normals"]):
