@@ -87,6 +87,8 @@ struct MptContext {
     DBuf<float4> env;
     DBuf<float> alias_p;
     DBuf<int32_t> alias_i;
+    DBuf<float> env_cdf;
+    float env_cdf_sum = 0.0f;
     int env_w = 0, env_h = 0;
     float env_sum = 0.0f;
     // paths
@@ -166,6 +168,8 @@ DevScene dev_scene(MptContext* c) {
     S.env_w = c->env_w;
     S.env_h = c->env_h;
     S.env_sum = c->env_sum;
+    S.env_cdf = c->env_cdf.p;
+    S.env_cdf_sum = c->env_cdf_sum;
     return S;
 }
 
@@ -296,7 +300,6 @@ int validate_frame(const MptFrame* f) {
     int lss = f->options.direct_light_sampling;
     if (lss < 0 || lss > MPT_LSS_RESTIR_DI) return fail(MPT_ERR_INVALID_ARGUMENT, "bad direct_light_sampling");
     if (lss == MPT_LSS_RESTIR_DI) return fail(MPT_ERR_UNSUPPORTED, "ReSTIR DI not implemented yet");
-    if (f->options.envmap_sampling == MPT_ESS_BINARY_SEARCH) return fail(MPT_ERR_UNSUPPORTED, "ESS_BINARY_SEARCH not implemented");
     if (f->options.bsdf_override != MPT_BSDF_NONE && f->options.bsdf_override != MPT_BSDF_LAMBERTIAN)
         return fail(MPT_ERR_UNSUPPORTED, "only BSDF_NONE (Principled) and BSDF_LAMBERTIAN are implemented");
     if (f->options.ris_use_visibility) return fail(MPT_ERR_UNSUPPORTED, "RISUseVisiblityTargetFunction not implemented");
@@ -533,7 +536,7 @@ int mpt_set_envmap(MptContext* c, const float* rgba, int32_t w, int32_t h, const
     if (!c) return fail(MPT_ERR_INVALID_ARGUMENT, "NULL context");
     HIPCHK(hipSetDevice(c->device));
     if (!rgba || w <= 0 || h <= 0) {
-        c->env.release(); c->alias_p.release(); c->alias_i.release();
+        c->env.release(); c->alias_p.release(); c->alias_i.release(); c->env_cdf.release();
         c->env_w = c->env_h = 0;
         return MPT_OK;
     }
@@ -553,6 +556,33 @@ int mpt_set_envmap(MptContext* c, const float* rgba, int32_t w, int32_t h, const
     c->env_w = w;
     c->env_h = h;
     c->env_sum = lsum;
+    c->env_cdf.release();   // a new envmap invalidates a previous CDF
+    return MPT_OK;
+}
+
+int mpt_build_envmap_cdf(const float* rgba, int32_t w, int32_t h, float* out_cdf, float* out_sum) {
+    // Image32Bit::compute_cdf (Image/Image.cpp:553-574): float running sum of the texel
+    // luminances in row-major order; the total is the last element (OrochiEnvmap.cpp:30-38)
+    if (!rgba || w <= 0 || h <= 0 || !out_cdf) return fail(MPT_ERR_INVALID_ARGUMENT, "bad CDF arguments");
+    const float wts[3] = {0.3086f, 0.6094f, 0.0820f};
+    size_t n = (size_t)w * h;
+    out_cdf[0] = 0.0f;
+    for (size_t i = 0; i < n; i++) {
+        float l = 0.0f;
+        for (int k = 0; k < 3; k++) l += rgba[4 * i + k] * wts[k];
+        out_cdf[i] = out_cdf[i > 0 ? i - 1 : 0] + l;
+    }
+    if (out_sum) *out_sum = out_cdf[n - 1];
+    return MPT_OK;
+}
+
+int mpt_set_envmap_cdf(MptContext* c, const float* cdf, float total_sum) {
+    if (!c || !cdf) return fail(MPT_ERR_INVALID_ARGUMENT, "NULL argument");
+    if (!c->env.p) return fail(MPT_ERR_INVALID_ARGUMENT, "mpt_set_envmap first");
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(c->env_cdf.upload(cdf, (size_t)c->env_w * c->env_h, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    c->env_cdf_sum = total_sum;
     return MPT_OK;
 }
 
@@ -585,6 +615,9 @@ int mpt_render_frame(MptContext* c, const MptFrame* f) {
     if (v != MPT_OK) return v;
     if (f->world_settings.ambient_light_type == MPT_AMBIENT_ENVMAP && !c->env.p)
         return fail(MPT_ERR_INVALID_ARGUMENT, "ENVMAP ambient light without mpt_set_envmap");
+    if (f->world_settings.ambient_light_type == MPT_AMBIENT_ENVMAP && f->options.envmap_sampling == MPT_ESS_BINARY_SEARCH &&
+        !c->env_cdf.p)
+        return fail(MPT_ERR_INVALID_ARGUMENT, "ESS_BINARY_SEARCH without mpt_set_envmap_cdf");
     HIPCHK(hipSetDevice(c->device));
     int r = ensure_paths(c, f->res_x, f->res_y, f->band_height, f->band_index, f->band_count);
     if (r != MPT_OK) return r;

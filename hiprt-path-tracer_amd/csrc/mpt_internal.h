@@ -51,6 +51,8 @@ struct DevScene {
     const int32_t* alias_i;
     int32_t env_w, env_h;
     float env_sum;
+    const float* env_cdf;         // ESS_BINARY_SEARCH: running luminance sum per texel (Image.cpp:553-574)
+    float env_cdf_sum;            // its last element (OrochiEnvmap::compute_cdf)
 };
 
 // NEE record written by the shade stage and consumed by the resolve stage (128 B / slot)

@@ -620,19 +620,47 @@ DEV Col eval_env_no_pdf(const DevScene& S, const MptFrame& F, v3 d) {
     float v = 0.5f + pasin(r.y) * INV_PI;
     return env_tex(S, F, mk2(u, 1.0f - v));
 }
+// envmap_cdf_search (Envmap.h:40-75): row by the last column, then the texel in the row
+DEV void env_cdf_search(const DevScene& S, float value, int& x, int& y) {
+    unsigned lower = 0;
+    int upper = S.env_h - 1;
+    int xi = S.env_w - 1;
+    while (lower < (unsigned)upper) {
+        int yi = (int)((lower + (unsigned)upper) / 2u);
+        if (value < S.env_cdf[yi * S.env_w + xi]) upper = yi;
+        else lower = (unsigned)yi + 1u;
+    }
+    y = (int)(lower < (unsigned)S.env_h ? lower : (unsigned)S.env_h);
+    lower = 0;
+    upper = S.env_w - 1;
+    while (lower < (unsigned)upper) {
+        int xm = (int)((lower + (unsigned)upper) / 2u);
+        if (value < S.env_cdf[y * S.env_w + xm]) upper = xm;
+        else lower = (unsigned)xm + 1u;
+    }
+    x = (int)(lower < (unsigned)S.env_w ? lower : (unsigned)S.env_w);
+}
+DEV float env_total(const DevScene& S, const MptFrame& F) {
+    return F.options.envmap_sampling == MPT_ESS_BINARY_SEARCH ? S.env_cdf_sum : S.env_sum;
+}
 DEV Col env_sample(const DevScene& S, const MptFrame& F, v3& dir, float& pdf, Rng& rng) {
-    int ri = rng.random_index(S.env_h * S.env_w);
-    float prob = S.alias_p[ri];
-    if (rng() > prob) ri = S.alias_i[ri];
-    int y = (int)((unsigned)ri / (unsigned)S.env_w);
-    int x = ri - y * S.env_w;
+    int x, y;
+    if (F.options.envmap_sampling == MPT_ESS_BINARY_SEARCH) {
+        env_cdf_search(S, rng() * S.env_cdf_sum, x, y);
+    } else {
+        int ri = rng.random_index(S.env_h * S.env_w);
+        float prob = S.alias_p[ri];
+        if (rng() > prob) ri = S.alias_i[ri];
+        y = (int)((unsigned)ri / (unsigned)S.env_w);
+        x = ri - y * S.env_w;
+    }
     float u = (float)x / (float)(unsigned)S.env_w, v = (float)y / (float)(unsigned)S.env_h;
     float phi = u * TWO_PI;
     float theta = maxr(1.0e-5f, v * PI);
     float ct = pcos(theta), st = psin(theta);
     dir = mat_x_vec(F.world_settings.envmap_to_world_matrix.m, mk3(-st * pcos(phi), -ct, -st * psin(phi)));
     Col rad = env_tex(S, F, mk2(u, 1.0f - v));
-    pdf = lum(rad) / (S.env_sum * F.world_settings.envmap_intensity);
+    pdf = lum(rad) / (env_total(S, F) * F.world_settings.envmap_intensity);
     pdf *= (float)((unsigned)S.env_w * (unsigned)S.env_h);
     pdf /= (TWO_PIPI * st);
     return rad;
@@ -640,7 +668,7 @@ DEV Col env_sample(const DevScene& S, const MptFrame& F, v3& dir, float& pdf, Rn
 DEV Col env_eval(const DevScene& S, const MptFrame& F, v3 d, float& pdf) {
     Col rad = eval_env_no_pdf(S, F, d);
     float st = psin(pacos(-d.y));
-    pdf = lum(rad) / (S.env_sum * F.world_settings.envmap_intensity);
+    pdf = lum(rad) / (env_total(S, F) * F.world_settings.envmap_intensity);
     pdf *= (float)((unsigned)S.env_w * (unsigned)S.env_h);
     pdf /= (TWO_PIPI * st);
     return rad;

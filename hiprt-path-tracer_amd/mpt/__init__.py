@@ -28,7 +28,7 @@ SYMBOLS = [
     "mpt_update_materials", "mpt_set_envmap", "mpt_build_alias_table", "mpt_set_luts", "mpt_resize",
     "mpt_render_frame", "mpt_synchronize", "mpt_query_done", "mpt_get_framebuffer", "mpt_partition_rows",
     "mpt_enable_stats", "mpt_get_stats", "mpt_trace_closest", "mpt_trace_any", "mpt_clear_status",
-    "mpt_query_status", "mpt_get_aux_buffer",
+    "mpt_query_status", "mpt_get_aux_buffer", "mpt_build_envmap_cdf", "mpt_set_envmap_cdf",
 ]
 
 
@@ -70,6 +70,8 @@ def lib() -> C.CDLL:
     L.mpt_get_stats.argtypes = [vp, C.POINTER(abi.Stats)]
     L.mpt_trace_closest.argtypes = [vp, vp, vp, i32, vp, vp, vp, vp, C.c_int]
     L.mpt_trace_any.argtypes = [vp, vp, vp, i32, vp, C.c_int]
+    L.mpt_build_envmap_cdf.argtypes = [vp, i32, i32, vp, vp]
+    L.mpt_set_envmap_cdf.argtypes = [vp, vp, f32]
     L.mpt_clear_status.argtypes = [vp]
     L.mpt_query_status.argtypes = [vp, C.POINTER(abi.Status)]
     L.mpt_get_aux_buffer.argtypes = [vp, C.c_int, vp, C.c_int]
@@ -106,7 +108,12 @@ def build_envmap(rgba):
     s = np.zeros(1, np.float32)
     _check(lib().mpt_build_alias_table(_p(rgba), w, h, _p(probas), _p(alias), _p(s)))
     alias = np.where(alias < 0, np.arange(h * w, dtype=np.int32), alias).astype(np.int32)
-    return {"rgba": rgba, "probas": probas, "alias": alias, "width": w, "height": h, "sum": float(s[0])}
+    # ESS_BINARY_SEARCH: luminance CDF, Image32Bit::compute_cdf (Image.cpp:553-574)
+    cdf = np.zeros(h * w, np.float32)
+    cs = np.zeros(1, np.float32)
+    _check(lib().mpt_build_envmap_cdf(_p(rgba), w, h, _p(cdf), _p(cs)))
+    return {"rgba": rgba, "probas": probas, "alias": alias, "width": w, "height": h, "sum": float(s[0]),
+            "cdf": cdf, "cdf_sum": float(cs[0])}
 
 
 class GPURenderer:
@@ -140,6 +147,8 @@ class GPURenderer:
         self._env = env
         _check(lib().mpt_set_envmap(self.h, _p(env["rgba"]), env["width"], env["height"], _p(env["probas"]),
                                     _p(env["alias"]), env["sum"]))
+        if env.get("cdf") is not None:
+            _check(lib().mpt_set_envmap_cdf(self.h, _p(env["cdf"]), env["cdf_sum"]))
 
     def set_luts(self, luts=None):
         luts = luts if luts is not None else scene.load_luts()

@@ -410,6 +410,10 @@ int mpt_set_envmap(MptContext* ctx, const float* rgba, int32_t width, int32_t he
 /* Vose alias table in double precision, Image32Bit::compute_alias_table (Image/Image.cpp:579-659) */
 int mpt_build_alias_table(const float* rgba, int32_t width, int32_t height,
                           float* out_probas, int32_t* out_alias, float* out_luminance_sum);
+/* ESS_BINARY_SEARCH: the envmap luminance CDF, Image32Bit::compute_cdf (Image/Image.cpp:553-574),
+ * and its upload (GPURenderer::set_envmap / RendererEnvmap.cpp:119-125; total = last element) */
+int mpt_build_envmap_cdf(const float* rgba, int32_t width, int32_t height, float* out_cdf, float* out_total_sum);
+int mpt_set_envmap_cdf(MptContext* ctx, const float* cdf, float total_sum);
 int mpt_set_luts(MptContext* ctx, const MptLuts* luts);
 int mpt_resize(MptContext* ctx, int32_t width, int32_t height);
 /* Renders one sample per pixel of the context's partition, accumulating into the

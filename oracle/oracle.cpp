@@ -74,6 +74,8 @@ struct OScene {
     const float* alias_p;
     const int32_t* alias_i;
     float env_sum;
+    const float* env_cdf = nullptr;   // ESS_BINARY_SEARCH
+    float env_cdf_sum = 0.0f;
     std::vector<Tri> tris;
     std::vector<BNode> nodes;
     std::vector<int> order;
@@ -812,14 +814,42 @@ inline Col eval_envmap_no_pdf(const Ctx& c, f3 d) {
     float v = 0.5f + pasin(r.y) * INV_PI;
     return env_texture(c, mk2(u, 1.0f - v));
 }
+// envmap_cdf_search (Envmap.h:40-75)
+inline void envmap_cdf_search(const OScene& s, float value, int& x, int& y) {
+    unsigned int lower = 0;
+    int upper = s.env_h - 1;
+    int x_index = s.env_w - 1;
+    while (lower < (unsigned)upper) {
+        int y_index = (int)((lower + (unsigned)upper) / 2);
+        if (value < s.env_cdf[y_index * s.env_w + x_index]) upper = y_index;
+        else lower = y_index + 1;
+    }
+    y = (int)std::max(std::min(lower, (unsigned)s.env_h), 0u);
+    lower = 0;
+    upper = s.env_w - 1;
+    while (lower < (unsigned)upper) {
+        int x_idx = (int)((lower + (unsigned)upper) / 2);
+        if (value < s.env_cdf[y * s.env_w + x_idx]) upper = x_idx;
+        else lower = x_idx + 1;
+    }
+    x = (int)std::max(std::min(lower, (unsigned)s.env_w), 0u);
+}
+inline float env_total(const Ctx& c) {
+    return c.f->options.envmap_sampling == MPT_ESS_BINARY_SEARCH ? c.s->env_cdf_sum : c.s->env_sum;
+}
 inline Col envmap_sample(const Ctx& c, f3& dir, float& pdf, Rng& rng) {
     const OScene& s = *c.s;
     const MptWorldSettings& w = c.f->world_settings;
-    int ri = rng.random_index(s.env_h * s.env_w);
-    float prob = s.alias_p[ri];
-    if (rng() > prob) ri = s.alias_i[ri];
-    int y = (int)((unsigned)ri / (unsigned)s.env_w);
-    int x = ri - y * s.env_w;
+    int x, y;
+    if (c.f->options.envmap_sampling == MPT_ESS_BINARY_SEARCH) {
+        envmap_cdf_search(s, rng() * s.env_cdf_sum, x, y);
+    } else {
+        int ri = rng.random_index(s.env_h * s.env_w);
+        float prob = s.alias_p[ri];
+        if (rng() > prob) ri = s.alias_i[ri];
+        y = (int)((unsigned)ri / (unsigned)s.env_w);
+        x = ri - y * s.env_w;
+    }
     float u = (float)x / (float)(unsigned)s.env_w, v = (float)y / (float)(unsigned)s.env_h;
     float phi = u * TWO_PI;
     float theta = fmaxr(1.0e-5f, v * PI);
@@ -827,7 +857,7 @@ inline Col envmap_sample(const Ctx& c, f3& dir, float& pdf, Rng& rng) {
     dir = mk3(-st * pcos(phi), -ct, -st * psin(phi));
     dir = mat_x_vec(w.envmap_to_world_matrix, dir);
     Col rad = env_texture(c, mk2(u, 1.0f - v));
-    pdf = rad.luminance() / (s.env_sum * w.envmap_intensity);
+    pdf = rad.luminance() / (env_total(c) * w.envmap_intensity);
     pdf *= (float)((unsigned)s.env_w * (unsigned)s.env_h);
     pdf /= (TWO_PIPI * st);
     return rad;
@@ -837,7 +867,7 @@ inline Col envmap_eval(const Ctx& c, f3 d, float& pdf) {
     Col rad = eval_envmap_no_pdf(c, d);
     float th = pacos(-d.y);
     float st = psin(th);
-    pdf = rad.luminance() / (s.env_sum * c.f->world_settings.envmap_intensity);
+    pdf = rad.luminance() / (env_total(c) * c.f->world_settings.envmap_intensity);
     pdf *= (float)((unsigned)s.env_w * (unsigned)s.env_h);
     pdf /= (TWO_PIPI * st);
     return rad;
@@ -1063,6 +1093,12 @@ OracleScene* oracle_create(const MptScene* sc, const MptLuts* luts, const float*
     return reinterpret_cast<OracleScene*>(s);
 }
 
+void oracle_set_envmap_cdf(OracleScene* sc, const float* cdf, float total_sum) {
+    OScene* s = reinterpret_cast<OScene*>(sc);
+    s->env_cdf = cdf;
+    s->env_cdf_sum = total_sum;
+}
+
 void oracle_destroy(OracleScene* s) { delete reinterpret_cast<OScene*>(s); }
 
 int oracle_trace_closest(OracleScene* sc, const float* rays, const int32_t* last_hit, int n, int32_t* prim, float* t, float* u, float* v) {
@@ -1129,7 +1165,8 @@ int oracle_render(OracleScene* sc, const MptFrame* frames, int nframes, float* s
     const MptFrame& f0 = frames[0];
     if ((has_adaptive_buffers(f0.render_settings) && !(as_count && as_sqlum && as_conv && status)) ||
         f0.render_settings.wants_render_low_resolution ||
-        f0.options.direct_light_sampling == MPT_LSS_RESTIR_DI || f0.options.envmap_sampling == MPT_ESS_BINARY_SEARCH)
+        f0.options.direct_light_sampling == MPT_LSS_RESTIR_DI ||
+        (f0.options.envmap_sampling == MPT_ESS_BINARY_SEARCH && s.env_rgba && !s.env_cdf))
         return -4;
     std::vector<int> rows;
     for (int y = 0; y < f0.res_y; y++)

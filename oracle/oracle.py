@@ -40,6 +40,7 @@ def lib():
         L.oracle_create.argtypes = [C.POINTER(abi.Scene), C.POINTER(abi.Luts), C.c_void_p, C.c_int, C.c_int,
                                     C.c_void_p, C.c_void_p, C.c_float]
         L.oracle_destroy.argtypes = [C.c_void_p]
+        L.oracle_set_envmap_cdf.argtypes = [C.c_void_p, C.c_void_p, C.c_float]
         L.oracle_trace_closest.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p,
                                            C.c_void_p, C.c_void_p]
         L.oracle_render.argtypes = [C.c_void_p, C.POINTER(abi.Frame), C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
@@ -79,6 +80,9 @@ class Oracle:
         else:
             ptrs = (None, 0, 0, None, None, 0.0)
         self.h = lib().oracle_create(C.byref(self._abi_scene), C.byref(self._abi_luts), *ptrs)
+        if envmap is not None and envmap.get("cdf") is not None:
+            self._cdf = np.ascontiguousarray(envmap["cdf"], np.float32)
+            lib().oracle_set_envmap_cdf(self.h, _p(self._cdf), envmap["cdf_sum"])
 
     def close(self):
         if self.h:

@@ -128,3 +128,17 @@ def test_alias_table_matches_vose_restatement(shape, seed):
         prob[env["alias"][i]] += (1.0 - env["probas"][i]) / n
     lum = (rgba[..., :3] @ np.array([0.3086, 0.6094, 0.0820])).ravel()
     assert np.allclose(prob, lum / lum.sum(), atol=1e-6)
+
+
+@pytest.mark.parametrize("shape,seed", [((8, 16), 0), ((5, 7), 2)])
+def test_envmap_cdf_matches_restatement(shape, seed):
+    """Image32Bit::compute_cdf (Image.cpp:553-574): float32 running sum of the texel
+    luminances ((0 + r w0) + g w1) + b w2, row-major; total = last element."""
+    rng = np.random.default_rng(seed)
+    rgba = np.concatenate([rng.random(shape + (3,)) ** 3 * 10, np.ones(shape + (1,))], -1).astype(np.float32)
+    env = mpt.build_envmap(rgba)
+    f = np.float32
+    lum = ((f(0) + rgba[..., 0] * f(0.3086)).astype(f) + rgba[..., 1] * f(0.6094)).astype(f) + rgba[..., 2] * f(0.0820)
+    cdf = np.add.accumulate(lum.astype(f).ravel(), dtype=f)
+    assert np.array_equal(env["cdf"], cdf)
+    assert env["cdf_sum"] == cdf[-1]

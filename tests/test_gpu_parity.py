@@ -174,7 +174,8 @@ def test_render_dielectric_scenes_bit_exact(scenes, luts, name, bounces, strateg
 
 
 @pytest.mark.parametrize("strategy,env_mis,ess", [("mis", 1, abi.ESS_ALIAS_TABLE), ("ris", 1, abi.ESS_ALIAS_TABLE),
-                                                  ("mis", 0, abi.ESS_ALIAS_TABLE), ("mis", 1, abi.ESS_NO_SAMPLING)])
+                                                  ("mis", 0, abi.ESS_ALIAS_TABLE), ("mis", 1, abi.ESS_NO_SAMPLING),
+                                                  ("mis", 1, abi.ESS_BINARY_SEARCH), ("ris", 0, abi.ESS_BINARY_SEARCH)])
 def test_render_envmap_bit_exact(scenes, luts, sky, strategy, env_mis, ess):
     sd = scenes["nested-dielectrics"]
     W, H = 40, 30
