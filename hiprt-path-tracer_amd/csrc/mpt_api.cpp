@@ -104,6 +104,13 @@ struct MptContext {
     DBuf<float> as_sqlum;
     DBuf<uint8_t> active;
     DBuf<uint32_t> status;
+    // ReSTIR DI (allocated on the first LSS_RESTIR_DI frame)
+    DBuf<float4> gb_pos, gb_sn, gb_gn, gb_view, pgb_pos, pgb_sn, pgb_gn, pgb_view;
+    DBuf<int4> gb_meta, pgb_meta;
+    DBuf<uint4> gb_vsA, gb_vsB, pgb_vsA, pgb_vsB;
+    DBuf<MptMaterial> gb_mat, pgb_mat;
+    DBuf<float4> rs_init, rs_sp1, rs_sp2, rs_plights;
+    int restir_out_sp2 = 0;
     DBuf<MptMaterial> mat_slot;
     DBuf<uint64_t> stats;
     DBuf<uint64_t> ray_counts;
@@ -210,6 +217,13 @@ DevPaths dev_paths(MptContext* c) {
     P.as_conv = c->as_conv.p;
     P.active = c->active.p;
     P.status = c->status.p;
+    P.gb_pos = c->gb_pos.p; P.gb_sn = c->gb_sn.p; P.gb_gn = c->gb_gn.p; P.gb_view = c->gb_view.p; P.gb_meta = c->gb_meta.p;
+    P.gb_vsA = c->gb_vsA.p; P.gb_vsB = c->gb_vsB.p; P.gb_mat = c->gb_mat.p;
+    P.pgb_pos = c->pgb_pos.p; P.pgb_sn = c->pgb_sn.p; P.pgb_gn = c->pgb_gn.p; P.pgb_view = c->pgb_view.p; P.pgb_meta = c->pgb_meta.p;
+    P.pgb_vsA = c->pgb_vsA.p; P.pgb_vsB = c->pgb_vsB.p; P.pgb_mat = c->pgb_mat.p;
+    P.rs_init = c->rs_init.p; P.rs_sp1 = c->rs_sp1.p; P.rs_sp2 = c->rs_sp2.p; P.rs_plights = c->rs_plights.p;
+    P.rs_out = c->restir_out_sp2 ? c->rs_sp2.p : c->rs_sp1.p;
+    P.rs_tin = P.rs_out;
     return P;
 }
 
@@ -271,6 +285,42 @@ int upload_alpha_flags(MptContext* c) {
     return MPT_OK;
 }
 
+// ReSTIR DI buffers (ReSTIRDIRenderPass::update / resize, ReSTIRDIRenderPass.cpp:130-205): the
+// G-buffer pair, three reservoir buffers reset to empty reservoirs, the presampled lights.
+// Zero-filled G-buffers decode as "never written" (see restir_di.h gb_surface).
+int ensure_restir(MptContext* c, const MptFrame* f) {
+    size_t N = (size_t)std::max(c->n_slots, 1);
+    const MptReSTIRDISettings& rd = f->render_settings.restir_di_settings;
+    size_t npl = (size_t)std::max(1, rd.number_of_subsets * rd.subset_size);
+    hipStream_t st = c->stream;
+    if (c->rs_init.n != 3 * N) {
+        HIPCHK(c->gb_pos.alloc(N)); HIPCHK(c->gb_sn.alloc(N)); HIPCHK(c->gb_gn.alloc(N)); HIPCHK(c->gb_view.alloc(N));
+        HIPCHK(c->pgb_pos.alloc(N)); HIPCHK(c->pgb_sn.alloc(N)); HIPCHK(c->pgb_gn.alloc(N)); HIPCHK(c->pgb_view.alloc(N));
+        HIPCHK(c->gb_meta.alloc(N)); HIPCHK(c->pgb_meta.alloc(N));
+        HIPCHK(c->gb_vsA.alloc(N)); HIPCHK(c->gb_vsB.alloc(N)); HIPCHK(c->pgb_vsA.alloc(N)); HIPCHK(c->pgb_vsB.alloc(N));
+        HIPCHK(c->rs_init.alloc(3 * N)); HIPCHK(c->rs_sp1.alloc(3 * N)); HIPCHK(c->rs_sp2.alloc(3 * N));
+        for (DBuf<float4>* b : {&c->gb_pos, &c->gb_sn, &c->gb_gn, &c->gb_view, &c->pgb_pos, &c->pgb_sn, &c->pgb_gn, &c->pgb_view})
+            HIPCHK(hipMemsetAsync(b->p, 0, N * sizeof(float4), st));
+        HIPCHK(hipMemsetAsync(c->gb_meta.p, 0, N * sizeof(int4), st));
+        HIPCHK(hipMemsetAsync(c->pgb_meta.p, 0, N * sizeof(int4), st));
+        for (DBuf<uint4>* b : {&c->gb_vsA, &c->gb_vsB, &c->pgb_vsA, &c->pgb_vsB})
+            HIPCHK(hipMemsetAsync(b->p, 0, N * sizeof(uint4), st));
+        HIPCHK(launch_restir_fill(c->rs_init.p, (int)N, st));
+        HIPCHK(launch_restir_fill(c->rs_sp1.p, (int)N, st));
+        HIPCHK(launch_restir_fill(c->rs_sp2.p, (int)N, st));
+        c->restir_out_sp2 = 0;
+    }
+    if ((c->any_tex || f->bsdf_flags.white_furnace_mode) && c->gb_mat.n < N) {
+        HIPCHK(c->gb_mat.alloc(N));
+        HIPCHK(c->pgb_mat.alloc(N));
+    }
+    if (c->rs_plights.n != 4 * npl) {
+        HIPCHK(c->rs_plights.alloc(4 * npl));
+        HIPCHK(launch_restir_fill_lights(c->rs_plights.p, (int)npl, st));
+    }
+    return MPT_OK;
+}
+
 int resolve_materials(MptContext* c) {
     size_t n = c->h_mats.size();
     HIPCHK(c->mats_res.alloc(n));
@@ -299,7 +349,21 @@ int validate_frame(const MptFrame* f) {
     if (rs.ris_number_of_light_candidates < 0) return fail(MPT_ERR_INVALID_ARGUMENT, "negative RIS light candidates");
     int lss = f->options.direct_light_sampling;
     if (lss < 0 || lss > MPT_LSS_RESTIR_DI) return fail(MPT_ERR_INVALID_ARGUMENT, "bad direct_light_sampling");
-    if (lss == MPT_LSS_RESTIR_DI) return fail(MPT_ERR_UNSUPPORTED, "ReSTIR DI not implemented yet");
+    if (lss == MPT_LSS_RESTIR_DI) {
+        const MptReSTIRDISettings& rd = rs.restir_di_settings;
+        if (f->band_count != 1)
+            return fail(MPT_ERR_UNSUPPORTED, "ReSTIR DI reuses neighbouring pixels: render the whole frame per context (band_count 1)");
+        if (!rd.do_fused_spatiotemporal)
+            return fail(MPT_ERR_UNSUPPORTED, "ReSTIR DI: only the fused spatiotemporal configuration (the reference default)");
+        if (rd.number_of_passes < 1 || rd.number_of_passes > 5)
+            return fail(MPT_ERR_UNSUPPORTED, "ReSTIR DI: number_of_passes must be in [1, 5] (restir_di_seeds)");
+        if (rd.number_of_subsets <= 0 || rd.subset_size <= 0 || rd.tile_size <= 0)
+            return fail(MPT_ERR_INVALID_ARGUMENT, "ReSTIR DI: bad light presampling settings");
+        if (rd.reuse_neighbor_count > 32 || rd.disocclusion_reuse_count > 32)
+            return fail(MPT_ERR_UNSUPPORTED, "ReSTIR DI: at most 32 spatial neighbours");
+        if (rs.wants_render_low_resolution && rs.allow_render_low_resolution)
+            return fail(MPT_ERR_UNSUPPORTED, "ReSTIR DI with low-resolution rendering");
+    }
     if (f->options.bsdf_override != MPT_BSDF_NONE && f->options.bsdf_override != MPT_BSDF_LAMBERTIAN)
         return fail(MPT_ERR_UNSUPPORTED, "only BSDF_NONE (Principled) and BSDF_LAMBERTIAN are implemented");
     if (f->options.ris_use_visibility) return fail(MPT_ERR_UNSUPPORTED, "RISUseVisiblityTargetFunction not implemented");
@@ -621,6 +685,10 @@ int mpt_render_frame(MptContext* c, const MptFrame* f) {
     HIPCHK(hipSetDevice(c->device));
     int r = ensure_paths(c, f->res_x, f->res_y, f->band_height, f->band_index, f->band_count);
     if (r != MPT_OK) return r;
+    if (f->options.direct_light_sampling == MPT_LSS_RESTIR_DI) {
+        r = ensure_restir(c, f);
+        if (r != MPT_OK) return r;
+    }
     if ((c->any_tex || f->bsdf_flags.white_furnace_mode) && c->mat_slot.n < (size_t)std::max(c->n_slots, 1)) {
         HIPCHK(hipStreamSynchronize(c->stream));
         HIPCHK(c->mat_slot.alloc((size_t)std::max(c->n_slots, 1)));
@@ -644,8 +712,10 @@ int mpt_render_frame(MptContext* c, const MptFrame* f) {
     cfg.ev_mode = c->ev_mode[pool];
     cfg.ev_cap = EV_POOL;
     cfg.ev_used = 0;
+    cfg.restir_out_sp2 = c->restir_out_sp2;
     if (c->timing) HIPCHK(hipEventRecord(c->ev_frame[pool][0], c->stream));
     hipError_t e = launch_frame(dev_scene(c), dev_paths(c), c->d_frames + slot, *f, cfg, c->stream);
+    c->restir_out_sp2 = cfg.restir_out_sp2;
     if (e != hipSuccess) return fail(MPT_ERR_HIP, std::string("kernel launch: ") + hipGetErrorString(e));
     if (c->timing) {
         HIPCHK(hipEventRecord(c->ev_frame[pool][1], c->stream));
@@ -764,6 +834,7 @@ int mpt_get_stats(MptContext* c, MptStats* out) {
     out->resolve_ms = c->stage_ms[KT_RESOLVE];
     out->accumulate_ms = c->stage_ms[KT_ACCUMULATE];
     out->compact_ms = c->stage_ms[KT_COMPACT];
+    out->restir_ms = c->stage_ms[KT_RESTIR];
     out->shade_launches = c->stage_launches[KT_SHADE];
     out->trace_launches = c->trace_launches;
     out->frames = c->frames;

@@ -79,6 +79,7 @@ enum : uint32_t {
     NF_IMM = 1u << 7,        // immediate light term (emissive textured material)
     NF_NOADD = 1u << 8,      // LSS_NO_DIRECT_LIGHT_SAMPLING: nothing to add at resolve
     NF_L = 1u << 9,          // the light-sampling strategy ran at this vertex
+    NF_AQ = 1u << 10,        // ReSTIR DI final shading: the light term waits for occlusion slot 0
 };
 
 struct DevPaths {
@@ -118,11 +119,29 @@ struct DevPaths {
     int32_t* as_conv;         // pixel_converged_sample_count (-1 = not converged)
     uint8_t* active;          // pixel_active
     uint32_t* status;         // [0] stop_noise_threshold_converged_count, [1] still_one_ray_active
+    // ReSTIR DI (LSS_RESTIR_DI only; NULL otherwise).  G-buffer of the camera hits as
+    // CameraRays writes it (CameraRays.h:144-166, GBuffer.h:17-34), current + previous frame:
+    float4* gb_pos;           // first hit xyz
+    float4* gb_sn;            // shading normal (as stored, not renormalised)
+    float4* gb_gn;            // geometric normal
+    float4* gb_view;          // view direction (-ray direction)
+    int4* gb_meta;            // x prim (-1 miss), y material index + 1 (0: never written), z camera_ray_hit, w per-pixel material
+    uint4* gb_vsA;            // ray volume state
+    uint4* gb_vsB;
+    MptMaterial* gb_mat;      // per-pixel resolved material (textured materials / white furnace)
+    float4* pgb_pos; float4* pgb_sn; float4* pgb_gn; float4* pgb_view; int4* pgb_meta;
+    uint4* pgb_vsA; uint4* pgb_vsB; MptMaterial* pgb_mat;
+    float4* rs_init;          // reservoirs (3 float4 each): initial candidates
+    float4* rs_sp1;           // spatial outputs, ping-pong
+    float4* rs_sp2;
+    float4* rs_out;           // restir_output_reservoirs of this frame (rs_sp1 or rs_sp2)
+    float4* rs_tin;           // temporal input of this frame (last frame's output)
+    float4* rs_plights;       // presampled lights (4 float4 each)
 };
 
 constexpr int N_TRACE_MODES = 5;
 // timed kernel kinds: 0..2 = traversal stages (trace modes), then the others
-enum { KT_CAMERA = 3, KT_SHADE = 4, KT_RESOLVE = 5, KT_ACCUMULATE = 6, KT_COMPACT = 7, KT_COUNT = 8 };
+enum { KT_CAMERA = 3, KT_SHADE = 4, KT_RESOLVE = 5, KT_ACCUMULATE = 6, KT_COMPACT = 7, KT_RESTIR = 8, KT_COUNT = 9 };
 constexpr uint32_t QM_CONT = 16u;
 constexpr int N_STATS = N_TRACE_MODES * 4;
 
@@ -140,12 +159,15 @@ struct LaunchCfg {
     int ev_cap;
     int ev_used;
     uint32_t launches;
+    int restir_out_sp2;       // in/out: restir_output_reservoirs is rs_sp2 (else rs_sp1)
 };
 
 hipError_t launch_frame(const DevScene& S, const DevPaths& P, const MptFrame* d_frame, const MptFrame& h_frame,
                         LaunchCfg& cfg, hipStream_t st);
 hipError_t launch_resolve_materials(const DevScene& S, MptMaterial* out_res, int32_t* out_tex, int n, float4* em_tab,
                                    hipStream_t st);
+hipError_t launch_restir_fill(float4* reservoirs, int n, hipStream_t st);
+hipError_t launch_restir_fill_lights(float4* lights, int n, hipStream_t st);
 hipError_t launch_trace_raw(const DevScene& S, const float4* o, const float4* d, int n, bool any, float4* out_hit,
                             uint8_t* out_occ, int32_t* fetch_ctr, uint32_t* spill, int grid, hipStream_t st);
 

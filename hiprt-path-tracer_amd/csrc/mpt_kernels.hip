@@ -228,6 +228,7 @@ struct TraceArgs {
 };
 DEV uint32_t slot_pixel(const MptFrame& F, int slot, int& x, int& y);
 DEV uint32_t pixel_seed(const MptFrame& F, uint32_t pix);
+DEV uint32_t camera_seed(const MptFrame& F, uint32_t pix);
 
 template <int MODE, bool STATS>
 __global__ __launch_bounds__(TB) void k_trace(TraceArgs A) {
@@ -266,7 +267,11 @@ __global__ __launch_bounds__(TB) void k_trace(TraceArgs A) {
             bool found;
             int skips = 0;
             uint32_t pseed = 0u;
-            if (A.alpha) { int px, py; pseed = pixel_seed(*A.F, slot_pixel(*A.F, slot, px, py)); }
+            if (A.alpha) {   // bounce 0: the camera launch's seed (CameraRays traces the camera ray)
+                int px, py;
+                uint32_t pix = slot_pixel(*A.F, slot, px, py);
+                pseed = A.bounce == 0 ? camera_seed(*A.F, pix) : pixel_seed(*A.F, pix);
+            }
             while (true) {
                 n_rays++;
                 found = traverse<false, STATS>(S, o, d, last_hit, INFINITY, h, lds, spill, n_nodes, n_tris, A.alpha != 0,
@@ -446,9 +451,14 @@ DEV uint32_t slot_pixel(const MptFrame& F, int slot, int& x, int& y) {
     y = ((r / bh) * F.band_count + F.band_index) * bh + (r % bh);
     return (uint32_t)x + (uint32_t)y * (uint32_t)F.res_x;
 }
-DEV uint32_t pixel_seed(const MptFrame& F, uint32_t pix) {
+DEV uint32_t pixel_seed(const MptFrame& F, uint32_t pix, uint32_t random_seed) {
     const MptRenderSettings& rs = F.render_settings;
-    return rs.freeze_random ? wang_hash(pix + 1u) : wang_hash((pix + 1u) * (uint32_t)(rs.sample_number + 1) * F.random_seed);
+    return rs.freeze_random ? wang_hash(pix + 1u) : wang_hash((pix + 1u) * (uint32_t)(rs.sample_number + 1) * random_seed);
+}
+DEV uint32_t pixel_seed(const MptFrame& F, uint32_t pix) { return pixel_seed(F, pix, F.random_seed); }
+// CameraRays' seed: its own launch seed when the frame carries one (GPURenderer.cpp:468-474)
+DEV uint32_t camera_seed(const MptFrame& F, uint32_t pix) {
+    return pixel_seed(F, pix, F.camera_random_seed ? F.camera_random_seed : F.random_seed);
 }
 
 // ----------------------------------------------------------------------------------
@@ -538,7 +548,7 @@ __global__ __launch_bounds__(TB) void k_camera(DevPaths P, const MptFrame* __res
     if (rs.do_update_status_buffers) P.status[1] = 1u;
     int x, y;
     uint32_t pix = slot_pixel(F, slot, x, y);
-    Rng rng = make_rng(pixel_seed(F, pix));
+    Rng rng = make_rng(camera_seed(F, pix));
     float xd = (float)x + 0.5f, yd = (float)y + 0.5f;
     if (F.current_camera.do_jittering) { xd += rng() - 0.5f; yd += rng() - 0.5f; }
     float xn = xd / (float)F.res_x * 2.0f - 1.0f;
@@ -708,9 +718,31 @@ __device__ unsigned long long g_sect[8];
 #define SECT_END() do {} while (0)
 #endif
 
+// ReSTIR DI reservoir in HBM: 3 float4 = {M, weight_sum, UCW, triangle}, {point, target},
+// {flags} (ReSTIRDIReservoir / ReSTIRDISample, Reservoir.h:22-116; SampleFlags.h:10-22)
+enum : uint32_t { RF_ENVMAP = 1u, RF_BSDF_REFRACTION = 2u, RF_UNOCCLUDED = 4u };
+struct RResv { int M; float wsum; float UCW; int tri; v3 point; float target; uint32_t flags; };
+DEV RResv rr_default() {
+    RResv r;
+    r.M = 0; r.wsum = 0.0f; r.UCW = 0.0f; r.tri = -1; r.point = mk3(0.0f, 0.0f, 0.0f); r.target = 0.0f; r.flags = 0u;
+    return r;
+}
+DEV RResv rr_load(const float4* b, int i) {
+    float4 a = b[3 * (size_t)i], c = b[3 * (size_t)i + 1], d = b[3 * (size_t)i + 2];
+    RResv r;
+    r.M = __float_as_int(a.x); r.wsum = a.y; r.UCW = a.z; r.tri = __float_as_int(a.w);
+    r.point = mk3(c.x, c.y, c.z); r.target = c.w; r.flags = __float_as_uint(d.x);
+    return r;
+}
+DEV void rr_store(float4* b, int i, const RResv& r) {
+    b[3 * (size_t)i] = make_float4(__int_as_float(r.M), r.wsum, r.UCW, __int_as_float(r.tri));
+    b[3 * (size_t)i + 1] = make_float4(r.point.x, r.point.y, r.point.z, r.target);
+    b[3 * (size_t)i + 2] = make_float4(__uint_as_float(r.flags), 0.0f, 0.0f, 0.0f);
+}
+
 enum ShadeOp {
     OP_DONE = 0, OP_RIS_LIGHT, OP_RIS_BSDF, OP_RIS_WIN, OP_MIS_LIGHT, OP_MIS_BSDF, OP_UNI_LIGHT, OP_BSDF_LIGHT,
-    OP_ENV_LIGHT, OP_ENV_BSDF, OP_CONT
+    OP_ENV_LIGHT, OP_ENV_BSDF, OP_CONT, OP_RESTIR
 };
 
 struct ShadeArgs {
@@ -815,15 +847,21 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MPT_SHADE_WA
             const int lss = F.options.direct_light_sampling;
             const MptWorldSettings& ws = F.world_settings;
             // ---------------- which BSDF operations this vertex runs, in RNG order ----------------
-            bool do_light = S.n_emissive != 0 && !(F.bsdf_flags.white_furnace_mode && F.bsdf_flags.white_furnace_mode_turn_off_emissives);
+            // sample_one_light (Lights.h:277-321); ReSTIR DI: the reservoir at bounce 0 (also
+            // with only an envmap), RIS at later bounces (Lights.h:243-275, RIS.h:292-302)
+            const bool restir = lss == MPT_LSS_RESTIR_DI;
+            bool do_light = (S.n_emissive != 0 || (restir && ws.ambient_light_type == MPT_AMBIENT_ENVMAP)) &&
+                            !(F.bsdf_flags.white_furnace_mode && F.bsdf_flags.white_furnace_mode_turn_off_emissives);
             if (do_light && is_emissive(m)) {
                 do_light = false;
                 if (m.emissive_texture_used && bounce > 0) { fl |= NF_IMM; store3(nr.imm, emission_of(m)); }
             }
             do_light = do_light && lss != MPT_LSS_NO_DIRECT_LIGHT_SAMPLING;
+            if (restir && bounce > 0 && S.n_emissive == 0) do_light = false;
             if (do_light) fl |= NF_L;
             const bool do_env = ws.ambient_light_type == MPT_AMBIENT_ENVMAP && !F.bsdf_flags.white_furnace_mode &&
-                                !is_emissive(m) && ws.envmap_intensity > 0.0f && F.options.envmap_sampling != MPT_ESS_NO_SAMPLING;
+                                !is_emissive(m) && ws.envmap_intensity > 0.0f && F.options.envmap_sampling != MPT_ESS_NO_SAMPLING &&
+                                !(restir && bounce == 0);
             const bool env_use = lss != MPT_LSS_NO_DIRECT_LIGHT_SAMPLING;
             const bool do_cont = bounce < A.last_bounce;
             const float ism = dot(view, gn) < 0 ? -1.0f : 1.0f;
@@ -831,7 +869,8 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MPT_SHADE_WA
             const int nl = rs.ris_number_of_light_candidates, nbc = rs.ris_number_of_bsdf_candidates;
             int op = OP_DONE;
             if (do_light) {
-                if (lss == MPT_LSS_RIS_BSDF_AND_LIGHT) op = nl > 0 ? OP_RIS_LIGHT : (nbc > 0 ? OP_RIS_BSDF : OP_RIS_WIN);
+                if (restir && bounce == 0) op = OP_RESTIR;
+                else if (lss == MPT_LSS_RIS_BSDF_AND_LIGHT || restir) op = nl > 0 ? OP_RIS_LIGHT : (nbc > 0 ? OP_RIS_BSDF : OP_RIS_WIN);
                 else if (lss == MPT_LSS_MIS_LIGHT_BSDF) op = OP_MIS_LIGHT;
                 else if (lss == MPT_LSS_UNIFORM_ONE_LIGHT) op = OP_UNI_LIGHT;
                 else if (lss == MPT_LSS_BSDF) op = OP_BSDF_LIGHT;
@@ -847,6 +886,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MPT_SHADE_WA
             SECT(0);
             bsdf_eval_pre<OVR>(bc, m, vs, view, sn, pe);
             SECT(5);
+            RResv rres;                        // ReSTIR DI output reservoir (OP_RESTIR)
             Col fW = col(0.0f);                // BSDF value / pdf at the RIS light winner
             float pdfW = 0.0f;
             // One BSDF evaluation site for every operation of the vertex: each iteration
@@ -901,6 +941,19 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MPT_SHADE_WA
                         geo = absr(dot(li.normal, -L));
                         lp = so;
                         do_eval = geo > 0.0f;
+                    }
+                } else if (op == OP_RESTIR) {
+                    // sample_light_ReSTIR_DI + evaluate_ReSTIR_DI_reservoir (FinalShading.h:16-115)
+                    rres = rr_load(P.rs_out, slot);
+                    if ((rres.flags & RF_ENVMAP) && ws.ambient_light_type != MPT_AMBIENT_ENVMAP) {
+                        rres.UCW = 0.0f;   // validate_reservoir writes through to the buffer
+                        float4 a = P.rs_out[3 * (size_t)slot];
+                        P.rs_out[3 * (size_t)slot] = make_float4(a.x, a.y, 0.0f, a.w);
+                    }
+                    if (rres.UCW > 0.0f) {
+                        if (rres.flags & RF_ENVMAP) { L = mat_x_vec(ws.envmap_to_world_matrix.m, rres.point); dist = 1.0e35f; }
+                        else { L = rres.point - ip; dist = length(L); L = L / dist; }
+                        do_eval = true;
                     }
                 } else if (op == OP_ENV_LIGHT) {
                     ec = env_sample(S, F, L, lpdf, rng);
@@ -1000,6 +1053,22 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MPT_SHADE_WA
                         nr.b_pdf = pdf;
                         store3(nr.dir, L);
                         nr.b_cos = maxr(0.0f, dot(sn, L));
+                    }
+                } else if (op == OP_RESTIR) {
+                    if (do_eval) {
+                        float c = dot(sn, L);
+                        if (rres.flags & RF_BSDF_REFRACTION) c = absr(c);
+                        if (c > 0.0f) {
+                            Col e;
+                            if (rres.flags & RF_ENVMAP) { float ep_; e = env_eval(S, F, L, ep_); }
+                            else e = emission_of(S.mats[S.mat_idx[rres.tri]]);
+                            store3(nr.a, f * rres.UCW * e * c);
+                            fl |= NF_A;
+                            if (!(rres.flags & RF_UNOCCLUDED) && rs.restir_di_settings.do_final_shading_visibility) {
+                                fl |= NF_AQ;
+                                stage_query(P, slot, 0, qm, ip, prim, L, dist - 1.0e-4f);
+                            }
+                        }
                     }
                 } else if (op == OP_ENV_LIGHT) {
                     // Envmap.h:151-246
@@ -1223,6 +1292,8 @@ DEV float pdf_emissive_hit(const DevScene& S, const ShadowLightHit& h, v3 d) {
     return pdf;
 }
 
+#include "restir_di.h"
+
 __global__ __launch_bounds__(TB) void k_resolve(DevScene S, DevPaths P, const MptFrame* __restrict__ Fp, int bounce,
                                                 const int32_t* q_cur, const int32_t* count_cur) {
     const MptFrame& F = *Fp;
@@ -1244,7 +1315,9 @@ __global__ __launch_bounds__(TB) void k_resolve(DevScene S, DevPaths P, const Mp
     const uint8_t* occ = P.occ + (size_t)slot * 4;
     if (fl & NF_IMM) ld = load3c(nr.imm);
     else if (!(fl & NF_L)) ld = col(0.0f);
-    else if (lss == MPT_LSS_RIS_BSDF_AND_LIGHT) {
+    else if (lss == MPT_LSS_RESTIR_DI && bounce == 0) {
+        if ((fl & NF_A) && !((fl & NF_AQ) && occ[0])) ld = load3c(nr.a);
+    } else if (lss == MPT_LSS_RIS_BSDF_AND_LIGHT || lss == MPT_LSS_RESTIR_DI) {
         float wsum = nr.ris_wsum;
         float cwb = 0.0f, targetb = 0.0f;
         int trib = -1;
@@ -1404,12 +1477,52 @@ static void timed_trace(const TraceArgs& a, LaunchCfg& cfg, hipStream_t st) {
     cfg.launches++;
 }
 
-hipError_t launch_frame(const DevScene& S, const DevPaths& P, const MptFrame* d_frame, const MptFrame& hf, LaunchCfg& cfg,
+template <template <int> class K, typename... Args>
+static void launch_ovr(int ovr, dim3 g, hipStream_t st, Args... args) {
+    if (ovr == MPT_BSDF_LAMBERTIAN) hipLaunchKernelGGL(K<MPT_BSDF_LAMBERTIAN>::fn, g, dim3(TB), 0, st, args...);
+    else hipLaunchKernelGGL(K<MPT_BSDF_NONE>::fn, g, dim3(TB), 0, st, args...);
+}
+template <int OVR> struct KInitial { static constexpr auto fn = k_restir_initial<OVR>; };
+template <int OVR> struct KSpatiotemporal { static constexpr auto fn = k_restir_spatiotemporal<OVR>; };
+template <int OVR> struct KSpatial { static constexpr auto fn = k_restir_spatial<OVR>; };
+
+// ReSTIRDIRenderPass::launch (ReSTIRDIRenderPass.cpp:233-264) for the fused configuration:
+// presampling, initial candidates, fused spatiotemporal, (number_of_passes - 1) spatial
+// passes ping-ponging between the two spatial buffers; returns the output buffer in P.rs_out
+static void launch_restir(const DevScene& S, DevPaths& P, const MptFrame* d_frame, const MptFrame& hf, LaunchCfg& cfg,
+                          hipStream_t st) {
+    TimedScope ts(cfg, st, KT_RESTIR);
+    const MptReSTIRDISettings& rd = hf.render_settings.restir_di_settings;
+    const int ovr = hf.options.bsdf_override;
+    const int n_pl = rd.number_of_subsets * rd.subset_size;
+    hipLaunchKernelGGL(k_restir_presample, dim3((n_pl + TB - 1) / TB), dim3(TB), 0, st, S, P, d_frame);
+    const dim3 g(cfg.grid_persistent);
+    launch_ovr<KInitial>(ovr, g, st, S, P, d_frame);
+    float4* last_out = cfg.restir_out_sp2 ? P.rs_sp2 : P.rs_sp1;
+    P.rs_tin = last_out;
+    P.rs_out = last_out == P.rs_sp1 ? P.rs_sp2 : P.rs_sp1;
+    launch_ovr<KSpatiotemporal>(ovr, g, st, S, P, d_frame);
+    for (int pass = 1; pass < rd.number_of_passes; pass++) {
+        float4* in = P.rs_out;
+        float4* out = in == P.rs_sp1 ? P.rs_sp2 : P.rs_sp1;
+        launch_ovr<KSpatial>(ovr, g, st, S, P, d_frame, pass, (const float4*)in, out);
+        P.rs_out = out;
+    }
+    cfg.restir_out_sp2 = P.rs_out == P.rs_sp2 ? 1 : 0;
+}
+
+hipError_t launch_frame(const DevScene& S, const DevPaths& P0, const MptFrame* d_frame, const MptFrame& hf, LaunchCfg& cfg,
                         hipStream_t st) {
+    DevPaths P = P0;
     const int n = P.n;
     if (n == 0) return hipSuccess;
     const MptRenderSettings& hrs = hf.render_settings;
     const bool as = (hrs.stop_pixel_noise_threshold > 0.0f || hrs.enable_adaptive_sampling) && hrs.accumulate;
+    const bool restir = hf.options.direct_light_sampling == MPT_LSS_RESTIR_DI;
+    if (restir) {
+        hipLaunchKernelGGL(k_restir_frame_begin, dim3(blocks_for(n)), dim3(TB), 0, st, P, d_frame);
+        P.rs_out = cfg.restir_out_sp2 ? P.rs_sp2 : P.rs_sp1;
+    }
     // all pixels start a path, unless adaptive sampling compacts the camera queue
     hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(&P.counters[CTR_Q0]), as ? 0 : n, 1, st);
     {
@@ -1427,6 +1540,10 @@ hipError_t launch_frame(const DevScene& S, const DevPaths& P, const MptFrame* d_
         ta.S = S; ta.P = P; ta.queue = q_cur; ta.count_ptr = &P.counters[c_cur]; ta.fetch = &P.counters[CTR_FETCH];
         ta.F = d_frame; ta.bounce = b; ta.alpha = hf.render_settings.do_alpha_testing ? 1 : 0;
         timed_trace<TM_PATH>(ta, cfg, st);
+        if (restir && b == 0) {
+            hipLaunchKernelGGL(k_gbuffer, dim3(blocks_for(n)), dim3(TB), 0, st, S, P, d_frame);
+            launch_restir(S, P, d_frame, hf, cfg, st);
+        }
         hipMemsetAsync(&P.counters[c_next], 0, sizeof(int32_t), st);
         hipMemsetAsync(&P.counters[CTR_ANY], 0, 2 * sizeof(int32_t), st);
         ShadeArgs sa;
@@ -1520,6 +1637,15 @@ extern "C" int mpt_debug_math(int fn, const float* a, const float* b, float* out
     hipMemcpy(out, dout, n * 4, hipMemcpyDeviceToHost);
     hipFree(da); hipFree(db); hipFree(dout);
     return 0;
+}
+
+hipError_t launch_restir_fill(float4* r, int n, hipStream_t st) {
+    hipLaunchKernelGGL(k_restir_fill, dim3((n + TB - 1) / TB), dim3(TB), 0, st, r, n);
+    return hipGetLastError();
+}
+hipError_t launch_restir_fill_lights(float4* l, int n, hipStream_t st) {
+    hipLaunchKernelGGL(k_restir_fill_lights, dim3((n + TB - 1) / TB), dim3(TB), 0, st, l, n);
+    return hipGetLastError();
 }
 
 hipError_t launch_resolve_materials(const DevScene& S, MptMaterial* out_res, int32_t* out_tex, int n, float4* em_tab,

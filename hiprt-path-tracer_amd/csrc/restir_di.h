@@ -1,0 +1,723 @@
+// restir_di.h -- ReSTIR DI passes of the MI355X path (LSS_RESTIR_DI), included by
+// mpt_kernels.hip after the light / envmap / traversal helpers.
+//
+// The reference's default kernel options (KernelOptions.h:270-366): lights presampling,
+// no visibility in the initial target function, visibility in the spatial target
+// function and the bias correction, visibility reuse, pairwise-MIS-defensive weights;
+// ReSTIRDIRenderPass::launch (ReSTIRDIRenderPass.cpp:233-264) with the fused
+// spatiotemporal pass followed by (number_of_passes - 1) spatial passes.
+//
+// MI355X mapping: one pass = one kernel over the pixels, persistent blocks of 256 lanes
+// (grid = the traversal grid, so the per-lane traversal spill area is reused); visibility
+// and BSDF rays are traced inline with the BVH8 traversal (LDS short stack), the passes
+// being short compared with the path-tracing wavefront.  Reservoirs live in three
+// ping-pong HBM buffers of 48 B per pixel (3 x float4), the G-buffer in SoA float4 arrays.
+
+// ---- surfaces (Surface.h:12-73) ----------------------------------------------------
+__device__ MptMaterial g_zero_mat;   // the material of a never-written G-buffer entry (zero-initialised)
+
+struct RSurf { const Mat* m; VState vs; int last; v3 view, sn, gn, sp, p; };
+DEV RSurf gb_surface(const DevScene& S, const DevPaths& P, int i, bool prev) {
+    int4 meta = prev ? P.pgb_meta[i] : P.gb_meta[i];
+    float4 pos = prev ? P.pgb_pos[i] : P.gb_pos[i];
+    float4 sn = prev ? P.pgb_sn[i] : P.gb_sn[i];
+    float4 gn = prev ? P.pgb_gn[i] : P.gb_gn[i];
+    float4 vw = prev ? P.pgb_view[i] : P.gb_view[i];
+    RSurf s;
+    if (meta.y == 0) s.m = &g_zero_mat;
+    else if (meta.w) s.m = prev ? &P.pgb_mat[i] : &P.gb_mat[i];
+    else s.m = &S.mats_res[meta.y - 1];
+    s.vs = meta.y == 0 ? vs_default() : vs_load(prev ? P.pgb_vsA : P.gb_vsA, prev ? P.pgb_vsB : P.gb_vsB, i);
+    s.last = meta.x;
+    s.view = mk3(vw.x, vw.y, vw.z);
+    s.sn = mk3(sn.x, sn.y, sn.z);
+    s.gn = mk3(gn.x, gn.y, gn.z);
+    s.p = mk3(pos.x, pos.y, pos.z);
+    s.sp = s.p + s.sn * 1.0e-4f;
+    return s;
+}
+
+// ---- traced rays of a pass (alpha keys: pass pixel seed, 0, 5 + pass, ray counter) ----
+struct RRays {
+    const DevScene* S;
+    uint2* lds;
+    uint32_t* spill;
+    bool alpha;
+    uint32_t pseed;
+    int kind;
+    int n;
+    uint32_t n_any, n_closest;
+    DEV bool any(v3 o, v3 d, float tmax, int last) {
+        n_any++;
+        uint32_t key = alpha ? alpha_key(pseed, 0, kind, n++) : 0u;
+        THit h;
+        uint32_t nn = 0, nt = 0;
+        // evaluate_shadow_ray: maxT = t_max - 1e-4 (Intersect.h:227)
+        return traverse<true, false>(*S, o, d, last, tmax - 1.0e-4f, h, lds, spill, nn, nt, alpha, key);
+    }
+    DEV bool closest(v3 o, v3 d, int last, THit& h) {
+        n_closest++;
+        uint32_t key = alpha ? alpha_key(pseed, 0, kind, n++) : 0u;
+        uint32_t nn = 0, nt = 0;
+        return traverse<false, false>(*S, o, d, last, INFINITY, h, lds, spill, nn, nt, alpha, key);
+    }
+};
+DEV void count_pass_rays(const DevPaths& P, uint32_t n_any, uint32_t n_closest) {
+    for (int off = 32; off > 0; off >>= 1) {
+        n_any += __shfl_xor(n_any, off);
+        n_closest += __shfl_xor(n_closest, off);
+    }
+    if (lane_id() == 0 && (n_any | n_closest)) {
+        atomicAdd((unsigned long long*)&P.ray_counts[1], (unsigned long long)n_any);
+        atomicAdd((unsigned long long*)&P.ray_counts[2], (unsigned long long)n_closest);
+    }
+}
+
+DEV float power_heuristic(float a, int na, float b, int nb) {   // Sampling.h:75-87
+    float pa = ((float)na * a) * ((float)na * a);
+    float pb = ((float)nb * b) * ((float)nb * b);
+    return (float)na * a * a / (pa + pb);
+}
+DEV float radical_inverse_base_2(uint32_t i) {   // Sampling.h:25-32
+    i = (i << 16u) | (i >> 16u);
+    i = ((i & 0x55555555u) << 1u) | ((i & 0xAAAAAAAAu) >> 1u);
+    i = ((i & 0x33333333u) << 2u) | ((i & 0xCCCCCCCCu) >> 2u);
+    i = ((i & 0x0F0F0F0Fu) << 4u) | ((i & 0xF0F0F0F0u) >> 4u);
+    i = ((i & 0x00FF00FFu) << 8u) | ((i & 0xFF00FF00u) >> 8u);
+    return (float)i * 2.3283064365386963e-10f;
+}
+DEV uint32_t pass_seed(const MptFrame& F, uint32_t pix, uint32_t seed) {
+    return F.render_settings.freeze_random ? wang_hash(pix + 1u) : wang_hash((pix + 1u) * (uint32_t)(F.render_settings.sample_number + 1) * seed);
+}
+
+// ---- reservoir operations (Reservoir.h:36-116) -------------------------------------
+DEV void rr_add(RResv& r, int tri, v3 p, float tf, uint32_t fl, float w, Rng& rng) {
+    r.M++;
+    r.wsum += w;
+    if (rng() < w / r.wsum) { r.tri = tri; r.point = p; r.target = tf; r.flags = fl; }
+}
+DEV bool rr_combine(RResv& r, const RResv& o, float mis, float tf, float jac, Rng& rng) {
+    if (o.UCW <= 0.0f) { r.M += o.M; return false; }
+    float w = mis * tf * o.UCW * jac;
+    r.M += o.M;
+    r.wsum += w;
+    if (rng() < w / r.wsum) {
+        r.tri = o.tri; r.point = o.point; r.flags = o.flags;
+        r.target = tf;
+        return true;
+    }
+    return false;
+}
+DEV void rr_end_normalized(RResv& r) {   // end_with_normalization(1, 1) of the pairwise weights
+    if (r.wsum == 0.0f || r.wsum < 1.0e-10f || r.wsum > 1.0e10f) r.UCW = 0.0f;
+    else r.UCW = 1.0f / r.target * r.wsum * 1.0f / 1.0f;
+    r.M = imin(r.M, 1000000);
+}
+
+// ReSTIR_DI_evaluate_target_function<vis> (Utils.h:20-128)
+DEV float restir_target(const DevScene& S, const MptFrame& F, const BCtx& bc, RRays& rr, int tri, v3 point, uint32_t flags,
+                        const RSurf& s, bool vis, int ovr) {
+    if (tri == -1 && !(flags & RF_ENVMAP)) return 0.0f;
+    float dist = 0.0f;
+    v3 dir;
+    if (flags & RF_ENVMAP) { dir = mat_x_vec(F.world_settings.envmap_to_world_matrix.m, point); dist = 1.0e35f; }
+    else if (vis) { dir = point - s.sp; dist = length(dir); dir = dir / dist; }
+    else dir = normalize(point - s.sp);
+    float cosv = maxr(0.0f, dot(s.sn, dir));
+    if (cosv == 0.0f) return 0.0f;
+    float bp;
+    VState tv = s.vs;
+    Col f = ovr == MPT_BSDF_LAMBERTIAN ? bsdf_eval<MPT_BSDF_LAMBERTIAN>(bc, *s.m, tv, s.view, s.sn, dir, bp)
+                                       : bsdf_eval<MPT_BSDF_NONE>(bc, *s.m, tv, s.view, s.sn, dir, bp);
+    Col e;
+    if (flags & RF_ENVMAP) { float ep; e = env_eval(S, F, dir, ep); }
+    else e = emission_of(S.mats[S.mat_idx[tri]]);
+    float t = lum(f * e * cosv);
+    if (t == 0.0f) return 0.0f;
+    if (vis) t *= rr.any(s.sp, dir, dist, s.last) ? 0.0f : 1.0f;
+    return t;
+}
+
+// ReSTIR_DI_visibility_reuse (Utils.h:134-171)
+DEV void restir_visibility_reuse(const MptFrame& F, RRays& rr, RResv& r, v3 sp, int last) {
+    if (r.UCW <= 0.0f) return;
+    if (r.flags & RF_UNOCCLUDED) return;
+    float dist;
+    v3 dir;
+    if (r.flags & RF_ENVMAP) { dir = mat_x_vec(F.world_settings.envmap_to_world_matrix.m, r.point); dist = 1.0e35f; }
+    else { dir = r.point - sp; dist = length(dir); dir = dir / dist; }
+    if (rr.any(sp, dir, dist, last)) r.UCW = -1.0f;
+    else r.flags |= RF_UNOCCLUDED;
+}
+
+// get_jacobian_determinant_reconnection_shift (Utils.h:173-206)
+DEV float restir_jacobian(const DevScene& S, const RResv& nr, v3 csp, v3 nsp) {
+    v3 tc = nr.point - csp, tn = nr.point - nsp;
+    float dc = length(tc);
+    tc = tc / dc;
+    float dn = length(tn);
+    tn = tn / dn;
+    int3 t = tri_idx(S, nr.tri);
+    v3 A = ld3(S.pos, t.x);
+    v3 ln = normalize(cross(ld3(S.pos, t.y) - A, ld3(S.pos, t.z) - A));
+    float cc = absr(dot(-tc, ln)), cn = absr(dot(-tn, ln));
+    float jac = cc / cn * ((dn * dn) / (dc * dc));
+    if (jac > 20.0f || jac < 1.0f / 20.0f || isnan(jac)) return -1.0f;
+    return jac;
+}
+
+// check_neighbor_similarity_heuristics (Utils.h:214-263), incl. the inverted normal test
+DEV bool restir_similar(const DevScene& S, const DevPaths& P, const MptReSTIRDISettings& rd, int nb, const Mat& center_m,
+                        v3 sp, v3 n, bool prev) {
+    float4 pos = prev ? P.pgb_pos[nb] : P.gb_pos[nb];
+    bool plane = !rd.use_plane_distance_heuristic || absr(dot(mk3(pos.x, pos.y, pos.z) - sp, n)) < rd.plane_distance_threshold;
+    bool normal = true;
+    if (!rd.use_normal_similarity_heuristic) {
+        float4 ns = P.gb_sn[nb];
+        normal = dot(n, mk3(ns.x, ns.y, ns.z)) > rd.normal_similarity_angle_precomp;
+    }
+    RSurf ns = gb_surface(S, P, nb, prev);
+    bool rough = !rd.use_roughness_similarity_heuristic || absr(ns.m->roughness - center_m.roughness) < rd.roughness_similarity_threshold;
+    return plane && normal && rough && !is_emissive(*ns.m);
+}
+
+// get_spatial_neighbor_pixel_index (Utils.h:289-339)
+DEV int restir_spatial_neighbor(const DevPaths& P, const MptFrame& F, int k, int count, int radius, int cx, int cy, float cr,
+                                float sr, uint32_t pass_random_seed) {
+    const MptRenderSettings& rs = F.render_settings;
+    int W = F.res_x, H = F.res_y;
+    if (k == count) return cx + cy * W;
+    float ux = (float)(unsigned)(k + 1) / (float)(unsigned)(count + 1), uy = radical_inverse_base_2((unsigned)(k + 1));
+    float rr = (float)radius * sqrtf(uy);
+    float ox = rr * pcos(TWO_PI * ux), oy = rr * psin(TWO_PI * ux);
+    float rx = ox * cr - oy * sr, ry = ox * sr + oy * cr;
+    int nx, ny;
+    if (rs.restir_di_settings.debug_neighbor_location) { nx = cx + 15; ny = cy; }
+    else { nx = cx + (int)rx; ny = cy + (int)ry; }
+    if (nx < 0 || nx >= W || ny < 0 || ny >= H) return -1;
+    int ni = nx + ny * W;
+    if (rs.enable_adaptive_sampling && rs.sample_number >= rs.adaptive_sampling_min_samples) {
+        if (rs.restir_di_settings.allow_converged_neighbors_reuse) {
+            Rng g = make_rng(pass_random_seed);
+            if (g() > rs.restir_di_settings.converged_neighbor_reuse_probability && P.as_conv[ni] != -1) return -1;
+        } else if (P.as_conv[ni] != -1) return -1;
+    }
+    return ni;
+}
+
+// pairwise MIS defensive (SpatiotemporalMISWeight.h:193-291, SpatialMISWeight.h:167-262)
+struct PairwiseMIS {
+    float mc;
+    DEV float weight(const DevScene& S, const MptFrame& F, const BCtx& bc, RRays& rr, const MptReSTIRDISettings& rd,
+                     const RResv& res, const RResv& center, float tf_center, const RSurf& nsurf, int vcount, int vM,
+                     bool update_mc, bool canonical, int ovr) {
+        if (!canonical) {
+            float tfn = res.target;
+            float rM = rd.use_confidence_weights ? (float)res.M : 1.0f;
+            float cM = rd.use_confidence_weights ? (float)center.M : 1.0f;
+            float nsum = rd.use_confidence_weights ? (float)vM : 1.0f;
+            float div = rd.use_confidence_weights ? 1.0f : (float)vcount;
+            float nume = tfn * rM;
+            float denom = tfn * nsum + tf_center / div * cM;
+            float mi = 0.0f;
+            if (denom != 0.0f) mi = nume / denom;
+            if (rd.use_confidence_weights) mi *= nsum / (nsum + cM);
+            if (update_mc) {
+                float tcn = restir_target(S, F, bc, rr, center.tri, center.point, center.flags, nsurf, true, ovr);
+                float tcc = center.target;
+                float nume_mc = tcc / div * cM;
+                float denom_mc = tcn * nsum + tcc / div * cM;
+                float conf = 1.0f;
+                if (rd.use_confidence_weights) conf = rM / (cM + nsum);
+                if (denom_mc != 0.0f) mc += nume_mc / denom_mc * conf;
+            }
+            if (rd.use_confidence_weights) return mi;
+            return mi / (float)(vcount + 1);
+        }
+        if (mc == 0.0f) return 1.0f;
+        if (rd.use_confidence_weights) return mc + (float)center.M / (float)(center.M + vM);
+        return (1.0f + mc) / (float)(vcount + 1);
+    }
+};
+
+DEV bool spatial_visibility(const MptReSTIRDISettings& rd, int k, int reuse_count) {   // SpatialReuse.h:36-50
+    bool v = rd.do_visibility_only_last_pass && rd.spatial_pass_index == rd.number_of_passes - 1;
+    v |= !rd.do_visibility_only_last_pass;
+    v &= k < rd.neighbor_visibility_count;
+    v &= k != reuse_count;
+    return v;
+}
+
+DEV BCtx make_bctx(const DevScene& S, const MptFrame& F) {
+    BCtx bc;
+    bc.mats = S.mats;
+    bc.luts = DevLuts{S.lut_conductor, S.lut_glossy, S.lut_glass, S.lut_glass_inv, S.lut_thin_glass, S.lut_sheen};
+    bc.clearcoat_comp = F.bsdf_flags.clearcoat_compensation_approximation;
+    bc.masking = F.bsdf_flags.ggx_masking_shadowing;
+    return bc;
+}
+
+// ---- G-buffer write: CameraRays (CameraRays.h:144-166) over the camera queue ----------
+__global__ __launch_bounds__(TB) void k_gbuffer(DevScene S, DevPaths P, const MptFrame* __restrict__ Fp) {
+    const MptFrame& F = *Fp;
+    int i = blockIdx.x * TB + threadIdx.x;
+    if (i >= P.counters[CTR_Q0]) return;
+    int slot = P.q0[i];
+    float4 ro = P.ray_o[slot], rdv = P.ray_d[slot], hv = P.hit[slot];
+    v3 o = mk3(ro.x, ro.y, ro.z), d = mk3(rdv.x, rdv.y, rdv.z);
+    int prim = (int)__float_as_uint(hv.w);
+    bool found = prim >= 0;
+    int4 meta = P.gb_meta[slot];
+    if (found) {
+        // trace_ray hit processing (Intersect.h:150-216), as k_shade does at bounce 0
+        VState vs = vs_load(P.vsA, P.vsB, slot);
+        Rng rng = make_rng(P.rng[slot]);
+        float t = hv.x;
+        v2 uv = mk2(hv.y, hv.z);
+        int3 ti = tri_idx(S, prim);
+        v3 ip = o + t * d;
+        v2 tc = uv_interp2(S.uv, ti, uv);
+        v3 gn = normalize(tri_normal(S, prim));
+        v3 sn = shading_normal_of(S, gn, prim, uv, tc);
+        const int mi = S.mat_idx[prim];
+        const Mat* mp;
+        int per_pixel = 0;
+        if (F.bsdf_flags.white_furnace_mode || S.mat_tex[mi]) {
+            P.gb_mat[slot] = intersection_material(S, mi, tc, F.bsdf_flags.white_furnace_mode);
+            mp = &P.gb_mat[slot];
+            per_pixel = 1;
+        } else {
+            mp = &S.mats_res[mi];
+        }
+        const Mat& m = *mp;
+        bool was_inside = P.hit_inside[slot] != 0;
+        if ((!was_inside || m.specular_transmission == 0.0f) && !m.thin_walled) {
+            gn *= dot(gn, -d) < 0.0f ? -1.0f : 1.0f;
+            sn *= dot(sn, gn) < 0.0f ? -1.0f : 1.0f;
+            float NoV = dot(sn, -d);
+            sn += (2.0f * clampr(0.0f, 1.0f, -NoV)) * -d;
+        }
+        if (m.dispersion_scale > 0.0f && m.specular_transmission > 0.0f && vs.wl == 0.0f)
+            vs.wl = -(rng() * (float)(830 - 360) + (float)360);
+        if (is_emissive(m) && dot(-d, gn) < 0) { gn = -gn; sn = -sn; }
+        P.gb_pos[slot] = make_float4(ip.x, ip.y, ip.z, 0.0f);
+        P.gb_sn[slot] = make_float4(sn.x, sn.y, sn.z, 0.0f);
+        P.gb_gn[slot] = make_float4(gn.x, gn.y, gn.z, 0.0f);
+        vs_store(P.gb_vsA, P.gb_vsB, slot, vs);
+        meta.y = mi + 1;
+        meta.w = per_pixel;
+    }
+    meta.x = found ? prim : -1;
+    meta.z = found ? 1 : 0;
+    P.gb_meta[slot] = meta;
+    P.gb_view[slot] = make_float4(-d.x, -d.y, -d.z, 0.0f);
+}
+
+// ---- ReSTIR_DI_LightsPresampling (LightsPresampling.h:22-130) ------------------------
+__global__ __launch_bounds__(TB) void k_restir_presample(DevScene S, DevPaths P, const MptFrame* __restrict__ Fp) {
+    const MptFrame& F = *Fp;
+    const MptReSTIRDISettings& rd = F.render_settings.restir_di_settings;
+    const MptWorldSettings& w = F.world_settings;
+    if (S.n_emissive == 0 && w.ambient_light_type != MPT_AMBIENT_ENVMAP) return;
+    int x = blockIdx.x * TB + threadIdx.x;
+    if (x >= rd.number_of_subsets * rd.subset_size) return;
+    Rng rng = make_rng(pass_seed(F, (uint32_t)x, F.restir_di_seeds[0]));
+    float env_p = 0.0f;
+    if (w.ambient_light_type == MPT_AMBIENT_ENVMAP) env_p = S.n_emissive == 0 ? 1.0f : rd.envmap_candidate_probability;
+    int tri = -1;
+    v3 point = mk3(0, 0, 0), nrm = mk3(0, 0, 0);
+    Col rad = col(0.0f);
+    float pdf = 0.0f;
+    uint32_t flags = 0;
+    if (rng() < env_p) {
+        flags |= RF_ENVMAP;
+        v3 dir;
+        rad = env_sample(S, F, dir, pdf, rng);
+        point = mat_x_vec(w.world_to_envmap_matrix.m, dir);
+        pdf *= env_p;
+    } else {
+        float lp = 1.0f - env_p;
+        int ri = rng.random_index(S.n_emissive);
+        int t = S.emissive[ri];
+        int3 ti = tri_idx(S, t);
+        v3 A = ld3(S.pos, ti.x), B = ld3(S.pos, ti.y), C = ld3(S.pos, ti.z);
+        float r1 = rng(), r2 = rng();
+        float sr1 = sqrtf(r1);
+        float u = 1.0f - sr1, v = (1.0f - r2) * sr1;
+        v3 AB = B - A, AC = C - A;
+        v3 pt = A + AB * u + AC * v;
+        v3 nn = cross(AB, AC);
+        float ln = length(nn);
+        if (ln > 1.0e-6f) {
+            point = pt;
+            nrm = nn / ln;
+            tri = t;
+            pdf = 1.0f / (ln * 0.5f);
+            pdf /= (float)S.n_emissive;
+            pdf *= lp;
+            rad = emission_of(S.mats[S.mat_idx[t]]);
+        }
+    }
+    float4* o = P.rs_plights + 4 * (size_t)x;
+    o[0] = make_float4(__int_as_float(tri), point.x, point.y, point.z);
+    o[1] = make_float4(nrm.x, nrm.y, nrm.z, pdf);
+    o[2] = make_float4(rad.r, rad.g, rad.b, __uint_as_float(flags));
+}
+
+// ---- ReSTIR_DI_InitialCandidates (InitialCandidates.h:24-508) ------------------------
+template <int OVR>
+__global__ __launch_bounds__(TB) void k_restir_initial(DevScene S, DevPaths P, const MptFrame* __restrict__ Fp) {
+    __shared__ uint2 lds[LDS_STACK * TB];
+    const MptFrame& F = *Fp;
+    const MptReSTIRDISettings& rd = F.render_settings.restir_di_settings;
+    const MptWorldSettings& w = F.world_settings;
+    if (S.n_emissive == 0 && w.ambient_light_type != MPT_AMBIENT_ENVMAP) return;
+    const BCtx bc = make_bctx(S, F);
+    RRays rr{&S, lds, P.stack_spill + ((size_t)blockIdx.x * TB + threadIdx.x) * (2 * SPILL_DEPTH),
+             F.render_settings.do_alpha_testing, 0u, 5, 0, 0u, 0u};
+    const int W = F.res_x;
+    for (int pix = blockIdx.x * TB + threadIdx.x; pix < P.n; pix += gridDim.x * TB) {
+        RSurf g = gb_surface(S, P, pix, false);
+        if (is_emissive(*g.m)) continue;
+        uint32_t seed = pass_seed(F, (uint32_t)pix, F.restir_di_seeds[1]);
+        Rng rng = make_rng(seed);
+        if (!P.active[pix] || !P.gb_meta[pix].z) continue;
+        rr.pseed = seed;
+        rr.n = 0;
+        const int x = pix % W, y = pix / W;
+        int nl = rd.number_of_initial_light_candidates, nb = rd.number_of_initial_bsdf_candidates;
+        float env_p = 0.0f;
+        if (w.ambient_light_type == MPT_AMBIENT_ENVMAP) env_p = S.n_emissive == 0 ? 1.0f : rd.envmap_candidate_probability;
+        RResv r = rr_default();
+        v3 ep = g.p + g.sn * 1.0e-4f * 1.0f;
+        PEval pe;
+        bsdf_eval_pre<OVR>(bc, *g.m, g.vs, g.view, g.sn, pe);
+        for (int i = 0; i < nl; i++) {
+            // use_presampled_light_candidate (InitialCandidates.h:30-90)
+            int tcs = (x / rd.tile_size + y / rd.tile_size + 1) * (x / rd.tile_size + y / rd.tile_size) / 2 + y / rd.tile_size;
+            Rng subset_rng = make_rng(F.restir_di_seeds[1] * (uint32_t)(tcs + 1));
+            int subset = subset_rng.random_index(rd.number_of_subsets);
+            int li = rng.random_index(rd.subset_size);
+            const float4* pl = P.rs_plights + 4 * (size_t)(subset * rd.subset_size + li);
+            float4 p0 = pl[0], p1 = pl[1], p2 = pl[2];
+            int tri = __float_as_int(p0.x);
+            v3 point = mk3(p0.y, p0.z, p0.w);
+            uint32_t flags = __float_as_uint(p2.w);
+            Col rad = col(p2.x, p2.y, p2.z);
+            float pdf = p1.w, dist = 0.0f, target = 0.0f;
+            v3 tl;
+            if (flags & RF_ENVMAP) { tl = mat_x_vec(w.envmap_to_world_matrix.m, point); dist = 1.0e35f; }
+            else { tl = point - ep; dist = length(tl); tl = tl / dist; }
+            float cosv = dot(g.sn, tl);
+            if (!(flags & RF_ENVMAP)) {
+                float cl = absr(dot(mk3(p1.x, p1.y, p1.z), -tl));
+                pdf *= dist * dist;
+                pdf /= cl;
+                if (!min_contrib(F.render_settings.minimum_light_contribution, rad * cosv / pdf)) { r.M++; continue; }
+            }
+            float weight = 0.0f;
+            if (cosv > 0.0f && pdf > 0.0f) {
+                float bp;
+                VState tv = g.vs;
+                Col f = bsdf_eval_post<OVR>(bc, *g.m, tv, pe, g.sn, tl, bp);
+                Col lc = f * rad * cosv;
+                float tf = lum(lc);
+                if (min_contrib(F.render_settings.minimum_light_contribution, lc / pdf / bp)) {
+                    float mis = power_heuristic(pdf, nl, bp, nb);
+                    weight = mis * tf / pdf;
+                    target = tf;
+                }
+            }
+            rr_add(r, tri, point, target, flags, weight, rng);
+        }
+        for (int i = 0; i < nb; i++) {
+            // sample_bsdf_candidates (InitialCandidates.h:273-394)
+            float bpdf = 0.0f;
+            v3 dir;
+            VState tv = g.vs;
+            Col f = bsdf_sample<OVR>(bc, *g.m, tv, g.view, g.sn, g.gn, dir, bpdf, rng);
+            bool refr = dot(dir, g.view) < 0.0f;   // the reference tests against the view direction
+            if (!(bpdf > 0.0f)) continue;
+            THit h;
+            bool found = rr.closest(g.p, dir, g.last, h) && h.t < 1.0e35f - 1.0e-4f;
+            ShadowLightHit sh;
+            if (found) found = shadow_light_hit(S, make_float4(h.t, h.u, h.v, __uint_as_float((uint32_t)h.prim)), sh);
+            if (found && !is_black(sh.em)) {
+                float ce = absr(dot(g.sn, dir));
+                Col lc = f * sh.em * ce;
+                float tf = lum(lc);
+                float lpdf = 0.0f;
+                if (!refr) lpdf = pdf_emissive_hit(S, sh, dir);
+                if (!min_contrib(F.render_settings.minimum_light_contribution, lc / lpdf / bpdf)) { r.M++; continue; }
+                lpdf *= (1.0f - env_p);
+                float mis = power_heuristic(bpdf, nb, lpdf, nl);
+                float weight = mis * tf / bpdf;
+                rr_add(r, sh.prim, g.p + dir * sh.dist, tf, RF_UNOCCLUDED | (refr ? RF_BSDF_REFRACTION : 0u), weight, rng);
+            } else if (!found && w.ambient_light_type == MPT_AMBIENT_ENVMAP) {
+                float ce = maxr(0.0f, dot(g.sn, dir));
+                if (ce > 0.0f) {
+                    float epdf;
+                    Col er = env_eval(S, F, dir, epdf);
+                    Col ec = f * er * ce;
+                    if (!min_contrib(F.render_settings.minimum_light_contribution, ec / epdf / bpdf)) { r.M++; continue; }
+                    float tf = lum(ec);
+                    epdf *= env_p;
+                    float mis = power_heuristic(bpdf, nb, epdf, nl);
+                    float weight = mis * tf / bpdf;
+                    rr_add(r, -1, mat_x_vec(w.world_to_envmap_matrix.m, dir), tf, RF_ENVMAP | RF_UNOCCLUDED, weight, rng);
+                }
+            }
+        }
+        r.UCW = r.wsum == 0.0f ? 0.0f : 1.0f / r.target * r.wsum;   // end()
+        r.M = 1;
+        restir_visibility_reuse(F, rr, r, g.p + g.sn * 1.0e-4f, g.last);
+        rr_store(P.rs_init, pix, r);
+    }
+    count_pass_rays(P, rr.n_any, rr.n_closest);
+}
+
+// find_temporal_neighbor_index (Utils.h:371-421)
+DEV int restir_temporal_neighbor(const DevScene& S, const DevPaths& P, const MptFrame& F, v3 p, v3 n, const Mat& cm,
+                                 Rng& rng, int& px, int& py) {
+    const MptReSTIRDISettings& rd = F.render_settings.restir_di_settings;
+    int W = F.res_x, H = F.res_y;
+    v3 ss = mat_x_point(F.prev_camera.view_projection.m, p);
+    float sx = ss.x, sy = ss.y;
+    sx += 1.0f; sy += 1.0f;
+    sx *= 0.5f; sy *= 0.5f;
+    float fx = sx * (float)W, fy = sy * (float)H;
+    fx -= 0.5f; fy -= 0.5f;
+    int idx = -1;
+    bool use_prev = rd.do_temporal_reuse_pass;
+    for (int i = 0; i < rd.max_neighbor_search_count + 1; i++) {
+        float ox = 0.0f, oy = 0.0f;
+        if (i > 0) {
+            float a = rng() - 0.5f, b = rng() - 0.5f;
+            ox = a * (float)rd.neighbor_search_radius;
+            oy = b * (float)rd.neighbor_search_radius;
+        }
+        int qx = (int)roundf(fx + ox), qy = (int)roundf(fy + oy);
+        if (rd.use_permutation_sampling && i == 0) {
+            int bits = rd.permutation_sampling_random_bits;
+            int ax = bits & 3, ay = (bits >> 2) & 3;
+            qx += ax; qy += ay;
+            qx ^= 3; qy ^= 3;
+            qx -= ax; qy -= ay;
+        }
+        if (qx < 0 || qx >= W || qy < 0 || qy >= H) continue;
+        idx = qx + qy * W;
+        if (restir_similar(S, P, rd, idx, cm, p, n, use_prev)) break;
+        idx = -1;
+    }
+    px = (int)roundf(fx);
+    py = (int)roundf(fy);
+    return idx;
+}
+
+// ---- ReSTIR_DI_SpatiotemporalReuse (FusedSpatiotemporalReuse.h:112-586) ----------------
+template <int OVR>
+__global__ __launch_bounds__(TB) void k_restir_spatiotemporal(DevScene S, DevPaths P, const MptFrame* __restrict__ Fp) {
+    __shared__ uint2 lds[LDS_STACK * TB];
+    const MptFrame& F = *Fp;
+    const BCtx bc = make_bctx(S, F);
+    RRays rr{&S, lds, P.stack_spill + ((size_t)blockIdx.x * TB + threadIdx.x) * (2 * SPILL_DEPTH),
+             F.render_settings.do_alpha_testing, 0u, 6, 0, 0u, 0u};
+    const int W = F.res_x;
+    float4* tin = P.rs_tin;
+    for (int center = blockIdx.x * TB + threadIdx.x; center < P.n; center += gridDim.x * TB) {
+        MptReSTIRDISettings rd = F.render_settings.restir_di_settings;
+        rd.spatial_pass_index = 0;   // configure_spatial_pass_for_fused_spatiotemporal(0)
+        if (!P.active[center] || !P.gb_meta[center].z) continue;
+        uint32_t seed = pass_seed(F, (uint32_t)center, F.restir_di_seeds[2]);
+        Rng rng = make_rng(seed);
+        rr.pseed = seed;
+        rr.n = 0;
+        RSurf cs = gb_surface(S, P, center, false);
+        if (is_emissive(*cs.m)) continue;
+        if (rd.temporal_buffer_clear_requested) rr_store(tin, center, rr_default());
+        const bool use_prev = rd.do_temporal_reuse_pass;
+        int tpx, tpy;
+        int tidx = restir_temporal_neighbor(S, P, F, cs.p, cs.sn, *cs.m, rng, tpx, tpy);
+        RResv tres = rr_default();
+        tres.tri = -1;
+        if (tidx != -1 && !F.render_settings.freeze_random) tres = rr_load(tin, tidx);
+        if ((tidx == -1 || tres.M <= 1) && rd.do_disocclusion_reuse_boost) rd.reuse_neighbor_count = rd.disocclusion_reuse_count;
+        float rot = rd.do_neighbor_rotation ? TWO_PI * rng() : 0.0f;
+        float cr = pcos(rot), sr = psin(rot);
+        const int reuse = rd.reuse_neighbor_count;
+        int cache = 0, vcount = 0, vM = 0;
+        for (int k = 0; k < reuse; k++) {
+            int ni = restir_spatial_neighbor(P, F, k, reuse, rd.reuse_radius, tpx, tpy, cr, sr, F.restir_di_seeds[2]);
+            if (ni == -1) continue;
+            if (!restir_similar(S, P, rd, ni, *cs.m, cs.sp, cs.sn, use_prev)) continue;
+            vM += rr_load(tin, ni).M;
+            vcount++;
+            cache |= 1 << k;
+        }
+        const bool temporal_ok = tidx != -1 && tres.M > 0;
+        if (temporal_ok) { vcount++; vM += tres.M; }
+        RResv o = rr_default();
+        const RResv ic = rr_load(P.rs_init, center);
+        PairwiseMIS mis{0.0f};
+        if (temporal_ok) {
+            RSurf ts = gb_surface(S, P, tidx, use_prev);
+            float tfc = 0.0f;
+            if (tres.UCW > 0.0f) tfc = restir_target(S, F, bc, rr, tres.tri, tres.point, tres.flags, cs, true, OVR);
+            float jac = 1.0f;
+            if (tfc > 0.0f && tres.UCW > 0.0f && !(tres.flags & RF_ENVMAP)) {
+                jac = restir_jacobian(S, tres, cs.sp, ts.sp - ts.sn * 1.0e-4f);
+                if (jac == -1.0f) jac = 0.0f;
+            }
+            bool update_mc = ic.M > 0 && ic.UCW > 0.0f;
+            float wgt = mis.weight(S, F, bc, rr, rd, tres, ic, tfc, ts, vcount, vM, update_mc, false, OVR);
+            if (rr_combine(o, tres, wgt, tfc, jac, rng)) o.flags |= RF_UNOCCLUDED;
+        }
+        int start = vM == 0 ? reuse : 0;
+        for (int k = start; k < reuse + 1; k++) {
+            if (k < reuse && reuse <= 32 && (cache & (1 << k)) == 0) continue;
+            int ni = k == reuse ? center : restir_spatial_neighbor(P, F, k, reuse, rd.reuse_radius, tpx, tpy, cr, sr, F.restir_di_seeds[2]);
+            if (ni == -1) continue;
+            if (k < reuse && reuse > 32 && !restir_similar(S, P, rd, ni, *cs.m, cs.sp, cs.sn, use_prev)) continue;
+            RResv nr = k == reuse ? ic : rr_load(tin, ni);
+            float tfc = 0.0f;
+            bool vis = spatial_visibility(rd, k, reuse);
+            if (nr.UCW > 0.0f) {
+                if (k == reuse) tfc = nr.target;
+                else tfc = restir_target(S, F, bc, rr, nr.tri, nr.point, nr.flags, cs, vis, OVR);
+            }
+            float jac = 1.0f;
+            if (tfc > 0.0f && nr.UCW > 0.0f && k != reuse && !(nr.flags & RF_ENVMAP)) {
+                RSurf ns = gb_surface(S, P, ni, use_prev);
+                jac = restir_jacobian(S, nr, cs.sp, ns.sp);
+                if (jac == -1.0f) { o.M += nr.M; continue; }
+            }
+            bool update_mc = ic.M > 0 && ic.UCW > 0.0f;
+            float wgt;
+            if (nr.UCW == 0.0f && !update_mc) wgt = 1.0f;
+            else {
+                RSurf ns = gb_surface(S, P, ni, use_prev);
+                wgt = mis.weight(S, F, bc, rr, rd, nr, ic, tfc, ns, vcount, vM, update_mc, k == reuse, OVR);
+            }
+            if (rr_combine(o, nr, wgt, tfc, jac, rng)) {
+                if (vis) o.flags |= RF_UNOCCLUDED;
+                else if (k == reuse) o.flags |= nr.flags & RF_UNOCCLUDED;
+                else o.flags &= ~RF_UNOCCLUDED;
+            }
+        }
+        rr_end_normalized(o);
+        if (rd.do_temporal_reuse_pass || rd.number_of_passes - 1 != rd.spatial_pass_index)
+            restir_visibility_reuse(F, rr, o, cs.sp, cs.last);
+        if (rd.m_cap > 0) o.M = imin(o.M, rd.m_cap);
+        rr_store(P.rs_out, center, o);
+    }
+    count_pass_rays(P, rr.n_any, rr.n_closest);
+}
+
+// ---- ReSTIR_DI_SpatialReuse (SpatialReuse.h:52-348) ------------------------------------
+template <int OVR>
+__global__ __launch_bounds__(TB) void k_restir_spatial(DevScene S, DevPaths P, const MptFrame* __restrict__ Fp, int pass,
+                                                       const float4* __restrict__ in, float4* out) {
+    __shared__ uint2 lds[LDS_STACK * TB];
+    const MptFrame& F = *Fp;
+    const BCtx bc = make_bctx(S, F);
+    RRays rr{&S, lds, P.stack_spill + ((size_t)blockIdx.x * TB + threadIdx.x) * (2 * SPILL_DEPTH),
+             F.render_settings.do_alpha_testing, 0u, 7, 0, 0u, 0u};
+    const int W = F.res_x;
+    const uint32_t pass_rs = F.restir_di_seeds[3 + pass];
+    for (int center = blockIdx.x * TB + threadIdx.x; center < P.n; center += gridDim.x * TB) {
+        MptReSTIRDISettings rd = F.render_settings.restir_di_settings;
+        rd.spatial_pass_index = pass;
+        if (!P.active[center] || !P.gb_meta[center].z) continue;
+        uint32_t seed = pass_seed(F, (uint32_t)center, pass_rs);
+        Rng rng = make_rng(seed);
+        rr.pseed = seed;
+        rr.n = 0;
+        const int x = center % W, y = center / W;
+        RResv o = rr_default();
+        RSurf cs = gb_surface(S, P, center, false);
+        if (is_emissive(*cs.m)) continue;
+        float rot = rd.do_neighbor_rotation ? TWO_PI * rng() : 0.0f;
+        float cr = pcos(rot), sr = psin(rot);
+        const RResv cres = rr_load(in, center);
+        if (cres.M <= 1 && rd.do_disocclusion_reuse_boost) rd.reuse_neighbor_count = rd.disocclusion_reuse_count;
+        const int reuse = rd.reuse_neighbor_count;
+        int cache = 0, vcount = 0, vM = 0;
+        for (int k = 0; k < reuse; k++) {
+            int ni = restir_spatial_neighbor(P, F, k, reuse, rd.reuse_radius, x, y, cr, sr, pass_rs);
+            if (ni == -1) continue;
+            if (!restir_similar(S, P, rd, ni, *cs.m, cs.sp, cs.sn, false)) continue;
+            vM += rr_load(in, ni).M;
+            vcount++;
+            cache |= 1 << k;
+        }
+        PairwiseMIS mis{0.0f};
+        int start = vM == 0 ? reuse : 0;
+        for (int k = start; k < reuse + 1; k++) {
+            if (k < reuse && reuse <= 32 && (cache & (1 << k)) == 0) continue;
+            int ni = restir_spatial_neighbor(P, F, k, reuse, rd.reuse_radius, x, y, cr, sr, pass_rs);
+            if (ni == -1) continue;
+            if (k < reuse && reuse > 32 && !restir_similar(S, P, rd, ni, *cs.m, cs.sp, cs.sn, false)) continue;
+            RResv nr = rr_load(in, ni);
+            float tfc = 0.0f;
+            bool vis = spatial_visibility(rd, k, reuse);
+            if (nr.UCW > 0.0f) {
+                if (k == reuse) tfc = nr.target;
+                else tfc = restir_target(S, F, bc, rr, nr.tri, nr.point, nr.flags, cs, vis, OVR);
+            }
+            float jac = 1.0f;
+            if (tfc > 0.0f && nr.UCW > 0.0f && k != reuse && !(nr.flags & RF_ENVMAP)) {
+                float4 np = P.gb_pos[ni];
+                jac = restir_jacobian(S, nr, cs.sp, mk3(np.x, np.y, np.z));
+                if (jac == -1.0f) { o.M += nr.M; continue; }
+            }
+            bool update_mc = cres.M > 0 && cres.UCW > 0.0f;
+            RSurf ns = gb_surface(S, P, ni, false);
+            float wgt = mis.weight(S, F, bc, rr, rd, nr, cres, tfc, ns, vcount, vM, update_mc, k == reuse, OVR);
+            if (rr_combine(o, nr, wgt, tfc, jac, rng)) {
+                if (vis) o.flags |= RF_UNOCCLUDED;
+                else if (k == reuse) o.flags |= nr.flags & RF_UNOCCLUDED;
+                else o.flags &= ~RF_UNOCCLUDED;
+            }
+        }
+        rr_end_normalized(o);
+        if (rd.do_temporal_reuse_pass || rd.number_of_passes - 1 != rd.spatial_pass_index)
+            restir_visibility_reuse(F, rr, o, cs.sp, cs.last);
+        if (rd.m_cap > 0) o.M = imin(o.M, rd.m_cap);
+        rr_store(out, center, o);
+    }
+    count_pass_rays(P, rr.n_any, rr.n_closest);
+}
+
+// CameraRays' reset / previous-frame G-buffer copy for LSS_RESTIR_DI (CameraRays.h:19-34, 78-91)
+__global__ __launch_bounds__(TB) void k_restir_frame_begin(DevPaths P, const MptFrame* __restrict__ Fp) {
+    const MptFrame& F = *Fp;
+    const MptRenderSettings& rs = F.render_settings;
+    int i = blockIdx.x * TB + threadIdx.x;
+    if (i >= P.n) return;
+    if (rs.restir_di_settings.do_temporal_reuse_pass) {
+        P.pgb_pos[i] = P.gb_pos[i]; P.pgb_sn[i] = P.gb_sn[i]; P.pgb_gn[i] = P.gb_gn[i]; P.pgb_view[i] = P.gb_view[i];
+        int4 meta = P.gb_meta[i];
+        P.pgb_meta[i] = meta;
+        P.pgb_vsA[i] = P.gb_vsA[i]; P.pgb_vsB[i] = P.gb_vsB[i];
+        if (meta.w) P.pgb_mat[i] = P.gb_mat[i];
+    }
+    if ((rs.sample_number == 0 || rs.need_to_reset) && rs.accumulate) {
+        rr_store(P.rs_init, i, rr_default());
+        rr_store(P.rs_sp1, i, rr_default());
+        rr_store(P.rs_sp2, i, rr_default());
+    }
+}
+
+__global__ void k_restir_fill(float4* r, int n) {   // default reservoirs (Reservoir.h:166-170)
+    int i = blockIdx.x * TB + threadIdx.x;
+    if (i < n) rr_store(r, i, rr_default());
+}
+__global__ void k_restir_fill_lights(float4* l, int n) {   // default presampled lights
+    int i = blockIdx.x * TB + threadIdx.x;
+    if (i < n) {
+        l[4 * (size_t)i + 0] = make_float4(__int_as_float(-1), 0.0f, 0.0f, 0.0f);
+        l[4 * (size_t)i + 1] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        l[4 * (size_t)i + 2] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        l[4 * (size_t)i + 3] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    }
+}

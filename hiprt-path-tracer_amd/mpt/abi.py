@@ -321,7 +321,8 @@ class Frame(C.Structure):
     _fields_ = [("render_settings", RenderSettings), ("world_settings", WorldSettings),
                 ("current_camera", Camera), ("prev_camera", Camera), ("options", KernelOptions),
                 ("bsdf_flags", BSDFFlags), ("random_seed", u32), ("res_x", i32), ("res_y", i32),
-                ("band_height", i32), ("band_index", i32), ("band_count", i32)]
+                ("band_height", i32), ("band_index", i32), ("band_count", i32),
+                ("camera_random_seed", u32), ("restir_di_seeds", u32 * 8)]
 
 
 class Scene(C.Structure):
@@ -351,7 +352,7 @@ class Stats(C.Structure):
                 ("stage_tris", C.c_uint64 * 3), ("stage_ms", C.c_double * 3),
                 ("stage_launches", u32 * 3), ("shade_launches", u32), ("camera_ms", C.c_double),
                 ("shade_ms", C.c_double), ("resolve_ms", C.c_double), ("accumulate_ms", C.c_double),
-                ("compact_ms", C.c_double)]
+                ("compact_ms", C.c_double), ("restir_ms", C.c_double)]
 
 
 BSDF_NONE, BSDF_LAMBERTIAN = 0, 1

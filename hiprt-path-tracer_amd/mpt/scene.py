@@ -403,8 +403,38 @@ def cpu_seed_schedule(nframes, first_sample=0):
     return out
 
 
+def _xorshift32(x):
+    x ^= (x << 13) & 0xFFFFFFFF
+    x ^= x >> 17
+    x ^= (x << 5) & 0xFFFFFFFF
+    return x & 0xFFFFFFFF
+
+
+def gpu_seed_schedule(nframes, restir_spatial_passes=None, first_sample=0):
+    """Per-sample seeds as GPURenderer::render draws them from m_rng (seeded 42,
+    GPURenderer.cpp:50, 424-486): the camera launch, then -- with ReSTIR DI -- lights
+    presampling, initial candidates, the fused spatiotemporal pass and its permutation
+    bits, one per extra spatial pass (ReSTIRDIRenderPass.cpp:233-264, 369-507), then the
+    path-tracing launch.  Returns dicts with sample_number, camera_random_seed,
+    restir_di_seeds (8, zero padded) and random_seed (path tracing)."""
+    rng = 42
+    out = []
+    for f in range(nframes):
+        rng = _xorshift32(rng)
+        cam = rng
+        rseeds = []
+        if restir_spatial_passes is not None:
+            for _ in range(4 + max(0, restir_spatial_passes - 1)):
+                rng = _xorshift32(rng)
+                rseeds.append(rng)
+        rng = _xorshift32(rng)
+        out.append({"sample_number": first_sample + f, "camera_random_seed": cam,
+                    "restir_di_seeds": (rseeds + [0] * 8)[:8], "random_seed": rng})
+    return out
+
+
 def make_frame(camera, width, height, options=None, settings=None, world=None, flags=None,
-               sample_number=0, random_seed=42, band=(1, 0, 1)):
+               sample_number=0, random_seed=42, band=(1, 0, 1), camera_random_seed=0, restir_di_seeds=None):
     fr = abi.Frame()
     fr.render_settings = settings if settings is not None else parity_settings()
     fr.render_settings.sample_number = sample_number
@@ -418,6 +448,13 @@ def make_frame(camera, width, height, options=None, settings=None, world=None, f
     fr.random_seed = random_seed
     fr.res_x, fr.res_y = width, height
     fr.band_height, fr.band_index, fr.band_count = band
+    fr.camera_random_seed = camera_random_seed
+    if restir_di_seeds is not None:
+        for i, v in enumerate(list(restir_di_seeds)[:8]):
+            fr.restir_di_seeds[i] = v
+        # ReSTIRDIRenderPass::configure_temporal_pass_for_fused_spatiotemporal draws the
+        # permutation-sampling bits right after the pass seed (ReSTIRDIRenderPass.cpp:416)
+        fr.render_settings.restir_di_settings.permutation_sampling_random_bits = abi.C.c_int32(restir_di_seeds[3]).value
     return fr
 
 

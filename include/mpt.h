@@ -315,6 +315,16 @@ typedef struct MptFrame {
      * the whole frame.  Per-pixel RNG seeds use the global pixel index so a
      * partitioned render is bit-identical to a single-device one. */
     int32_t band_height, band_index, band_count;
+    /* Seed of the CameraRays launch (GPURenderer::launch_camera_rays draws a new
+     * m_rng.xorshift32() per launch, GPURenderer.cpp:468-474); 0 = use random_seed for
+     * the camera rays too (CPURenderer: one seed per sample, CPURenderer.cpp:271-287). */
+    uint32_t camera_random_seed;
+    /* LSS_RESTIR_DI: the seeds ReSTIRDIRenderPass::launch draws from the renderer's RNG
+     * (ReSTIRDIRenderPass.cpp:233-264, 369-507), in order: [0] lights presampling,
+     * [1] initial candidates, [2] fused spatiotemporal pass, [3] the permutation-sampling
+     * bits drawn next (the kernels read them from render_settings.restir_di_settings,
+     * where the caller stores them as the reference does), [3 + i] spatial pass i >= 1. */
+    uint32_t restir_di_seeds[8];
 } MptFrame;
 
 /* Scene arrays as produced by the reference's SceneParser (Scene/SceneParser.h:80-131). */
@@ -377,6 +387,7 @@ typedef struct MptStats {
     double resolve_ms;
     double accumulate_ms;
     double compact_ms;
+    double restir_ms;           /* ReSTIR DI passes (presampling .. spatial reuse) */
 } MptStats;
 
 #define MPT_FB_COLOR 0        /* 'pixels': running SUM of samples (RenderData.h:34-36) */

@@ -307,6 +307,7 @@ struct Ctx {
     bool alpha = false;
     uint32_t pseed = 0;
     int bounce = 0;
+    struct OResv* restir_out = nullptr;   // this pixel's ReSTIR DI output reservoir (bounce 0)
     uint32_t akey(int kind, int iter = 0) const { return alpha_key(pseed, bounce, kind, iter); }
 };
 
@@ -759,9 +760,11 @@ Col sample_lights_ris(Ctx& c, const Payload& pl, const HitInfo& hi, f3 view, Rng
     return fc;
 }
 
+Col restir_final_shading(Ctx& c, struct OResv& res, const Payload& pl, const HitInfo& hi, f3 view);
 Col sample_one_light(Ctx& c, const Payload& pl, const HitInfo& hi, f3 view, Rng& rng, int bounce) {
     const OScene& s = *c.s;
-    if (s.n_emissive == 0) return Col(0.0f);
+    const bool restir = c.lss == MPT_LSS_RESTIR_DI;
+    if (s.n_emissive == 0 && !(c.f->world_settings.ambient_light_type == MPT_AMBIENT_ENVMAP && restir)) return Col(0.0f);
     if (c.f->bsdf_flags.white_furnace_mode && c.f->bsdf_flags.white_furnace_mode_turn_off_emissives) return Col(0.0f);
     if (is_emissive(pl.material)) {
         if (pl.material.emissive_texture_used && bounce > 0) return emission_of(pl.material);
@@ -770,6 +773,13 @@ Col sample_one_light(Ctx& c, const Payload& pl, const HitInfo& hi, f3 view, Rng&
     if (c.lss == MPT_LSS_NO_DIRECT_LIGHT_SAMPLING) return Col(0.0f);
     Col dl;
     int n = c.f->render_settings.number_of_light_samples;
+    if (restir) {
+        // sample_one_light_ReSTIR_DI (Lights.h:243-275): the reservoir at bounce 0, RIS after
+        if (bounce == 0) return restir_final_shading(c, *c.restir_out, pl, hi, view);
+        if (s.n_emissive == 0) return Col(0.0f);   // sample_lights_RIS (RIS.h:292-302)
+        for (int i = 0; i < n; i++) dl += sample_lights_ris(c, pl, hi, view, rng);
+        return dl / (float)n;
+    }
     for (int i = 0; i < n; i++) {
         if (c.lss == MPT_LSS_UNIFORM_ONE_LIGHT) dl += sample_one_light_no_mis(c, pl, hi, view, rng);
         else if (c.lss == MPT_LSS_BSDF) dl += sample_one_light_bsdf(c, pl, hi, view, rng);
@@ -877,7 +887,7 @@ Col sample_environment_map(Ctx& c, const Payload& pl, const HitInfo& hi, f3 view
     if (w.ambient_light_type != MPT_AMBIENT_ENVMAP || c.f->bsdf_flags.white_furnace_mode) return Col(0.0f);
     if (is_emissive(pl.material)) return Col(0.0f);
     if (w.envmap_intensity <= 0.0f) return Col(0.0f);
-    (void)bounce;
+    if (bounce == 0 && c.lss == MPT_LSS_RESTIR_DI) return Col(0.0f);   // Envmap.h:236-238
     if (c.f->options.envmap_sampling == MPT_ESS_NO_SAMPLING) return Col(0.0f);
     float epdf;
     f3 sdir;
@@ -946,13 +956,19 @@ void camera_ray(const MptCamera& cam, float x, float y, int rx, int ry, f3& o, f
 struct PixelOut { Col color; Col albedo; f3 normal; bool valid; };
 
 // CameraRays (CameraRays.h:45-179) followed by FullPathTracer (FullPathTracer.h:99-327)
-PixelOut render_pixel(Ctx& c, int x, int y, GB& gb) {
+inline uint32_t frame_pixel_seed(const MptFrame& f, uint32_t pix, uint32_t random_seed) {
+    const MptRenderSettings& rs = f.render_settings;
+    return rs.freeze_random ? wang_hash(pix + 1u) : wang_hash((pix + 1u) * (uint32_t)(rs.sample_number + 1) * random_seed);
+}
+
+// CameraRays (CameraRays.h:127-179): primary ray + G-buffer write.  The seed is the
+// camera launch's (GPURenderer::launch_camera_rays) when the frame carries one, else
+// the frame seed (CPURenderer: one seed per sample).
+void camera_pixel(Ctx& c, int x, int y, GB& gb) {
     const MptFrame& f = *c.f;
-    { static int dbg_pix = getenv("ORACLE_DBG_PIX") ? atoi(getenv("ORACLE_DBG_PIX")) : -1;
-      g_dbg = (int)((uint32_t)x + (uint32_t)y * (uint32_t)f.res_x) == dbg_pix; }
     const MptRenderSettings& rs = f.render_settings;
     uint32_t pix = (uint32_t)x + (uint32_t)y * (uint32_t)f.res_x;
-    uint32_t seed = rs.freeze_random ? wang_hash(pix + 1u) : wang_hash((pix + 1u) * (uint32_t)(rs.sample_number + 1) * f.random_seed);
+    uint32_t seed = frame_pixel_seed(f, pix, f.camera_random_seed ? f.camera_random_seed : f.random_seed);
     c.alpha = rs.do_alpha_testing;
     c.pseed = seed;
     c.bounce = 0;
@@ -977,7 +993,19 @@ PixelOut render_pixel(Ctx& c, int x, int y, GB& gb) {
         gb.view = -d;
         gb.hit = found;
     }
-    // ---- FullPathTracer
+}
+
+// FullPathTracer (FullPathTracer.h:99-327) from the G-buffer
+PixelOut path_pixel(Ctx& c, int x, int y, GB& gb) {
+    const MptFrame& f = *c.f;
+    { static int dbg_pix = getenv("ORACLE_DBG_PIX") ? atoi(getenv("ORACLE_DBG_PIX")) : -1;
+      g_dbg = (int)((uint32_t)x + (uint32_t)y * (uint32_t)f.res_x) == dbg_pix; }
+    const MptRenderSettings& rs = f.render_settings;
+    uint32_t pix = (uint32_t)x + (uint32_t)y * (uint32_t)f.res_x;
+    uint32_t seed = frame_pixel_seed(f, pix, f.random_seed);
+    c.alpha = rs.do_alpha_testing;
+    c.pseed = seed;
+    c.bounce = 0;
     Rng rng(seed);
     Col albedo(0.0f);
     f3 dn = mk3(0, 0, 0);
@@ -1050,6 +1078,8 @@ PixelOut render_pixel(Ctx& c, int x, int y, GB& gb) {
     po.normal = dn;
     return po;
 }
+
+#include "oracle_restir.h"
 
 }  // namespace
 
@@ -1157,46 +1187,65 @@ inline bool adaptive_sampling(const MptRenderSettings& rs, const float* px, floa
 
 /* as_count / as_sqlum / as_conv: the adaptive-sampling buffers (one per pixel of the
  * partition, kept by the caller across calls); status[0] converged count, status[1]
- * one ray active.  All four may be NULL when adaptive sampling is off. */
+ * one ray active.  All four may be NULL when adaptive sampling is off.
+ * Per frame: CameraRays over every pixel (G-buffer), the ReSTIR DI passes when
+ * LSS_RESTIR_DI (ReSTIRDIRenderPass::launch), then FullPathTracer + accumulation. */
 int oracle_render(OracleScene* sc, const MptFrame* frames, int nframes, float* sum_rgb, float* albedo, float* normals,
                   uint64_t* rays, int nthreads, int32_t* as_count, float* as_sqlum, int32_t* as_conv, uint32_t* status) {
     OScene& s = *reinterpret_cast<OScene*>(sc);
     if (nframes <= 0) return 0;
     const MptFrame& f0 = frames[0];
+    const bool restir = f0.options.direct_light_sampling == MPT_LSS_RESTIR_DI;
     if ((has_adaptive_buffers(f0.render_settings) && !(as_count && as_sqlum && as_conv && status)) ||
         f0.render_settings.wants_render_low_resolution ||
-        f0.options.direct_light_sampling == MPT_LSS_RESTIR_DI ||
+        (restir && (f0.band_count != 1 || !f0.render_settings.restir_di_settings.do_fused_spatiotemporal ||
+                    f0.render_settings.number_of_light_samples != 1)) ||
         (f0.options.envmap_sampling == MPT_ESS_BINARY_SEARCH && s.env_rgba && !s.env_cdf))
         return -4;
     std::vector<int> rows;
     for (int y = 0; y < f0.res_y; y++)
         if ((y / f0.band_height) % f0.band_count == f0.band_index) rows.push_back(y);
     int W = f0.res_x;
-    std::vector<GB> gbuf((size_t)W * rows.size(), GB{});
+    size_t npx = (size_t)W * rows.size();
+    std::vector<GB> gbuf(npx, GB{}), gprev(npx, GB{});
+    std::vector<uint8_t> active(npx, 0);
+    RestirBuffers B;
+    if (restir) { B.init.assign(npx, OResv()); B.sp1.assign(npx, OResv()); B.sp2.assign(npx, OResv()); B.output = &B.sp1; }
     uint64_t rc = 0, ra = 0;
     if (nthreads <= 0) nthreads = omp_get_max_threads();
+    auto make_ctx = [&](Ctx& c, const MptFrame& f) {
+        c.s = &s;
+        c.f = &f;
+        c.bc.materials = s.mats;
+        c.bc.luts = s.luts;
+        c.bc.clearcoat_compensation = f.bsdf_flags.clearcoat_compensation_approximation;
+        c.bc.ggx_masking = f.bsdf_flags.ggx_masking_shadowing;
+        c.bc.white_furnace = f.bsdf_flags.white_furnace_mode;
+        c.override_ = f.options.bsdf_override;
+        c.lss = f.options.direct_light_sampling;
+        c.alpha = f.render_settings.do_alpha_testing;
+    };
     for (int fi = 0; fi < nframes; fi++) {
         const MptFrame& f = frames[fi];
+        const MptRenderSettings& rs = f.render_settings;
+        const bool as = has_adaptive_buffers(rs);
+        const bool use_prev = restir && rs.restir_di_settings.do_temporal_reuse_pass;   // use_prev_frame_g_buffer
+        // ---- CameraRays over all pixels (CameraRays.h:45-179)
 #pragma omp parallel for schedule(dynamic) reduction(+ : rc, ra) num_threads(nthreads)
         for (int r = 0; r < (int)rows.size(); r++) {
             Ctx c;
-            c.s = &s;
-            c.f = &f;
-            c.bc.materials = s.mats;
-            c.bc.luts = s.luts;
-            c.bc.clearcoat_compensation = f.bsdf_flags.clearcoat_compensation_approximation;
-            c.bc.ggx_masking = f.bsdf_flags.ggx_masking_shadowing;
-            c.bc.white_furnace = f.bsdf_flags.white_furnace_mode;
-            c.override_ = f.options.bsdf_override;
-            c.lss = f.options.direct_light_sampling;
+            make_ctx(c, f);
             int y = rows[r];
-            const MptRenderSettings& rs = f.render_settings;
-            const bool as = has_adaptive_buffers(rs);
             for (int x = 0; x < W; x++) {
                 size_t o = (size_t)r * W + x;
                 float* p = sum_rgb + 3 * o;
+                if (use_prev) gprev[o] = gbuf[o];
+                if ((rs.sample_number == 0 || rs.need_to_reset) && restir && rs.accumulate) {
+                    B.init[o] = OResv(); B.sp1[o] = OResv(); B.sp2[o] = OResv();   // reset_render (CameraRays.h:19-34)
+                }
+                active[o] = 1;
                 if (as) {
-                    // CameraRays: reset_render + adaptive gate (CameraRays.h:19-43, 88-125)
+                    // reset_render + adaptive gate (CameraRays.h:35-43, 88-125)
                     if (rs.sample_number == 0 || rs.need_to_reset) { as_count[o] = 0; as_sqlum[o] = 0.0f; as_conv[o] = -1; }
                     bool converged = false;
                     bool needed = adaptive_sampling(rs, p, as_sqlum[o], as_count[o], as_conv[o], converged);
@@ -1207,20 +1256,67 @@ int oracle_render(OracleScene* sc, const MptFrame* frames, int nframes, float* s
                     if (!needed) {
                         Col cc = Col(p[0], p[1], p[2]) / (float)rs.sample_number * (float)(rs.sample_number + 1);
                         p[0] = cc.r; p[1] = cc.g; p[2] = cc.b;
+                        active[o] = 0;
                         continue;
                     }
                     as_count[o]++;
                 }
-                PixelOut po = render_pixel(c, x, y, gbuf[o]);
+                camera_pixel(c, x, y, gbuf[o]);
+            }
+            rc += c.rays_closest;
+            ra += c.rays_any;
+        }
+        // ---- ReSTIR DI (ReSTIRDIRenderPass::launch, ReSTIRDIRenderPass.cpp:233-264, 480-507)
+        if (restir) {
+            RestirPassCtx R{f, B, gbuf, gprev, active, as ? as_conv : nullptr};
+            {
+                Ctx c;
+                make_ctx(c, f);
+                restir_presample(c, R);
+            }
+            auto per_pixel = [&](auto fn) {
+#pragma omp parallel for schedule(dynamic) reduction(+ : rc, ra) num_threads(nthreads)
+                for (int y = 0; y < f.res_y; y++) {
+                    Ctx c;
+                    make_ctx(c, f);
+                    for (int x = 0; x < W; x++) fn(c, x, y);
+                    rc += c.rays_closest;
+                    ra += c.rays_any;
+                }
+            };
+            per_pixel([&](Ctx& c, int x, int y) { restir_initial(c, R, x, y); });
+            // fused spatiotemporal: temporal input = last output, spatial output = the other buffer
+            std::vector<OResv>* tin = B.output;
+            std::vector<OResv>* out = tin == &B.sp1 ? &B.sp2 : &B.sp1;
+            per_pixel([&](Ctx& c, int x, int y) { restir_spatiotemporal(c, R, x, y, *tin, *out); });
+            for (int pass = 1; pass < rs.restir_di_settings.number_of_passes; pass++) {
+                std::vector<OResv>* in = out;
+                out = in == &B.sp1 ? &B.sp2 : &B.sp1;
+                per_pixel([&](Ctx& c, int x, int y) { restir_spatial(c, R, x, y, pass, *in, *out); });
+            }
+            B.output = out;
+        }
+        // ---- FullPathTracer + accumulation (FullPathTracer.h:99-327)
+#pragma omp parallel for schedule(dynamic) reduction(+ : rc, ra) num_threads(nthreads)
+        for (int r = 0; r < (int)rows.size(); r++) {
+            Ctx c;
+            make_ctx(c, f);
+            int y = rows[r];
+            for (int x = 0; x < W; x++) {
+                size_t o = (size_t)r * W + x;
+                if (!active[o]) continue;
+                float* p = sum_rgb + 3 * o;
+                if (restir) c.restir_out = &(*B.output)[o];
+                PixelOut po = path_pixel(c, x, y, gbuf[o]);
                 if (!po.valid) continue;   // sanity_check fails -> no buffer write (FullPathTracer.h:293-294)
                 if (status) status[1] = 1u;
                 if (as) { float l = po.color.luminance(); as_sqlum[o] += l * l; }
-                if (f.render_settings.sample_number == 0) { p[0] = po.color.r; p[1] = po.color.g; p[2] = po.color.b; }
+                if (rs.sample_number == 0) { p[0] = po.color.r; p[1] = po.color.g; p[2] = po.color.b; }
                 else { p[0] += po.color.r; p[1] += po.color.g; p[2] += po.color.b; }
-                float cnt = (float)f.render_settings.denoiser_AOV_accumulation_counter;
+                float cnt = (float)rs.denoiser_AOV_accumulation_counter;
                 if (albedo) {
                     float* a = albedo + 3 * o;
-                    if (f.render_settings.sample_number == 0) { a[0] = po.albedo.r; a[1] = po.albedo.g; a[2] = po.albedo.b; }
+                    if (rs.sample_number == 0) { a[0] = po.albedo.r; a[1] = po.albedo.g; a[2] = po.albedo.b; }
                     else {
                         a[0] = (a[0] * cnt + po.albedo.r) / (cnt + 1.0f);
                         a[1] = (a[1] * cnt + po.albedo.g) / (cnt + 1.0f);
@@ -1229,7 +1325,7 @@ int oracle_render(OracleScene* sc, const MptFrame* frames, int nframes, float* s
                 }
                 if (normals) {
                     float* nn = normals + 3 * o;
-                    if (f.render_settings.sample_number == 0) { nn[0] = po.normal.x; nn[1] = po.normal.y; nn[2] = po.normal.z; }
+                    if (rs.sample_number == 0) { nn[0] = po.normal.x; nn[1] = po.normal.y; nn[2] = po.normal.z; }
                     else {
                         f3 acc = (mk3(nn[0], nn[1], nn[2]) * cnt + po.normal) / (cnt + 1.0f);
                         float len = length(acc);

@@ -213,7 +213,7 @@ def test_unsupported_options_fail_loudly(scenes, luts):
     with pytest.raises(mpt.MptError) as e:
         r.render(f)
     assert e.value.code == -4
-    f = frames(sd, 16, 16, 1, lss=abi.LSS_RESTIR_DI)[0]
+    f = frames(sd, 16, 16, 1, lss=abi.LSS_RESTIR_DI, band=(8, 0, 2))[0]   # ReSTIR DI needs the whole frame
     with pytest.raises(mpt.MptError):
         r.render(f)
 
