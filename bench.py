@@ -43,13 +43,13 @@ BAND_H = 8
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--workload", default="c3", choices=["c2", "c3"])
+    ap.add_argument("--workload", default="c3", choices=["c2", "c3", "c4"])
     ap.add_argument("--steps", type=int, default=None, help="default: the workload's spp (c3 256, c2 64)")
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--scene", default=None, help="c2: a glTF of data/scenes (default cornell_pbr)")
-    ap.add_argument("--strategy", default=None, choices=["mis", "ris", "uniform", "bsdf"],
+    ap.add_argument("--strategy", default=None, choices=["mis", "ris", "uniform", "bsdf", "restir"],
                     help="default: c3 ris (reference default), c2 mis")
     ap.add_argument("--bounces", type=int, default=3)
     ap.add_argument("--bsdf", default="principled", choices=["principled", "lambert"])
@@ -59,11 +59,20 @@ def parse():
 
 
 LSS = {"mis": abi.LSS_MIS_LIGHT_BSDF, "ris": abi.LSS_RIS_BSDF_AND_LIGHT, "uniform": abi.LSS_UNIFORM_ONE_LIGHT,
-       "bsdf": abi.LSS_BSDF}
+       "bsdf": abi.LSS_BSDF, "restir": abi.LSS_RESTIR_DI}
 
 
 def frames_for(cam, W, H, opt, band, n, first=0, bounces=3, world=None, alpha=False):
     out = []
+    if opt.direct_light_sampling == abi.LSS_RESTIR_DI:
+        # GPURenderer's seed schedule: camera, ReSTIR passes, path tracing per sample
+        for d in scene.gpu_seed_schedule(n, 2, first_sample=first):
+            st = scene.parity_settings(bounces)
+            st.do_alpha_testing = alpha
+            out.append(scene.make_frame(cam, W, H, options=opt, settings=st, world=world, sample_number=d["sample_number"],
+                                        random_seed=d["random_seed"], camera_random_seed=d["camera_random_seed"],
+                                        restir_di_seeds=d["restir_di_seeds"], band=band))
+        return out
     for s, seed in scene.cpu_seed_schedule(n):
         st = scene.parity_settings(bounces)
         st.do_alpha_testing = alpha
@@ -129,16 +138,19 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     W, H = a.width, a.height
-    if a.workload == "c3":
+    if a.workload == "c4" and world > 1:
+        raise SystemExit("c4 (ReSTIR DI) renders the whole frame per context: multi-GPU halo exchange is not built yet")
+    if a.workload in ("c3", "c4"):
         from mpt import synthetic
         sd = synthetic.procedural_city(1234)
         env = mpt.build_envmap(scene.procedural_sky(2048, 1024, seed=7))
         wset = scene.envmap_world(1.0)
-        strategy = a.strategy or "ris"
+        strategy = a.strategy or ("ris" if a.workload == "c3" else "restir")
         K = a.steps or 256
         alpha = True      # C3 pins do_alpha_testing = true (the Bistro's foliage)
-        desc = ("C3 stand-in: procedural city (2.86 M tris incl. alpha-tested leaf cards, seed 1234) + procedural "
-                "HDR sky 2048x1024, alpha testing on")
+        desc = (f"{a.workload.upper()} stand-in: procedural city (2.86 M tris incl. alpha-tested leaf cards, seed 1234) + "
+                "procedural HDR sky 2048x1024, alpha testing on"
+                + (", ReSTIR DI fused spatiotemporal + 1 spatial pass, GPURenderer seed schedule" if a.workload == "c4" else ""))
     else:
         sd = scene.load_scene(a.scene or "cornell_pbr")
         env, wset = None, None
@@ -152,7 +164,7 @@ def main():
     opt.bsdf_override = abi.BSDF_NONE if a.bsdf == "principled" else abi.BSDF_LAMBERTIAN
     opt.direct_light_sampling = LSS[strategy]
 
-    band = (BAND_H, rank, world)
+    band = (BAND_H, rank, world) if a.workload != "c4" else (1, 0, 1)
 
     r = mpt.GPURenderer(local)
     r.set_scene(sd)
@@ -269,7 +281,7 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": ("synthetic (seeded procedural city + sky standing in for Bistro + its HDR, CPU seed schedule)"
-                     if a.workload == "c3" else "synthetic (reference Cornell glTF, seeded CPU seed schedule)"),
+                     if a.workload in ("c3", "c4") else "synthetic (reference Cornell glTF, seeded CPU seed schedule)"),
             "msample_per_s": round(W * H * K / elapsed / 1e6, 3),
             "rays_per_sample": round(rays_total / (W * H * K), 4),
             "config": {"workload": f"{desc}, {W}x{H}, {K} spp, "
@@ -284,7 +296,7 @@ def main():
                                    "trace_nee_closest": round(st.stage_ms[2] / K, 4), "shade": round(st.shade_ms / K, 4),
                                    "resolve": round(st.resolve_ms / K, 4), "camera": round(st.camera_ms / K, 4),
                                    "accumulate": round(st.accumulate_ms / K, 4),
-                                   "compact": round(st.compact_ms / K, 4),
+                                   "compact": round(st.compact_ms / K, 4), "restir": round(st.restir_ms / K, 4),
                                    "frame_gpu": round(st.frame_ms / max(1, st.frames), 4)},
             "cpu_baseline": cpu,
         }
