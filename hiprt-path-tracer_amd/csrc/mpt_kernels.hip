@@ -882,11 +882,15 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MPT_SHADE_WA
             int triW = -1, ris_c = 0;
             bool hasW = false;
             const Col thr_vertex = thr;
-            PEval pe;                          // per-vertex half of every BSDF evaluation below
+            // per-vertex half of every BSDF evaluation below, one LDS record per lane (55
+            // dwords: an odd stride, so lane-parallel accesses are bank-conflict free).  Held
+            // in registers it pushed the kernel into ~140 spilled VGPRs; in LDS it costs one
+            // ds_read per field per evaluation (-23% k_shade time on C3)
+            __shared__ PEval pe_lds[TB];
+            PEval& pe = pe_lds[threadIdx.x];
             SECT(0);
             bsdf_eval_pre<OVR>(bc, m, vs, view, sn, pe);
             SECT(5);
-            RResv rres;                        // ReSTIR DI output reservoir (OP_RESTIR)
             Col fW = col(0.0f);                // BSDF value / pdf at the RIS light winner
             float pdfW = 0.0f;
             // One BSDF evaluation site for every operation of the vertex: each iteration
@@ -895,6 +899,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MPT_SHADE_WA
             // evaluation whatever operation they are on.
             while (op != OP_DONE) {
                 VState tv = vs;
+                RResv rres;                    // ReSTIR DI output reservoir (OP_RESTIR)
                 v3 L = mk3(0.0f, 0.0f, 0.0f);
                 bool do_eval = false;
                 float lpdf = 0.0f, dist = 0.0f, geo = 0.0f;
