@@ -229,6 +229,8 @@ def main():
         ach = st.stage_rays[m] * b_ray / launches / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
         lines.append({"kernel": names[m], "symbol": f"void mpt::k_trace<{m}, false>(mpt::TraceArgs)", "total_ms": st.stage_ms[m], "achieved": ach, "avg_launch_ms": avg_ms,
                       "bytes_per_unit": b_ray, "unit_of_work": "ray", "nodes_per_ray": n_node, "tris_per_ray": n_tri,
+                      "node_simd_util": cal.stage_nodes[m] / max(1, cal.stage_node_slots[m]),
+                      "tri_simd_util": cal.stage_tris[m] / max(1, cal.stage_tri_slots[m]),
                       "units_per_launch": st.stage_rays[m] / launches})
     # shade: per path vertex = material 256 + vertex gathers 12+36+36+24 + path state 2x96 (§8d)
     b_vtx = 256 + 12 + 36 + 36 + 24 + 2 * 96
@@ -257,7 +259,8 @@ def main():
                      traffic_per_unit=round(tr["traffic_bytes"] / max(1.0, x["units_per_launch"]), 1),
                      traffic_source=pmc["file"])
         if "nodes_per_ray" in x:
-            r.update(nodes_per_ray=round(x["nodes_per_ray"], 3), tris_per_ray=round(x["tris_per_ray"], 3))
+            r.update(nodes_per_ray=round(x["nodes_per_ray"], 3), tris_per_ray=round(x["tris_per_ray"], 3),
+                     node_simd_util=round(x["node_simd_util"], 3), tri_simd_util=round(x["tri_simd_util"], 3))
         return r
 
     cpu = None
@@ -292,6 +295,9 @@ def main():
                        "partition": f"interleaved {BAND_H}-row bands over {world} rank(s), RCCL all_gather"},
             "roofline": roof(dom),
             "roofline_traversal": roof(max(lines[:3], key=lambda x: x["total_ms"])),
+            "traversal_stages": [{"kernel": x["kernel"].split(" ")[0], "nodes_per_ray": round(x["nodes_per_ray"], 3),
+                                  "tris_per_ray": round(x["tris_per_ray"], 3), "node_simd_util": round(x["node_simd_util"], 3),
+                                  "tri_simd_util": round(x["tri_simd_util"], 3)} for x in lines[:3]],
             "kernel_ms_per_step": {"trace_path": round(st.stage_ms[0] / K, 4), "trace_nee_any": round(st.stage_ms[1] / K, 4),
                                    "trace_nee_closest": round(st.stage_ms[2] / K, 4), "shade": round(st.shade_ms / K, 4),
                                    "resolve": round(st.resolve_ms / K, 4), "camera": round(st.camera_ms / K, 4),

@@ -53,6 +53,9 @@ struct DBuf {
 
 constexpr int FRAME_RING = 64;
 constexpr int EV_POOL = 256;
+#ifndef MPT_TRACE_BLOCKS_PER_CU
+#define MPT_TRACE_BLOCKS_PER_CU 4
+#endif
 constexpr int SPILL_WORDS = 2 * TRAV_SPILL_DEPTH;
 constexpr int MAX_STACK = TRAV_LDS_STACK + TRAV_SPILL_DEPTH;
 
@@ -421,7 +424,7 @@ int mpt_create(int device, void* hip_stream, MptContext** out) {
     hipDeviceProp_t prop;
     HIPCHK(hipGetDeviceProperties(&prop, device));
     c->num_cus = prop.multiProcessorCount;
-    c->grid = c->num_cus * 4;
+    c->grid = c->num_cus * MPT_TRACE_BLOCKS_PER_CU;   // persistent traversal / ReSTIR grids
     if (hip_stream) c->stream = (hipStream_t)hip_stream;
     else { HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)); c->own_stream = true; }
     HIPCHK(hipHostMalloc((void**)&c->h_frames, sizeof(MptFrame) * FRAME_RING));
@@ -490,7 +493,8 @@ int mpt_upload_scene(MptContext* c, const MptScene* s) {
             return fail(MPT_ERR_INVALID_ARGUMENT, "emissive triangle index out of range");
     HIPCHK(hipSetDevice(c->device));
     build_bvh8(s->vertices, s->triangle_indices, s->num_triangles, c->bvh, 3);
-    if (c->bvh.depth > MAX_STACK) return fail(MPT_ERR_UNSUPPORTED, "BVH8 deeper than the traversal stack");
+    // per level: at most one node group and one postponed triangle group on the stack
+    if (2 * c->bvh.depth + 2 > MAX_STACK) return fail(MPT_ERR_UNSUPPORTED, "BVH8 deeper than the traversal stack");
     hipStream_t st = c->stream;
     HIPCHK(c->nodes.upload(c->bvh.nodes.data(), c->bvh.nodes.size(), st));
     HIPCHK(c->tris.upload(c->bvh.tris.data(), c->bvh.tris.size(), st));
@@ -820,11 +824,13 @@ int mpt_get_stats(MptContext* c, MptStats* out) {
     out->rays_any = rc[1];
     for (int m = 0; m < 3; m++) {
         out->stage_rays[m] = rc[m];
-        out->stage_traversals[m] = s[m * 4 + 0];
-        out->stage_nodes[m] = s[m * 4 + 1];
-        out->stage_tris[m] = s[m * 4 + 2];
-        out->node_visits += s[m * 4 + 1];
-        out->triangle_tests += s[m * 4 + 2];
+        out->stage_traversals[m] = s[m * STATS_STRIDE + 0];
+        out->stage_nodes[m] = s[m * STATS_STRIDE + 1];
+        out->stage_tris[m] = s[m * STATS_STRIDE + 2];
+        out->stage_node_slots[m] = s[m * STATS_STRIDE + 4];
+        out->stage_tri_slots[m] = s[m * STATS_STRIDE + 5];
+        out->node_visits += s[m * STATS_STRIDE + 1];
+        out->triangle_tests += s[m * STATS_STRIDE + 2];
         out->stage_ms[m] = c->stage_ms[m];
         out->stage_launches[m] = c->stage_launches[m];
         out->trace_ms += c->stage_ms[m];

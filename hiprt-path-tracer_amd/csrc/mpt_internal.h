@@ -14,8 +14,11 @@ namespace mpt {
 
 // traversal stack: LDS part + per-thread global spill (entries of 2 words)
 constexpr int TRAV_BLOCK = 256;
-constexpr int TRAV_LDS_STACK = 12;
-constexpr int TRAV_SPILL_DEPTH = 52;
+#ifndef MPT_LDS_STACK
+#define MPT_LDS_STACK 12
+#endif
+constexpr int TRAV_LDS_STACK = MPT_LDS_STACK;
+constexpr int TRAV_SPILL_DEPTH = 64 - TRAV_LDS_STACK;
 
 struct DevScene {
     const Node8* nodes;
@@ -143,7 +146,8 @@ constexpr int N_TRACE_MODES = 5;
 // timed kernel kinds: 0..2 = traversal stages (trace modes), then the others
 enum { KT_CAMERA = 3, KT_SHADE = 4, KT_RESOLVE = 5, KT_ACCUMULATE = 6, KT_COMPACT = 7, KT_RESTIR = 8, KT_COUNT = 9 };
 constexpr uint32_t QM_CONT = 16u;
-constexpr int N_STATS = N_TRACE_MODES * 4;
+constexpr int STATS_STRIDE = 6;   // per mode: traversals, nodes, tris, (unused), node slots, tri slots
+constexpr int N_STATS = N_TRACE_MODES * STATS_STRIDE;
 
 enum {
     CTR_Q0 = 0, CTR_Q1 = 1, CTR_ANY = 2, CTR_CL = 3, CTR_FETCH = 4,

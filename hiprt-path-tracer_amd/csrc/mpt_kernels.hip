@@ -36,10 +36,19 @@ namespace mpt {
 
 constexpr int TB = TRAV_BLOCK;
 constexpr int MAX_BOUNDARY_SKIPS = 16;   // trace_ray's volume-boundary skip loop bound
-#ifndef MPT_TRACE_FETCH
-#define MPT_TRACE_FETCH 64
+#ifndef MPT_TRACE_REFILL
+#define MPT_TRACE_REFILL 32
 #endif
-constexpr int TRACE_FETCH = MPT_TRACE_FETCH;   // rays claimed per wave and atomic
+#ifndef MPT_TRACE_BUDGET
+#define MPT_TRACE_BUDGET 16
+#endif
+constexpr int TRACE_REFILL = MPT_TRACE_REFILL;   // idle lanes of a wave that trigger a refill
+constexpr int TRACE_BUDGET = MPT_TRACE_BUDGET;   // nodes a lane opens between refill checks
+#ifndef MPT_TRI_POSTPONE
+#define MPT_TRI_POSTPONE 3
+#endif
+constexpr int TRI_POSTPONE = MPT_TRI_POSTPONE;   // triangle loop runs with >= 1/TRI_POSTPONE of the lanes
+constexpr uint32_t TRI_GROUP = 0x80000000u;      // stack entry tag of a triangle group
 constexpr int LDS_STACK = TRAV_LDS_STACK;
 constexpr int SPILL_DEPTH = TRAV_SPILL_DEPTH;
 
@@ -83,93 +92,154 @@ DEV bool alpha_rejects(const DevScene& S, int prim, float u, float v, uint32_t k
 
 DEV uint32_t qbyte(uint32_t w0, uint32_t w1, int s) { return ((s < 4 ? w0 : w1) >> ((s & 3) * 8)) & 0xffu; }
 
+// Resumable BVH8 traversal of one ray: init() sets it up, run() opens nodes until the
+// traversal ends (true) or `budget` nodes have been opened (false, the state is kept for
+// the next call).  Stopping between nodes lets the traversal kernel hand a finished lane
+// a new ray while the rest of its wave is still traversing.
 template <bool ANY, bool STATS>
-DEV bool traverse(const DevScene& S, v3 o, v3 d, int last_hit, float tmax, THit& out, uint2* lds, uint32_t* spill,
-                  uint32_t& n_nodes, uint32_t& n_tris, bool alpha_on = false, uint32_t akey = 0u) {
-    const float4* nodes = reinterpret_cast<const float4*>(S.nodes);
-    const float4* tris = reinterpret_cast<const float4*>(S.tris);
-    float ix = 1.0f / (fabsf(d.x) > 1e-30f ? d.x : copysignf(1e-30f, d.x));
-    float iy = 1.0f / (fabsf(d.y) > 1e-30f ? d.y : copysignf(1e-30f, d.y));
-    float iz = 1.0f / (fabsf(d.z) > 1e-30f ? d.z : copysignf(1e-30f, d.z));
-    int oct = (d.x > 0.0f ? 1 : 0) | (d.y > 0.0f ? 2 : 0) | (d.z > 0.0f ? 4 : 0);
-    int xr = oct ^ 7;
-    float best = ANY ? tmax : INFINITY;
-    int bprim = -1;
-    float bu = 0.0f, bv = 0.0f;
-    uint32_t gbase = 0, gimask = 1u, gk = 1u << (0 ^ xr);
-    int sp = 0;
-    const int tid = threadIdx.x;
-    while (true) {
-        if (gk == 0) {
-            if (sp == 0) break;
-            --sp;
-            uint2 e;
-            if (sp < LDS_STACK) e = lds[sp * TB + tid];
-            else { e.x = spill[2 * (sp - LDS_STACK)]; e.y = spill[2 * (sp - LDS_STACK) + 1]; }
-            gbase = e.x; gimask = e.y & 0xffu; gk = e.y >> 8;
-        }
-        int k = __builtin_ctz(gk);
-        gk &= gk - 1u;
-        int s = k ^ xr;
-        uint32_t ni = gbase + (uint32_t)__builtin_popcount(gimask & ((1u << s) - 1u));
-        if (gk) {
-            uint2 e = make_uint2(gbase, gimask | (gk << 8));
-            if (sp < LDS_STACK) lds[sp * TB + tid] = e;
-            else { spill[2 * (sp - LDS_STACK)] = e.x; spill[2 * (sp - LDS_STACK) + 1] = e.y; }
-            ++sp;
-        }
-        if (STATS) n_nodes++;
-        const float4 n0 = nodes[5 * (size_t)ni + 0];
-        const float4 n1 = nodes[5 * (size_t)ni + 1];
-        const float4 n2 = nodes[5 * (size_t)ni + 2];
-        const float4 n3 = nodes[5 * (size_t)ni + 3];
-        const float4 n4 = nodes[5 * (size_t)ni + 4];
-        uint32_t eb = __float_as_uint(n0.w);
-        float sx = __uint_as_float((eb & 0xffu) << 23), sy = __uint_as_float(((eb >> 8) & 0xffu) << 23),
-              sz = __uint_as_float(((eb >> 16) & 0xffu) << 23);
-        uint32_t imask = eb >> 24;
-        float ax = (n0.x - o.x) * ix, ay = (n0.y - o.y) * iy, az = (n0.z - o.z) * iz;
-        float cx = sx * ix, cy = sy * iy, cz = sz * iz;
-        uint32_t lox0 = __float_as_uint(n2.x), lox1 = __float_as_uint(n2.y);
-        uint32_t loy0 = __float_as_uint(n2.z), loy1 = __float_as_uint(n2.w);
-        uint32_t loz0 = __float_as_uint(n3.x), loz1 = __float_as_uint(n3.y);
-        uint32_t hix0 = __float_as_uint(n3.z), hix1 = __float_as_uint(n3.w);
-        uint32_t hiy0 = __float_as_uint(n4.x), hiy1 = __float_as_uint(n4.y);
-        uint32_t hiz0 = __float_as_uint(n4.z), hiz1 = __float_as_uint(n4.w);
-        // near / far planes by direction sign
-        uint32_t nx0 = ix >= 0.0f ? lox0 : hix0, nx1 = ix >= 0.0f ? lox1 : hix1;
-        uint32_t fx0 = ix >= 0.0f ? hix0 : lox0, fx1 = ix >= 0.0f ? hix1 : lox1;
-        uint32_t ny0 = iy >= 0.0f ? loy0 : hiy0, ny1 = iy >= 0.0f ? loy1 : hiy1;
-        uint32_t fy0 = iy >= 0.0f ? hiy0 : loy0, fy1 = iy >= 0.0f ? hiy1 : loy1;
-        uint32_t nz0 = iz >= 0.0f ? loz0 : hiz0, nz1 = iz >= 0.0f ? loz1 : hiz1;
-        uint32_t fz0 = iz >= 0.0f ? hiz0 : loz0, fz1 = iz >= 0.0f ? hiz1 : loz1;
-        uint32_t meta0 = __float_as_uint(n1.z), meta1 = __float_as_uint(n1.w);
-        uint32_t child_base = __float_as_uint(n1.x), tri_base = __float_as_uint(n1.y);
-        uint32_t hit_internal = 0u;   // k-ordered
-        uint32_t hit_leaf = 0u;       // slot-ordered
+struct Trav {
+    v3 o, d;
+    float ix, iy, iz;
+    int xr;
+    float best;          // closest: current closest t; any: t_max (unchanged until the hit)
+    int bprim;
+    float bu, bv;
+    uint32_t gbase, gimask, gk;   // current node group: child base, internal mask, remaining hits
+    int sp;
+    int last_hit;
+    uint32_t akey;
+    bool alpha_on;
+
+    DEV void init(v3 o_, v3 d_, int lh, float tmax, bool al, uint32_t key) {
+        o = o_;
+        d = d_;
+        ix = 1.0f / (fabsf(d.x) > 1e-30f ? d.x : copysignf(1e-30f, d.x));
+        iy = 1.0f / (fabsf(d.y) > 1e-30f ? d.y : copysignf(1e-30f, d.y));
+        iz = 1.0f / (fabsf(d.z) > 1e-30f ? d.z : copysignf(1e-30f, d.z));
+        int oct = (d.x > 0.0f ? 1 : 0) | (d.y > 0.0f ? 2 : 0) | (d.z > 0.0f ? 4 : 0);
+        xr = oct ^ 7;
+        best = ANY ? tmax : INFINITY;
+        bprim = -1;
+        bu = 0.0f;
+        bv = 0.0f;
+        gbase = 0;
+        gimask = 1u;
+        gk = 1u << (0 ^ xr);
+        sp = 0;
+        last_hit = lh;
+        akey = key;
+        alpha_on = al;
+    }
+
+    DEV void push(uint2* lds, uint32_t* spill, uint2 e) {
+        if (sp < LDS_STACK) lds[sp * TB + threadIdx.x] = e;
+        else { spill[2 * (sp - LDS_STACK)] = e.x; spill[2 * (sp - LDS_STACK) + 1] = e.y; }
+        ++sp;
+    }
+
+    // Node groups (child base, internal mask | remaining hits << 8) and triangle groups
+    // (first triangle record, hit mask | TRI_GROUP) share the stack.  A node's hit leaves
+    // form one triangle group (a node's triangles are contiguous, at most 8 x 3).  The
+    // triangle loop tests one triangle per iteration and is postponed (its group pushed)
+    // while fewer than 1/TRI_POSTPONE of the wave's traversing lanes have triangles to
+    // test, so that triangle tests run with more lanes at a time (the closest hit does
+    // not depend on the test order: ties go to the lower primitive index).
+    DEV bool run(const DevScene& S, uint2* lds, uint32_t* spill, int budget, uint32_t& n_nodes, uint32_t& n_tris,
+                 uint32_t* n_slots = nullptr) {
+        const float4* nodes = reinterpret_cast<const float4*>(S.nodes);
+        const float4* tris = reinterpret_cast<const float4*>(S.tris);
+        const int tid = threadIdx.x;
+        uint32_t tbase = 0u, tmask = 0u;   // current triangle group
+        while (true) {
+            if (gk == 0) {
+                if (sp == 0) return true;
+                if (budget <= 0) return false;
+                --sp;
+                uint2 e;
+                if (sp < LDS_STACK) e = lds[sp * TB + tid];
+                else { e.x = spill[2 * (sp - LDS_STACK)]; e.y = spill[2 * (sp - LDS_STACK) + 1]; }
+                if (e.y & TRI_GROUP) { tbase = e.x; tmask = e.y & ~TRI_GROUP; }
+                else { gbase = e.x; gimask = e.y & 0xffu; gk = e.y >> 8; }
+            } else if (budget <= 0) {
+                return false;
+            }
+            if (gk != 0) {
+                --budget;
+                int k = __builtin_ctz(gk);
+                gk &= gk - 1u;
+                int s = k ^ xr;
+                uint32_t ni = gbase + (uint32_t)__builtin_popcount(gimask & ((1u << s) - 1u));
+                if (gk) push(lds, spill, make_uint2(gbase, gimask | (gk << 8)));
+                if (STATS) {
+                    n_nodes++;
+                    if (n_slots && lane_id() == __ffsll((long long)__ballot(1)) - 1) n_slots[0] += 64;
+                }
+                const float4 n0 = nodes[5 * (size_t)ni + 0];
+                const float4 n1 = nodes[5 * (size_t)ni + 1];
+                const float4 n2 = nodes[5 * (size_t)ni + 2];
+                const float4 n3 = nodes[5 * (size_t)ni + 3];
+                const float4 n4 = nodes[5 * (size_t)ni + 4];
+                uint32_t eb = __float_as_uint(n0.w);
+                float sx = __uint_as_float((eb & 0xffu) << 23), sy = __uint_as_float(((eb >> 8) & 0xffu) << 23),
+                      sz = __uint_as_float(((eb >> 16) & 0xffu) << 23);
+                uint32_t imask = eb >> 24;
+                float ax = (n0.x - o.x) * ix, ay = (n0.y - o.y) * iy, az = (n0.z - o.z) * iz;
+                float cx = sx * ix, cy = sy * iy, cz = sz * iz;
+                uint32_t lox0 = __float_as_uint(n2.x), lox1 = __float_as_uint(n2.y);
+                uint32_t loy0 = __float_as_uint(n2.z), loy1 = __float_as_uint(n2.w);
+                uint32_t loz0 = __float_as_uint(n3.x), loz1 = __float_as_uint(n3.y);
+                uint32_t hix0 = __float_as_uint(n3.z), hix1 = __float_as_uint(n3.w);
+                uint32_t hiy0 = __float_as_uint(n4.x), hiy1 = __float_as_uint(n4.y);
+                uint32_t hiz0 = __float_as_uint(n4.z), hiz1 = __float_as_uint(n4.w);
+                // near / far planes by direction sign
+                uint32_t nx0 = ix >= 0.0f ? lox0 : hix0, nx1 = ix >= 0.0f ? lox1 : hix1;
+                uint32_t fx0 = ix >= 0.0f ? hix0 : lox0, fx1 = ix >= 0.0f ? hix1 : lox1;
+                uint32_t ny0 = iy >= 0.0f ? loy0 : hiy0, ny1 = iy >= 0.0f ? loy1 : hiy1;
+                uint32_t fy0 = iy >= 0.0f ? hiy0 : loy0, fy1 = iy >= 0.0f ? hiy1 : loy1;
+                uint32_t nz0 = iz >= 0.0f ? loz0 : hiz0, nz1 = iz >= 0.0f ? loz1 : hiz1;
+                uint32_t fz0 = iz >= 0.0f ? hiz0 : loz0, fz1 = iz >= 0.0f ? hiz1 : loz1;
+                uint32_t meta0 = __float_as_uint(n1.z), meta1 = __float_as_uint(n1.w);
+                uint32_t hit_internal = 0u;   // k-ordered
+                uint32_t hit_tris = 0u;       // triangle offsets from the node's tri_base
 #pragma unroll
-        for (int c = 0; c < 8; c++) {
-            float tnx = fmaf((float)qbyte(nx0, nx1, c), cx, ax), tfx = fmaf((float)qbyte(fx0, fx1, c), cx, ax);
-            float tny = fmaf((float)qbyte(ny0, ny1, c), cy, ay), tfy = fmaf((float)qbyte(fy0, fy1, c), cy, ay);
-            float tnz = fmaf((float)qbyte(nz0, nz1, c), cz, az), tfz = fmaf((float)qbyte(fz0, fz1, c), cz, az);
-            float tn = fmaxf(fmaxf(tnx, tny), fmaxf(tnz, 0.0f));
-            float tf = fminf(fminf(tfx, tfy), fminf(tfz, best)) * 1.0000009f;
-            bool h = tn <= tf;
-            uint32_t meta = qbyte(meta0, meta1, c);
-            bool internal = (imask >> c) & 1u;
-            if (h && internal) hit_internal |= 1u << (c ^ xr);
-            if (h && !internal && (meta >> 5)) hit_leaf |= 1u << c;
-        }
-        while (hit_leaf) {
-            int c = __builtin_ctz(hit_leaf);
-            hit_leaf &= hit_leaf - 1u;
-            uint32_t meta = qbyte(meta0, meta1, c);
-            uint32_t first = tri_base + (meta & 31u), cnt = meta >> 5;
-            for (uint32_t j = 0; j < cnt; j++) {
-                if (STATS) n_tris++;
-                const float4 t0 = tris[3 * (size_t)(first + j) + 0];
-                const float4 t1 = tris[3 * (size_t)(first + j) + 1];
-                const float4 t2 = tris[3 * (size_t)(first + j) + 2];
+                for (int c = 0; c < 8; c++) {
+                    float tnx = fmaf((float)qbyte(nx0, nx1, c), cx, ax), tfx = fmaf((float)qbyte(fx0, fx1, c), cx, ax);
+                    float tny = fmaf((float)qbyte(ny0, ny1, c), cy, ay), tfy = fmaf((float)qbyte(fy0, fy1, c), cy, ay);
+                    float tnz = fmaf((float)qbyte(nz0, nz1, c), cz, az), tfz = fmaf((float)qbyte(fz0, fz1, c), cz, az);
+                    float tn = fmaxf(fmaxf(tnx, tny), fmaxf(tnz, 0.0f));
+                    float tf = fminf(fminf(tfx, tfy), fminf(tfz, best)) * 1.0000009f;
+                    bool h = tn <= tf;
+                    uint32_t meta = qbyte(meta0, meta1, c);
+                    bool internal = (imask >> c) & 1u;
+                    if (h && internal) hit_internal |= 1u << (c ^ xr);
+                    // leaf: count (meta >> 5) triangles from offset (meta & 31); empty slots have meta 0
+                    if (h && !internal) hit_tris |= ((1u << (meta >> 5)) - 1u) << (meta & 31u);
+                }
+                if (hit_tris) {
+                    // the current triangle group is empty here (popped groups go straight to the loop)
+                    tbase = __float_as_uint(n1.y);
+                    tmask = hit_tris;
+                }
+                gbase = __float_as_uint(n1.x);
+                gimask = imask;
+                gk = hit_internal;
+            }
+            const int n_act = __popcll(__ballot(1));
+            while (tmask) {
+                if (__popcll(__ballot(1)) * TRI_POSTPONE < n_act) {
+                    push(lds, spill, make_uint2(tbase, tmask | TRI_GROUP));
+                    tmask = 0u;
+                    break;
+                }
+                const uint32_t ti = tbase + (uint32_t)__builtin_ctz(tmask);
+                tmask &= tmask - 1u;
+                if (STATS) {
+                    n_tris++;
+                    if (n_slots && lane_id() == __ffsll((long long)__ballot(1)) - 1) n_slots[1] += 64;
+                }
+                const float4 t0 = tris[3 * (size_t)ti + 0];
+                const float4 t1 = tris[3 * (size_t)ti + 1];
+                const float4 t2 = tris[3 * (size_t)ti + 2];
                 int prim = (int)__float_as_uint(t0.w);
                 // Moller-Trumbore exactly as Renderer/Triangle.h:20-62 (no contraction)
                 v3 e1 = mk3(t1.x, t1.y, t1.z), e2 = mk3(t2.x, t2.y, t2.z);
@@ -188,24 +258,33 @@ DEV bool traverse(const DevScene& S, v3 o, v3 d, int last_hit, float tmax, THit&
                 if (prim == last_hit) continue;
                 // alpha-tested triangle (flag in the record): only when it would be kept
                 if (alpha_on && __float_as_uint(t1.w) != 0u &&
-                    (ANY ? t < tmax : (t < best || (t == best && prim < bprim))) && alpha_rejects(S, prim, u, v, akey))
+                    (ANY ? t < best : (t < best || (t == best && prim < bprim))) && alpha_rejects(S, prim, u, v, akey))
                     continue;
                 if (ANY) {
-                    if (t < tmax) { out.prim = prim; out.t = t; out.u = u; out.v = v; return true; }
+                    if (t < best) {
+                        bprim = prim; best = t; bu = u; bv = v;
+                        gk = 0u; sp = 0;
+                        return true;
+                    }
                 } else if (t < best || (t == best && prim < bprim)) {
                     best = t; bprim = prim; bu = u; bv = v;
                 }
             }
         }
-        gbase = child_base;
-        gimask = imask;
-        gk = hit_internal;
     }
-    out.prim = bprim;
-    out.t = best;
-    out.u = bu;
-    out.v = bv;
-    return bprim >= 0;
+};
+
+template <bool ANY, bool STATS>
+DEV bool traverse(const DevScene& S, v3 o, v3 d, int last_hit, float tmax, THit& out, uint2* lds, uint32_t* spill,
+                  uint32_t& n_nodes, uint32_t& n_tris, bool alpha_on = false, uint32_t akey = 0u) {
+    Trav<ANY, STATS> tr;
+    tr.init(o, d, last_hit, tmax, alpha_on, akey);
+    tr.run(S, lds, spill, 0x7fffffff, n_nodes, n_tris);
+    out.prim = tr.bprim;
+    out.t = tr.best;
+    out.u = tr.bu;
+    out.v = tr.bv;
+    return tr.bprim >= 0;
 }
 
 // Ray sources of the persistent traversal kernel
@@ -230,89 +309,125 @@ DEV uint32_t slot_pixel(const MptFrame& F, int slot, int& x, int& y);
 DEV uint32_t pixel_seed(const MptFrame& F, uint32_t pix);
 DEV uint32_t camera_seed(const MptFrame& F, uint32_t pix);
 
+#ifndef MPT_TRACE_WAVES
+#define MPT_TRACE_WAVES 1
+#endif
+#ifndef MPT_TRACE_WAVES_PATH
+#define MPT_TRACE_WAVES_PATH MPT_TRACE_WAVES
+#endif
 template <int MODE, bool STATS>
-__global__ __launch_bounds__(TB) void k_trace(TraceArgs A) {
+__global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MODE == TM_PATH ? MPT_TRACE_WAVES_PATH : MPT_TRACE_WAVES))) void k_trace(TraceArgs A) {
     __shared__ uint2 lds[LDS_STACK * TB];
     const DevScene& S = A.S;
     const DevPaths& P = A.P;
     const int count = (MODE == TM_RAW_CLOSEST || MODE == TM_RAW_ANY) ? A.count_const : *A.count_ptr;
     uint32_t* spill = P.stack_spill + ((size_t)blockIdx.x * TB + threadIdx.x) * (2 * SPILL_DEPTH);
     uint32_t n_nodes = 0, n_tris = 0, n_rays = 0;
-    const bool any = (MODE == TM_NEE_ANY || MODE == TM_RAW_ANY);
+    uint32_t n_slots[2] = {0u, 0u};
+    constexpr bool ANY = (MODE == TM_NEE_ANY || MODE == TM_RAW_ANY);
+    // Persistent waves with per-lane ray replacement: a lane whose ray has finished takes
+    // a new one as soon as at least TRACE_REFILL lanes of its wave are idle (one atomic
+    // per refill), instead of the whole wave waiting for its longest ray.  Between refill
+    // checks every lane opens at most TRACE_BUDGET nodes.
+    Trav<ANY, STATS> tr;
+    bool alive = false;
+    bool exhausted = false;   // wave-uniform: the ray counter has passed `count`
+    int ray = 0;              // RAW: ray index; NEE: staged query (slot * 4 + kind); PATH: slot
+    int skips = 0;            // PATH: volume-boundary re-traces so far
+    uint32_t pseed = 0u;      // PATH: pixel seed of the alpha keys
+    bool was_inside = false;  // PATH: kept over re-traces, as in trace_ray's loop
+    float qmax = 0.0f;        // NEE closest: the query's t_max
     while (true) {
-        // one atomic per TRACE_FETCH rays (same-address atomics serialise in L2)
-        int base = 0;
-        if (lane_id() == 0) base = atomicAdd(A.fetch, TRACE_FETCH);
-        base = __shfl(base, 0);
-        if (base >= count) break;
-        for (int sub = 0; sub < TRACE_FETCH / 64; sub++) {
-        int i = base + sub * 64 + lane_id();
-        if (i >= count) break;
-        float4 ro, rd;
-        int slot = 0;
-        if (MODE == TM_PATH) { slot = A.queue[i]; ro = P.ray_o[slot]; rd = P.ray_d[slot]; }
-        else if (MODE == TM_NEE_ANY || MODE == TM_NEE_CLOSEST) {
-            // compacted list of staged queries (entry = slot * 4 + kind), see k_compact
-            slot = P.nq_tgt[MODE == TM_NEE_ANY ? (size_t)i : (size_t)P.n * 3 + i];
-            ro = P.nq_o[slot]; rd = P.nq_d[slot];
+        const unsigned long long idle = __ballot(!alive);
+        if (!exhausted && __popcll(idle) >= (unsigned)TRACE_REFILL) {
+            const int need = __popcll(idle);
+            int base = 0;
+            if (lane_id() == 0) base = atomicAdd(A.fetch, need);
+            base = __shfl(base, 0);
+            if (base + need >= count) exhausted = true;
+            if (!alive) {
+                const int i = base + __popcll(idle & ((1ull << lane_id()) - 1ull));
+                if (i < count) {
+                    alive = true;
+                    n_rays++;
+                    float4 ro, rd;
+                    if (MODE == TM_PATH) {
+                        ray = A.queue[i];
+                        ro = P.ray_o[ray];
+                        rd = P.ray_d[ray];
+                        skips = 0;
+                        was_inside = false;
+                        if (A.alpha) {   // bounce 0: the camera launch's seed (CameraRays traces the camera ray)
+                            int px, py;
+                            uint32_t pix = slot_pixel(*A.F, ray, px, py);
+                            pseed = A.bounce == 0 ? camera_seed(*A.F, pix) : pixel_seed(*A.F, pix);
+                        }
+                        tr.init(mk3(ro.x, ro.y, ro.z), mk3(rd.x, rd.y, rd.z), (int)__float_as_uint(ro.w), INFINITY,
+                                A.alpha != 0, A.alpha ? alpha_key(pseed, A.bounce, 0, 0) : 0u);
+                    } else if (MODE == TM_NEE_ANY || MODE == TM_NEE_CLOSEST) {
+                        // compacted list of staged queries (entry = slot * 4 + kind), see k_compact
+                        ray = P.nq_tgt[MODE == TM_NEE_ANY ? (size_t)i : (size_t)P.n * 3 + i];
+                        ro = P.nq_o[ray];
+                        rd = P.nq_d[ray];
+                        qmax = rd.w;
+                        const bool al = A.alpha != 0;
+                        uint32_t akey = 0u;
+                        if (al) { int px, py; akey = alpha_key(pixel_seed(*A.F, slot_pixel(*A.F, ray >> 2, px, py)), A.bounce, (ray & 3) + 1, 0); }
+                        tr.init(mk3(ro.x, ro.y, ro.z), mk3(rd.x, rd.y, rd.z), (int)__float_as_uint(ro.w), ANY ? rd.w : INFINITY, al, akey);
+                    } else {
+                        ray = i;
+                        ro = A.raw_o[i];
+                        rd = A.raw_d[i];
+                        tr.init(mk3(ro.x, ro.y, ro.z), mk3(rd.x, rd.y, rd.z), (int)__float_as_uint(ro.w), ANY ? rd.w : INFINITY, false, 0u);
+                    }
+                }
+            }
         }
-        else { ro = A.raw_o[i]; rd = A.raw_d[i]; }
-        v3 o = mk3(ro.x, ro.y, ro.z), d = mk3(rd.x, rd.y, rd.z);
-        int last_hit = (int)__float_as_uint(ro.w);
-        THit h;
+        if (__ballot(alive) == 0) {
+            if (exhausted) break;
+            continue;
+        }
+        if (!alive) continue;
+        if (!tr.run(S, lds, spill, TRACE_BUDGET, n_nodes, n_tris, STATS ? n_slots : nullptr)) continue;
+        const bool found = tr.bprim >= 0;
         if (MODE == TM_PATH) {
             // trace_ray's boundary-skipping loop (Intersect.h:117-206)
-            VState vs = vs_load(P.vsA, P.vsB, slot);
-            bool was_inside = false;
-            bool found;
-            int skips = 0;
-            uint32_t pseed = 0u;
-            if (A.alpha) {   // bounce 0: the camera launch's seed (CameraRays traces the camera ray)
-                int px, py;
-                uint32_t pix = slot_pixel(*A.F, slot, px, py);
-                pseed = A.bounce == 0 ? camera_seed(*A.F, pix) : pixel_seed(*A.F, pix);
-            }
-            while (true) {
-                n_rays++;
-                found = traverse<false, STATS>(S, o, d, last_hit, INFINITY, h, lds, spill, n_nodes, n_tris, A.alpha != 0,
-                                               A.alpha ? alpha_key(pseed, A.bounce, 0, skips) : 0u);
-                if (!found) break;
+            VState vs = vs_load(P.vsA, P.vsB, ray);
+            bool again = false;
+            if (found) {
                 was_inside = vs.pos > 0;
-                if (was_inside) vs.dist += h.t;
-                int mi = S.mat_idx[h.prim];
+                if (was_inside) vs.dist += tr.best;
+                int mi = S.mat_idx[tr.bprim];
                 bool skip = vs_push(vs, mi, S.mat_prio[mi]);
-                if (!skip) break;
                 // bounded like the oracle: a re-traced ray can keep re-hitting the triangle
                 // it sits on (only the original last hit is filtered), see DESIGN.md
-                if (++skips >= MAX_BOUNDARY_SKIPS) break;
-                o = o + h.t * d;
-                vs.dist += h.t;
+                if (skip && ++skips < MAX_BOUNDARY_SKIPS) {
+                    vs.dist += tr.best;
+                    again = true;
+                }
             }
-            vs_store(P.vsA, P.vsB, slot, vs);
-            P.ray_o[slot] = make_float4(o.x, o.y, o.z, ro.w);
-            P.hit[slot] = make_float4(h.t, h.u, h.v, __uint_as_float((uint32_t)(found ? h.prim : -1)));
-            P.hit_inside[slot] = was_inside ? 1 : 0;
+            vs_store(P.vsA, P.vsB, ray, vs);
+            if (again) {
+                n_rays++;
+                tr.init(tr.o + tr.best * tr.d, tr.d, tr.last_hit, INFINITY, A.alpha != 0,
+                        A.alpha ? alpha_key(pseed, A.bounce, 0, skips) : 0u);
+                continue;
+            }
+            P.ray_o[ray] = make_float4(tr.o.x, tr.o.y, tr.o.z, __uint_as_float((uint32_t)tr.last_hit));
+            P.hit[ray] = make_float4(tr.best, tr.bu, tr.bv, __uint_as_float((uint32_t)(found ? tr.bprim : -1)));
+            P.hit_inside[ray] = was_inside ? 1 : 0;
+        } else if (MODE == TM_NEE_ANY) {
+            P.occ[ray] = found ? 1 : 0;
+        } else if (MODE == TM_NEE_CLOSEST) {
+            // evaluate_shadow_light_ray: a hit counts only below t_max - 1e-4 (Intersect.h:337-343)
+            bool ok = found && tr.best < qmax;
+            P.nhit[ray >> 2] = make_float4(tr.best, tr.bu, tr.bv, __uint_as_float((uint32_t)(ok ? tr.bprim : -1)));
+        } else if (MODE == TM_RAW_ANY) {
+            A.raw_occ[ray] = found ? 1 : 0;
         } else {
-            n_rays++;
-            uint32_t akey = 0u;
-            bool al = (MODE == TM_NEE_ANY || MODE == TM_NEE_CLOSEST) && A.alpha;
-            if (al) { int px, py; akey = alpha_key(pixel_seed(*A.F, slot_pixel(*A.F, slot >> 2, px, py)), A.bounce, (slot & 3) + 1, 0); }
-            bool found = any ? traverse<true, STATS>(S, o, d, last_hit, rd.w, h, lds, spill, n_nodes, n_tris, al, akey)
-                             : traverse<false, STATS>(S, o, d, last_hit, INFINITY, h, lds, spill, n_nodes, n_tris, al, akey);
-            if (MODE == TM_NEE_ANY) {
-                P.occ[slot] = found ? 1 : 0;
-            } else if (MODE == TM_NEE_CLOSEST) {
-                int tgt = slot;
-                // evaluate_shadow_light_ray: a hit counts only below t_max - 1e-4 (Intersect.h:337-343)
-                bool ok = found && h.t < rd.w;
-                P.nhit[tgt >> 2] = make_float4(h.t, h.u, h.v, __uint_as_float((uint32_t)(ok ? h.prim : -1)));
-            } else if (MODE == TM_RAW_ANY) {
-                A.raw_occ[i] = found ? 1 : 0;
-            } else {
-                A.raw_hit[i] = make_float4(h.t, h.u, h.v, __uint_as_float((uint32_t)(found ? h.prim : -1)));
-            }
+            A.raw_hit[ray] = make_float4(tr.best, tr.bu, tr.bv, __uint_as_float((uint32_t)(found ? tr.bprim : -1)));
         }
-        }
+        alive = false;
     }
     if (STATS) {
         // wave-aggregated counters
@@ -320,11 +435,16 @@ __global__ __launch_bounds__(TB) void k_trace(TraceArgs A) {
             n_nodes += __shfl_xor(n_nodes, off);
             n_tris += __shfl_xor(n_tris, off);
             n_rays += __shfl_xor(n_rays, off);
+            n_slots[0] += __shfl_xor(n_slots[0], off);
+            n_slots[1] += __shfl_xor(n_slots[1], off);
         }
         if (lane_id() == 0) {
-            atomicAdd((unsigned long long*)&P.stats[MODE * 4 + 0], (unsigned long long)n_rays);
-            atomicAdd((unsigned long long*)&P.stats[MODE * 4 + 1], (unsigned long long)n_nodes);
-            atomicAdd((unsigned long long*)&P.stats[MODE * 4 + 2], (unsigned long long)n_tris);
+            unsigned long long* st = (unsigned long long*)&P.stats[MODE * STATS_STRIDE];
+            atomicAdd(st + 0, (unsigned long long)n_rays);
+            atomicAdd(st + 1, (unsigned long long)n_nodes);
+            atomicAdd(st + 2, (unsigned long long)n_tris);
+            atomicAdd(st + 4, (unsigned long long)n_slots[0]);
+            atomicAdd(st + 5, (unsigned long long)n_slots[1]);
         }
     }
 }

@@ -352,7 +352,8 @@ class Stats(C.Structure):
                 ("stage_tris", C.c_uint64 * 3), ("stage_ms", C.c_double * 3),
                 ("stage_launches", u32 * 3), ("shade_launches", u32), ("camera_ms", C.c_double),
                 ("shade_ms", C.c_double), ("resolve_ms", C.c_double), ("accumulate_ms", C.c_double),
-                ("compact_ms", C.c_double), ("restir_ms", C.c_double)]
+                ("compact_ms", C.c_double), ("restir_ms", C.c_double),
+                ("stage_node_slots", C.c_uint64 * 3), ("stage_tri_slots", C.c_uint64 * 3)]
 
 
 BSDF_NONE, BSDF_LAMBERTIAN = 0, 1

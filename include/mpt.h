@@ -388,6 +388,10 @@ typedef struct MptStats {
     double accumulate_ms;
     double compact_ms;
     double restir_ms;           /* ReSTIR DI passes (presampling .. spatial reuse) */
+    /* instrumented traversal, per stage: wave-level node / triangle iterations x 64 (the
+     * lane slots they occupied); stage_nodes / stage_node_slots = SIMD utilisation */
+    uint64_t stage_node_slots[3];
+    uint64_t stage_tri_slots[3];
 } MptStats;
 
 #define MPT_FB_COLOR 0        /* 'pixels': running SUM of samples (RenderData.h:34-36) */

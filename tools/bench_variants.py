@@ -26,7 +26,7 @@ def main():
         line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
         j = json.loads(line)
         print(json.dumps({"lib": lib, "ms_per_step": j["ms_per_step"], "value": j["value"],
-                          "kernels": j["kernel_ms_per_step"]}), flush=True)
+                          "kernels": j["kernel_ms_per_step"], "trav": j.get("traversal_stages")}), flush=True)
 
 
 if __name__ == "__main__":
