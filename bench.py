@@ -7,7 +7,11 @@ Workloads (BASELINE.json configs):
   sampling + BSDF MIS), 1920x1080, layered Principled BSDF, reference-default RIS light
   sampling, alpha testing on (C3 pins it for the foliage); K = 256.
 * c2: the Cornell box glTF at 1920x1080, Principled + NEE/MIS (LSS_MIS_LIGHT_BSDF); K = 64.
-Both: 3 bounces, reference defaults otherwise (adaptive sampling off so that every step
+* c4: c3 with ReSTIR DI (fused spatiotemporal + spatial reuse), GPURenderer seed schedule.
+* c5: the glass-dispersion stress scene (multi-dispersion.gltf; --scene
+  nested-dielectrics-complex for the nested-dielectrics one) at 3840x2160, 16 bounces,
+  Principled + RIS, K = 1024.
+All: 3 bounces unless stated, reference defaults otherwise (adaptive sampling off so that every step
 samples every pixel).  One *step* = one sample per pixel over the frame (one
 mpt_render_frame); K steps = the config's spp.  Multi-GPU: one process per GPU, the framebuffer is split into
 interleaved 8-row bands (each rank renders every N-th band), and the per-rank sum
@@ -43,18 +47,19 @@ BAND_H = 8
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--workload", default="c3", choices=["c2", "c3", "c4"])
-    ap.add_argument("--steps", type=int, default=None, help="default: the workload's spp (c3 256, c2 64)")
+    ap.add_argument("--workload", default="c3", choices=["c2", "c3", "c4", "c5"])
+    ap.add_argument("--steps", type=int, default=None, help="default: the workload's spp (c3/c4 256, c2 64, c5 1024)")
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--width", type=int, default=1920)
-    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--width", type=int, default=None, help="default 1920 (c5: 3840)")
+    ap.add_argument("--height", type=int, default=None, help="default 1080 (c5: 2160)")
     ap.add_argument("--scene", default=None, help="c2: a glTF of data/scenes (default cornell_pbr)")
     ap.add_argument("--strategy", default=None, choices=["mis", "ris", "uniform", "bsdf", "restir"],
                     help="default: c3 ris (reference default), c2 mis")
-    ap.add_argument("--bounces", type=int, default=3)
+    ap.add_argument("--bounces", type=int, default=None, help="default 3 (c5: 16)")
     ap.add_argument("--bsdf", default="principled", choices=["principled", "lambert"])
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="target CPU-baseline sample duration")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-parity", action="store_true", help="skip the RMSE-vs-oracle band check")
     return ap.parse_args()
 
 
@@ -110,13 +115,35 @@ def cpu_baseline(sd, luts, cam, W, H, opt, bounces, target_s, env=None, world=No
                       f"({BAND_H}-row bands, 1 of every {bc2}) of the same {W}x{H} frame, {dt:.1f} s"}
 
 
+def parity_band(sd, luts, cam, W, H, opt, bounces, K, env=None, world=None, alpha=False, max_s=20.0):
+    """RMSE of the GPU's K-spp radiance (sum / K) against the CPU oracle on the same frames,
+    over one 8-row band through the middle of the frame (the metric's "RMSE vs ref @256spp";
+    the oracle is the pinned CPU restatement).  The spp of the check is
+    cut down (prefix of the same frame sequence) if the oracle would take longer than max_s."""
+    sys.path.insert(0, ROOT)
+    from oracle import oracle as orc
+    cores = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    bc = H // BAND_H
+    bi = bc // 2
+    o = orc.Oracle(sd, luts, envmap=env)
+    t0 = time.perf_counter()
+    probe = o.render(frames_for(cam, W, H, opt, (BAND_H, bi, bc), 1, bounces=bounces, world=world, alpha=alpha),
+                     nthreads=cores)
+    dt1 = max(time.perf_counter() - t0, 1e-4)
+    k = K if dt1 * K <= max_s else max(1, int(max_s / dt1))
+    ref = o.render(frames_for(cam, W, H, opt, (BAND_H, bi, bc), k, bounces=bounces, world=world, alpha=alpha),
+                   nthreads=cores) if k > 1 else probe
+    o.close()
+    return k, bi, ref
+
+
 def load_traffic(workload, W, H):
     """HBM bytes per launch from the newest committed PMC summary of this workload
     (profiles/r*_<workload>_pmc_traffic.json, made by tools/profile_round.sh +
     tools/pmc_traffic.py from separate rocprofv3 --pmc passes of this same command).
     PMC counters need rocprofv3 around the process, so they cannot be read live here."""
     import glob
-    if (W, H) != (1920, 1080):
+    if (W, H) not in ((1920, 1080), (3840, 2160)):
         return None
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{workload}_pmc_traffic.json")))
     if not files:
@@ -137,7 +164,10 @@ def main():
         import torch.distributed as dist
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    W, H = a.width, a.height
+    W = a.width or (3840 if a.workload == "c5" else 1920)
+    H = a.height or (2160 if a.workload == "c5" else 1080)
+    default_bounces = a.bounces is None
+    a.bounces = a.bounces if a.bounces is not None else (16 if a.workload == "c5" else 3)
     if a.workload == "c4" and world > 1:
         raise SystemExit("c4 (ReSTIR DI) renders the whole frame per context: multi-GPU halo exchange is not built yet")
     if a.workload in ("c3", "c4"):
@@ -151,6 +181,15 @@ def main():
         desc = (f"{a.workload.upper()} stand-in: procedural city (2.86 M tris incl. alpha-tested leaf cards, seed 1234) + "
                 "procedural HDR sky 2048x1024, alpha testing on"
                 + (", ReSTIR DI fused spatiotemporal + 1 spatial pass, GPURenderer seed schedule" if a.workload == "c4" else ""))
+    elif a.workload == "c5":
+        # glass dispersion + nested dielectrics stress: ISS_WITH_PRIORITIES,
+        # stack 3, nb_bounces raised to 16; uniform ambient world
+        sd = scene.load_scene(a.scene or "multi-dispersion")
+        env, wset = None, None
+        strategy = a.strategy or "ris"
+        K = a.steps or 1024
+        alpha = False
+        desc = f"C5: {sd.name or a.scene or 'multi-dispersion'} (glass dispersion, nested dielectrics)"
     else:
         sd = scene.load_scene(a.scene or "cornell_pbr")
         env, wset = None, None
@@ -243,7 +282,7 @@ def main():
                   "achieved": st.stage_rays[0] * b_vtx / sl / (s_avg * 1e-3) / 1e9 if s_avg > 0 else 0.0})
     dom = max(lines, key=lambda x: x["total_ms"])
 
-    default_cfg = a.strategy is None and a.bounces == 3 and a.bsdf == "principled" and a.scene is None
+    default_cfg = a.strategy is None and default_bounces and a.bsdf == "principled" and a.scene is None
     pmc = load_traffic(a.workload, W, H) if default_cfg else None
 
     def roof(x):
@@ -262,6 +301,21 @@ def main():
             r.update(nodes_per_ray=round(x["nodes_per_ray"], 3), tris_per_ray=round(x["tris_per_ray"], 3),
                      node_simd_util=round(x["node_simd_util"], 3), tri_simd_util=round(x["tri_simd_util"], 3))
         return r
+
+    parity = None
+    if rank == 0 and world == 1 and not a.no_parity and a.workload != "c4":
+        # the GPU leg of the check: a fresh K'-spp accumulation restarting at sample 0 over
+        # the same frames (sample 0 overwrites the sums)
+        k, bi, ref = parity_band(sd, luts, cam, W, H, opt, a.bounces, K, env=env, world=wset, alpha=alpha)
+        r.enable_stats(timing=False, instrumented=False)
+        for f in frames[:k]:
+            r.render(f)
+        r.synchronize_kernel()
+        gpu = r.framebuffer(abi.FB_COLOR)[bi * BAND_H:(bi + 1) * BAND_H]
+        d = (gpu.astype(np.float64) - ref.astype(np.float64)) / k
+        parity = {"oracle": "CPU restatement (oracle/, pinned: DESIGN.md §2)", "rows": f"{bi * BAND_H}-{(bi + 1) * BAND_H - 1}",
+                  "spp": k, "rmse": float(np.sqrt(np.mean(d * d))), "max_abs": float(np.abs(d).max()),
+                  "bit_exact": bool(np.array_equal(gpu, ref)), "tolerance_rmse": 1e-3}
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
@@ -284,7 +338,7 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": ("synthetic (seeded procedural city + sky standing in for Bistro + its HDR, CPU seed schedule)"
-                     if a.workload in ("c3", "c4") else "synthetic (reference Cornell glTF, seeded CPU seed schedule)"),
+                     if a.workload in ("c3", "c4") else f"synthetic (reference glTF {sd.name}, seeded CPU seed schedule)"),
             "msample_per_s": round(W * H * K / elapsed / 1e6, 3),
             "rays_per_sample": round(rays_total / (W * H * K), 4),
             "config": {"workload": f"{desc}, {W}x{H}, {K} spp, "
@@ -305,6 +359,7 @@ def main():
                                    "compact": round(st.compact_ms / K, 4), "restir": round(st.restir_ms / K, 4),
                                    "frame_gpu": round(st.frame_ms / max(1, st.frames), 4)},
             "cpu_baseline": cpu,
+            "parity_vs_oracle": parity,
         }
         print(json.dumps(out), flush=True)
     r.close()
