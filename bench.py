@@ -168,8 +168,6 @@ def main():
     H = a.height or (2160 if a.workload == "c5" else 1080)
     default_bounces = a.bounces is None
     a.bounces = a.bounces if a.bounces is not None else (16 if a.workload == "c5" else 3)
-    if a.workload == "c4" and world > 1:
-        raise SystemExit("c4 (ReSTIR DI) renders the whole frame per context: multi-GPU halo exchange is not built yet")
     if a.workload in ("c3", "c4"):
         from mpt import synthetic
         sd = synthetic.procedural_city(1234)
@@ -203,13 +201,24 @@ def main():
     opt.bsdf_override = abi.BSDF_NONE if a.bsdf == "principled" else abi.BSDF_LAMBERTIAN
     opt.direct_light_sampling = LSS[strategy]
 
-    band = (BAND_H, rank, world) if a.workload != "c4" else (1, 0, 1)
+    from mpt import partition
+    if a.workload == "c4":
+        # ReSTIR DI reuses neighbouring pixels: one contiguous band per rank, halo rows
+        # exchanged after the G-buffer pass and before every reuse pass (RCCL send/recv)
+        band = partition.contiguous_band(H, world, rank) if world > 1 else (1, 0, 1)
+    else:
+        band = (BAND_H, rank, world)
+    band_h = band[0]
 
     r = mpt.GPURenderer(local)
     r.set_scene(sd)
     r.set_luts(luts)
     if env is not None:
         r.set_envmap(env)
+    halo = None
+    if a.workload == "c4" and world > 1:
+        halo = partition.TorchHaloExchange(dist, band_h)
+        r.set_halo_exchange(halo)
 
     # calibration: instrumented traversal -> nodes / triangles per query per stage
     r.enable_stats(timing=False, instrumented=True)
@@ -224,10 +233,9 @@ def main():
     r.synchronize_kernel()
     r.enable_stats(timing=True, instrumented=False)
 
-    rows = mpt.partition_rows(H, BAND_H, rank, world)
+    rows = mpt.partition_rows(H, band[0], band[1], band[2])
     if dist is not None:
         import torch
-        from mpt import partition
         local_fb = torch.zeros((rows, W, 3), dtype=torch.float32, device="cuda")
         dist.barrier()
         torch.cuda.synchronize()
@@ -237,7 +245,7 @@ def main():
     r.synchronize_kernel()
     if dist is not None:
         r.framebuffer_to_device(abi.FB_COLOR, local_fb.data_ptr())
-        frame = partition.gather_frame(local_fb, H, BAND_H, dist)
+        frame = partition.gather_frame(local_fb, H, band_h, dist)
         torch.cuda.synchronize()
         dist.barrier()
     elapsed = time.perf_counter() - t0
@@ -346,7 +354,9 @@ def main():
                                    f"({strategy.upper()}), {a.bounces} bounces, 1 step = 1 spp",
                        "scene": sd.name, "triangles": int(sd.num_triangles), "width": W, "height": H, "spp": K,
                        "strategy": strategy,
-                       "partition": f"interleaved {BAND_H}-row bands over {world} rank(s), RCCL all_gather"},
+                       "partition": (f"contiguous {band_h}-row bands over {world} rank(s), halo exchange by RCCL send/recv, "
+                                     "RCCL all_gather" if a.workload == "c4" and world > 1 else
+                                     f"interleaved {BAND_H}-row bands over {world} rank(s), RCCL all_gather")},
             "roofline": roof(dom),
             "roofline_traversal": roof(max(lines[:3], key=lambda x: x["total_ms"])),
             "traversal_stages": [{"kernel": x["kernel"].split(" ")[0], "nodes_per_ray": round(x["nodes_per_ray"], 3),
@@ -361,6 +371,10 @@ def main():
             "cpu_baseline": cpu,
             "parity_vs_oracle": parity,
         }
+        if halo is not None:
+            nfr = 2 + a.warmup + K
+            out["halo_exchange"] = {"calls_per_frame": round(halo.calls / nfr, 2),
+                                    "mb_received_per_frame_rank0": round(halo.bytes_moved / nfr / 1e6, 3)}
         print(json.dumps(out), flush=True)
     r.close()
     if dist is not None:

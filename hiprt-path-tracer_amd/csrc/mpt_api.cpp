@@ -113,7 +113,12 @@ struct MptContext {
     DBuf<uint4> gb_vsA, gb_vsB, pgb_vsA, pgb_vsB;
     DBuf<MptMaterial> gb_mat, pgb_mat;
     DBuf<float4> rs_init, rs_sp1, rs_sp2, rs_plights;
+    DBuf<int32_t> rs_conv;
     int restir_out_sp2 = 0;
+    MptHaloExchangeFn halo_fn = nullptr;   // ReSTIR DI across a row partition
+    void* halo_user = nullptr;
+    int halo_prev = 0;                     // halo agreed in the previous frame
+    int32_t* h_reproj = nullptr;           // pinned readback of the reprojection offset
     DBuf<MptMaterial> mat_slot;
     DBuf<uint64_t> stats;
     DBuf<uint64_t> ray_counts;
@@ -227,6 +232,12 @@ DevPaths dev_paths(MptContext* c) {
     P.rs_init = c->rs_init.p; P.rs_sp1 = c->rs_sp1.p; P.rs_sp2 = c->rs_sp2.p; P.rs_plights = c->rs_plights.p;
     P.rs_out = c->restir_out_sp2 ? c->rs_sp2.p : c->rs_sp1.p;
     P.rs_tin = P.rs_out;
+    // contiguous band (ReSTIR DI across a partition) or the whole frame: slot s = pixel s + pix_off
+    const bool part = c->band_c > 1;
+    P.pix_off = part ? c->band_i * c->band_h * c->res_x : 0;
+    P.rs_lo = P.pix_off;
+    P.rs_hi = P.pix_off + c->n_slots;
+    P.rs_conv = part ? c->rs_conv.p : c->as_conv.p;
     return P;
 }
 
@@ -292,7 +303,7 @@ int upload_alpha_flags(MptContext* c) {
 // G-buffer pair, three reservoir buffers reset to empty reservoirs, the presampled lights.
 // Zero-filled G-buffers decode as "never written" (see restir_di.h gb_surface).
 int ensure_restir(MptContext* c, const MptFrame* f) {
-    size_t N = (size_t)std::max(c->n_slots, 1);
+    size_t N = (size_t)c->res_x * (size_t)c->res_y;   // frame-sized, indexed by pixel (band + halo used)
     const MptReSTIRDISettings& rd = f->render_settings.restir_di_settings;
     size_t npl = (size_t)std::max(1, rd.number_of_subsets * rd.subset_size);
     hipStream_t st = c->stream;
@@ -316,6 +327,10 @@ int ensure_restir(MptContext* c, const MptFrame* f) {
     if ((c->any_tex || f->bsdf_flags.white_furnace_mode) && c->gb_mat.n < N) {
         HIPCHK(c->gb_mat.alloc(N));
         HIPCHK(c->pgb_mat.alloc(N));
+    }
+    if (c->band_c > 1 && c->rs_conv.n != N) {
+        HIPCHK(c->rs_conv.alloc(N));
+        HIPCHK(hipMemsetAsync(c->rs_conv.p, 0xff, N * sizeof(int32_t), st));
     }
     if (c->rs_plights.n != 4 * npl) {
         HIPCHK(c->rs_plights.alloc(4 * npl));
@@ -354,8 +369,9 @@ int validate_frame(const MptFrame* f) {
     if (lss < 0 || lss > MPT_LSS_RESTIR_DI) return fail(MPT_ERR_INVALID_ARGUMENT, "bad direct_light_sampling");
     if (lss == MPT_LSS_RESTIR_DI) {
         const MptReSTIRDISettings& rd = rs.restir_di_settings;
-        if (f->band_count != 1)
-            return fail(MPT_ERR_UNSUPPORTED, "ReSTIR DI reuses neighbouring pixels: render the whole frame per context (band_count 1)");
+        if (f->band_count != 1 && (int64_t)f->band_height * f->band_count < f->res_y)
+            return fail(MPT_ERR_UNSUPPORTED, "ReSTIR DI across a partition needs one contiguous band per context "
+                                             "(band_height * band_count >= res_y)");
         if (!rd.do_fused_spatiotemporal)
             return fail(MPT_ERR_UNSUPPORTED, "ReSTIR DI: only the fused spatiotemporal configuration (the reference default)");
         if (rd.number_of_passes < 1 || rd.number_of_passes > 5)
@@ -471,6 +487,7 @@ int mpt_destroy(MptContext* c) {
     c->fb_albedo.release(); c->fb_normal.release(); c->stats.release(); c->ray_counts.release();
     c->raw_o.release(); c->raw_d.release(); c->raw_hit.release(); c->raw_occ.release();
     if (c->h_frames) (void)hipHostFree(c->h_frames);
+    if (c->h_reproj) (void)hipHostFree(c->h_reproj);
     if (c->d_frames) (void)hipFree(c->d_frames);
     if (c->own_stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -689,6 +706,9 @@ int mpt_render_frame(MptContext* c, const MptFrame* f) {
     HIPCHK(hipSetDevice(c->device));
     int r = ensure_paths(c, f->res_x, f->res_y, f->band_height, f->band_index, f->band_count);
     if (r != MPT_OK) return r;
+    const bool restir_part = f->options.direct_light_sampling == MPT_LSS_RESTIR_DI && f->band_count > 1;
+    if (restir_part && !c->halo_fn)
+        return fail(MPT_ERR_INVALID_ARGUMENT, "ReSTIR DI across a partition needs mpt_set_halo_exchange");
     if (f->options.direct_light_sampling == MPT_LSS_RESTIR_DI) {
         r = ensure_restir(c, f);
         if (r != MPT_OK) return r;
@@ -717,10 +737,27 @@ int mpt_render_frame(MptContext* c, const MptFrame* f) {
     cfg.ev_cap = EV_POOL;
     cfg.ev_used = 0;
     cfg.restir_out_sp2 = c->restir_out_sp2;
+    if (restir_part) {
+        if (!c->h_reproj) HIPCHK(hipHostMalloc((void**)&c->h_reproj, sizeof(int32_t), hipHostMallocDefault));
+        cfg.halo_fn = c->halo_fn;
+        cfg.halo_user = c->halo_user;
+        cfg.own_y0 = f->band_index * f->band_height;
+        cfg.own_y1 = std::min(f->res_y, cfg.own_y0 + f->band_height);
+        cfg.halo_prev = c->halo_prev;
+        cfg.halo_rows = c->halo_prev;
+        cfg.h_reproj = c->h_reproj;
+    }
     if (c->timing) HIPCHK(hipEventRecord(c->ev_frame[pool][0], c->stream));
-    hipError_t e = launch_frame(dev_scene(c), dev_paths(c), c->d_frames + slot, *f, cfg, c->stream);
+    DevPaths P = dev_paths(c);
+    if (restir_part) {   // frame_begin maintains the band and the previous frame's halo rows
+        P.rs_lo = std::max(0, cfg.own_y0 - cfg.halo_prev) * f->res_x;
+        P.rs_hi = std::min(f->res_y, cfg.own_y1 + cfg.halo_prev) * f->res_x;
+    }
+    hipError_t e = launch_frame(dev_scene(c), P, c->d_frames + slot, *f, cfg, c->stream);
     c->restir_out_sp2 = cfg.restir_out_sp2;
+    if (restir_part) c->halo_prev = cfg.halo_rows;
     if (e != hipSuccess) return fail(MPT_ERR_HIP, std::string("kernel launch: ") + hipGetErrorString(e));
+    if (cfg.halo_rc != 0) return fail(MPT_ERR_HIP, "halo exchange callback failed (" + std::to_string(cfg.halo_rc) + ")");
     if (c->timing) {
         HIPCHK(hipEventRecord(c->ev_frame[pool][1], c->stream));
         c->ev_used[pool] = cfg.ev_used;
@@ -729,6 +766,13 @@ int mpt_render_frame(MptContext* c, const MptFrame* f) {
     c->frames_submitted++;
     c->frames++;
     c->trace_launches += cfg.launches;
+    return MPT_OK;
+}
+
+int mpt_set_halo_exchange(MptContext* c, MptHaloExchangeFn fn, void* user) {
+    if (!c) return fail(MPT_ERR_INVALID_ARGUMENT, "NULL context");
+    c->halo_fn = fn;
+    c->halo_user = fn ? user : nullptr;
     return MPT_OK;
 }
 

@@ -140,6 +140,12 @@ struct DevPaths {
     float4* rs_out;           // restir_output_reservoirs of this frame (rs_sp1 or rs_sp2)
     float4* rs_tin;           // temporal input of this frame (last frame's output)
     float4* rs_plights;       // presampled lights (4 float4 each)
+    // The G-buffer / reservoir / rs_conv arrays are frame-sized and indexed by the global
+    // pixel index; path-state slot s of this context is pixel s + pix_off (contiguous band).
+    // [rs_lo, rs_hi) = the pixels of the band plus its halo rows (what frame_begin maintains).
+    int32_t pix_off;
+    int32_t rs_lo, rs_hi;
+    int32_t* rs_conv;         // pixel_converged_sample_count by pixel (== as_conv when unpartitioned)
 };
 
 constexpr int N_TRACE_MODES = 5;
@@ -151,6 +157,7 @@ constexpr int N_STATS = N_TRACE_MODES * STATS_STRIDE;
 
 enum {
     CTR_Q0 = 0, CTR_Q1 = 1, CTR_ANY = 2, CTR_CL = 3, CTR_FETCH = 4,
+    CTR_REPROJ = 5,           // max |reprojected row - row| of the frame's G-buffer (partitioned ReSTIR DI)
     CTR_COUNT = 16
 };
 
@@ -164,6 +171,14 @@ struct LaunchCfg {
     int ev_used;
     uint32_t launches;
     int restir_out_sp2;       // in/out: restir_output_reservoirs is rs_sp2 (else rs_sp1)
+    // ReSTIR DI across a row partition: the host's halo exchange (mpt_set_halo_exchange)
+    MptHaloExchangeFn halo_fn;
+    void* halo_user;
+    int own_y0, own_y1;
+    int halo_prev;            // halo agreed in the previous frame (the rows frame_begin maintained)
+    int halo_rows;            // out: halo agreed in this frame's G-buffer exchange
+    int32_t* h_reproj;        // pinned host word for the measured reprojection offset
+    int halo_rc;              // out: first non-zero callback return
 };
 
 hipError_t launch_frame(const DevScene& S, const DevPaths& P, const MptFrame* d_frame, const MptFrame& h_frame,

@@ -28,6 +28,8 @@
 #include <hip/hip_runtime.h>
 
 #include <cfloat>
+#include <initializer_list>
+#include <utility>
 
 #include "dev_bsdf.h"
 #include "mpt_internal.h"
@@ -1069,11 +1071,12 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MPT_SHADE_WA
                     }
                 } else if (op == OP_RESTIR) {
                     // sample_light_ReSTIR_DI + evaluate_ReSTIR_DI_reservoir (FinalShading.h:16-115)
-                    rres = rr_load(P.rs_out, slot);
+                    const size_t rpix = (size_t)slot + P.pix_off;
+                    rres = rr_load(P.rs_out, (int)rpix);
                     if ((rres.flags & RF_ENVMAP) && ws.ambient_light_type != MPT_AMBIENT_ENVMAP) {
                         rres.UCW = 0.0f;   // validate_reservoir writes through to the buffer
-                        float4 a = P.rs_out[3 * (size_t)slot];
-                        P.rs_out[3 * (size_t)slot] = make_float4(a.x, a.y, 0.0f, a.w);
+                        float4 a = P.rs_out[3 * rpix];
+                        P.rs_out[3 * rpix] = make_float4(a.x, a.y, 0.0f, a.w);
                     }
                     if (rres.UCW > 0.0f) {
                         if (rres.flags & RF_ENVMAP) { L = mat_x_vec(ws.envmap_to_world_matrix.m, rres.point); dist = 1.0e35f; }
@@ -1611,25 +1614,75 @@ template <int OVR> struct KInitial { static constexpr auto fn = k_restir_initial
 template <int OVR> struct KSpatiotemporal { static constexpr auto fn = k_restir_spatiotemporal<OVR>; };
 template <int OVR> struct KSpatial { static constexpr auto fn = k_restir_spatial<OVR>; };
 
+// Halo exchange of a partitioned context (mpt.h MptHaloExchange): the host fills the rows
+// around the band from the contexts that own them.  No-op for a whole-frame context.
+static int halo_exchange(const MptFrame& hf, LaunchCfg& cfg, hipStream_t st, int phase, int pass, int halo,
+                         std::initializer_list<std::pair<void*, int64_t>> bufs) {
+    if (!cfg.halo_fn || cfg.halo_rc) return halo;
+    MptHaloExchange x{};
+    x.phase = phase;
+    x.pass = pass;
+    x.res_x = hf.res_x;
+    x.res_y = hf.res_y;
+    x.own_y0 = cfg.own_y0;
+    x.own_y1 = cfg.own_y1;
+    x.halo_rows = halo;
+    for (const auto& b : bufs) {
+        if (!b.first || x.n_buffers >= MPT_HALO_MAX_BUFFERS) continue;
+        x.buffers[x.n_buffers] = b.first;
+        x.bytes_per_pixel[x.n_buffers] = b.second;
+        x.n_buffers++;
+    }
+    x.stream = (void*)st;
+    cfg.halo_rc = cfg.halo_fn(cfg.halo_user, &x);
+    return x.halo_rows;
+}
+
 // ReSTIRDIRenderPass::launch (ReSTIRDIRenderPass.cpp:233-264) for the fused configuration:
 // presampling, initial candidates, fused spatiotemporal, (number_of_passes - 1) spatial
-// passes ping-ponging between the two spatial buffers; returns the output buffer in P.rs_out
+// passes ping-ponging between the two spatial buffers; returns the output buffer in P.rs_out.
+// A partitioned context exchanges the halo of the G-buffer (after k_gbuffer) and of every
+// reservoir buffer a reuse pass reads at neighbours: the temporal input right before the
+// fused pass (so the final-shading write-through of the previous frame is included), then
+// each pass's output before the next pass.
 static void launch_restir(const DevScene& S, DevPaths& P, const MptFrame* d_frame, const MptFrame& hf, LaunchCfg& cfg,
                           hipStream_t st) {
     TimedScope ts(cfg, st, KT_RESTIR);
     const MptReSTIRDISettings& rd = hf.render_settings.restir_di_settings;
     const int ovr = hf.options.bsdf_override;
     const int n_pl = rd.number_of_subsets * rd.subset_size;
+    const int64_t RB = 3 * sizeof(float4);
+    if (cfg.halo_fn) {
+        // halo this context needs: its pixels' largest reprojection offset (measured by
+        // k_gbuffer) + the reuse radius + the temporal search / permutation extent
+        // (Utils.h:371-421); agreed over all contexts by the host's G-buffer exchange
+        hipMemcpyAsync(cfg.h_reproj, &P.counters[CTR_REPROJ], sizeof(int32_t), hipMemcpyDeviceToHost, st);
+        hipStreamSynchronize(st);
+        const int need = std::min(hf.res_y, *cfg.h_reproj + std::max(0, rd.reuse_radius) +
+                                                std::max(0, rd.neighbor_search_radius) + 8);
+        const bool as = hf.render_settings.enable_adaptive_sampling;
+        if (as) hipLaunchKernelGGL(k_restir_conv, dim3(blocks_for(P.n)), dim3(TB), 0, st, P);
+        const int64_t MS = sizeof(MptMaterial);
+        cfg.halo_rows = halo_exchange(hf, cfg, st, MPT_HALO_GBUFFER, 0, need,
+                                      {{P.gb_pos, 16}, {P.gb_sn, 16}, {P.gb_gn, 16}, {P.gb_view, 16}, {P.gb_meta, 16},
+                                       {P.gb_vsA, 16}, {P.gb_vsB, 16}, {P.gb_mat, MS}, {as ? P.rs_conv : nullptr, 4}});
+        if (cfg.halo_rows > cfg.halo_prev)   // rows frame_begin did not maintain last frame
+            halo_exchange(hf, cfg, st, MPT_HALO_PREV_GBUFFER, 0, cfg.halo_rows,
+                          {{P.pgb_pos, 16}, {P.pgb_sn, 16}, {P.pgb_gn, 16}, {P.pgb_view, 16}, {P.pgb_meta, 16},
+                           {P.pgb_vsA, 16}, {P.pgb_vsB, 16}, {P.pgb_mat, MS}});
+    }
     hipLaunchKernelGGL(k_restir_presample, dim3((n_pl + TB - 1) / TB), dim3(TB), 0, st, S, P, d_frame);
     const dim3 g(cfg.grid_persistent);
     launch_ovr<KInitial>(ovr, g, st, S, P, d_frame);
     float4* last_out = cfg.restir_out_sp2 ? P.rs_sp2 : P.rs_sp1;
     P.rs_tin = last_out;
     P.rs_out = last_out == P.rs_sp1 ? P.rs_sp2 : P.rs_sp1;
+    halo_exchange(hf, cfg, st, MPT_HALO_RESERVOIRS, 0, cfg.halo_rows, {{P.rs_tin, RB}});
     launch_ovr<KSpatiotemporal>(ovr, g, st, S, P, d_frame);
     for (int pass = 1; pass < rd.number_of_passes; pass++) {
         float4* in = P.rs_out;
         float4* out = in == P.rs_sp1 ? P.rs_sp2 : P.rs_sp1;
+        halo_exchange(hf, cfg, st, MPT_HALO_RESERVOIRS, pass, cfg.halo_rows, {{in, RB}});
         launch_ovr<KSpatial>(ovr, g, st, S, P, d_frame, pass, (const float4*)in, out);
         P.rs_out = out;
     }
@@ -1645,7 +1698,7 @@ hipError_t launch_frame(const DevScene& S, const DevPaths& P0, const MptFrame* d
     const bool as = (hrs.stop_pixel_noise_threshold > 0.0f || hrs.enable_adaptive_sampling) && hrs.accumulate;
     const bool restir = hf.options.direct_light_sampling == MPT_LSS_RESTIR_DI;
     if (restir) {
-        hipLaunchKernelGGL(k_restir_frame_begin, dim3(blocks_for(n)), dim3(TB), 0, st, P, d_frame);
+        hipLaunchKernelGGL(k_restir_frame_begin, dim3(blocks_for(P.rs_hi - P.rs_lo)), dim3(TB), 0, st, P, d_frame);
         P.rs_out = cfg.restir_out_sp2 ? P.rs_sp2 : P.rs_sp1;
     }
     // all pixels start a path, unless adaptive sampling compacts the camera queue
@@ -1666,6 +1719,7 @@ hipError_t launch_frame(const DevScene& S, const DevPaths& P0, const MptFrame* d
         ta.F = d_frame; ta.bounce = b; ta.alpha = hf.render_settings.do_alpha_testing ? 1 : 0;
         timed_trace<TM_PATH>(ta, cfg, st);
         if (restir && b == 0) {
+            if (cfg.halo_fn) hipMemsetAsync(&P.counters[CTR_REPROJ], 0, sizeof(int32_t), st);
             hipLaunchKernelGGL(k_gbuffer, dim3(blocks_for(n)), dim3(TB), 0, st, S, P, d_frame);
             launch_restir(S, P, d_frame, hf, cfg, st);
         }

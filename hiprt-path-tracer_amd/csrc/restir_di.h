@@ -199,8 +199,8 @@ DEV int restir_spatial_neighbor(const DevPaths& P, const MptFrame& F, int k, int
     if (rs.enable_adaptive_sampling && rs.sample_number >= rs.adaptive_sampling_min_samples) {
         if (rs.restir_di_settings.allow_converged_neighbors_reuse) {
             Rng g = make_rng(pass_random_seed);
-            if (g() > rs.restir_di_settings.converged_neighbor_reuse_probability && P.as_conv[ni] != -1) return -1;
-        } else if (P.as_conv[ni] != -1) return -1;
+            if (g() > rs.restir_di_settings.converged_neighbor_reuse_probability && P.rs_conv[ni] != -1) return -1;
+        } else if (P.rs_conv[ni] != -1) return -1;
     }
     return ni;
 }
@@ -257,17 +257,28 @@ DEV BCtx make_bctx(const DevScene& S, const MptFrame& F) {
     return bc;
 }
 
+// the previous frame's pixel coordinates of a point (Utils.h:378-384)
+DEV void restir_reproject(const MptFrame& F, v3 p, float& fx, float& fy) {
+    v3 ss = mat_x_point(F.prev_camera.view_projection.m, p);
+    float sx = ss.x, sy = ss.y;
+    sx += 1.0f; sy += 1.0f;
+    sx *= 0.5f; sy *= 0.5f;
+    fx = sx * (float)F.res_x; fy = sy * (float)F.res_y;
+    fx -= 0.5f; fy -= 0.5f;
+}
+
 // ---- G-buffer write: CameraRays (CameraRays.h:144-166) over the camera queue ----------
 __global__ __launch_bounds__(TB) void k_gbuffer(DevScene S, DevPaths P, const MptFrame* __restrict__ Fp) {
     const MptFrame& F = *Fp;
     int i = blockIdx.x * TB + threadIdx.x;
     if (i >= P.counters[CTR_Q0]) return;
     int slot = P.q0[i];
+    const int gp = slot + P.pix_off;   // G-buffer entry of the slot's pixel
     float4 ro = P.ray_o[slot], rdv = P.ray_d[slot], hv = P.hit[slot];
     v3 o = mk3(ro.x, ro.y, ro.z), d = mk3(rdv.x, rdv.y, rdv.z);
     int prim = (int)__float_as_uint(hv.w);
     bool found = prim >= 0;
-    int4 meta = P.gb_meta[slot];
+    int4 meta = P.gb_meta[gp];
     if (found) {
         // trace_ray hit processing (Intersect.h:150-216), as k_shade does at bounce 0
         VState vs = vs_load(P.vsA, P.vsB, slot);
@@ -283,8 +294,8 @@ __global__ __launch_bounds__(TB) void k_gbuffer(DevScene S, DevPaths P, const Mp
         const Mat* mp;
         int per_pixel = 0;
         if (F.bsdf_flags.white_furnace_mode || S.mat_tex[mi]) {
-            P.gb_mat[slot] = intersection_material(S, mi, tc, F.bsdf_flags.white_furnace_mode);
-            mp = &P.gb_mat[slot];
+            P.gb_mat[gp] = intersection_material(S, mi, tc, F.bsdf_flags.white_furnace_mode);
+            mp = &P.gb_mat[gp];
             per_pixel = 1;
         } else {
             mp = &S.mats_res[mi];
@@ -300,17 +311,27 @@ __global__ __launch_bounds__(TB) void k_gbuffer(DevScene S, DevPaths P, const Mp
         if (m.dispersion_scale > 0.0f && m.specular_transmission > 0.0f && vs.wl == 0.0f)
             vs.wl = -(rng() * (float)(830 - 360) + (float)360);
         if (is_emissive(m) && dot(-d, gn) < 0) { gn = -gn; sn = -sn; }
-        P.gb_pos[slot] = make_float4(ip.x, ip.y, ip.z, 0.0f);
-        P.gb_sn[slot] = make_float4(sn.x, sn.y, sn.z, 0.0f);
-        P.gb_gn[slot] = make_float4(gn.x, gn.y, gn.z, 0.0f);
-        vs_store(P.gb_vsA, P.gb_vsB, slot, vs);
+        if (F.band_count > 1) {
+            // rows between this pixel and its reprojection (restir_temporal_neighbor's base
+            // position): the halo a partitioned context needs for the temporal reuse
+            float fx, fy;
+            restir_reproject(F, ip, fx, fy);
+            const float H = (float)F.res_y;
+            int off = F.res_y;
+            if (fy > -H && fy < 2.0f * H) off = min(F.res_y, abs((int)roundf(fy) - gp / F.res_x));
+            atomicMax(&P.counters[CTR_REPROJ], off);
+        }
+        P.gb_pos[gp] = make_float4(ip.x, ip.y, ip.z, 0.0f);
+        P.gb_sn[gp] = make_float4(sn.x, sn.y, sn.z, 0.0f);
+        P.gb_gn[gp] = make_float4(gn.x, gn.y, gn.z, 0.0f);
+        vs_store(P.gb_vsA, P.gb_vsB, gp, vs);
         meta.y = mi + 1;
         meta.w = per_pixel;
     }
     meta.x = found ? prim : -1;
     meta.z = found ? 1 : 0;
-    P.gb_meta[slot] = meta;
-    P.gb_view[slot] = make_float4(-d.x, -d.y, -d.z, 0.0f);
+    P.gb_meta[gp] = meta;
+    P.gb_view[gp] = make_float4(-d.x, -d.y, -d.z, 0.0f);
 }
 
 // ---- ReSTIR_DI_LightsPresampling (LightsPresampling.h:22-130) ------------------------
@@ -376,12 +397,13 @@ __global__ __launch_bounds__(TB) void k_restir_initial(DevScene S, DevPaths P, c
     RRays rr{&S, lds, P.stack_spill + ((size_t)blockIdx.x * TB + threadIdx.x) * (2 * SPILL_DEPTH),
              F.render_settings.do_alpha_testing, 0u, 5, 0, 0u, 0u};
     const int W = F.res_x;
-    for (int pix = blockIdx.x * TB + threadIdx.x; pix < P.n; pix += gridDim.x * TB) {
+    for (int s = blockIdx.x * TB + threadIdx.x; s < P.n; s += gridDim.x * TB) {
+        const int pix = s + P.pix_off;
         RSurf g = gb_surface(S, P, pix, false);
         if (is_emissive(*g.m)) continue;
         uint32_t seed = pass_seed(F, (uint32_t)pix, F.restir_di_seeds[1]);
         Rng rng = make_rng(seed);
-        if (!P.active[pix] || !P.gb_meta[pix].z) continue;
+        if (!P.active[s] || !P.gb_meta[pix].z) continue;
         rr.pseed = seed;
         rr.n = 0;
         const int x = pix % W, y = pix / W;
@@ -481,12 +503,8 @@ DEV int restir_temporal_neighbor(const DevScene& S, const DevPaths& P, const Mpt
                                  Rng& rng, int& px, int& py) {
     const MptReSTIRDISettings& rd = F.render_settings.restir_di_settings;
     int W = F.res_x, H = F.res_y;
-    v3 ss = mat_x_point(F.prev_camera.view_projection.m, p);
-    float sx = ss.x, sy = ss.y;
-    sx += 1.0f; sy += 1.0f;
-    sx *= 0.5f; sy *= 0.5f;
-    float fx = sx * (float)W, fy = sy * (float)H;
-    fx -= 0.5f; fy -= 0.5f;
+    float fx, fy;
+    restir_reproject(F, p, fx, fy);
     int idx = -1;
     bool use_prev = rd.do_temporal_reuse_pass;
     for (int i = 0; i < rd.max_neighbor_search_count + 1; i++) {
@@ -524,10 +542,11 @@ __global__ __launch_bounds__(TB) void k_restir_spatiotemporal(DevScene S, DevPat
              F.render_settings.do_alpha_testing, 0u, 6, 0, 0u, 0u};
     const int W = F.res_x;
     float4* tin = P.rs_tin;
-    for (int center = blockIdx.x * TB + threadIdx.x; center < P.n; center += gridDim.x * TB) {
+    for (int s = blockIdx.x * TB + threadIdx.x; s < P.n; s += gridDim.x * TB) {
+        const int center = s + P.pix_off;
         MptReSTIRDISettings rd = F.render_settings.restir_di_settings;
         rd.spatial_pass_index = 0;   // configure_spatial_pass_for_fused_spatiotemporal(0)
-        if (!P.active[center] || !P.gb_meta[center].z) continue;
+        if (!P.active[s] || !P.gb_meta[center].z) continue;
         uint32_t seed = pass_seed(F, (uint32_t)center, F.restir_di_seeds[2]);
         Rng rng = make_rng(seed);
         rr.pseed = seed;
@@ -624,10 +643,11 @@ __global__ __launch_bounds__(TB) void k_restir_spatial(DevScene S, DevPaths P, c
              F.render_settings.do_alpha_testing, 0u, 7, 0, 0u, 0u};
     const int W = F.res_x;
     const uint32_t pass_rs = F.restir_di_seeds[3 + pass];
-    for (int center = blockIdx.x * TB + threadIdx.x; center < P.n; center += gridDim.x * TB) {
+    for (int s = blockIdx.x * TB + threadIdx.x; s < P.n; s += gridDim.x * TB) {
+        const int center = s + P.pix_off;
         MptReSTIRDISettings rd = F.render_settings.restir_di_settings;
         rd.spatial_pass_index = pass;
-        if (!P.active[center] || !P.gb_meta[center].z) continue;
+        if (!P.active[s] || !P.gb_meta[center].z) continue;
         uint32_t seed = pass_seed(F, (uint32_t)center, pass_rs);
         Rng rng = make_rng(seed);
         rr.pseed = seed;
@@ -692,8 +712,8 @@ __global__ __launch_bounds__(TB) void k_restir_spatial(DevScene S, DevPaths P, c
 __global__ __launch_bounds__(TB) void k_restir_frame_begin(DevPaths P, const MptFrame* __restrict__ Fp) {
     const MptFrame& F = *Fp;
     const MptRenderSettings& rs = F.render_settings;
-    int i = blockIdx.x * TB + threadIdx.x;
-    if (i >= P.n) return;
+    int i = P.rs_lo + blockIdx.x * TB + threadIdx.x;   // the band and its halo rows
+    if (i >= P.rs_hi) return;
     if (rs.restir_di_settings.do_temporal_reuse_pass) {
         P.pgb_pos[i] = P.gb_pos[i]; P.pgb_sn[i] = P.gb_sn[i]; P.pgb_gn[i] = P.gb_gn[i]; P.pgb_view[i] = P.gb_view[i];
         int4 meta = P.gb_meta[i];
@@ -706,6 +726,13 @@ __global__ __launch_bounds__(TB) void k_restir_frame_begin(DevPaths P, const Mpt
         rr_store(P.rs_sp1, i, rr_default());
         rr_store(P.rs_sp2, i, rr_default());
     }
+}
+
+// pixel_converged_sample_count by pixel for the neighbour tests of a partitioned context
+// (restir_spatial_neighbor reads it at neighbouring pixels; exchanged with the G-buffer)
+__global__ __launch_bounds__(TB) void k_restir_conv(DevPaths P) {
+    int s = blockIdx.x * TB + threadIdx.x;
+    if (s < P.n) P.rs_conv[s + P.pix_off] = P.as_conv[s];
 }
 
 __global__ void k_restir_fill(float4* r, int n) {   // default reservoirs (Reservoir.h:166-170)

@@ -49,6 +49,15 @@ def lib() -> C.CDLL:
     path = os.environ.get("MPT_LIB_PATH", str(LIB_PATH))   # development variants
     if not os.path.exists(path):
         raise ImportError(f"libmpt.so not found at {path}; run __graft_entry__.build() (no CPU fallback)")
+    # One HIP runtime per process.  The torch wheel ships its own libamdhip64 (same SONAME,
+    # libamdhip64.so.7) next to libc10_hip; loading libmpt first would map /opt/rocm's copy
+    # and torch's would then find no device.  Loading torch first makes libmpt bind to the
+    # runtime torch already mapped, so libmpt buffers, torch tensors and RCCL share one
+    # runtime (measured: same bit-exact results and the same C3 throughput on either).
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = C.CDLL(path)
     vp, i32, f32 = C.c_void_p, C.c_int32, C.c_float
     L.mpt_last_error.restype = C.c_char_p
@@ -75,6 +84,7 @@ def lib() -> C.CDLL:
     L.mpt_clear_status.argtypes = [vp]
     L.mpt_query_status.argtypes = [vp, C.POINTER(abi.Status)]
     L.mpt_get_aux_buffer.argtypes = [vp, C.c_int, vp, C.c_int]
+    L.mpt_set_halo_exchange.argtypes = [vp, abi.HaloExchangeFn, vp]
     _lib = L
     return L
 
@@ -158,10 +168,36 @@ class GPURenderer:
     def resize(self, w, h):
         _check(lib().mpt_resize(self.h, w, h))
 
+    def set_halo_exchange(self, exchange):
+        """ReSTIR DI across a row partition (mpt.h MptHaloExchange): exchange(x) is called
+        with an abi.HaloExchange at every exchange point of mpt_render_frame and fills the
+        halo rows (mpt.partition.TorchHaloExchange / LocalHaloGroup).  None removes it."""
+        if exchange is None:
+            self._halo_cb = None
+            _check(lib().mpt_set_halo_exchange(self.h, abi.HaloExchangeFn(), None))
+            return
+
+        def _cb(_user, xp):
+            try:
+                exchange(xp.contents)
+                return 0
+            except BaseException as e:   # reported by render(); never unwinds through C
+                self._halo_error = e
+                return 1
+
+        self._halo_error = None
+        self._halo_cb = abi.HaloExchangeFn(_cb)   # kept alive with the renderer
+        _check(lib().mpt_set_halo_exchange(self.h, self._halo_cb, None))
+
     # --- frames --------------------------------------------------------------------
     def render(self, frame: "abi.Frame"):
         """Enqueues one sample per pixel (asynchronous)."""
-        _check(lib().mpt_render_frame(self.h, C.byref(frame)))
+        rc = lib().mpt_render_frame(self.h, C.byref(frame))
+        err = getattr(self, "_halo_error", None)
+        if err is not None:
+            self._halo_error = None
+            raise MptError(rc or -1, f"halo exchange failed: {err!r}") from err
+        _check(rc)
         self.frame = frame
 
     def synchronize_kernel(self):

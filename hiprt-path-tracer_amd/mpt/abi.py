@@ -369,6 +369,20 @@ class Status(C.Structure):
     """MptStatus == StatusBuffersValues (Renderer/StatusBuffersValues.h:9-21)."""
     _fields_ = [("one_ray_active", C.c_bool), ("pixel_converged_count", C.c_uint32)]
 
+# ReSTIR DI across a row partition: the halo-exchange callback (mpt.h MptHaloExchange)
+HALO_GBUFFER, HALO_RESERVOIRS, HALO_PREV_GBUFFER = 0, 1, 2
+HALO_MAX_BUFFERS = 12
+
+
+class HaloExchange(C.Structure):
+    _fields_ = [("phase", C.c_int32), ("pass_index", C.c_int32), ("res_x", C.c_int32), ("res_y", C.c_int32),
+                ("own_y0", C.c_int32), ("own_y1", C.c_int32), ("halo_rows", C.c_int32), ("n_buffers", C.c_int32),
+                ("buffers", C.c_void_p * HALO_MAX_BUFFERS), ("bytes_per_pixel", C.c_int64 * HALO_MAX_BUFFERS),
+                ("stream", C.c_void_p)]
+
+
+HaloExchangeFn = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(HaloExchange))
+
 ABI_SIZES = {"Material": 332, "RenderSettings": 304, "WorldSettings": 200, "Camera": 196}
 
 

@@ -411,6 +411,51 @@ typedef struct MptStatus {
 
 typedef struct MptContext MptContext;
 
+/* ReSTIR DI across a row partition (the C4 configuration on 1-8 GPUs).
+ * The spatial / spatiotemporal reuse passes read neighbouring pixels' G-buffer entries and
+ * reservoirs (FusedSpatiotemporalReuse.h:112-586, SpatialReuse.h:52-348), and the temporal
+ * reuse reads the previous frame's data around each pixel's reprojection (Utils.h:371-421),
+ * so a context that renders one contiguous band of rows (band_count > 1,
+ * band_height * band_count >= res_y) keeps its ReSTIR buffers frame-sized and asks the host
+ * to fill the rows around its band from the contexts that own them.  The result is
+ * bit-identical to a single-context render.
+ *
+ * Each buffer is a frame-sized, row-major array of per-pixel records on the context's device
+ * (pixel (x, y) at byte (y * res_x + x) * bytes_per_pixel).  The callback is invoked from
+ * mpt_render_frame after the producing kernels were enqueued on `stream` (not necessarily
+ * finished).  Before it returns it must have arranged (enqueued on `stream`, or completed)
+ * that rows [max(0, own_y0 - halo_rows), own_y0) and [own_y1, min(res_y, own_y1 + halo_rows))
+ * of every buffer hold the owning contexts' values, and must provide its own rows to its
+ * neighbours' callbacks of the same phase.  Returns 0, or non-zero to fail the frame.
+ *
+ * Phases, in order, per frame:
+ *  MPT_HALO_GBUFFER       after the G-buffer pass.  On entry halo_rows is what THIS context
+ *                         needs (measured: the largest reprojection offset of its pixels
+ *                         plus the reuse radius and temporal search extent -- the
+ *                         reference's reprojection is not confined to a pixel's
+ *                         neighbourhood).  The callback agrees on the maximum over all
+ *                         contexts, exchanges with it and stores it back in halo_rows.
+ *  MPT_HALO_PREV_GBUFFER  only when the agreed halo grew since the previous frame: the
+ *                         previous frame's G-buffer rows the context did not maintain.
+ *  MPT_HALO_RESERVOIRS    the temporal input before the fused pass (pass 0), then the
+ *                         output of pass i - 1 before spatial pass i. */
+#define MPT_HALO_GBUFFER 0
+#define MPT_HALO_RESERVOIRS 1
+#define MPT_HALO_PREV_GBUFFER 2
+#define MPT_HALO_MAX_BUFFERS 12
+typedef struct MptHaloExchange {
+    int32_t phase;        /* MPT_HALO_* */
+    int32_t pass;         /* reservoirs: the reuse pass about to read them (0 = fused spatiotemporal) */
+    int32_t res_x, res_y;
+    int32_t own_y0, own_y1;
+    int32_t halo_rows;    /* MPT_HALO_GBUFFER: in = needed here, out = agreed maximum */
+    int32_t n_buffers;
+    void* buffers[MPT_HALO_MAX_BUFFERS];
+    int64_t bytes_per_pixel[MPT_HALO_MAX_BUFFERS];
+    void* stream;         /* hipStream_t */
+} MptHaloExchange;
+typedef int (*MptHaloExchangeFn)(void* user, MptHaloExchange* x);
+
 const char* mpt_last_error(void);
 int mpt_version(void);
 /* sizes of the mirrored structs as compiled into the library (ABI check) */
@@ -434,6 +479,9 @@ int mpt_resize(MptContext* ctx, int32_t width, int32_t height);
 /* Renders one sample per pixel of the context's partition, accumulating into the
  * sum framebuffer (assign when render_settings.sample_number == 0). Asynchronous. */
 int mpt_render_frame(MptContext* ctx, const MptFrame* frame);
+/* Installs the halo exchange of a partitioned ReSTIR DI context (see MptHaloExchange);
+ * fn = NULL removes it.  Required before rendering LSS_RESTIR_DI with band_count > 1. */
+int mpt_set_halo_exchange(MptContext* ctx, MptHaloExchangeFn fn, void* user);
 int mpt_synchronize(MptContext* ctx);
 int mpt_query_done(MptContext* ctx, int* out_done);
 /* Copies the partition's rows of a framebuffer (band-major compact layout: the

@@ -16,8 +16,15 @@ from mpt import abi, scene, synthetic
 W, H = 32, 24
 
 
-def frames(sd, lss, n, passes=2, ovr=abi.BSDF_NONE, bounces=3, world=None, alpha=False, w=W, h=H, adaptive=False, **rd):
+def frames(sd, lss, n, passes=2, ovr=abi.BSDF_NONE, bounces=3, world=None, alpha=False, w=W, h=H, adaptive=False,
+           band=(1, 0, 1), move_at=None, **rd):
+    """move_at: from that frame on the camera is moved (prev_camera = the old one for one frame)."""
     cam = scene.make_camera(sd.camera_info, w, h)
+    cam2 = None
+    if move_at is not None:
+        ci = dict(sd.camera_info)
+        ci["position"] = np.asarray(ci["position"], np.float64) + np.array([0.05, 0.02, 0.0])
+        cam2 = scene.make_camera(ci, w, h)
     opt = abi.KernelOptions.default()
     opt.direct_light_sampling = lss
     opt.bsdf_override = ovr
@@ -32,9 +39,14 @@ def frames(sd, lss, n, passes=2, ovr=abi.BSDF_NONE, bounces=3, world=None, alpha
         st.restir_di_settings.number_of_passes = passes
         for k, v in rd.items():
             setattr(st.restir_di_settings, k, v)
-        out.append(scene.make_frame(cam, w, h, options=opt, settings=st, world=world, sample_number=d["sample_number"],
-                                    random_seed=d["random_seed"], camera_random_seed=d["camera_random_seed"],
-                                    restir_di_seeds=d["restir_di_seeds"]))
+        i = len(out)
+        cur = cam2 if move_at is not None and i >= move_at else cam
+        fr = scene.make_frame(cur, w, h, options=opt, settings=st, world=world, sample_number=d["sample_number"],
+                              random_seed=d["random_seed"], camera_random_seed=d["camera_random_seed"],
+                              restir_di_seeds=d["restir_di_seeds"], band=band)
+        if move_at is not None and i == move_at:
+            fr.prev_camera = cam
+        out.append(fr)
     return out
 
 
@@ -127,3 +139,150 @@ def test_gpu_restir_scenes_bit_exact(cornell, luts, case):
     assert np.array_equal(g, c), f"{case}: {(g != c).sum()} values differ"
     o.close()
     r.close()
+
+
+# ---- ReSTIR DI across a row partition (contiguous bands + halo exchange) ----
+
+PART_CASES = {
+    # name: (W, H, bands, frames kwargs)
+    "radius4_3bands": (32, 48, 3, dict(reuse_radius=4)),
+    "default_radius_4bands": (24, 96, 4, dict()),          # halo 28 rows > band 24: two peers
+    "three_passes": (24, 64, 2, dict(passes=3, reuse_radius=6)),
+    "adaptive": (24, 64, 3, dict(adaptive=True, reuse_radius=5)),
+    "camera_moves": (24, 64, 3, dict(move_at=2, reuse_radius=5)),
+    "permutation_sampling": (24, 64, 2, dict(use_permutation_sampling=True, reuse_radius=5)),
+}
+
+
+def _renderer(sd, luts, env=None):
+    import mpt
+    r = mpt.GPURenderer(0)
+    r.set_scene(sd)
+    r.set_luts(luts)
+    if env is not None:
+        r.set_envmap(env)
+    return r
+
+
+def render_partitioned_local(sd, luts, make_frames, w, h, nb, env=None):
+    """nb contexts on cuda:0, one contiguous band each, rendered from nb threads with the
+    in-process halo exchange; returns the assembled frame (sums) and the bytes exchanged."""
+    import threading
+    from mpt import partition
+    bh = partition.contiguous_band(h, nb, 0)[0]
+    group = partition.LocalHaloGroup(bh, nb)
+    rs = [_renderer(sd, luts, env) for _ in range(nb)]
+    for k, r in enumerate(rs):
+        r.set_halo_exchange(group.member(k))
+    errs = []
+
+    def run(k):
+        try:
+            for f in make_frames(partition.contiguous_band(h, nb, k)):
+                rs[k].render(f)
+            rs[k].synchronize_kernel()
+        except BaseException as e:
+            errs.append(e)
+            group.barrier.abort()
+
+    th = [threading.Thread(target=run, args=(k,)) for k in range(nb)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    if errs:
+        raise errs[0]
+    out = np.concatenate([r.framebuffer(abi.FB_COLOR) for r in rs])
+    for r in rs:
+        r.close()
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", list(PART_CASES))
+def test_gpu_restir_partitioned_bit_exact(cornell, luts, case):
+    """Bands + halo exchange render exactly the single-context frame (which is bit-exact
+    against the oracle), over several frames of temporal reuse."""
+    w, h, nb, kw = PART_CASES[case]
+    n = 5
+    r = _renderer(cornell, luts)
+    for f in frames(cornell, abi.LSS_RESTIR_DI, n, w=w, h=h, **kw):
+        r.render(f)
+    r.synchronize_kernel()
+    ref = r.framebuffer(abi.FB_COLOR)
+    r.close()
+    got = render_partitioned_local(cornell, luts, lambda band: frames(cornell, abi.LSS_RESTIR_DI, n, w=w, h=h, band=band, **kw),
+                                   w, h, nb)
+    assert got.shape == ref.shape
+    assert np.array_equal(got, ref), f"{case}: {(got != ref).sum()} values differ"
+    assert got.mean() > 0
+    if case == "radius4_3bands":
+        from oracle import oracle as orc
+        o = orc.Oracle(cornell, luts)
+        c = o.render(frames(cornell, abi.LSS_RESTIR_DI, n, w=w, h=h, **kw))
+        o.close()
+        assert np.array_equal(got, c)
+
+
+@pytest.mark.gpu
+def test_gpu_restir_partition_needs_halo_exchange(cornell, luts):
+    import mpt
+    r = _renderer(cornell, luts)
+    f = frames(cornell, abi.LSS_RESTIR_DI, 1, w=24, h=64, band=(32, 0, 2))[0]
+    with pytest.raises(mpt.MptError):
+        r.render(f)
+    f = frames(cornell, abi.LSS_RESTIR_DI, 1, w=24, h=64, band=(8, 0, 2))[0]   # interleaved: refused
+    r.set_halo_exchange(lambda x: None)
+    with pytest.raises(mpt.MptError):
+        r.render(f)
+    r.close()
+
+
+def _proc_worker(rank, world, port, w, h, n, out_dir):
+    import os
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "hiprt-path-tracer_amd"))
+    sys.path.insert(0, root)
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from mpt import partition
+    sd = scene.load_scene("cornell_pbr")
+    lt = scene.load_luts()
+    band = partition.contiguous_band(h, world, rank)
+    r = _renderer(sd, lt)
+    ex = partition.TorchHaloExchange(dist, band[0], device=torch.device("cuda", 0))
+    r.set_halo_exchange(ex)
+    for f in frames(sd, abi.LSS_RESTIR_DI, n, w=w, h=h, band=band, reuse_radius=5):
+        r.render(f)
+    r.synchronize_kernel()
+    np.save(os.path.join(out_dir, f"band{rank}.npy"), r.framebuffer(abi.FB_COLOR))
+    r.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_gpu_restir_partitioned_two_processes(cornell, luts, tmp_path):
+    """One process per band (the bench's multi-GPU layout) with TorchHaloExchange; both
+    processes share the box's single GPU, so the transport is gloo (host-staged) -- the
+    nccl transport runs the same plan over RCCL when each rank has its own GPU."""
+    import socket
+    import torch.multiprocessing as tmp
+    w, h, n = 24, 64, 4
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    tmp.spawn(_proc_worker, args=(2, port, w, h, n, str(tmp_path)), nprocs=2, join=True)
+    got = np.concatenate([np.load(tmp_path / f"band{k}.npy") for k in range(2)])
+    r = _renderer(cornell, luts)
+    for f in frames(cornell, abi.LSS_RESTIR_DI, n, w=w, h=h, reuse_radius=5):
+        r.render(f)
+    r.synchronize_kernel()
+    ref = r.framebuffer(abi.FB_COLOR)
+    r.close()
+    assert np.array_equal(got, ref), f"{(got != ref).sum()} values differ"
