@@ -28,7 +28,7 @@ SYMBOLS = [
     "mpt_update_materials", "mpt_set_envmap", "mpt_build_alias_table", "mpt_set_luts", "mpt_resize",
     "mpt_render_frame", "mpt_synchronize", "mpt_query_done", "mpt_get_framebuffer", "mpt_partition_rows",
     "mpt_enable_stats", "mpt_get_stats", "mpt_trace_closest", "mpt_trace_any", "mpt_clear_status",
-    "mpt_query_status", "mpt_get_aux_buffer", "mpt_build_envmap_cdf", "mpt_set_envmap_cdf",
+    "mpt_query_status", "mpt_get_aux_buffer", "mpt_build_envmap_cdf", "mpt_set_envmap_cdf", "mpt_set_halo_exchange",
 ]
 
 
