@@ -42,6 +42,8 @@ METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
 HBM_PEAK_GBS = 8000.0
 S_NODE, S_TRI = 80, 48
 BAND_H = 8
+BATCH_1GPU = 8     # samples per wavefront on a whole-frame context (measured: DESIGN.md §5)
+MAX_BATCH = 64     # MPT_MAX_BATCH
 
 
 def parse():
@@ -60,6 +62,12 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="target CPU-baseline sample duration")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true", help="skip the RMSE-vs-oracle band check")
+    ap.add_argument("--batch", type=int, default=0,
+                    help="samples per pixel traced as one wavefront (mpt_render_frames); 0 = auto: "
+                         "BATCH_1GPU x the ranks' share of the frame, so a rank's launches stay frame-sized")
+    ap.add_argument("--emulate-rank-of", type=int, default=1,
+                    help="scaling rehearsal on one GPU: render only rank 0's share of an N-way row split "
+                         "(the line then reports that rank's rate; not a bench line)")
     return ap.parse_args()
 
 
@@ -208,7 +216,14 @@ def main():
         band = partition.contiguous_band(H, world, rank) if world > 1 else (1, 0, 1)
     else:
         band = (BAND_H, rank, world)
+    if world == 1 and a.emulate_rank_of > 1 and a.workload != "c4":
+        band = (BAND_H, 0, a.emulate_rank_of)
+        a.no_parity = a.no_cpu_baseline = True
     band_h = band[0]
+    share = band[2] if a.workload != "c4" else world   # ranks the frame is split over
+    batch = min(MAX_BATCH, a.batch or (BATCH_1GPU * share))
+    while K % batch:                                     # whole batches in the timed region
+        batch -= 1
 
     r = mpt.GPURenderer(local)
     r.set_scene(sd)
@@ -222,13 +237,14 @@ def main():
 
     # calibration: instrumented traversal -> nodes / triangles per query per stage
     r.enable_stats(timing=False, instrumented=True)
-    for f in frames_for(cam, W, H, opt, band, 2, first=0, bounces=a.bounces, world=wset, alpha=alpha):
-        r.render(f)
+    # (one batch, so every launch of the run has the timed region's size)
+    r.render_samples(frames_for(cam, W, H, opt, band, max(2, batch), first=0, bounces=a.bounces, world=wset, alpha=alpha),
+                     max_batch=batch)
     cal = r.stats()
     # warmup (untimed), then the timed K-frame accumulation restarting at sample 0
     r.enable_stats(timing=False, instrumented=False)
-    for f in frames_for(cam, W, H, opt, band, a.warmup, bounces=a.bounces, world=wset, alpha=alpha):
-        r.render(f)
+    r.render_samples(frames_for(cam, W, H, opt, band, a.warmup, bounces=a.bounces, world=wset, alpha=alpha),
+                     max_batch=batch)
     frames = frames_for(cam, W, H, opt, band, K, bounces=a.bounces, world=wset, alpha=alpha)
     r.synchronize_kernel()
     r.enable_stats(timing=True, instrumented=False)
@@ -240,8 +256,7 @@ def main():
         dist.barrier()
         torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for f in frames:
-        r.render(f)
+    r.render_samples(frames, max_batch=batch)
     r.synchronize_kernel()
     if dist is not None:
         r.framebuffer_to_device(abi.FB_COLOR, local_fb.data_ptr())
@@ -348,6 +363,7 @@ def main():
             "data": ("synthetic (seeded procedural city + sky standing in for Bistro + its HDR, CPU seed schedule)"
                      if a.workload in ("c3", "c4") else f"synthetic (reference glTF {sd.name}, seeded CPU seed schedule)"),
             "msample_per_s": round(W * H * K / elapsed / 1e6, 3),
+            "samples_per_launch": round(st.frames / max(1, st.shade_launches / (a.bounces + 1)), 3),
             "rays_per_sample": round(rays_total / (W * H * K), 4),
             "config": {"workload": f"{desc}, {W}x{H}, {K} spp, "
                                    f"{'layered Principled' if a.bsdf == 'principled' else 'Lambert-override'} BSDF + NEE "
@@ -371,6 +387,9 @@ def main():
             "cpu_baseline": cpu,
             "parity_vs_oracle": parity,
         }
+        if band[2] > world:
+            out["emulated_rank_of"] = band[2]
+            out["msample_per_s"] = round(rows * W * K / elapsed / 1e6, 3)
         if halo is not None:
             nfr = 2 + a.warmup + K
             out["halo_exchange"] = {"calls_per_frame": round(halo.calls / nfr, 2),

@@ -51,7 +51,7 @@ struct DBuf {
     }
 };
 
-constexpr int FRAME_RING = 64;
+constexpr int FRAME_RING = 128;   // >= 2 x MPT_MAX_BATCH
 constexpr int EV_POOL = 256;
 #ifndef MPT_TRACE_BLOCKS_PER_CU
 #define MPT_TRACE_BLOCKS_PER_CU 4
@@ -95,7 +95,9 @@ struct MptContext {
     int env_w = 0, env_h = 0;
     float env_sum = 0.0f;
     // paths
-    int res_x = 0, res_y = 0, band_h = 1, band_i = 0, band_c = 1, n_slots = 0;
+    int res_x = 0, res_y = 0, band_h = 1, band_i = 0, band_c = 1, n_slots = 0;   // n_slots = pixels of the partition
+    int batch_cap = 0;      // samples per pixel the path state is sized for (mpt_render_frames)
+    int batch = 1;          // samples of the launch being set up
     DBuf<float4> ray_o, ray_d, hit, thr, col, alb, nrmv, nq_o, nq_d, nhit;
     DBuf<uint8_t> hit_inside, occ, qmask;
     DBuf<uint32_t> rng, spill;
@@ -190,7 +192,8 @@ DevScene dev_scene(MptContext* c) {
 
 DevPaths dev_paths(MptContext* c) {
     DevPaths P{};
-    P.n = c->n_slots;
+    P.n = c->n_slots * c->batch;
+    P.n_pix = c->n_slots;
     P.res_x = c->res_x;
     P.ray_o = c->ray_o.p;
     P.ray_d = c->ray_d.p;
@@ -248,27 +251,42 @@ int rows_of(int res_y, int bh, int bi, int bc) {
     return r;
 }
 
+// Path state (everything indexed by path slot) for `batch` samples per pixel of the
+// partition; grows on demand, never shrinks while the partition stays the same.
+int ensure_batch(MptContext* c, int batch) {
+    if (batch <= c->batch_cap && c->ray_o.p) return MPT_OK;
+    HIPCHK(hipStreamSynchronize(c->stream));
+    const size_t N = (size_t)std::max(c->n_slots, 1) * (size_t)batch;
+    HIPCHK(c->ray_o.alloc(N)); HIPCHK(c->ray_d.alloc(N)); HIPCHK(c->hit.alloc(N)); HIPCHK(c->hit_inside.alloc(N));
+    HIPCHK(c->rng.alloc(N)); HIPCHK(c->thr.alloc(N)); HIPCHK(c->col.alloc(N)); HIPCHK(c->vsA.alloc(N)); HIPCHK(c->vsB.alloc(N));
+    HIPCHK(c->alb.alloc(N)); HIPCHK(c->nrmv.alloc(N)); HIPCHK(c->q0.alloc(N)); HIPCHK(c->q1.alloc(N));
+    HIPCHK(c->nee.alloc(N)); HIPCHK(c->nq_o.alloc(4 * N)); HIPCHK(c->nq_d.alloc(4 * N)); HIPCHK(c->nq_tgt.alloc(4 * N));
+    HIPCHK(c->occ.alloc(4 * N)); HIPCHK(c->nhit.alloc(N)); HIPCHK(c->qmask.alloc(N)); HIPCHK(c->active.alloc(N));
+    HIPCHK(hipMemsetAsync(c->active.p, 0, N, c->stream));
+    if (c->mat_slot.p) HIPCHK(c->mat_slot.alloc(N));
+    c->batch_cap = batch;
+    return MPT_OK;
+}
+
 int ensure_paths(MptContext* c, int rx, int ry, int bh, int bi, int bc) {
     int rows = rows_of(ry, bh, bi, bc);
     int n = rows * rx;
     bool same = c->res_x == rx && c->res_y == ry && c->band_h == bh && c->band_i == bi && c->band_c == bc && c->n_slots == n && c->ray_o.p;
     if (same) return MPT_OK;
+    HIPCHK(hipStreamSynchronize(c->stream));
     c->res_x = rx; c->res_y = ry; c->band_h = bh; c->band_i = bi; c->band_c = bc; c->n_slots = n;
     size_t N = (size_t)std::max(n, 1);
-    HIPCHK(c->ray_o.alloc(N)); HIPCHK(c->ray_d.alloc(N)); HIPCHK(c->hit.alloc(N)); HIPCHK(c->hit_inside.alloc(N));
-    HIPCHK(c->rng.alloc(N)); HIPCHK(c->thr.alloc(N)); HIPCHK(c->col.alloc(N)); HIPCHK(c->vsA.alloc(N)); HIPCHK(c->vsB.alloc(N));
-    HIPCHK(c->alb.alloc(N)); HIPCHK(c->nrmv.alloc(N)); HIPCHK(c->q0.alloc(N)); HIPCHK(c->q1.alloc(N));
-    HIPCHK(c->nee.alloc(N)); HIPCHK(c->nq_o.alloc(4 * N)); HIPCHK(c->nq_d.alloc(4 * N)); HIPCHK(c->nq_tgt.alloc(4 * N));
-    HIPCHK(c->occ.alloc(4 * N)); HIPCHK(c->nhit.alloc(N)); HIPCHK(c->qmask.alloc(N));
+    c->batch_cap = 0;
+    int r = ensure_batch(c, 1);
+    if (r != MPT_OK) return r;
     HIPCHK(c->fb_color.alloc(3 * N)); HIPCHK(c->fb_albedo.alloc(3 * N)); HIPCHK(c->fb_normal.alloc(3 * N));
     HIPCHK(hipMemsetAsync(c->fb_color.p, 0, 3 * N * sizeof(float), c->stream));
     HIPCHK(hipMemsetAsync(c->fb_albedo.p, 0, 3 * N * sizeof(float), c->stream));
     HIPCHK(hipMemsetAsync(c->fb_normal.p, 0, 3 * N * sizeof(float), c->stream));
-    HIPCHK(c->as_count.alloc(N)); HIPCHK(c->as_sqlum.alloc(N)); HIPCHK(c->as_conv.alloc(N)); HIPCHK(c->active.alloc(N));
+    HIPCHK(c->as_count.alloc(N)); HIPCHK(c->as_sqlum.alloc(N)); HIPCHK(c->as_conv.alloc(N));
     HIPCHK(hipMemsetAsync(c->as_count.p, 0, N * sizeof(int32_t), c->stream));
     HIPCHK(hipMemsetAsync(c->as_sqlum.p, 0, N * sizeof(float), c->stream));
     HIPCHK(hipMemsetAsync(c->as_conv.p, 0xff, N * sizeof(int32_t), c->stream));
-    HIPCHK(hipMemsetAsync(c->active.p, 0, N, c->stream));
     return MPT_OK;
 }
 
@@ -692,8 +710,8 @@ int mpt_resize(MptContext* c, int32_t w, int32_t h) {
     return ensure_paths(c, w, h, c->band_h, c->band_i, c->band_c);
 }
 
-int mpt_render_frame(MptContext* c, const MptFrame* f) {
-    if (!c || !f) return fail(MPT_ERR_INVALID_ARGUMENT, "NULL argument");
+// `batch` consecutive samples (f[0..batch-1], checked by mpt_render_frames) as one wavefront
+static int render_batch(MptContext* c, const MptFrame* f, int batch) {
     if (!c->has_scene) return fail(MPT_ERR_NO_SCENE, "no scene uploaded");
     if (!c->lut_conductor.p && f->options.bsdf_override == MPT_BSDF_NONE) return fail(MPT_ERR_INVALID_ARGUMENT, "Principled BSDF needs mpt_set_luts");
     int v = validate_frame(f);
@@ -713,17 +731,22 @@ int mpt_render_frame(MptContext* c, const MptFrame* f) {
         r = ensure_restir(c, f);
         if (r != MPT_OK) return r;
     }
-    if ((c->any_tex || f->bsdf_flags.white_furnace_mode) && c->mat_slot.n < (size_t)std::max(c->n_slots, 1)) {
+    r = ensure_batch(c, batch);
+    if (r != MPT_OK) return r;
+    const size_t n_paths = (size_t)std::max(c->n_slots, 1) * (size_t)c->batch_cap;
+    if ((c->any_tex || f->bsdf_flags.white_furnace_mode) && c->mat_slot.n < n_paths) {
         HIPCHK(hipStreamSynchronize(c->stream));
-        HIPCHK(c->mat_slot.alloc((size_t)std::max(c->n_slots, 1)));
+        HIPCHK(c->mat_slot.alloc(n_paths));
     }
     // stage the frame constants through a pinned ring (the previous use of the slot
     // has completed once 64 frames later are enqueued; synchronise defensively)
+    if (c->frame_slot + batch > FRAME_RING) c->frame_slot = 0;
     int slot = c->frame_slot;
-    c->frame_slot = (c->frame_slot + 1) % FRAME_RING;
+    c->frame_slot = (c->frame_slot + batch) % FRAME_RING;
     if (slot == 0) HIPCHK(hipStreamSynchronize(c->stream));
-    c->h_frames[slot] = *f;
-    HIPCHK(hipMemcpyAsync(c->d_frames + slot, c->h_frames + slot, sizeof(MptFrame), hipMemcpyHostToDevice, c->stream));
+    for (int k = 0; k < batch; k++) c->h_frames[slot + k] = f[k];
+    HIPCHK(hipMemcpyAsync(c->d_frames + slot, c->h_frames + slot, batch * sizeof(MptFrame), hipMemcpyHostToDevice,
+                          c->stream));
     int pool = (int)(c->frames_submitted & 1u);
     if (c->timing) {
         int rc = collect_pool(c, pool);
@@ -748,7 +771,9 @@ int mpt_render_frame(MptContext* c, const MptFrame* f) {
         cfg.h_reproj = c->h_reproj;
     }
     if (c->timing) HIPCHK(hipEventRecord(c->ev_frame[pool][0], c->stream));
+    c->batch = batch;
     DevPaths P = dev_paths(c);
+    c->batch = 1;
     if (restir_part) {   // frame_begin maintains the band and the previous frame's halo rows
         P.rs_lo = std::max(0, cfg.own_y0 - cfg.halo_prev) * f->res_x;
         P.rs_hi = std::min(f->res_y, cfg.own_y1 + cfg.halo_prev) * f->res_x;
@@ -764,8 +789,46 @@ int mpt_render_frame(MptContext* c, const MptFrame* f) {
         c->ev_pending[pool] = true;
     }
     c->frames_submitted++;
-    c->frames++;
+    c->frames += batch;
     c->trace_launches += cfg.launches;
+    return MPT_OK;
+}
+
+int mpt_render_frame(MptContext* c, const MptFrame* f) {
+    if (!c || !f) return fail(MPT_ERR_INVALID_ARGUMENT, "NULL argument");
+    return render_batch(c, f, 1);
+}
+
+// Frames that differ only in what GPURenderer::render changes between the samples of one
+// call (GPURenderer.cpp:424-449: sample number, seeds, AOV counter, reset / status flags)
+// and need no per-sample feedback (adaptive sampling, the stop-noise threshold and ReSTIR
+// DI read the previous sample's results) are rendered as one wavefront.
+static bool batchable(const MptFrame& a, const MptFrame& b) {
+    if (a.options.direct_light_sampling == MPT_LSS_RESTIR_DI) return false;
+    const MptRenderSettings& rs = a.render_settings;
+    if ((rs.stop_pixel_noise_threshold > 0.0f || rs.enable_adaptive_sampling) && rs.accumulate) return false;
+    MptFrame t = b;
+    t.render_settings.sample_number = a.render_settings.sample_number;
+    t.render_settings.denoiser_AOV_accumulation_counter = a.render_settings.denoiser_AOV_accumulation_counter;
+    t.render_settings.need_to_reset = a.render_settings.need_to_reset;
+    t.render_settings.do_update_status_buffers = a.render_settings.do_update_status_buffers;
+    t.random_seed = a.random_seed;
+    t.camera_random_seed = a.camera_random_seed;
+    return std::memcmp(&t, &a, sizeof(MptFrame)) == 0;
+}
+
+int mpt_render_frames(MptContext* c, const MptFrame* frames, int32_t count, int32_t max_batch) {
+    if (!c || !frames || count < 0) return fail(MPT_ERR_INVALID_ARGUMENT, "NULL argument or negative count");
+    if (max_batch <= 0) max_batch = MPT_MAX_BATCH;
+    max_batch = std::min<int32_t>(max_batch, MPT_MAX_BATCH);
+    int i = 0;
+    while (i < count) {
+        int b = 1;
+        while (i + b < count && b < max_batch && batchable(frames[i], frames[i + b])) b++;
+        int r = render_batch(c, frames + i, b);
+        if (r != MPT_OK) return r;
+        i += b;
+    }
     return MPT_OK;
 }
 

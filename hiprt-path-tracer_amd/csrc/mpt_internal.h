@@ -1,6 +1,7 @@
 // mpt_internal.h -- device-side data layout shared by the C ABI (mpt_api.cpp) and the
-// kernels (mpt_kernels.hip).  All buffers are SoA in HBM, indexed by "slot" = the
-// index of a pixel inside the context's row partition.
+// kernels (mpt_kernels.hip).  All buffers are SoA in HBM.  Per-pixel buffers are indexed
+// by the index of a pixel inside the context's row partition; path state by "slot" =
+// sample-in-batch * n_pix + pixel (a single-sample frame has slot == pixel).
 #ifndef MPT_INTERNAL_H
 #define MPT_INTERNAL_H
 
@@ -86,7 +87,8 @@ enum : uint32_t {
 };
 
 struct DevPaths {
-    int32_t n;                // slots
+    int32_t n;                // path slots of the launch = batch samples x n_pix
+    int32_t n_pix;            // pixels of the partition (per-pixel buffers: framebuffers, adaptive, ReSTIR)
     int32_t res_x;
     float4* ray_o;            // xyz + last_hit bits
     float4* ray_d;            // xyz + tmax

@@ -310,6 +310,7 @@ struct TraceArgs {
 DEV uint32_t slot_pixel(const MptFrame& F, int slot, int& x, int& y);
 DEV uint32_t pixel_seed(const MptFrame& F, uint32_t pix);
 DEV uint32_t camera_seed(const MptFrame& F, uint32_t pix);
+DEV uint32_t path_seed(const MptFrame* Fp, const DevPaths& P, int slot, bool camera);
 
 #ifndef MPT_TRACE_WAVES
 #define MPT_TRACE_WAVES 1
@@ -359,11 +360,8 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MODE == TM_P
                         rd = P.ray_d[ray];
                         skips = 0;
                         was_inside = false;
-                        if (A.alpha) {   // bounce 0: the camera launch's seed (CameraRays traces the camera ray)
-                            int px, py;
-                            uint32_t pix = slot_pixel(*A.F, ray, px, py);
-                            pseed = A.bounce == 0 ? camera_seed(*A.F, pix) : pixel_seed(*A.F, pix);
-                        }
+                        if (A.alpha)     // bounce 0: the camera launch's seed (CameraRays traces the camera ray)
+                            pseed = path_seed(A.F, P, ray, A.bounce == 0);
                         tr.init(mk3(ro.x, ro.y, ro.z), mk3(rd.x, rd.y, rd.z), (int)__float_as_uint(ro.w), INFINITY,
                                 A.alpha != 0, A.alpha ? alpha_key(pseed, A.bounce, 0, 0) : 0u);
                     } else if (MODE == TM_NEE_ANY || MODE == TM_NEE_CLOSEST) {
@@ -374,7 +372,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MODE == TM_P
                         qmax = rd.w;
                         const bool al = A.alpha != 0;
                         uint32_t akey = 0u;
-                        if (al) { int px, py; akey = alpha_key(pixel_seed(*A.F, slot_pixel(*A.F, ray >> 2, px, py)), A.bounce, (ray & 3) + 1, 0); }
+                        if (al) akey = alpha_key(path_seed(A.F, P, ray >> 2, false), A.bounce, (ray & 3) + 1, 0);
                         tr.init(mk3(ro.x, ro.y, ro.z), mk3(rd.x, rd.y, rd.z), (int)__float_as_uint(ro.w), ANY ? rd.w : INFINITY, al, akey);
                     } else {
                         ray = i;
@@ -582,6 +580,17 @@ DEV uint32_t pixel_seed(const MptFrame& F, uint32_t pix) { return pixel_seed(F, 
 DEV uint32_t camera_seed(const MptFrame& F, uint32_t pix) {
     return pixel_seed(F, pix, F.camera_random_seed ? F.camera_random_seed : F.random_seed);
 }
+// Sample batch (mpt_render_frames; GPURenderer::render's samples_per_frame loop,
+// GPURenderer.cpp:424-449, run as one wavefront): path slot s is pixel slot s % n_pix of
+// the batch's sample s / n_pix, whose seeds and sample number are those of Fp[s / n_pix].
+DEV int batch_sub(const DevPaths& P, int slot) { return slot < P.n_pix ? 0 : slot / P.n_pix; }
+DEV uint32_t path_seed(const MptFrame* Fp, const DevPaths& P, int slot, bool camera) {
+    const int sub = batch_sub(P, slot);
+    const MptFrame& F = Fp[sub];
+    int x, y;
+    const uint32_t pix = slot_pixel(F, slot - sub * P.n_pix, x, y);
+    return camera ? camera_seed(F, pix) : pixel_seed(F, pix);
+}
 
 // ----------------------------------------------------------------------------------
 // k_camera: CameraRays ray generation (CameraRays.h:127-142, HIPRTCamera.h:27-47)
@@ -625,9 +634,10 @@ DEV bool adaptive_sampling(const DevPaths& P, const MptRenderSettings& rs, int s
 }
 
 __global__ __launch_bounds__(TB) void k_camera(DevPaths P, const MptFrame* __restrict__ Fp) {
-    const MptFrame& F = *Fp;
-    const MptRenderSettings& rs = F.render_settings;
     int slot = blockIdx.x * TB + threadIdx.x;
+    const int sub = slot < P.n ? batch_sub(P, slot) : 0;   // batched launches never use the adaptive buffers
+    const MptFrame& F = Fp[sub];
+    const MptRenderSettings& rs = F.render_settings;
     const bool as = has_adaptive_buffers(rs);
     bool act = slot < P.n;
     if (act) {
@@ -669,7 +679,7 @@ __global__ __launch_bounds__(TB) void k_camera(DevPaths P, const MptFrame* __res
     if (!act) return;
     if (rs.do_update_status_buffers) P.status[1] = 1u;
     int x, y;
-    uint32_t pix = slot_pixel(F, slot, x, y);
+    uint32_t pix = slot_pixel(F, slot - sub * P.n_pix, x, y);
     Rng rng = make_rng(camera_seed(F, pix));
     float xd = (float)x + 0.5f, yd = (float)y + 0.5f;
     if (F.current_camera.do_jittering) { xd += rng() - 0.5f; yd += rng() - 0.5f; }
@@ -951,8 +961,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MPT_SHADE_WA
             gn = normalize(gn);
             sn = normalize(sn);
             d = normalize(d);
-            int x, y;
-            rng = make_rng(pixel_seed(F, slot_pixel(F, slot, x, y)));
+            rng = make_rng(path_seed(A.F, P, slot, false));
         }
         NeeRec& nr = P.nee[slot];   // written field by field, straight to HBM
         uint32_t fl = 0;
@@ -1527,11 +1536,7 @@ __global__ __launch_bounds__(TB) void k_resolve(DevScene S, DevPaths P, const Mp
 // ----------------------------------------------------------------------------------
 // k_accumulate (FullPathTracer.h:292-327)
 // ----------------------------------------------------------------------------------
-__global__ __launch_bounds__(TB) void k_accumulate(DevPaths P, const MptFrame* __restrict__ Fp) {
-    const MptFrame& F = *Fp;
-    const MptRenderSettings& rs = F.render_settings;
-    int slot = blockIdx.x * TB + threadIdx.x;
-    if (slot >= P.n) return;
+DEV void accumulate_sample(const DevPaths& P, const MptRenderSettings& rs, int pixel, int slot) {
     if (!P.active[slot]) return;          // FullPathTracer.h:114-115
     float4 cv = P.col[slot];
     Col c = col(cv.x, cv.y, cv.z);
@@ -1539,7 +1544,7 @@ __global__ __launch_bounds__(TB) void k_accumulate(DevPaths P, const MptFrame* _
     bool invalid = false;
     if (wl == 0.0f) invalid |= (c.r < 0 || c.g < 0 || c.b < 0);
     invalid |= has_nan(c);
-    float* fb = P.fb_color + 3 * (size_t)slot;
+    float* fb = P.fb_color + 3 * (size_t)pixel;
     if (invalid) {
         if (rs.display_NaNs) {
             Col dc = col(1.0e30f, 0.0f, 1.0e30f);
@@ -1551,14 +1556,14 @@ __global__ __launch_bounds__(TB) void k_accumulate(DevPaths P, const MptFrame* _
     P.status[1] = 1u;                     // still_one_ray_active (FullPathTracer.h:299)
     if (has_adaptive_buffers(rs)) {
         float l = lum(c);
-        P.as_sqlum[slot] += l * l;
+        P.as_sqlum[pixel] += l * l;
     }
     if (rs.sample_number == 0) { fb[0] = c.r; fb[1] = c.g; fb[2] = c.b; }
     else { fb[0] += c.r; fb[1] += c.g; fb[2] += c.b; }
     float cnt = (float)rs.denoiser_AOV_accumulation_counter;
     float4 a = P.alb[slot], n = P.nrm[slot];
-    float* fa = P.fb_albedo + 3 * (size_t)slot;
-    float* fn = P.fb_normal + 3 * (size_t)slot;
+    float* fa = P.fb_albedo + 3 * (size_t)pixel;
+    float* fn = P.fb_normal + 3 * (size_t)pixel;
     if (rs.sample_number == 0) {
         fa[0] = a.x; fa[1] = a.y; fa[2] = a.z;
         fn[0] = n.x; fn[1] = n.y; fn[2] = n.z;
@@ -1570,6 +1575,14 @@ __global__ __launch_bounds__(TB) void k_accumulate(DevPaths P, const MptFrame* _
         float len = length(acc);
         if (!is_zero(len)) { acc = acc / len; fn[0] = acc.x; fn[1] = acc.y; fn[2] = acc.z; }
     }
+}
+// one pixel per lane; the samples of a batch are added in sample order, exactly as
+// consecutive single-sample frames would add them
+__global__ __launch_bounds__(TB) void k_accumulate(DevPaths P, const MptFrame* __restrict__ Fp) {
+    const int pixel = blockIdx.x * TB + threadIdx.x;
+    if (pixel >= P.n_pix) return;
+    const int nsub = P.n / P.n_pix;
+    for (int sub = 0; sub < nsub; sub++) accumulate_sample(P, Fp[sub].render_settings, pixel, sub * P.n_pix + pixel);
 }
 
 // ----------------------------------------------------------------------------------
@@ -1759,7 +1772,7 @@ hipError_t launch_frame(const DevScene& S, const DevPaths& P0, const MptFrame* d
     }
     {
         TimedScope ts(cfg, st, KT_ACCUMULATE);
-        hipLaunchKernelGGL(k_accumulate, dim3(blocks_for(n)), dim3(TB), 0, st, P, d_frame);
+        hipLaunchKernelGGL(k_accumulate, dim3(blocks_for(P.n_pix)), dim3(TB), 0, st, P, d_frame);
     }
     return hipGetLastError();
 }

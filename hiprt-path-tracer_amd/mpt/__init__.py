@@ -26,7 +26,7 @@ __all__ = ["abi", "scene", "lib", "GPURenderer", "MptError", "build_envmap", "pa
 SYMBOLS = [
     "mpt_last_error", "mpt_version", "mpt_abi_sizes", "mpt_create", "mpt_destroy", "mpt_upload_scene",
     "mpt_update_materials", "mpt_set_envmap", "mpt_build_alias_table", "mpt_set_luts", "mpt_resize",
-    "mpt_render_frame", "mpt_synchronize", "mpt_query_done", "mpt_get_framebuffer", "mpt_partition_rows",
+    "mpt_render_frame", "mpt_render_frames", "mpt_synchronize", "mpt_query_done", "mpt_get_framebuffer", "mpt_partition_rows",
     "mpt_enable_stats", "mpt_get_stats", "mpt_trace_closest", "mpt_trace_any", "mpt_clear_status",
     "mpt_query_status", "mpt_get_aux_buffer", "mpt_build_envmap_cdf", "mpt_set_envmap_cdf", "mpt_set_halo_exchange",
 ]
@@ -71,6 +71,7 @@ def lib() -> C.CDLL:
     L.mpt_set_luts.argtypes = [vp, C.POINTER(abi.Luts)]
     L.mpt_resize.argtypes = [vp, i32, i32]
     L.mpt_render_frame.argtypes = [vp, C.POINTER(abi.Frame)]
+    L.mpt_render_frames.argtypes = [vp, C.POINTER(abi.Frame), i32, i32]
     L.mpt_synchronize.argtypes = [vp]
     L.mpt_query_done.argtypes = [vp, C.POINTER(C.c_int)]
     L.mpt_get_framebuffer.argtypes = [vp, C.c_int, vp, C.c_int]
@@ -199,6 +200,21 @@ class GPURenderer:
             raise MptError(rc or -1, f"halo exchange failed: {err!r}") from err
         _check(rc)
         self.frame = frame
+
+    def render_samples(self, frames, max_batch: int = 0):
+        """GPURenderer::render with samples_per_frame = len(frames): enqueues every frame's
+        sample; runs of batchable frames (mpt.h mpt_render_frames) are traced as one
+        wavefront of up to max_batch samples per pixel (0: the library maximum)."""
+        if not frames:
+            return
+        arr = (abi.Frame * len(frames))(*frames)
+        rc = lib().mpt_render_frames(self.h, arr, len(frames), int(max_batch))
+        err = getattr(self, "_halo_error", None)
+        if err is not None:
+            self._halo_error = None
+            raise MptError(rc or -1, f"halo exchange failed: {err!r}") from err
+        _check(rc)
+        self.frame = frames[-1]
 
     def synchronize_kernel(self):
         _check(lib().mpt_synchronize(self.h))

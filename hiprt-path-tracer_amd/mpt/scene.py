@@ -62,14 +62,18 @@ class SceneData:
         return self
 
     def to_abi(self):
-        """Builds an abi.Scene (keeps references to the numpy arrays alive on self)."""
+        """Builds an abi.Scene.  The arrays it points to are kept alive by the returned
+        struct itself (`_keep`), so every caller that holds the struct -- e.g. a CPU oracle
+        that reads the scene in place -- keeps its own copy valid, whatever later calls do."""
         C = abi.C
         s = abi.Scene()
-        self._keep = []
+        keep = []
+        s._keep = keep
+        self._keep = keep
 
         def ptr(a, t):
             a = np.ascontiguousarray(a)
-            self._keep.append(a)
+            keep.append(a)
             return a.ctypes.data_as(C.POINTER(t))
 
         s.triangle_indices = ptr(self.triangle_indices.astype(np.int32), abi.i32)
@@ -81,7 +85,7 @@ class SceneData:
         s.num_vertices = len(self.vertices)
         s.material_indices = ptr(self.material_indices.astype(np.int32), abi.i32)
         mats = (abi.Material * len(self.materials))(*self.materials)
-        self._keep.append(mats)
+        keep.append(mats)
         s.materials = C.cast(mats, C.POINTER(abi.Material))
         s.num_materials = len(self.materials)
         s.emissive_triangle_indices = ptr(self.emissive.astype(np.int32) if len(self.emissive) else np.zeros(1, np.int32), abi.i32)
@@ -89,9 +93,9 @@ class SceneData:
         s.num_textures = len(self.textures)
         if self.textures:
             texs = [np.ascontiguousarray(t, dtype=np.uint8) for t in self.textures]
-            self._keep.extend(texs)
+            keep.extend(texs)
             arr = (C.POINTER(C.c_uint8) * len(texs))(*[t.ctypes.data_as(C.POINTER(C.c_uint8)) for t in texs])
-            self._keep.append(arr)
+            keep.append(arr)
             s.texture_data = C.cast(arr, C.POINTER(C.POINTER(C.c_uint8)))
             dims = np.array([[t.shape[1], t.shape[0]] for t in texs], np.int32).ravel()
             s.texture_dims = ptr(dims, abi.i32)

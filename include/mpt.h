@@ -19,6 +19,8 @@
  *                                    .cpp:408-486), i.e. the CameraRays and FullPathTracer
  *                                    kernels (Device/kernels/CameraRays.h:45,
  *                                    Device/kernels/FullPathTracer.h:99)
+ *   mpt_render_frames             <- GPURenderer::render's samples_per_frame loop
+ *                                    (GPURenderer.cpp:424-449) as one batched wavefront
  *   mpt_synchronize / mpt_query_done <- GPURenderer::synchronize_kernel / frame_render_done
  *                                    (GPURenderer.h:149-156)
  *   mpt_get_framebuffer           <- the 'pixels' / denoiser AOV interop buffers
@@ -369,7 +371,7 @@ typedef struct MptStats {
     uint64_t node_visits;       /* BVH8 node fetches, all stages (instrumented) */
     uint64_t triangle_tests;    /* triangle record fetches, all stages (instrumented) */
     uint32_t trace_launches;    /* traversal kernel launches */
-    uint32_t frames;            /* mpt_render_frame calls */
+    uint32_t frames;            /* samples rendered (one per mpt_render_frame, count per mpt_render_frames) */
     double trace_ms;            /* summed traversal kernel time */
     double frame_ms;            /* summed whole-frame time */
     /* per traversal stage: 0 = path rays (camera / continuation, closest hit),
@@ -479,6 +481,17 @@ int mpt_resize(MptContext* ctx, int32_t width, int32_t height);
 /* Renders one sample per pixel of the context's partition, accumulating into the
  * sum framebuffer (assign when render_settings.sample_number == 0). Asynchronous. */
 int mpt_render_frame(MptContext* ctx, const MptFrame* frame);
+/* Renders count consecutive samples (GPURenderer::render's samples_per_frame loop,
+ * GPURenderer.cpp:424-449): frames[k] is the frame of the k-th sample, each with its own
+ * sample_number / seeds.  Runs of frames that differ only in sample_number, random_seed,
+ * camera_random_seed, denoiser_AOV_accumulation_counter, need_to_reset and
+ * do_update_status_buffers, and need no per-sample feedback (no adaptive sampling or
+ * stop-noise threshold, not ReSTIR DI), are traced as ONE wavefront of up to max_batch
+ * (<= MPT_MAX_BATCH; <= 0: MPT_MAX_BATCH) samples per pixel; the result is bit-identical
+ * to count mpt_render_frame calls (samples are added to the sums in order).  Other frames
+ * are rendered one by one.  Asynchronous. */
+#define MPT_MAX_BATCH 64
+int mpt_render_frames(MptContext* ctx, const MptFrame* frames, int32_t count, int32_t max_batch);
 /* Installs the halo exchange of a partitioned ReSTIR DI context (see MptHaloExchange);
  * fn = NULL removes it.  Required before rendering LSS_RESTIR_DI with band_count > 1. */
 int mpt_set_halo_exchange(MptContext* ctx, MptHaloExchangeFn fn, void* user);

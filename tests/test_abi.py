@@ -58,6 +58,7 @@ def test_null_arguments_rejected():
     L = mpt.lib()
     assert L.mpt_create(0, None, None) == -1
     assert L.mpt_render_frame(None, None) == -1
+    assert L.mpt_render_frames(None, None, 0, 0) == -1
     assert L.mpt_upload_scene(None, None) == -1
     assert L.mpt_destroy(None) == 0
 

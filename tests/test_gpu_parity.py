@@ -275,3 +275,57 @@ def test_traversal_grazing_rays_city(city, luts):
     rays[:, 7] = np.float32(1e35) - np.float32(1e-4)
     occ = r.trace_any(rays, lh)
     assert_same(occ, hit & (ot < rays[:, 7]), "grazing occluded")
+
+
+def gpu_render_batched(r, frs, max_batch):
+    r.render_samples(frs, max_batch=max_batch)
+    r.synchronize_kernel()
+    return r.framebuffer(abi.FB_COLOR), r.framebuffer(abi.FB_ALBEDO), r.framebuffer(abi.FB_NORMALS)
+
+
+@pytest.mark.parametrize("max_batch,band,strategy", [(4, (1, 0, 1), "mis"), (2, (1, 0, 1), "ris"), (5, (4, 1, 3), "mis"),
+                                                     (32, (1, 0, 1), "ris")])
+def test_batched_samples_bit_exact(scenes, luts, max_batch, band, strategy):
+    """mpt_render_frames (GPURenderer::render's samples_per_frame loop as one wavefront of
+    several samples per pixel) equals one mpt_render_frame per sample and the oracle,
+    including a batch that does not divide the sample count and a partitioned context."""
+    sd = scenes["cornell_pbr"]
+    W, H = 40, 36
+    r = renderer(sd, luts)
+    frs = frames(sd, W, H, 5, lss=STRATEGIES[strategy], band=band)
+    seq = gpu_render(r, frs)
+    bat = gpu_render_batched(r, frs, max_batch)
+    ref = oracle_for(sd, luts).render(frs, aov=True)
+    for k, what in enumerate(["color", "albedo", "normals"]):
+        assert_same(bat[k], seq[k], f"batched vs sequential {what}")
+        assert_same(bat[k], ref[k], f"batched vs oracle {what}")
+
+
+def test_batched_samples_city_alpha_bit_exact(city, luts):
+    """Batching on the bench workload with alpha testing (alpha keys from each sample's own
+    seed) and textured materials (per-path resolved materials)."""
+    env = mpt.build_envmap(scene.procedural_sky(512, 256, seed=7))
+    band = (8, 7, 48)
+    frs = frames(city, 1920, 1080, 3, lss=abi.LSS_RIS_BSDF_AND_LIGHT, world=scene.envmap_world(1.0), band=band)
+    for f in frs:
+        f.render_settings.do_alpha_testing = True
+    r = renderer(city, luts, env)
+    bat = gpu_render_batched(r, frs, 3)
+    ref = oracle_for(city, luts, env).render(frs, aov=True)
+    for k, what in enumerate(["color", "albedo", "normals"]):
+        assert_same(bat[k], ref[k], f"city batched {what}")
+
+
+def test_batched_samples_fall_back_for_adaptive(scenes, luts):
+    """Adaptive sampling reads each sample's result before the next: such frames are
+    rendered one by one and equal the sequential render."""
+    sd = scenes["cornell_pbr"]
+    r = renderer(sd, luts)
+    frs = frames(sd, 32, 16, 6)
+    for f in frs:
+        f.render_settings.enable_adaptive_sampling = True
+        f.render_settings.adaptive_sampling_min_samples = 2
+        f.render_settings.adaptive_sampling_noise_threshold = 0.5
+    seq = gpu_render(r, frs)[0]
+    bat = gpu_render_batched(r, frs, 4)[0]
+    assert_same(bat, seq, "adaptive frames through mpt_render_frames")
