@@ -13,6 +13,11 @@
 // being short compared with the path-tracing wavefront.  Reservoirs live in three
 // ping-pong HBM buffers of 48 B per pixel (3 x float4), the G-buffer in SoA float4 arrays.
 
+#ifndef MPT_RESTIR_WAVES
+#define MPT_RESTIR_WAVES 2
+#endif
+#define RESTIR_KERNEL __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MPT_RESTIR_WAVES)))
+
 // ---- surfaces (Surface.h:12-73) ----------------------------------------------------
 __device__ MptMaterial g_zero_mat;   // the material of a never-written G-buffer entry (zero-initialised)
 
@@ -387,7 +392,7 @@ __global__ __launch_bounds__(TB) void k_restir_presample(DevScene S, DevPaths P,
 
 // ---- ReSTIR_DI_InitialCandidates (InitialCandidates.h:24-508) ------------------------
 template <int OVR>
-__global__ __launch_bounds__(TB) void k_restir_initial(DevScene S, DevPaths P, const MptFrame* __restrict__ Fp) {
+RESTIR_KERNEL void k_restir_initial(DevScene S, DevPaths P, const MptFrame* __restrict__ Fp) {
     __shared__ uint2 lds[LDS_STACK * TB];
     const MptFrame& F = *Fp;
     const MptReSTIRDISettings& rd = F.render_settings.restir_di_settings;
@@ -534,7 +539,7 @@ DEV int restir_temporal_neighbor(const DevScene& S, const DevPaths& P, const Mpt
 
 // ---- ReSTIR_DI_SpatiotemporalReuse (FusedSpatiotemporalReuse.h:112-586) ----------------
 template <int OVR>
-__global__ __launch_bounds__(TB) void k_restir_spatiotemporal(DevScene S, DevPaths P, const MptFrame* __restrict__ Fp) {
+RESTIR_KERNEL void k_restir_spatiotemporal(DevScene S, DevPaths P, const MptFrame* __restrict__ Fp) {
     __shared__ uint2 lds[LDS_STACK * TB];
     const MptFrame& F = *Fp;
     const BCtx bc = make_bctx(S, F);
@@ -634,7 +639,7 @@ __global__ __launch_bounds__(TB) void k_restir_spatiotemporal(DevScene S, DevPat
 
 // ---- ReSTIR_DI_SpatialReuse (SpatialReuse.h:52-348) ------------------------------------
 template <int OVR>
-__global__ __launch_bounds__(TB) void k_restir_spatial(DevScene S, DevPaths P, const MptFrame* __restrict__ Fp, int pass,
+RESTIR_KERNEL void k_restir_spatial(DevScene S, DevPaths P, const MptFrame* __restrict__ Fp, int pass,
                                                        const float4* __restrict__ in, float4* out) {
     __shared__ uint2 lds[LDS_STACK * TB];
     const MptFrame& F = *Fp;
