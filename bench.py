@@ -167,11 +167,20 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    # rehearsal of the N-rank path on a one-GPU box: MPT_BENCH_BACKEND=gloo (host-staged
+    # collectives) + MPT_BENCH_SHARE_GPU=1 (every rank on device 0); not a bench line
+    backend = os.environ.get("MPT_BENCH_BACKEND", "nccl")
+    if os.environ.get("MPT_BENCH_SHARE_GPU"):
+        local = 0
+    coll_dev = "cuda" if backend == "nccl" else "cpu"
     if world > 1:
         import torch
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     W = a.width or (3840 if a.workload == "c5" else 1920)
     H = a.height or (2160 if a.workload == "c5" else 1080)
     default_bounces = a.bounces is None
@@ -253,6 +262,7 @@ def main():
     if dist is not None:
         import torch
         local_fb = torch.zeros((rows, W, 3), dtype=torch.float32, device="cuda")
+        host_fb = None if coll_dev == "cuda" else torch.zeros((rows, W, 3), dtype=torch.float32)
         dist.barrier()
         torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -260,7 +270,9 @@ def main():
     r.synchronize_kernel()
     if dist is not None:
         r.framebuffer_to_device(abi.FB_COLOR, local_fb.data_ptr())
-        frame = partition.gather_frame(local_fb, H, band_h, dist)
+        if host_fb is not None:
+            host_fb.copy_(local_fb)
+        frame = partition.gather_frame(local_fb if host_fb is None else host_fb, H, band_h, dist)
         torch.cuda.synchronize()
         dist.barrier()
     elapsed = time.perf_counter() - t0
@@ -268,10 +280,10 @@ def main():
 
     rays_local = st.rays_closest + st.rays_any
     if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        n = torch.tensor([rays_local], dtype=torch.float64, device="cuda")
+        n = torch.tensor([rays_local], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(n, op=dist.ReduceOp.SUM)
         rays_total = float(n.item())
     else:

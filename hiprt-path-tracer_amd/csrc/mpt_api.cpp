@@ -233,7 +233,7 @@ DevPaths dev_paths(MptContext* c) {
     P.pgb_pos = c->pgb_pos.p; P.pgb_sn = c->pgb_sn.p; P.pgb_gn = c->pgb_gn.p; P.pgb_view = c->pgb_view.p; P.pgb_meta = c->pgb_meta.p;
     P.pgb_vsA = c->pgb_vsA.p; P.pgb_vsB = c->pgb_vsB.p; P.pgb_mat = c->pgb_mat.p;
     P.rs_init = c->rs_init.p; P.rs_sp1 = c->rs_sp1.p; P.rs_sp2 = c->rs_sp2.p; P.rs_plights = c->rs_plights.p;
-    P.rs_out = c->restir_out_sp2 ? c->rs_sp2.p : c->rs_sp1.p;
+    P.rs_out = c->restir_out_sp2 == 1 ? c->rs_sp2.p : c->restir_out_sp2 == 2 ? c->rs_init.p : c->rs_sp1.p;
     P.rs_tin = P.rs_out;
     // contiguous band (ReSTIR DI across a partition) or the whole frame: slot s = pixel s + pix_off
     const bool part = c->band_c > 1;
@@ -390,10 +390,8 @@ int validate_frame(const MptFrame* f) {
         if (f->band_count != 1 && (int64_t)f->band_height * f->band_count < f->res_y)
             return fail(MPT_ERR_UNSUPPORTED, "ReSTIR DI across a partition needs one contiguous band per context "
                                              "(band_height * band_count >= res_y)");
-        if (!rd.do_fused_spatiotemporal)
-            return fail(MPT_ERR_UNSUPPORTED, "ReSTIR DI: only the fused spatiotemporal configuration (the reference default)");
-        if (rd.number_of_passes < 1 || rd.number_of_passes > 5)
-            return fail(MPT_ERR_UNSUPPORTED, "ReSTIR DI: number_of_passes must be in [1, 5] (restir_di_seeds)");
+        if (rd.number_of_passes < 1 || rd.number_of_passes > 4)
+            return fail(MPT_ERR_UNSUPPORTED, "ReSTIR DI: number_of_passes must be in [1, 4] (restir_di_seeds)");
         if (rd.number_of_subsets <= 0 || rd.subset_size <= 0 || rd.tile_size <= 0)
             return fail(MPT_ERR_INVALID_ARGUMENT, "ReSTIR DI: bad light presampling settings");
         if (rd.reuse_neighbor_count > 32 || rd.disocclusion_reuse_count > 32)

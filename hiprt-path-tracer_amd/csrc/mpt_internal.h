@@ -172,7 +172,7 @@ struct LaunchCfg {
     int ev_cap;
     int ev_used;
     uint32_t launches;
-    int restir_out_sp2;       // in/out: restir_output_reservoirs is rs_sp2 (else rs_sp1)
+    int restir_out_sp2;       // in/out: restir_output_reservoirs: 0 rs_sp1, 1 rs_sp2, 2 rs_init
     // ReSTIR DI across a row partition: the host's halo exchange (mpt_set_halo_exchange)
     MptHaloExchangeFn halo_fn;
     void* halo_user;

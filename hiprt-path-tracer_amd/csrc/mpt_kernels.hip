@@ -1626,6 +1626,11 @@ static void launch_ovr(int ovr, dim3 g, hipStream_t st, Args... args) {
 template <int OVR> struct KInitial { static constexpr auto fn = k_restir_initial<OVR>; };
 template <int OVR> struct KSpatiotemporal { static constexpr auto fn = k_restir_spatiotemporal<OVR>; };
 template <int OVR> struct KSpatial { static constexpr auto fn = k_restir_spatial<OVR>; };
+template <int OVR> struct KTemporal { static constexpr auto fn = k_restir_temporal<OVR>; };
+
+// restir_output_reservoirs of a frame, as a code kept by the context between frames
+static float4* restir_buffer(const DevPaths& P, int code) { return code == 1 ? P.rs_sp2 : code == 2 ? P.rs_init : P.rs_sp1; }
+static int restir_code(const DevPaths& P, const float4* b) { return b == P.rs_sp2 ? 1 : b == P.rs_init ? 2 : 0; }
 
 // Halo exchange of a partitioned context (mpt.h MptHaloExchange): the host fills the rows
 // around the band from the contexts that own them.  No-op for a whole-frame context.
@@ -1687,19 +1692,44 @@ static void launch_restir(const DevScene& S, DevPaths& P, const MptFrame* d_fram
     hipLaunchKernelGGL(k_restir_presample, dim3((n_pl + TB - 1) / TB), dim3(TB), 0, st, S, P, d_frame);
     const dim3 g(cfg.grid_persistent);
     launch_ovr<KInitial>(ovr, g, st, S, P, d_frame);
-    float4* last_out = cfg.restir_out_sp2 ? P.rs_sp2 : P.rs_sp1;
-    P.rs_tin = last_out;
-    P.rs_out = last_out == P.rs_sp1 ? P.rs_sp2 : P.rs_sp1;
-    halo_exchange(hf, cfg, st, MPT_HALO_RESERVOIRS, 0, cfg.halo_rows, {{P.rs_tin, RB}});
-    launch_ovr<KSpatiotemporal>(ovr, g, st, S, P, d_frame);
-    for (int pass = 1; pass < rd.number_of_passes; pass++) {
-        float4* in = P.rs_out;
-        float4* out = in == P.rs_sp1 ? P.rs_sp2 : P.rs_sp1;
-        halo_exchange(hf, cfg, st, MPT_HALO_RESERVOIRS, pass, cfg.halo_rows, {{in, RB}});
-        launch_ovr<KSpatial>(ovr, g, st, S, P, d_frame, pass, (const float4*)in, out);
-        P.rs_out = out;
+    float4* last_out = restir_buffer(P, cfg.restir_out_sp2);
+    if (rd.do_fused_spatiotemporal) {
+        P.rs_tin = last_out;
+        P.rs_out = last_out == P.rs_sp1 ? P.rs_sp2 : P.rs_sp1;
+        halo_exchange(hf, cfg, st, MPT_HALO_RESERVOIRS, 0, cfg.halo_rows, {{P.rs_tin, RB}});
+        launch_ovr<KSpatiotemporal>(ovr, g, st, S, P, d_frame);
+        for (int pass = 1; pass < rd.number_of_passes; pass++) {
+            float4* in = P.rs_out;
+            float4* out = in == P.rs_sp1 ? P.rs_sp2 : P.rs_sp1;
+            halo_exchange(hf, cfg, st, MPT_HALO_RESERVOIRS, pass, cfg.halo_rows, {{in, RB}});
+            launch_ovr<KSpatial>(ovr, g, st, S, P, d_frame, pass, (const float4*)in, out);
+            P.rs_out = out;
+        }
+    } else {
+        // separate temporal and spatial passes (ReSTIRDIRenderPass::configure_temporal_pass /
+        // configure_spatial_pass, ReSTIRDIRenderPass.cpp:332-418): the temporal pass writes
+        // into the initial-candidates buffer when spatial passes follow (each pixel reads
+        // only its own entry there), spatial pass 0 writes sp1, later passes ping-pong
+        float4* cur = P.rs_init;
+        if (rd.do_temporal_reuse_pass) {
+            P.rs_tin = last_out;
+            float4* tout = rd.do_spatial_reuse_pass ? P.rs_init : (last_out == P.rs_sp1 ? P.rs_sp2 : P.rs_sp1);
+            halo_exchange(hf, cfg, st, MPT_HALO_RESERVOIRS, 0, cfg.halo_rows, {{P.rs_tin, RB}});
+            launch_ovr<KTemporal>(ovr, g, st, S, P, d_frame, (const float4*)P.rs_tin, tout);
+            cur = tout;
+        }
+        if (rd.do_spatial_reuse_pass) {
+            for (int pass = 0; pass < rd.number_of_passes; pass++) {
+                float4* in = pass == 0 ? cur : ((pass & 1) ? P.rs_sp1 : P.rs_sp2);
+                float4* out = pass == 0 ? P.rs_sp1 : ((pass & 1) ? P.rs_sp2 : P.rs_sp1);
+                halo_exchange(hf, cfg, st, MPT_HALO_RESERVOIRS, pass + 1, cfg.halo_rows, {{in, RB}});
+                launch_ovr<KSpatial>(ovr, g, st, S, P, d_frame, pass, (const float4*)in, out);
+                cur = out;
+            }
+        }
+        P.rs_out = cur;   // configure_output_buffer (ReSTIRDIRenderPass.cpp:566-576)
     }
-    cfg.restir_out_sp2 = P.rs_out == P.rs_sp2 ? 1 : 0;
+    cfg.restir_out_sp2 = restir_code(P, P.rs_out);
 }
 
 hipError_t launch_frame(const DevScene& S, const DevPaths& P0, const MptFrame* d_frame, const MptFrame& hf, LaunchCfg& cfg,
@@ -1712,7 +1742,7 @@ hipError_t launch_frame(const DevScene& S, const DevPaths& P0, const MptFrame* d
     const bool restir = hf.options.direct_light_sampling == MPT_LSS_RESTIR_DI;
     if (restir) {
         hipLaunchKernelGGL(k_restir_frame_begin, dim3(blocks_for(P.rs_hi - P.rs_lo)), dim3(TB), 0, st, P, d_frame);
-        P.rs_out = cfg.restir_out_sp2 ? P.rs_sp2 : P.rs_sp1;
+        P.rs_out = restir_buffer(P, cfg.restir_out_sp2);
     }
     // all pixels start a path, unless adaptive sampling compacts the camera queue
     hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(&P.counters[CTR_Q0]), as ? 0 : n, 1, st);

@@ -637,6 +637,78 @@ RESTIR_KERNEL void k_restir_spatiotemporal(DevScene S, DevPaths P, const MptFram
     count_pass_rays(P, rr.n_any, rr.n_closest);
 }
 
+// ---- ReSTIR_DI_TemporalReuse (TemporalReuse.h:48-306), the non-fused chain ---------------
+// Pairwise-MIS-defensive weights (TemporalMISWeight.h:203-279), normalisation 1 / 1
+// (TemporalNormalizationWeight.h), visibility in the target function (BiasCorrectionUseVisibility).
+template <int OVR>
+RESTIR_KERNEL void k_restir_temporal(DevScene S, DevPaths P, const MptFrame* __restrict__ Fp, const float4* __restrict__ tin_c,
+                                     float4* out) {
+    __shared__ uint2 lds[LDS_STACK * TB];
+    const MptFrame& F = *Fp;
+    const BCtx bc = make_bctx(S, F);
+    RRays rr{&S, lds, P.stack_spill + ((size_t)blockIdx.x * TB + threadIdx.x) * (2 * SPILL_DEPTH),
+             F.render_settings.do_alpha_testing, 0u, 8, 0, 0u, 0u};
+    float4* tin = const_cast<float4*>(tin_c);
+    const MptReSTIRDISettings& rd = F.render_settings.restir_di_settings;
+    for (int s = blockIdx.x * TB + threadIdx.x; s < P.n; s += gridDim.x * TB) {
+        const int center = s + P.pix_off;
+        if (!P.active[s] || !P.gb_meta[center].z) continue;
+        uint32_t seed = pass_seed(F, (uint32_t)center, F.restir_di_seeds[2]);
+        Rng rng = make_rng(seed);
+        rr.pseed = seed;
+        rr.n = 0;
+        if (rd.temporal_buffer_clear_requested) rr_store(tin, center, rr_default());
+        RSurf cs = gb_surface(S, P, center, false);
+        if (is_emissive(*cs.m)) continue;
+        const bool use_prev = rd.do_temporal_reuse_pass;   // use_prev_frame_g_buffer (RenderSettings.h:237-247)
+        int tpx, tpy;
+        int tidx = restir_temporal_neighbor(S, P, F, cs.p, cs.sn, *cs.m, rng, tpx, tpy);
+        const RResv ic = rr_load(P.rs_init, center);
+        if (tidx == -1 || F.render_settings.freeze_random) { rr_store(out, center, ic); continue; }
+        const RResv tres = rr_load(tin, tidx);
+        if (tres.M == 0) { rr_store(out, center, ic); continue; }
+        RSurf ts = gb_surface(S, P, tidx, use_prev);
+        if (is_emissive(*ts.m)) { rr_store(out, center, ic); continue; }
+        RResv o = rr_default();
+        float mc = 0.0f;
+        {
+            float tfc = 0.0f;
+            if (tres.UCW > 0.0f) tfc = restir_target(S, F, bc, rr, tres.tri, tres.point, tres.flags, cs, true, OVR);
+            float jac = 1.0f;
+            if (tfc > 0.0f && tres.UCW > 0.0f && !(tres.flags & RF_ENVMAP)) {
+                jac = restir_jacobian(S, tres, cs.sp, ts.sp - ts.sn * 1.0e-4f);
+                if (jac == -1.0f) jac = 0.0f;
+            }
+            // get_resampling_MIS_weight(TEMPORAL_NEIGHBOR_ID)
+            const bool cw = rd.use_confidence_weights;
+            float tM = cw ? (float)tres.M : 1.0f, cM = cw ? (float)ic.M : 1.0f, nsum = cw ? (float)tres.M : 1.0f;
+            float tfn = tres.target;
+            float nume = tfn * tM;
+            float denom = tfn * nsum + tfc * cM;
+            float mi = denom == 0.0f ? 0.0f : (nume / denom);
+            if (cw) mi *= nsum / (nsum + cM);
+            float tcn = restir_target(S, F, bc, rr, ic.tri, ic.point, ic.flags, ts, true, OVR);
+            float tcc = ic.target;
+            float nume_mc = tcc * cM;
+            float denom_mc = tcn * nsum + tcc * cM;
+            float conf = cw ? nsum / (nsum + cM) : 1.0f;
+            if (denom_mc != 0.0f) mc += nume_mc / denom_mc * conf;
+            float wgt = cw ? mi : mi * 0.5f;
+            if (rr_combine(o, tres, wgt, tfc, jac, rng)) o.flags |= RF_UNOCCLUDED;
+        }
+        // the initial candidates (INITIAL_CANDIDATES_ID)
+        float wc;
+        if (mc == 0.0f) wc = 1.0f;
+        else if (rd.use_confidence_weights) wc = mc + (float)ic.M / (float)(ic.M + tres.M);
+        else wc = (1.0f + mc) * 0.5f;
+        if (rr_combine(o, ic, wc, ic.target, 1.0f, rng)) o.flags |= RF_UNOCCLUDED;
+        rr_end_normalized(o);
+        if (rd.m_cap > 0) o.M = imin(o.M, rd.m_cap);
+        rr_store(out, center, o);
+    }
+    count_pass_rays(P, rr.n_any, rr.n_closest);
+}
+
 // ---- ReSTIR_DI_SpatialReuse (SpatialReuse.h:52-348) ------------------------------------
 template <int OVR>
 RESTIR_KERNEL void k_restir_spatial(DevScene S, DevPaths P, const MptFrame* __restrict__ Fp, int pass,
@@ -647,7 +719,7 @@ RESTIR_KERNEL void k_restir_spatial(DevScene S, DevPaths P, const MptFrame* __re
     RRays rr{&S, lds, P.stack_spill + ((size_t)blockIdx.x * TB + threadIdx.x) * (2 * SPILL_DEPTH),
              F.render_settings.do_alpha_testing, 0u, 7, 0, 0u, 0u};
     const int W = F.res_x;
-    const uint32_t pass_rs = F.restir_di_seeds[3 + pass];
+    const uint32_t pass_rs = F.restir_di_seeds[4 + pass];
     for (int s = blockIdx.x * TB + threadIdx.x; s < P.n; s += gridDim.x * TB) {
         const int center = s + P.pix_off;
         MptReSTIRDISettings rd = F.render_settings.restir_di_settings;

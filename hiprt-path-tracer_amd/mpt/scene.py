@@ -414,26 +414,50 @@ def _xorshift32(x):
     return x & 0xFFFFFFFF
 
 
-def gpu_seed_schedule(nframes, restir_spatial_passes=None, first_sample=0):
-    """Per-sample seeds as GPURenderer::render draws them from m_rng (seeded 42,
-    GPURenderer.cpp:50, 424-486): the camera launch, then -- with ReSTIR DI -- lights
-    presampling, initial candidates, the fused spatiotemporal pass and its permutation
-    bits, one per extra spatial pass (ReSTIRDIRenderPass.cpp:233-264, 369-507), then the
-    path-tracing launch.  Returns dicts with sample_number, camera_random_seed,
-    restir_di_seeds (8, zero padded) and random_seed (path tracing)."""
-    rng = 42
+def gpu_seed_schedule(nframes, restir_spatial_passes=None, first_sample=0, fused=True, temporal=True, spatial=True,
+                      samples_per_frame=1):
+    """Per-sample seeds as the reference's GPU front-end draws them from m_rng (seeded 42,
+    GPURenderer.cpp:50): GPURenderer::update once per displayed frame (update_render_data,
+    GPURenderer.cpp:980-983; its value is overwritten before any launch), then per sample
+    of GPURenderer::render (GPURenderer.cpp:424-486) the camera launch, the ReSTIR DI passes
+    (ReSTIRDIRenderPass.cpp:233-264, 298-431) and the path-tracing launch.  ReSTIR draws:
+    presampling, initial candidates, then fused: temporal seed + permutation bits
+    (configure_temporal_pass_for_fused_spatiotemporal) and the fused kernel's seed
+    (configure_spatial_pass_for_fused_spatiotemporal(0)), one per extra spatial pass;
+    unfused: temporal seed + permutation bits if the temporal pass runs, one per spatial
+    pass.  Returns dicts with sample_number, camera_random_seed, restir_di_seeds (the
+    MptFrame layout, include/mpt.h) and random_seed (path tracing)."""
+    st = [42]
+
+    def draw():
+        st[0] = _xorshift32(st[0])
+        return st[0]
+
     out = []
     for f in range(nframes):
-        rng = _xorshift32(rng)
-        cam = rng
-        rseeds = []
+        if f % samples_per_frame == 0:
+            draw()                                   # GPURenderer::update
+        cam = draw()
+        seeds = [0] * 8
         if restir_spatial_passes is not None:
-            for _ in range(4 + max(0, restir_spatial_passes - 1)):
-                rng = _xorshift32(rng)
-                rseeds.append(rng)
-        rng = _xorshift32(rng)
+            seeds[0] = draw()
+            seeds[1] = draw()
+            if fused:
+                draw()                               # temporal seed, overwritten before the launch
+                seeds[3] = draw()
+                seeds[2] = draw()
+                for p in range(1, restir_spatial_passes):
+                    seeds[4 + p] = draw()
+            else:
+                if temporal:
+                    seeds[2] = draw()
+                    seeds[3] = draw()
+                if spatial:
+                    for p in range(restir_spatial_passes):
+                        seeds[4 + p] = draw()
+        rs = draw()
         out.append({"sample_number": first_sample + f, "camera_random_seed": cam,
-                    "restir_di_seeds": (rseeds + [0] * 8)[:8], "random_seed": rng})
+                    "restir_di_seeds": seeds, "random_seed": rs})
     return out
 
 

@@ -322,10 +322,14 @@ typedef struct MptFrame {
      * the camera rays too (CPURenderer: one seed per sample, CPURenderer.cpp:271-287). */
     uint32_t camera_random_seed;
     /* LSS_RESTIR_DI: the seeds ReSTIRDIRenderPass::launch draws from the renderer's RNG
-     * (ReSTIRDIRenderPass.cpp:233-264, 369-507), in order: [0] lights presampling,
-     * [1] initial candidates, [2] fused spatiotemporal pass, [3] the permutation-sampling
-     * bits drawn next (the kernels read them from render_settings.restir_di_settings,
-     * where the caller stores them as the reference does), [3 + i] spatial pass i >= 1. */
+     * (ReSTIRDIRenderPass.cpp:233-264, 298-431) that its kernels see as random_seed:
+     * [0] lights presampling, [1] initial candidates, [2] the fused spatiotemporal pass
+     * (the draw of configure_spatial_pass_for_fused_spatiotemporal(0), after the temporal
+     * seed and the permutation bits) or, unfused, the temporal pass, [3] the
+     * permutation-sampling bits (the kernels read them from
+     * render_settings.restir_di_settings, where the caller stores them as the reference
+     * does), [4 + i] spatial pass i (unfused: i >= 0; fused: i >= 1).  Hence
+     * number_of_passes <= 4. */
     uint32_t restir_di_seeds[8];
 } MptFrame;
 

@@ -1198,8 +1198,8 @@ int oracle_render(OracleScene* sc, const MptFrame* frames, int nframes, float* s
     const bool restir = f0.options.direct_light_sampling == MPT_LSS_RESTIR_DI;
     if ((has_adaptive_buffers(f0.render_settings) && !(as_count && as_sqlum && as_conv && status)) ||
         f0.render_settings.wants_render_low_resolution ||
-        (restir && (f0.band_count != 1 || !f0.render_settings.restir_di_settings.do_fused_spatiotemporal ||
-                    f0.render_settings.number_of_light_samples != 1)) ||
+        (restir && (f0.band_count != 1 || f0.render_settings.number_of_light_samples != 1 ||
+                    f0.render_settings.restir_di_settings.number_of_passes > 4)) ||
         (f0.options.envmap_sampling == MPT_ESS_BINARY_SEARCH && s.env_rgba && !s.env_cdf))
         return -4;
     std::vector<int> rows;
@@ -1285,16 +1285,38 @@ int oracle_render(OracleScene* sc, const MptFrame* frames, int nframes, float* s
                 }
             };
             per_pixel([&](Ctx& c, int x, int y) { restir_initial(c, R, x, y); });
-            // fused spatiotemporal: temporal input = last output, spatial output = the other buffer
-            std::vector<OResv>* tin = B.output;
-            std::vector<OResv>* out = tin == &B.sp1 ? &B.sp2 : &B.sp1;
-            per_pixel([&](Ctx& c, int x, int y) { restir_spatiotemporal(c, R, x, y, *tin, *out); });
-            for (int pass = 1; pass < rs.restir_di_settings.number_of_passes; pass++) {
-                std::vector<OResv>* in = out;
-                out = in == &B.sp1 ? &B.sp2 : &B.sp1;
-                per_pixel([&](Ctx& c, int x, int y) { restir_spatial(c, R, x, y, pass, *in, *out); });
+            const MptReSTIRDISettings& rd = rs.restir_di_settings;
+            if (rd.do_fused_spatiotemporal) {
+                // fused spatiotemporal: temporal input = last output, spatial output = the other buffer
+                std::vector<OResv>* tin = B.output;
+                std::vector<OResv>* out = tin == &B.sp1 ? &B.sp2 : &B.sp1;
+                per_pixel([&](Ctx& c, int x, int y) { restir_spatiotemporal(c, R, x, y, *tin, *out); });
+                for (int pass = 1; pass < rd.number_of_passes; pass++) {
+                    std::vector<OResv>* in = out;
+                    out = in == &B.sp1 ? &B.sp2 : &B.sp1;
+                    per_pixel([&](Ctx& c, int x, int y) { restir_spatial(c, R, x, y, pass, *in, *out); });
+                }
+                B.output = out;
+            } else {
+                // separate passes (ReSTIRDIRenderPass.cpp:249-258, 332-418, 566-576): the temporal
+                // pass writes into the initial-candidates buffer when spatial passes follow
+                std::vector<OResv>* cur = &B.init;
+                if (rd.do_temporal_reuse_pass) {
+                    std::vector<OResv>* tin = B.output;
+                    std::vector<OResv>* tout = rd.do_spatial_reuse_pass ? &B.init : (tin == &B.sp1 ? &B.sp2 : &B.sp1);
+                    per_pixel([&](Ctx& c, int x, int y) { restir_temporal(c, R, x, y, *tin, *tout); });
+                    cur = tout;
+                }
+                if (rd.do_spatial_reuse_pass) {
+                    for (int pass = 0; pass < rd.number_of_passes; pass++) {
+                        std::vector<OResv>* in = pass == 0 ? cur : ((pass & 1) ? &B.sp1 : &B.sp2);
+                        std::vector<OResv>* out = pass == 0 ? &B.sp1 : ((pass & 1) ? &B.sp2 : &B.sp1);
+                        per_pixel([&](Ctx& c, int x, int y) { restir_spatial(c, R, x, y, pass, *in, *out); });
+                        cur = out;
+                    }
+                }
+                B.output = cur;
             }
-            B.output = out;
         }
         // ---- FullPathTracer + accumulation (FullPathTracer.h:99-327)
 #pragma omp parallel for schedule(dynamic) reduction(+ : rc, ra) num_threads(nthreads)

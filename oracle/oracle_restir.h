@@ -542,6 +542,70 @@ void restir_spatiotemporal(Ctx& c, RestirPassCtx& R, int x, int y, std::vector<O
     out[(size_t)center] = o;
 }
 
+// ReSTIR_DI_TemporalReuse (TemporalReuse.h:48-306) of the unfused chain: pairwise-MIS-
+// defensive weights (TemporalMISWeight.h:203-279), normalisation 1 / 1, visibility in the
+// target function (ReSTIR_DI_BiasCorrectionUseVisibility).  tin = last frame's output.
+void restir_temporal(Ctx& c, RestirPassCtx& R, int x, int y, std::vector<OResv>& tin, std::vector<OResv>& out) {
+    const MptFrame& f = R.f;
+    const MptReSTIRDISettings& rd = f.render_settings.restir_di_settings;
+    const OScene& s = *c.s;
+    int W = f.res_x;
+    int center = x + y * W;
+    const GB& g = R.cur[(size_t)center];
+    if (!R.active[(size_t)center] || !g.hit) return;
+    uint32_t seed = pass_seed(f, (uint32_t)center, f.restir_di_seeds[2]);
+    Rng rng(seed);
+    c.pseed = seed;
+    RestirRays rr{c, 8};
+    if (rd.temporal_buffer_clear_requested) tin[(size_t)center] = OResv();
+    RSurface cs = surface_of(g);
+    if (is_emissive(g.mat)) return;
+    const bool use_prev = rd.do_temporal_reuse_pass;   // use_prev_frame_g_buffer (RenderSettings.h:237-247)
+    int tidx, tpx, tpy;
+    restir_temporal_neighbor(c, R, g.first_hit, cs.sn, center, rng, tidx, tpx, tpy);
+    const OResv ic = R.B.init[(size_t)center];
+    if (tidx == -1 || f.render_settings.freeze_random) { out[(size_t)center] = ic; return; }
+    const OResv tres = tin[(size_t)tidx];
+    if (tres.M == 0) { out[(size_t)center] = ic; return; }
+    const GB& tg = use_prev ? R.prev[(size_t)tidx] : R.cur[(size_t)tidx];
+    if (is_emissive(tg.mat)) { out[(size_t)center] = ic; return; }
+    RSurface ts = surface_of(tg);
+    OResv o;
+    float mc = 0.0f;
+    const bool cw = rd.use_confidence_weights;
+    {
+        float tfc = 0.0f;
+        if (tres.UCW > 0.0f) tfc = restir_target(c, rr, tres.tri, tres.point, tres.flags, cs, true);
+        float jac = 1.0f;
+        if (tfc > 0.0f && tres.UCW > 0.0f && !(tres.flags & RF_ENVMAP)) {
+            jac = restir_jacobian(s, tres, cs.sp, ts.sp - ts.sn * 1.0e-4f);
+            if (jac == -1.0f) jac = 0.0f;
+        }
+        float tM = cw ? (float)tres.M : 1.0f, cM = cw ? (float)ic.M : 1.0f, nsum = cw ? (float)tres.M : 1.0f;
+        float tfn = tres.target;
+        float nume = tfn * tM;
+        float denom = tfn * nsum + tfc * cM;
+        float mi = denom == 0.0f ? 0.0f : (nume / denom);
+        if (cw) mi *= nsum / (nsum + cM);
+        float tcn = restir_target(c, rr, ic.tri, ic.point, ic.flags, ts, true);
+        float tcc = ic.target;
+        float nume_mc = tcc * cM;
+        float denom_mc = tcn * nsum + tcc * cM;
+        float conf = cw ? nsum / (nsum + cM) : 1.0f;
+        if (denom_mc != 0.0f) mc += nume_mc / denom_mc * conf;
+        float w = cw ? mi : mi * 0.5f;
+        if (o.combine_with(tres, w, tfc, jac, rng)) o.flags |= RF_UNOCCLUDED;
+    }
+    float wc;
+    if (mc == 0.0f) wc = 1.0f;
+    else if (cw) wc = mc + (float)ic.M / (float)(ic.M + tres.M);
+    else wc = (1.0f + mc) * 0.5f;
+    if (o.combine_with(ic, wc, ic.target, 1.0f, rng)) o.flags |= RF_UNOCCLUDED;
+    o.end_with_normalization(1.0f, 1.0f);
+    if (rd.m_cap > 0) o.M = std::min(o.M, rd.m_cap);
+    out[(size_t)center] = o;
+}
+
 // ReSTIR_DI_SpatialReuse (SpatialReuse.h:52-348)
 void restir_spatial(Ctx& c, RestirPassCtx& R, int x, int y, int pass, std::vector<OResv>& in, std::vector<OResv>& out) {
     const MptFrame& f = R.f;
@@ -552,7 +616,7 @@ void restir_spatial(Ctx& c, RestirPassCtx& R, int x, int y, int pass, std::vecto
     int center = x + y * W;
     const GB& g = R.cur[(size_t)center];
     if (!R.active[(size_t)center] || !g.hit) return;
-    uint32_t seed = pass_seed(f, (uint32_t)center, f.restir_di_seeds[3 + pass]);
+    uint32_t seed = pass_seed(f, (uint32_t)center, f.restir_di_seeds[4 + pass]);
     Rng rng(seed);
     c.pseed = seed;
     RestirRays rr{c, 7};
@@ -567,7 +631,7 @@ void restir_spatial(Ctx& c, RestirPassCtx& R, int x, int y, int pass, std::vecto
     // count_valid_spatial_neighbors (Utils.h:356-378): current-frame G-buffer
     int cache = 0, vcount = 0, vM = 0;
     for (int k = 0; k < reuse; k++) {
-        int ni = restir_spatial_neighbor(f, k, reuse, rd.reuse_radius, x, y, cr, sr, R.conv, f.restir_di_seeds[3 + pass]);
+        int ni = restir_spatial_neighbor(f, k, reuse, rd.reuse_radius, x, y, cr, sr, R.conv, f.restir_di_seeds[4 + pass]);
         if (ni == -1) continue;
         if (!restir_similar(rd, R.cur[(size_t)ni], R.prev[(size_t)ni], g, cs.sp, cs.sn, false)) continue;
         vM += in[(size_t)ni].M;
@@ -578,7 +642,7 @@ void restir_spatial(Ctx& c, RestirPassCtx& R, int x, int y, int pass, std::vecto
     int start = vM == 0 ? reuse : 0;
     for (int k = start; k < reuse + 1; k++) {
         if (k < reuse && reuse <= 32 && (cache & (1 << k)) == 0) continue;
-        int ni = restir_spatial_neighbor(f, k, reuse, rd.reuse_radius, x, y, cr, sr, R.conv, f.restir_di_seeds[3 + pass]);
+        int ni = restir_spatial_neighbor(f, k, reuse, rd.reuse_radius, x, y, cr, sr, R.conv, f.restir_di_seeds[4 + pass]);
         if (ni == -1) continue;
         if (k < reuse && reuse > 32 && !restir_similar(rd, R.cur[(size_t)ni], R.prev[(size_t)ni], g, cs.sp, cs.sn, false)) continue;
         OResv nr = in[(size_t)ni];

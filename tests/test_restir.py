@@ -29,7 +29,10 @@ def frames(sd, lss, n, passes=2, ovr=abi.BSDF_NONE, bounces=3, world=None, alpha
     opt.direct_light_sampling = lss
     opt.bsdf_override = ovr
     out = []
-    for d in scene.gpu_seed_schedule(n, passes if lss == abi.LSS_RESTIR_DI else None):
+    for d in scene.gpu_seed_schedule(n, passes if lss == abi.LSS_RESTIR_DI else None,
+                                     fused=rd.get("do_fused_spatiotemporal", True),
+                                     temporal=rd.get("do_temporal_reuse_pass", True),
+                                     spatial=rd.get("do_spatial_reuse_pass", True)):
         st = scene.parity_settings(bounces)
         st.do_alpha_testing = alpha
         if adaptive:
@@ -70,10 +73,22 @@ def test_oracle_restir_bsdf_candidate_refraction_quirk(cornell, luts, oracle_lib
     o.close()
 
 
+def test_oracle_restir_unfused_light_candidates_unbiased(cornell, luts, oracle_lib):
+    """The unfused chain (temporal pass with pairwise-MIS-defensive weights, then spatial
+    passes) is unbiased against NEE/MIS with light-only initial candidates, with and
+    without each of its passes."""
+    o = oracle_lib.Oracle(cornell, luts)
+    ref = o.render(frames(cornell, abi.LSS_MIS_LIGHT_BSDF, 384, bounces=0)).mean() / 384
+    for kw in (dict(), dict(do_spatial_reuse_pass=False), dict(do_temporal_reuse_pass=False, passes=2)):
+        a = o.render(frames(cornell, abi.LSS_RESTIR_DI, 96, bounces=0, number_of_initial_bsdf_candidates=0,
+                            do_fused_spatiotemporal=False, **kw)).mean() / 96
+        assert abs(a / ref - 1.0) < 0.02, (kw, a, ref)
+    o.close()
+
+
 def test_oracle_restir_rejects_unsupported(cornell, luts, oracle_lib):
     o = oracle_lib.Oracle(cornell, luts)
-    fr = frames(cornell, abi.LSS_RESTIR_DI, 1)
-    fr[0].render_settings.restir_di_settings.do_fused_spatiotemporal = False
+    fr = frames(cornell, abi.LSS_RESTIR_DI, 1, band=(8, 0, 3))   # one contiguous band per context only
     with pytest.raises(RuntimeError):
         o.render(fr)
     o.close()
@@ -86,6 +101,12 @@ CASES = {
     "no_temporal_g_buffer": dict(do_temporal_reuse_pass=False),
     "permutation_sampling": dict(use_permutation_sampling=True),
     "adaptive": dict(adaptive=True),
+    "unfused": dict(do_fused_spatiotemporal=False),
+    "unfused_three_passes_no_confidence": dict(do_fused_spatiotemporal=False, passes=3, use_confidence_weights=False),
+    "unfused_temporal_only": dict(do_fused_spatiotemporal=False, do_spatial_reuse_pass=False),
+    "unfused_spatial_only": dict(do_fused_spatiotemporal=False, do_temporal_reuse_pass=False),
+    "unfused_no_reuse": dict(do_fused_spatiotemporal=False, do_temporal_reuse_pass=False, do_spatial_reuse_pass=False),
+    "unfused_permutation": dict(do_fused_spatiotemporal=False, use_permutation_sampling=True),
 }
 
 
@@ -112,14 +133,16 @@ def test_gpu_restir_bit_exact(cornell, luts, case):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("case", ["envmap", "envmap_only", "alpha_cards"])
+@pytest.mark.parametrize("case", ["envmap", "envmap_only", "alpha_cards", "alpha_cards_unfused", "envmap_unfused"])
 def test_gpu_restir_scenes_bit_exact(cornell, luts, case):
     import mpt
     from oracle import oracle as orc
     sd = synthetic.with_alpha_cards(cornell) if case == "alpha_cards" else cornell
     env = mpt.build_envmap(scene.procedural_sky(128, 64, seed=7)) if case.startswith("envmap") else None
     world = scene.envmap_world(1.0) if env is not None else None
-    kw = dict(world=world, alpha=case == "alpha_cards")
+    kw = dict(world=world, alpha=case.startswith("alpha_cards"))
+    if case.endswith("_unfused"):
+        kw["do_fused_spatiotemporal"] = False
     frs = frames(sd, abi.LSS_RESTIR_DI, 4, **kw)
     if case == "envmap_only":
         sd = scene.SceneData.__new__(scene.SceneData)
@@ -151,6 +174,8 @@ PART_CASES = {
     "adaptive": (24, 64, 3, dict(adaptive=True, reuse_radius=5)),
     "camera_moves": (24, 64, 3, dict(move_at=2, reuse_radius=5)),
     "permutation_sampling": (24, 64, 2, dict(use_permutation_sampling=True, reuse_radius=5)),
+    "unfused": (24, 64, 3, dict(do_fused_spatiotemporal=False, reuse_radius=5)),
+    "unfused_three_passes_moves": (24, 64, 2, dict(do_fused_spatiotemporal=False, passes=3, move_at=2, reuse_radius=4)),
 }
 
 
