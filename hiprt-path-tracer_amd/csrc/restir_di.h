@@ -113,11 +113,12 @@ DEV bool rr_combine(RResv& r, const RResv& o, float mis, float tf, float jac, Rn
     }
     return false;
 }
-DEV void rr_end_normalized(RResv& r) {   // end_with_normalization(1, 1) of the pairwise weights
-    if (r.wsum == 0.0f || r.wsum < 1.0e-10f || r.wsum > 1.0e10f) r.UCW = 0.0f;
-    else r.UCW = 1.0f / r.target * r.wsum * 1.0f / 1.0f;
+DEV void rr_end_norm(RResv& r, float nume, float denom) {   // end_with_normalization (Reservoir.h:96-106)
+    if (r.wsum == 0.0f || r.wsum < 1.0e-10f || r.wsum > 1.0e10f || denom == 0.0f || nume == 0.0f) r.UCW = 0.0f;
+    else r.UCW = 1.0f / r.target * r.wsum * nume / denom;
     r.M = imin(r.M, 1000000);
 }
+DEV void rr_end_normalized(RResv& r) { rr_end_norm(r, 1.0f, 1.0f); }   // the pairwise weights' 1 / 1
 
 // ReSTIR_DI_evaluate_target_function<vis> (Utils.h:20-128)
 DEV float restir_target(const DevScene& S, const MptFrame& F, const BCtx& bc, RRays& rr, int tri, v3 point, uint32_t flags,
@@ -213,9 +214,30 @@ DEV int restir_spatial_neighbor(const DevPaths& P, const MptFrame& F, int k, int
 // pairwise MIS defensive (SpatiotemporalMISWeight.h:193-291, SpatialMISWeight.h:167-262)
 struct PairwiseMIS {
     float mc;
+    bool defensive;   // PAIRWISE_MIS_DEFENSIVE (else PAIRWISE_MIS, SpatialMISWeight.h:95-165)
+    bool bvis;        // ReSTIR_DI_BiasCorrectionUseVisibility
     DEV float weight(const DevScene& S, const MptFrame& F, const BCtx& bc, RRays& rr, const MptReSTIRDISettings& rd,
                      const RResv& res, const RResv& center, float tf_center, const RSurf& nsurf, int vcount, int vM,
                      bool update_mc, bool canonical, int ovr) {
+        if (!defensive) {
+            const bool cw = rd.use_confidence_weights;
+            if (canonical) return mc == 0.0f ? 1.0f : mc;
+            float tfn = res.target;
+            float rM = cw ? (float)res.M : 1.0f, cM = cw ? (float)center.M : 1.0f, nsum = cw ? (float)vM : 1.0f;
+            float div = cw ? 1.0f : (float)vcount;
+            float nume = tfn * rM;
+            float denom = tfn * nsum + tf_center / div * cM;
+            float mi = denom == 0.0f ? 0.0f : (nume / denom);
+            if (update_mc) {
+                float tcn = restir_target(S, F, bc, rr, center.tri, center.point, center.flags, nsurf, bvis, ovr);
+                float tcc = center.target;
+                float nume_mc = tcc / div * cM;
+                float denom_mc = tcn * nsum + tcc / div * cM;
+                float conf = cw ? rM / nsum : 1.0f;
+                if (denom_mc != 0.0f) mc += nume_mc / denom_mc / div * conf;
+            }
+            return mi / div;
+        }
         if (!canonical) {
             float tfn = res.target;
             float rM = rd.use_confidence_weights ? (float)res.M : 1.0f;
@@ -228,7 +250,7 @@ struct PairwiseMIS {
             if (denom != 0.0f) mi = nume / denom;
             if (rd.use_confidence_weights) mi *= nsum / (nsum + cM);
             if (update_mc) {
-                float tcn = restir_target(S, F, bc, rr, center.tri, center.point, center.flags, nsurf, true, ovr);
+                float tcn = restir_target(S, F, bc, rr, center.tri, center.point, center.flags, nsurf, bvis, ovr);
                 float tcc = center.target;
                 float nume_mc = tcc / div * cM;
                 float denom_mc = tcn * nsum + tcc / div * cM;
@@ -582,11 +604,11 @@ RESTIR_KERNEL void k_restir_spatiotemporal(DevScene S, DevPaths P, const MptFram
         if (temporal_ok) { vcount++; vM += tres.M; }
         RResv o = rr_default();
         const RResv ic = rr_load(P.rs_init, center);
-        PairwiseMIS mis{0.0f};
+        PairwiseMIS mis{0.0f, true, F.options.restir_di_bias_correction_use_visibility != 0};
         if (temporal_ok) {
             RSurf ts = gb_surface(S, P, tidx, use_prev);
             float tfc = 0.0f;
-            if (tres.UCW > 0.0f) tfc = restir_target(S, F, bc, rr, tres.tri, tres.point, tres.flags, cs, true, OVR);
+            if (tres.UCW > 0.0f) tfc = restir_target(S, F, bc, rr, tres.tri, tres.point, tres.flags, cs, mis.bvis, OVR);
             float jac = 1.0f;
             if (tfc > 0.0f && tres.UCW > 0.0f && !(tres.flags & RF_ENVMAP)) {
                 jac = restir_jacobian(S, tres, cs.sp, ts.sp - ts.sn * 1.0e-4f);
@@ -650,6 +672,9 @@ RESTIR_KERNEL void k_restir_temporal(DevScene S, DevPaths P, const MptFrame* __r
              F.render_settings.do_alpha_testing, 0u, 8, 0, 0u, 0u};
     float4* tin = const_cast<float4*>(tin_c);
     const MptReSTIRDISettings& rd = F.render_settings.restir_di_settings;
+    const int mode = F.options.restir_di_bias_correction_weights;
+    const bool bvis = F.options.restir_di_bias_correction_use_visibility != 0;
+    const bool cw = rd.use_confidence_weights;
     for (int s = blockIdx.x * TB + threadIdx.x; s < P.n; s += gridDim.x * TB) {
         const int center = s + P.pix_off;
         if (!P.active[s] || !P.gb_meta[center].z) continue;
@@ -671,38 +696,85 @@ RESTIR_KERNEL void k_restir_temporal(DevScene S, DevPaths P, const MptFrame* __r
         if (is_emissive(*ts.m)) { rr_store(out, center, ic); continue; }
         RResv o = rr_default();
         float mc = 0.0f;
+        int selected = 0;   // MIS-like: TEMPORAL_NEIGHBOR_ID 0 / INITIAL_CANDIDATES_ID 1
+        // GBH weight of a reservoir's sample between the temporal neighbour and the center (TemporalMISWeight.h:62-110)
+        auto gbh = [&](const RResv& r, bool temporal_id) -> float {
+            float tt = restir_target(S, F, bc, rr, r.tri, r.point, r.flags, ts, bvis, OVR);   // temporal M != 0 here
+            if (temporal_id && tt == 0.0f) return 0.0f;
+            float tc = restir_target(S, F, bc, rr, r.tri, r.point, r.flags, cs, bvis, OVR);
+            int tM = cw ? tres.M : 1, cM = cw ? ic.M : 1;
+            float nume = temporal_id ? tt * (float)tM : tc * (float)cM;
+            float denom = tt * (float)tM + tc * (float)cM;
+            return denom == 0.0f ? 0.0f : nume / denom;
+        };
         {
             float tfc = 0.0f;
-            if (tres.UCW > 0.0f) tfc = restir_target(S, F, bc, rr, tres.tri, tres.point, tres.flags, cs, true, OVR);
+            if (tres.UCW > 0.0f) tfc = restir_target(S, F, bc, rr, tres.tri, tres.point, tres.flags, cs, bvis, OVR);
             float jac = 1.0f;
             if (tfc > 0.0f && tres.UCW > 0.0f && !(tres.flags & RF_ENVMAP)) {
                 jac = restir_jacobian(S, tres, cs.sp, ts.sp - ts.sn * 1.0e-4f);
                 if (jac == -1.0f) jac = 0.0f;
             }
-            // get_resampling_MIS_weight(TEMPORAL_NEIGHBOR_ID)
-            const bool cw = rd.use_confidence_weights;
-            float tM = cw ? (float)tres.M : 1.0f, cM = cw ? (float)ic.M : 1.0f, nsum = cw ? (float)tres.M : 1.0f;
-            float tfn = tres.target;
-            float nume = tfn * tM;
-            float denom = tfn * nsum + tfc * cM;
-            float mi = denom == 0.0f ? 0.0f : (nume / denom);
-            if (cw) mi *= nsum / (nsum + cM);
-            float tcn = restir_target(S, F, bc, rr, ic.tri, ic.point, ic.flags, ts, true, OVR);
-            float tcc = ic.target;
-            float nume_mc = tcc * cM;
-            float denom_mc = tcn * nsum + tcc * cM;
-            float conf = cw ? nsum / (nsum + cM) : 1.0f;
-            if (denom_mc != 0.0f) mc += nume_mc / denom_mc * conf;
-            float wgt = cw ? mi : mi * 0.5f;
-            if (rr_combine(o, tres, wgt, tfc, jac, rng)) o.flags |= RF_UNOCCLUDED;
+            float wgt;
+            if (mode == MPT_RESTIR_DI_BIAS_1_OVER_M || mode == MPT_RESTIR_DI_BIAS_1_OVER_Z) wgt = (float)tres.M;
+            else if (mode == MPT_RESTIR_DI_BIAS_MIS_LIKE) wgt = cw ? (float)tres.M : 1.0f;
+            else if (mode == MPT_RESTIR_DI_BIAS_MIS_GBH) wgt = gbh(tres, true);
+            else {
+                // pairwise (TemporalMISWeight.h:139-279): TEMPORAL_NEIGHBOR_ID
+                const bool def = mode == MPT_RESTIR_DI_BIAS_PAIRWISE_MIS_DEFENSIVE;
+                float tM = cw ? (float)tres.M : 1.0f, cM = cw ? (float)ic.M : 1.0f, nsum = cw ? (float)tres.M : 1.0f;
+                float tfn = tres.target;
+                float nume = tfn * tM;
+                float denom = tfn * nsum + tfc * cM;
+                float mi = denom == 0.0f ? 0.0f : (nume / denom);
+                if (def && cw) mi *= nsum / (nsum + cM);
+                float tcn = restir_target(S, F, bc, rr, ic.tri, ic.point, ic.flags, ts, bvis, OVR);
+                float tcc = ic.target;
+                float nume_mc = tcc * cM;
+                float denom_mc = tcn * nsum + tcc * cM;
+                float conf = cw ? (def ? nsum / (nsum + cM) : tM / nsum) : 1.0f;
+                if (denom_mc != 0.0f) mc += nume_mc / denom_mc * conf;
+                wgt = def && !cw ? mi * 0.5f : mi;
+            }
+            if (rr_combine(o, tres, wgt, tfc, jac, rng)) {
+                selected = 0;
+                if (bvis) o.flags |= RF_UNOCCLUDED;
+                else o.flags &= ~RF_UNOCCLUDED;
+            }
         }
         // the initial candidates (INITIAL_CANDIDATES_ID)
         float wc;
-        if (mc == 0.0f) wc = 1.0f;
-        else if (rd.use_confidence_weights) wc = mc + (float)ic.M / (float)(ic.M + tres.M);
+        if (mode == MPT_RESTIR_DI_BIAS_1_OVER_M || mode == MPT_RESTIR_DI_BIAS_1_OVER_Z) wc = (float)ic.M;
+        else if (mode == MPT_RESTIR_DI_BIAS_MIS_LIKE) wc = cw ? (float)ic.M : 1.0f;
+        else if (mode == MPT_RESTIR_DI_BIAS_MIS_GBH) wc = gbh(ic, false);
+        else if (mc == 0.0f) wc = 1.0f;
+        else if (mode == MPT_RESTIR_DI_BIAS_PAIRWISE_MIS) wc = mc;
+        else if (cw) wc = mc + (float)ic.M / (float)(ic.M + tres.M);
         else wc = (1.0f + mc) * 0.5f;
-        if (rr_combine(o, ic, wc, ic.target, 1.0f, rng)) o.flags |= RF_UNOCCLUDED;
-        rr_end_normalized(o);
+        if (rr_combine(o, ic, wc, ic.target, 1.0f, rng)) {
+            selected = 1;
+            if (bvis) o.flags |= RF_UNOCCLUDED;
+            else o.flags |= ic.flags & RF_UNOCCLUDED;
+        }
+        // normalisation (TemporalNormalizationWeight.h)
+        float nn = 1.0f, nd = 1.0f;
+        if (o.wsum > 0.0f) {
+            if (mode == MPT_RESTIR_DI_BIAS_1_OVER_M) nd = (float)(ic.M + tres.M);
+            else if (mode == MPT_RESTIR_DI_BIAS_1_OVER_Z) {
+                nd = 0.0f;
+                float tc = restir_target(S, F, bc, rr, o.tri, o.point, o.flags, cs, bvis, OVR);
+                nd += (float)((tc > 0.0f) * ic.M);
+                float tt = restir_target(S, F, bc, rr, o.tri, o.point, o.flags, ts, bvis, OVR);   // temporal M > 0
+                nd += (float)((tt > 0.0f) * tres.M);
+            } else if (mode == MPT_RESTIR_DI_BIAS_MIS_LIKE) {
+                float tc = restir_target(S, F, bc, rr, o.tri, o.point, o.flags, cs, bvis, OVR);
+                float tt = restir_target(S, F, bc, rr, o.tri, o.point, o.flags, ts, bvis, OVR);
+                nn = selected == 1 ? tc : tt;
+                int icM = cw ? ic.M : 1, tM = cw ? tres.M : 1;
+                nd = tc * (float)icM + tt * (float)tM;
+            }
+        }
+        rr_end_norm(o, nn, nd);
         if (rd.m_cap > 0) o.M = imin(o.M, rd.m_cap);
         rr_store(out, center, o);
     }
@@ -712,7 +784,7 @@ RESTIR_KERNEL void k_restir_temporal(DevScene S, DevPaths P, const MptFrame* __r
 // ---- ReSTIR_DI_SpatialReuse (SpatialReuse.h:52-348) ------------------------------------
 template <int OVR>
 RESTIR_KERNEL void k_restir_spatial(DevScene S, DevPaths P, const MptFrame* __restrict__ Fp, int pass,
-                                                       const float4* __restrict__ in, float4* out) {
+                                    const float4* __restrict__ in, float4* out) {
     __shared__ uint2 lds[LDS_STACK * TB];
     const MptFrame& F = *Fp;
     const BCtx bc = make_bctx(S, F);
@@ -720,6 +792,8 @@ RESTIR_KERNEL void k_restir_spatial(DevScene S, DevPaths P, const MptFrame* __re
              F.render_settings.do_alpha_testing, 0u, 7, 0, 0u, 0u};
     const int W = F.res_x;
     const uint32_t pass_rs = F.restir_di_seeds[4 + pass];
+    const int mode = F.options.restir_di_bias_correction_weights;
+    const bool bvis = F.options.restir_di_bias_correction_use_visibility != 0;
     for (int s = blockIdx.x * TB + threadIdx.x; s < P.n; s += gridDim.x * TB) {
         const int center = s + P.pix_off;
         MptReSTIRDISettings rd = F.render_settings.restir_di_settings;
@@ -738,6 +812,7 @@ RESTIR_KERNEL void k_restir_spatial(DevScene S, DevPaths P, const MptFrame* __re
         const RResv cres = rr_load(in, center);
         if (cres.M <= 1 && rd.do_disocclusion_reuse_boost) rd.reuse_neighbor_count = rd.disocclusion_reuse_count;
         const int reuse = rd.reuse_neighbor_count;
+        const bool cw = rd.use_confidence_weights;
         int cache = 0, vcount = 0, vM = 0;
         for (int k = 0; k < reuse; k++) {
             int ni = restir_spatial_neighbor(P, F, k, reuse, rd.reuse_radius, x, y, cr, sr, pass_rs);
@@ -747,7 +822,15 @@ RESTIR_KERNEL void k_restir_spatial(DevScene S, DevPaths P, const MptFrame* __re
             vcount++;
             cache |= 1 << k;
         }
-        PairwiseMIS mis{0.0f};
+        // the neighbours (center included, k == reuse) the normalisation / GBH loops visit
+        // (get_spatial_neighbor_pixel_index + check_neighbor_similarity_heuristics)
+        auto valid_nb = [&](int j) -> int {
+            int nj = restir_spatial_neighbor(P, F, j, reuse, rd.reuse_radius, x, y, cr, sr, pass_rs);
+            if (nj == -1) return -1;
+            return restir_similar(S, P, rd, nj, *cs.m, cs.sp, cs.sn, false) ? nj : -1;
+        };
+        PairwiseMIS mis{0.0f, mode == MPT_RESTIR_DI_BIAS_PAIRWISE_MIS_DEFENSIVE, bvis};
+        int selected = 0;   // MIS-like
         int start = vM == 0 ? reuse : 0;
         for (int k = start; k < reuse + 1; k++) {
             if (k < reuse && reuse <= 32 && (cache & (1 << k)) == 0) continue;
@@ -767,17 +850,64 @@ RESTIR_KERNEL void k_restir_spatial(DevScene S, DevPaths P, const MptFrame* __re
                 jac = restir_jacobian(S, nr, cs.sp, mk3(np.x, np.y, np.z));
                 if (jac == -1.0f) { o.M += nr.M; continue; }
             }
-            bool update_mc = cres.M > 0 && cres.UCW > 0.0f;
-            RSurf ns = gb_surface(S, P, ni, false);
-            float wgt = mis.weight(S, F, bc, rr, rd, nr, cres, tfc, ns, vcount, vM, update_mc, k == reuse, OVR);
+            float wgt;
+            if (mode == MPT_RESTIR_DI_BIAS_1_OVER_M || mode == MPT_RESTIR_DI_BIAS_1_OVER_Z) wgt = (float)nr.M;
+            else if (mode == MPT_RESTIR_DI_BIAS_MIS_LIKE) wgt = cw ? (float)nr.M : 1.0f;
+            else if (mode == MPT_RESTIR_DI_BIAS_MIS_GBH) {
+                // SpatialMISWeight.h:36-93
+                if (nr.UCW <= 0.0f) wgt = 1.0f;
+                else {
+                    float nume = 0.0f, denom = 0.0f;
+                    for (int j = 0; j < reuse + 1; j++) {
+                        int nj = valid_nb(j);
+                        if (nj == -1) continue;
+                        RSurf js = gb_surface(S, P, nj, false);
+                        float tj = restir_target(S, F, bc, rr, nr.tri, nr.point, nr.flags, js, bvis, OVR);
+                        int M = cw ? rr_load(in, nj).M : 1;
+                        denom += tj * (float)M;
+                        if (j == k) nume = tj * (float)M;
+                    }
+                    wgt = denom == 0.0f ? 0.0f : nume / denom;
+                }
+            } else {
+                bool update_mc = cres.M > 0 && cres.UCW > 0.0f;
+                RSurf ns = gb_surface(S, P, ni, false);
+                wgt = mis.weight(S, F, bc, rr, rd, nr, cres, tfc, ns, vcount, vM, update_mc, k == reuse, OVR);
+            }
             if (rr_combine(o, nr, wgt, tfc, jac, rng)) {
+                selected = k;
                 if (vis) o.flags |= RF_UNOCCLUDED;
                 else if (k == reuse) o.flags |= nr.flags & RF_UNOCCLUDED;
                 else o.flags &= ~RF_UNOCCLUDED;
             }
         }
-        rr_end_normalized(o);
-        if (rd.do_temporal_reuse_pass || rd.number_of_passes - 1 != rd.spatial_pass_index)
+        // normalisation (SpatialNormalizationWeight.h)
+        float nn = 1.0f, nd = 1.0f;
+        if (o.wsum > 0.0f && (mode == MPT_RESTIR_DI_BIAS_1_OVER_M || mode == MPT_RESTIR_DI_BIAS_1_OVER_Z ||
+                              mode == MPT_RESTIR_DI_BIAS_MIS_LIKE)) {
+            nn = mode == MPT_RESTIR_DI_BIAS_MIS_LIKE ? 0.0f : 1.0f;
+            nd = 0.0f;
+            for (int j = 0; j < reuse + 1; j++) {
+                int nj = valid_nb(j);
+                if (nj == -1) continue;
+                if (mode == MPT_RESTIR_DI_BIAS_1_OVER_M) { nd += (float)rr_load(in, nj).M; continue; }
+                RSurf js = gb_surface(S, P, nj, false);
+                float tj = restir_target(S, F, bc, rr, o.tri, o.point, o.flags, js, bvis, OVR);
+                if (tj > 0.0f) {
+                    int M = rr_load(in, nj).M;
+                    if (mode == MPT_RESTIR_DI_BIAS_1_OVER_Z) nd += (float)M;
+                    else {
+                        if (!cw) M = 1;
+                        if (j == selected) nn += tj;
+                        nd += tj * (float)M;
+                    }
+                }
+            }
+        }
+        rr_end_norm(o, nn, nd);
+        const bool vreuse = bvis && (mode == MPT_RESTIR_DI_BIAS_1_OVER_Z || mode == MPT_RESTIR_DI_BIAS_PAIRWISE_MIS ||
+                                     mode == MPT_RESTIR_DI_BIAS_PAIRWISE_MIS_DEFENSIVE);
+        if (vreuse && (rd.do_temporal_reuse_pass || rd.number_of_passes - 1 != rd.spatial_pass_index))
             restir_visibility_reuse(F, rr, o, cs.sp, cs.last);
         if (rd.m_cap > 0) o.M = imin(o.M, rd.m_cap);
         rr_store(out, center, o);

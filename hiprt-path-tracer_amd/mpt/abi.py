@@ -298,14 +298,19 @@ class Camera(C.Structure):
                 ("view_projection", Float4x4), ("do_jittering", c_bool)]
 
 
+RESTIR_DI_BIAS_1_OVER_M, RESTIR_DI_BIAS_1_OVER_Z, RESTIR_DI_BIAS_MIS_LIKE = 0, 1, 2
+RESTIR_DI_BIAS_MIS_GBH, RESTIR_DI_BIAS_PAIRWISE_MIS, RESTIR_DI_BIAS_PAIRWISE_MIS_DEFENSIVE = 3, 4, 5
+
+
 class KernelOptions(C.Structure):
     _fields_ = [("bsdf_override", i32), ("direct_light_sampling", i32), ("envmap_sampling", i32),
-                ("envmap_bsdf_mis", i32), ("ris_use_visibility", i32)]
+                ("envmap_bsdf_mis", i32), ("ris_use_visibility", i32), ("restir_di_bias_correction_weights", i32),
+                ("restir_di_bias_correction_use_visibility", i32)]
 
     @classmethod
     def default(cls):
-        # KernelOptions.h:116, 218, 231, 242, 252
-        return cls(BSDF_NONE, LSS_RIS_BSDF_AND_LIGHT, ESS_ALIAS_TABLE, 1, 0)
+        # KernelOptions.h:116, 218, 231, 242, 252, 335, 304
+        return cls(BSDF_NONE, LSS_RIS_BSDF_AND_LIGHT, ESS_ALIAS_TABLE, 1, 0, RESTIR_DI_BIAS_PAIRWISE_MIS_DEFENSIVE, 1)
 
 
 class BSDFFlags(C.Structure):

@@ -290,7 +290,17 @@ typedef struct MptKernelOptions {
     int32_t envmap_sampling;               /* EnvmapSamplingStrategy (KernelOptions.h:231) */
     int32_t envmap_bsdf_mis;               /* EnvmapSamplingDoBSDFMIS (KernelOptions.h:242) */
     int32_t ris_use_visibility;            /* RISUseVisiblityTargetFunction (KernelOptions.h:252) */
+    int32_t restir_di_bias_correction_weights;        /* ReSTIR_DI_BiasCorrectionWeights (KernelOptions.h:335),
+                                                         MPT_RESTIR_DI_BIAS_* */
+    int32_t restir_di_bias_correction_use_visibility; /* ReSTIR_DI_BiasCorrectionUseVisibility (KernelOptions.h:304) */
 } MptKernelOptions;
+
+#define MPT_RESTIR_DI_BIAS_1_OVER_M 0 /* KernelOptions.h:66-71 */
+#define MPT_RESTIR_DI_BIAS_1_OVER_Z 1
+#define MPT_RESTIR_DI_BIAS_MIS_LIKE 2
+#define MPT_RESTIR_DI_BIAS_MIS_GBH 3
+#define MPT_RESTIR_DI_BIAS_PAIRWISE_MIS 4
+#define MPT_RESTIR_DI_BIAS_PAIRWISE_MIS_DEFENSIVE 5
 
 /* BRDFsData flags (HostDeviceCommon/BSDFsData.h:24-62), the LUTs themselves are
  * uploaded once with mpt_set_luts. */

@@ -365,8 +365,30 @@ void restir_initial(Ctx& c, RestirPassCtx& R, int x, int y) {
 // pairwise MIS defensive weights (SpatiotemporalMISWeight.h:193-291, SpatialMISWeight.h:167-262)
 struct PairwiseMIS {
     float mc = 0.0f;
+    bool defensive = true;   // PAIRWISE_MIS_DEFENSIVE (else PAIRWISE_MIS, SpatialMISWeight.h:95-165)
+    bool bvis = true;        // ReSTIR_DI_BiasCorrectionUseVisibility
     float weight(Ctx& c, RestirRays& rr, const MptReSTIRDISettings& rd, const OResv& res, const OResv& center, float tf_center,
                  const GB& neighbor_gb, int valid_count, int valid_M, bool update_mc, bool canonical) {
+        if (!defensive) {
+            const bool cw = rd.use_confidence_weights;
+            if (canonical) return mc == 0.0f ? 1.0f : mc;
+            float tfn = res.target;
+            float rM = cw ? (float)res.M : 1.0f, cM = cw ? (float)center.M : 1.0f, nsum = cw ? (float)valid_M : 1.0f;
+            float div = cw ? 1.0f : (float)valid_count;
+            float nume = tfn * rM;
+            float denom = tfn * nsum + tf_center / div * cM;
+            float mi = denom == 0.0f ? 0.0f : (nume / denom);
+            if (update_mc) {
+                RSurface ns = surface_of(neighbor_gb);
+                float tcn = restir_target(c, rr, center.tri, center.point, center.flags, ns, bvis);
+                float tcc = center.target;
+                float nume_mc = tcc / div * cM;
+                float denom_mc = tcn * nsum + tcc / div * cM;
+                float conf = cw ? rM / nsum : 1.0f;
+                if (denom_mc != 0.0f) mc += nume_mc / denom_mc / div * conf;
+            }
+            return mi / div;
+        }
         if (!canonical) {
             float tfn = res.target;
             float rM = rd.use_confidence_weights ? (float)res.M : 1.0f;
@@ -380,7 +402,7 @@ struct PairwiseMIS {
             if (rd.use_confidence_weights) mi *= nsum / (nsum + cM);
             if (update_mc) {
                 RSurface ns = surface_of(neighbor_gb);
-                float tcn = restir_target(c, rr, center.tri, center.point, center.flags, ns, true);
+                float tcn = restir_target(c, rr, center.tri, center.point, center.flags, ns, bvis);
                 float tcc = center.target;
                 float nume_mc = tcc / div * cM;
                 float denom_mc = tcn * nsum + tcc / div * cM;
@@ -549,6 +571,9 @@ void restir_temporal(Ctx& c, RestirPassCtx& R, int x, int y, std::vector<OResv>&
     const MptFrame& f = R.f;
     const MptReSTIRDISettings& rd = f.render_settings.restir_di_settings;
     const OScene& s = *c.s;
+    const int mode = f.options.restir_di_bias_correction_weights;
+    const bool bvis = f.options.restir_di_bias_correction_use_visibility != 0;
+    const bool cw = rd.use_confidence_weights;
     int W = f.res_x;
     int center = x + y * W;
     const GB& g = R.cur[(size_t)center];
@@ -572,36 +597,84 @@ void restir_temporal(Ctx& c, RestirPassCtx& R, int x, int y, std::vector<OResv>&
     RSurface ts = surface_of(tg);
     OResv o;
     float mc = 0.0f;
-    const bool cw = rd.use_confidence_weights;
+    int selected = 0;   // MIS-like: TEMPORAL_NEIGHBOR_ID 0 / INITIAL_CANDIDATES_ID 1
+    // ReSTIRDITemporalResamplingMISWeight<MIS_GBH> (TemporalMISWeight.h:62-110)
+    auto gbh = [&](const OResv& r, bool temporal_id) -> float {
+        float tt = restir_target(c, rr, r.tri, r.point, r.flags, ts, bvis);
+        if (temporal_id && tt == 0.0f) return 0.0f;
+        float tc = restir_target(c, rr, r.tri, r.point, r.flags, cs, bvis);
+        int tM = cw ? tres.M : 1, cM = cw ? ic.M : 1;
+        float nume = temporal_id ? tt * (float)tM : tc * (float)cM;
+        float denom = tt * (float)tM + tc * (float)cM;
+        return denom == 0.0f ? 0.0f : nume / denom;
+    };
     {
         float tfc = 0.0f;
-        if (tres.UCW > 0.0f) tfc = restir_target(c, rr, tres.tri, tres.point, tres.flags, cs, true);
+        if (tres.UCW > 0.0f) tfc = restir_target(c, rr, tres.tri, tres.point, tres.flags, cs, bvis);
         float jac = 1.0f;
         if (tfc > 0.0f && tres.UCW > 0.0f && !(tres.flags & RF_ENVMAP)) {
             jac = restir_jacobian(s, tres, cs.sp, ts.sp - ts.sn * 1.0e-4f);
             if (jac == -1.0f) jac = 0.0f;
         }
-        float tM = cw ? (float)tres.M : 1.0f, cM = cw ? (float)ic.M : 1.0f, nsum = cw ? (float)tres.M : 1.0f;
-        float tfn = tres.target;
-        float nume = tfn * tM;
-        float denom = tfn * nsum + tfc * cM;
-        float mi = denom == 0.0f ? 0.0f : (nume / denom);
-        if (cw) mi *= nsum / (nsum + cM);
-        float tcn = restir_target(c, rr, ic.tri, ic.point, ic.flags, ts, true);
-        float tcc = ic.target;
-        float nume_mc = tcc * cM;
-        float denom_mc = tcn * nsum + tcc * cM;
-        float conf = cw ? nsum / (nsum + cM) : 1.0f;
-        if (denom_mc != 0.0f) mc += nume_mc / denom_mc * conf;
-        float w = cw ? mi : mi * 0.5f;
-        if (o.combine_with(tres, w, tfc, jac, rng)) o.flags |= RF_UNOCCLUDED;
+        float w;
+        if (mode == MPT_RESTIR_DI_BIAS_1_OVER_M || mode == MPT_RESTIR_DI_BIAS_1_OVER_Z) w = (float)tres.M;
+        else if (mode == MPT_RESTIR_DI_BIAS_MIS_LIKE) w = cw ? (float)tres.M : 1.0f;
+        else if (mode == MPT_RESTIR_DI_BIAS_MIS_GBH) w = gbh(tres, true);
+        else {
+            // pairwise (TemporalMISWeight.h:139-279), TEMPORAL_NEIGHBOR_ID
+            const bool def = mode == MPT_RESTIR_DI_BIAS_PAIRWISE_MIS_DEFENSIVE;
+            float tM = cw ? (float)tres.M : 1.0f, cM = cw ? (float)ic.M : 1.0f, nsum = cw ? (float)tres.M : 1.0f;
+            float tfn = tres.target;
+            float nume = tfn * tM;
+            float denom = tfn * nsum + tfc * cM;
+            float mi = denom == 0.0f ? 0.0f : (nume / denom);
+            if (def && cw) mi *= nsum / (nsum + cM);
+            float tcn = restir_target(c, rr, ic.tri, ic.point, ic.flags, ts, bvis);
+            float tcc = ic.target;
+            float nume_mc = tcc * cM;
+            float denom_mc = tcn * nsum + tcc * cM;
+            float conf = cw ? (def ? nsum / (nsum + cM) : tM / nsum) : 1.0f;
+            if (denom_mc != 0.0f) mc += nume_mc / denom_mc * conf;
+            w = def && !cw ? mi * 0.5f : mi;
+        }
+        if (o.combine_with(tres, w, tfc, jac, rng)) {
+            selected = 0;
+            if (bvis) o.flags |= RF_UNOCCLUDED;
+            else o.flags &= ~RF_UNOCCLUDED;
+        }
     }
     float wc;
-    if (mc == 0.0f) wc = 1.0f;
+    if (mode == MPT_RESTIR_DI_BIAS_1_OVER_M || mode == MPT_RESTIR_DI_BIAS_1_OVER_Z) wc = (float)ic.M;
+    else if (mode == MPT_RESTIR_DI_BIAS_MIS_LIKE) wc = cw ? (float)ic.M : 1.0f;
+    else if (mode == MPT_RESTIR_DI_BIAS_MIS_GBH) wc = gbh(ic, false);
+    else if (mc == 0.0f) wc = 1.0f;
+    else if (mode == MPT_RESTIR_DI_BIAS_PAIRWISE_MIS) wc = mc;
     else if (cw) wc = mc + (float)ic.M / (float)(ic.M + tres.M);
     else wc = (1.0f + mc) * 0.5f;
-    if (o.combine_with(ic, wc, ic.target, 1.0f, rng)) o.flags |= RF_UNOCCLUDED;
-    o.end_with_normalization(1.0f, 1.0f);
+    if (o.combine_with(ic, wc, ic.target, 1.0f, rng)) {
+        selected = 1;
+        if (bvis) o.flags |= RF_UNOCCLUDED;
+        else o.flags |= ic.flags & RF_UNOCCLUDED;
+    }
+    // ReSTIRDITemporalNormalizationWeight (TemporalNormalizationWeight.h)
+    float nn = 1.0f, nd = 1.0f;
+    if (o.wsum > 0.0f) {
+        if (mode == MPT_RESTIR_DI_BIAS_1_OVER_M) nd = (float)(ic.M + tres.M);
+        else if (mode == MPT_RESTIR_DI_BIAS_1_OVER_Z) {
+            nd = 0.0f;
+            float tc = restir_target(c, rr, o.tri, o.point, o.flags, cs, bvis);
+            nd += (float)((tc > 0.0f) * ic.M);
+            float tt = restir_target(c, rr, o.tri, o.point, o.flags, ts, bvis);
+            nd += (float)((tt > 0.0f) * tres.M);
+        } else if (mode == MPT_RESTIR_DI_BIAS_MIS_LIKE) {
+            float tc = restir_target(c, rr, o.tri, o.point, o.flags, cs, bvis);
+            float tt = restir_target(c, rr, o.tri, o.point, o.flags, ts, bvis);
+            nn = selected == 1 ? tc : tt;
+            int icM = cw ? ic.M : 1, tM = cw ? tres.M : 1;
+            nd = tc * (float)icM + tt * (float)tM;
+        }
+    }
+    o.end_with_normalization(nn, nd);
     if (rd.m_cap > 0) o.M = std::min(o.M, rd.m_cap);
     out[(size_t)center] = o;
 }
@@ -612,11 +685,14 @@ void restir_spatial(Ctx& c, RestirPassCtx& R, int x, int y, int pass, std::vecto
     MptReSTIRDISettings rd = f.render_settings.restir_di_settings;
     rd.spatial_pass_index = pass;
     const OScene& s = *c.s;
+    const int mode = f.options.restir_di_bias_correction_weights;
+    const bool bvis = f.options.restir_di_bias_correction_use_visibility != 0;
     int W = f.res_x;
     int center = x + y * W;
     const GB& g = R.cur[(size_t)center];
     if (!R.active[(size_t)center] || !g.hit) return;
-    uint32_t seed = pass_seed(f, (uint32_t)center, f.restir_di_seeds[4 + pass]);
+    const uint32_t pass_rs = f.restir_di_seeds[4 + pass];
+    uint32_t seed = pass_seed(f, (uint32_t)center, pass_rs);
     Rng rng(seed);
     c.pseed = seed;
     RestirRays rr{c, 7};
@@ -628,21 +704,31 @@ void restir_spatial(Ctx& c, RestirPassCtx& R, int x, int y, int pass, std::vecto
     OResv cres = in[(size_t)center];
     if (cres.M <= 1 && rd.do_disocclusion_reuse_boost) rd.reuse_neighbor_count = rd.disocclusion_reuse_count;
     int reuse = rd.reuse_neighbor_count;
+    const bool cw = rd.use_confidence_weights;
     // count_valid_spatial_neighbors (Utils.h:356-378): current-frame G-buffer
     int cache = 0, vcount = 0, vM = 0;
     for (int k = 0; k < reuse; k++) {
-        int ni = restir_spatial_neighbor(f, k, reuse, rd.reuse_radius, x, y, cr, sr, R.conv, f.restir_di_seeds[4 + pass]);
+        int ni = restir_spatial_neighbor(f, k, reuse, rd.reuse_radius, x, y, cr, sr, R.conv, pass_rs);
         if (ni == -1) continue;
         if (!restir_similar(rd, R.cur[(size_t)ni], R.prev[(size_t)ni], g, cs.sp, cs.sn, false)) continue;
         vM += in[(size_t)ni].M;
         vcount++;
         cache |= 1 << k;
     }
+    // neighbours visited by the normalisation / GBH loops (center included, j == reuse)
+    auto valid_nb = [&](int j) -> int {
+        int nj = restir_spatial_neighbor(f, j, reuse, rd.reuse_radius, x, y, cr, sr, R.conv, pass_rs);
+        if (nj == -1) return -1;
+        return restir_similar(rd, R.cur[(size_t)nj], R.prev[(size_t)nj], g, cs.sp, cs.sn, false) ? nj : -1;
+    };
     PairwiseMIS mis;
+    mis.defensive = mode == MPT_RESTIR_DI_BIAS_PAIRWISE_MIS_DEFENSIVE;
+    mis.bvis = bvis;
+    int selected = 0;
     int start = vM == 0 ? reuse : 0;
     for (int k = start; k < reuse + 1; k++) {
         if (k < reuse && reuse <= 32 && (cache & (1 << k)) == 0) continue;
-        int ni = restir_spatial_neighbor(f, k, reuse, rd.reuse_radius, x, y, cr, sr, R.conv, f.restir_di_seeds[4 + pass]);
+        int ni = restir_spatial_neighbor(f, k, reuse, rd.reuse_radius, x, y, cr, sr, R.conv, pass_rs);
         if (ni == -1) continue;
         if (k < reuse && reuse > 32 && !restir_similar(rd, R.cur[(size_t)ni], R.prev[(size_t)ni], g, cs.sp, cs.sn, false)) continue;
         OResv nr = in[(size_t)ni];
@@ -658,16 +744,63 @@ void restir_spatial(Ctx& c, RestirPassCtx& R, int x, int y, int pass, std::vecto
             jac = restir_jacobian(s, nr, cs.sp, ng.first_hit);
             if (jac == -1.0f) { o.M += nr.M; continue; }
         }
-        bool update_mc = cres.M > 0 && cres.UCW > 0.0f;
-        float w = mis.weight(c, rr, rd, nr, cres, tfc, R.cur[(size_t)ni], vcount, vM, update_mc, k == reuse);
+        float w;
+        if (mode == MPT_RESTIR_DI_BIAS_1_OVER_M || mode == MPT_RESTIR_DI_BIAS_1_OVER_Z) w = (float)nr.M;
+        else if (mode == MPT_RESTIR_DI_BIAS_MIS_LIKE) w = cw ? (float)nr.M : 1.0f;
+        else if (mode == MPT_RESTIR_DI_BIAS_MIS_GBH) {
+            // ReSTIRDISpatialResamplingMISWeight<MIS_GBH> (SpatialMISWeight.h:36-93)
+            if (nr.UCW <= 0.0f) w = 1.0f;
+            else {
+                float nume = 0.0f, denom = 0.0f;
+                for (int j = 0; j < reuse + 1; j++) {
+                    int nj = valid_nb(j);
+                    if (nj == -1) continue;
+                    RSurface js = surface_of(R.cur[(size_t)nj]);
+                    float tj = restir_target(c, rr, nr.tri, nr.point, nr.flags, js, bvis);
+                    int M = cw ? in[(size_t)nj].M : 1;
+                    denom += tj * (float)M;
+                    if (j == k) nume = tj * (float)M;
+                }
+                w = denom == 0.0f ? 0.0f : nume / denom;
+            }
+        } else {
+            bool update_mc = cres.M > 0 && cres.UCW > 0.0f;
+            w = mis.weight(c, rr, rd, nr, cres, tfc, R.cur[(size_t)ni], vcount, vM, update_mc, k == reuse);
+        }
         if (o.combine_with(nr, w, tfc, jac, rng)) {
+            selected = k;
             if (vis) o.flags |= RF_UNOCCLUDED;
             else if (k == reuse) o.flags |= nr.flags & RF_UNOCCLUDED;
             else o.flags &= ~RF_UNOCCLUDED;
         }
     }
-    o.end_with_normalization(1.0f, 1.0f);
-    if (rd.do_temporal_reuse_pass || rd.number_of_passes - 1 != rd.spatial_pass_index)
+    // ReSTIRDISpatialNormalizationWeight (SpatialNormalizationWeight.h)
+    float nn = 1.0f, nd = 1.0f;
+    if (o.wsum > 0.0f && (mode == MPT_RESTIR_DI_BIAS_1_OVER_M || mode == MPT_RESTIR_DI_BIAS_1_OVER_Z ||
+                          mode == MPT_RESTIR_DI_BIAS_MIS_LIKE)) {
+        nn = mode == MPT_RESTIR_DI_BIAS_MIS_LIKE ? 0.0f : 1.0f;
+        nd = 0.0f;
+        for (int j = 0; j < reuse + 1; j++) {
+            int nj = valid_nb(j);
+            if (nj == -1) continue;
+            if (mode == MPT_RESTIR_DI_BIAS_1_OVER_M) { nd += (float)in[(size_t)nj].M; continue; }
+            RSurface js = surface_of(R.cur[(size_t)nj]);
+            float tj = restir_target(c, rr, o.tri, o.point, o.flags, js, bvis);
+            if (tj > 0.0f) {
+                int M = in[(size_t)nj].M;
+                if (mode == MPT_RESTIR_DI_BIAS_1_OVER_Z) nd += (float)M;
+                else {
+                    if (!cw) M = 1;
+                    if (j == selected) nn += tj;
+                    nd += tj * (float)M;
+                }
+            }
+        }
+    }
+    o.end_with_normalization(nn, nd);
+    const bool vreuse = bvis && (mode == MPT_RESTIR_DI_BIAS_1_OVER_Z || mode == MPT_RESTIR_DI_BIAS_PAIRWISE_MIS ||
+                                 mode == MPT_RESTIR_DI_BIAS_PAIRWISE_MIS_DEFENSIVE);
+    if (vreuse && (rd.do_temporal_reuse_pass || rd.number_of_passes - 1 != rd.spatial_pass_index))
         restir_visibility_reuse(c, rr, o, cs.sp, cs.last_hit);
     if (rd.m_cap > 0) o.M = std::min(o.M, rd.m_cap);
     out[(size_t)center] = o;

@@ -17,7 +17,7 @@ W, H = 32, 24
 
 
 def frames(sd, lss, n, passes=2, ovr=abi.BSDF_NONE, bounces=3, world=None, alpha=False, w=W, h=H, adaptive=False,
-           band=(1, 0, 1), move_at=None, **rd):
+           band=(1, 0, 1), move_at=None, bias=abi.RESTIR_DI_BIAS_PAIRWISE_MIS_DEFENSIVE, bias_vis=1, **rd):
     """move_at: from that frame on the camera is moved (prev_camera = the old one for one frame)."""
     cam = scene.make_camera(sd.camera_info, w, h)
     cam2 = None
@@ -28,6 +28,8 @@ def frames(sd, lss, n, passes=2, ovr=abi.BSDF_NONE, bounces=3, world=None, alpha
     opt = abi.KernelOptions.default()
     opt.direct_light_sampling = lss
     opt.bsdf_override = ovr
+    opt.restir_di_bias_correction_weights = bias
+    opt.restir_di_bias_correction_use_visibility = bias_vis
     out = []
     for d in scene.gpu_seed_schedule(n, passes if lss == abi.LSS_RESTIR_DI else None,
                                      fused=rd.get("do_fused_spatiotemporal", True),
@@ -86,6 +88,26 @@ def test_oracle_restir_unfused_light_candidates_unbiased(cornell, luts, oracle_l
     o.close()
 
 
+BIAS_MODES = {"1_over_m": abi.RESTIR_DI_BIAS_1_OVER_M, "1_over_z": abi.RESTIR_DI_BIAS_1_OVER_Z,
+              "mis_like": abi.RESTIR_DI_BIAS_MIS_LIKE, "gbh": abi.RESTIR_DI_BIAS_MIS_GBH,
+              "pairwise": abi.RESTIR_DI_BIAS_PAIRWISE_MIS}
+
+
+@pytest.mark.parametrize("mode", list(BIAS_MODES))
+def test_oracle_restir_bias_correction_modes(cornell, luts, oracle_lib, mode):
+    """Every bias-correction mode of the unfused chain (TemporalMISWeight.h,
+    SpatialMISWeight.h, *NormalizationWeight.h) on light-only candidates: the unbiased
+    ones (1/Z, MIS-like, generalized balance heuristic, pairwise) match NEE/MIS; 1/M is
+    the biased reference estimator and only has to stay close."""
+    o = oracle_lib.Oracle(cornell, luts)
+    ref = o.render(frames(cornell, abi.LSS_MIS_LIGHT_BSDF, 384, bounces=0)).mean() / 384
+    a = o.render(frames(cornell, abi.LSS_RESTIR_DI, 96, bounces=0, number_of_initial_bsdf_candidates=0,
+                        do_fused_spatiotemporal=False, bias=BIAS_MODES[mode])).mean() / 96
+    tol = 0.15 if mode == "1_over_m" else 0.025
+    assert abs(a / ref - 1.0) < tol, (mode, a, ref)
+    o.close()
+
+
 def test_oracle_restir_rejects_unsupported(cornell, luts, oracle_lib):
     o = oracle_lib.Oracle(cornell, luts)
     fr = frames(cornell, abi.LSS_RESTIR_DI, 1, band=(8, 0, 3))   # one contiguous band per context only
@@ -107,6 +129,17 @@ CASES = {
     "unfused_spatial_only": dict(do_fused_spatiotemporal=False, do_temporal_reuse_pass=False),
     "unfused_no_reuse": dict(do_fused_spatiotemporal=False, do_temporal_reuse_pass=False, do_spatial_reuse_pass=False),
     "unfused_permutation": dict(do_fused_spatiotemporal=False, use_permutation_sampling=True),
+    "bias_1_over_m": dict(do_fused_spatiotemporal=False, bias=abi.RESTIR_DI_BIAS_1_OVER_M),
+    "bias_1_over_z": dict(do_fused_spatiotemporal=False, bias=abi.RESTIR_DI_BIAS_1_OVER_Z, passes=3),
+    "bias_mis_like": dict(do_fused_spatiotemporal=False, bias=abi.RESTIR_DI_BIAS_MIS_LIKE),
+    "bias_mis_like_no_confidence": dict(do_fused_spatiotemporal=False, bias=abi.RESTIR_DI_BIAS_MIS_LIKE,
+                                        use_confidence_weights=False),
+    "bias_gbh": dict(do_fused_spatiotemporal=False, bias=abi.RESTIR_DI_BIAS_MIS_GBH),
+    "bias_pairwise": dict(do_fused_spatiotemporal=False, bias=abi.RESTIR_DI_BIAS_PAIRWISE_MIS),
+    "bias_pairwise_no_confidence": dict(do_fused_spatiotemporal=False, bias=abi.RESTIR_DI_BIAS_PAIRWISE_MIS,
+                                        use_confidence_weights=False),
+    "bias_defensive_no_visibility": dict(do_fused_spatiotemporal=False, bias_vis=0),
+    "bias_1_over_z_no_visibility": dict(do_fused_spatiotemporal=False, bias=abi.RESTIR_DI_BIAS_1_OVER_Z, bias_vis=0),
 }
 
 
@@ -133,16 +166,20 @@ def test_gpu_restir_bit_exact(cornell, luts, case):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("case", ["envmap", "envmap_only", "alpha_cards", "alpha_cards_unfused", "envmap_unfused"])
+@pytest.mark.parametrize("case", ["envmap", "envmap_only", "alpha_cards", "alpha_cards_unfused", "envmap_unfused",
+                                  "alpha_cards_gbh", "envmap_mis_like"])
 def test_gpu_restir_scenes_bit_exact(cornell, luts, case):
     import mpt
     from oracle import oracle as orc
-    sd = synthetic.with_alpha_cards(cornell) if case == "alpha_cards" else cornell
+    sd = synthetic.with_alpha_cards(cornell) if case.startswith("alpha_cards") else cornell
     env = mpt.build_envmap(scene.procedural_sky(128, 64, seed=7)) if case.startswith("envmap") else None
     world = scene.envmap_world(1.0) if env is not None else None
     kw = dict(world=world, alpha=case.startswith("alpha_cards"))
     if case.endswith("_unfused"):
         kw["do_fused_spatiotemporal"] = False
+    if case.endswith("_gbh") or case.endswith("_mis_like"):
+        kw.update(do_fused_spatiotemporal=False,
+                  bias=abi.RESTIR_DI_BIAS_MIS_GBH if case.endswith("_gbh") else abi.RESTIR_DI_BIAS_MIS_LIKE)
     frs = frames(sd, abi.LSS_RESTIR_DI, 4, **kw)
     if case == "envmap_only":
         sd = scene.SceneData.__new__(scene.SceneData)
