@@ -393,10 +393,6 @@ int validate_frame(const MptFrame* f) {
         const int bw = f->options.restir_di_bias_correction_weights;
         if (bw < MPT_RESTIR_DI_BIAS_1_OVER_M || bw > MPT_RESTIR_DI_BIAS_PAIRWISE_MIS_DEFENSIVE)
             return fail(MPT_ERR_INVALID_ARGUMENT, "ReSTIR DI: bad bias correction weights");
-        if (rd.do_fused_spatiotemporal && (bw != MPT_RESTIR_DI_BIAS_PAIRWISE_MIS_DEFENSIVE ||
-                                           !f->options.restir_di_bias_correction_use_visibility))
-            return fail(MPT_ERR_UNSUPPORTED, "ReSTIR DI: the fused spatiotemporal pass implements the pairwise-MIS-defensive "
-                                             "weights with visibility only (unfused passes: all six modes)");
         if (rd.number_of_passes < 1 || rd.number_of_passes > 4)
             return fail(MPT_ERR_UNSUPPORTED, "ReSTIR DI: number_of_passes must be in [1, 4] (restir_di_seeds)");
         if (rd.number_of_subsets <= 0 || rd.subset_size <= 0 || rd.tile_size <= 0)

@@ -604,19 +604,65 @@ RESTIR_KERNEL void k_restir_spatiotemporal(DevScene S, DevPaths P, const MptFram
         if (temporal_ok) { vcount++; vM += tres.M; }
         RResv o = rr_default();
         const RResv ic = rr_load(P.rs_init, center);
-        PairwiseMIS mis{0.0f, true, F.options.restir_di_bias_correction_use_visibility != 0};
+        const int mode = F.options.restir_di_bias_correction_weights;
+        const bool bvis = F.options.restir_di_bias_correction_use_visibility != 0;
+        const bool cw = rd.use_confidence_weights;
+        PairwiseMIS mis{0.0f, mode == MPT_RESTIR_DI_BIAS_PAIRWISE_MIS_DEFENSIVE, bvis};
+        // the temporal neighbour's surface as load_temporal_neighbor_data leaves it: loaded when
+        // its reservoir is not empty, else a default ReSTIRDISurface (zero normals: target 0)
+        RSurf ts;
+        if (temporal_ok) ts = gb_surface(S, P, tidx, use_prev);
+        else { ts = cs; ts.m = &g_zero_mat; ts.sn = ts.gn = ts.view = ts.sp = ts.p = mk3(0.0f, 0.0f, 0.0f); }
+        // neighbours around the temporal position (center included, j == reuse) visited by the
+        // GBH weight / normalisation loops (SpatiotemporalMISWeight.h, SpatiotemporalNormalizationWeight.h)
+        auto valid_nb = [&](int j) -> int {
+            if (j == reuse) return center;
+            int nj = restir_spatial_neighbor(P, F, j, reuse, rd.reuse_radius, tpx, tpy, cr, sr, F.restir_di_seeds[2]);
+            if (nj == -1) return -1;
+            return restir_similar(S, P, rd, nj, *cs.m, cs.sp, cs.sn, use_prev) ? nj : -1;
+        };
+        // ReSTIRDISpatiotemporalResamplingMISWeight<MIS_GBH>: current = 0 temporal, k + 1 spatial k
+        auto gbh = [&](const RResv& r, int current) -> float {
+            if (r.UCW <= 0.0f) return 1.0f;
+            float nume = 0.0f, denom = 0.0f;
+            for (int j = 0; j < reuse + 1; j++) {
+                int nj = valid_nb(j);
+                if (nj == -1) continue;
+                RSurf js = j == reuse ? cs : gb_surface(S, P, nj, use_prev);
+                float tj = restir_target(S, F, bc, rr, r.tri, r.point, r.flags, js, bvis, OVR);
+                int M = 1;
+                if (cw) M = j == reuse ? ic.M : rr_load(tin, nj).M;
+                denom += tj * (float)M;
+                if (j + 1 == current) nume = tj * (float)M;
+            }
+            float tt = restir_target(S, F, bc, rr, r.tri, r.point, r.flags, ts, bvis, OVR);
+            int M = cw ? tres.M : 1;
+            denom += tt * (float)M;
+            if (current == 0) nume = tt * (float)M;
+            return denom == 0.0f ? 0.0f : nume / denom;
+        };
+        int selected = 0;   // MIS-like: 0 temporal, k + 1 spatial k
         if (temporal_ok) {
-            RSurf ts = gb_surface(S, P, tidx, use_prev);
             float tfc = 0.0f;
-            if (tres.UCW > 0.0f) tfc = restir_target(S, F, bc, rr, tres.tri, tres.point, tres.flags, cs, mis.bvis, OVR);
+            if (tres.UCW > 0.0f) tfc = restir_target(S, F, bc, rr, tres.tri, tres.point, tres.flags, cs, bvis, OVR);
             float jac = 1.0f;
             if (tfc > 0.0f && tres.UCW > 0.0f && !(tres.flags & RF_ENVMAP)) {
                 jac = restir_jacobian(S, tres, cs.sp, ts.sp - ts.sn * 1.0e-4f);
                 if (jac == -1.0f) jac = 0.0f;
             }
-            bool update_mc = ic.M > 0 && ic.UCW > 0.0f;
-            float wgt = mis.weight(S, F, bc, rr, rd, tres, ic, tfc, ts, vcount, vM, update_mc, false, OVR);
-            if (rr_combine(o, tres, wgt, tfc, jac, rng)) o.flags |= RF_UNOCCLUDED;
+            float wgt;
+            if (mode == MPT_RESTIR_DI_BIAS_1_OVER_M || mode == MPT_RESTIR_DI_BIAS_1_OVER_Z) wgt = (float)tres.M;
+            else if (mode == MPT_RESTIR_DI_BIAS_MIS_LIKE) wgt = cw ? (float)tres.M : 1.0f;
+            else if (mode == MPT_RESTIR_DI_BIAS_MIS_GBH) wgt = gbh(tres, 0);
+            else {
+                bool update_mc = ic.M > 0 && ic.UCW > 0.0f;
+                wgt = mis.weight(S, F, bc, rr, rd, tres, ic, tfc, ts, vcount, vM, update_mc, false, OVR);
+            }
+            if (rr_combine(o, tres, wgt, tfc, jac, rng)) {
+                selected = 0;
+                if (bvis) o.flags |= RF_UNOCCLUDED;
+                else o.flags &= ~RF_UNOCCLUDED;
+            }
         }
         int start = vM == 0 ? reuse : 0;
         for (int k = start; k < reuse + 1; k++) {
@@ -637,21 +683,65 @@ RESTIR_KERNEL void k_restir_spatiotemporal(DevScene S, DevPaths P, const MptFram
                 jac = restir_jacobian(S, nr, cs.sp, ns.sp);
                 if (jac == -1.0f) { o.M += nr.M; continue; }
             }
-            bool update_mc = ic.M > 0 && ic.UCW > 0.0f;
             float wgt;
-            if (nr.UCW == 0.0f && !update_mc) wgt = 1.0f;
+            if (mode == MPT_RESTIR_DI_BIAS_1_OVER_M || mode == MPT_RESTIR_DI_BIAS_1_OVER_Z) wgt = (float)nr.M;
+            else if (mode == MPT_RESTIR_DI_BIAS_MIS_LIKE) wgt = cw ? (float)nr.M : 1.0f;
+            else if (mode == MPT_RESTIR_DI_BIAS_MIS_GBH) wgt = gbh(nr, k + 1);
             else {
-                RSurf ns = gb_surface(S, P, ni, use_prev);
-                wgt = mis.weight(S, F, bc, rr, rd, nr, ic, tfc, ns, vcount, vM, update_mc, k == reuse, OVR);
+                bool update_mc = ic.M > 0 && ic.UCW > 0.0f;
+                if (nr.UCW == 0.0f && !update_mc) wgt = 1.0f;
+                else {
+                    RSurf ns = gb_surface(S, P, ni, use_prev);
+                    wgt = mis.weight(S, F, bc, rr, rd, nr, ic, tfc, ns, vcount, vM, update_mc, k == reuse, OVR);
+                }
             }
             if (rr_combine(o, nr, wgt, tfc, jac, rng)) {
+                selected = k + 1;
                 if (vis) o.flags |= RF_UNOCCLUDED;
                 else if (k == reuse) o.flags |= nr.flags & RF_UNOCCLUDED;
                 else o.flags &= ~RF_UNOCCLUDED;
             }
         }
-        rr_end_normalized(o);
-        if (rd.do_temporal_reuse_pass || rd.number_of_passes - 1 != rd.spatial_pass_index)
+        // normalisation (SpatiotemporalNormalizationWeight.h)
+        float nn = 1.0f, nd = 1.0f;
+        if (o.wsum > 0.0f && (mode == MPT_RESTIR_DI_BIAS_1_OVER_M || mode == MPT_RESTIR_DI_BIAS_1_OVER_Z ||
+                              mode == MPT_RESTIR_DI_BIAS_MIS_LIKE)) {
+            nn = mode == MPT_RESTIR_DI_BIAS_MIS_LIKE ? 0.0f : 1.0f;
+            nd = 0.0f;
+            for (int j = 0; j < reuse + 1; j++) {
+                int nj = valid_nb(j);
+                if (nj == -1) continue;
+                if (mode == MPT_RESTIR_DI_BIAS_1_OVER_M) {
+                    nd += (float)(j == reuse ? ic.M : rr_load(tin, nj).M);
+                    continue;
+                }
+                // the MIS-like loop reads the current frame's G-buffer (SpatiotemporalNormalizationWeight.h:130)
+                RSurf js = j == reuse ? cs : gb_surface(S, P, nj, mode == MPT_RESTIR_DI_BIAS_MIS_LIKE ? false : use_prev);
+                float tj = restir_target(S, F, bc, rr, o.tri, o.point, o.flags, js, bvis, OVR);
+                if (tj > 0.0f) {
+                    if (mode == MPT_RESTIR_DI_BIAS_1_OVER_Z) nd += (float)(j == reuse ? ic.M : rr_load(tin, nj).M);
+                    else {
+                        int M = 1;
+                        if (cw) M = j == reuse ? ic.M : rr_load(tin, nj).M;
+                        if (j + 1 == selected) nn += tj;
+                        nd += tj * (float)M;
+                    }
+                }
+            }
+            if (mode == MPT_RESTIR_DI_BIAS_1_OVER_M) nd += (float)tres.M;
+            else {
+                float tt = restir_target(S, F, bc, rr, o.tri, o.point, o.flags, ts, bvis, OVR);
+                if (mode == MPT_RESTIR_DI_BIAS_1_OVER_Z) { if (tt > 0.0f) nd += (float)tres.M; }
+                else {
+                    if (selected == 0) nn += tt;
+                    nd += tt * (float)(cw ? tres.M : 1);
+                }
+            }
+        }
+        rr_end_norm(o, nn, nd);
+        const bool vreuse = bvis && (mode == MPT_RESTIR_DI_BIAS_1_OVER_Z || mode == MPT_RESTIR_DI_BIAS_PAIRWISE_MIS ||
+                                     mode == MPT_RESTIR_DI_BIAS_PAIRWISE_MIS_DEFENSIVE);
+        if (vreuse && (rd.do_temporal_reuse_pass || rd.number_of_passes - 1 != rd.spatial_pass_index))
             restir_visibility_reuse(F, rr, o, cs.sp, cs.last);
         if (rd.m_cap > 0) o.M = imin(o.M, rd.m_cap);
         rr_store(P.rs_out, center, o);

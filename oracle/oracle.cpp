@@ -1199,10 +1199,7 @@ int oracle_render(OracleScene* sc, const MptFrame* frames, int nframes, float* s
     if ((has_adaptive_buffers(f0.render_settings) && !(as_count && as_sqlum && as_conv && status)) ||
         f0.render_settings.wants_render_low_resolution ||
         (restir && (f0.band_count != 1 || f0.render_settings.number_of_light_samples != 1 ||
-                    f0.render_settings.restir_di_settings.number_of_passes > 4 ||
-                    (f0.render_settings.restir_di_settings.do_fused_spatiotemporal &&
-                     (f0.options.restir_di_bias_correction_weights != MPT_RESTIR_DI_BIAS_PAIRWISE_MIS_DEFENSIVE ||
-                      !f0.options.restir_di_bias_correction_use_visibility)))) ||
+                    f0.render_settings.restir_di_settings.number_of_passes > 4)) ||
         (f0.options.envmap_sampling == MPT_ESS_BINARY_SEARCH && s.env_rgba && !s.env_cdf))
         return -4;
     std::vector<int> rows;

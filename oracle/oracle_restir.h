@@ -510,10 +510,48 @@ void restir_spatiotemporal(Ctx& c, RestirPassCtx& R, int x, int y, std::vector<O
     if (tidx != -1 && tres.M > 0) { vcount++; vM += tres.M; }
     OResv o;
     OResv ic = R.B.init[(size_t)center];
+    const int mode = f.options.restir_di_bias_correction_weights;
+    const bool bvis = f.options.restir_di_bias_correction_use_visibility != 0;
+    const bool cw = rd.use_confidence_weights;
     PairwiseMIS mis;
+    mis.defensive = mode == MPT_RESTIR_DI_BIAS_PAIRWISE_MIS_DEFENSIVE;
+    mis.bvis = bvis;
+    // load_temporal_neighbor_data: the temporal surface is loaded when its reservoir is not
+    // empty, else it stays a default ReSTIRDISurface (zero normals: target function 0)
+    RSurface ts;
+    if (tgb) ts = surface_of(*tgb);
+    else { ts = cs; ts.mat = &g.mat; ts.sn = ts.gn = ts.view = ts.sp = f3{0.0f, 0.0f, 0.0f}; }
+    auto nb_gb = [&](int nj, bool prev) -> const GB& { return prev ? R.prev[(size_t)nj] : R.cur[(size_t)nj]; };
+    auto valid_nb = [&](int j) -> int {
+        if (j == reuse) return center;
+        int nj = restir_spatial_neighbor(f, j, reuse, rd.reuse_radius, tpx, tpy, cr, sr, R.conv, f.restir_di_seeds[2]);
+        if (nj == -1) return -1;
+        return restir_similar(rd, R.cur[(size_t)nj], R.prev[(size_t)nj], g, cs.sp, cs.sn, use_prev) ? nj : -1;
+    };
+    // ReSTIRDISpatiotemporalResamplingMISWeight<MIS_GBH> (SpatiotemporalMISWeight.h:36-100)
+    auto gbh = [&](const OResv& r, int current) -> float {
+        if (r.UCW <= 0.0f) return 1.0f;
+        float nume = 0.0f, denom = 0.0f;
+        for (int j = 0; j < reuse + 1; j++) {
+            int nj = valid_nb(j);
+            if (nj == -1) continue;
+            RSurface js = j == reuse ? cs : surface_of(nb_gb(nj, use_prev));
+            float tj = restir_target(c, rr, r.tri, r.point, r.flags, js, bvis);
+            int M = 1;
+            if (cw) M = j == reuse ? ic.M : tin[(size_t)nj].M;
+            denom += tj * (float)M;
+            if (j + 1 == current) nume = tj * (float)M;
+        }
+        float tt = restir_target(c, rr, r.tri, r.point, r.flags, ts, bvis);
+        int M = cw ? tres.M : 1;
+        denom += tt * (float)M;
+        if (current == 0) nume = tt * (float)M;
+        return denom == 0.0f ? 0.0f : nume / denom;
+    };
+    int selected = 0;
     if (tidx != -1 && tres.M > 0) {
         float tfc = 0.0f;
-        if (tres.UCW > 0.0f) tfc = restir_target(c, rr, tres.tri, tres.point, tres.flags, cs, true);
+        if (tres.UCW > 0.0f) tfc = restir_target(c, rr, tres.tri, tres.point, tres.flags, cs, bvis);
         float jac = 1.0f;
         if (tfc > 0.0f && tres.UCW > 0.0f && !(tres.flags & RF_ENVMAP)) {
             const GB& tg = use_prev ? R.prev[(size_t)tidx] : R.cur[(size_t)tidx];
@@ -521,9 +559,19 @@ void restir_spatiotemporal(Ctx& c, RestirPassCtx& R, int x, int y, std::vector<O
             jac = restir_jacobian(s, tres, cs.sp, tsp - tg.sn * 1.0e-4f);
             if (jac == -1.0f) jac = 0.0f;
         }
-        bool update_mc = ic.M > 0 && ic.UCW > 0.0f;
-        float w = mis.weight(c, rr, rd, tres, ic, tfc, *tgb, vcount, vM, update_mc, false);
-        if (o.combine_with(tres, w, tfc, jac, rng)) o.flags |= RF_UNOCCLUDED;
+        float w;
+        if (mode == MPT_RESTIR_DI_BIAS_1_OVER_M || mode == MPT_RESTIR_DI_BIAS_1_OVER_Z) w = (float)tres.M;
+        else if (mode == MPT_RESTIR_DI_BIAS_MIS_LIKE) w = cw ? (float)tres.M : 1.0f;
+        else if (mode == MPT_RESTIR_DI_BIAS_MIS_GBH) w = gbh(tres, 0);
+        else {
+            bool update_mc = ic.M > 0 && ic.UCW > 0.0f;
+            w = mis.weight(c, rr, rd, tres, ic, tfc, *tgb, vcount, vM, update_mc, false);
+        }
+        if (o.combine_with(tres, w, tfc, jac, rng)) {
+            selected = 0;
+            if (bvis) o.flags |= RF_UNOCCLUDED;
+            else o.flags &= ~RF_UNOCCLUDED;
+        }
     }
     int start = vM == 0 ? reuse : 0;
     for (int k = start; k < reuse + 1; k++) {
@@ -544,21 +592,65 @@ void restir_spatiotemporal(Ctx& c, RestirPassCtx& R, int x, int y, std::vector<O
             jac = restir_jacobian(s, nr, cs.sp, ng.first_hit + ng.sn * 1.0e-4f);
             if (jac == -1.0f) { o.M += nr.M; continue; }
         }
-        bool update_mc = ic.M > 0 && ic.UCW > 0.0f;
         float w;
-        if (nr.UCW == 0.0f && !update_mc) w = 1.0f;
+        if (mode == MPT_RESTIR_DI_BIAS_1_OVER_M || mode == MPT_RESTIR_DI_BIAS_1_OVER_Z) w = (float)nr.M;
+        else if (mode == MPT_RESTIR_DI_BIAS_MIS_LIKE) w = cw ? (float)nr.M : 1.0f;
+        else if (mode == MPT_RESTIR_DI_BIAS_MIS_GBH) w = gbh(nr, k + 1);
         else {
-            const GB& ng = use_prev ? R.prev[(size_t)ni] : R.cur[(size_t)ni];
-            w = mis.weight(c, rr, rd, nr, ic, tfc, ng, vcount, vM, update_mc, k == reuse);
+            bool update_mc = ic.M > 0 && ic.UCW > 0.0f;
+            if (nr.UCW == 0.0f && !update_mc) w = 1.0f;
+            else {
+                const GB& ng = use_prev ? R.prev[(size_t)ni] : R.cur[(size_t)ni];
+                w = mis.weight(c, rr, rd, nr, ic, tfc, ng, vcount, vM, update_mc, k == reuse);
+            }
         }
         if (o.combine_with(nr, w, tfc, jac, rng)) {
+            selected = k + 1;
             if (vis) o.flags |= RF_UNOCCLUDED;
             else if (k == reuse) o.flags |= nr.flags & RF_UNOCCLUDED;
             else o.flags &= ~RF_UNOCCLUDED;
         }
     }
-    o.end_with_normalization(1.0f, 1.0f);
-    if (rd.do_temporal_reuse_pass || rd.number_of_passes - 1 != rd.spatial_pass_index)
+    // ReSTIRDISpatiotemporalNormalizationWeight (SpatiotemporalNormalizationWeight.h)
+    float nn = 1.0f, nd = 1.0f;
+    if (o.wsum > 0.0f && (mode == MPT_RESTIR_DI_BIAS_1_OVER_M || mode == MPT_RESTIR_DI_BIAS_1_OVER_Z ||
+                          mode == MPT_RESTIR_DI_BIAS_MIS_LIKE)) {
+        nn = mode == MPT_RESTIR_DI_BIAS_MIS_LIKE ? 0.0f : 1.0f;
+        nd = 0.0f;
+        for (int j = 0; j < reuse + 1; j++) {
+            int nj = valid_nb(j);
+            if (nj == -1) continue;
+            if (mode == MPT_RESTIR_DI_BIAS_1_OVER_M) {
+                nd += (float)(j == reuse ? ic.M : tin[(size_t)nj].M);
+                continue;
+            }
+            // the MIS-like loop reads the current frame's G-buffer (SpatiotemporalNormalizationWeight.h:130)
+            RSurface js = j == reuse ? cs : surface_of(nb_gb(nj, mode == MPT_RESTIR_DI_BIAS_MIS_LIKE ? false : use_prev));
+            float tj = restir_target(c, rr, o.tri, o.point, o.flags, js, bvis);
+            if (tj > 0.0f) {
+                if (mode == MPT_RESTIR_DI_BIAS_1_OVER_Z) nd += (float)(j == reuse ? ic.M : tin[(size_t)nj].M);
+                else {
+                    int M = 1;
+                    if (cw) M = j == reuse ? ic.M : tin[(size_t)nj].M;
+                    if (j + 1 == selected) nn += tj;
+                    nd += tj * (float)M;
+                }
+            }
+        }
+        if (mode == MPT_RESTIR_DI_BIAS_1_OVER_M) nd += (float)tres.M;
+        else {
+            float tt = restir_target(c, rr, o.tri, o.point, o.flags, ts, bvis);
+            if (mode == MPT_RESTIR_DI_BIAS_1_OVER_Z) { if (tt > 0.0f) nd += (float)tres.M; }
+            else {
+                if (selected == 0) nn += tt;
+                nd += tt * (float)(cw ? tres.M : 1);
+            }
+        }
+    }
+    o.end_with_normalization(nn, nd);
+    const bool vreuse = bvis && (mode == MPT_RESTIR_DI_BIAS_1_OVER_Z || mode == MPT_RESTIR_DI_BIAS_PAIRWISE_MIS ||
+                                 mode == MPT_RESTIR_DI_BIAS_PAIRWISE_MIS_DEFENSIVE);
+    if (vreuse && (rd.do_temporal_reuse_pass || rd.number_of_passes - 1 != rd.spatial_pass_index))
         restir_visibility_reuse(c, rr, o, cs.sp, cs.last_hit);
     if (rd.m_cap > 0) o.M = std::min(o.M, rd.m_cap);
     out[(size_t)center] = o;

@@ -93,8 +93,9 @@ BIAS_MODES = {"1_over_m": abi.RESTIR_DI_BIAS_1_OVER_M, "1_over_z": abi.RESTIR_DI
               "pairwise": abi.RESTIR_DI_BIAS_PAIRWISE_MIS}
 
 
+@pytest.mark.parametrize("fused", [False, True], ids=["unfused", "fused"])
 @pytest.mark.parametrize("mode", list(BIAS_MODES))
-def test_oracle_restir_bias_correction_modes(cornell, luts, oracle_lib, mode):
+def test_oracle_restir_bias_correction_modes(cornell, luts, oracle_lib, mode, fused):
     """Every bias-correction mode of the unfused chain (TemporalMISWeight.h,
     SpatialMISWeight.h, *NormalizationWeight.h) on light-only candidates: the unbiased
     ones (1/Z, MIS-like, generalized balance heuristic, pairwise) match NEE/MIS; 1/M is
@@ -102,7 +103,7 @@ def test_oracle_restir_bias_correction_modes(cornell, luts, oracle_lib, mode):
     o = oracle_lib.Oracle(cornell, luts)
     ref = o.render(frames(cornell, abi.LSS_MIS_LIGHT_BSDF, 384, bounces=0)).mean() / 384
     a = o.render(frames(cornell, abi.LSS_RESTIR_DI, 96, bounces=0, number_of_initial_bsdf_candidates=0,
-                        do_fused_spatiotemporal=False, bias=BIAS_MODES[mode])).mean() / 96
+                        do_fused_spatiotemporal=fused, bias=BIAS_MODES[mode])).mean() / 96
     tol = 0.15 if mode == "1_over_m" else 0.025
     assert abs(a / ref - 1.0) < tol, (mode, a, ref)
     o.close()
@@ -140,6 +141,13 @@ CASES = {
                                         use_confidence_weights=False),
     "bias_defensive_no_visibility": dict(do_fused_spatiotemporal=False, bias_vis=0),
     "bias_1_over_z_no_visibility": dict(do_fused_spatiotemporal=False, bias=abi.RESTIR_DI_BIAS_1_OVER_Z, bias_vis=0),
+    "fused_1_over_m": dict(bias=abi.RESTIR_DI_BIAS_1_OVER_M),
+    "fused_1_over_z": dict(bias=abi.RESTIR_DI_BIAS_1_OVER_Z, passes=3),
+    "fused_mis_like": dict(bias=abi.RESTIR_DI_BIAS_MIS_LIKE),
+    "fused_mis_like_moving": dict(bias=abi.RESTIR_DI_BIAS_MIS_LIKE, move_at=2, use_confidence_weights=False),
+    "fused_gbh": dict(bias=abi.RESTIR_DI_BIAS_MIS_GBH),
+    "fused_pairwise": dict(bias=abi.RESTIR_DI_BIAS_PAIRWISE_MIS),
+    "fused_defensive_no_visibility": dict(bias_vis=0),
 }
 
 
