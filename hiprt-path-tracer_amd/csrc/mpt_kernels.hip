@@ -1624,8 +1624,10 @@ static void launch_ovr(int ovr, dim3 g, hipStream_t st, Args... args) {
     else hipLaunchKernelGGL(K<MPT_BSDF_NONE>::fn, g, dim3(TB), 0, st, args...);
 }
 template <int OVR> struct KInitial { static constexpr auto fn = k_restir_initial<OVR>; };
-template <int OVR> struct KSpatiotemporal { static constexpr auto fn = k_restir_spatiotemporal<OVR>; };
-template <int OVR> struct KSpatial { static constexpr auto fn = k_restir_spatial<OVR>; };
+template <int OVR> struct KSpatiotemporal { static constexpr auto fn = k_restir_spatiotemporal<OVR, MPT_RESTIR_DI_BIAS_PAIRWISE_MIS_DEFENSIVE>; };
+template <int OVR> struct KSpatial { static constexpr auto fn = k_restir_spatial<OVR, MPT_RESTIR_DI_BIAS_PAIRWISE_MIS_DEFENSIVE>; };
+template <int OVR> struct KSpatiotemporalAny { static constexpr auto fn = k_restir_spatiotemporal<OVR, -1>; };
+template <int OVR> struct KSpatialAny { static constexpr auto fn = k_restir_spatial<OVR, -1>; };
 template <int OVR> struct KTemporal { static constexpr auto fn = k_restir_temporal<OVR>; };
 
 // restir_output_reservoirs of a frame, as a code kept by the context between frames
@@ -1693,16 +1695,21 @@ static void launch_restir(const DevScene& S, DevPaths& P, const MptFrame* d_fram
     const dim3 g(cfg.grid_persistent);
     launch_ovr<KInitial>(ovr, g, st, S, P, d_frame);
     float4* last_out = restir_buffer(P, cfg.restir_out_sp2);
+    // the reference-default weights run a kernel variant with the mode compiled in
+    const bool def_bias = hf.options.restir_di_bias_correction_weights == MPT_RESTIR_DI_BIAS_PAIRWISE_MIS_DEFENSIVE &&
+                          hf.options.restir_di_bias_correction_use_visibility != 0;
     if (rd.do_fused_spatiotemporal) {
         P.rs_tin = last_out;
         P.rs_out = last_out == P.rs_sp1 ? P.rs_sp2 : P.rs_sp1;
         halo_exchange(hf, cfg, st, MPT_HALO_RESERVOIRS, 0, cfg.halo_rows, {{P.rs_tin, RB}});
-        launch_ovr<KSpatiotemporal>(ovr, g, st, S, P, d_frame);
+        if (def_bias) launch_ovr<KSpatiotemporal>(ovr, g, st, S, P, d_frame);
+        else launch_ovr<KSpatiotemporalAny>(ovr, g, st, S, P, d_frame);
         for (int pass = 1; pass < rd.number_of_passes; pass++) {
             float4* in = P.rs_out;
             float4* out = in == P.rs_sp1 ? P.rs_sp2 : P.rs_sp1;
             halo_exchange(hf, cfg, st, MPT_HALO_RESERVOIRS, pass, cfg.halo_rows, {{in, RB}});
-            launch_ovr<KSpatial>(ovr, g, st, S, P, d_frame, pass, (const float4*)in, out);
+            if (def_bias) launch_ovr<KSpatial>(ovr, g, st, S, P, d_frame, pass, (const float4*)in, out);
+            else launch_ovr<KSpatialAny>(ovr, g, st, S, P, d_frame, pass, (const float4*)in, out);
             P.rs_out = out;
         }
     } else {
@@ -1723,7 +1730,8 @@ static void launch_restir(const DevScene& S, DevPaths& P, const MptFrame* d_fram
                 float4* in = pass == 0 ? cur : ((pass & 1) ? P.rs_sp1 : P.rs_sp2);
                 float4* out = pass == 0 ? P.rs_sp1 : ((pass & 1) ? P.rs_sp2 : P.rs_sp1);
                 halo_exchange(hf, cfg, st, MPT_HALO_RESERVOIRS, pass + 1, cfg.halo_rows, {{in, RB}});
-                launch_ovr<KSpatial>(ovr, g, st, S, P, d_frame, pass, (const float4*)in, out);
+                if (def_bias) launch_ovr<KSpatial>(ovr, g, st, S, P, d_frame, pass, (const float4*)in, out);
+                else launch_ovr<KSpatialAny>(ovr, g, st, S, P, d_frame, pass, (const float4*)in, out);
                 cur = out;
             }
         }

@@ -560,7 +560,9 @@ DEV int restir_temporal_neighbor(const DevScene& S, const DevPaths& P, const Mpt
 }
 
 // ---- ReSTIR_DI_SpatiotemporalReuse (FusedSpatiotemporalReuse.h:112-586) ----------------
-template <int OVR>
+// BM: the bias-correction mode compiled in (MPT_RESTIR_DI_BIAS_PAIRWISE_MIS_DEFENSIVE with
+// visibility, the reference default) or -1 = read it from the frame (every mode)
+template <int OVR, int BM>
 RESTIR_KERNEL void k_restir_spatiotemporal(DevScene S, DevPaths P, const MptFrame* __restrict__ Fp) {
     __shared__ uint2 lds[LDS_STACK * TB];
     const MptFrame& F = *Fp;
@@ -604,8 +606,8 @@ RESTIR_KERNEL void k_restir_spatiotemporal(DevScene S, DevPaths P, const MptFram
         if (temporal_ok) { vcount++; vM += tres.M; }
         RResv o = rr_default();
         const RResv ic = rr_load(P.rs_init, center);
-        const int mode = F.options.restir_di_bias_correction_weights;
-        const bool bvis = F.options.restir_di_bias_correction_use_visibility != 0;
+        const int mode = BM >= 0 ? BM : F.options.restir_di_bias_correction_weights;
+        const bool bvis = BM >= 0 ? true : F.options.restir_di_bias_correction_use_visibility != 0;
         const bool cw = rd.use_confidence_weights;
         PairwiseMIS mis{0.0f, mode == MPT_RESTIR_DI_BIAS_PAIRWISE_MIS_DEFENSIVE, bvis};
         // the temporal neighbour's surface as load_temporal_neighbor_data leaves it: loaded when
@@ -872,7 +874,7 @@ RESTIR_KERNEL void k_restir_temporal(DevScene S, DevPaths P, const MptFrame* __r
 }
 
 // ---- ReSTIR_DI_SpatialReuse (SpatialReuse.h:52-348) ------------------------------------
-template <int OVR>
+template <int OVR, int BM>
 RESTIR_KERNEL void k_restir_spatial(DevScene S, DevPaths P, const MptFrame* __restrict__ Fp, int pass,
                                     const float4* __restrict__ in, float4* out) {
     __shared__ uint2 lds[LDS_STACK * TB];
@@ -882,8 +884,8 @@ RESTIR_KERNEL void k_restir_spatial(DevScene S, DevPaths P, const MptFrame* __re
              F.render_settings.do_alpha_testing, 0u, 7, 0, 0u, 0u};
     const int W = F.res_x;
     const uint32_t pass_rs = F.restir_di_seeds[4 + pass];
-    const int mode = F.options.restir_di_bias_correction_weights;
-    const bool bvis = F.options.restir_di_bias_correction_use_visibility != 0;
+    const int mode = BM >= 0 ? BM : F.options.restir_di_bias_correction_weights;
+    const bool bvis = BM >= 0 ? true : F.options.restir_di_bias_correction_use_visibility != 0;
     for (int s = blockIdx.x * TB + threadIdx.x; s < P.n; s += gridDim.x * TB) {
         const int center = s + P.pix_off;
         MptReSTIRDISettings rd = F.render_settings.restir_di_settings;
