@@ -343,8 +343,7 @@ def main():
         # the same frames (sample 0 overwrites the sums)
         k, bi, ref = parity_band(sd, luts, cam, W, H, opt, a.bounces, K, env=env, world=wset, alpha=alpha)
         r.enable_stats(timing=False, instrumented=False)
-        for f in frames[:k]:
-            r.render(f)
+        r.render_samples(frames[:k], max_batch=batch)   # the same batched path as the timed region
         r.synchronize_kernel()
         gpu = r.framebuffer(abi.FB_COLOR)[bi * BAND_H:(bi + 1) * BAND_H]
         d = (gpu.astype(np.float64) - ref.astype(np.float64)) / k
