@@ -390,6 +390,11 @@ int validate_frame(const MptFrame* f) {
         if (f->band_count != 1 && (int64_t)f->band_height * f->band_count < f->res_y)
             return fail(MPT_ERR_UNSUPPORTED, "ReSTIR DI across a partition needs one contiguous band per context "
                                              "(band_height * band_count >= res_y)");
+        const int lb = f->options.restir_di_later_bounces_sampling_strategy;
+        if (lb < MPT_RESTIR_DI_LATER_BOUNCES_UNIFORM_ONE_LIGHT || lb > MPT_RESTIR_DI_LATER_BOUNCES_RIS_BSDF_AND_LIGHT)
+            return fail(MPT_ERR_INVALID_ARGUMENT, "ReSTIR DI: bad later-bounces sampling strategy");
+        if (!f->options.restir_di_do_lights_presampling)
+            return fail(MPT_ERR_UNSUPPORTED, "ReSTIR DI: initial candidates without lights presampling not implemented");
         const int bw = f->options.restir_di_bias_correction_weights;
         if (bw < MPT_RESTIR_DI_BIAS_1_OVER_M || bw > MPT_RESTIR_DI_BIAS_PAIRWISE_MIS_DEFENSIVE)
             return fail(MPT_ERR_INVALID_ARGUMENT, "ReSTIR DI: bad bias correction weights");
@@ -732,6 +737,11 @@ static int render_batch(MptContext* c, const MptFrame* f, int batch) {
         r = ensure_restir(c, f);
         if (r != MPT_OK) return r;
     }
+    if (f->options.direct_light_sampling == MPT_LSS_RESTIR_DI && c->emissive.n == 0 &&
+        (f->options.restir_di_later_bounces_sampling_strategy == MPT_RESTIR_DI_LATER_BOUNCES_UNIFORM_ONE_LIGHT ||
+         f->options.restir_di_later_bounces_sampling_strategy == MPT_RESTIR_DI_LATER_BOUNCES_MIS_LIGHT_BSDF))
+        return fail(MPT_ERR_UNSUPPORTED, "ReSTIR DI later bounces: uniform / MIS light sampling without emissive "
+                                         "triangles picks from an empty list in the reference (Lights.h:22-220)");
     r = ensure_batch(c, batch);
     if (r != MPT_OK) return r;
     const size_t n_paths = (size_t)std::max(c->n_slots, 1) * (size_t)c->batch_cap;

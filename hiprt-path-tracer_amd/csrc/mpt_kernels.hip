@@ -580,6 +580,18 @@ DEV uint32_t pixel_seed(const MptFrame& F, uint32_t pix) { return pixel_seed(F, 
 DEV uint32_t camera_seed(const MptFrame& F, uint32_t pix) {
     return pixel_seed(F, pix, F.camera_random_seed ? F.camera_random_seed : F.random_seed);
 }
+// The strategy sample_one_light runs at a bounce: ReSTIR DI's later bounces use
+// ReSTIR_DI_LaterBouncesSamplingStrategy (Lights.h:243-275)
+DEV int bounce_lss(const MptFrame& F, int bounce) {
+    const int lss = F.options.direct_light_sampling;
+    if (lss != MPT_LSS_RESTIR_DI || bounce == 0) return lss;
+    switch (F.options.restir_di_later_bounces_sampling_strategy) {
+    case MPT_RESTIR_DI_LATER_BOUNCES_UNIFORM_ONE_LIGHT: return MPT_LSS_UNIFORM_ONE_LIGHT;
+    case MPT_RESTIR_DI_LATER_BOUNCES_BSDF: return MPT_LSS_BSDF;
+    case MPT_RESTIR_DI_LATER_BOUNCES_MIS_LIGHT_BSDF: return MPT_LSS_MIS_LIGHT_BSDF;
+    default: return MPT_LSS_RIS_BSDF_AND_LIGHT;
+    }
+}
 // Sample batch (mpt_render_frames; GPURenderer::render's samples_per_frame loop,
 // GPURenderer.cpp:424-449, run as one wavefront): path slot s is pixel slot s % n_pix of
 // the batch's sample s / n_pix, whose seeds and sample number are those of Fp[s / n_pix].
@@ -988,7 +1000,9 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MPT_SHADE_WA
                 if (m.emissive_texture_used && bounce > 0) { fl |= NF_IMM; store3(nr.imm, emission_of(m)); }
             }
             do_light = do_light && lss != MPT_LSS_NO_DIRECT_LIGHT_SAMPLING;
-            if (restir && bounce > 0 && S.n_emissive == 0) do_light = false;
+            const int lssb = bounce_lss(F, bounce);
+            // sample_lights_RIS returns 0 without emissive triangles (RIS.h:292-302)
+            if (restir && bounce > 0 && S.n_emissive == 0 && lssb == MPT_LSS_RIS_BSDF_AND_LIGHT) do_light = false;
             if (do_light) fl |= NF_L;
             const bool do_env = ws.ambient_light_type == MPT_AMBIENT_ENVMAP && !F.bsdf_flags.white_furnace_mode &&
                                 !is_emissive(m) && ws.envmap_intensity > 0.0f && F.options.envmap_sampling != MPT_ESS_NO_SAMPLING &&
@@ -1001,10 +1015,10 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MPT_SHADE_WA
             int op = OP_DONE;
             if (do_light) {
                 if (restir && bounce == 0) op = OP_RESTIR;
-                else if (lss == MPT_LSS_RIS_BSDF_AND_LIGHT || restir) op = nl > 0 ? OP_RIS_LIGHT : (nbc > 0 ? OP_RIS_BSDF : OP_RIS_WIN);
-                else if (lss == MPT_LSS_MIS_LIGHT_BSDF) op = OP_MIS_LIGHT;
-                else if (lss == MPT_LSS_UNIFORM_ONE_LIGHT) op = OP_UNI_LIGHT;
-                else if (lss == MPT_LSS_BSDF) op = OP_BSDF_LIGHT;
+                else if (lssb == MPT_LSS_RIS_BSDF_AND_LIGHT) op = nl > 0 ? OP_RIS_LIGHT : (nbc > 0 ? OP_RIS_BSDF : OP_RIS_WIN);
+                else if (lssb == MPT_LSS_MIS_LIGHT_BSDF) op = OP_MIS_LIGHT;
+                else if (lssb == MPT_LSS_UNIFORM_ONE_LIGHT) op = OP_UNI_LIGHT;
+                else if (lssb == MPT_LSS_BSDF) op = OP_BSDF_LIGHT;
             }
             if (op == OP_DONE) op = do_env ? OP_ENV_LIGHT : (do_cont ? OP_CONT : OP_DONE);
             // RIS reservoir (sample_bsdf_and_lights_RIS_reservoir, RIS.h:82-289)
@@ -1448,13 +1462,14 @@ __global__ __launch_bounds__(TB) void k_resolve(DevScene S, DevPaths P, const Mp
     uint32_t fl = nr.flags;
     if (!(fl & NF_SHADED) || (fl & NF_NOADD)) return;
     const int lss = F.options.direct_light_sampling;
+    const int lssb = bounce_lss(F, bounce);
     Col ld = col(0.0f), ed = col(0.0f);
     const uint8_t* occ = P.occ + (size_t)slot * 4;
     if (fl & NF_IMM) ld = load3c(nr.imm);
     else if (!(fl & NF_L)) ld = col(0.0f);
     else if (lss == MPT_LSS_RESTIR_DI && bounce == 0) {
         if ((fl & NF_A) && !((fl & NF_AQ) && occ[0])) ld = load3c(nr.a);
-    } else if (lss == MPT_LSS_RIS_BSDF_AND_LIGHT || lss == MPT_LSS_RESTIR_DI) {
+    } else if (lssb == MPT_LSS_RIS_BSDF_AND_LIGHT) {
         float wsum = nr.ris_wsum;
         float cwb = 0.0f, targetb = 0.0f;
         int trib = -1;
@@ -1489,7 +1504,7 @@ __global__ __launch_bounds__(TB) void k_resolve(DevScene S, DevPaths P, const Mp
                 if (c > 0.0f) ld = load3c(nr.a) * ucw * emission_of(S.mats[S.mat_idx[nr.ris_tri]]) * c;
             }
         }
-    } else if (lss == MPT_LSS_MIS_LIGHT_BSDF) {
+    } else if (lssb == MPT_LSS_MIS_LIGHT_BSDF) {
         Col lrad = col(0.0f), brad = col(0.0f);
         if ((fl & NF_A) && !occ[0]) lrad = load3c(nr.a);
         if (fl & NF_B) {
@@ -1502,9 +1517,9 @@ __global__ __launch_bounds__(TB) void k_resolve(DevScene S, DevPaths P, const Mp
             }
         }
         ld = lrad + brad;
-    } else if (lss == MPT_LSS_UNIFORM_ONE_LIGHT) {
+    } else if (lssb == MPT_LSS_UNIFORM_ONE_LIGHT) {
         if ((fl & NF_A) && !occ[0]) ld = load3c(nr.a);
-    } else if (lss == MPT_LSS_BSDF) {
+    } else if (lssb == MPT_LSS_BSDF) {
         if (fl & NF_B) {
             ShadowLightHit sh;
             if (shadow_light_hit(S, P.nhit[slot], sh) && !is_black(sh.em))

@@ -267,10 +267,11 @@ struct PairwiseMIS {
     }
 };
 
-DEV bool spatial_visibility(const MptReSTIRDISettings& rd, int k, int reuse_count) {   // SpatialReuse.h:36-50
+DEV bool spatial_visibility(const MptFrame& F, const MptReSTIRDISettings& rd, int k, int reuse_count) {   // SpatialReuse.h:36-50
     bool v = rd.do_visibility_only_last_pass && rd.spatial_pass_index == rd.number_of_passes - 1;
     v |= !rd.do_visibility_only_last_pass;
     v &= k < rd.neighbor_visibility_count;
+    v &= F.options.restir_di_spatial_target_visibility != 0;
     v &= k != reuse_count;
     return v;
 }
@@ -477,6 +478,11 @@ RESTIR_KERNEL void k_restir_initial(DevScene S, DevPaths P, const MptFrame* __re
                     target = tf;
                 }
             }
+            // ReSTIR_DI_InitialTargetFunctionVisibility (InitialCandidates.h:248-264)
+            if (F.options.restir_di_initial_target_visibility && target > 0.0f) {
+                if (rr.any(ep, tl, dist, g.last)) { r.M++; continue; }
+                flags |= RF_UNOCCLUDED;
+            }
             rr_add(r, tri, point, target, flags, weight, rng);
         }
         for (int i = 0; i < nb; i++) {
@@ -519,7 +525,7 @@ RESTIR_KERNEL void k_restir_initial(DevScene S, DevPaths P, const MptFrame* __re
         }
         r.UCW = r.wsum == 0.0f ? 0.0f : 1.0f / r.target * r.wsum;   // end()
         r.M = 1;
-        restir_visibility_reuse(F, rr, r, g.p + g.sn * 1.0e-4f, g.last);
+        if (F.options.restir_di_do_visibility_reuse) restir_visibility_reuse(F, rr, r, g.p + g.sn * 1.0e-4f, g.last);
         rr_store(P.rs_init, pix, r);
     }
     count_pass_rays(P, rr.n_any, rr.n_closest);
@@ -674,7 +680,7 @@ RESTIR_KERNEL void k_restir_spatiotemporal(DevScene S, DevPaths P, const MptFram
             if (k < reuse && reuse > 32 && !restir_similar(S, P, rd, ni, *cs.m, cs.sp, cs.sn, use_prev)) continue;
             RResv nr = k == reuse ? ic : rr_load(tin, ni);
             float tfc = 0.0f;
-            bool vis = spatial_visibility(rd, k, reuse);
+            bool vis = spatial_visibility(F, rd, k, reuse);
             if (nr.UCW > 0.0f) {
                 if (k == reuse) tfc = nr.target;
                 else tfc = restir_target(S, F, bc, rr, nr.tri, nr.point, nr.flags, cs, vis, OVR);
@@ -742,7 +748,9 @@ RESTIR_KERNEL void k_restir_spatiotemporal(DevScene S, DevPaths P, const MptFram
         }
         rr_end_norm(o, nn, nd);
         const bool vreuse = bvis && (mode == MPT_RESTIR_DI_BIAS_1_OVER_Z || mode == MPT_RESTIR_DI_BIAS_PAIRWISE_MIS ||
-                                     mode == MPT_RESTIR_DI_BIAS_PAIRWISE_MIS_DEFENSIVE);
+                                     mode == MPT_RESTIR_DI_BIAS_PAIRWISE_MIS_DEFENSIVE) &&
+                            (F.options.restir_di_do_visibility_reuse ||
+                             (F.options.restir_di_initial_target_visibility && F.options.restir_di_spatial_target_visibility));
         if (vreuse && (rd.do_temporal_reuse_pass || rd.number_of_passes - 1 != rd.spatial_pass_index))
             restir_visibility_reuse(F, rr, o, cs.sp, cs.last);
         if (rd.m_cap > 0) o.M = imin(o.M, rd.m_cap);
@@ -931,7 +939,7 @@ RESTIR_KERNEL void k_restir_spatial(DevScene S, DevPaths P, const MptFrame* __re
             if (k < reuse && reuse > 32 && !restir_similar(S, P, rd, ni, *cs.m, cs.sp, cs.sn, false)) continue;
             RResv nr = rr_load(in, ni);
             float tfc = 0.0f;
-            bool vis = spatial_visibility(rd, k, reuse);
+            bool vis = spatial_visibility(F, rd, k, reuse);
             if (nr.UCW > 0.0f) {
                 if (k == reuse) tfc = nr.target;
                 else tfc = restir_target(S, F, bc, rr, nr.tri, nr.point, nr.flags, cs, vis, OVR);
@@ -998,7 +1006,9 @@ RESTIR_KERNEL void k_restir_spatial(DevScene S, DevPaths P, const MptFrame* __re
         }
         rr_end_norm(o, nn, nd);
         const bool vreuse = bvis && (mode == MPT_RESTIR_DI_BIAS_1_OVER_Z || mode == MPT_RESTIR_DI_BIAS_PAIRWISE_MIS ||
-                                     mode == MPT_RESTIR_DI_BIAS_PAIRWISE_MIS_DEFENSIVE);
+                                     mode == MPT_RESTIR_DI_BIAS_PAIRWISE_MIS_DEFENSIVE) &&
+                            (F.options.restir_di_do_visibility_reuse ||
+                             (F.options.restir_di_initial_target_visibility && F.options.restir_di_spatial_target_visibility));
         if (vreuse && (rd.do_temporal_reuse_pass || rd.number_of_passes - 1 != rd.spatial_pass_index))
             restir_visibility_reuse(F, rr, o, cs.sp, cs.last);
         if (rd.m_cap > 0) o.M = imin(o.M, rd.m_cap);

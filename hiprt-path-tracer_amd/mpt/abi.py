@@ -300,17 +300,22 @@ class Camera(C.Structure):
 
 RESTIR_DI_BIAS_1_OVER_M, RESTIR_DI_BIAS_1_OVER_Z, RESTIR_DI_BIAS_MIS_LIKE = 0, 1, 2
 RESTIR_DI_BIAS_MIS_GBH, RESTIR_DI_BIAS_PAIRWISE_MIS, RESTIR_DI_BIAS_PAIRWISE_MIS_DEFENSIVE = 3, 4, 5
+RESTIR_DI_LATER_BOUNCES_UNIFORM_ONE_LIGHT, RESTIR_DI_LATER_BOUNCES_BSDF = 0, 1
+RESTIR_DI_LATER_BOUNCES_MIS_LIGHT_BSDF, RESTIR_DI_LATER_BOUNCES_RIS_BSDF_AND_LIGHT = 2, 3
 
 
 class KernelOptions(C.Structure):
     _fields_ = [("bsdf_override", i32), ("direct_light_sampling", i32), ("envmap_sampling", i32),
                 ("envmap_bsdf_mis", i32), ("ris_use_visibility", i32), ("restir_di_bias_correction_weights", i32),
-                ("restir_di_bias_correction_use_visibility", i32)]
+                ("restir_di_bias_correction_use_visibility", i32), ("restir_di_later_bounces_sampling_strategy", i32),
+                ("restir_di_initial_target_visibility", i32), ("restir_di_spatial_target_visibility", i32),
+                ("restir_di_do_visibility_reuse", i32), ("restir_di_do_lights_presampling", i32)]
 
     @classmethod
     def default(cls):
-        # KernelOptions.h:116, 218, 231, 242, 252, 335, 304
-        return cls(BSDF_NONE, LSS_RIS_BSDF_AND_LIGHT, ESS_ALIAS_TABLE, 1, 0, RESTIR_DI_BIAS_PAIRWISE_MIS_DEFENSIVE, 1)
+        # KernelOptions.h:116, 218, 231, 242, 252, 335, 304, 355, 270, 279, 289, 366
+        return cls(BSDF_NONE, LSS_RIS_BSDF_AND_LIGHT, ESS_ALIAS_TABLE, 1, 0, RESTIR_DI_BIAS_PAIRWISE_MIS_DEFENSIVE, 1,
+                   RESTIR_DI_LATER_BOUNCES_RIS_BSDF_AND_LIGHT, 0, 1, 1, 1)
 
 
 class BSDFFlags(C.Structure):

@@ -293,7 +293,18 @@ typedef struct MptKernelOptions {
     int32_t restir_di_bias_correction_weights;        /* ReSTIR_DI_BiasCorrectionWeights (KernelOptions.h:335),
                                                          MPT_RESTIR_DI_BIAS_* */
     int32_t restir_di_bias_correction_use_visibility; /* ReSTIR_DI_BiasCorrectionUseVisibility (KernelOptions.h:304) */
+    int32_t restir_di_later_bounces_sampling_strategy; /* ReSTIR_DI_LaterBouncesSamplingStrategy (KernelOptions.h:355),
+                                                          MPT_RESTIR_DI_LATER_BOUNCES_* */
+    int32_t restir_di_initial_target_visibility; /* ReSTIR_DI_InitialTargetFunctionVisibility (KernelOptions.h:270), 0 */
+    int32_t restir_di_spatial_target_visibility; /* ReSTIR_DI_SpatialTargetFunctionVisibility (KernelOptions.h:279), 1 */
+    int32_t restir_di_do_visibility_reuse;       /* ReSTIR_DI_DoVisibilityReuse (KernelOptions.h:289), 1 */
+    int32_t restir_di_do_lights_presampling;     /* ReSTIR_DI_DoLightsPresampling (KernelOptions.h:366), 1 (only 1) */
 } MptKernelOptions;
+
+#define MPT_RESTIR_DI_LATER_BOUNCES_UNIFORM_ONE_LIGHT 0 /* KernelOptions.h:73-76 */
+#define MPT_RESTIR_DI_LATER_BOUNCES_BSDF 1
+#define MPT_RESTIR_DI_LATER_BOUNCES_MIS_LIGHT_BSDF 2
+#define MPT_RESTIR_DI_LATER_BOUNCES_RIS_BSDF_AND_LIGHT 3
 
 #define MPT_RESTIR_DI_BIAS_1_OVER_M 0 /* KernelOptions.h:66-71 */
 #define MPT_RESTIR_DI_BIAS_1_OVER_Z 1

@@ -776,8 +776,15 @@ Col sample_one_light(Ctx& c, const Payload& pl, const HitInfo& hi, f3 view, Rng&
     if (restir) {
         // sample_one_light_ReSTIR_DI (Lights.h:243-275): the reservoir at bounce 0, RIS after
         if (bounce == 0) return restir_final_shading(c, *c.restir_out, pl, hi, view);
-        if (s.n_emissive == 0) return Col(0.0f);   // sample_lights_RIS (RIS.h:292-302)
-        for (int i = 0; i < n; i++) dl += sample_lights_ris(c, pl, hi, view, rng);
+        // later bounces: ReSTIR_DI_LaterBouncesSamplingStrategy (Lights.h:250-263)
+        const int later = c.f->options.restir_di_later_bounces_sampling_strategy;
+        for (int i = 0; i < n; i++) {
+            if (later == MPT_RESTIR_DI_LATER_BOUNCES_UNIFORM_ONE_LIGHT) dl += sample_one_light_no_mis(c, pl, hi, view, rng);
+            else if (later == MPT_RESTIR_DI_LATER_BOUNCES_BSDF) dl += sample_one_light_bsdf(c, pl, hi, view, rng);
+            else if (later == MPT_RESTIR_DI_LATER_BOUNCES_MIS_LIGHT_BSDF) dl += sample_one_light_mis(c, pl, hi, view, rng);
+            else if (s.n_emissive == 0) return Col(0.0f);   // sample_lights_RIS (RIS.h:292-302)
+            else dl += sample_lights_ris(c, pl, hi, view, rng);
+        }
         return dl / (float)n;
     }
     for (int i = 0; i < n; i++) {

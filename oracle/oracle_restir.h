@@ -301,6 +301,11 @@ void restir_initial(Ctx& c, RestirPassCtx& R, int x, int y) {
                 target = tf;
             }
         }
+        // ReSTIR_DI_InitialTargetFunctionVisibility (InitialCandidates.h:248-264)
+        if (f.options.restir_di_initial_target_visibility && target > 0.0f) {
+            if (rr.any(ep, tl, dist, g.prim)) { r.M++; continue; }
+            flags |= RF_UNOCCLUDED;
+        }
         r.add_one_candidate(tri, point, target, flags, weight, rng);
     }
     // sample_bsdf_candidates (InitialCandidates.h:273-394)
@@ -358,7 +363,7 @@ void restir_initial(Ctx& c, RestirPassCtx& R, int x, int y) {
     }
     r.end();
     r.M = 1;
-    restir_visibility_reuse(c, rr, r, g.first_hit + g.sn * 1.0e-4f, g.prim);
+    if (f.options.restir_di_do_visibility_reuse) restir_visibility_reuse(c, rr, r, g.first_hit + g.sn * 1.0e-4f, g.prim);
     R.B.init[(size_t)pix] = r;
 }
 
@@ -420,10 +425,11 @@ struct PairwiseMIS {
 };
 
 // do_include_spatial_visibility_term_or_not (FusedSpatiotemporalReuse.h:41-56, SpatialReuse.h:36-50)
-inline bool spatial_visibility(const MptReSTIRDISettings& rd, int k, int reuse_count) {
+inline bool spatial_visibility(const MptFrame& f, const MptReSTIRDISettings& rd, int k, int reuse_count) {
     bool v = rd.do_visibility_only_last_pass && rd.spatial_pass_index == rd.number_of_passes - 1;
     v |= !rd.do_visibility_only_last_pass;
     v &= k < rd.neighbor_visibility_count;
+    v &= f.options.restir_di_spatial_target_visibility != 0;
     v &= k != reuse_count;
     return v;
 }
@@ -581,7 +587,7 @@ void restir_spatiotemporal(Ctx& c, RestirPassCtx& R, int x, int y, std::vector<O
         if (k < reuse && reuse > 32 && !restir_similar(rd, R.cur[(size_t)ni], R.prev[(size_t)ni], g, cs.sp, cs.sn, use_prev)) continue;
         OResv nr = k == reuse ? ic : tin[(size_t)ni];
         float tfc = 0.0f;
-        bool vis = spatial_visibility(rd, k, reuse);
+        bool vis = spatial_visibility(f, rd, k, reuse);
         if (nr.UCW > 0.0f) {
             if (k == reuse) tfc = nr.target;
             else tfc = restir_target(c, rr, nr.tri, nr.point, nr.flags, cs, vis);
@@ -649,7 +655,9 @@ void restir_spatiotemporal(Ctx& c, RestirPassCtx& R, int x, int y, std::vector<O
     }
     o.end_with_normalization(nn, nd);
     const bool vreuse = bvis && (mode == MPT_RESTIR_DI_BIAS_1_OVER_Z || mode == MPT_RESTIR_DI_BIAS_PAIRWISE_MIS ||
-                                 mode == MPT_RESTIR_DI_BIAS_PAIRWISE_MIS_DEFENSIVE);
+                                 mode == MPT_RESTIR_DI_BIAS_PAIRWISE_MIS_DEFENSIVE) &&
+                        (f.options.restir_di_do_visibility_reuse ||
+                         (f.options.restir_di_initial_target_visibility && f.options.restir_di_spatial_target_visibility));
     if (vreuse && (rd.do_temporal_reuse_pass || rd.number_of_passes - 1 != rd.spatial_pass_index))
         restir_visibility_reuse(c, rr, o, cs.sp, cs.last_hit);
     if (rd.m_cap > 0) o.M = std::min(o.M, rd.m_cap);
@@ -825,7 +833,7 @@ void restir_spatial(Ctx& c, RestirPassCtx& R, int x, int y, int pass, std::vecto
         if (k < reuse && reuse > 32 && !restir_similar(rd, R.cur[(size_t)ni], R.prev[(size_t)ni], g, cs.sp, cs.sn, false)) continue;
         OResv nr = in[(size_t)ni];
         float tfc = 0.0f;
-        bool vis = spatial_visibility(rd, k, reuse);
+        bool vis = spatial_visibility(f, rd, k, reuse);
         if (nr.UCW > 0.0f) {
             if (k == reuse) tfc = nr.target;
             else tfc = restir_target(c, rr, nr.tri, nr.point, nr.flags, cs, vis);
@@ -891,7 +899,9 @@ void restir_spatial(Ctx& c, RestirPassCtx& R, int x, int y, int pass, std::vecto
     }
     o.end_with_normalization(nn, nd);
     const bool vreuse = bvis && (mode == MPT_RESTIR_DI_BIAS_1_OVER_Z || mode == MPT_RESTIR_DI_BIAS_PAIRWISE_MIS ||
-                                 mode == MPT_RESTIR_DI_BIAS_PAIRWISE_MIS_DEFENSIVE);
+                                 mode == MPT_RESTIR_DI_BIAS_PAIRWISE_MIS_DEFENSIVE) &&
+                        (f.options.restir_di_do_visibility_reuse ||
+                         (f.options.restir_di_initial_target_visibility && f.options.restir_di_spatial_target_visibility));
     if (vreuse && (rd.do_temporal_reuse_pass || rd.number_of_passes - 1 != rd.spatial_pass_index))
         restir_visibility_reuse(c, rr, o, cs.sp, cs.last_hit);
     if (rd.m_cap > 0) o.M = std::min(o.M, rd.m_cap);

@@ -17,7 +17,7 @@ W, H = 32, 24
 
 
 def frames(sd, lss, n, passes=2, ovr=abi.BSDF_NONE, bounces=3, world=None, alpha=False, w=W, h=H, adaptive=False,
-           band=(1, 0, 1), move_at=None, bias=abi.RESTIR_DI_BIAS_PAIRWISE_MIS_DEFENSIVE, bias_vis=1, **rd):
+           band=(1, 0, 1), move_at=None, bias=abi.RESTIR_DI_BIAS_PAIRWISE_MIS_DEFENSIVE, bias_vis=1, kopt=None, **rd):
     """move_at: from that frame on the camera is moved (prev_camera = the old one for one frame)."""
     cam = scene.make_camera(sd.camera_info, w, h)
     cam2 = None
@@ -30,6 +30,8 @@ def frames(sd, lss, n, passes=2, ovr=abi.BSDF_NONE, bounces=3, world=None, alpha
     opt.bsdf_override = ovr
     opt.restir_di_bias_correction_weights = bias
     opt.restir_di_bias_correction_use_visibility = bias_vis
+    for k, v in (kopt or {}).items():
+        setattr(opt, k, v)
     out = []
     for d in scene.gpu_seed_schedule(n, passes if lss == abi.LSS_RESTIR_DI else None,
                                      fused=rd.get("do_fused_spatiotemporal", True),
@@ -109,6 +111,20 @@ def test_oracle_restir_bias_correction_modes(cornell, luts, oracle_lib, mode, fu
     o.close()
 
 
+@pytest.mark.parametrize("kopt", [dict(restir_di_initial_target_visibility=1), dict(restir_di_do_visibility_reuse=0),
+                                  dict(restir_di_spatial_target_visibility=0)],
+                         ids=["initial_visibility", "no_visibility_reuse", "no_spatial_visibility"])
+def test_oracle_restir_visibility_options_unbiased(cornell, luts, oracle_lib, kopt):
+    """ReSTIR DI's visibility kernel options (KernelOptions.h:270-304) keep the light-only
+    estimator unbiased against NEE/MIS."""
+    o = oracle_lib.Oracle(cornell, luts)
+    ref = o.render(frames(cornell, abi.LSS_MIS_LIGHT_BSDF, 384, bounces=0)).mean() / 384
+    a = o.render(frames(cornell, abi.LSS_RESTIR_DI, 96, bounces=0, number_of_initial_bsdf_candidates=0,
+                        kopt=kopt)).mean() / 96
+    assert abs(a / ref - 1.0) < 0.025, (kopt, a, ref)
+    o.close()
+
+
 def test_oracle_restir_rejects_unsupported(cornell, luts, oracle_lib):
     o = oracle_lib.Oracle(cornell, luts)
     fr = frames(cornell, abi.LSS_RESTIR_DI, 1, band=(8, 0, 3))   # one contiguous band per context only
@@ -148,6 +164,14 @@ CASES = {
     "fused_gbh": dict(bias=abi.RESTIR_DI_BIAS_MIS_GBH),
     "fused_pairwise": dict(bias=abi.RESTIR_DI_BIAS_PAIRWISE_MIS),
     "fused_defensive_no_visibility": dict(bias_vis=0),
+    "later_bounces_uniform": dict(kopt=dict(restir_di_later_bounces_sampling_strategy=abi.RESTIR_DI_LATER_BOUNCES_UNIFORM_ONE_LIGHT)),
+    "later_bounces_bsdf": dict(kopt=dict(restir_di_later_bounces_sampling_strategy=abi.RESTIR_DI_LATER_BOUNCES_BSDF)),
+    "later_bounces_mis": dict(kopt=dict(restir_di_later_bounces_sampling_strategy=abi.RESTIR_DI_LATER_BOUNCES_MIS_LIGHT_BSDF)),
+    "initial_target_visibility": dict(kopt=dict(restir_di_initial_target_visibility=1)),
+    "no_spatial_target_visibility": dict(kopt=dict(restir_di_spatial_target_visibility=0)),
+    "no_visibility_reuse": dict(kopt=dict(restir_di_do_visibility_reuse=0)),
+    "no_visibility_reuse_target_vis": dict(do_fused_spatiotemporal=False,
+                                           kopt=dict(restir_di_do_visibility_reuse=0, restir_di_initial_target_visibility=1)),
 }
 
 
