@@ -42,7 +42,7 @@ METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
 HBM_PEAK_GBS = 8000.0
 S_NODE, S_TRI = 80, 48
 BAND_H = 8
-BATCH_1GPU = 8     # samples per wavefront on a whole-frame context (measured: DESIGN.md §5)
+TARGET_PATHS = 8 * 1920 * 1080   # paths per wavefront launch (mpt_render_frames batch x rank pixels)
 MAX_BATCH = 64     # MPT_MAX_BATCH
 
 
@@ -64,7 +64,7 @@ def parse():
     ap.add_argument("--no-parity", action="store_true", help="skip the RMSE-vs-oracle band check")
     ap.add_argument("--batch", type=int, default=0,
                     help="samples per pixel traced as one wavefront (mpt_render_frames); 0 = auto: "
-                         "BATCH_1GPU x the ranks' share of the frame, so a rank's launches stay frame-sized")
+                         "TARGET_PATHS / the rank's pixels, so a rank's launches keep the same size")
     ap.add_argument("--emulate-rank-of", type=int, default=1,
                     help="scaling rehearsal on one GPU: render only rank 0's share of an N-way row split "
                          "(the line then reports that rank's rate; not a bench line)")
@@ -229,8 +229,10 @@ def main():
         band = (BAND_H, 0, a.emulate_rank_of)
         a.no_parity = a.no_cpu_baseline = True
     band_h = band[0]
-    share = band[2] if a.workload != "c4" else world   # ranks the frame is split over
-    batch = min(MAX_BATCH, a.batch or (BATCH_1GPU * share))
+    # samples per wavefront: launches of ~TARGET_PATHS paths whatever the rank's share of the
+    # frame (measured: 8 x 1080p is past the knee of the throughput curve)
+    rows_rank = mpt.partition_rows(H, band[0], band[1], band[2])
+    batch = min(MAX_BATCH, a.batch or max(1, int(round(TARGET_PATHS / max(1, rows_rank * W)))))
     while K % batch:                                     # whole batches in the timed region
         batch -= 1
 
