@@ -58,6 +58,9 @@ struct RRays {
         THit h;
         uint32_t nn = 0, nt = 0;
         // evaluate_shadow_ray: maxT = t_max - 1e-4 (Intersect.h:227)
+#ifdef MPT_RESTIR_NO_TRACE   // timing experiment only: how much of a pass is traversal
+        return false;
+#endif
         return traverse<true, false>(*S, o, d, last, tmax - 1.0e-4f, h, lds, spill, nn, nt, alpha, key);
     }
     DEV bool closest(v3 o, v3 d, int last, THit& h) {

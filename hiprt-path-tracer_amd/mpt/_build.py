@@ -71,6 +71,29 @@ def build(force: bool = False, verbose: bool = True, defines=(), out: Path | Non
     return lib_path
 
 
+HOST_DIR = ROOT / "host"
+HOST_TEST = HOST_DIR / "gpurenderer_parity"
+HOST_SOURCES = [HOST_DIR / "gpu_renderer.cpp", ROOT.parent / "tests" / "cpp" / "gpurenderer_parity.cpp"]
+
+
+def build_host_test(verbose: bool = True) -> Path:
+    """The C++ GPURenderer mirror (host/) linked with libmpt into the test driver of
+    tests/test_host_cpp.py (plain g++: the host side is ordinary C++ over the C ABI)."""
+    lib = build(verbose=verbose)
+    deps = HOST_SOURCES + sorted(HOST_DIR.glob("*.h")) + [lib]
+    if HOST_TEST.exists() and all(p.stat().st_mtime <= HOST_TEST.stat().st_mtime for p in deps):
+        return HOST_TEST
+    cmd = ["g++", "-O2", "-std=c++17", f"-I{INCLUDE}", f"-I{HOST_DIR}", *map(str, HOST_SOURCES),
+           f"-L{PKG_DIR}", "-lmpt", "-Wl,-rpath,$ORIGIN/../mpt", "-Wl,-rpath,/opt/rocm/lib",
+           "-Wl,-rpath-link,/opt/rocm/lib", "-o", str(HOST_TEST)]
+    if verbose:
+        print("[mpt build]", " ".join(cmd), file=sys.stderr)
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+    if r.returncode != 0:
+        raise RuntimeError("host test build failed:\n" + r.stdout.decode(errors="replace"))
+    return HOST_TEST
+
+
 if __name__ == "__main__":
     args = sys.argv[1:]
     defs = [a for a in args if a.startswith("-D")]

@@ -1,0 +1,93 @@
+// Test driver (tests/test_host_cpp.py): the C++ GPURenderer mirror (hiprt-path-tracer_amd/host)
+// rendering a scene handed over as a raw blob by the test, through libmpt.
+// usage: gpurenderer_parity <in.blob> <out.bin>
+//   out.bin = int32 n_frames, MptFrame[n_frames] (every frame render() built), float sums[W*H*3]
+#include <cstdio>
+#include <cstring>
+#include <stdexcept>
+#include <vector>
+
+#include "gpu_renderer.h"
+
+namespace {
+struct Reader {
+    FILE* f;
+    template <typename T> T get() { T v; if (fread(&v, sizeof(T), 1, f) != 1) throw std::runtime_error("short blob"); return v; }
+    template <typename T> std::vector<T> arr(size_t n) {
+        std::vector<T> v(n);
+        if (n && fread(v.data(), sizeof(T), n, f) != n) throw std::runtime_error("short blob");
+        return v;
+    }
+};
+}  // namespace
+
+int main(int argc, char** argv) {
+    if (argc != 3) { fprintf(stderr, "usage: %s in.blob out.bin\n", argv[0]); return 2; }
+    try {
+        FILE* fin = fopen(argv[1], "rb");
+        if (!fin) throw std::runtime_error("cannot open blob");
+        Reader r{fin};
+        if (r.get<uint32_t>() != 0x4254504du) throw std::runtime_error("bad magic");
+        const auto settings = r.get<MptRenderSettings>();
+        const auto world = r.get<MptWorldSettings>();
+        const auto options = r.get<MptKernelOptions>();
+        const auto flags = r.get<MptBSDFFlags>();
+        const auto camera = r.get<MptCamera>();
+        const int W = r.get<int32_t>(), H = r.get<int32_t>(), n_updates = r.get<int32_t>();
+        const int T = r.get<int32_t>(), V = r.get<int32_t>(), M = r.get<int32_t>(), E = r.get<int32_t>();
+        auto idx = r.arr<int32_t>(3 * (size_t)T);
+        auto pos = r.arr<float>(3 * (size_t)V);
+        auto nrm = r.arr<float>(3 * (size_t)V);
+        auto has_n = r.arr<uint8_t>((size_t)V);
+        auto uv = r.arr<float>(2 * (size_t)V);
+        auto mat_idx = r.arr<int32_t>((size_t)T);
+        auto mats = r.arr<MptMaterial>((size_t)M);
+        auto emissive = r.arr<int32_t>((size_t)(E > 0 ? E : 1));
+        const size_t lut_n[6] = {128 * 128, 128 * 64 * 128, 256 * 16 * 128, 256 * 16 * 128, 32 * 32 * 96, 32 * 32 * 3};
+        std::vector<float> lut[6];
+        for (int k = 0; k < 6; k++) lut[k] = r.arr<float>(lut_n[k]);
+        fclose(fin);
+
+        mpt_host::GPURenderer gr(0);
+        MptScene s{};
+        s.triangle_indices = idx.data(); s.num_triangles = T;
+        s.vertices = pos.data(); s.vertex_normals = nrm.data(); s.has_vertex_normals = has_n.data();
+        s.texcoords = uv.data(); s.num_vertices = V;
+        s.material_indices = mat_idx.data(); s.materials = mats.data(); s.num_materials = M;
+        s.emissive_triangle_indices = emissive.data(); s.num_emissive_triangles = E;
+        gr.set_scene(s);
+        MptLuts L{};
+        L.ggx_conductor_ess = lut[0].data(); L.glossy_dielectric_ess = lut[1].data(); L.ggx_glass_ess = lut[2].data();
+        L.ggx_glass_inverse_ess = lut[3].data(); L.ggx_thin_glass_ess = lut[4].data(); L.sheen_ltc_params = lut[5].data();
+        gr.setup_brdfs_data(L);
+        gr.resize(W, H);
+        gr.get_render_settings() = settings;
+        gr.get_world_settings() = world;
+        gr.get_kernel_options() = options;
+        gr.get_bsdf_flags() = flags;
+        gr.set_camera(camera);
+        gr.reset();
+        std::vector<MptFrame> frames;
+        for (int u = 0; u < n_updates; u++) {   // RenderWindow::render: update() then render() per displayed frame
+            gr.update();
+            gr.render();
+            frames.insert(frames.end(), gr.last_frames().begin(), gr.last_frames().end());
+        }
+        gr.synchronize_kernel();
+        std::vector<float> img((size_t)W * H * 3);
+        gr.get_framebuffer(MPT_FB_COLOR, img.data());
+        MptStatus st = gr.get_status_buffer_values();
+        FILE* fo = fopen(argv[2], "wb");
+        if (!fo) throw std::runtime_error("cannot open output");
+        int32_t nf = (int32_t)frames.size();
+        fwrite(&nf, sizeof(nf), 1, fo);
+        fwrite(frames.data(), sizeof(MptFrame), frames.size(), fo);
+        fwrite(img.data(), sizeof(float), img.size(), fo);
+        fclose(fo);
+        printf("ok %d frames, one_ray_active %d\n", nf, (int)st.one_ray_active);
+    } catch (const std::exception& e) {
+        fprintf(stderr, "error: %s\n", e.what());
+        return 1;
+    }
+    return 0;
+}
