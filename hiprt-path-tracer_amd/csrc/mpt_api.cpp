@@ -393,8 +393,6 @@ int validate_frame(const MptFrame* f) {
         const int lb = f->options.restir_di_later_bounces_sampling_strategy;
         if (lb < MPT_RESTIR_DI_LATER_BOUNCES_UNIFORM_ONE_LIGHT || lb > MPT_RESTIR_DI_LATER_BOUNCES_RIS_BSDF_AND_LIGHT)
             return fail(MPT_ERR_INVALID_ARGUMENT, "ReSTIR DI: bad later-bounces sampling strategy");
-        if (!f->options.restir_di_do_lights_presampling)
-            return fail(MPT_ERR_UNSUPPORTED, "ReSTIR DI: initial candidates without lights presampling not implemented");
         const int bw = f->options.restir_di_bias_correction_weights;
         if (bw < MPT_RESTIR_DI_BIAS_1_OVER_M || bw > MPT_RESTIR_DI_BIAS_PAIRWISE_MIS_DEFENSIVE)
             return fail(MPT_ERR_INVALID_ARGUMENT, "ReSTIR DI: bad bias correction weights");

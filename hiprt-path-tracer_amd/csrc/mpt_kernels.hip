@@ -1706,7 +1706,8 @@ static void launch_restir(const DevScene& S, DevPaths& P, const MptFrame* d_fram
                           {{P.pgb_pos, 16}, {P.pgb_sn, 16}, {P.pgb_gn, 16}, {P.pgb_view, 16}, {P.pgb_meta, 16},
                            {P.pgb_vsA, 16}, {P.pgb_vsB, 16}, {P.pgb_mat, MS}});
     }
-    hipLaunchKernelGGL(k_restir_presample, dim3((n_pl + TB - 1) / TB), dim3(TB), 0, st, S, P, d_frame);
+    if (hf.options.restir_di_do_lights_presampling)   // ReSTIRDIRenderPass::launch (.cpp:241-242)
+        hipLaunchKernelGGL(k_restir_presample, dim3((n_pl + TB - 1) / TB), dim3(TB), 0, st, S, P, d_frame);
     const dim3 g(cfg.grid_persistent);
     launch_ovr<KInitial>(ovr, g, st, S, P, d_frame);
     float4* last_out = restir_buffer(P, cfg.restir_out_sp2);

@@ -446,27 +446,63 @@ RESTIR_KERNEL void k_restir_initial(DevScene S, DevPaths P, const MptFrame* __re
         PEval pe;
         bsdf_eval_pre<OVR>(bc, *g.m, g.vs, g.view, g.sn, pe);
         for (int i = 0; i < nl; i++) {
-            // use_presampled_light_candidate (InitialCandidates.h:30-90)
-            int tcs = (x / rd.tile_size + y / rd.tile_size + 1) * (x / rd.tile_size + y / rd.tile_size) / 2 + y / rd.tile_size;
-            Rng subset_rng = make_rng(F.restir_di_seeds[1] * (uint32_t)(tcs + 1));
-            int subset = subset_rng.random_index(rd.number_of_subsets);
-            int li = rng.random_index(rd.subset_size);
-            const float4* pl = P.rs_plights + 4 * (size_t)(subset * rd.subset_size + li);
-            float4 p0 = pl[0], p1 = pl[1], p2 = pl[2];
-            int tri = __float_as_int(p0.x);
-            v3 point = mk3(p0.y, p0.z, p0.w);
-            uint32_t flags = __float_as_uint(p2.w);
-            Col rad = col(p2.x, p2.y, p2.z);
-            float pdf = p1.w, dist = 0.0f, target = 0.0f;
-            v3 tl;
-            if (flags & RF_ENVMAP) { tl = mat_x_vec(w.envmap_to_world_matrix.m, point); dist = 1.0e35f; }
-            else { tl = point - ep; dist = length(tl); tl = tl / dist; }
-            float cosv = dot(g.sn, tl);
-            if (!(flags & RF_ENVMAP)) {
-                float cl = absr(dot(mk3(p1.x, p1.y, p1.z), -tl));
-                pdf *= dist * dist;
-                pdf /= cl;
-                if (!min_contrib(F.render_settings.minimum_light_contribution, rad * cosv / pdf)) { r.M++; continue; }
+            int tri;
+            v3 point, tl;
+            uint32_t flags;
+            Col rad;
+            float pdf, dist = 0.0f, target = 0.0f, cosv;
+            if (F.options.restir_di_do_lights_presampling) {
+                // use_presampled_light_candidate (InitialCandidates.h:30-90)
+                int tcs = (x / rd.tile_size + y / rd.tile_size + 1) * (x / rd.tile_size + y / rd.tile_size) / 2 + y / rd.tile_size;
+                Rng subset_rng = make_rng(F.restir_di_seeds[1] * (uint32_t)(tcs + 1));
+                int subset = subset_rng.random_index(rd.number_of_subsets);
+                int li = rng.random_index(rd.subset_size);
+                const float4* pl = P.rs_plights + 4 * (size_t)(subset * rd.subset_size + li);
+                float4 p0 = pl[0], p1 = pl[1], p2 = pl[2];
+                tri = __float_as_int(p0.x);
+                point = mk3(p0.y, p0.z, p0.w);
+                flags = __float_as_uint(p2.w);
+                rad = col(p2.x, p2.y, p2.z);
+                pdf = p1.w;
+                if (flags & RF_ENVMAP) { tl = mat_x_vec(w.envmap_to_world_matrix.m, point); dist = 1.0e35f; }
+                else { tl = point - ep; dist = length(tl); tl = tl / dist; }
+                cosv = dot(g.sn, tl);
+                if (!(flags & RF_ENVMAP)) {
+                    float cl = absr(dot(mk3(p1.x, p1.y, p1.z), -tl));
+                    pdf *= dist * dist;
+                    pdf /= cl;
+                    if (!min_contrib(F.render_settings.minimum_light_contribution, rad * cosv / pdf)) { r.M++; continue; }
+                }
+            } else {
+                // sample_fresh_light_candidate (InitialCandidates.h:93-170)
+                tri = -1; point = mk3(0.0f, 0.0f, 0.0f); flags = 0u; rad = col(0.0f); pdf = 0.0f; cosv = 0.0f;
+                if (rng() > env_p) {
+                    LightInfo lsi;
+                    point = sample_emissive_triangle(S, rng, pdf, lsi);
+                    tri = lsi.tri;
+                    if (pdf > 0.0f) {
+                        v3 d2 = point - ep;
+                        float dl = length(d2);
+                        d2 = d2 / dl;
+                        cosv = maxr(0.0f, dot(g.sn, d2));
+                        float cl = absr(dot(lsi.normal, -d2));
+                        pdf *= dl * dl;
+                        pdf /= cl;
+                        if (!min_contrib(F.render_settings.minimum_light_contribution, lsi.emission * cosv / pdf)) { r.M++; continue; }
+                        pdf *= (1.0f - env_p);
+                        rad = lsi.emission;
+                    }
+                } else {
+                    v3 edir;
+                    rad = env_sample(S, F, edir, pdf, rng);
+                    cosv = maxr(0.0f, dot(edir, g.sn));
+                    if (!min_contrib(F.render_settings.minimum_light_contribution, rad * cosv / pdf)) { r.M++; continue; }
+                    pdf *= env_p;
+                    point = mat_x_vec(w.world_to_envmap_matrix.m, edir);
+                    flags = RF_ENVMAP;
+                }
+                if (flags & RF_ENVMAP) { tl = mat_x_vec(w.envmap_to_world_matrix.m, point); dist = 1.0e35f; }
+                else { tl = point - ep; dist = length(tl); tl = tl / dist; }
             }
             float weight = 0.0f;
             if (cosv > 0.0f && pdf > 0.0f) {

@@ -73,7 +73,8 @@ void GPURenderer::render() {
         if (m_options.direct_light_sampling == MPT_LSS_RESTIR_DI) {
             // ReSTIRDIRenderPass::launch (ReSTIRDIRenderPass.cpp:233-264, 298-431)
             MptReSTIRDISettings& rd = m_settings.restir_di_settings;
-            f.restir_di_seeds[0] = m_rng.xorshift32();   // lights presampling
+            if (m_options.restir_di_do_lights_presampling)
+                f.restir_di_seeds[0] = m_rng.xorshift32();   // lights presampling (launched only when enabled)
             f.restir_di_seeds[1] = m_rng.xorshift32();   // initial candidates
             if (rd.do_fused_spatiotemporal) {
                 m_rng.xorshift32();                      // temporal seed, overwritten before the launch

@@ -415,7 +415,7 @@ def _xorshift32(x):
 
 
 def gpu_seed_schedule(nframes, restir_spatial_passes=None, first_sample=0, fused=True, temporal=True, spatial=True,
-                      samples_per_frame=1):
+                      samples_per_frame=1, presampling=True):
     """Per-sample seeds as the reference's GPU front-end draws them from m_rng (seeded 42,
     GPURenderer.cpp:50): GPURenderer::update once per displayed frame (update_render_data,
     GPURenderer.cpp:980-983; its value is overwritten before any launch), then per sample
@@ -440,7 +440,8 @@ def gpu_seed_schedule(nframes, restir_spatial_passes=None, first_sample=0, fused
         cam = draw()
         seeds = [0] * 8
         if restir_spatial_passes is not None:
-            seeds[0] = draw()
+            if presampling:                          # launch_presampling_lights_pass only when enabled
+                seeds[0] = draw()
             seeds[1] = draw()
             if fused:
                 draw()                               # temporal seed, overwritten before the launch

@@ -298,7 +298,8 @@ typedef struct MptKernelOptions {
     int32_t restir_di_initial_target_visibility; /* ReSTIR_DI_InitialTargetFunctionVisibility (KernelOptions.h:270), 0 */
     int32_t restir_di_spatial_target_visibility; /* ReSTIR_DI_SpatialTargetFunctionVisibility (KernelOptions.h:279), 1 */
     int32_t restir_di_do_visibility_reuse;       /* ReSTIR_DI_DoVisibilityReuse (KernelOptions.h:289), 1 */
-    int32_t restir_di_do_lights_presampling;     /* ReSTIR_DI_DoLightsPresampling (KernelOptions.h:366), 1 (only 1) */
+    int32_t restir_di_do_lights_presampling;     /* ReSTIR_DI_DoLightsPresampling (KernelOptions.h:366), 1; 0: no
+                                                    presampling pass and no seed drawn for it (restir_di_seeds[0] unused) */
 } MptKernelOptions;
 
 #define MPT_RESTIR_DI_LATER_BOUNCES_UNIFORM_ONE_LIGHT 0 /* KernelOptions.h:73-76 */

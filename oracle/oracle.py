@@ -20,7 +20,8 @@ LIB_PATH = os.path.join(HERE, "liboracle.so")
 
 
 def build(force=False):
-    srcs = [os.path.join(HERE, f) for f in ("oracle.cpp", "oracle_math.h", "oracle_bsdf.h", "Makefile")]
+    srcs = [os.path.join(HERE, f) for f in ("oracle.cpp", "oracle_math.h", "oracle_bsdf.h", "oracle_restir.h", "Makefile",
+                                            os.path.join("..", "include", "mpt.h"))]
     stale = os.path.exists(LIB_PATH) and any(os.path.getmtime(f) > os.path.getmtime(LIB_PATH) for f in srcs
                                              if os.path.exists(f))
     if force or stale or not os.path.exists(LIB_PATH):

@@ -267,26 +267,62 @@ void restir_initial(Ctx& c, RestirPassCtx& R, int x, int y) {
     f3 ep = g.first_hit + g.sn * 1.0e-4f * 1.0f;
     // sample_light_candidates with presampled lights (InitialCandidates.h:30-121, 171-271)
     for (int i = 0; i < nl; i++) {
-        int tc = cantor(x / rd.tile_size, y / rd.tile_size);
-        Rng subset_rng(f.restir_di_seeds[1] * (uint32_t)(tc + 1));
-        int subset = subset_rng.random_index(rd.number_of_subsets);
-        int li = rng.random_index(rd.subset_size);
-        const OPLight& pl = R.B.plights[(size_t)(subset * rd.subset_size + li)];
-        int tri = pl.tri;
-        f3 point = pl.point;
-        uint32_t flags = pl.flags;
+        int tri;
+        f3 point, tl;
+        uint32_t flags;
         float target = 0.0f;
-        Col rad = pl.radiance;
-        float pdf = pl.pdf, dist = 0.0f;
-        f3 tl;
-        if (flags & RF_ENVMAP) { tl = mat_x_vec(w.envmap_to_world_matrix, point); dist = 1.0e35f; }
-        else { tl = point - ep; tl = tl / (dist = length(tl)); }
-        float cosv = dot(g.sn, tl);
-        if (!(flags & RF_ENVMAP)) {
-            float cl = absf(dot(pl.normal, -tl));
-            pdf *= dist * dist;
-            pdf /= cl;
-            if (!min_contrib(f.render_settings.minimum_light_contribution, rad * cosv / pdf)) { r.M++; continue; }
+        Col rad;
+        float pdf, dist = 0.0f, cosv;
+        if (f.options.restir_di_do_lights_presampling) {
+            int tc = cantor(x / rd.tile_size, y / rd.tile_size);
+            Rng subset_rng(f.restir_di_seeds[1] * (uint32_t)(tc + 1));
+            int subset = subset_rng.random_index(rd.number_of_subsets);
+            int li = rng.random_index(rd.subset_size);
+            const OPLight& pl = R.B.plights[(size_t)(subset * rd.subset_size + li)];
+            tri = pl.tri;
+            point = pl.point;
+            flags = pl.flags;
+            rad = pl.radiance;
+            pdf = pl.pdf;
+            if (flags & RF_ENVMAP) { tl = mat_x_vec(w.envmap_to_world_matrix, point); dist = 1.0e35f; }
+            else { tl = point - ep; tl = tl / (dist = length(tl)); }
+            cosv = dot(g.sn, tl);
+            if (!(flags & RF_ENVMAP)) {
+                float cl = absf(dot(pl.normal, -tl));
+                pdf *= dist * dist;
+                pdf /= cl;
+                if (!min_contrib(f.render_settings.minimum_light_contribution, rad * cosv / pdf)) { r.M++; continue; }
+            }
+        } else {
+            // sample_fresh_light_candidate (InitialCandidates.h:93-170)
+            tri = -1; point = f3{0.0f, 0.0f, 0.0f}; flags = 0u; rad = Col(0.0f); pdf = 0.0f; cosv = 0.0f;
+            if (rng() > env_p) {
+                LightInfo lsi;
+                point = sample_emissive_triangle(c, rng, pdf, lsi);
+                tri = lsi.tri;
+                if (pdf > 0.0f) {
+                    f3 d2 = point - ep;
+                    float dl = length(d2);
+                    d2 = d2 / dl;
+                    cosv = std::max(0.0f, dot(g.sn, d2));
+                    float cl = absf(dot(lsi.normal, -d2));
+                    pdf *= dl * dl;
+                    pdf /= cl;
+                    if (!min_contrib(f.render_settings.minimum_light_contribution, lsi.emission * cosv / pdf)) { r.M++; continue; }
+                    pdf *= (1.0f - env_p);
+                    rad = lsi.emission;
+                }
+            } else {
+                f3 edir;
+                rad = envmap_sample(c, edir, pdf, rng);
+                cosv = std::max(0.0f, dot(edir, g.sn));
+                if (!min_contrib(f.render_settings.minimum_light_contribution, rad * cosv / pdf)) { r.M++; continue; }
+                pdf *= env_p;
+                point = mat_x_vec(w.world_to_envmap_matrix, edir);
+                flags = RF_ENVMAP;
+            }
+            if (flags & RF_ENVMAP) { tl = mat_x_vec(w.envmap_to_world_matrix, point); dist = 1.0e35f; }
+            else { tl = point - ep; tl = tl / (dist = length(tl)); }
         }
         float weight = 0.0f;
         if (cosv > 0.0f && pdf > 0.0f) {

@@ -329,3 +329,20 @@ def test_batched_samples_fall_back_for_adaptive(scenes, luts):
     seq = gpu_render(r, frs)[0]
     bat = gpu_render_batched(r, frs, 4)[0]
     assert_same(bat, seq, "adaptive frames through mpt_render_frames")
+
+
+def test_city_full_frame_batched_equals_sequential(city, luts):
+    """The bench configuration at its full size (C3 stand-in, 1920x1080, RIS + envmap +
+    alpha testing): one 4-sample wavefront equals four single-sample frames over the whole
+    frame, and the sums are finite -- the size-independent property behind the bench's
+    batched timing (the oracle checks a band of the same frames in bench.py)."""
+    env = mpt.build_envmap(scene.procedural_sky(512, 256, seed=7))
+    frs = frames(city, 1920, 1080, 4, lss=abi.LSS_RIS_BSDF_AND_LIGHT, world=scene.envmap_world(1.0))
+    for f in frs:
+        f.render_settings.do_alpha_testing = True
+    r = renderer(city, luts, env)
+    seq = gpu_render(r, frs)
+    bat = gpu_render_batched(r, frs, 4)
+    for k, what in enumerate(["color", "albedo", "normals"]):
+        assert_same(bat[k], seq[k], f"full-frame batched vs sequential {what}")
+    assert np.isfinite(bat[0]).all() and bat[0].mean() > 0

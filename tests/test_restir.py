@@ -36,7 +36,8 @@ def frames(sd, lss, n, passes=2, ovr=abi.BSDF_NONE, bounces=3, world=None, alpha
     for d in scene.gpu_seed_schedule(n, passes if lss == abi.LSS_RESTIR_DI else None,
                                      fused=rd.get("do_fused_spatiotemporal", True),
                                      temporal=rd.get("do_temporal_reuse_pass", True),
-                                     spatial=rd.get("do_spatial_reuse_pass", True)):
+                                     spatial=rd.get("do_spatial_reuse_pass", True),
+                                     presampling=(kopt or {}).get("restir_di_do_lights_presampling", 1) != 0):
         st = scene.parity_settings(bounces)
         st.do_alpha_testing = alpha
         if adaptive:
@@ -112,8 +113,8 @@ def test_oracle_restir_bias_correction_modes(cornell, luts, oracle_lib, mode, fu
 
 
 @pytest.mark.parametrize("kopt", [dict(restir_di_initial_target_visibility=1), dict(restir_di_do_visibility_reuse=0),
-                                  dict(restir_di_spatial_target_visibility=0)],
-                         ids=["initial_visibility", "no_visibility_reuse", "no_spatial_visibility"])
+                                  dict(restir_di_spatial_target_visibility=0), dict(restir_di_do_lights_presampling=0)],
+                         ids=["initial_visibility", "no_visibility_reuse", "no_spatial_visibility", "no_presampling"])
 def test_oracle_restir_visibility_options_unbiased(cornell, luts, oracle_lib, kopt):
     """ReSTIR DI's visibility kernel options (KernelOptions.h:270-304) keep the light-only
     estimator unbiased against NEE/MIS."""
@@ -170,6 +171,8 @@ CASES = {
     "initial_target_visibility": dict(kopt=dict(restir_di_initial_target_visibility=1)),
     "no_spatial_target_visibility": dict(kopt=dict(restir_di_spatial_target_visibility=0)),
     "no_visibility_reuse": dict(kopt=dict(restir_di_do_visibility_reuse=0)),
+    "no_presampling": dict(kopt=dict(restir_di_do_lights_presampling=0)),
+    "no_presampling_unfused": dict(do_fused_spatiotemporal=False, kopt=dict(restir_di_do_lights_presampling=0)),
     "no_visibility_reuse_target_vis": dict(do_fused_spatiotemporal=False,
                                            kopt=dict(restir_di_do_visibility_reuse=0, restir_di_initial_target_visibility=1)),
 }
@@ -199,7 +202,7 @@ def test_gpu_restir_bit_exact(cornell, luts, case):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("case", ["envmap", "envmap_only", "alpha_cards", "alpha_cards_unfused", "envmap_unfused",
-                                  "alpha_cards_gbh", "envmap_mis_like"])
+                                  "alpha_cards_gbh", "envmap_mis_like", "envmap_no_presampling", "envmap_only_no_presampling"])
 def test_gpu_restir_scenes_bit_exact(cornell, luts, case):
     import mpt
     from oracle import oracle as orc
@@ -209,11 +212,13 @@ def test_gpu_restir_scenes_bit_exact(cornell, luts, case):
     kw = dict(world=world, alpha=case.startswith("alpha_cards"))
     if case.endswith("_unfused"):
         kw["do_fused_spatiotemporal"] = False
+    if case.endswith("_no_presampling"):
+        kw["kopt"] = dict(restir_di_do_lights_presampling=0)
     if case.endswith("_gbh") or case.endswith("_mis_like"):
         kw.update(do_fused_spatiotemporal=False,
                   bias=abi.RESTIR_DI_BIAS_MIS_GBH if case.endswith("_gbh") else abi.RESTIR_DI_BIAS_MIS_LIKE)
     frs = frames(sd, abi.LSS_RESTIR_DI, 4, **kw)
-    if case == "envmap_only":
+    if case.startswith("envmap_only"):
         sd = scene.SceneData.__new__(scene.SceneData)
         sd.__dict__.update(cornell.__dict__)
         sd.emissive = np.zeros(0, np.int32)
