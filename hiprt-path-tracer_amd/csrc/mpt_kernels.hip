@@ -1458,7 +1458,13 @@ __global__ __launch_bounds__(TB) void k_resolve(DevScene S, DevPaths P, const Mp
     }
     if (i >= *count_cur) return;
     int slot = q_cur[i];
+#ifdef MPT_RESOLVE_BYREF
     const NeeRec& nr = P.nee[slot];
+#else
+    // the whole 128-B record in eight back-to-back 16-B loads: each cache line is consumed
+    // while it is resident (field-by-field loads re-fetched lines from HBM, PMC)
+    const NeeRec nr = P.nee[slot];
+#endif
     uint32_t fl = nr.flags;
     if (!(fl & NF_SHADED) || (fl & NF_NOADD)) return;
     const int lss = F.options.direct_light_sampling;
