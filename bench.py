@@ -42,8 +42,8 @@ METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
 HBM_PEAK_GBS = 8000.0
 S_NODE, S_TRI = 80, 48
 BAND_H = 8
-TARGET_PATHS = 8 * 1920 * 1080   # paths per wavefront launch (mpt_render_frames batch x rank pixels)
-MAX_BATCH = 64     # MPT_MAX_BATCH
+TARGET_PATHS = 16 * 1920 * 1080  # paths per wavefront launch (mpt_render_frames batch x rank pixels)
+MAX_BATCH = 128    # MPT_MAX_BATCH
 
 
 def parse():
@@ -232,9 +232,13 @@ def main():
     # samples per wavefront: launches of ~TARGET_PATHS paths whatever the rank's share of the
     # frame (measured: 8 x 1080p is past the knee of the throughput curve)
     rows_rank = mpt.partition_rows(H, band[0], band[1], band[2])
-    batch = min(MAX_BATCH, a.batch or max(1, int(round(TARGET_PATHS / max(1, rows_rank * W)))))
-    while K % batch:                                     # whole batches in the timed region
-        batch -= 1
+    if a.batch:
+        batch = min(MAX_BATCH, a.batch)
+        while K % batch:                                 # whole batches in the timed region
+            batch -= 1
+    else:   # the divisor of K nearest to TARGET_PATHS / the rank's pixels
+        want = TARGET_PATHS / max(1, rows_rank * W)
+        batch = min((d for d in range(1, min(MAX_BATCH, K) + 1) if K % d == 0), key=lambda d: (abs(d - want), -d))
 
     r = mpt.GPURenderer(local)
     r.set_scene(sd)

@@ -51,7 +51,7 @@ struct DBuf {
     }
 };
 
-constexpr int FRAME_RING = 128;   // >= 2 x MPT_MAX_BATCH
+constexpr int FRAME_RING = 256;   // >= 2 x MPT_MAX_BATCH
 constexpr int EV_POOL = 256;
 #ifndef MPT_TRACE_BLOCKS_PER_CU
 #define MPT_TRACE_BLOCKS_PER_CU 4

@@ -516,7 +516,7 @@ int mpt_render_frame(MptContext* ctx, const MptFrame* frame);
  * (<= MPT_MAX_BATCH; <= 0: MPT_MAX_BATCH) samples per pixel; the result is bit-identical
  * to count mpt_render_frame calls (samples are added to the sums in order).  Other frames
  * are rendered one by one.  Asynchronous. */
-#define MPT_MAX_BATCH 64
+#define MPT_MAX_BATCH 128
 int mpt_render_frames(MptContext* ctx, const MptFrame* frames, int32_t count, int32_t max_batch);
 /* Installs the halo exchange of a partitioned ReSTIR DI context (see MptHaloExchange);
  * fn = NULL removes it.  Required before rendering LSS_RESTIR_DI with band_count > 1. */

@@ -9,7 +9,7 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout
 tail -n 1 $o/pytest_gpu.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $o/smoke.log 2>&1 || { cat $o/smoke.log; exit 1; }
 tail -n 1 $o/smoke.log
-bash tools/profile_round.sh $tag --steps 16 --warmup 8 "$@" || exit 1
+bash tools/profile_round.sh $tag --steps 16 --warmup 16 "$@" || exit 1
 timeout -k 10 400 python bench.py "$@" > $o/bench.json 2> $o/bench.err || { tail -n 20 $o/bench.err; exit 1; }
 cat $o/bench.json
 echo done
