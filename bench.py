@@ -312,15 +312,17 @@ def main():
                       "node_simd_util": cal.stage_nodes[m] / max(1, cal.stage_node_slots[m]),
                       "tri_simd_util": cal.stage_tris[m] / max(1, cal.stage_tri_slots[m]),
                       "units_per_launch": st.stage_rays[m] / launches})
-    # shade: per path vertex = material 256 + vertex gathers 12+36+36+24 + path state 2x96 (§8d)
+    # shade: per path vertex (a path ray that hit a surface: k_split sends the misses to
+    # k_miss) = material 256 + vertex gathers 12+36+36+24 + path state 2x96 (§8d)
     b_vtx = 256 + 12 + 36 + 36 + 24 + 2 * 96
     sl = max(1, st.shade_launches)
     s_avg = st.shade_ms / sl
+    hits = st.path_hits or st.stage_rays[0]
     lines.append({"kernel": "k_shade<BSDF_NONE> (path vertex: hit, NEE sampling, BSDF sampling, RR)",
                   "symbol": "void mpt::k_shade<0>(mpt::ShadeArgs)",
-                  "total_ms": st.shade_ms, "avg_launch_ms": s_avg, "bytes_per_unit": b_vtx, "unit_of_work": "path vertex",
-                  "units_per_launch": st.stage_rays[0] / sl,
-                  "achieved": st.stage_rays[0] * b_vtx / sl / (s_avg * 1e-3) / 1e9 if s_avg > 0 else 0.0})
+                  "total_ms": st.shade_ms, "avg_launch_ms": s_avg, "bytes_per_unit": b_vtx, "unit_of_work": "path vertex (hit)",
+                  "units_per_launch": hits / sl,
+                  "achieved": hits * b_vtx / sl / (s_avg * 1e-3) / 1e9 if s_avg > 0 else 0.0})
     dom = max(lines, key=lambda x: x["total_ms"])
 
     default_cfg = a.strategy is None and default_bounces and a.bsdf == "principled" and a.scene is None
@@ -382,6 +384,7 @@ def main():
             "msample_per_s": round(W * H * K / elapsed / 1e6, 3),
             "samples_per_launch": round(st.frames / max(1, st.shade_launches / (a.bounces + 1)), 3),
             "rays_per_sample": round(rays_total / (W * H * K), 4),
+            "path_hit_fraction": round(st.path_hits / max(1, st.stage_rays[0]), 4),
             "config": {"workload": f"{desc}, {W}x{H}, {K} spp, "
                                    f"{'layered Principled' if a.bsdf == 'principled' else 'Lambert-override'} BSDF + NEE "
                                    f"({strategy.upper()}), {a.bounces} bounces, 1 step = 1 spp",
@@ -399,7 +402,8 @@ def main():
                                    "trace_nee_closest": round(st.stage_ms[2] / K, 4), "shade": round(st.shade_ms / K, 4),
                                    "resolve": round(st.resolve_ms / K, 4), "camera": round(st.camera_ms / K, 4),
                                    "accumulate": round(st.accumulate_ms / K, 4),
-                                   "compact": round(st.compact_ms / K, 4), "restir": round(st.restir_ms / K, 4),
+                                   "compact": round(st.compact_ms / K, 4), "split": round(st.split_ms / K, 4),
+                                   "miss": round(st.miss_ms / K, 4), "restir": round(st.restir_ms / K, 4),
                                    "frame_gpu": round(st.frame_ms / max(1, st.frames), 4)},
             "cpu_baseline": cpu,
             "parity_vs_oracle": parity,

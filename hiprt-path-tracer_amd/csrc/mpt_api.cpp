@@ -31,10 +31,22 @@ int fail(int code, const std::string& msg) {
         if (e_ != hipSuccess) return fail(MPT_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
     } while (0)
 
+// Status of a failed allocation / memset: MPT_ERR_OUT_OF_MEMORY for hipErrorOutOfMemory.
+// Clears HIP's last error so that a later launch check does not report it again.
+int alloc_fail(hipError_t e, const std::string& what) {
+    (void)hipGetLastError();
+    return fail(e == hipErrorOutOfMemory ? MPT_ERR_OUT_OF_MEMORY : MPT_ERR_HIP, what + ": " + hipGetErrorString(e));
+}
+
+// Device buffer owned by a context (freed by the context's destructor at the latest).
 template <typename T>
 struct DBuf {
     T* p = nullptr;
     size_t n = 0;
+    DBuf() = default;
+    DBuf(const DBuf&) = delete;
+    DBuf& operator=(const DBuf&) = delete;
+    ~DBuf() { release(); }
     void release() { if (p) (void)hipFree(p); p = nullptr; n = 0; }
     hipError_t alloc(size_t count) {
         if (count == n && p) return hipSuccess;
@@ -52,7 +64,9 @@ struct DBuf {
 };
 
 constexpr int FRAME_RING = 256;   // >= 2 x MPT_MAX_BATCH
-constexpr int EV_POOL = 256;
+// timing events per frame: one pair per kernel, 8 per bounce (3 traversals, split, shade,
+// miss, compact, resolve) for up to 65 bounces (validate_frame), + camera, ReSTIR, accumulate
+constexpr int EV_POOL = 2 * (8 * 65 + 3);
 #ifndef MPT_TRACE_BLOCKS_PER_CU
 #define MPT_TRACE_BLOCKS_PER_CU 4
 #endif
@@ -102,7 +116,7 @@ struct MptContext {
     DBuf<uint8_t> hit_inside, occ, qmask;
     DBuf<uint32_t> rng, spill;
     DBuf<uint4> vsA, vsB;
-    DBuf<int32_t> q0, q1, counters, nq_tgt, fetch_raw;
+    DBuf<int32_t> q0, q1, qh, qm, counters, nq_tgt, fetch_raw;
     DBuf<NeeRec> nee;
     DBuf<float> fb_color, fb_albedo, fb_normal;
     DBuf<int32_t> as_count, as_conv;
@@ -194,6 +208,8 @@ DevPaths dev_paths(MptContext* c) {
     DevPaths P{};
     P.n = c->n_slots * c->batch;
     P.n_pix = c->n_slots;
+    P.batch = c->batch;
+    P.group = (c->batch > 1 && c->n_slots % 4 == 0) ? 4 : 1;
     P.res_x = c->res_x;
     P.ray_o = c->ray_o.p;
     P.ray_d = c->ray_d.p;
@@ -208,6 +224,8 @@ DevPaths dev_paths(MptContext* c) {
     P.nrm = c->nrmv.p;
     P.q0 = c->q0.p;
     P.q1 = c->q1.p;
+    P.qh = c->qh.p;
+    P.qm = c->qm.p;
     P.counters = c->counters.p;
     P.nee = c->nee.p;
     P.nq_o = c->nq_o.p;
@@ -251,42 +269,90 @@ int rows_of(int res_y, int bh, int bi, int bc) {
     return r;
 }
 
+template <typename... B>
+void release_all(B&... b) { (b.release(), ...); }
+
+// Allocation chain of one buffer group: stops at the first failure, which the caller
+// reports after releasing the whole group (a half-allocated group is never kept).
+struct Allocs {
+    hipError_t e = hipSuccess;
+    template <typename T>
+    void operator()(DBuf<T>& b, size_t n) { if (e == hipSuccess) e = b.alloc(n); }
+    void operator()(hipError_t r) { if (e == hipSuccess) e = r; }
+};
+
+// Bytes of path state per path slot (ensure_batch): ray_o, ray_d, hit, thr, col, alb, nrmv,
+// nhit (8 x 16), vsA + vsB (32), the NEE record, 4 staged NEE query rays (2 x 64), the
+// compacted query entries (16), occlusion bytes (4), 4 queues (16), rng (4), hit_inside,
+// qmask, active (3).  Textured scenes add a resolved material per slot.
+constexpr size_t PATH_BYTES = 8 * 16 + 32 + sizeof(NeeRec) + 128 + 16 + 4 + 16 + 4 + 3;
+
+void release_batch(MptContext* c) {
+    release_all(c->ray_o, c->ray_d, c->hit, c->hit_inside, c->rng, c->thr, c->col, c->vsA, c->vsB, c->alb, c->nrmv,
+                c->q0, c->q1, c->qh, c->qm, c->nee, c->nq_o, c->nq_d, c->nq_tgt, c->occ, c->nhit, c->qmask, c->active,
+                c->mat_slot);
+    c->batch_cap = 0;
+}
+
 // Path state (everything indexed by path slot) for `batch` samples per pixel of the
-// partition; grows on demand, never shrinks while the partition stays the same.
-int ensure_batch(MptContext* c, int batch) {
-    if (batch <= c->batch_cap && c->ray_o.p) return MPT_OK;
+// partition (+ the per-slot resolved materials when `mat_slot`); grows on demand.  On a
+// failure every path-state buffer is released (batch_cap = 0), so that the next call
+// allocates again instead of launching on a half-allocated state.
+int ensure_batch(MptContext* c, int batch, bool mat_slot) {
+    const size_t pix = (size_t)std::max(c->n_slots, 1);
+    const bool have = batch <= c->batch_cap && c->ray_o.p;
+    if (have && (!mat_slot || c->mat_slot.n >= pix * (size_t)c->batch_cap)) return MPT_OK;
     HIPCHK(hipStreamSynchronize(c->stream));
-    const size_t N = (size_t)std::max(c->n_slots, 1) * (size_t)batch;
-    HIPCHK(c->ray_o.alloc(N)); HIPCHK(c->ray_d.alloc(N)); HIPCHK(c->hit.alloc(N)); HIPCHK(c->hit_inside.alloc(N));
-    HIPCHK(c->rng.alloc(N)); HIPCHK(c->thr.alloc(N)); HIPCHK(c->col.alloc(N)); HIPCHK(c->vsA.alloc(N)); HIPCHK(c->vsB.alloc(N));
-    HIPCHK(c->alb.alloc(N)); HIPCHK(c->nrmv.alloc(N)); HIPCHK(c->q0.alloc(N)); HIPCHK(c->q1.alloc(N));
-    HIPCHK(c->nee.alloc(N)); HIPCHK(c->nq_o.alloc(4 * N)); HIPCHK(c->nq_d.alloc(4 * N)); HIPCHK(c->nq_tgt.alloc(4 * N));
-    HIPCHK(c->occ.alloc(4 * N)); HIPCHK(c->nhit.alloc(N)); HIPCHK(c->qmask.alloc(N)); HIPCHK(c->active.alloc(N));
-    HIPCHK(hipMemsetAsync(c->active.p, 0, N, c->stream));
-    if (c->mat_slot.p) HIPCHK(c->mat_slot.alloc(N));
-    c->batch_cap = batch;
+    const int cap = have ? c->batch_cap : batch;
+    const size_t N = pix * (size_t)cap;
+    Allocs A;
+    if (!have) {
+        c->batch_cap = 0;
+        A(c->ray_o, N); A(c->ray_d, N); A(c->hit, N); A(c->hit_inside, N); A(c->rng, N); A(c->thr, N); A(c->col, N);
+        A(c->vsA, N); A(c->vsB, N); A(c->alb, N); A(c->nrmv, N); A(c->q0, N); A(c->q1, N); A(c->qh, N); A(c->qm, N);
+        A(c->nee, N); A(c->nq_o, 4 * N); A(c->nq_d, 4 * N); A(c->nq_tgt, 4 * N); A(c->occ, 4 * N); A(c->nhit, N);
+        A(c->qmask, N); A(c->active, N);
+        if (A.e == hipSuccess) A(hipMemsetAsync(c->active.p, 0, N, c->stream));
+    }
+    if (mat_slot || c->mat_slot.p) A(c->mat_slot, N);
+    if (A.e != hipSuccess) {
+        release_batch(c);
+        return alloc_fail(A.e, "path state for " + std::to_string(N) + " paths");
+    }
+    c->batch_cap = cap;
     return MPT_OK;
 }
 
+// Framebuffers and adaptive-sampling buffers of a row partition (n_slots pixels).  The
+// partition keys are set only once everything is allocated; a failure releases the group
+// and leaves the context without a partition (the next frame allocates again).
 int ensure_paths(MptContext* c, int rx, int ry, int bh, int bi, int bc) {
-    int rows = rows_of(ry, bh, bi, bc);
-    int n = rows * rx;
-    bool same = c->res_x == rx && c->res_y == ry && c->band_h == bh && c->band_i == bi && c->band_c == bc && c->n_slots == n && c->ray_o.p;
+    const int rows = rows_of(ry, bh, bi, bc);
+    const int n = rows * rx;
+    const bool same = c->res_x == rx && c->res_y == ry && c->band_h == bh && c->band_i == bi && c->band_c == bc &&
+                      c->n_slots == n && c->fb_color.p;
     if (same) return MPT_OK;
     HIPCHK(hipStreamSynchronize(c->stream));
+    release_batch(c);                       // sized for the previous partition
+    c->res_x = c->res_y = c->n_slots = 0;   // no partition until the group below is complete
+    const size_t N = (size_t)std::max(n, 1);
+    hipStream_t st = c->stream;
+    Allocs A;
+    A(c->fb_color, 3 * N); A(c->fb_albedo, 3 * N); A(c->fb_normal, 3 * N);
+    A(c->as_count, N); A(c->as_sqlum, N); A(c->as_conv, N);
+    if (A.e == hipSuccess) {
+        A(hipMemsetAsync(c->fb_color.p, 0, 3 * N * sizeof(float), st));
+        A(hipMemsetAsync(c->fb_albedo.p, 0, 3 * N * sizeof(float), st));
+        A(hipMemsetAsync(c->fb_normal.p, 0, 3 * N * sizeof(float), st));
+        A(hipMemsetAsync(c->as_count.p, 0, N * sizeof(int32_t), st));
+        A(hipMemsetAsync(c->as_sqlum.p, 0, N * sizeof(float), st));
+        A(hipMemsetAsync(c->as_conv.p, 0xff, N * sizeof(int32_t), st));
+    }
+    if (A.e != hipSuccess) {
+        release_all(c->fb_color, c->fb_albedo, c->fb_normal, c->as_count, c->as_sqlum, c->as_conv);
+        return alloc_fail(A.e, "framebuffers for " + std::to_string(N) + " pixels");
+    }
     c->res_x = rx; c->res_y = ry; c->band_h = bh; c->band_i = bi; c->band_c = bc; c->n_slots = n;
-    size_t N = (size_t)std::max(n, 1);
-    c->batch_cap = 0;
-    int r = ensure_batch(c, 1);
-    if (r != MPT_OK) return r;
-    HIPCHK(c->fb_color.alloc(3 * N)); HIPCHK(c->fb_albedo.alloc(3 * N)); HIPCHK(c->fb_normal.alloc(3 * N));
-    HIPCHK(hipMemsetAsync(c->fb_color.p, 0, 3 * N * sizeof(float), c->stream));
-    HIPCHK(hipMemsetAsync(c->fb_albedo.p, 0, 3 * N * sizeof(float), c->stream));
-    HIPCHK(hipMemsetAsync(c->fb_normal.p, 0, 3 * N * sizeof(float), c->stream));
-    HIPCHK(c->as_count.alloc(N)); HIPCHK(c->as_sqlum.alloc(N)); HIPCHK(c->as_conv.alloc(N));
-    HIPCHK(hipMemsetAsync(c->as_count.p, 0, N * sizeof(int32_t), c->stream));
-    HIPCHK(hipMemsetAsync(c->as_sqlum.p, 0, N * sizeof(float), c->stream));
-    HIPCHK(hipMemsetAsync(c->as_conv.p, 0xff, N * sizeof(int32_t), c->stream));
     return MPT_OK;
 }
 
@@ -320,39 +386,54 @@ int upload_alpha_flags(MptContext* c) {
 // ReSTIR DI buffers (ReSTIRDIRenderPass::update / resize, ReSTIRDIRenderPass.cpp:130-205): the
 // G-buffer pair, three reservoir buffers reset to empty reservoirs, the presampled lights.
 // Zero-filled G-buffers decode as "never written" (see restir_di.h gb_surface).
+void release_restir(MptContext* c) {
+    release_all(c->gb_pos, c->gb_sn, c->gb_gn, c->gb_view, c->pgb_pos, c->pgb_sn, c->pgb_gn, c->pgb_view, c->gb_meta,
+                c->pgb_meta, c->gb_vsA, c->gb_vsB, c->pgb_vsA, c->pgb_vsB, c->gb_mat, c->pgb_mat, c->rs_init, c->rs_sp1,
+                c->rs_sp2, c->rs_plights, c->rs_conv);
+    c->restir_out_sp2 = 0;
+}
+
+// ReSTIR DI buffers: a failure releases all of them, so the next frame rebuilds the set.
 int ensure_restir(MptContext* c, const MptFrame* f) {
     size_t N = (size_t)c->res_x * (size_t)c->res_y;   // frame-sized, indexed by pixel (band + halo used)
     const MptReSTIRDISettings& rd = f->render_settings.restir_di_settings;
     size_t npl = (size_t)std::max(1, rd.number_of_subsets * rd.subset_size);
     hipStream_t st = c->stream;
+    Allocs A;
     if (c->rs_init.n != 3 * N) {
-        HIPCHK(c->gb_pos.alloc(N)); HIPCHK(c->gb_sn.alloc(N)); HIPCHK(c->gb_gn.alloc(N)); HIPCHK(c->gb_view.alloc(N));
-        HIPCHK(c->pgb_pos.alloc(N)); HIPCHK(c->pgb_sn.alloc(N)); HIPCHK(c->pgb_gn.alloc(N)); HIPCHK(c->pgb_view.alloc(N));
-        HIPCHK(c->gb_meta.alloc(N)); HIPCHK(c->pgb_meta.alloc(N));
-        HIPCHK(c->gb_vsA.alloc(N)); HIPCHK(c->gb_vsB.alloc(N)); HIPCHK(c->pgb_vsA.alloc(N)); HIPCHK(c->pgb_vsB.alloc(N));
-        HIPCHK(c->rs_init.alloc(3 * N)); HIPCHK(c->rs_sp1.alloc(3 * N)); HIPCHK(c->rs_sp2.alloc(3 * N));
-        for (DBuf<float4>* b : {&c->gb_pos, &c->gb_sn, &c->gb_gn, &c->gb_view, &c->pgb_pos, &c->pgb_sn, &c->pgb_gn, &c->pgb_view})
-            HIPCHK(hipMemsetAsync(b->p, 0, N * sizeof(float4), st));
-        HIPCHK(hipMemsetAsync(c->gb_meta.p, 0, N * sizeof(int4), st));
-        HIPCHK(hipMemsetAsync(c->pgb_meta.p, 0, N * sizeof(int4), st));
-        for (DBuf<uint4>* b : {&c->gb_vsA, &c->gb_vsB, &c->pgb_vsA, &c->pgb_vsB})
-            HIPCHK(hipMemsetAsync(b->p, 0, N * sizeof(uint4), st));
-        HIPCHK(launch_restir_fill(c->rs_init.p, (int)N, st));
-        HIPCHK(launch_restir_fill(c->rs_sp1.p, (int)N, st));
-        HIPCHK(launch_restir_fill(c->rs_sp2.p, (int)N, st));
+        A(c->gb_pos, N); A(c->gb_sn, N); A(c->gb_gn, N); A(c->gb_view, N);
+        A(c->pgb_pos, N); A(c->pgb_sn, N); A(c->pgb_gn, N); A(c->pgb_view, N);
+        A(c->gb_meta, N); A(c->pgb_meta, N);
+        A(c->gb_vsA, N); A(c->gb_vsB, N); A(c->pgb_vsA, N); A(c->pgb_vsB, N);
+        A(c->rs_init, 3 * N); A(c->rs_sp1, 3 * N); A(c->rs_sp2, 3 * N);
+        if (A.e == hipSuccess) {
+            for (DBuf<float4>* b : {&c->gb_pos, &c->gb_sn, &c->gb_gn, &c->gb_view, &c->pgb_pos, &c->pgb_sn, &c->pgb_gn, &c->pgb_view})
+                A(hipMemsetAsync(b->p, 0, N * sizeof(float4), st));
+            A(hipMemsetAsync(c->gb_meta.p, 0, N * sizeof(int4), st));
+            A(hipMemsetAsync(c->pgb_meta.p, 0, N * sizeof(int4), st));
+            for (DBuf<uint4>* b : {&c->gb_vsA, &c->gb_vsB, &c->pgb_vsA, &c->pgb_vsB})
+                A(hipMemsetAsync(b->p, 0, N * sizeof(uint4), st));
+            A(launch_restir_fill(c->rs_init.p, (int)N, st));
+            A(launch_restir_fill(c->rs_sp1.p, (int)N, st));
+            A(launch_restir_fill(c->rs_sp2.p, (int)N, st));
+        }
         c->restir_out_sp2 = 0;
     }
     if ((c->any_tex || f->bsdf_flags.white_furnace_mode) && c->gb_mat.n < N) {
-        HIPCHK(c->gb_mat.alloc(N));
-        HIPCHK(c->pgb_mat.alloc(N));
+        A(c->gb_mat, N);
+        A(c->pgb_mat, N);
     }
     if (c->band_c > 1 && c->rs_conv.n != N) {
-        HIPCHK(c->rs_conv.alloc(N));
-        HIPCHK(hipMemsetAsync(c->rs_conv.p, 0xff, N * sizeof(int32_t), st));
+        A(c->rs_conv, N);
+        if (A.e == hipSuccess) A(hipMemsetAsync(c->rs_conv.p, 0xff, N * sizeof(int32_t), st));
     }
     if (c->rs_plights.n != 4 * npl) {
-        HIPCHK(c->rs_plights.alloc(4 * npl));
-        HIPCHK(launch_restir_fill_lights(c->rs_plights.p, (int)npl, st));
+        A(c->rs_plights, 4 * npl);
+        if (A.e == hipSuccess) A(launch_restir_fill_lights(c->rs_plights.p, (int)npl, st));
+    }
+    if (A.e != hipSuccess) {
+        release_restir(c);
+        return alloc_fail(A.e, "ReSTIR DI buffers");
     }
     return MPT_OK;
 }
@@ -376,6 +457,8 @@ int validate_frame(const MptFrame* f) {
     if (f->res_x <= 0 || f->res_y <= 0) return fail(MPT_ERR_INVALID_ARGUMENT, "resolution must be positive");
     if (f->band_height <= 0 || f->band_count <= 0 || f->band_index < 0 || f->band_index >= f->band_count)
         return fail(MPT_ERR_INVALID_ARGUMENT, "invalid row partition");
+    if ((int64_t)f->res_x * f->res_y > MPT_MAX_WAVEFRONT_PATHS)
+        return fail(MPT_ERR_UNSUPPORTED, "more than MPT_MAX_WAVEFRONT_PATHS pixels per frame");
     if (rs.nb_bounces < 0 || rs.nb_bounces > 64) return fail(MPT_ERR_INVALID_ARGUMENT, "nb_bounces out of range");
     if (rs.wants_render_low_resolution && rs.allow_render_low_resolution && rs.accumulate)
         return fail(MPT_ERR_UNSUPPORTED, "low-resolution interactive mode not implemented");
@@ -451,12 +534,7 @@ int mpt_partition_rows(int32_t res_y, int32_t bh, int32_t bi, int32_t bc) {
     return rows_of(res_y, bh, bi, bc);
 }
 
-int mpt_create(int device, void* hip_stream, MptContext** out) {
-    if (!out) return fail(MPT_ERR_INVALID_ARGUMENT, "out_ctx is NULL");
-    int ndev = 0;
-    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(MPT_ERR_HIP, "no HIP device available");
-    if (device < 0 || device >= ndev) return fail(MPT_ERR_INVALID_ARGUMENT, "device index out of range");
-    MptContext* c = new MptContext();
+static int create_context(MptContext* c, int device, void* hip_stream) {
     c->device = device;
     HIPCHK(hipSetDevice(device));
     hipDeviceProp_t prop;
@@ -482,37 +560,44 @@ int mpt_create(int device, void* hip_stream, MptContext** out) {
         HIPCHK(hipEventCreate(&c->ev_frame[p][0]));
         HIPCHK(hipEventCreate(&c->ev_frame[p][1]));
     }
+    return MPT_OK;
+}
+
+int mpt_create(int device, void* hip_stream, MptContext** out) {
+    if (!out) return fail(MPT_ERR_INVALID_ARGUMENT, "out_ctx is NULL");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(MPT_ERR_HIP, "no HIP device available");
+    if (device < 0 || device >= ndev) return fail(MPT_ERR_INVALID_ARGUMENT, "device index out of range");
+    MptContext* c = new MptContext();   // value-initialised: every handle starts null
+    int r = create_context(c, device, hip_stream);
+    if (r != MPT_OK) {
+        const std::string msg = g_err;
+        mpt_destroy(c);                 // frees what was created before the failure
+        g_err = msg;
+        return r;
+    }
     *out = c;
     return MPT_OK;
 }
 
+// Tolerates a partially created context (mpt_create's failure path).  Every device buffer
+// is a DBuf, released by the context's destructor on the context's device.
 int mpt_destroy(MptContext* c) {
     if (!c) return MPT_OK;
     (void)hipSetDevice(c->device);
-    (void)hipStreamSynchronize(c->stream);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (int p = 0; p < 2; p++) {
-        for (int i = 0; i < EV_POOL; i++) (void)hipEventDestroy(c->ev[p][i]);
-        (void)hipEventDestroy(c->ev_frame[p][0]);
-        (void)hipEventDestroy(c->ev_frame[p][1]);
+        for (int i = 0; i < EV_POOL; i++)
+            if (c->ev[p][i]) (void)hipEventDestroy(c->ev[p][i]);
+        for (int k = 0; k < 2; k++)
+            if (c->ev_frame[p][k]) (void)hipEventDestroy(c->ev_frame[p][k]);
     }
-    c->nodes.release(); c->tris.release(); c->idx.release(); c->mat_idx.release(); c->mat_prio.release();
-    c->emissive.release(); c->tex_dims.release(); c->pos.release(); c->nrm.release(); c->uv.release();
-    c->has_n.release(); c->tex.release(); c->tex_off.release(); c->mats.release();
-    c->mats_res.release(); c->mat_tex.release(); c->as_count.release(); c->as_sqlum.release(); c->as_conv.release();
-    c->active.release(); c->status.release(); c->mat_slot.release(); c->em_tab.release();
-    c->lut_conductor.release(); c->lut_glossy.release(); c->lut_glass.release(); c->lut_glass_inv.release();
-    c->lut_thin.release(); c->lut_sheen.release(); c->env.release(); c->alias_p.release(); c->alias_i.release();
-    c->ray_o.release(); c->ray_d.release(); c->hit.release(); c->thr.release(); c->col.release(); c->alb.release();
-    c->nrmv.release(); c->nq_o.release(); c->nq_d.release(); c->nhit.release(); c->hit_inside.release(); c->occ.release(); c->qmask.release();
-    c->rng.release(); c->spill.release(); c->vsA.release(); c->vsB.release(); c->q0.release(); c->q1.release();
-    c->counters.release(); c->nq_tgt.release(); c->fetch_raw.release(); c->nee.release(); c->fb_color.release();
-    c->fb_albedo.release(); c->fb_normal.release(); c->stats.release(); c->ray_counts.release();
-    c->raw_o.release(); c->raw_d.release(); c->raw_hit.release(); c->raw_occ.release();
     if (c->h_frames) (void)hipHostFree(c->h_frames);
     if (c->h_reproj) (void)hipHostFree(c->h_reproj);
     if (c->d_frames) (void)hipFree(c->d_frames);
-    if (c->own_stream) (void)hipStreamDestroy(c->stream);
+    if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
+    (void)hipGetLastError();
     return MPT_OK;
 }
 
@@ -711,11 +796,30 @@ int mpt_set_luts(MptContext* c, const MptLuts* L) {
 int mpt_resize(MptContext* c, int32_t w, int32_t h) {
     if (!c || w <= 0 || h <= 0) return fail(MPT_ERR_INVALID_ARGUMENT, "bad resolution");
     HIPCHK(hipSetDevice(c->device));
-    return ensure_paths(c, w, h, c->band_h, c->band_i, c->band_c);
+    if ((int64_t)w * h > MPT_MAX_WAVEFRONT_PATHS) return fail(MPT_ERR_UNSUPPORTED, "more than MPT_MAX_WAVEFRONT_PATHS pixels");
+    int r = ensure_paths(c, w, h, c->band_h, c->band_i, c->band_c);
+    if (r != MPT_OK) return r;
+    return ensure_batch(c, 1, false);
 }
 
-// `batch` consecutive samples (f[0..batch-1], checked by mpt_render_frames) as one wavefront
-static int render_batch(MptContext* c, const MptFrame* f, int batch) {
+// Samples per pixel of one wavefront when mpt_render_frames is not given a maximum:
+// MPT_DEFAULT_WAVEFRONT_PATHS paths per launch, within half of the device memory that is
+// free or already held by this context's path state, at most MPT_MAX_BATCH.
+static int default_batch(MptContext* c, const MptFrame& f) {
+    if (f.band_height <= 0 || f.band_count <= 0 || f.band_index < 0 || f.band_index >= f.band_count || f.res_x <= 0)
+        return 1;
+    const size_t pix = (size_t)std::max(1, rows_of(f.res_y, f.band_height, f.band_index, f.band_count)) * (size_t)f.res_x;
+    const size_t per = PATH_BYTES + ((c->any_tex || f.bsdf_flags.white_furnace_mode) ? sizeof(MptMaterial) : 0);
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) != hipSuccess) { (void)hipGetLastError(); fr = 0; }
+    const size_t held = (size_t)c->batch_cap * (size_t)std::max(c->n_slots, 1) * per;
+    const size_t paths = std::min<size_t>(MPT_DEFAULT_WAVEFRONT_PATHS, (fr + held) / 2 / per);
+    return (int)std::max<size_t>(1, std::min<size_t>(MPT_MAX_BATCH, paths / pix));
+}
+
+// Validation and every allocation of a wavefront of `batch` consecutive samples
+// (f[0..batch-1]); nothing is enqueued, so a failure leaves the stream untouched.
+static int prepare_batch(MptContext* c, const MptFrame* f, int batch) {
     if (!c->has_scene) return fail(MPT_ERR_NO_SCENE, "no scene uploaded");
     if (!c->lut_conductor.p && f->options.bsdf_override == MPT_BSDF_NONE) return fail(MPT_ERR_INVALID_ARGUMENT, "Principled BSDF needs mpt_set_luts");
     int v = validate_frame(f);
@@ -740,13 +844,14 @@ static int render_batch(MptContext* c, const MptFrame* f, int batch) {
          f->options.restir_di_later_bounces_sampling_strategy == MPT_RESTIR_DI_LATER_BOUNCES_MIS_LIGHT_BSDF))
         return fail(MPT_ERR_UNSUPPORTED, "ReSTIR DI later bounces: uniform / MIS light sampling without emissive "
                                          "triangles picks from an empty list in the reference (Lights.h:22-220)");
-    r = ensure_batch(c, batch);
-    if (r != MPT_OK) return r;
-    const size_t n_paths = (size_t)std::max(c->n_slots, 1) * (size_t)c->batch_cap;
-    if ((c->any_tex || f->bsdf_flags.white_furnace_mode) && c->mat_slot.n < n_paths) {
-        HIPCHK(hipStreamSynchronize(c->stream));
-        HIPCHK(c->mat_slot.alloc(n_paths));
-    }
+    if ((int64_t)std::max(c->n_slots, 1) * batch > MPT_MAX_WAVEFRONT_PATHS)
+        return fail(MPT_ERR_OUT_OF_MEMORY, "wavefront above MPT_MAX_WAVEFRONT_PATHS paths");
+    return ensure_batch(c, batch, c->any_tex || f->bsdf_flags.white_furnace_mode);
+}
+
+// Enqueues a prepared wavefront (prepare_batch).
+static int launch_batch(MptContext* c, const MptFrame* f, int batch) {
+    const bool restir_part = f->options.direct_light_sampling == MPT_LSS_RESTIR_DI && f->band_count > 1;
     // stage the frame constants through a pinned ring (the previous use of the slot
     // has completed once 64 frames later are enqueued; synchronise defensively)
     if (c->frame_slot + batch > FRAME_RING) c->frame_slot = 0;
@@ -805,7 +910,8 @@ static int render_batch(MptContext* c, const MptFrame* f, int batch) {
 
 int mpt_render_frame(MptContext* c, const MptFrame* f) {
     if (!c || !f) return fail(MPT_ERR_INVALID_ARGUMENT, "NULL argument");
-    return render_batch(c, f, 1);
+    int r = prepare_batch(c, f, 1);
+    return r != MPT_OK ? r : launch_batch(c, f, 1);
 }
 
 // Frames that differ only in what GPURenderer::render changes between the samples of one
@@ -828,13 +934,23 @@ static bool batchable(const MptFrame& a, const MptFrame& b) {
 
 int mpt_render_frames(MptContext* c, const MptFrame* frames, int32_t count, int32_t max_batch) {
     if (!c || !frames || count < 0) return fail(MPT_ERR_INVALID_ARGUMENT, "NULL argument or negative count");
-    if (max_batch <= 0) max_batch = MPT_MAX_BATCH;
+    if (count == 0) return MPT_OK;
+    if (max_batch <= 0) max_batch = default_batch(c, frames[0]);
     max_batch = std::min<int32_t>(max_batch, MPT_MAX_BATCH);
     int i = 0;
     while (i < count) {
         int b = 1;
         while (i + b < count && b < max_batch && batchable(frames[i], frames[i + b])) b++;
-        int r = render_batch(c, frames + i, b);
+        int r = prepare_batch(c, frames + i, b);
+        // a wavefront that does not fit in device memory is halved (bit-identical result),
+        // and the smaller size is kept for the rest of the call
+        while (r == MPT_ERR_OUT_OF_MEMORY && b > 1) {
+            b = (b + 1) / 2;
+            max_batch = b;
+            r = prepare_batch(c, frames + i, b);
+        }
+        if (r != MPT_OK) return r;
+        r = launch_batch(c, frames + i, b);
         if (r != MPT_OK) return r;
         i += b;
     }
@@ -957,6 +1073,9 @@ int mpt_get_stats(MptContext* c, MptStats* out) {
     out->accumulate_ms = c->stage_ms[KT_ACCUMULATE];
     out->compact_ms = c->stage_ms[KT_COMPACT];
     out->restir_ms = c->stage_ms[KT_RESTIR];
+    out->split_ms = c->stage_ms[KT_SPLIT];
+    out->miss_ms = c->stage_ms[KT_MISS];
+    out->path_hits = rc[3];
     out->shade_launches = c->stage_launches[KT_SHADE];
     out->trace_launches = c->trace_launches;
     out->frames = c->frames;

@@ -1,7 +1,9 @@
 // mpt_internal.h -- device-side data layout shared by the C ABI (mpt_api.cpp) and the
 // kernels (mpt_kernels.hip).  All buffers are SoA in HBM.  Per-pixel buffers are indexed
-// by the index of a pixel inside the context's row partition; path state by "slot" =
-// sample-in-batch * n_pix + pixel (a single-sample frame has slot == pixel).
+// by the index of a pixel inside the context's row partition; path state by "slot": the
+// samples of one pixel are consecutive slots, in groups of `group` pixels
+// (slot = ((pixel / group) * batch + sample) * group + pixel % group, see batch_slot in
+// mpt_kernels.hip); a single-sample frame has slot == pixel.
 #ifndef MPT_INTERNAL_H
 #define MPT_INTERNAL_H
 
@@ -89,6 +91,8 @@ enum : uint32_t {
 struct DevPaths {
     int32_t n;                // path slots of the launch = batch samples x n_pix
     int32_t n_pix;            // pixels of the partition (per-pixel buffers: framebuffers, adaptive, ReSTIR)
+    int32_t batch;            // samples per pixel of the launch (mpt_render_frames)
+    int32_t group;            // pixels whose samples are interleaved in the slot order (4, or 1)
     int32_t res_x;
     float4* ray_o;            // xyz + last_hit bits
     float4* ray_d;            // xyz + tmax
@@ -103,6 +107,8 @@ struct DevPaths {
     float4* nrm;
     int32_t* q0;
     int32_t* q1;
+    int32_t* qh;              // this bounce's path queue split: paths that hit a surface ...
+    int32_t* qm;              // ... and paths that left the scene (k_split)
     int32_t* counters;        // see CTR_*
     NeeRec* nee;
     float4* nq_o;             // staged NEE query rays, slot * 4 + kind (kinds 0..2 any hit, 3 closest)
@@ -117,7 +123,7 @@ struct DevPaths {
     float* fb_normal;
     uint32_t* stack_spill;    // global spill area of the traversal stacks
     uint64_t* stats;          // [trace mode][rays, nodes, tris, -] (instrumented traversal)
-    uint64_t* ray_counts;     // path rays, NEE any-hit rays, NEE closest rays (always on)
+    uint64_t* ray_counts;     // path rays, NEE any-hit rays, NEE closest rays, path hits (always on)
     // adaptive sampling / stop-noise threshold (AuxiliaryBuffers, RenderData.h:62-84)
     int32_t* as_count;        // pixel_sample_count
     float* as_sqlum;          // pixel_squared_luminance
@@ -152,7 +158,8 @@ struct DevPaths {
 
 constexpr int N_TRACE_MODES = 5;
 // timed kernel kinds: 0..2 = traversal stages (trace modes), then the others
-enum { KT_CAMERA = 3, KT_SHADE = 4, KT_RESOLVE = 5, KT_ACCUMULATE = 6, KT_COMPACT = 7, KT_RESTIR = 8, KT_COUNT = 9 };
+enum { KT_CAMERA = 3, KT_SHADE = 4, KT_RESOLVE = 5, KT_ACCUMULATE = 6, KT_COMPACT = 7, KT_RESTIR = 8, KT_SPLIT = 9,
+       KT_MISS = 10, KT_COUNT = 11 };
 constexpr uint32_t QM_CONT = 16u;
 constexpr int STATS_STRIDE = 6;   // per mode: traversals, nodes, tris, (unused), node slots, tri slots
 constexpr int N_STATS = N_TRACE_MODES * STATS_STRIDE;
@@ -160,6 +167,7 @@ constexpr int N_STATS = N_TRACE_MODES * STATS_STRIDE;
 enum {
     CTR_Q0 = 0, CTR_Q1 = 1, CTR_ANY = 2, CTR_CL = 3, CTR_FETCH = 4,
     CTR_REPROJ = 5,           // max |reprojected row - row| of the frame's G-buffer (partitioned ReSTIR DI)
+    CTR_HIT = 6, CTR_MISS = 7,  // lengths of the hit / miss queues of the bounce (k_split)
     CTR_COUNT = 16
 };
 

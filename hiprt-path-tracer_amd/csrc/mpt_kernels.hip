@@ -593,15 +593,33 @@ DEV int bounce_lss(const MptFrame& F, int bounce) {
     }
 }
 // Sample batch (mpt_render_frames; GPURenderer::render's samples_per_frame loop,
-// GPURenderer.cpp:424-449, run as one wavefront): path slot s is pixel slot s % n_pix of
-// the batch's sample s / n_pix, whose seeds and sample number are those of Fp[s / n_pix].
-DEV int batch_sub(const DevPaths& P, int slot) { return slot < P.n_pix ? 0 : slot / P.n_pix; }
+// GPURenderer.cpp:424-449, run as one wavefront): the `batch` samples of a pixel occupy
+// consecutive slots, interleaved over groups of `group` (4) pixels,
+//   slot = ((pixel / group) * batch + sample) * group + pixel % group,
+// so a wave's 64 lanes hold the samples of a few neighbouring pixels -- their camera rays,
+// and often their later rays, open the same BVH nodes together -- while k_accumulate's
+// per-pixel loads stay coalesced in runs of `group` slots.  Sample k's seeds and sample
+// number are those of Fp[k].
+DEV void batch_split(const DevPaths& P, int slot, int& pix, int& sub) {
+    if (P.batch == 1) { pix = slot; sub = 0; return; }
+    const int g = P.group;
+    const int q = slot / g;
+    const int grp = q / P.batch;
+    sub = q - grp * P.batch;
+    pix = grp * g + (slot - q * g);
+}
+DEV int batch_slot(const DevPaths& P, int pix, int sub) {
+    const int g = P.group;
+    const int grp = pix / g;
+    return (grp * P.batch + sub) * g + (pix - grp * g);
+}
 DEV uint32_t path_seed(const MptFrame* Fp, const DevPaths& P, int slot, bool camera) {
-    const int sub = batch_sub(P, slot);
+    int pix, sub;
+    batch_split(P, slot, pix, sub);
     const MptFrame& F = Fp[sub];
     int x, y;
-    const uint32_t pix = slot_pixel(F, slot - sub * P.n_pix, x, y);
-    return camera ? camera_seed(F, pix) : pixel_seed(F, pix);
+    const uint32_t gpix = slot_pixel(F, pix, x, y);
+    return camera ? camera_seed(F, gpix) : pixel_seed(F, gpix);
 }
 
 // ----------------------------------------------------------------------------------
@@ -647,7 +665,8 @@ DEV bool adaptive_sampling(const DevPaths& P, const MptRenderSettings& rs, int s
 
 __global__ __launch_bounds__(TB) void k_camera(DevPaths P, const MptFrame* __restrict__ Fp) {
     int slot = blockIdx.x * TB + threadIdx.x;
-    const int sub = slot < P.n ? batch_sub(P, slot) : 0;   // batched launches never use the adaptive buffers
+    int pslot = slot, sub = 0;   // pixel of the partition, sample of the batch
+    if (slot < P.n) batch_split(P, slot, pslot, sub);   // batched launches never use the adaptive buffers
     const MptFrame& F = Fp[sub];
     const MptRenderSettings& rs = F.render_settings;
     const bool as = has_adaptive_buffers(rs);
@@ -691,7 +710,7 @@ __global__ __launch_bounds__(TB) void k_camera(DevPaths P, const MptFrame* __res
     if (!act) return;
     if (rs.do_update_status_buffers) P.status[1] = 1u;
     int x, y;
-    uint32_t pix = slot_pixel(F, slot - sub * P.n_pix, x, y);
+    uint32_t pix = slot_pixel(F, pslot, x, y);
     Rng rng = make_rng(camera_seed(F, pix));
     float xd = (float)x + 0.5f, yd = (float)y + 0.5f;
     if (F.current_camera.do_jittering) { xd += rng() - 0.5f; yd += rng() - 0.5f; }
@@ -882,6 +901,24 @@ DEV void rr_store(float4* b, int i, const RResv& r) {
     b[3 * (size_t)i] = make_float4(__int_as_float(r.M), r.wsum, r.UCW, __int_as_float(r.tri));
     b[3 * (size_t)i + 1] = make_float4(r.point.x, r.point.y, r.point.z, r.target);
     b[3 * (size_t)i + 2] = make_float4(__uint_as_float(r.flags), 0.0f, 0.0f, 0.0f);
+}
+
+// the sky seen by a path that left the scene (FullPathTracer.h:243-286), clamped
+DEV Col miss_radiance(const DevScene& S, const MptFrame& F, int bounce, v3 d, Col thr) {
+    const MptRenderSettings& rs = F.render_settings;
+    const MptWorldSettings& ws = F.world_settings;
+    Col sky = col(0.0f);
+    if (ws.ambient_light_type == MPT_AMBIENT_UNIFORM || F.bsdf_flags.white_furnace_mode) sky = C3(ws.uniform_light_color);
+    else if (ws.ambient_light_type == MPT_AMBIENT_ENVMAP) {
+        bool sampled = F.options.envmap_sampling != MPT_ESS_NO_SAMPLING;
+        if (!sampled || bounce == 0) {
+            sky = eval_env_no_pdf(S, F, d);
+            bool unscale = sampled ? !ws.envmap_scale_background_intensity : (!ws.envmap_scale_background_intensity && bounce == 0);
+            if (unscale) sky /= ws.envmap_intensity;
+        }
+    }
+    sky = clamp_contrib(sky, rs.envmap_contribution_clamp, true);
+    return clamp_contrib(sky * thr, rs.indirect_contribution_clamp, bounce > 0);
 }
 
 enum ShadeOp {
@@ -1292,23 +1329,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MPT_SHADE_WA
             }
             store3(nr.thr, thr_vertex);
         } else {
-            // miss (FullPathTracer.h:250-284)
-            const MptWorldSettings& ws = F.world_settings;
-            Col sky = col(0.0f);
-            if (ws.ambient_light_type == MPT_AMBIENT_UNIFORM || F.bsdf_flags.white_furnace_mode) sky = C3(ws.uniform_light_color);
-            else if (ws.ambient_light_type == MPT_AMBIENT_ENVMAP) {
-                bool sampled = F.options.envmap_sampling != MPT_ESS_NO_SAMPLING;
-                if (!sampled || bounce == 0) {
-                    sky = eval_env_no_pdf(S, F, d);
-                    bool unscale = sampled ? !ws.envmap_scale_background_intensity : (!ws.envmap_scale_background_intensity && bounce == 0);
-                    if (unscale) sky /= ws.envmap_intensity;
-                }
-            }
-            sky = clamp_contrib(sky, rs.envmap_contribution_clamp, true);
-            rcol += clamp_contrib(sky * thr, rs.indirect_contribution_clamp, bounce > 0);
-#ifdef MPT_DEBUG_SLOT
-            if (slot == MPT_DEBUG_SLOT) printf("GPU b%d miss sky %a %a %a rc %a %a %a\n", bounce, sky.r, sky.g, sky.b, rcol.r, rcol.g, rcol.b);
-#endif
+            rcol += miss_radiance(S, F, bounce, d, thr);   // not reached: k_split sends misses to k_miss
         }
         nr.flags = fl;
         P.qmask[slot] = (uint8_t)(qm | (cont ? QM_CONT : 0u));
@@ -1323,11 +1344,30 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MPT_SHADE_WA
 }
 
 // ----------------------------------------------------------------------------------
-// k_compact: next path queue + NEE query lists from the per-path masks (wave64 ballot,
-// one atomic per wave and list; all atomics before any store)
+// k_miss: the paths of the bounce's miss queue (k_split) add the sky and end.  The
+// camera ray of bounce 0 is re-normalised as FullPathTracer's re-read of the G-buffer does
+// (FullPathTracer.h:131-150, see k_shade).
 // ----------------------------------------------------------------------------------
-constexpr int CP_NT = 1024;        // threads per k_compact block
-constexpr int CP_ITEMS = 8;        // queue entries per thread -> 8192 per block, 5 atomics per block
+__global__ __launch_bounds__(TB) void k_miss(DevScene S, DevPaths P, const MptFrame* __restrict__ Fp, int bounce) {
+    const int i = blockIdx.x * TB + threadIdx.x;
+    if (i >= P.counters[CTR_MISS]) return;
+    const int slot = P.qm[i];
+    const float4 rdv = P.ray_d[slot], t4 = P.thr[slot], cv = P.col[slot];
+    v3 d = mk3(rdv.x, rdv.y, rdv.z);
+    if (bounce == 0) d = normalize(d);
+    const Col rc = col(cv.x, cv.y, cv.z) + miss_radiance(S, *Fp, bounce, d, col(t4.x, t4.y, t4.z));
+    P.col[slot] = make_float4(rc.r, rc.g, rc.b, 0.0f);
+}
+
+// ----------------------------------------------------------------------------------
+// Queue compaction (k_split, k_compact): thread t of a block takes the CP_ITEMS
+// consecutive entries [b0 + t * CP_ITEMS, +CP_ITEMS) of the input queue, so the output
+// lists keep the queue order inside each block's 8192 entries (the samples of a pixel, and
+// neighbouring pixels, stay neighbours from bounce to bounce); block-wide scans give every
+// entry its place, one atomic per block and list reserves the block's range.
+// ----------------------------------------------------------------------------------
+constexpr int CP_NT = 1024;        // threads per block
+constexpr int CP_ITEMS = 8;        // queue entries per thread -> 8192 per block
 
 // exclusive block-wide scan of one int per thread (wave64 shuffles + LDS across waves)
 DEV int block_scan_excl(int v, int* tmp, int& total) {
@@ -1359,21 +1399,71 @@ DEV int block_scan_excl(int v, int* tmp, int& total) {
     return excl;
 }
 
+// this thread's consecutive queue entries (two 16-B loads when the run is complete)
+DEV int load_items(const int32_t* q, int b0, int count, int slots[CP_ITEMS]) {
+    const int i0 = b0 + (int)threadIdx.x * CP_ITEMS;
+    const int n = max(0, min(CP_ITEMS, count - i0));
+    if (n == CP_ITEMS) {
+        const int4 a = *reinterpret_cast<const int4*>(q + i0), b = *reinterpret_cast<const int4*>(q + i0 + 4);
+        slots[0] = a.x; slots[1] = a.y; slots[2] = a.z; slots[3] = a.w;
+        slots[4] = b.x; slots[5] = b.y; slots[6] = b.z; slots[7] = b.w;
+    } else {
+#pragma unroll
+        for (int j = 0; j < CP_ITEMS; j++) slots[j] = j < n ? q[i0 + j] : 0;
+    }
+    return n;
+}
+
+// k_split: the bounce's path queue -> the paths that hit a surface (k_shade, k_compact,
+// k_resolve) and those that left the scene (k_miss), so that every lane of a shading wave
+// has a vertex to shade instead of idling through the light-sampling loop beside a miss.
+__global__ __launch_bounds__(CP_NT) void k_split(DevPaths P, const int32_t* q, const int32_t* count_q) {
+    __shared__ int tmp[CP_NT / 64 + 1];
+    __shared__ int base[2];
+    const int count = *count_q;
+    const int b0 = blockIdx.x * CP_NT * CP_ITEMS;
+    if (b0 >= count) return;
+    int slots[CP_ITEMS];
+    const int n = load_items(q, b0, count, slots);
+    uint32_t hm = 0u;
+    int nh = 0;
+#pragma unroll
+    for (int j = 0; j < CP_ITEMS; j++) {
+        if (j < n && __float_as_int(P.hit[slots[j]].w) >= 0) { hm |= 1u << j; nh++; }
+    }
+    int th, tm;
+    int oh = block_scan_excl(nh, tmp, th);
+    int om = block_scan_excl(n - nh, tmp, tm);
+    if (threadIdx.x == 0) {
+        base[0] = th ? atomicAdd(&P.counters[CTR_HIT], th) : 0;
+        base[1] = tm ? atomicAdd(&P.counters[CTR_MISS], tm) : 0;
+    }
+    __syncthreads();
+    oh += base[0];
+    om += base[1];
+#pragma unroll
+    for (int j = 0; j < CP_ITEMS; j++) {
+        if (j >= n) break;
+        if ((hm >> j) & 1u) P.qh[oh++] = slots[j];
+        else P.qm[om++] = slots[j];
+    }
+}
+
+// k_compact: next path queue + NEE query lists from the per-path masks of the shaded paths
 __global__ __launch_bounds__(CP_NT) void k_compact(DevPaths P, const int32_t* q_cur, const int32_t* count_cur,
                                                    int32_t* q_next, int32_t* count_next) {
     __shared__ int tmp[CP_NT / 64 + 1];
     __shared__ int base[5];
     const int count = *count_cur;
     const int b0 = blockIdx.x * CP_NT * CP_ITEMS;
-    if (b0 >= count) return;                       // whole block beyond the queue
-    uint8_t m[CP_ITEMS];
+    if (b0 >= count) return;
     int slots[CP_ITEMS];
+    const int n = load_items(q_cur, b0, count, slots);
+    uint8_t m[CP_ITEMS];
     int c[5] = {0, 0, 0, 0, 0};
 #pragma unroll
     for (int j = 0; j < CP_ITEMS; j++) {
-        int i = b0 + j * CP_NT + threadIdx.x;      // coalesced
-        slots[j] = i < count ? q_cur[i] : 0;
-        m[j] = i < count ? P.qmask[slots[j]] : 0;
+        m[j] = j < n ? P.qmask[slots[j]] : 0;
         c[0] += (m[j] & QM_CONT) ? 1 : 0;
         c[1] += m[j] & 1u;
         c[2] += (m[j] >> 1) & 1u;
@@ -1445,16 +1535,18 @@ DEV float pdf_emissive_hit(const DevScene& S, const ShadowLightHit& h, v3 d) {
 
 #include "restir_di.h"
 
+// over the bounce's hit queue (the shaded paths); count_paths: the bounce's path rays
 __global__ __launch_bounds__(TB) void k_resolve(DevScene S, DevPaths P, const MptFrame* __restrict__ Fp, int bounce,
-                                                const int32_t* q_cur, const int32_t* count_cur) {
+                                                const int32_t* q_cur, const int32_t* count_cur, const int32_t* count_paths) {
     const MptFrame& F = *Fp;
     const MptRenderSettings& rs = F.render_settings;
     int i = blockIdx.x * TB + threadIdx.x;
     if (i == 0) {
-        // always-on ray accounting: path rays + NEE any-hit + NEE closest of this bounce
-        P.ray_counts[0] += (uint64_t)*count_cur;
+        // always-on ray accounting: path rays + NEE any-hit + NEE closest of this bounce, path hits
+        P.ray_counts[0] += (uint64_t)*count_paths;
         P.ray_counts[1] += (uint64_t)P.counters[CTR_ANY];
         P.ray_counts[2] += (uint64_t)P.counters[CTR_CL];
+        P.ray_counts[3] += (uint64_t)*count_cur;
     }
     if (i >= *count_cur) return;
     int slot = q_cur[i];
@@ -1602,8 +1694,7 @@ DEV void accumulate_sample(const DevPaths& P, const MptRenderSettings& rs, int p
 __global__ __launch_bounds__(TB) void k_accumulate(DevPaths P, const MptFrame* __restrict__ Fp) {
     const int pixel = blockIdx.x * TB + threadIdx.x;
     if (pixel >= P.n_pix) return;
-    const int nsub = P.n / P.n_pix;
-    for (int sub = 0; sub < nsub; sub++) accumulate_sample(P, Fp[sub].render_settings, pixel, sub * P.n_pix + pixel);
+    for (int sub = 0; sub < P.batch; sub++) accumulate_sample(P, Fp[sub].render_settings, pixel, batch_slot(P, pixel, sub));
 }
 
 // ----------------------------------------------------------------------------------
@@ -1798,9 +1889,15 @@ hipError_t launch_frame(const DevScene& S, const DevPaths& P0, const MptFrame* d
         }
         hipMemsetAsync(&P.counters[c_next], 0, sizeof(int32_t), st);
         hipMemsetAsync(&P.counters[CTR_ANY], 0, 2 * sizeof(int32_t), st);
+        hipMemsetAsync(&P.counters[CTR_HIT], 0, 2 * sizeof(int32_t), st);
+        const dim3 cp_grid((n + CP_NT * CP_ITEMS - 1) / (CP_NT * CP_ITEMS));
+        {
+            TimedScope ts(cfg, st, KT_SPLIT);
+            hipLaunchKernelGGL(k_split, cp_grid, dim3(CP_NT), 0, st, P, q_cur, &P.counters[c_cur]);
+        }
         ShadeArgs sa;
         sa.S = S; sa.P = P; sa.F = d_frame; sa.bounce = b; sa.last_bounce = nb;
-        sa.q_cur = q_cur; sa.count_cur = &P.counters[c_cur]; sa.q_next = q_next; sa.count_next = &P.counters[c_next];
+        sa.q_cur = P.qh; sa.count_cur = &P.counters[CTR_HIT]; sa.q_next = q_next; sa.count_next = &P.counters[c_next];
         {
             TimedScope ts(cfg, st, KT_SHADE);
             if (hf.options.bsdf_override == MPT_BSDF_LAMBERTIAN)
@@ -1809,9 +1906,13 @@ hipError_t launch_frame(const DevScene& S, const DevPaths& P0, const MptFrame* d
                 hipLaunchKernelGGL((k_shade<MPT_BSDF_NONE>), dim3(blocks_for(n)), dim3(TB), 0, st, sa);
         }
         {
+            TimedScope ts(cfg, st, KT_MISS);
+            hipLaunchKernelGGL(k_miss, dim3(blocks_for(n)), dim3(TB), 0, st, S, P, d_frame, b);
+        }
+        {
             TimedScope ts(cfg, st, KT_COMPACT);
-            hipLaunchKernelGGL(k_compact, dim3((n + CP_NT * CP_ITEMS - 1) / (CP_NT * CP_ITEMS)), dim3(CP_NT), 0, st, P, q_cur,
-                               &P.counters[c_cur], q_next, &P.counters[c_next]);
+            hipLaunchKernelGGL(k_compact, cp_grid, dim3(CP_NT), 0, st, P, (const int32_t*)P.qh, &P.counters[CTR_HIT], q_next,
+                               &P.counters[c_next]);
         }
         // NEE queries
         hipMemsetAsync(&P.counters[CTR_FETCH], 0, sizeof(int32_t), st);
@@ -1824,7 +1925,8 @@ hipError_t launch_frame(const DevScene& S, const DevPaths& P0, const MptFrame* d
         timed_trace<TM_NEE_CLOSEST>(tn, cfg, st);
         {
             TimedScope ts(cfg, st, KT_RESOLVE);
-            hipLaunchKernelGGL(k_resolve, dim3(blocks_for(n)), dim3(TB), 0, st, S, P, d_frame, b, q_cur, &P.counters[c_cur]);
+            hipLaunchKernelGGL(k_resolve, dim3(blocks_for(n)), dim3(TB), 0, st, S, P, d_frame, b, (const int32_t*)P.qh,
+                               &P.counters[CTR_HIT], &P.counters[c_cur]);
         }
         // swap queues
         int32_t* tq = q_cur; q_cur = q_next; q_next = tq;

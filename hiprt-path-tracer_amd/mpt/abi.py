@@ -363,9 +363,14 @@ class Stats(C.Structure):
                 ("stage_launches", u32 * 3), ("shade_launches", u32), ("camera_ms", C.c_double),
                 ("shade_ms", C.c_double), ("resolve_ms", C.c_double), ("accumulate_ms", C.c_double),
                 ("compact_ms", C.c_double), ("restir_ms", C.c_double),
-                ("stage_node_slots", C.c_uint64 * 3), ("stage_tri_slots", C.c_uint64 * 3)]
+                ("stage_node_slots", C.c_uint64 * 3), ("stage_tri_slots", C.c_uint64 * 3),
+                ("path_hits", C.c_uint64), ("split_ms", C.c_double), ("miss_ms", C.c_double)]
 
 
+OK, ERR_INVALID_ARGUMENT, ERR_HIP, ERR_NO_SCENE, ERR_UNSUPPORTED, ERR_OUT_OF_MEMORY = 0, -1, -2, -3, -4, -5
+MAX_BATCH = 128
+DEFAULT_WAVEFRONT_PATHS = 1 << 25
+MAX_WAVEFRONT_PATHS = 1 << 29
 BSDF_NONE, BSDF_LAMBERTIAN = 0, 1
 (LSS_NO_DIRECT_LIGHT_SAMPLING, LSS_UNIFORM_ONE_LIGHT, LSS_BSDF, LSS_MIS_LIGHT_BSDF,
  LSS_RIS_BSDF_AND_LIGHT, LSS_RESTIR_DI) = range(6)

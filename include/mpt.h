@@ -420,6 +420,10 @@ typedef struct MptStats {
      * lane slots they occupied); stage_nodes / stage_node_slots = SIMD utilisation */
     uint64_t stage_node_slots[3];
     uint64_t stage_tri_slots[3];
+    /* path rays that hit a surface (shaded by the shade stage; the rest by the miss stage) */
+    uint64_t path_hits;
+    double split_ms;            /* hit / miss partition of the path queue */
+    double miss_ms;             /* miss shading (sky / envmap) */
 } MptStats;
 
 #define MPT_FB_COLOR 0        /* 'pixels': running SUM of samples (RenderData.h:34-36) */
@@ -513,10 +517,18 @@ int mpt_render_frame(MptContext* ctx, const MptFrame* frame);
  * camera_random_seed, denoiser_AOV_accumulation_counter, need_to_reset and
  * do_update_status_buffers, and need no per-sample feedback (no adaptive sampling or
  * stop-noise threshold, not ReSTIR DI), are traced as ONE wavefront of up to max_batch
- * (<= MPT_MAX_BATCH; <= 0: MPT_MAX_BATCH) samples per pixel; the result is bit-identical
+ * (<= MPT_MAX_BATCH; <= 0: see MPT_DEFAULT_WAVEFRONT_PATHS) samples per pixel; the result is bit-identical
  * to count mpt_render_frame calls (samples are added to the sums in order).  Other frames
  * are rendered one by one.  Asynchronous. */
 #define MPT_MAX_BATCH 128
+/* max_batch <= 0 picks the wavefront size: MPT_DEFAULT_WAVEFRONT_PATHS paths (samples x pixels of
+ * the partition) per launch, at most MPT_MAX_BATCH samples, and at most half of the device
+ * memory that is free or already held by the context's path state (~460 B per path, +332 B in
+ * textured scenes).  Whatever max_batch is, a wavefront whose path state cannot be allocated
+ * is halved (the result is bit-identical) before MPT_ERR_OUT_OF_MEMORY is returned. */
+#define MPT_DEFAULT_WAVEFRONT_PATHS (1 << 25)
+/* paths of one wavefront (and pixels of one frame) are limited to 2^29 */
+#define MPT_MAX_WAVEFRONT_PATHS (1 << 29)
 int mpt_render_frames(MptContext* ctx, const MptFrame* frames, int32_t count, int32_t max_batch);
 /* Installs the halo exchange of a partitioned ReSTIR DI context (see MptHaloExchange);
  * fn = NULL removes it.  Required before rendering LSS_RESTIR_DI with band_count > 1. */
