@@ -6,13 +6,15 @@
 // The whole library is compiled with -ffp-contract=off so that every product and
 // sum rounds separately, as on the reference's x86-64 CPU build; fused multiply-adds
 // are only written explicitly where bit-exactness with the reference does not matter
-// (BVH box tests).  Transcendentals go through the double-precision ocml functions and
-// are rounded once to float, which reproduces the CPU oracle bit-for-bit.
+// (BVH box tests).  Transcendentals are tmath.h's double-precision kernels rounded once to
+// float, the same code as the CPU oracle's.
 #ifndef MPT_DEV_MATH_H
 #define MPT_DEV_MATH_H
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include "tmath.h"
 
 #define DEV __device__ __forceinline__
 
@@ -52,13 +54,11 @@ DEV float pow3(float x) { return x * x * x; }
 DEV float pow4(float x) { float x2 = x * x; return x2 * x2; }
 DEV float pow6(float x) { float x2 = x * x; float x4 = x2 * x2; return x4 * x2; }
 
-// transcendentals: double ocml, rounded once.  Out of line (one copy each): inlined,
-// the f64 ocml bodies made k_shade 282 KB of code, far beyond the instruction cache.
-#ifdef MPT_TRANS_INLINE
-#define TRANS DEV
-#else
+// Transcendentals: tmath.h -- double-precision kernels rounded once to float, the same code
+// as the CPU oracle's.  MPT_TRANS_OCML (A/B experiments only) restores the previous
+// layer: the device library's double functions, out of line.
+#ifdef MPT_TRANS_OCML
 #define TRANS static __device__ __attribute__((noinline))
-#endif
 TRANS float psin(float x) { return (float)::sin((double)x); }
 TRANS float pcos(float x) { return (float)::cos((double)x); }
 TRANS float pexp(float x) { return (float)::exp((double)x); }
@@ -67,6 +67,23 @@ TRANS float ppow(float x, float y) { return (float)::pow((double)x, (double)y); 
 TRANS float patan2(float y, float x) { return (float)::atan2((double)y, (double)x); }
 TRANS float pasin(float x) { return (float)::asin((double)x); }
 TRANS float pacos(float x) { return (float)::acos((double)x); }
+#else
+// Out of line: inlined at their ~60 call sites they push k_shade from 272 to 1072 B of
+// scratch per lane and k_trace<PATH> (the sRGB pow of the alpha test) from 4 to 3 waves/SIMD.
+#ifdef MPT_TRANS_INLINE
+#define TRANS DEV
+#else
+#define TRANS static __device__ __attribute__((noinline))
+#endif
+TRANS float psin(float x) { return tmath::sinf_(x); }
+TRANS float pcos(float x) { return tmath::cosf_(x); }
+TRANS float pexp(float x) { return tmath::expf_(x); }
+TRANS float plog(float x) { return tmath::logf_(x); }
+TRANS float ppow(float x, float y) { return tmath::powf_(x, y); }
+TRANS float patan2(float y, float x) { return tmath::atan2f_(y, x); }
+TRANS float pasin(float x) { return tmath::asinf_(x); }
+TRANS float pacos(float x) { return tmath::acosf_(x); }
+#endif
 
 constexpr float PI = 3.14159265358979323846f;
 constexpr float TWO_PI = 6.28318530717958647693f;

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <deque>
@@ -68,7 +69,7 @@ constexpr int FRAME_RING = 256;   // >= 2 x MPT_MAX_BATCH
 // miss, compact, resolve) for up to 65 bounces (validate_frame), + camera, ReSTIR, accumulate
 constexpr int EV_POOL = 2 * (8 * 65 + 3);
 #ifndef MPT_TRACE_BLOCKS_PER_CU
-#define MPT_TRACE_BLOCKS_PER_CU 4
+#define MPT_TRACE_BLOCKS_PER_CU 5
 #endif
 constexpr int SPILL_WORDS = 2 * TRAV_SPILL_DEPTH;
 constexpr int MAX_STACK = TRAV_LDS_STACK + TRAV_SPILL_DEPTH;
@@ -1080,6 +1081,38 @@ int mpt_get_stats(MptContext* c, MptStats* out) {
     out->trace_launches = c->trace_launches;
     out->frames = c->frames;
     out->frame_ms = c->frame_ms;
+    return MPT_OK;
+}
+
+// GPUBakerKernel::bake_internal (GPUBakerKernel.cpp:98-113): launches of ipk samples per texel,
+// in float arithmetic as the reference computes them; nb_samples as each kernel derives it
+// (the GGX Fresnel kernel from cos_theta x roughness only, GGXFresnelDirectionalAlbedo.h:64-66)
+int mpt_bake_lut(MptContext* c, int kind, int32_t w, int32_t h, int32_t d, int32_t samples, float* out, int dev) {
+    if (!c || !out) return fail(MPT_ERR_INVALID_ARGUMENT, "NULL argument");
+    if (kind < MPT_BAKE_GGX_CONDUCTOR || kind > MPT_BAKE_GGX_THIN_GLASS) return fail(MPT_ERR_INVALID_ARGUMENT, "bad LUT kind");
+    if (w < 2 || h < 2 || d < 1 || (kind != MPT_BAKE_GGX_CONDUCTOR && d < 2) || (kind == MPT_BAKE_GGX_CONDUCTOR && d != 1) ||
+        samples < 1 || (int64_t)w * h * d > (1 << 28))
+        return fail(MPT_ERR_INVALID_ARGUMENT, "bad LUT size or sample count");
+    HIPCHK(hipSetDevice(c->device));
+    const float elems = 100000000.0f;   // GPUBakerConstants::COMPUTE_ELEMENT_PER_BAKE_KERNEL_LAUNCH
+    const int texels = w * h * d;
+    const int ipk = (int)std::floor(std::max(1.0f, elems / (float)texels));
+    const int launches = (int)std::ceil((float)samples / (float)ipk);
+    int nb = launches * ipk;
+    if (kind == MPT_BAKE_GGX_FRESNEL) {
+        const int ipk2 = (int)std::floor(std::max(1.0f, elems / (float)(w * h)));
+        nb = (int)std::ceil((float)samples / (float)ipk2) * ipk2;
+    }
+    DBuf<float> buf;
+    Allocs A;
+    A(buf, (size_t)texels);
+    if (A.e == hipSuccess) A(hipMemsetAsync(buf.p, 0, (size_t)texels * sizeof(float), c->stream));
+    for (int i = 0; i < launches && A.e == hipSuccess; i++) A(launch_bake(kind, w, h, d, ipk, nb, i + 1, buf.p, c->stream));
+    if (A.e == hipSuccess)
+        A(hipMemcpyAsync(out, buf.p, (size_t)texels * sizeof(float), dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost,
+                         c->stream));
+    if (A.e == hipSuccess) A(hipStreamSynchronize(c->stream));
+    if (A.e != hipSuccess) return alloc_fail(A.e, "LUT bake");
     return MPT_OK;
 }
 

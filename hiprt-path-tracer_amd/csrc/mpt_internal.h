@@ -197,6 +197,7 @@ hipError_t launch_resolve_materials(const DevScene& S, MptMaterial* out_res, int
                                    hipStream_t st);
 hipError_t launch_restir_fill(float4* reservoirs, int n, hipStream_t st);
 hipError_t launch_restir_fill_lights(float4* lights, int n, hipStream_t st);
+hipError_t launch_bake(int kind, int w, int h, int d, int ipk, int nb_samples, int iteration, float* out, hipStream_t st);
 hipError_t launch_trace_raw(const DevScene& S, const float4* o, const float4* d, int n, bool any, float4* out_hit,
                             uint8_t* out_occ, int32_t* fetch_ctr, uint32_t* spill, int grid, hipStream_t st);
 

@@ -313,7 +313,7 @@ DEV uint32_t camera_seed(const MptFrame& F, uint32_t pix);
 DEV uint32_t path_seed(const MptFrame* Fp, const DevPaths& P, int slot, bool camera);
 
 #ifndef MPT_TRACE_WAVES
-#define MPT_TRACE_WAVES 1
+#define MPT_TRACE_WAVES 5   // 5 waves / SIMD (<= 96 VGPRs): C3 traversal -4 % vs 4 (VGPR-capped), 6 and 8 no better (r02 A/B)
 #endif
 #ifndef MPT_TRACE_WAVES_PATH
 #define MPT_TRACE_WAVES_PATH MPT_TRACE_WAVES

@@ -29,6 +29,7 @@ SYMBOLS = [
     "mpt_render_frame", "mpt_render_frames", "mpt_synchronize", "mpt_query_done", "mpt_get_framebuffer", "mpt_partition_rows",
     "mpt_enable_stats", "mpt_get_stats", "mpt_trace_closest", "mpt_trace_any", "mpt_clear_status",
     "mpt_query_status", "mpt_get_aux_buffer", "mpt_build_envmap_cdf", "mpt_set_envmap_cdf", "mpt_set_halo_exchange",
+    "mpt_bake_lut",
 ]
 
 
@@ -86,6 +87,7 @@ def lib() -> C.CDLL:
     L.mpt_query_status.argtypes = [vp, C.POINTER(abi.Status)]
     L.mpt_get_aux_buffer.argtypes = [vp, C.c_int, vp, C.c_int]
     L.mpt_set_halo_exchange.argtypes = [vp, abi.HaloExchangeFn, vp]
+    L.mpt_bake_lut.argtypes = [vp, C.c_int, i32, i32, i32, i32, vp, C.c_int]
     _lib = L
     return L
 
@@ -281,6 +283,14 @@ class GPURenderer:
         lh = None if last_hit is None else np.ascontiguousarray(last_hit, np.int32)
         _check(lib().mpt_trace_any(self.h, _p(rays), _p(lh), n, _p(occ), 0))
         return occ.astype(bool)
+
+    # --- LUT baker (GPUBaker, Renderer/Baker/GPUBaker.cpp:35-97) -------------------------
+    def bake_lut(self, kind, width, height, depth=1, samples=65536):
+        """abi.BAKE_* table -> float32 [depth, height, width], rows as the reference's baker
+        writes them (the renderer's LUTs are each slice flipped: out[:, ::-1])."""
+        out = np.zeros((depth, height, width), np.float32)
+        _check(lib().mpt_bake_lut(self.h, kind, width, height, depth, samples, _p(out), 0))
+        return out
 
     def close(self):
         if getattr(self, "h", None):

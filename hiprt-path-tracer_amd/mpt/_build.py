@@ -19,7 +19,7 @@ INCLUDE = ROOT.parent / "include"
 LIB_PATH = PKG_DIR / "libmpt.so"
 OBJ_DIR = CSRC / "build"
 
-SOURCES = ["bvh8.cpp", "mpt_kernels.hip", "mpt_api.cpp"]
+SOURCES = ["bvh8.cpp", "mpt_kernels.hip", "bake.hip", "mpt_api.cpp"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 CXXFLAGS = [

@@ -372,6 +372,8 @@ MAX_BATCH = 128
 DEFAULT_WAVEFRONT_PATHS = 1 << 25
 MAX_WAVEFRONT_PATHS = 1 << 29
 BSDF_NONE, BSDF_LAMBERTIAN = 0, 1
+(BAKE_GGX_CONDUCTOR, BAKE_GGX_FRESNEL, BAKE_GLOSSY_DIELECTRIC, BAKE_GGX_GLASS, BAKE_GGX_GLASS_INVERSE,
+ BAKE_GGX_THIN_GLASS) = range(6)
 (LSS_NO_DIRECT_LIGHT_SAMPLING, LSS_UNIFORM_ONE_LIGHT, LSS_BSDF, LSS_MIS_LIGHT_BSDF,
  LSS_RIS_BSDF_AND_LIGHT, LSS_RESTIR_DI) = range(6)
 ESS_NO_SAMPLING, ESS_BINARY_SEARCH, ESS_ALIAS_TABLE = range(3)

@@ -27,6 +27,8 @@
  *                                    (GPURenderer.h:193-197, RenderData.h:32-36)
  *   mpt_trace_closest / mpt_trace_any <- hiprtGeomTraversalClosest/AnyHit as called by
  *                                    trace_ray / evaluate_shadow_ray (Device/includes/Intersect.h:114-286)
+ *   mpt_bake_lut                  <- GPUBaker::bake_* (Renderer/Baker/GPUBaker.cpp:35-97) and the
+ *                                    Device/kernels/Baking/ headers kernels
  *
  * Conventions: every function returns MPT_OK (0) or a negative error code; the
  * message of the last error of the calling thread is in mpt_last_error().  The
@@ -548,6 +550,26 @@ int mpt_query_status(MptContext* ctx, MptStatus* out);
 int mpt_get_aux_buffer(MptContext* ctx, int kind, void* dst, int dst_is_device);
 int mpt_enable_stats(MptContext* ctx, int enable, int instrumented);
 int mpt_get_stats(MptContext* ctx, MptStats* out);
+/* Energy-compensation LUT baker, GPUBaker::bake_* (Renderer/Baker/GPUBaker.cpp:35-97,
+ * GPUBakerKernel.cpp:22-151, Device/kernels/Baking/ headers): Monte-Carlo directional albedo of
+ * a GGX lobe per texel, x = cos(theta_o) fastest, then y = roughness, then z = IOR (F0^4
+ * parameterisation), with the reference's launch structure and seeds (so the table is
+ * deterministic), integration_sample_count samples per texel.  The output is the baked
+ * buffer as the reference writes it to its .hdr files (rows not flipped; the renderer's
+ * MptLuts hold each slice flipped vertically, as read_image_hdr(flipY=true) loads them).
+ * Reference sizes / sample counts (GPUBakerConstants.h:15-32, *Settings.h):
+ *   GGX_CONDUCTOR       128 x 128 x 1,  65536        GGX_FRESNEL 256 x 256 x 256, 65536
+ *   GLOSSY_DIELECTRIC   128 x 64 x 128, 131072       GGX_GLASS(_INVERSE) 256 x 16 x 128, 65536
+ *   GGX_THIN_GLASS      32 x 32 x 96,   65536
+ * Synchronous; out may be host or device memory. */
+#define MPT_BAKE_GGX_CONDUCTOR 0
+#define MPT_BAKE_GGX_FRESNEL 1
+#define MPT_BAKE_GLOSSY_DIELECTRIC 2
+#define MPT_BAKE_GGX_GLASS 3
+#define MPT_BAKE_GGX_GLASS_INVERSE 4
+#define MPT_BAKE_GGX_THIN_GLASS 5
+int mpt_bake_lut(MptContext* ctx, int kind, int32_t width, int32_t height, int32_t depth, int32_t sample_count,
+                 float* out, int out_is_device);
 /* Raw ray queries against the uploaded BVH8 (parity / microbenchmarks).
  * rays: n * 8 floats (ox, oy, oz, tmin_unused, dx, dy, dz, tmax); last_hit: n ints (-1 = none).
  * Outputs (may be NULL): prim (n ints, -1 on miss), t, u, v (n floats).  Host or device pointers. */

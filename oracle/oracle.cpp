@@ -35,6 +35,7 @@
  * white-furnace energy check (BSDFsData.h:26).
  */
 #include <algorithm>
+#include <cmath>
 #include <cfloat>
 #include <cstdio>
 #include <cstring>
@@ -1445,10 +1446,160 @@ int oracle_directional_albedo(const MptMaterial* mat, const MptMaterial* all_mat
     return 0;
 }
 
+// ---------------------------------------------------------------------------------------------
+// LUT baker: GPUBaker::bake_* (Renderer/Baker/GPUBaker.cpp:35-97) with the launch loop of
+// GPUBakerKernel::bake_internal (GPUBakerKernel.cpp:98-113) and the kernels of
+// Device/kernels/Baking/ (GGXConductorDirectionalAlbedo.h, GGXFresnelDirectionalAlbedo.h,
+// GlossyDielectricDirectionalAlbedo.h, GGXGlassDirectionalAlbedo.h, GGXThinGlassDirectionalAlbedo.h).
+// kind: 0 conductor, 1 GGX Fresnel, 2 glossy dielectric, 3 glass, 4 glass (inverse IOR), 5 thin glass
+// ---------------------------------------------------------------------------------------------
+static f3 bake_glass_dir(bool thin, float rel, float r, f3 V, Rng& rng) {   // GGX_glass_E_sample / thin_glass_sample
+    if (absf(rel - 1.0f) < 1.0e-5f) rel = 1.0f + 1.0e-5f;
+    float ax, ay;
+    get_alphas(r, 0.0f, ax, ay);
+    f3 m = GGX_VNDF_sample(V, ax, ay, rng);
+    float F = full_fresnel_dielectric(dot(V, m), rel);
+    if (thin && r < 0.1f) F += sq(1.0f - F) * F / (1.0f - sq(F));   // thin slab inter-reflections
+    if (rng() < F) return reflect_ray(V, m);
+    if (dot(m, V) < 0.0f) m = -m;
+    if (thin) { f3 o = reflect_ray(V, m); o.z = -o.z; return o; }
+    f3 o = mk3(0.0f, 0.0f, 0.0f);
+    refract_ray(V, m, o, rel);
+    return o;
+}
+static float bake_glass_value(const BsdfCtx& bc, bool thin, float rel, float r, f3 V, f3 L, float& pdf) {   // *_eval
+    pdf = 0.0f;
+    if (absf(L.z) < 1.0e-8f) return 0.0f;
+    const bool reflection = L.z * V.z > 0;
+    if (absf(rel - 1.0f) < 1.0e-5f) rel = 1.0f + 1.0e-5f;
+    f3 H = reflection ? L + V : (thin ? mk3(L.x, L.y, -L.z) + V : L * rel + V);
+    H = normalize(H);
+    if (H.z < 0.0f) H = -H;
+    const float HoL = dot(L, H), HoV = dot(V, H);
+    if (HoL * L.z < 0.0f || HoV * V.z < 0.0f) return 0.0f;
+    float F = full_fresnel_dielectric(HoV, rel);
+    if (thin && r < 0.1f) F += sq(1.0f - F) * F / (1.0f - sq(F));
+    if (reflection) {
+        const float v = torrance_sparrow0(bc, r, 0.0f, Col(F), V, L, H, pdf).r;
+        pdf *= F;
+        return v;
+    }
+    float ax, ay;
+    get_alphas(r, 0.0f, ax, ay);
+    const float dp = HoL + HoV / rel, dp2 = dp * dp;
+    const float D = GGX_anisotropic(ax, ay, H);
+    const float g1v = G1_Smith(ax, ay, V), g1l = G1_Smith(ax, ay, L);
+    pdf = absf(HoL) / dp2 * (g1v / absf(V.z) * D * absf(HoV));
+    pdf *= 1.0f - F;
+    return D * (1.0f - F) * (g1v * g1l) * absf(HoL * HoV / (dp2 * L.z * V.z));
+}
+static float bake_sample(const BsdfCtx& bc, int kind, float rel, float r, f3 V, Rng& rng, bool& keep) {
+    keep = false;
+    if (kind <= 1) {   // conductor / GGX Fresnel: GGX-reflection sampling, F = 1 or dielectric(N.L)
+        f3 L = ggx_sample_reflection(r, 0.0f, V, rng);
+        if (L.z < 0) return 0.0f;
+        float pdf;
+        float a = torrance_sparrow0(bc, r, 0.0f, Col(kind == 1 ? full_fresnel_dielectric(L.z, rel) : 1.0f), V, L,
+                                    normalize(V + L), pdf).r;
+        keep = true;
+        return a / pdf * L.z;
+    }
+    if (kind == 2) {   // glossy dielectric: half GGX reflection, half cosine, one-sample MIS over the two lobes
+        const float lobe = rng();
+        f3 L;
+        if (lobe < 0.5f) {
+            L = ggx_sample_reflection(r, 0.0f, V, rng);
+            if (L.z < 0) return 0.0f;
+        } else {
+            L = cosine_weighted_sample_z_up_frame(rng);
+        }
+        const f3 H = normalize(V + L);
+        float ps;
+        const float spec = torrance_sparrow0(bc, r, 0.0f, Col(full_fresnel_dielectric(dot(H, L), rel)), V, L, H, ps).r;
+        float total = ps * 0.5f;
+        const float layer = (1.0f - full_fresnel_dielectric(L.z, rel)) * (1.0f - full_fresnel_dielectric(V.z, rel));
+        float pd = 0.0f, diff = 0.0f;
+        if (L.z > 0.0f) { pd = L.z * INV_PI; diff = INV_PI; }
+        total += pd * 0.5f;
+        keep = true;
+        return (spec + diff * layer) * L.z / total;
+    }
+    const bool thin = kind == 5;
+    const float rr = thin ? thin_walled_roughness(true, r, rel) : r;
+    const f3 L = bake_glass_dir(thin, rel, rr, V, rng);
+    float pdf;
+    const float a = bake_glass_value(bc, thin, rel, rr, V, L, pdf);
+    if (pdf == 0.0f) return 0.0f;
+    keep = true;
+    return a / pdf * absf(L.z);
+}
+// out[z][y][x] (w*h*d floats): the table as the reference writes it (rows not flipped)
+int oracle_bake(int kind, int w, int h, int d, int samples, float* out) {
+    if (kind < 0 || kind > 5 || w < 2 || h < 2 || d < 1 || samples < 1) return -1;
+    const float elems = 100000000.0f;   // COMPUTE_ELEMENT_PER_BAKE_KERNEL_LAUNCH
+    const int texels = w * h * d;
+    const int ipk = (int)std::floor(std::max(1.0f, elems / (float)texels));
+    const int launches = (int)std::ceil((float)samples / (float)ipk);
+    int nb = launches * ipk;
+    if (kind == 1) {   // the GGX Fresnel kernel derives its sample count from cos_theta x roughness
+        const int ipk2 = (int)std::floor(std::max(1.0f, elems / (float)(w * h)));
+        nb = (int)std::ceil((float)samples / (float)ipk2) * ipk2;
+    }
+    BsdfCtx bc{};
+    bc.ggx_masking = 0;
+#pragma omp parallel for schedule(dynamic, 64)
+    for (int idx = 0; idx < texels; idx++) {
+        const int x = idx % w, y = (idx / w) % h, z = idx / (w * h);
+        float ct = fmaxr(1.0e-3f, 1.0f / (float)(w - 1) * (float)x);
+        if (kind != 0 && kind != 5) ct = ppow(ct, 2.5f);
+        const float st = psin(pacos(ct));
+        const f3 V = normalize(mk3(pcos(0.0f) * st, psin(0.0f) * st, ct));
+        const float r = fmaxr(1.0f / (float)(h - 1) * (float)y, 1.0e-4f);
+        float rel = 1.0f;
+        if (kind != 0) {
+            float F0 = 1.0f / (float)(d - 1) * (float)z;
+            F0 = F0 * F0 * F0 * F0;
+            const float s = psqrt(clampf(0.0f, 0.99f, F0));
+            rel = (1.0f + s) / (1.0f - s);
+            if (kind == 4) rel = 1.0f / rel;
+        }
+        float acc = 0.0f;
+        for (int it = 1; it <= launches; it++) {
+            Rng rng(wang_hash((uint32_t)idx + 1u) * (uint32_t)it);
+            for (int k = 0; k < ipk; k++) {
+                bool keep;
+                const float a = bake_sample(bc, kind, rel, r, V, rng, keep);
+                if (keep) acc += a / (float)nb;
+            }
+        }
+        out[idx] = acc;
+    }
+    return 0;
+}
+
 uint32_t oracle_wang_hash(uint32_t s) { return wang_hash(s); }
 void oracle_xorshift(uint32_t seed, int n, uint32_t* out_u, float* out_f) {
     Rng a(seed), b(seed);
     for (int i = 0; i < n; i++) { out_u[i] = a.xorshift32(); out_f[i] = b(); }
+}
+
+// the parity transcendentals (tmath.h) on host arrays: fn 0 sin 1 cos 2 exp 3 log 4 pow
+// 5 atan2 (a = y, b = x) 6 asin 7 acos -- the numbering of libmpt's mpt_debug_math
+void oracle_tmath(int fn, const float* a, const float* b, float* out, int n) {
+    for (int i = 0; i < n; i++) {
+        float x = a[i], y = b[i], r;
+        switch (fn) {
+            case 0: r = psin(x); break;
+            case 1: r = pcos(x); break;
+            case 2: r = pexp(x); break;
+            case 3: r = plog(x); break;
+            case 4: r = ppow(x, y); break;
+            case 5: r = patan2(x, y); break;
+            case 6: r = pasin(x); break;
+            default: r = pacos(x); break;
+        }
+        out[i] = r;
+    }
 }
 
 }  // extern "C"

@@ -21,7 +21,8 @@ LIB_PATH = os.path.join(HERE, "liboracle.so")
 
 def build(force=False):
     srcs = [os.path.join(HERE, f) for f in ("oracle.cpp", "oracle_math.h", "oracle_bsdf.h", "oracle_restir.h", "Makefile",
-                                            os.path.join("..", "include", "mpt.h"))]
+                                            os.path.join("..", "include", "mpt.h"),
+                                            os.path.join("..", "hiprt-path-tracer_amd", "csrc", "tmath.h"))]
     stale = os.path.exists(LIB_PATH) and any(os.path.getmtime(f) > os.path.getmtime(LIB_PATH) for f in srcs
                                              if os.path.exists(f))
     if force or stale or not os.path.exists(LIB_PATH):
@@ -56,6 +57,8 @@ def lib():
         L.oracle_wang_hash.restype = C.c_uint32
         L.oracle_wang_hash.argtypes = [C.c_uint32]
         L.oracle_xorshift.argtypes = [C.c_uint32, C.c_int, C.c_void_p, C.c_void_p]
+        L.oracle_tmath.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
+        L.oracle_bake.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p]
         _lib = L
     return _lib
 
@@ -166,3 +169,11 @@ def xorshift(seed, n):
 
 def wang_hash(s):
     return lib().oracle_wang_hash(s)
+
+
+def bake(kind, width, height, depth=1, samples=65536):
+    """oracle_bake: the reference baker's table (GPUBaker.cpp:35-97) as float32 [depth, height, width]."""
+    out = np.zeros((depth, height, width), np.float32)
+    if lib().oracle_bake(kind, width, height, depth, samples, _p(out)) != 0:
+        raise ValueError("bad bake arguments")
+    return out
