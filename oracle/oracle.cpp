@@ -1558,7 +1558,8 @@ int oracle_bake(int kind, int w, int h, int d, int samples, float* out) {
         float rel = 1.0f;
         if (kind != 0) {
             float F0 = 1.0f / (float)(d - 1) * (float)z;
-            F0 = F0 * F0 * F0 * F0;
+            F0 *= F0;   // F0^2
+            F0 *= F0;   // F0^4 (squared twice, not F0*F0*F0*F0: the rounding differs)
             const float s = psqrt(clampf(0.0f, 0.99f, F0));
             rel = (1.0f + s) / (1.0f - s);
             if (kind == 4) rel = 1.0f / rel;
