@@ -95,12 +95,6 @@ struct Builder {
     }
 };
 
-inline float scene_box_pad(const float* vertices, int num_triangles, const int32_t* indices) {
-    float m = 0.0f;
-    for (size_t k = 0; k < 3 * (size_t)num_triangles; k++)
-        for (int i = 0; i < 3; i++) m = std::max(m, std::fabs(vertices[3 * (size_t)indices[k] + i]));
-    return std::ldexp(std::max(m, 1.0f), -20);
-}
 
 inline uint8_t quant_exp(float ext) {
     // smallest e with 255 * 2^e >= ext, clamped to normal floats
@@ -115,7 +109,15 @@ inline uint8_t quant_exp(float ext) {
 
 }  // namespace
 
-void build_bvh8(const float* vertices, const int32_t* indices, int32_t num_triangles, BVH8& out, int max_leaf) {
+float scene_box_pad(const float* vertices, int num_triangles, const int32_t* indices) {
+    float m = 0.0f;
+    for (size_t k = 0; k < 3 * (size_t)num_triangles; k++)
+        for (int i = 0; i < 3; i++) m = std::max(m, std::fabs(vertices[3 * (size_t)indices[k] + i]));
+    return std::ldexp(std::max(m, 1.0f), -20);
+}
+
+void build_bvh8(const float* vertices, const int32_t* indices, int32_t num_triangles, BVH8& out, int max_leaf,
+                float pad_in) {
     out.nodes.clear();
     out.tris.clear();
     if (num_triangles <= 0) return;
@@ -138,7 +140,7 @@ void build_bvh8(const float* vertices, const int32_t* indices, int32_t num_trian
     // ray grazing along a wall that holds an edge of the triangle), so unpadded boxes can
     // cull a triangle the test would accept.  With the pad, box culling never changes a
     // result: traversal equals brute force (the oracle pads its boxes the same way).
-    const float pad = scene_box_pad(vertices, num_triangles, indices);
+    const float pad = pad_in >= 0.0f ? pad_in : scene_box_pad(vertices, num_triangles, indices);
     for (int t = 0; t < num_triangles; t++)
         for (int i = 0; i < 3; i++) { b.tbox[t].lo[i] -= pad; b.tbox[t].hi[i] += pad; }
     b.nodes.reserve(2 * (size_t)num_triangles);

@@ -44,7 +44,11 @@ struct BVH8 {
 };
 
 // Builds the BVH8 over indexed triangles.  max_leaf: triangles per leaf child (<= 4).
-void build_bvh8(const float* vertices, const int32_t* indices, int32_t num_triangles, BVH8& out, int max_leaf = 3);
+// pad: triangle-box padding (< 0: 2^-20 of the largest coordinate of these triangles; a
+// BVH over a subset of a scene passes the whole scene's pad, scene_box_pad).
+void build_bvh8(const float* vertices, const int32_t* indices, int32_t num_triangles, BVH8& out, int max_leaf = 3,
+                float pad = -1.0f);
+float scene_box_pad(const float* vertices, int num_triangles, const int32_t* indices);
 
 }  // namespace mpt
 

@@ -488,11 +488,15 @@ DEV float thin_walled_roughness(bool thin, float r, float eta) {
     float rem = r * sqrtf(3.7f * (eta - 1.0f) * sq(eta - 0.5f) / pow3(eta));
     return clampr(0.0f, 1.0f, rem / 1.39f);
 }
+// FULL = false: the material is of the plain-dielectric class (MC_PLAIN below: no coat,
+// sheen, metal, transmission or thin film), so the lobes and terms that are exactly zero for
+// it are not compiled in.  Same result as FULL = true for such a material, bit for bit.
+template <bool FULL = true>
 DEV Col spec_fresnel(const Mat& m, float rel, float ci) {
     float above = m.ior / rel;
     Col Fs = col(0.0f), Ft = col(0.0f);
     if (m.thin_film < 1.0f) Fs = col(fresnel_dielectric(ci, rel));
-    if (m.thin_film > 0.0f) Ft = thin_film_fresnel(m, above, ci);
+    if (FULL && m.thin_film > 0.0f) Ft = thin_film_fresnel(m, above, ci);
     return lerpc(Fs, Ft, m.thin_film);
 }
 DEV float ior_or_air(const BCtx& c, int idx) { return idx == MAX_MAT ? 1.0f : c.mats[idx].ior; }
@@ -629,6 +633,7 @@ struct PEval {
     float gbc, ccc;
 };
 
+template <bool FULL = true>
 DEV void principled_eval_pre(const BCtx& c, const Mat& m, const VState& vs, v3 view, v3 sn, PEval& e) {
     v3 n = sn;
     e.outside = dot(view, n) > 0 || m.thin_walled;
@@ -644,7 +649,7 @@ DEV void principled_eval_pre(const BCtx& c, const Mat& m, const VState& vs, v3 v
     // coat, view side (entered when the coat has weight or the light refracts, which
     // needs 'outside')
     e.coat_vdf = 0.0f; e.coat_oa = 0.0f; e.coat_dark = col(1.0f);
-    if (e.w[0] > 0.0f || e.outside) {
+    if (FULL && (e.w[0] > 0.0f || e.outside)) {
         e.coat_vdf = fresnel_dielectric(absr(e.lv.z), e.inc, m.coat_ior);
         if (!is_white(C3(m.coat_medium_absorption)))
             e.coat_oa = maxr(1.0e-6f, sqrtf(1.0f - (1.0f - e.lv.z * e.lv.z) / (m.coat_ior * m.coat_ior)));
@@ -658,7 +663,7 @@ DEV void principled_eval_pre(const BCtx& c, const Mat& m, const VState& vs, v3 v
         e.spec_ok = absr(e.rel - 1.0f) > 1.0e-3f;
         if (e.spec_ok) {
             e.spec_tint = lerpc(col(1.0f), m.specular_tint * C3(m.specular_color), m.specular);
-            e.spec_vdf = spec_fresnel(m, e.rel, e.lvr.z);
+            e.spec_vdf = spec_fresnel<FULL>(m, e.rel, e.lvr.z);
             e.spec_dark = spec_darkening(m, e.rel);
         }
     }
@@ -666,6 +671,12 @@ DEV void principled_eval_pre(const BCtx& c, const Mat& m, const VState& vs, v3 v
     e.ccc = c.clearcoat_comp ? clearcoat_comp(c, m, e.inc, e.lv.z) : 1.0f;
 }
 
+// A plain-dielectric material (FULL = false) has zero coat / sheen / metal weights and,
+// seen from outside (the only way k_shade evaluates it, see MC_PLAIN), zero glass weight:
+// the generic code skips those lobes too, except the coat block on a refracting direction,
+// which then only scales the throughput of lobes that are all skipped (nr = 0, w[6] = 0),
+// and adds cp * p[0] = 0 to the pdf and a zero colour to fc -- no effect on the result.
+template <bool FULL = true>
 DEV Col principled_eval_post(const BCtx& c, const Mat& m, VState& vs, const PEval& e, v3 sn, v3 L, float& pdf) {
     pdf = 0.0f;
     const bool refracting = dot(sn, L) < 0.0f && e.outside;
@@ -679,7 +690,7 @@ DEV Col principled_eval_post(const BCtx& c, const Mat& m, VState& vs, const PEva
     Col thr = col(1.0f), fc = col(0.0f);
     float nr = refracting ? 0.0f : 1.0f;
     // coat (Principled.h:493-593)
-    if (e.w[0] > 0.0f || refracting) {
+    if (FULL && (e.w[0] > 0.0f || refracting)) {
         float cp = 0.0f;
         Col ct = col(0.0f);
         if (!refracting) {
@@ -703,7 +714,7 @@ DEV Col principled_eval_post(const BCtx& c, const Mat& m, VState& vs, const PEva
         fc += ct;
     }
     // sheen
-    if (e.w[1] > 0.0f) {
+    if (FULL && e.w[1] > 0.0f) {
         float refl, sp;
         Col ct = sheen_eval(c, m, ll, lv, sp, refl);
         ct *= e.w[1];
@@ -716,7 +727,7 @@ DEV Col principled_eval_post(const BCtx& c, const Mat& m, VState& vs, const PEva
 #pragma unroll
     for (int k = 0; k < 2; k++) {
         float wk = e.w[2 + k] * nr;
-        if (wk > 0.0f) {
+        if (FULL && wk > 0.0f) {
             float mp;
             float HoL = clampr(1.0e-8f, 1.0f, dot(lhr, llr));
             Col Fm = f82_tint(C3(m.base_color), C3(m.metallic_F82), C3(m.metallic_F90), m.metallic_F90_falloff_exponent, HoL);
@@ -729,7 +740,7 @@ DEV Col principled_eval_post(const BCtx& c, const Mat& m, VState& vs, const PEva
         }
     }
     // glass
-    if (e.w[6] > 0.0f) {
+    if (FULL && e.w[6] > 0.0f) {
         float gp;
         Col ct = glass_eval(c, m, vs, lvr, llr, gp);
         ct *= e.w[6];
@@ -743,13 +754,13 @@ DEV Col principled_eval_post(const BCtx& c, const Mat& m, VState& vs, const PEva
         float ws = e.w[4] * nr;
         if (ws > 0.0f) {
             float sp;
-            Col ct = ts_ggx0(c, m.roughness, m.anisotropy, spec_fresnel(m, e.rel, dot(llr, lhr)), lvr, llr, lhr, sp);
+            Col ct = ts_ggx0(c, m.roughness, m.anisotropy, spec_fresnel<FULL>(m, e.rel, dot(llr, lhr)), lvr, llr, lhr, sp);
             if (e.spec_ok) {
                 ct *= e.spec_tint;
                 ct *= ws;
                 ct *= thr;
                 Col att = col(1.0f);
-                att *= col(1.0f) - spec_fresnel(m, e.rel, llr.z);
+                att *= col(1.0f) - spec_fresnel<FULL>(m, e.rel, llr.z);
                 att *= col(1.0f) - e.spec_vdf;
                 att *= e.spec_dark;
                 att = lerpc(col(1.0f), att, m.specular);
@@ -782,6 +793,10 @@ DEV Col principled_eval(const BCtx& c, const Mat& m, VState& vs, v3 view, v3 n, 
 // Direction half of PrincipledBSDF sampling (Principled.h:1050-1120): picks a lobe, samples
 // it, updates the nested-dielectric state.  Returns false where the reference returns a
 // zero BSDF without evaluating it (direction below the surface for a non-glass lobe).
+// FULL = false (plain dielectric): p[0] = p[1] = 0, so r1 < c0 and r1 < c1 never hold (r1 >= 0)
+// and the coat / sheen samplers are not compiled in; the glass branch stays (r1 > c5 can
+// hold by rounding when p[6] = 0).
+template <bool FULL = true>
 DEV bool principled_sample_dir(const BCtx& c, const Mat& m, VState& vs, v3 view, v3 sn, v3 gn, v3& out, Rng& rng) {
     v3 n = sn;
     bool outside = dot(view, n) > 0 || m.thin_walled;
@@ -803,11 +818,11 @@ DEV bool principled_sample_dir(const BCtx& c, const Mat& m, VState& vs, v3 view,
     v3 TR, BR;
     build_rotated_onb(n, TR, BR, m.anisotropy_rotation * PI);
     v3 lvr = to_local(TR, BR, n, view);
-    if (r1 < c0) {
+    if (FULL && r1 < c0) {
         v3 TC, BC;
         build_rotated_onb(n, TC, BC, m.coat_anisotropy_rotation * PI);
         out = to_world(TC, BC, n, ggx_sample_reflection(m.coat_roughness, m.coat_anisotropy, to_local(TC, BC, n, view), rng));
-    } else if (r1 < c1) {
+    } else if (FULL && r1 < c1) {
         v3 T, B;
         build_onb(n, T, B);
         out = to_world(T, B, n, sheen_sample(c, m, to_local(T, B, n, view), rng));
@@ -835,20 +850,20 @@ DEV Col bsdf_eval(const BCtx& c, const Mat& m, VState& vs, v3 view, v3 sn, v3 L,
     return principled_eval(c, m, vs, view, sn, L, pdf);
 }
 // evaluation split into a per-vertex part and a per-light-direction part (see PEval)
-template <int OVERRIDE>
+template <int OVERRIDE, bool FULL = true>
 DEV void bsdf_eval_pre(const BCtx& c, const Mat& m, const VState& vs, v3 view, v3 sn, PEval& e) {
-    if (OVERRIDE != MPT_BSDF_LAMBERTIAN) principled_eval_pre(c, m, vs, view, sn, e);
+    if (OVERRIDE != MPT_BSDF_LAMBERTIAN) principled_eval_pre<FULL>(c, m, vs, view, sn, e);
 }
-template <int OVERRIDE>
+template <int OVERRIDE, bool FULL = true>
 DEV Col bsdf_eval_post(const BCtx& c, const Mat& m, VState& vs, const PEval& e, v3 sn, v3 L, float& pdf) {
     if (OVERRIDE == MPT_BSDF_LAMBERTIAN) return lambert_eval(m, dot(L, sn), pdf);
-    return principled_eval_post(c, m, vs, e, sn, L, pdf);
+    return principled_eval_post<FULL>(c, m, vs, e, sn, L, pdf);
 }
 // sample = sample_dir + bsdf_eval on the updated state (eval skipped when sample_dir is false)
-template <int OVERRIDE>
+template <int OVERRIDE, bool FULL = true>
 DEV bool bsdf_sample_dir(const BCtx& c, const Mat& m, VState& vs, v3 view, v3 sn, v3 gn, v3& dir, Rng& rng) {
     if (OVERRIDE == MPT_BSDF_LAMBERTIAN) { dir = cosine_sample_around(sn, rng); return true; }
-    return principled_sample_dir(c, m, vs, view, sn, gn, dir, rng);
+    return principled_sample_dir<FULL>(c, m, vs, view, sn, gn, dir, rng);
 }
 template <int OVERRIDE>
 DEV Col bsdf_sample(const BCtx& c, const Mat& m, VState& vs, v3 view, v3 sn, v3 gn, v3& dir, float& pdf, Rng& rng) {

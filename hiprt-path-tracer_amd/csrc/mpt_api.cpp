@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <string>
@@ -87,6 +88,15 @@ struct MptContext {
     BVH8 bvh;
     DBuf<Node8> nodes;
     DBuf<TriRec> tris;
+    // light-hit BVH (k_trace TM_NEE_LIGHT): the triangles whose emission can be non-black
+    BVH8 bvh_light;
+    DBuf<Node8> nodes_light;
+    DBuf<TriRec> tris_light;
+    std::vector<int32_t> h_light_prims;
+    std::vector<int32_t> h_idx;           // host copies for rebuilding the light BVH on material edits
+    std::vector<float> h_pos;
+    float box_pad = 0.0f;
+    int light_bvh = 1;                    // MPT_LIGHT_BVH at mpt_create: 0 = one closest-hit traversal per light-hit query
     DBuf<int32_t> idx, mat_idx, mat_prio, emissive, tex_dims;
     DBuf<float> pos, nrm, uv;
     DBuf<uint8_t> has_n, tex;
@@ -96,6 +106,9 @@ struct MptContext {
     DBuf<int32_t> mat_tex;
     DBuf<float4> em_tab;
     bool any_tex = false;
+    // material-class shading (k_split / k_shade): 1 on (default), 0 off, 2 on with every
+    // plain vertex deferred to the generic kernel (test hook); MPT_SHADE_CLASSES at mpt_create
+    int shade_classes = 1;
     std::vector<MptMaterial> h_mats;
     std::vector<int32_t> h_mat_idx;       // per triangle (alpha flags of the triangle records)
     std::vector<uint8_t> h_tex_alpha;     // per texture: some texel has alpha < 255
@@ -117,7 +130,7 @@ struct MptContext {
     DBuf<uint8_t> hit_inside, occ, qmask;
     DBuf<uint32_t> rng, spill;
     DBuf<uint4> vsA, vsB;
-    DBuf<int32_t> q0, q1, qh, qm, counters, nq_tgt, fetch_raw;
+    DBuf<int32_t> q0, q1, qh, qm, qf, nq_light, counters, nq_tgt, fetch_raw;
     DBuf<NeeRec> nee;
     DBuf<float> fb_color, fb_albedo, fb_normal;
     DBuf<int32_t> as_count, as_conv;
@@ -170,6 +183,9 @@ DevScene dev_scene(MptContext* c) {
     DevScene S{};
     S.nodes = c->nodes.p;
     S.tris = c->tris.p;
+    S.nodes_light = c->nodes_light.p;
+    S.tris_light = c->tris_light.p;
+    S.n_light_tris = (int32_t)c->h_light_prims.size();
     S.idx = c->idx.p;
     S.pos = c->pos.p;
     S.nrm = c->nrm.p;
@@ -227,6 +243,8 @@ DevPaths dev_paths(MptContext* c) {
     P.q1 = c->q1.p;
     P.qh = c->qh.p;
     P.qm = c->qm.p;
+    P.qf = c->qf.p;
+    P.nq_light = c->nq_light.p;
     P.counters = c->counters.p;
     P.nee = c->nee.p;
     P.nq_o = c->nq_o.p;
@@ -284,13 +302,13 @@ struct Allocs {
 
 // Bytes of path state per path slot (ensure_batch): ray_o, ray_d, hit, thr, col, alb, nrmv,
 // nhit (8 x 16), vsA + vsB (32), the NEE record, 4 staged NEE query rays (2 x 64), the
-// compacted query entries (16), occlusion bytes (4), 4 queues (16), rng (4), hit_inside,
+// compacted query entries (16), occlusion bytes (4), 6 queues (24), rng (4), hit_inside,
 // qmask, active (3).  Textured scenes add a resolved material per slot.
-constexpr size_t PATH_BYTES = 8 * 16 + 32 + sizeof(NeeRec) + 128 + 16 + 4 + 16 + 4 + 3;
+constexpr size_t PATH_BYTES = 8 * 16 + 32 + sizeof(NeeRec) + 128 + 16 + 4 + 24 + 4 + 3;
 
 void release_batch(MptContext* c) {
     release_all(c->ray_o, c->ray_d, c->hit, c->hit_inside, c->rng, c->thr, c->col, c->vsA, c->vsB, c->alb, c->nrmv,
-                c->q0, c->q1, c->qh, c->qm, c->nee, c->nq_o, c->nq_d, c->nq_tgt, c->occ, c->nhit, c->qmask, c->active,
+                c->q0, c->q1, c->qh, c->qm, c->qf, c->nq_light, c->nee, c->nq_o, c->nq_d, c->nq_tgt, c->occ, c->nhit, c->qmask, c->active,
                 c->mat_slot);
     c->batch_cap = 0;
 }
@@ -310,7 +328,7 @@ int ensure_batch(MptContext* c, int batch, bool mat_slot) {
     if (!have) {
         c->batch_cap = 0;
         A(c->ray_o, N); A(c->ray_d, N); A(c->hit, N); A(c->hit_inside, N); A(c->rng, N); A(c->thr, N); A(c->col, N);
-        A(c->vsA, N); A(c->vsB, N); A(c->alb, N); A(c->nrmv, N); A(c->q0, N); A(c->q1, N); A(c->qh, N); A(c->qm, N);
+        A(c->vsA, N); A(c->vsB, N); A(c->alb, N); A(c->nrmv, N); A(c->q0, N); A(c->q1, N); A(c->qh, N); A(c->qm, N); A(c->qf, N); A(c->nq_light, N);
         A(c->nee, N); A(c->nq_o, 4 * N); A(c->nq_d, 4 * N); A(c->nq_tgt, 4 * N); A(c->occ, 4 * N); A(c->nhit, N);
         A(c->qmask, N); A(c->active, N);
         if (A.e == hipSuccess) A(hipMemsetAsync(c->active.p, 0, N, c->stream));
@@ -384,6 +402,63 @@ int upload_alpha_flags(MptContext* c) {
     return MPT_OK;
 }
 
+// Light-hit BVH: the triangles whose emission, as evaluate_shadow_light_ray reads it
+// (Intersect.h:293-410; shadow_light_hit in the kernels), can be non-black -- an emissive
+// texture, or emission * strength with a positive channel.  A light-hit query (the BSDF
+// ray of MIS / RIS / BSDF light sampling) only needs the closest hit when it is one of
+// these: the closest hit among them, confirmed by an any-hit query over the whole scene
+// for a nearer (or equally near, lower-index) triangle, equals the whole-scene closest hit
+// whenever that one is a light, and every other outcome contributes nothing.  Rebuilt when
+// a material edit changes the set; alpha-test flags as upload_alpha_flags.
+int build_light_bvh(MptContext* c) {
+    std::vector<uint8_t> lit(c->h_mats.size()), aflag(c->h_mats.size());
+    for (size_t i = 0; i < c->h_mats.size(); i++) {
+        const MptMaterial& m = c->h_mats[i];
+        const float k = m.emission_strength;
+        lit[i] = (m.emission_texture_index != MPT_NO_TEXTURE || m.emission.r * k > 0.0f || m.emission.g * k > 0.0f ||
+                  m.emission.b * k > 0.0f) ? 1 : 0;
+        int bt = m.base_color_texture_index;
+        bool tex_alpha = bt >= 0 && bt < (int)c->h_tex_alpha.size() && c->h_tex_alpha[bt];
+        aflag[i] = (m.alpha_opacity < 1.0f || tex_alpha) ? 1 : 0;
+    }
+    std::vector<int32_t> prims;
+    for (size_t t = 0; t < c->h_mat_idx.size(); t++)
+        if (lit[c->h_mat_idx[t]]) prims.push_back((int32_t)t);
+    hipStream_t st = c->stream;
+    if (prims != c->h_light_prims || (!prims.empty() && !c->nodes_light.p)) {
+        c->h_light_prims = prims;
+        c->nodes_light.release();
+        c->tris_light.release();
+        if (!prims.empty()) {
+            std::vector<int32_t> sub(3 * prims.size());
+            for (size_t k = 0; k < prims.size(); k++)
+                for (int j = 0; j < 3; j++) sub[3 * k + j] = c->h_idx[3 * (size_t)prims[k] + j];
+            build_bvh8(c->h_pos.data(), sub.data(), (int32_t)prims.size(), c->bvh_light, 3, c->box_pad);
+            if (2 * c->bvh_light.depth + 2 > MAX_STACK) {
+                c->h_light_prims.clear();
+                return fail(MPT_ERR_UNSUPPORTED, "light BVH8 deeper than the traversal stack");
+            }
+            for (TriRec& tr : c->bvh_light.tris) {   // subset index -> scene primitive
+                int32_t k;
+                std::memcpy(&k, &tr.prim_bits, 4);
+                std::memcpy(&tr.prim_bits, &prims[k], 4);
+            }
+            HIPCHK(c->nodes_light.upload(c->bvh_light.nodes.data(), c->bvh_light.nodes.size(), st));
+        }
+    }
+    if (!prims.empty()) {
+        for (TriRec& tr : c->bvh_light.tris) {
+            int32_t prim;
+            std::memcpy(&prim, &tr.prim_bits, 4);
+            uint32_t f = aflag[c->h_mat_idx[prim]];
+            std::memcpy(&tr.pad0, &f, 4);
+        }
+        HIPCHK(c->tris_light.upload(c->bvh_light.tris.data(), c->bvh_light.tris.size(), st));
+    }
+    HIPCHK(hipStreamSynchronize(st));
+    return MPT_OK;
+}
+
 // ReSTIR DI buffers (ReSTIRDIRenderPass::update / resize, ReSTIRDIRenderPass.cpp:130-205): the
 // G-buffer pair, three reservoir buffers reset to empty reservoirs, the presampled lights.
 // Zero-filled G-buffers decode as "never written" (see restir_di.h gb_surface).
@@ -449,7 +524,7 @@ int resolve_materials(MptContext* c) {
     HIPCHK(hipMemcpyAsync(t.data(), c->mat_tex.p, n * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     c->any_tex = false;
-    for (int32_t v : t) c->any_tex |= v != 0;
+    for (int32_t v : t) c->any_tex |= (v & MT_TEXTURED) != 0;
     return MPT_OK;
 }
 
@@ -570,6 +645,8 @@ int mpt_create(int device, void* hip_stream, MptContext** out) {
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(MPT_ERR_HIP, "no HIP device available");
     if (device < 0 || device >= ndev) return fail(MPT_ERR_INVALID_ARGUMENT, "device index out of range");
     MptContext* c = new MptContext();   // value-initialised: every handle starts null
+    if (const char* e = std::getenv("MPT_SHADE_CLASSES")) c->shade_classes = std::atoi(e);
+    if (const char* e = std::getenv("MPT_LIGHT_BVH")) c->light_bvh = std::atoi(e);
     int r = create_context(c, device, hip_stream);
     if (r != MPT_OK) {
         const std::string msg = g_err;
@@ -618,6 +695,12 @@ int mpt_upload_scene(MptContext* c, const MptScene* s) {
             return fail(MPT_ERR_INVALID_ARGUMENT, "emissive triangle index out of range");
     HIPCHK(hipSetDevice(c->device));
     build_bvh8(s->vertices, s->triangle_indices, s->num_triangles, c->bvh, 3);
+    c->box_pad = scene_box_pad(s->vertices, s->num_triangles, s->triangle_indices);
+    c->h_idx.assign(s->triangle_indices, s->triangle_indices + 3 * (size_t)s->num_triangles);
+    c->h_pos.assign(s->vertices, s->vertices + 3 * (size_t)s->num_vertices);
+    c->h_light_prims.clear();
+    c->nodes_light.release();
+    c->tris_light.release();
     // per level: at most one node group and one postponed triangle group on the stack
     if (2 * c->bvh.depth + 2 > MAX_STACK) return fail(MPT_ERR_UNSUPPORTED, "BVH8 deeper than the traversal stack");
     hipStream_t st = c->stream;
@@ -670,6 +753,8 @@ int mpt_upload_scene(MptContext* c, const MptScene* s) {
     }
     int rr = upload_alpha_flags(c);
     if (rr != MPT_OK) return rr;
+    rr = build_light_bvh(c);
+    if (rr != MPT_OK) return rr;
     rr = resolve_materials(c);
     if (rr != MPT_OK) return rr;
     c->has_scene = true;
@@ -688,6 +773,8 @@ int mpt_update_materials(MptContext* c, const MptMaterial* m, int32_t count) {
     HIPCHK(c->mat_prio.upload(prio.data(), prio.size(), c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     int rr = upload_alpha_flags(c);
+    if (rr != MPT_OK) return rr;
+    rr = build_light_bvh(c);
     if (rr != MPT_OK) return rr;
     return resolve_materials(c);
 }
@@ -875,6 +962,9 @@ static int launch_batch(MptContext* c, const MptFrame* f, int batch) {
     cfg.ev_cap = EV_POOL;
     cfg.ev_used = 0;
     cfg.restir_out_sp2 = c->restir_out_sp2;
+    cfg.shade_classes = c->shade_classes;
+    cfg.light_bvh = c->light_bvh;
+    cfg.light_static = !c->h_light_prims.empty() && 2 * c->bvh_light.depth + 2 <= TRAV_LDS_STACK;
     if (restir_part) {
         if (!c->h_reproj) HIPCHK(hipHostMalloc((void**)&c->h_reproj, sizeof(int32_t), hipHostMallocDefault));
         cfg.halo_fn = c->halo_fn;

@@ -26,6 +26,9 @@ constexpr int TRAV_SPILL_DEPTH = 64 - TRAV_LDS_STACK;
 struct DevScene {
     const Node8* nodes;
     const TriRec* tris;
+    const Node8* nodes_light;     // light-hit BVH (build_light_bvh): triangles with possibly non-black emission
+    const TriRec* tris_light;
+    int32_t n_light_tris;
     const int32_t* idx;          // 3 per triangle
     const float* pos;            // 3 per vertex
     const float* nrm;            // 3 per vertex
@@ -34,7 +37,7 @@ struct DevScene {
     const int32_t* mat_idx;      // per triangle
     const MptMaterial* mats;
     const MptMaterial* mats_res;  // per material: intersection-time resolution without textures
-    const int32_t* mat_tex;       // per material: 1 if any texture feeds the resolved material
+    const int32_t* mat_tex;       // per material: MT_TEXTURED | MT_FULL (k_resolve_materials)
     const int32_t* mat_prio;     // dielectric_priority per material (nested-dielectric push)
     const int32_t* emissive;
     const float4* em_tab;         // 5 float4 per emissive triangle (k_emissive_table)
@@ -109,6 +112,8 @@ struct DevPaths {
     int32_t* q1;
     int32_t* qh;              // this bounce's path queue split: paths that hit a surface ...
     int32_t* qm;              // ... and paths that left the scene (k_split)
+    int32_t* qf;              // hits on materials outside the plain-dielectric class (k_split, k_shade)
+    int32_t* nq_light;        // light-hit queries whose light candidate needs the whole-scene check (slot * 4 + 3)
     int32_t* counters;        // see CTR_*
     NeeRec* nee;
     float4* nq_o;             // staged NEE query rays, slot * 4 + kind (kinds 0..2 any hit, 3 closest)
@@ -161,6 +166,9 @@ constexpr int N_TRACE_MODES = 5;
 enum { KT_CAMERA = 3, KT_SHADE = 4, KT_RESOLVE = 5, KT_ACCUMULATE = 6, KT_COMPACT = 7, KT_RESTIR = 8, KT_SPLIT = 9,
        KT_MISS = 10, KT_COUNT = 11 };
 constexpr uint32_t QM_CONT = 16u;
+// mat_tex bits: a texture feeds the resolved material; the material is outside the
+// plain-dielectric class (coat, sheen, metallic, transmission or thin film may be non-zero)
+constexpr int32_t MT_TEXTURED = 1, MT_FULL = 2;
 constexpr int STATS_STRIDE = 6;   // per mode: traversals, nodes, tris, (unused), node slots, tri slots
 constexpr int N_STATS = N_TRACE_MODES * STATS_STRIDE;
 
@@ -168,6 +176,9 @@ enum {
     CTR_Q0 = 0, CTR_Q1 = 1, CTR_ANY = 2, CTR_CL = 3, CTR_FETCH = 4,
     CTR_REPROJ = 5,           // max |reprojected row - row| of the frame's G-buffer (partitioned ReSTIR DI)
     CTR_HIT = 6, CTR_MISS = 7,  // lengths of the hit / miss queues of the bounce (k_split)
+    CTR_FULL = 8,             // length of the generic-material hit queue (k_split + k_shade deferrals)
+    CTR_DEFER = 9,            // plain-class hits deferred to the generic queue (tombstones in qh)
+    CTR_LIGHT = 10,           // length of nq_light (k_trace TM_NEE_LIGHT)
     CTR_COUNT = 16
 };
 
@@ -189,6 +200,9 @@ struct LaunchCfg {
     int halo_rows;            // out: halo agreed in this frame's G-buffer exchange
     int32_t* h_reproj;        // pinned host word for the measured reprojection offset
     int halo_rc;              // out: first non-zero callback return
+    int shade_classes;        // material-class shading: 0 off, 1 on, 2 on + defer every plain vertex (test hook)
+    int light_bvh;            // light-hit queries through the light BVH (1) or one closest-hit traversal (0)
+    int light_static;         // the light BVH's traversal stack fits in LDS (one query per lane, no spill)
 };
 
 hipError_t launch_frame(const DevScene& S, const DevPaths& P, const MptFrame* d_frame, const MptFrame& h_frame,

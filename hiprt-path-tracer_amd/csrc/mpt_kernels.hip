@@ -98,7 +98,10 @@ DEV uint32_t qbyte(uint32_t w0, uint32_t w1, int s) { return ((s < 4 ? w0 : w1) 
 // traversal ends (true) or `budget` nodes have been opened (false, the state is kept for
 // the next call).  Stopping between nodes lets the traversal kernel hand a finished lane
 // a new ray while the rest of its wave is still traversing.
-template <bool ANY, bool STATS>
+// TIE (any hit only): a triangle also counts when it lies exactly at t_max with a primitive
+// index below `tie` -- the whole-scene check of a light-hit candidate (TM_NEE_LIGHT_OCC),
+// where that triangle would win the closest-hit tie against the light.
+template <bool ANY, bool STATS, bool TIE = false>
 struct Trav {
     v3 o, d;
     float ix, iy, iz;
@@ -111,6 +114,7 @@ struct Trav {
     int last_hit;
     uint32_t akey;
     bool alpha_on;
+    int tie;
 
     DEV void init(v3 o_, v3 d_, int lh, float tmax, bool al, uint32_t key) {
         o = o_;
@@ -146,10 +150,10 @@ struct Trav {
     // while fewer than 1/TRI_POSTPONE of the wave's traversing lanes have triangles to
     // test, so that triangle tests run with more lanes at a time (the closest hit does
     // not depend on the test order: ties go to the lower primitive index).
-    DEV bool run(const DevScene& S, uint2* lds, uint32_t* spill, int budget, uint32_t& n_nodes, uint32_t& n_tris,
-                 uint32_t* n_slots = nullptr) {
-        const float4* nodes = reinterpret_cast<const float4*>(S.nodes);
-        const float4* tris = reinterpret_cast<const float4*>(S.tris);
+    DEV bool run(const DevScene& S, const Node8* bvh_nodes, const TriRec* bvh_tris, uint2* lds, uint32_t* spill, int budget,
+                 uint32_t& n_nodes, uint32_t& n_tris, uint32_t* n_slots = nullptr) {
+        const float4* nodes = reinterpret_cast<const float4*>(bvh_nodes);
+        const float4* tris = reinterpret_cast<const float4*>(bvh_tris);
         const int tid = threadIdx.x;
         uint32_t tbase = 0u, tmask = 0u;   // current triangle group
         while (true) {
@@ -259,11 +263,12 @@ struct Trav {
                 if (!(t > 0.0000001f)) continue;
                 if (prim == last_hit) continue;
                 // alpha-tested triangle (flag in the record): only when it would be kept
-                if (alpha_on && __float_as_uint(t1.w) != 0u &&
-                    (ANY ? t < best : (t < best || (t == best && prim < bprim))) && alpha_rejects(S, prim, u, v, akey))
+                const bool nearer = ANY ? (t < best || (TIE && t == best && prim < tie))
+                                        : (t < best || (t == best && prim < bprim));
+                if (alpha_on && __float_as_uint(t1.w) != 0u && nearer && alpha_rejects(S, prim, u, v, akey))
                     continue;
                 if (ANY) {
-                    if (t < best) {
+                    if (nearer) {
                         bprim = prim; best = t; bu = u; bv = v;
                         gk = 0u; sp = 0;
                         return true;
@@ -281,7 +286,7 @@ DEV bool traverse(const DevScene& S, v3 o, v3 d, int last_hit, float tmax, THit&
                   uint32_t& n_nodes, uint32_t& n_tris, bool alpha_on = false, uint32_t akey = 0u) {
     Trav<ANY, STATS> tr;
     tr.init(o, d, last_hit, tmax, alpha_on, akey);
-    tr.run(S, lds, spill, 0x7fffffff, n_nodes, n_tris);
+    tr.run(S, S.nodes, S.tris, lds, spill, 0x7fffffff, n_nodes, n_tris);
     out.prim = tr.bprim;
     out.t = tr.best;
     out.u = tr.bu;
@@ -290,7 +295,19 @@ DEV bool traverse(const DevScene& S, v3 o, v3 d, int last_hit, float tmax, THit&
 }
 
 // Ray sources of the persistent traversal kernel
-enum TraceMode { TM_PATH = 0, TM_NEE_ANY = 1, TM_NEE_CLOSEST = 2, TM_RAW_CLOSEST = 3, TM_RAW_ANY = 4 };
+// TM_NEE_LIGHT / TM_NEE_LIGHT_OCC answer the light-hit queries (kind 3) exactly like
+// TM_NEE_CLOSEST in two steps (build_light_bvh in mpt_api.cpp): the closest hit among the
+// triangles that can emit, then an any-hit query over the whole scene up to that hit for
+// the candidates found; they report in TM_NEE_CLOSEST's stage (timing, counters).
+enum TraceMode { TM_PATH = 0, TM_NEE_ANY = 1, TM_NEE_CLOSEST = 2, TM_RAW_CLOSEST = 3, TM_RAW_ANY = 4, TM_NEE_LIGHT = 5,
+                 TM_NEE_LIGHT_OCC = 6 };
+constexpr int trace_stage(int mode) { return mode >= TM_NEE_LIGHT ? TM_NEE_CLOSEST : mode; }
+// Short traversals (the light BVH: ~1.5 nodes per query) run one query per lane over a grid
+// covering the list instead of persistent waves: with so little work per query the shared
+// work counter of the persistent kernel (one device-scope atomic per wave refill) is what
+// the launch would wait on (2.96 ms per C3 launch).  Only when the BVH is shallow enough
+// for the stack to stay in LDS (the global spill area is sized for the persistent grid):
+// TraceArgs::static_grid, set by the host from the light BVH's depth.
 
 struct TraceArgs {
     DevScene S;
@@ -306,6 +323,7 @@ struct TraceArgs {
     const MptFrame* F;         // frame constants (alpha keys); NULL for raw queries
     int bounce;
     int alpha;                 // render_settings.do_alpha_testing
+    int static_grid;           // TM_NEE_LIGHT: one query per lane (the light BVH's stack fits in LDS)
 };
 DEV uint32_t slot_pixel(const MptFrame& F, int slot, int& x, int& y);
 DEV uint32_t pixel_seed(const MptFrame& F, uint32_t pix);
@@ -324,15 +342,19 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MODE == TM_P
     const DevScene& S = A.S;
     const DevPaths& P = A.P;
     const int count = (MODE == TM_RAW_CLOSEST || MODE == TM_RAW_ANY) ? A.count_const : *A.count_ptr;
-    uint32_t* spill = P.stack_spill + ((size_t)blockIdx.x * TB + threadIdx.x) * (2 * SPILL_DEPTH);
+    // (a static grid never spills: static_grid requires the stack to fit in LDS)
+    uint32_t* spill = P.stack_spill + (MODE == TM_NEE_LIGHT && A.static_grid ? 0 : ((size_t)blockIdx.x * TB + threadIdx.x) * (2 * SPILL_DEPTH));
     uint32_t n_nodes = 0, n_tris = 0, n_rays = 0;
     uint32_t n_slots[2] = {0u, 0u};
-    constexpr bool ANY = (MODE == TM_NEE_ANY || MODE == TM_RAW_ANY);
+    constexpr bool ANY = (MODE == TM_NEE_ANY || MODE == TM_RAW_ANY || MODE == TM_NEE_LIGHT_OCC);
+    constexpr bool TIE = MODE == TM_NEE_LIGHT_OCC;
+    const Node8* bvh_nodes = MODE == TM_NEE_LIGHT ? S.nodes_light : S.nodes;
+    const TriRec* bvh_tris = MODE == TM_NEE_LIGHT ? S.tris_light : S.tris;
     // Persistent waves with per-lane ray replacement: a lane whose ray has finished takes
     // a new one as soon as at least TRACE_REFILL lanes of its wave are idle (one atomic
     // per refill), instead of the whole wave waiting for its longest ray.  Between refill
     // checks every lane opens at most TRACE_BUDGET nodes.
-    Trav<ANY, STATS> tr;
+    Trav<ANY, STATS, TIE> tr;
     bool alive = false;
     bool exhausted = false;   // wave-uniform: the ray counter has passed `count`
     int ray = 0;              // RAW: ray index; NEE: staged query (slot * 4 + kind); PATH: slot
@@ -345,9 +367,15 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MODE == TM_P
         if (!exhausted && __popcll(idle) >= (unsigned)TRACE_REFILL) {
             const int need = __popcll(idle);
             int base = 0;
-            if (lane_id() == 0) base = atomicAdd(A.fetch, need);
-            base = __shfl(base, 0);
-            if (base + need >= count) exhausted = true;
+            if (MODE == TM_NEE_LIGHT && A.static_grid) {
+                // one ray per lane, 64 consecutive queries per wave, no refill
+                base = (int)(blockIdx.x * TB + (threadIdx.x & ~63u));
+                exhausted = true;
+            } else {
+                if (lane_id() == 0) base = atomicAdd(A.fetch, need);
+                base = __shfl(base, 0);
+                if (base + need >= count) exhausted = true;
+            }
             if (!alive) {
                 const int i = base + __popcll(idle & ((1ull << lane_id()) - 1ull));
                 if (i < count) {
@@ -364,16 +392,26 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MODE == TM_P
                             pseed = path_seed(A.F, P, ray, A.bounce == 0);
                         tr.init(mk3(ro.x, ro.y, ro.z), mk3(rd.x, rd.y, rd.z), (int)__float_as_uint(ro.w), INFINITY,
                                 A.alpha != 0, A.alpha ? alpha_key(pseed, A.bounce, 0, 0) : 0u);
-                    } else if (MODE == TM_NEE_ANY || MODE == TM_NEE_CLOSEST) {
+                    } else if (MODE == TM_NEE_ANY || MODE == TM_NEE_CLOSEST || MODE == TM_NEE_LIGHT || MODE == TM_NEE_LIGHT_OCC) {
                         // compacted list of staged queries (entry = slot * 4 + kind), see k_compact
-                        ray = P.nq_tgt[MODE == TM_NEE_ANY ? (size_t)i : (size_t)P.n * 3 + i];
+                        ray = MODE == TM_NEE_LIGHT_OCC ? P.nq_light[i]
+                                                       : P.nq_tgt[MODE == TM_NEE_ANY ? (size_t)i : (size_t)P.n * 3 + i];
                         ro = P.nq_o[ray];
                         rd = P.nq_d[ray];
                         qmax = rd.w;
                         const bool al = A.alpha != 0;
                         uint32_t akey = 0u;
                         if (al) akey = alpha_key(path_seed(A.F, P, ray >> 2, false), A.bounce, (ray & 3) + 1, 0);
-                        tr.init(mk3(ro.x, ro.y, ro.z), mk3(rd.x, rd.y, rd.z), (int)__float_as_uint(ro.w), ANY ? rd.w : INFINITY, al, akey);
+                        float tmax = ANY ? rd.w : INFINITY;
+                        if (TIE) {
+                            // the light candidate of TM_NEE_LIGHT: anything nearer, or as near with a
+                            // lower index, is the closest hit instead
+                            const float4 h = P.nhit[ray >> 2];
+                            tmax = h.x;
+                            tr.tie = (int)__float_as_uint(h.w);
+                        }
+                        tr.init(mk3(ro.x, ro.y, ro.z), mk3(rd.x, rd.y, rd.z), (int)__float_as_uint(ro.w), tmax, al, akey);
+                        if (MODE == TM_NEE_LIGHT && S.n_light_tris == 0) tr.gk = 0u;   // no light: nothing to traverse
                     } else {
                         ray = i;
                         ro = A.raw_o[i];
@@ -388,7 +426,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MODE == TM_P
             continue;
         }
         if (!alive) continue;
-        if (!tr.run(S, lds, spill, TRACE_BUDGET, n_nodes, n_tris, STATS ? n_slots : nullptr)) continue;
+        if (!tr.run(S, bvh_nodes, bvh_tris, lds, spill, TRACE_BUDGET, n_nodes, n_tris, STATS ? n_slots : nullptr)) continue;
         const bool found = tr.bprim >= 0;
         if (MODE == TM_PATH) {
             // trace_ray's boundary-skipping loop (Intersect.h:117-206)
@@ -418,10 +456,14 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MODE == TM_P
             P.hit_inside[ray] = was_inside ? 1 : 0;
         } else if (MODE == TM_NEE_ANY) {
             P.occ[ray] = found ? 1 : 0;
-        } else if (MODE == TM_NEE_CLOSEST) {
+        } else if (MODE == TM_NEE_CLOSEST || MODE == TM_NEE_LIGHT) {
             // evaluate_shadow_light_ray: a hit counts only below t_max - 1e-4 (Intersect.h:337-343)
             bool ok = found && tr.best < qmax;
             P.nhit[ray >> 2] = make_float4(tr.best, tr.bu, tr.bv, __uint_as_float((uint32_t)(ok ? tr.bprim : -1)));
+            if (MODE == TM_NEE_LIGHT && ok) P.nq_light[atomicAdd(&P.counters[CTR_LIGHT], 1)] = ray;
+        } else if (MODE == TM_NEE_LIGHT_OCC) {
+            // a nearer triangle is not a light: the query contributes nothing, as a miss
+            if (found) P.nhit[ray >> 2].w = __uint_as_float(0xffffffffu);
         } else if (MODE == TM_RAW_ANY) {
             A.raw_occ[ray] = found ? 1 : 0;
         } else {
@@ -439,7 +481,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MODE == TM_P
             n_slots[1] += __shfl_xor(n_slots[1], off);
         }
         if (lane_id() == 0) {
-            unsigned long long* st = (unsigned long long*)&P.stats[MODE * STATS_STRIDE];
+            unsigned long long* st = (unsigned long long*)&P.stats[trace_stage(MODE) * STATS_STRIDE];
             atomicAdd(st + 0, (unsigned long long)n_rays);
             atomicAdd(st + 1, (unsigned long long)n_nodes);
             atomicAdd(st + 2, (unsigned long long)n_tris);
@@ -932,17 +974,28 @@ struct ShadeArgs {
     const MptFrame* F;
     int bounce;
     int last_bounce;
-    const int32_t* q_cur;
+    int32_t* q_cur;            // the vertices to shade (k_split's class list)
     const int32_t* count_cur;
-    int32_t* q_next;
-    int32_t* count_next;
+    int32_t* q_defer;          // PLAIN: vertices handed to the generic kernel (seen from inside)
+    int32_t* count_defer;
+    int force_defer;           // test hook (MPT_SHADE_CLASSES=2): defer every plain vertex
 };
 
 #ifndef MPT_SHADE_WAVES
 #define MPT_SHADE_WAVES 2
 #endif
-template <int OVR>
-__global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MPT_SHADE_WAVES))) void k_shade(ShadeArgs A) {
+// Material classes (mat_tex bit MT_FULL, k_resolve_materials): k_split sorts the hit
+// vertices into the plain-dielectric list (no coat, sheen, metal, transmission or thin film:
+// the diffuse + specular base of the Principled BSDF, most of a city) and the list of every
+// other material.  k_shade<OVR, true> shades the plain list with those lobes compiled out
+// (fewer registers and instructions, dev_bsdf.h FULL = false), k_shade<OVR, false> the rest
+// with the generic code.  A plain vertex seen from inside (the glass lobe then has weight 1)
+// is deferred to the generic kernel before it writes anything.
+#ifndef MPT_SHADE_WAVES_PLAIN
+#define MPT_SHADE_WAVES_PLAIN MPT_SHADE_WAVES
+#endif
+template <int OVR, bool PLAIN>
+__global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_SHADE_WAVES_PLAIN : MPT_SHADE_WAVES))) void k_shade(ShadeArgs A) {
     const DevScene& S = A.S;
     const DevPaths& P = A.P;
     const MptFrame& F = *A.F;
@@ -985,7 +1038,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MPT_SHADE_WA
             gn = normalize(tri_normal(S, prim));
             sn = shading_normal_of(S, gn, prim, uv, tc);
             const int mi = S.mat_idx[prim];
-            if (F.bsdf_flags.white_furnace_mode || S.mat_tex[mi]) {
+            if (F.bsdf_flags.white_furnace_mode || (S.mat_tex[mi] & MT_TEXTURED)) {
                 P.mat_slot[slot] = intersection_material(S, mi, tc, F.bsdf_flags.white_furnace_mode);
                 mp = &P.mat_slot[slot];
             } else {
@@ -1011,6 +1064,16 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MPT_SHADE_WA
             sn = normalize(sn);
             d = normalize(d);
             rng = make_rng(path_seed(A.F, P, slot, false));
+        }
+        if (PLAIN) {
+            // principled_eval_pre's 'outside' with the normal the vertex is shaded with
+            const v3 sn_f = (is_emissive(m) && dot(-d, gn) < 0) ? -sn : sn;
+            if (!(dot(-d, sn_f) > 0 || m.thin_walled) || A.force_defer) {
+                A.q_defer[atomicAdd(A.count_defer, 1)] = slot;
+                atomicAdd(&P.counters[CTR_DEFER], 1);
+                A.q_cur[i] = -1;    // k_compact / k_resolve skip the entry here
+                return;             // nothing written (no block-wide operation follows)
+            }
         }
         NeeRec& nr = P.nee[slot];   // written field by field, straight to HBM
         uint32_t fl = 0;
@@ -1071,7 +1134,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MPT_SHADE_WA
             __shared__ PEval pe_lds[TB];
             PEval& pe = pe_lds[threadIdx.x];
             SECT(0);
-            bsdf_eval_pre<OVR>(bc, m, vs, view, sn, pe);
+            bsdf_eval_pre<OVR, !PLAIN>(bc, m, vs, view, sn, pe);
             SECT(5);
             Col fW = col(0.0f);                // BSDF value / pdf at the RIS light winner
             float pdfW = 0.0f;
@@ -1091,7 +1154,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MPT_SHADE_WA
                 Col ec = col(0.0f);
                 bool inner = false;
                 if (op == OP_RIS_BSDF || op == OP_MIS_BSDF || op == OP_BSDF_LIGHT || op == OP_ENV_BSDF || op == OP_CONT) {
-                    do_eval = bsdf_sample_dir<OVR>(bc, m, tv, view, sn, gn, L, rng);
+                    do_eval = bsdf_sample_dir<OVR, !PLAIN>(bc, m, tv, view, sn, gn, L, rng);
                 } else if (op == OP_RIS_LIGHT) {
                     lp = sample_emissive_triangle(S, rng, lpdf, li);
                     if (lpdf > 0.0f) {
@@ -1154,7 +1217,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MPT_SHADE_WA
                 float pdf = 0.0f;
                 Col f = col(0.0f);
                 SECT(1);
-                if (do_eval) f = bsdf_eval_post<OVR>(bc, m, tv, pe, sn, L, pdf);
+                if (do_eval) f = bsdf_eval_post<OVR, !PLAIN>(bc, m, tv, pe, sn, L, pdf);
                 SECT(2);
                 int next = OP_DONE;
                 if (op == OP_RIS_LIGHT) {
@@ -1417,53 +1480,76 @@ DEV int load_items(const int32_t* q, int b0, int count, int slots[CP_ITEMS]) {
 // k_split: the bounce's path queue -> the paths that hit a surface (k_shade, k_compact,
 // k_resolve) and those that left the scene (k_miss), so that every lane of a shading wave
 // has a vertex to shade instead of idling through the light-sampling loop beside a miss.
-__global__ __launch_bounds__(CP_NT) void k_split(DevPaths P, const int32_t* q, const int32_t* count_q) {
+// With `classes`, the hits are further sorted by material class (see k_shade): plain
+// dielectrics into qh (CTR_HIT), every other material into qf (CTR_FULL).
+__global__ __launch_bounds__(CP_NT) void k_split(DevScene S, DevPaths P, const int32_t* q, const int32_t* count_q,
+                                                 int classes) {
     __shared__ int tmp[CP_NT / 64 + 1];
-    __shared__ int base[2];
+    __shared__ int base[3];
     const int count = *count_q;
     const int b0 = blockIdx.x * CP_NT * CP_ITEMS;
     if (b0 >= count) return;
     int slots[CP_ITEMS];
     const int n = load_items(q, b0, count, slots);
-    uint32_t hm = 0u;
-    int nh = 0;
+    uint32_t hm = 0u, fm = 0u;
+    int nh = 0, nf = 0;
 #pragma unroll
     for (int j = 0; j < CP_ITEMS; j++) {
-        if (j < n && __float_as_int(P.hit[slots[j]].w) >= 0) { hm |= 1u << j; nh++; }
+        const int prim = j < n ? __float_as_int(P.hit[slots[j]].w) : -1;
+        if (prim >= 0) {
+            if (classes && (S.mat_tex[S.mat_idx[prim]] & MT_FULL)) { fm |= 1u << j; nf++; }
+            else { hm |= 1u << j; nh++; }
+        }
     }
-    int th, tm;
+    int th, tm, tf;
     int oh = block_scan_excl(nh, tmp, th);
-    int om = block_scan_excl(n - nh, tmp, tm);
+    int om = block_scan_excl(n - nh - nf, tmp, tm);
+    int of = block_scan_excl(nf, tmp, tf);
     if (threadIdx.x == 0) {
         base[0] = th ? atomicAdd(&P.counters[CTR_HIT], th) : 0;
         base[1] = tm ? atomicAdd(&P.counters[CTR_MISS], tm) : 0;
+        base[2] = tf ? atomicAdd(&P.counters[CTR_FULL], tf) : 0;
     }
     __syncthreads();
     oh += base[0];
     om += base[1];
+    of += base[2];
 #pragma unroll
     for (int j = 0; j < CP_ITEMS; j++) {
         if (j >= n) break;
         if ((hm >> j) & 1u) P.qh[oh++] = slots[j];
+        else if ((fm >> j) & 1u) P.qf[of++] = slots[j];
         else P.qm[om++] = slots[j];
     }
 }
 
+// The bounce's shaded vertices: qh[0, CTR_HIT) followed by qf[0, CTR_FULL); entries that
+// k_shade<PLAIN> deferred to qf are -1 in qh.
+DEV int shaded_count(const DevPaths& P) { return P.counters[CTR_HIT] + P.counters[CTR_FULL]; }
+DEV int shaded_entry(const DevPaths& P, int nh, int i) { return i < nh ? P.qh[i] : P.qf[i - nh]; }
+
 // k_compact: next path queue + NEE query lists from the per-path masks of the shaded paths
-__global__ __launch_bounds__(CP_NT) void k_compact(DevPaths P, const int32_t* q_cur, const int32_t* count_cur,
-                                                   int32_t* q_next, int32_t* count_next) {
+__global__ __launch_bounds__(CP_NT) void k_compact(DevPaths P, int32_t* q_next, int32_t* count_next) {
     __shared__ int tmp[CP_NT / 64 + 1];
     __shared__ int base[5];
-    const int count = *count_cur;
+    const int nh = P.counters[CTR_HIT];
+    const int count = nh + P.counters[CTR_FULL];
     const int b0 = blockIdx.x * CP_NT * CP_ITEMS;
     if (b0 >= count) return;
     int slots[CP_ITEMS];
-    const int n = load_items(q_cur, b0, count, slots);
+    int n;
+    if (b0 + CP_NT * CP_ITEMS <= nh) n = load_items(P.qh, b0, nh, slots);
+    else {
+        const int i0 = b0 + (int)threadIdx.x * CP_ITEMS;
+        n = max(0, min(CP_ITEMS, count - i0));
+#pragma unroll
+        for (int j = 0; j < CP_ITEMS; j++) slots[j] = j < n ? shaded_entry(P, nh, i0 + j) : 0;
+    }
     uint8_t m[CP_ITEMS];
     int c[5] = {0, 0, 0, 0, 0};
 #pragma unroll
     for (int j = 0; j < CP_ITEMS; j++) {
-        m[j] = j < n ? P.qmask[slots[j]] : 0;
+        m[j] = (j < n && slots[j] >= 0) ? P.qmask[slots[j]] : 0;
         c[0] += (m[j] & QM_CONT) ? 1 : 0;
         c[1] += m[j] & 1u;
         c[2] += (m[j] >> 1) & 1u;
@@ -1537,7 +1623,7 @@ DEV float pdf_emissive_hit(const DevScene& S, const ShadowLightHit& h, v3 d) {
 
 // over the bounce's hit queue (the shaded paths); count_paths: the bounce's path rays
 __global__ __launch_bounds__(TB) void k_resolve(DevScene S, DevPaths P, const MptFrame* __restrict__ Fp, int bounce,
-                                                const int32_t* q_cur, const int32_t* count_cur, const int32_t* count_paths) {
+                                                const int32_t* count_paths) {
     const MptFrame& F = *Fp;
     const MptRenderSettings& rs = F.render_settings;
     int i = blockIdx.x * TB + threadIdx.x;
@@ -1546,10 +1632,12 @@ __global__ __launch_bounds__(TB) void k_resolve(DevScene S, DevPaths P, const Mp
         P.ray_counts[0] += (uint64_t)*count_paths;
         P.ray_counts[1] += (uint64_t)P.counters[CTR_ANY];
         P.ray_counts[2] += (uint64_t)P.counters[CTR_CL];
-        P.ray_counts[3] += (uint64_t)*count_cur;
+        P.ray_counts[3] += (uint64_t)(shaded_count(P) - P.counters[CTR_DEFER]);
     }
-    if (i >= *count_cur) return;
-    int slot = q_cur[i];
+    const int nh = P.counters[CTR_HIT];
+    if (i >= nh + P.counters[CTR_FULL]) return;
+    const int slot = shaded_entry(P, nh, i);
+    if (slot < 0) return;   // deferred to the generic shading list
 #ifdef MPT_RESOLVE_BYREF
     const NeeRec& nr = P.nee[slot];
 #else
@@ -1704,6 +1792,7 @@ static int blocks_for(int n) { return (n + TB - 1) / TB; }
 
 template <int MODE>
 static void launch_trace_mode(const TraceArgs& a, int grid, bool stats, hipStream_t st) {
+    if (MODE == TM_NEE_LIGHT && a.static_grid) grid = blocks_for(a.P.n);   // the query list holds at most n entries
     if (stats) hipLaunchKernelGGL((k_trace<MODE, true>), dim3(grid), dim3(TB), 0, st, a);
     else hipLaunchKernelGGL((k_trace<MODE, false>), dim3(grid), dim3(TB), 0, st, a);
 }
@@ -1724,7 +1813,7 @@ struct TimedScope {
 template <int MODE>
 static void timed_trace(const TraceArgs& a, LaunchCfg& cfg, hipStream_t st) {
     bool timed = cfg.ev_pool && cfg.ev_used + 2 <= cfg.ev_cap;
-    if (timed) { cfg.ev_mode[cfg.ev_used / 2] = MODE; hipEventRecord(cfg.ev_pool[cfg.ev_used], st); }
+    if (timed) { cfg.ev_mode[cfg.ev_used / 2] = trace_stage(MODE); hipEventRecord(cfg.ev_pool[cfg.ev_used], st); }
     launch_trace_mode<MODE>(a, cfg.grid_persistent, cfg.stats, st);
     if (timed) { hipEventRecord(cfg.ev_pool[cfg.ev_used + 1], st); cfg.ev_used += 2; }
     cfg.launches++;
@@ -1875,6 +1964,8 @@ hipError_t launch_frame(const DevScene& S, const DevPaths& P0, const MptFrame* d
     int32_t* q_next = P.q1;
     int c_cur = CTR_Q0, c_next = CTR_Q1;
     const int nb = hf.render_settings.nb_bounces;
+    // material classes (k_split / k_shade): Principled BSDF only (the Lambert override has one class)
+    const int classes = hf.options.bsdf_override == MPT_BSDF_LAMBERTIAN ? 0 : (cfg.shade_classes != 0 ? 1 : 0);
     for (int b = 0; b <= nb; b++) {
         // continuation / camera rays
         hipMemsetAsync(&P.counters[CTR_FETCH], 0, sizeof(int32_t), st);
@@ -1889,21 +1980,28 @@ hipError_t launch_frame(const DevScene& S, const DevPaths& P0, const MptFrame* d
         }
         hipMemsetAsync(&P.counters[c_next], 0, sizeof(int32_t), st);
         hipMemsetAsync(&P.counters[CTR_ANY], 0, 2 * sizeof(int32_t), st);
-        hipMemsetAsync(&P.counters[CTR_HIT], 0, 2 * sizeof(int32_t), st);
+        hipMemsetAsync(&P.counters[CTR_HIT], 0, 4 * sizeof(int32_t), st);   // HIT, MISS, FULL, DEFER
         const dim3 cp_grid((n + CP_NT * CP_ITEMS - 1) / (CP_NT * CP_ITEMS));
         {
             TimedScope ts(cfg, st, KT_SPLIT);
-            hipLaunchKernelGGL(k_split, cp_grid, dim3(CP_NT), 0, st, P, q_cur, &P.counters[c_cur]);
+            hipLaunchKernelGGL(k_split, cp_grid, dim3(CP_NT), 0, st, S, P, q_cur, &P.counters[c_cur], classes);
         }
         ShadeArgs sa;
         sa.S = S; sa.P = P; sa.F = d_frame; sa.bounce = b; sa.last_bounce = nb;
-        sa.q_cur = P.qh; sa.count_cur = &P.counters[CTR_HIT]; sa.q_next = q_next; sa.count_next = &P.counters[c_next];
+        sa.q_cur = P.qh; sa.count_cur = &P.counters[CTR_HIT]; sa.q_defer = P.qf; sa.count_defer = &P.counters[CTR_FULL];
+        sa.force_defer = cfg.shade_classes == 2 ? 1 : 0;
         {
             TimedScope ts(cfg, st, KT_SHADE);
-            if (hf.options.bsdf_override == MPT_BSDF_LAMBERTIAN)
-                hipLaunchKernelGGL((k_shade<MPT_BSDF_LAMBERTIAN>), dim3(blocks_for(n)), dim3(TB), 0, st, sa);
-            else
-                hipLaunchKernelGGL((k_shade<MPT_BSDF_NONE>), dim3(blocks_for(n)), dim3(TB), 0, st, sa);
+            if (hf.options.bsdf_override == MPT_BSDF_LAMBERTIAN) {
+                hipLaunchKernelGGL((k_shade<MPT_BSDF_LAMBERTIAN, false>), dim3(blocks_for(n)), dim3(TB), 0, st, sa);
+            } else if (!classes) {
+                hipLaunchKernelGGL((k_shade<MPT_BSDF_NONE, false>), dim3(blocks_for(n)), dim3(TB), 0, st, sa);
+            } else {
+                hipLaunchKernelGGL((k_shade<MPT_BSDF_NONE, true>), dim3(blocks_for(n)), dim3(TB), 0, st, sa);
+                ShadeArgs sf = sa;
+                sf.q_cur = P.qf; sf.count_cur = &P.counters[CTR_FULL]; sf.q_defer = nullptr; sf.count_defer = nullptr;
+                hipLaunchKernelGGL((k_shade<MPT_BSDF_NONE, false>), dim3(blocks_for(n)), dim3(TB), 0, st, sf);
+            }
         }
         {
             TimedScope ts(cfg, st, KT_MISS);
@@ -1911,8 +2009,9 @@ hipError_t launch_frame(const DevScene& S, const DevPaths& P0, const MptFrame* d
         }
         {
             TimedScope ts(cfg, st, KT_COMPACT);
-            hipLaunchKernelGGL(k_compact, cp_grid, dim3(CP_NT), 0, st, P, (const int32_t*)P.qh, &P.counters[CTR_HIT], q_next,
-                               &P.counters[c_next]);
+            // the shaded list (qh ++ qf) holds up to 2n entries: deferred vertices appear in both
+            const dim3 cp_grid2((2 * n + CP_NT * CP_ITEMS - 1) / (CP_NT * CP_ITEMS));
+            hipLaunchKernelGGL(k_compact, classes ? cp_grid2 : cp_grid, dim3(CP_NT), 0, st, P, q_next, &P.counters[c_next]);
         }
         // NEE queries
         hipMemsetAsync(&P.counters[CTR_FETCH], 0, sizeof(int32_t), st);
@@ -1922,11 +2021,21 @@ hipError_t launch_frame(const DevScene& S, const DevPaths& P0, const MptFrame* d
         timed_trace<TM_NEE_ANY>(tn, cfg, st);
         hipMemsetAsync(&P.counters[CTR_FETCH], 0, sizeof(int32_t), st);
         tn.count_ptr = &P.counters[CTR_CL];
-        timed_trace<TM_NEE_CLOSEST>(tn, cfg, st);
+        if (cfg.light_bvh) {
+            hipMemsetAsync(&P.counters[CTR_LIGHT], 0, sizeof(int32_t), st);
+            tn.static_grid = cfg.light_static;
+            timed_trace<TM_NEE_LIGHT>(tn, cfg, st);
+            tn.static_grid = 0;
+            hipMemsetAsync(&P.counters[CTR_FETCH], 0, sizeof(int32_t), st);
+            tn.count_ptr = &P.counters[CTR_LIGHT];
+            timed_trace<TM_NEE_LIGHT_OCC>(tn, cfg, st);
+        } else {
+            timed_trace<TM_NEE_CLOSEST>(tn, cfg, st);
+        }
         {
             TimedScope ts(cfg, st, KT_RESOLVE);
-            hipLaunchKernelGGL(k_resolve, dim3(blocks_for(n)), dim3(TB), 0, st, S, P, d_frame, b, (const int32_t*)P.qh,
-                               &P.counters[CTR_HIT], &P.counters[c_cur]);
+            hipLaunchKernelGGL(k_resolve, dim3(blocks_for(classes ? 2 * n : n)), dim3(TB), 0, st, S, P, d_frame, b,
+                               &P.counters[c_cur]);
         }
         // swap queues
         int32_t* tq = q_cur; q_cur = q_next; q_next = tq;
@@ -1950,10 +2059,18 @@ __global__ void k_resolve_materials(DevScene S, MptMaterial* out, int32_t* tex, 
         const int32_t* ti = &m.emission_texture_index;
         for (int k = 0; k < 18; k++) textured |= ti[k] != MPT_NO_TEXTURE;
     }
-    tex[i] = textured;
     DevScene S0 = S;
     S0.n_tex = 0;
-    out[i] = intersection_material(S0, i, mk2(0.0f, 0.0f), false);
+    const Mat r = intersection_material(S0, i, mk2(0.0f, 0.0f), false);
+    out[i] = r;
+    // plain-dielectric class (k_shade): coat, sheen, metallic, transmission and thin film are
+    // zero and no texture can make them non-zero
+    const bool plain = r.coat == 0.0f && r.sheen == 0.0f && r.metallic == 0.0f && r.specular_transmission == 0.0f &&
+                       r.thin_film == 0.0f && m.coat_texture_index == MPT_NO_TEXTURE &&
+                       m.sheen_texture_index == MPT_NO_TEXTURE && m.metallic_texture_index == MPT_NO_TEXTURE &&
+                       m.roughness_metallic_texture_index == MPT_NO_TEXTURE &&
+                       m.specular_transmission_texture_index == MPT_NO_TEXTURE;
+    tex[i] = (textured ? MT_TEXTURED : 0) | (plain ? 0 : MT_FULL);
 }
 
 #ifdef MPT_SECTION_TIMING

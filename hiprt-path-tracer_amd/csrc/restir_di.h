@@ -324,7 +324,7 @@ __global__ __launch_bounds__(TB) void k_gbuffer(DevScene S, DevPaths P, const Mp
         const int mi = S.mat_idx[prim];
         const Mat* mp;
         int per_pixel = 0;
-        if (F.bsdf_flags.white_furnace_mode || S.mat_tex[mi]) {
+        if (F.bsdf_flags.white_furnace_mode || (S.mat_tex[mi] & MT_TEXTURED)) {
             P.gb_mat[gp] = intersection_material(S, mi, tc, F.bsdf_flags.white_furnace_mode);
             mp = &P.gb_mat[gp];
             per_pixel = 1;
