@@ -46,6 +46,11 @@ constexpr int MAX_BOUNDARY_SKIPS = 16;   // trace_ray's volume-boundary skip loo
 #endif
 constexpr int TRACE_REFILL = MPT_TRACE_REFILL;   // idle lanes of a wave that trigger a refill
 constexpr int TRACE_BUDGET = MPT_TRACE_BUDGET;   // nodes a lane opens between refill checks
+#ifndef MPT_TRACE_CHUNK
+#define MPT_TRACE_CHUNK 256
+#endif
+constexpr int TRACE_CHUNK = MPT_TRACE_CHUNK;     // rays a wave claims per atomic on the work counter
+static_assert(TRACE_CHUNK >= 64, "a refill of up to 64 lanes must fit in one new chunk");
 #ifndef MPT_TRI_POSTPONE
 #define MPT_TRI_POSTPONE 3
 #endif
@@ -351,9 +356,12 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MODE == TM_P
     const Node8* bvh_nodes = MODE == TM_NEE_LIGHT ? S.nodes_light : S.nodes;
     const TriRec* bvh_tris = MODE == TM_NEE_LIGHT ? S.tris_light : S.tris;
     // Persistent waves with per-lane ray replacement: a lane whose ray has finished takes
-    // a new one as soon as at least TRACE_REFILL lanes of its wave are idle (one atomic
-    // per refill), instead of the whole wave waiting for its longest ray.  Between refill
-    // checks every lane opens at most TRACE_BUDGET nodes.
+    // a new one as soon as at least TRACE_REFILL lanes of its wave are idle, instead of the
+    // whole wave waiting for its longest ray.  Between refill checks every lane opens at
+    // most TRACE_BUDGET nodes.  A wave claims TRACE_CHUNK consecutive rays per atomic on
+    // the shared counter and serves its refills from that chunk: the device-scope atomic
+    // is a serial point for all 5k waves (one per refill put the short light-BVH
+    // traversals at 12 ns per refill, the counter's throughput).
     Trav<ANY, STATS, TIE> tr;
     bool alive = false;
     bool exhausted = false;   // wave-uniform: the ray counter has passed `count`
@@ -362,6 +370,8 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MODE == TM_P
     uint32_t pseed = 0u;      // PATH: pixel seed of the alpha keys
     bool was_inside = false;  // PATH: kept over re-traces, as in trace_ray's loop
     float qmax = 0.0f;        // NEE closest: the query's t_max
+    int chunk_next = 0, chunk_end = 0;   // wave-uniform: the unserved part of the wave's chunk
+    bool counter_done = false;           // wave-uniform: the shared counter has passed `count`
     while (true) {
         const unsigned long long idle = __ballot(!alive);
         if (!exhausted && __popcll(idle) >= (unsigned)TRACE_REFILL) {
@@ -371,13 +381,29 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MODE == TM_P
                 // one ray per lane, 64 consecutive queries per wave, no refill
                 base = (int)(blockIdx.x * TB + (threadIdx.x & ~63u));
                 exhausted = true;
-            } else {
-                if (lane_id() == 0) base = atomicAdd(A.fetch, need);
-                base = __shfl(base, 0);
-                if (base + need >= count) exhausted = true;
+            }
+            int take0 = need, base1 = 0;
+            if (!(MODE == TM_NEE_LIGHT && A.static_grid)) {
+                // the rest of the chunk first, then (if short) a new chunk
+                base = chunk_next;
+                take0 = min(need, chunk_end - chunk_next);
+                chunk_next += take0;
+                if (take0 < need && !counter_done) {
+                    int b = 0;
+                    if (lane_id() == 0) b = atomicAdd(A.fetch, TRACE_CHUNK);
+                    b = __shfl(b, 0);
+                    counter_done = b + TRACE_CHUNK >= count;
+                    chunk_end = min(b + TRACE_CHUNK, count);
+                    base1 = b;
+                    chunk_next = min(b + (need - take0), chunk_end);
+                } else {
+                    base1 = chunk_end;   // nothing left: the remaining lanes get i >= count
+                }
+                exhausted = counter_done && chunk_next >= chunk_end;
             }
             if (!alive) {
-                const int i = base + __popcll(idle & ((1ull << lane_id()) - 1ull));
+                const int r = __popcll(idle & ((1ull << lane_id()) - 1ull));
+                const int i = r < take0 ? base + r : base1 + (r - take0);
                 if (i < count) {
                     alive = true;
                     n_rays++;
