@@ -298,7 +298,9 @@ def main():
     # rooflines (SURVEY.md §8d algorithmic bytes): every traversal stage and the shade
     # kernel; "roofline" is the one with the largest summed time in the timed region
     names = ["k_trace<TM_PATH> (camera/continuation rays, closest hit)", "k_trace<TM_NEE_ANY> (NEE shadow rays, any hit)",
-             "k_trace<TM_NEE_CLOSEST> (NEE BSDF/light rays, closest hit)"]
+             "k_trace<TM_NEE_LIGHT> + <TM_NEE_LIGHT_OCC> (NEE BSDF light-hit rays: light BVH, then whole-scene any-hit check)"]
+    symbols = ["void mpt::k_trace<0, false>(mpt::TraceArgs)", "void mpt::k_trace<1, false>(mpt::TraceArgs)",
+               "void mpt::k_trace<5, false>(mpt::TraceArgs)"]
     lines = []
     for m in range(3):
         q_cal = max(1, cal.stage_rays[m])
@@ -307,19 +309,22 @@ def main():
         launches = max(1, st.stage_launches[m])
         avg_ms = st.stage_ms[m] / launches
         ach = st.stage_rays[m] * b_ray / launches / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
-        lines.append({"kernel": names[m], "symbol": f"void mpt::k_trace<{m}, false>(mpt::TraceArgs)", "total_ms": st.stage_ms[m], "achieved": ach, "avg_launch_ms": avg_ms,
+        lines.append({"kernel": names[m], "symbol": symbols[m], "total_ms": st.stage_ms[m], "achieved": ach, "avg_launch_ms": avg_ms,
                       "bytes_per_unit": b_ray, "unit_of_work": "ray", "nodes_per_ray": n_node, "tris_per_ray": n_tri,
                       "node_simd_util": cal.stage_nodes[m] / max(1, cal.stage_node_slots[m]),
                       "tri_simd_util": cal.stage_tris[m] / max(1, cal.stage_tri_slots[m]),
                       "units_per_launch": st.stage_rays[m] / launches})
     # shade: per path vertex (a path ray that hit a surface: k_split sends the misses to
-    # k_miss) = material 256 + vertex gathers 12+36+36+24 + path state 2x96 (§8d)
+    # k_miss) = material 256 + vertex gathers 12+36+36+24 + path state 2x96 (§8d); the
+    # plain-dielectric kernel (material classes) shades all but the generic
+    # class's vertices
     b_vtx = 256 + 12 + 36 + 36 + 24 + 2 * 96
     sl = max(1, st.shade_launches)
     s_avg = st.shade_ms / sl
-    hits = st.path_hits or st.stage_rays[0]
-    lines.append({"kernel": "k_shade<BSDF_NONE> (path vertex: hit, NEE sampling, BSDF sampling, RR)",
-                  "symbol": "void mpt::k_shade<0>(mpt::ShadeArgs)",
+    hits = (st.path_hits or st.stage_rays[0]) - st.shade_generic_vertices
+    lines.append({"kernel": "k_shade<BSDF_NONE, plain> (path vertex of a plain-dielectric material: hit, NEE sampling, "
+                            "BSDF sampling, RR)",
+                  "symbol": "void mpt::k_shade<0, true>(mpt::ShadeArgs)",
                   "total_ms": st.shade_ms, "avg_launch_ms": s_avg, "bytes_per_unit": b_vtx, "unit_of_work": "path vertex (hit)",
                   "units_per_launch": hits / sl,
                   "achieved": hits * b_vtx / sl / (s_avg * 1e-3) / 1e9 if s_avg > 0 else 0.0})
@@ -400,6 +405,7 @@ def main():
                                   "tri_simd_util": round(x["tri_simd_util"], 3)} for x in lines[:3]],
             "kernel_ms_per_step": {"trace_path": round(st.stage_ms[0] / K, 4), "trace_nee_any": round(st.stage_ms[1] / K, 4),
                                    "trace_nee_closest": round(st.stage_ms[2] / K, 4), "shade": round(st.shade_ms / K, 4),
+                                   "shade_generic": round(st.shade_generic_ms / K, 4),
                                    "resolve": round(st.resolve_ms / K, 4), "camera": round(st.camera_ms / K, 4),
                                    "accumulate": round(st.accumulate_ms / K, 4),
                                    "compact": round(st.compact_ms / K, 4), "split": round(st.split_ms / K, 4),

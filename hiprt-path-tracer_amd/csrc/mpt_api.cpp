@@ -66,9 +66,10 @@ struct DBuf {
 };
 
 constexpr int FRAME_RING = 256;   // >= 2 x MPT_MAX_BATCH
-// timing events per frame: one pair per kernel, 8 per bounce (3 traversals, split, shade,
-// miss, compact, resolve) for up to 65 bounces (validate_frame), + camera, ReSTIR, accumulate
-constexpr int EV_POOL = 2 * (8 * 65 + 3);
+// timing events per frame: one pair per timed launch, 10 per bounce (path, any-hit and two
+// light-hit traversals, split, plain and generic shade, miss, compact, resolve) for up to 65
+// bounces (validate_frame), + camera, ReSTIR, accumulate
+constexpr int EV_POOL = 2 * (10 * 65 + 3);
 #ifndef MPT_TRACE_BLOCKS_PER_CU
 #define MPT_TRACE_BLOCKS_PER_CU 5
 #endif
@@ -626,10 +627,10 @@ static int create_context(MptContext* c, int device, void* hip_stream) {
     HIPCHK(c->fetch_raw.alloc(4));
     HIPCHK(c->stats.alloc(N_STATS));
     HIPCHK(hipMemsetAsync(c->stats.p, 0, N_STATS * sizeof(uint64_t), c->stream));
-    HIPCHK(c->ray_counts.alloc(4));
+    HIPCHK(c->ray_counts.alloc(N_RAY_COUNTS));
     HIPCHK(c->status.alloc(4));
     HIPCHK(hipMemsetAsync(c->status.p, 0, 4 * sizeof(uint32_t), c->stream));
-    HIPCHK(hipMemsetAsync(c->ray_counts.p, 0, 4 * sizeof(uint64_t), c->stream));
+    HIPCHK(hipMemsetAsync(c->ray_counts.p, 0, N_RAY_COUNTS * sizeof(uint64_t), c->stream));
     HIPCHK(c->spill.alloc((size_t)c->grid * TRAV_BLOCK * SPILL_WORDS));
     for (int p = 0; p < 2; p++) {
         for (int i = 0; i < EV_POOL; i++) HIPCHK(hipEventCreate(&c->ev[p][i]));
@@ -1125,7 +1126,7 @@ int mpt_enable_stats(MptContext* c, int enable, int instrumented) {
     c->frame_ms = 0.0;
     for (int m = 0; m < KT_COUNT; m++) { c->stage_ms[m] = 0.0; c->stage_launches[m] = 0; }
     HIPCHK(hipMemsetAsync(c->stats.p, 0, N_STATS * sizeof(uint64_t), c->stream));
-    HIPCHK(hipMemsetAsync(c->ray_counts.p, 0, 4 * sizeof(uint64_t), c->stream));
+    HIPCHK(hipMemsetAsync(c->ray_counts.p, 0, N_RAY_COUNTS * sizeof(uint64_t), c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     return MPT_OK;
 }
@@ -1141,7 +1142,7 @@ int mpt_get_stats(MptContext* c, MptStats* out) {
     std::memset(out, 0, sizeof(*out));
     uint64_t s[N_STATS];
     HIPCHK(hipMemcpy(s, c->stats.p, sizeof(s), hipMemcpyDeviceToHost));
-    uint64_t rc[4];
+    uint64_t rc[N_RAY_COUNTS];
     HIPCHK(hipMemcpy(rc, c->ray_counts.p, sizeof(rc), hipMemcpyDeviceToHost));
     out->rays_closest = rc[0] + rc[2];
     out->rays_any = rc[1];
@@ -1167,6 +1168,8 @@ int mpt_get_stats(MptContext* c, MptStats* out) {
     out->split_ms = c->stage_ms[KT_SPLIT];
     out->miss_ms = c->stage_ms[KT_MISS];
     out->path_hits = rc[3];
+    out->shade_generic_vertices = rc[4];
+    out->shade_generic_ms = c->stage_ms[KT_SHADE_GENERIC];
     out->shade_launches = c->stage_launches[KT_SHADE];
     out->trace_launches = c->trace_launches;
     out->frames = c->frames;

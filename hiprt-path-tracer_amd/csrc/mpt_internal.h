@@ -128,7 +128,7 @@ struct DevPaths {
     float* fb_normal;
     uint32_t* stack_spill;    // global spill area of the traversal stacks
     uint64_t* stats;          // [trace mode][rays, nodes, tris, -] (instrumented traversal)
-    uint64_t* ray_counts;     // path rays, NEE any-hit rays, NEE closest rays, path hits (always on)
+    uint64_t* ray_counts;     // path rays, NEE any-hit rays, NEE closest rays, path hits, generic-class vertices (always on)
     // adaptive sampling / stop-noise threshold (AuxiliaryBuffers, RenderData.h:62-84)
     int32_t* as_count;        // pixel_sample_count
     float* as_sqlum;          // pixel_squared_luminance
@@ -162,9 +162,10 @@ struct DevPaths {
 };
 
 constexpr int N_TRACE_MODES = 5;
+constexpr int N_RAY_COUNTS = 5;   // DevPaths::ray_counts
 // timed kernel kinds: 0..2 = traversal stages (trace modes), then the others
 enum { KT_CAMERA = 3, KT_SHADE = 4, KT_RESOLVE = 5, KT_ACCUMULATE = 6, KT_COMPACT = 7, KT_RESTIR = 8, KT_SPLIT = 9,
-       KT_MISS = 10, KT_COUNT = 11 };
+       KT_MISS = 10, KT_SHADE_GENERIC = 11, KT_COUNT = 12 };
 constexpr uint32_t QM_CONT = 16u;
 // mat_tex bits: a texture feeds the resolved material; the material is outside the
 // plain-dielectric class (coat, sheen, metallic, transmission or thin film may be non-zero)

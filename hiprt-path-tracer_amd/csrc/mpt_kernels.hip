@@ -1659,6 +1659,7 @@ __global__ __launch_bounds__(TB) void k_resolve(DevScene S, DevPaths P, const Mp
         P.ray_counts[1] += (uint64_t)P.counters[CTR_ANY];
         P.ray_counts[2] += (uint64_t)P.counters[CTR_CL];
         P.ray_counts[3] += (uint64_t)(shaded_count(P) - P.counters[CTR_DEFER]);
+        P.ray_counts[4] += (uint64_t)P.counters[CTR_FULL];
     }
     const int nh = P.counters[CTR_HIT];
     if (i >= nh + P.counters[CTR_FULL]) return;
@@ -2024,10 +2025,13 @@ hipError_t launch_frame(const DevScene& S, const DevPaths& P0, const MptFrame* d
                 hipLaunchKernelGGL((k_shade<MPT_BSDF_NONE, false>), dim3(blocks_for(n)), dim3(TB), 0, st, sa);
             } else {
                 hipLaunchKernelGGL((k_shade<MPT_BSDF_NONE, true>), dim3(blocks_for(n)), dim3(TB), 0, st, sa);
-                ShadeArgs sf = sa;
-                sf.q_cur = P.qf; sf.count_cur = &P.counters[CTR_FULL]; sf.q_defer = nullptr; sf.count_defer = nullptr;
-                hipLaunchKernelGGL((k_shade<MPT_BSDF_NONE, false>), dim3(blocks_for(n)), dim3(TB), 0, st, sf);
             }
+        }
+        if (classes) {
+            TimedScope ts(cfg, st, KT_SHADE_GENERIC);
+            ShadeArgs sf = sa;
+            sf.q_cur = P.qf; sf.count_cur = &P.counters[CTR_FULL]; sf.q_defer = nullptr; sf.count_defer = nullptr;
+            hipLaunchKernelGGL((k_shade<MPT_BSDF_NONE, false>), dim3(blocks_for(n)), dim3(TB), 0, st, sf);
         }
         {
             TimedScope ts(cfg, st, KT_MISS);

@@ -426,6 +426,11 @@ typedef struct MptStats {
     uint64_t path_hits;
     double split_ms;            /* hit / miss partition of the path queue */
     double miss_ms;             /* miss shading (sky / envmap) */
+    /* material-class shading: shade_ms / shade_launches time the plain-dielectric kernel
+     * (the Lambert override and MPT_SHADE_CLASSES=0: the one shading kernel), these the
+     * generic-material kernel and the vertices it shaded */
+    double shade_generic_ms;
+    uint64_t shade_generic_vertices;
 } MptStats;
 
 #define MPT_FB_COLOR 0        /* 'pixels': running SUM of samples (RenderData.h:34-36) */
