@@ -89,6 +89,7 @@ struct MptContext {
     BVH8 bvh;
     DBuf<Node8> nodes;
     DBuf<TriRec> tris;
+    DBuf<float4> tri_attr;               // 5 per triangle (launch_tri_attr)
     // light-hit BVH (k_trace TM_NEE_LIGHT): the triangles whose emission can be non-black
     BVH8 bvh_light;
     DBuf<Node8> nodes_light;
@@ -117,8 +118,7 @@ struct MptContext {
     // luts / envmap
     DBuf<float> lut_conductor, lut_glossy, lut_glass, lut_glass_inv, lut_thin, lut_sheen;
     DBuf<float4> env;
-    DBuf<float> alias_p;
-    DBuf<int32_t> alias_i;
+    DBuf<int2> alias;
     DBuf<float> env_cdf;
     float env_cdf_sum = 0.0f;
     int env_w = 0, env_h = 0;
@@ -193,6 +193,7 @@ DevScene dev_scene(MptContext* c) {
     S.has_n = c->has_n.p;
     S.uv = c->uv.p;
     S.mat_idx = c->mat_idx.p;
+    S.tri_attr = c->tri_attr.p;
     S.mats = c->mats.p;
     S.mats_res = c->mats_res.p;
     S.mat_tex = c->mat_tex.p;
@@ -212,8 +213,7 @@ DevScene dev_scene(MptContext* c) {
     S.lut_thin_glass = c->lut_thin.p;
     S.lut_sheen = c->lut_sheen.p;
     S.env = c->env.p;
-    S.alias_p = c->alias_p.p;
-    S.alias_i = c->alias_i.p;
+    S.alias = c->alias.p;
     S.env_w = c->env_w;
     S.env_h = c->env_h;
     S.env_sum = c->env_sum;
@@ -721,6 +721,8 @@ int mpt_upload_scene(MptContext* c, const MptScene* s) {
     HIPCHK(c->uv.upload(uv, 2 * (size_t)s->num_vertices, st));
     HIPCHK(c->has_n.upload(hn, (size_t)s->num_vertices, st));
     HIPCHK(c->mat_idx.upload(s->material_indices, (size_t)s->num_triangles, st));
+    HIPCHK(c->tri_attr.alloc(5 * (size_t)s->num_triangles));
+    HIPCHK(launch_tri_attr(dev_scene(c), c->tri_attr.p, st));
     c->h_mat_idx.assign(s->material_indices, s->material_indices + s->num_triangles);
     c->h_mats.assign(s->materials, s->materials + s->num_materials);
     HIPCHK(c->mats.upload(c->h_mats.data(), c->h_mats.size(), st));
@@ -817,7 +819,7 @@ int mpt_set_envmap(MptContext* c, const float* rgba, int32_t w, int32_t h, const
     if (!c) return fail(MPT_ERR_INVALID_ARGUMENT, "NULL context");
     HIPCHK(hipSetDevice(c->device));
     if (!rgba || w <= 0 || h <= 0) {
-        c->env.release(); c->alias_p.release(); c->alias_i.release(); c->env_cdf.release();
+        c->env.release(); c->alias.release(); c->env_cdf.release();
         c->env_w = c->env_h = 0;
         return MPT_OK;
     }
@@ -828,11 +830,16 @@ int mpt_set_envmap(MptContext* c, const float* rgba, int32_t w, int32_t h, const
             // entries never reached by Vose's loop keep probability 1 and are never aliased
             if (probas[i] < 1.0f) return fail(MPT_ERR_INVALID_ARGUMENT, "alias index out of range");
         }
-    std::vector<int32_t> al(alias, alias + n);
-    for (size_t i = 0; i < n; i++) if (al[i] < 0 || (size_t)al[i] >= n) al[i] = (int32_t)i;
+    // interleaved (probability, alias) pairs: the sampler reads both with one load
+    std::vector<int2> pa(n);
+    for (size_t i = 0; i < n; i++) {
+        int32_t a = (alias[i] < 0 || (size_t)alias[i] >= n) ? (int32_t)i : alias[i];
+        int32_t pb;
+        std::memcpy(&pb, &probas[i], 4);
+        pa[i] = make_int2(pb, a);
+    }
     HIPCHK(c->env.upload(reinterpret_cast<const float4*>(rgba), n, c->stream));
-    HIPCHK(c->alias_p.upload(probas, n, c->stream));
-    HIPCHK(c->alias_i.upload(al.data(), n, c->stream));
+    HIPCHK(c->alias.upload(pa.data(), n, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     c->env_w = w;
     c->env_h = h;

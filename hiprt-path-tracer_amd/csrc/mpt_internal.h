@@ -35,6 +35,7 @@ struct DevScene {
     const uint8_t* has_n;
     const float* uv;             // 2 per vertex
     const int32_t* mat_idx;      // per triangle
+    const float4* tri_attr;      // per triangle: 5 float4 of hit attributes (k_tri_attr / hit_attributes)
     const MptMaterial* mats;
     const MptMaterial* mats_res;  // per material: intersection-time resolution without textures
     const int32_t* mat_tex;       // per material: MT_TEXTURED | MT_FULL (k_resolve_materials)
@@ -56,8 +57,7 @@ struct DevScene {
     const float* lut_sheen;
     // envmap
     const float4* env;
-    const float* alias_p;
-    const int32_t* alias_i;
+    const int2* alias;            // alias table, one entry per texel: (probability bits, alias index)
     int32_t env_w, env_h;
     float env_sum;
     const float* env_cdf;         // ESS_BINARY_SEARCH: running luminance sum per texel (Image.cpp:553-574)
@@ -213,6 +213,7 @@ hipError_t launch_resolve_materials(const DevScene& S, MptMaterial* out_res, int
 hipError_t launch_restir_fill(float4* reservoirs, int n, hipStream_t st);
 hipError_t launch_restir_fill_lights(float4* lights, int n, hipStream_t st);
 hipError_t launch_bake(int kind, int w, int h, int d, int ipk, int nb_samples, int iteration, float* out, hipStream_t st);
+hipError_t launch_tri_attr(const DevScene& S, float4* out, hipStream_t st);
 hipError_t launch_trace_raw(const DevScene& S, const float4* o, const float4* d, int n, bool any, float4* out_hit,
                             uint8_t* out_occ, int32_t* fetch_ctr, uint32_t* spill, int grid, hipStream_t st);
 

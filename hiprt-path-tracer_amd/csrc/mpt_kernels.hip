@@ -545,11 +545,18 @@ DEV bool has_tex(int ti) { return ti != MPT_NO_TEXTURE && ti != MPT_CONSTANT_EMI
 // filter_function's test: keep the candidate iff u < alpha_opacity * base-colour alpha
 // (get_hit_base_color_alpha, Material.h:23-37; the sRGB pow(2.2) of Texture.h:72-75 also
 // applies to the alpha channel)
+// interpolated texture coordinates from the triangle's attribute record (k_tri_attr):
+// uv_interp2's values and arithmetic, without the index gather
+DEV v2 attr_tc(const DevScene& S, int prim, v2 uv) {
+    const float4* r = S.tri_attr + 5 * (size_t)prim;
+    const float4 c = r[2], d = r[3];
+    return mk2(c.w, d.x) * uv.x + mk2(d.y, d.z) * uv.y + mk2(c.y, c.z) * (1.0f - uv.x - uv.y);
+}
 DEV bool alpha_rejects(const DevScene& S, int prim, float u, float v, uint32_t key) {
     const Mat& m = S.mats[S.mat_idx[prim]];
     float a = 1.0f;
     if (S.n_tex > 0 && has_tex(m.base_color_texture_index)) {
-        v2 tc = uv_interp2(S.uv, tri_idx(S, prim), mk2(u, v));
+        v2 tc = attr_tc(S, prim, mk2(u, v));
         float r[4];
         tex_rgba(S, m.base_color_texture_index, true, tc, r);
         a = r[3];
@@ -613,22 +620,64 @@ DEV Mat intersection_material(const DevScene& S, int mi, v2 uv, bool white_furna
     return m;
 }
 
+// normal_mapping (Texture.h:209-222): tangent frame from the triangle's positions and uvs
+DEV v3 normal_mapped(const DevScene& S, const Mat& m, v3 n, int p, v2 tc) {
+    int3 t = tri_idx(S, p);
+    v2 d1 = ld2(S.uv, t.y) - ld2(S.uv, t.x), d2 = ld2(S.uv, t.z) - ld2(S.uv, t.x);
+    v3 e1 = ld3(S.pos, t.y) - ld3(S.pos, t.x), e2 = ld3(S.pos, t.z) - ld3(S.pos, t.x);
+    float di = 1.0f / (d1.x * d2.y - d1.y * d2.x);
+    v3 T = (e1 * d2.y - e2 * d1.y) * di;
+    v3 B = (e2 * d1.x - e1 * d2.x) * di;
+    float r[4];
+    tex_rgba(S, m.normal_map_texture_index, false, tc, r);
+    v3 ts = normalize(mk3(r[0] - 0.5f, r[1] - 0.5f, r[2] - 0.5f));
+    return to_world(normalize(T), normalize(B), n, ts);
+}
 DEV v3 shading_normal_of(const DevScene& S, v3 gn, int p, v2 uv, v2 tc) {
     int3 t = tri_idx(S, p);
     const Mat& m = S.mats[S.mat_idx[p]];
     v3 n = S.has_n[t.x] ? normalize(uv_interp3(S.nrm, t, uv)) : gn;
-    if (S.n_tex > 0 && m.normal_map_texture_index != MPT_NO_TEXTURE) {
-        v2 d1 = ld2(S.uv, t.y) - ld2(S.uv, t.x), d2 = ld2(S.uv, t.z) - ld2(S.uv, t.x);
-        v3 e1 = ld3(S.pos, t.y) - ld3(S.pos, t.x), e2 = ld3(S.pos, t.z) - ld3(S.pos, t.x);
-        float di = 1.0f / (d1.x * d2.y - d1.y * d2.x);
-        v3 T = (e1 * d2.y - e2 * d1.y) * di;
-        v3 B = (e2 * d1.x - e1 * d2.x) * di;
-        float r[4];
-        tex_rgba(S, m.normal_map_texture_index, false, tc, r);
-        v3 ts = normalize(mk3(r[0] - 0.5f, r[1] - 0.5f, r[2] - 0.5f));
-        n = to_world(normalize(T), normalize(B), n, ts);
-    }
+    if (S.n_tex > 0 && m.normal_map_texture_index != MPT_NO_TEXTURE) n = normal_mapped(S, m, n, p, tc);
     return n;
+}
+
+// The vertex attributes trace_ray reads at a hit (Intersect.h:30-83, 154-192) from the
+// triangle's attribute record (k_tri_attr, 5 float4: the three vertex normals, the three
+// texture coordinates, has_vertex_normals of vertex A, the normalised geometric normal,
+// the material index): one 80-B read at the primitive index replaces the index triple and
+// the nine dependent vertex gathers.  Same values, same arithmetic as uv_interp2 /
+// tri_normal / shading_normal_of (bit-identical).
+struct HitAttr { v2 tc; v3 gn, sn; int mi; };
+DEV HitAttr hit_attributes(const DevScene& S, int prim, v2 uv) {
+    const float4* r = S.tri_attr + 5 * (size_t)prim;
+    const float4 a = r[0], b = r[1], c = r[2], d = r[3], e = r[4];
+    const v3 n0 = mk3(a.x, a.y, a.z), n1 = mk3(a.w, b.x, b.y), n2 = mk3(b.z, b.w, c.x);
+    const v2 t0 = mk2(c.y, c.z), t1 = mk2(c.w, d.x), t2 = mk2(d.y, d.z);
+    HitAttr h;
+    h.tc = t1 * uv.x + t2 * uv.y + t0 * (1.0f - uv.x - uv.y);
+    h.gn = normalize(mk3(e.x, e.y, e.z));
+    h.mi = __float_as_int(e.w);
+    v3 n = __float_as_uint(d.w) ? normalize(n1 * uv.x + n2 * uv.y + n0 * (1.0f - uv.x - uv.y)) : h.gn;
+    if (S.n_tex > 0) {
+        const Mat& m = S.mats[h.mi];
+        if (m.normal_map_texture_index != MPT_NO_TEXTURE) n = normal_mapped(S, m, n, prim, h.tc);
+    }
+    h.sn = n;
+    return h;
+}
+__global__ void k_tri_attr(DevScene S, float4* out) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= S.n_tris) return;
+    const int3 t = tri_idx(S, p);
+    const v3 n0 = ld3(S.nrm, t.x), n1 = ld3(S.nrm, t.y), n2 = ld3(S.nrm, t.z);
+    const v2 t0 = ld2(S.uv, t.x), t1 = ld2(S.uv, t.y), t2 = ld2(S.uv, t.z);
+    const v3 g = tri_normal(S, p);
+    float4* r = out + 5 * (size_t)p;
+    r[0] = make_float4(n0.x, n0.y, n0.z, n1.x);
+    r[1] = make_float4(n1.y, n1.z, n2.x, n2.y);
+    r[2] = make_float4(n2.z, t0.x, t0.y, t1.x);
+    r[3] = make_float4(t1.y, t2.x, t2.y, __uint_as_float(S.has_n[t.x] ? 1u : 0u));
+    r[4] = make_float4(g.x, g.y, g.z, __int_as_float(S.mat_idx[p]));
 }
 
 // slot -> pixel of the band partition (rows y with (y / bh) % bc == bi, increasing y)
@@ -890,8 +939,8 @@ DEV Col env_sample(const DevScene& S, const MptFrame& F, v3& dir, float& pdf, Rn
         env_cdf_search(S, rng() * S.env_cdf_sum, x, y);
     } else {
         int ri = rng.random_index(S.env_h * S.env_w);
-        float prob = S.alias_p[ri];
-        if (rng() > prob) ri = S.alias_i[ri];
+        const int2 e = S.alias[ri];   // one 8-B load: probability bits + alias index
+        if (rng() > __int_as_float(e.x)) ri = e.y;
         y = (int)((unsigned)ri / (unsigned)S.env_w);
         x = ri - y * S.env_w;
     }
@@ -1058,12 +1107,12 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_
             // trace_ray hit processing (Intersect.h:154-216)
             float t = hv.x;
             v2 uv = mk2(hv.y, hv.z);
-            int3 ti = tri_idx(S, prim);
             ip = o + t * d;
-            v2 tc = uv_interp2(S.uv, ti, uv);
-            gn = normalize(tri_normal(S, prim));
-            sn = shading_normal_of(S, gn, prim, uv, tc);
-            const int mi = S.mat_idx[prim];
+            const HitAttr ha = hit_attributes(S, prim, uv);
+            const v2 tc = ha.tc;
+            gn = ha.gn;
+            sn = ha.sn;
+            const int mi = ha.mi;
             if (F.bsdf_flags.white_furnace_mode || (S.mat_tex[mi] & MT_TEXTURED)) {
                 P.mat_slot[slot] = intersection_material(S, mi, tc, F.bsdf_flags.white_furnace_mode);
                 mp = &P.mat_slot[slot];
@@ -1619,16 +1668,16 @@ struct ShadowLightHit { int prim; float dist; v3 sn; Col em; };
 DEV bool shadow_light_hit(const DevScene& S, float4 h, ShadowLightHit& out) {
     int prim = (int)__float_as_uint(h.w);
     if (prim < 0) return false;
-    const Mat& m = S.mats[S.mat_idx[prim]];
-    int3 ti = tri_idx(S, prim);
     v2 uv = mk2(h.y, h.z);
-    v2 tc = uv_interp2(S.uv, ti, uv);
+    const HitAttr ha = hit_attributes(S, prim, uv);
+    const Mat& m = S.mats[ha.mi];
+    const v2 tc = ha.tc;
     if (m.emission_texture_index != MPT_NO_TEXTURE) {
         MptColor e; e.r = 0.0f; e.g = 0.0f; e.b = 0.0f;
         if (S.n_tex > 0) prop_c(S, e, tc, m.emission_texture_index);
         out.em = C3(e);
     } else out.em = emission_of(m);
-    out.sn = shading_normal_of(S, normalize(tri_normal(S, prim)), prim, uv, tc);
+    out.sn = ha.sn;
     out.prim = prim;
     out.dist = h.x;
     return true;
@@ -2154,6 +2203,11 @@ hipError_t launch_resolve_materials(const DevScene& S, MptMaterial* out_res, int
     hipLaunchKernelGGL(k_resolve_materials, dim3((n + 63) / 64), dim3(64), 0, st, S, out_res, out_tex, n);
     if (S.n_emissive > 0)
         hipLaunchKernelGGL(k_emissive_table, dim3((S.n_emissive + 63) / 64), dim3(64), 0, st, S, em_tab);
+    return hipGetLastError();
+}
+
+hipError_t launch_tri_attr(const DevScene& S, float4* out, hipStream_t st) {
+    hipLaunchKernelGGL(k_tri_attr, dim3((S.n_tris + 255) / 256), dim3(256), 0, st, S, out);
     return hipGetLastError();
 }
 

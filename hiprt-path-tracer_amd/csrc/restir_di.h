@@ -316,12 +316,12 @@ __global__ __launch_bounds__(TB) void k_gbuffer(DevScene S, DevPaths P, const Mp
         Rng rng = make_rng(P.rng[slot]);
         float t = hv.x;
         v2 uv = mk2(hv.y, hv.z);
-        int3 ti = tri_idx(S, prim);
         v3 ip = o + t * d;
-        v2 tc = uv_interp2(S.uv, ti, uv);
-        v3 gn = normalize(tri_normal(S, prim));
-        v3 sn = shading_normal_of(S, gn, prim, uv, tc);
-        const int mi = S.mat_idx[prim];
+        const HitAttr ha = hit_attributes(S, prim, uv);
+        const v2 tc = ha.tc;
+        v3 gn = ha.gn;
+        v3 sn = ha.sn;
+        const int mi = ha.mi;
         const Mat* mp;
         int per_pixel = 0;
         if (F.bsdf_flags.white_furnace_mode || (S.mat_tex[mi] & MT_TEXTURED)) {
