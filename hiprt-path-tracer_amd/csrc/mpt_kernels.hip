@@ -1868,8 +1868,14 @@ static int blocks_for(int n) { return (n + TB - 1) / TB; }
 
 template <int MODE>
 static void launch_trace_mode(const TraceArgs& a, int grid, bool stats, hipStream_t st) {
-    if (MODE == TM_NEE_LIGHT && a.static_grid) grid = blocks_for(a.P.n);   // the query list holds at most n entries
-    if (stats) hipLaunchKernelGGL((k_trace<MODE, true>), dim3(grid), dim3(TB), 0, st, a);
+    if (MODE == TM_NEE_LIGHT && a.static_grid && !stats) grid = blocks_for(a.P.n);   // the query list holds at most n entries
+    if (stats) {
+        // instrumented (calibration) launches stay persistent: their per-wave counter atomics
+        // over a static grid of ~500 k waves would serialise the launch
+        TraceArgs b = a;
+        b.static_grid = 0;
+        hipLaunchKernelGGL((k_trace<MODE, true>), dim3(grid), dim3(TB), 0, st, b);
+    }
     else hipLaunchKernelGGL((k_trace<MODE, false>), dim3(grid), dim3(TB), 0, st, a);
 }
 
