@@ -695,7 +695,10 @@ int mpt_upload_scene(MptContext* c, const MptScene* s) {
         if (s->emissive_triangle_indices[i] < 0 || s->emissive_triangle_indices[i] >= s->num_triangles)
             return fail(MPT_ERR_INVALID_ARGUMENT, "emissive triangle index out of range");
     HIPCHK(hipSetDevice(c->device));
-    build_bvh8(s->vertices, s->triangle_indices, s->num_triangles, c->bvh, 3);
+    // triangles per leaf child: 3 (MPT_BVH_LEAF, 1..4, development A/B)
+    int max_leaf = 3;
+    if (const char* e = std::getenv("MPT_BVH_LEAF")) max_leaf = std::max(1, std::min(4, std::atoi(e)));
+    build_bvh8(s->vertices, s->triangle_indices, s->num_triangles, c->bvh, max_leaf);
     c->box_pad = scene_box_pad(s->vertices, s->num_triangles, s->triangle_indices);
     c->h_idx.assign(s->triangle_indices, s->triangle_indices + 3 * (size_t)s->num_triangles);
     c->h_pos.assign(s->vertices, s->vertices + 3 * (size_t)s->num_vertices);
