@@ -69,7 +69,7 @@ constexpr int FRAME_RING = 256;   // >= 2 x MPT_MAX_BATCH
 // timing events per frame: one pair per timed launch, 10 per bounce (path, any-hit and two
 // light-hit traversals, split, plain and generic shade, miss, compact, resolve) for up to 65
 // bounces (validate_frame), + camera, ReSTIR, accumulate
-constexpr int EV_POOL = 2 * (10 * 65 + 3);
+constexpr int EV_POOL = 2 * 2 * (10 * 65 + 3);   // x2: the two halves of an overlapped batch
 #ifndef MPT_TRACE_BLOCKS_PER_CU
 #define MPT_TRACE_BLOCKS_PER_CU 5
 #endif
@@ -82,6 +82,12 @@ struct MptContext {
     int device = 0;
     hipStream_t stream = nullptr;
     bool own_stream = false;
+    // overlapped batches (MPT_OVERLAP at mpt_create): the second half of a sample batch runs
+    // on stream2, one pipeline stage behind the first, so that shading waves of one half and
+    // traversal waves of the other share the CUs
+    int overlap = 0;   // opt-in: +1.2 % on C3, but per-kernel times then overlap
+    hipStream_t stream2 = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_first = nullptr, ev_acc = nullptr, ev_join = nullptr;
     int num_cus = 256;
     int grid = 1024;
     // scene
@@ -129,7 +135,7 @@ struct MptContext {
     int batch = 1;          // samples of the launch being set up
     DBuf<float4> ray_o, ray_d, hit, thr, col, alb, nrmv, nq_o, nq_d, nhit;
     DBuf<uint8_t> hit_inside, occ, qmask;
-    DBuf<uint32_t> rng, spill;
+    DBuf<uint32_t> rng, spill, spill2;
     DBuf<uint4> vsA, vsB;
     DBuf<int32_t> q0, q1, qh, qm, qf, nq_light, counters, nq_tgt, fetch_raw;
     DBuf<NeeRec> nee;
@@ -622,8 +628,8 @@ static int create_context(MptContext* c, int device, void* hip_stream) {
     else { HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)); c->own_stream = true; }
     HIPCHK(hipHostMalloc((void**)&c->h_frames, sizeof(MptFrame) * FRAME_RING));
     HIPCHK(hipMalloc((void**)&c->d_frames, sizeof(MptFrame) * FRAME_RING));
-    HIPCHK(c->counters.alloc(CTR_COUNT));
-    HIPCHK(hipMemsetAsync(c->counters.p, 0, CTR_COUNT * sizeof(int32_t), c->stream));
+    HIPCHK(c->counters.alloc(2 * CTR_COUNT));   // second set: the second half of an overlapped batch
+    HIPCHK(hipMemsetAsync(c->counters.p, 0, 2 * CTR_COUNT * sizeof(int32_t), c->stream));
     HIPCHK(c->fetch_raw.alloc(4));
     HIPCHK(c->stats.alloc(N_STATS));
     HIPCHK(hipMemsetAsync(c->stats.p, 0, N_STATS * sizeof(uint64_t), c->stream));
@@ -648,6 +654,7 @@ int mpt_create(int device, void* hip_stream, MptContext** out) {
     MptContext* c = new MptContext();   // value-initialised: every handle starts null
     if (const char* e = std::getenv("MPT_SHADE_CLASSES")) c->shade_classes = std::atoi(e);
     if (const char* e = std::getenv("MPT_LIGHT_BVH")) c->light_bvh = std::atoi(e);
+    if (const char* e = std::getenv("MPT_OVERLAP")) c->overlap = std::atoi(e);
     int r = create_context(c, device, hip_stream);
     if (r != MPT_OK) {
         const std::string msg = g_err;
@@ -675,6 +682,9 @@ int mpt_destroy(MptContext* c) {
     if (c->h_reproj) (void)hipHostFree(c->h_reproj);
     if (c->d_frames) (void)hipFree(c->d_frames);
     if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
+    if (c->stream2) (void)hipStreamDestroy(c->stream2);
+    for (hipEvent_t e : {c->ev_fork, c->ev_first, c->ev_acc, c->ev_join})
+        if (e) (void)hipEventDestroy(e);
     delete c;
     (void)hipGetLastError();
     return MPT_OK;
@@ -948,6 +958,27 @@ static int prepare_batch(MptContext* c, const MptFrame* f, int batch) {
     return ensure_batch(c, batch, c->any_tex || f->bsdf_flags.white_furnace_mode);
 }
 
+// The second stream, its events and traversal spill area (overlapped batches), on first use.
+static int ensure_overlap(MptContext* c) {
+    if (c->stream2) return MPT_OK;
+    HIPCHK(c->spill2.alloc(c->spill.n));
+    for (hipEvent_t* e : {&c->ev_fork, &c->ev_first, &c->ev_acc, &c->ev_join})
+        HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+    HIPCHK(hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking));
+    return MPT_OK;
+}
+
+// Moves every per-slot pointer of P by `off` slots (the second half of an overlapped batch
+// owns slots [off, off + P.n) of the path state; per-pixel buffers stay shared).
+static void offset_slots(DevPaths& P, size_t off) {
+    P.ray_o += off; P.ray_d += off; P.hit += off; P.hit_inside += off; P.rng += off; P.thr += off; P.col += off;
+    P.vsA += off; P.vsB += off; P.alb += off; P.nrm += off;
+    P.q0 += off; P.q1 += off; P.qh += off; P.qm += off; P.qf += off; P.nq_light += off;
+    P.nee += off; P.nq_o += 4 * off; P.nq_d += 4 * off; P.nq_tgt += 4 * off; P.occ += 4 * off;
+    P.nhit += off; P.qmask += off; P.active += off;
+    if (P.mat_slot) P.mat_slot += off;
+}
+
 // Enqueues a prepared wavefront (prepare_batch).
 static int launch_batch(MptContext* c, const MptFrame* f, int batch) {
     const bool restir_part = f->options.direct_light_sampling == MPT_LSS_RESTIR_DI && f->band_count > 1;
@@ -994,7 +1025,43 @@ static int launch_batch(MptContext* c, const MptFrame* f, int batch) {
         P.rs_lo = std::max(0, cfg.own_y0 - cfg.halo_prev) * f->res_x;
         P.rs_hi = std::min(f->res_y, cfg.own_y1 + cfg.halo_prev) * f->res_x;
     }
-    hipError_t e = launch_frame(dev_scene(c), P, c->d_frames + slot, *f, cfg, c->stream);
+    const bool ovl = c->overlap && batch >= 2 && f->options.direct_light_sampling != MPT_LSS_RESTIR_DI;
+    hipError_t e = hipSuccess;
+    if (ovl) {
+        int rr = ensure_overlap(c);
+        if (rr != MPT_OK) return rr;
+        // samples [0, b0) on the context's stream, [b0, batch) on stream2 over their own
+        // slots, counters and traversal spill area; the second half starts once the first
+        // half's camera-ray traversal is done and accumulates after the first half's
+        const int b0 = batch / 2, b1 = batch - b0;
+        c->batch = b0;
+        DevPaths P0 = dev_paths(c);
+        c->batch = b1;
+        DevPaths P1 = dev_paths(c);
+        c->batch = 1;
+        offset_slots(P1, (size_t)std::max(c->n_slots, 1) * b0);
+        P1.counters += CTR_COUNT;
+        P1.stack_spill = c->spill2.p;
+        HIPCHK(hipEventRecord(c->ev_fork, c->stream));
+        HIPCHK(hipStreamWaitEvent(c->stream2, c->ev_fork, 0));
+        LaunchCfg cfg0 = cfg;
+        cfg0.ev_first_trace = c->ev_first;
+        cfg0.ev_acc_done = c->ev_acc;
+        e = launch_frame(dev_scene(c), P0, c->d_frames + slot, f[0], cfg0, c->stream);
+        LaunchCfg cfg1 = cfg0;
+        cfg1.ev_first_trace = nullptr;
+        cfg1.ev_acc_done = nullptr;
+        cfg1.ev_acc_wait = c->ev_acc;
+        cfg1.launches = 0;
+        HIPCHK(hipStreamWaitEvent(c->stream2, c->ev_first, 0));
+        if (e == hipSuccess) e = launch_frame(dev_scene(c), P1, c->d_frames + slot + b0, f[b0], cfg1, c->stream2);
+        HIPCHK(hipEventRecord(c->ev_join, c->stream2));
+        HIPCHK(hipStreamWaitEvent(c->stream, c->ev_join, 0));
+        cfg.ev_used = cfg1.ev_used;
+        cfg.launches = cfg0.launches + cfg1.launches;
+    } else {
+        e = launch_frame(dev_scene(c), P, c->d_frames + slot, *f, cfg, c->stream);
+    }
     c->restir_out_sp2 = cfg.restir_out_sp2;
     if (restir_part) c->halo_prev = cfg.halo_rows;
     if (e != hipSuccess) return fail(MPT_ERR_HIP, std::string("kernel launch: ") + hipGetErrorString(e));

@@ -204,6 +204,11 @@ struct LaunchCfg {
     int shade_classes;        // material-class shading: 0 off, 1 on, 2 on + defer every plain vertex (test hook)
     int light_bvh;            // light-hit queries through the light BVH (1) or one closest-hit traversal (0)
     int light_static;         // the light BVH's traversal stack fits in LDS (one query per lane, no spill)
+    // overlapped batch halves (mpt_api.cpp launch_batch): recorded after the bounce-0 path
+    // traversal / after k_accumulate; waited for before k_accumulate (all optional)
+    hipEvent_t ev_first_trace;
+    hipEvent_t ev_acc_done;
+    hipEvent_t ev_acc_wait;
 };
 
 hipError_t launch_frame(const DevScene& S, const DevPaths& P, const MptFrame* d_frame, const MptFrame& h_frame,

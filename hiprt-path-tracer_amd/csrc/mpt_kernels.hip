@@ -1704,11 +1704,13 @@ __global__ __launch_bounds__(TB) void k_resolve(DevScene S, DevPaths P, const Mp
     int i = blockIdx.x * TB + threadIdx.x;
     if (i == 0) {
         // always-on ray accounting: path rays + NEE any-hit + NEE closest of this bounce, path hits
-        P.ray_counts[0] += (uint64_t)*count_paths;
-        P.ray_counts[1] += (uint64_t)P.counters[CTR_ANY];
-        P.ray_counts[2] += (uint64_t)P.counters[CTR_CL];
-        P.ray_counts[3] += (uint64_t)(shaded_count(P) - P.counters[CTR_DEFER]);
-        P.ray_counts[4] += (uint64_t)P.counters[CTR_FULL];
+        // (atomic: the two halves of an overlapped batch resolve concurrently)
+        unsigned long long* rc = (unsigned long long*)P.ray_counts;
+        atomicAdd(rc + 0, (unsigned long long)*count_paths);
+        atomicAdd(rc + 1, (unsigned long long)P.counters[CTR_ANY]);
+        atomicAdd(rc + 2, (unsigned long long)P.counters[CTR_CL]);
+        atomicAdd(rc + 3, (unsigned long long)(shaded_count(P) - P.counters[CTR_DEFER]));
+        atomicAdd(rc + 4, (unsigned long long)P.counters[CTR_FULL]);
     }
     const int nh = P.counters[CTR_HIT];
     if (i >= nh + P.counters[CTR_FULL]) return;
@@ -2055,6 +2057,7 @@ hipError_t launch_frame(const DevScene& S, const DevPaths& P0, const MptFrame* d
         ta.S = S; ta.P = P; ta.queue = q_cur; ta.count_ptr = &P.counters[c_cur]; ta.fetch = &P.counters[CTR_FETCH];
         ta.F = d_frame; ta.bounce = b; ta.alpha = hf.render_settings.do_alpha_testing ? 1 : 0;
         timed_trace<TM_PATH>(ta, cfg, st);
+        if (b == 0 && cfg.ev_first_trace) hipEventRecord(cfg.ev_first_trace, st);
         if (restir && b == 0) {
             if (cfg.halo_fn) hipMemsetAsync(&P.counters[CTR_REPROJ], 0, sizeof(int32_t), st);
             hipLaunchKernelGGL(k_gbuffer, dim3(blocks_for(n)), dim3(TB), 0, st, S, P, d_frame);
@@ -2126,10 +2129,13 @@ hipError_t launch_frame(const DevScene& S, const DevPaths& P0, const MptFrame* d
         int32_t* tq = q_cur; q_cur = q_next; q_next = tq;
         int tc = c_cur; c_cur = c_next; c_next = tc;
     }
+    // an overlapped batch's second half adds its samples after the first half's (sample order)
+    if (cfg.ev_acc_wait) hipStreamWaitEvent(st, cfg.ev_acc_wait, 0);
     {
         TimedScope ts(cfg, st, KT_ACCUMULATE);
         hipLaunchKernelGGL(k_accumulate, dim3(blocks_for(P.n_pix)), dim3(TB), 0, st, P, d_frame);
     }
+    if (cfg.ev_acc_done) hipEventRecord(cfg.ev_acc_done, st);
     return hipGetLastError();
 }
 
