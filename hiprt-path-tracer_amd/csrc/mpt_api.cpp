@@ -105,6 +105,7 @@ struct MptContext {
     std::vector<float> h_pos;
     float box_pad = 0.0f;
     int light_bvh = 1;                    // MPT_LIGHT_BVH at mpt_create: 0 = one closest-hit traversal per light-hit query
+    bool light_bvh_ok = false;            // the light BVH matches the materials (else: the exact closest-hit path)
     DBuf<int32_t> idx, mat_idx, mat_prio, emissive, tex_dims;
     DBuf<float> pos, nrm, uv;
     DBuf<uint8_t> has_n, tex;
@@ -432,6 +433,7 @@ int build_light_bvh(MptContext* c) {
     for (size_t t = 0; t < c->h_mat_idx.size(); t++)
         if (lit[c->h_mat_idx[t]]) prims.push_back((int32_t)t);
     hipStream_t st = c->stream;
+    c->light_bvh_ok = false;   // until the set below is built and uploaded
     if (prims != c->h_light_prims || (!prims.empty() && !c->nodes_light.p)) {
         c->h_light_prims = prims;
         c->nodes_light.release();
@@ -442,8 +444,10 @@ int build_light_bvh(MptContext* c) {
                 for (int j = 0; j < 3; j++) sub[3 * k + j] = c->h_idx[3 * (size_t)prims[k] + j];
             build_bvh8(c->h_pos.data(), sub.data(), (int32_t)prims.size(), c->bvh_light, 3, c->box_pad);
             if (2 * c->bvh_light.depth + 2 > MAX_STACK) {
+                // too deep for the traversal stack: light-hit queries take the (exact)
+                // whole-scene closest-hit path instead
                 c->h_light_prims.clear();
-                return fail(MPT_ERR_UNSUPPORTED, "light BVH8 deeper than the traversal stack");
+                return MPT_OK;
             }
             for (TriRec& tr : c->bvh_light.tris) {   // subset index -> scene primitive
                 int32_t k;
@@ -463,6 +467,7 @@ int build_light_bvh(MptContext* c) {
         HIPCHK(c->tris_light.upload(c->bvh_light.tris.data(), c->bvh_light.tris.size(), st));
     }
     HIPCHK(hipStreamSynchronize(st));
+    c->light_bvh_ok = true;
     return MPT_OK;
 }
 
@@ -1005,7 +1010,7 @@ static int launch_batch(MptContext* c, const MptFrame* f, int batch) {
     cfg.ev_used = 0;
     cfg.restir_out_sp2 = c->restir_out_sp2;
     cfg.shade_classes = c->shade_classes;
-    cfg.light_bvh = c->light_bvh;
+    cfg.light_bvh = c->light_bvh && c->light_bvh_ok;
     cfg.light_static = !c->h_light_prims.empty() && 2 * c->bvh_light.depth + 2 <= TRAV_LDS_STACK;
     if (restir_part) {
         if (!c->h_reproj) HIPCHK(hipHostMalloc((void**)&c->h_reproj, sizeof(int32_t), hipHostMallocDefault));
