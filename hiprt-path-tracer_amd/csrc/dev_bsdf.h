@@ -170,14 +170,16 @@ DEV v3 cosine_sample_around(v3 n, Rng& rng) {
     if (r1 < 1.0e-8f && r2 < -0.999999f && n.z > 0.999999f) { r1 += 1.0e-7f; r2 += 1.0e-7f; }
     float theta = TWO_PI * r1;
     float s = sqrtf(1.0f - r2 * r2);
-    return normalize(n + mk3(s * pcos(theta), s * psin(theta), r2));
+    const float2 sc = psincos(theta);
+    return normalize(n + mk3(s * sc.y, s * sc.x, r2));
 }
 DEV v3 cosine_sample_z_up(Rng& rng) {
     float r1 = rng(), r2 = rng();
     float phi = TWO_PI * r1;
     float ct = sqrtf(r2);
     float st = sqrtf(1.0f - ct * ct);
-    return normalize(mk3(pcos(phi) * st, psin(phi) * st, ct));
+    const float2 sc = psincos(phi);
+    return normalize(mk3(sc.y * st, sc.x * st, ct));
 }
 DEV Col lambert_eval(const Mat& m, float NoL, float& pdf) {
     pdf = 0.0f;
@@ -347,7 +349,8 @@ DEV v3 ggx_vndf(v3 V, float ax, float ay, Rng& rng) {
     v3 T1 = lensq > 0.0f ? mk3(-Vh.y, Vh.x, 0.0f) / sqrtf(lensq) : mk3(1.0f, 0.0f, 0.0f);
     v3 T2 = cross(Vh, T1);
     float r = sqrtf(r1), phi = TWO_PI * r2;
-    float t1 = r * pcos(phi), t2 = r * psin(phi);
+    const float2 sc = psincos(phi);
+    float t1 = r * sc.y, t2 = r * sc.x;
     float s = 0.5f * (1.0f + Vh.z);
     t2 = (1.0f - s) * sqrtf(1.0f - t1 * t1) + s * t2;
     v3 Nh = t1 * T1 + t2 * T2 + sqrtf(maxr(0.0f, 1.0f - t1 * t1 - t2 * t2)) * Vh;
@@ -453,7 +456,8 @@ DEV Col read_ltc(const BCtx& c, float r, float ct) {
 DEV float get_phi(v3 d) { float p = patan2(d.y, d.x); if (p < 0.0f) p += TWO_PI; return p; }
 DEV v3 rotate_z(v3 v, float angle) {
     v3 axis = mk3(0.0f, 0.0f, 1.0f);
-    float s = psin(angle), co = pcos(angle);
+    const float2 sc = psincos(angle);
+    float s = sc.x, co = sc.y;
     return v * co + axis * dot(v, axis) * (1.0f - co) + s * cross(axis, v);
 }
 DEV Col sheen_eval(const BCtx& c, const Mat& m, v3 L, v3 V, float& pdf, float& refl) {

@@ -67,6 +67,7 @@ TRANS float ppow(float x, float y) { return (float)::pow((double)x, (double)y); 
 TRANS float patan2(float y, float x) { return (float)::atan2((double)y, (double)x); }
 TRANS float pasin(float x) { return (float)::asin((double)x); }
 TRANS float pacos(float x) { return (float)::acos((double)x); }
+TRANS float2 psincos(float x) { return make_float2((float)::sin((double)x), (float)::cos((double)x)); }
 #else
 // Out of line: inlined at their ~60 call sites they push k_shade from 272 to 1072 B of
 // scratch per lane and k_trace<PATH> (the sRGB pow of the alpha test) from 4 to 3 waves/SIMD.
@@ -77,6 +78,8 @@ TRANS float pacos(float x) { return (float)::acos((double)x); }
 #endif
 TRANS float psin(float x) { return tmath::sinf_(x); }
 TRANS float pcos(float x) { return tmath::cosf_(x); }
+// (psin(x), pcos(x)) with one call and one range reduction
+TRANS float2 psincos(float x) { float s, c; tmath::sincosf_(x, s, c); return make_float2(s, c); }
 TRANS float pexp(float x) { return tmath::expf_(x); }
 TRANS float plog(float x) { return tmath::logf_(x); }
 TRANS float ppow(float x, float y) { return tmath::powf_(x, y); }
@@ -148,7 +151,8 @@ DEV void build_rotated_onb(v3 n, v3& t, v3& b, float rot) {
     v3 up = absr(n.z) < 0.9999999f ? mk3(0.0f, 0.0f, 1.0f) : mk3(1.0f, 0.0f, 0.0f);
     t = normalize(cross(up, n));
     // rot == +-0 (no anisotropy rotation, the common case): cos = 1, sin = rot exactly
-    float c = rot == 0.0f ? 1.0f : pcos(rot), s = rot == 0.0f ? rot : psin(rot);
+    float c = 1.0f, s = rot;
+    if (rot != 0.0f) { const float2 sc = psincos(rot); s = sc.x; c = sc.y; }
     t = t * c + cross(n, t) * s + n * dot(n, t) * (1.0f - c);
     b = cross(n, t);
 }

@@ -947,8 +947,9 @@ DEV Col env_sample(const DevScene& S, const MptFrame& F, v3& dir, float& pdf, Rn
     float u = (float)x / (float)(unsigned)S.env_w, v = (float)y / (float)(unsigned)S.env_h;
     float phi = u * TWO_PI;
     float theta = maxr(1.0e-5f, v * PI);
-    float ct = pcos(theta), st = psin(theta);
-    dir = mat_x_vec(F.world_settings.envmap_to_world_matrix.m, mk3(-st * pcos(phi), -ct, -st * psin(phi)));
+    const float2 sct = psincos(theta), scp = psincos(phi);
+    float ct = sct.y, st = sct.x;
+    dir = mat_x_vec(F.world_settings.envmap_to_world_matrix.m, mk3(-st * scp.y, -ct, -st * scp.x));
     Col rad = env_tex(S, F, mk2(u, 1.0f - v));
     pdf = lum(rad) / (env_total(S, F) * F.world_settings.envmap_intensity);
     pdf *= (float)((unsigned)S.env_w * (unsigned)S.env_h);
@@ -2186,6 +2187,8 @@ __global__ void k_debug_math(int fn, const float* a, const float* b, float* out,
         case 4: r = ppow(x, y); break;
         case 5: r = patan2(x, y); break;
         case 6: r = pasin(x); break;
+        case 8: r = psincos(x).x; break;
+        case 9: r = psincos(x).y; break;
         default: r = pacos(x); break;
     }
     out[i] = r;

@@ -83,6 +83,18 @@ TM_FN float cosf_(float xf) {
     return (float)((q == 1 || q == 2) ? -c : c);
 }
 
+// sinf_(x) and cosf_(x) from one reduction (bit-identical to the two calls)
+TM_FN void sincosf_(float xf, float& sf, float& cf) {
+    const double x = xf;
+    if (!(fabs(x) <= 1.0e5)) { sf = (float)sin(x); cf = (float)cos(x); return; }
+    double r;
+    const int q = reduce_pio2(x, r) & 3;
+    const double sk = sin_kernel(r), ck = cos_kernel(r);
+    const double s = (q & 1) ? ck : sk, c = (q & 1) ? sk : ck;
+    sf = x == 0.0 ? (float)sin(x) : (float)((q & 2) ? -s : s);
+    cf = (float)((q == 1 || q == 2) ? -c : c);
+}
+
 // e^t for |t| <= 200: t = k ln2 + r, |r| <= ln2 / 2, Taylor series through r^13 (tail < 5e-18)
 TM_FN double exp_d(double t) {
     const double k = rint(t * INV_LN2);

@@ -84,3 +84,21 @@ def test_tmath_device_equals_oracle(oracle_lib, fn, name):
     same = (gpu.view(np.int32) == cpu.view(np.int32)) | (np.isnan(gpu) & np.isnan(cpu))
     bad = np.flatnonzero(~same)
     assert len(bad) == 0, (name, len(bad), [(float(a[i]), float(b[i]), float(gpu[i]), float(cpu[i])) for i in bad[:3]])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dev_fn,fn,name", [(8, 0, "sin"), (9, 1, "cos")])
+def test_tmath_device_sincos_equals_oracle(oracle_lib, dev_fn, fn, name):
+    """psincos (one range reduction for the sine and cosine the samplers need together)
+    gives psin / pcos bit for bit."""
+    import ctypes as C
+
+    import mpt
+    L = mpt.lib()
+    L.mpt_debug_math.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
+    a, b = args(name, 1_000_000, 200 + fn)
+    gpu = np.zeros_like(a)
+    L.mpt_debug_math(dev_fn, a.ctypes.data, b.ctypes.data, gpu.ctypes.data, len(a))
+    cpu = oracle_fn(oracle_lib, fn, a, b)
+    same = (gpu.view(np.int32) == cpu.view(np.int32)) | (np.isnan(gpu) & np.isnan(cpu))
+    assert same.all(), (name, int((~same).sum()))
