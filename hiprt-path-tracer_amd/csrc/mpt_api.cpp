@@ -96,6 +96,7 @@ struct MptContext {
     DBuf<Node8> nodes;
     DBuf<TriRec> tris;
     DBuf<float4> tri_attr;               // 5 per triangle (launch_tri_attr)
+    DBuf<float> srgb;                    // 256-entry sRGB decode table (launch_srgb_table)
     // light-hit BVH (k_trace TM_NEE_LIGHT): the triangles whose emission can be non-black
     BVH8 bvh_light;
     DBuf<Node8> nodes_light;
@@ -212,6 +213,7 @@ DevScene dev_scene(MptContext* c) {
     S.tex = c->tex.p;
     S.tex_off = c->tex_off.p;
     S.tex_dims = c->tex_dims.p;
+    S.srgb = c->srgb.p;
     S.n_tex = c->n_tex;
     S.lut_conductor = c->lut_conductor.p;
     S.lut_glossy = c->lut_glossy.p;
@@ -643,6 +645,8 @@ static int create_context(MptContext* c, int device, void* hip_stream) {
     HIPCHK(hipMemsetAsync(c->status.p, 0, 4 * sizeof(uint32_t), c->stream));
     HIPCHK(hipMemsetAsync(c->ray_counts.p, 0, N_RAY_COUNTS * sizeof(uint64_t), c->stream));
     HIPCHK(c->spill.alloc((size_t)c->grid * TRAV_BLOCK * SPILL_WORDS));
+    HIPCHK(c->srgb.alloc(256));
+    HIPCHK(launch_srgb_table(c->srgb.p, c->stream));
     for (int p = 0; p < 2; p++) {
         for (int i = 0; i < EV_POOL; i++) HIPCHK(hipEventCreate(&c->ev[p][i]));
         HIPCHK(hipEventCreate(&c->ev_frame[p][0]));

@@ -47,6 +47,7 @@ struct DevScene {
     const uint8_t* tex;          // all textures, RGBA8, concatenated
     const uint64_t* tex_off;     // byte offset per texture
     const int32_t* tex_dims;     // w, h per texture
+    const float* srgb;           // 256: pow(v / 255, 2.2), the sRGB decode of 8-bit texels
     int32_t n_tex;
     // LUTs
     const float* lut_conductor;
@@ -219,6 +220,7 @@ hipError_t launch_restir_fill(float4* reservoirs, int n, hipStream_t st);
 hipError_t launch_restir_fill_lights(float4* lights, int n, hipStream_t st);
 hipError_t launch_bake(int kind, int w, int h, int d, int ipk, int nb_samples, int iteration, float* out, hipStream_t st);
 hipError_t launch_tri_attr(const DevScene& S, float4* out, hipStream_t st);
+hipError_t launch_srgb_table(float* out, hipStream_t st);
 hipError_t launch_trace_raw(const DevScene& S, const float4* o, const float4* d, int n, bool any, float4* out_hit,
                             uint8_t* out_occ, int32_t* fetch_ctr, uint32_t* spill, int grid, hipStream_t st);
 

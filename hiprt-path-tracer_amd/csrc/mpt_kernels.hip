@@ -538,8 +538,12 @@ DEV void tex_rgba(const DevScene& S, int ti, bool srgb, v2 uv, float out[4]) {
     int x = (int)(u * (float)(w - 1)), y = (int)(v * (float)(h - 1));
     const uint8_t* p = S.tex + S.tex_off[ti] + (size_t)(x + y * w) * 4;
     uchar4 c = *reinterpret_cast<const uchar4*>(p);
+    if (srgb) {
+        // pow(c / 255, 2.2) per 8-bit value, precomputed with the same ppow (k_srgb_table)
+        out[0] = S.srgb[c.x]; out[1] = S.srgb[c.y]; out[2] = S.srgb[c.z]; out[3] = S.srgb[c.w];
+        return;
+    }
     out[0] = (float)c.x / 255.0f; out[1] = (float)c.y / 255.0f; out[2] = (float)c.z / 255.0f; out[3] = (float)c.w / 255.0f;
-    if (srgb) for (int i = 0; i < 4; i++) out[i] = ppow(out[i], 2.2f);
 }
 DEV bool has_tex(int ti) { return ti != MPT_NO_TEXTURE && ti != MPT_CONSTANT_EMISSIVE_TEXTURE; }
 // filter_function's test: keep the candidate iff u < alpha_opacity * base-colour alpha
@@ -2218,6 +2222,16 @@ hipError_t launch_resolve_materials(const DevScene& S, MptMaterial* out_res, int
     hipLaunchKernelGGL(k_resolve_materials, dim3((n + 63) / 64), dim3(64), 0, st, S, out_res, out_tex, n);
     if (S.n_emissive > 0)
         hipLaunchKernelGGL(k_emissive_table, dim3((S.n_emissive + 63) / 64), dim3(64), 0, st, S, em_tab);
+    return hipGetLastError();
+}
+
+// the sRGB decode of Texture.h:72-75 for every 8-bit value: ppow((float)v / 255, 2.2)
+__global__ void k_srgb_table(float* out) {
+    const int v = threadIdx.x;
+    out[v] = ppow((float)v / 255.0f, 2.2f);
+}
+hipError_t launch_srgb_table(float* out, hipStream_t st) {
+    hipLaunchKernelGGL(k_srgb_table, dim3(1), dim3(256), 0, st, out);
     return hipGetLastError();
 }
 
