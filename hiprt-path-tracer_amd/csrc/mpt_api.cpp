@@ -138,6 +138,7 @@ struct MptContext {
     DBuf<float4> ray_o, ray_d, hit, thr, col, alb, nrmv, nq_o, nq_d, nhit;
     DBuf<uint8_t> hit_inside, occ, qmask;
     DBuf<uint32_t> rng, spill, spill2;
+    DBuf<uint2> seeds;
     DBuf<uint4> vsA, vsB;
     DBuf<int32_t> q0, q1, qh, qm, qf, nq_light, counters, nq_tgt, fetch_raw;
     DBuf<NeeRec> nee;
@@ -243,6 +244,7 @@ DevPaths dev_paths(MptContext* c) {
     P.hit = c->hit.p;
     P.hit_inside = c->hit_inside.p;
     P.rng = c->rng.p;
+    P.seeds = c->seeds.p;
     P.thr = c->thr.p;
     P.col = c->col.p;
     P.vsA = c->vsA.p;
@@ -312,12 +314,12 @@ struct Allocs {
 
 // Bytes of path state per path slot (ensure_batch): ray_o, ray_d, hit, thr, col, alb, nrmv,
 // nhit (8 x 16), vsA + vsB (32), the NEE record, 4 staged NEE query rays (2 x 64), the
-// compacted query entries (16), occlusion bytes (4), 6 queues (24), rng (4), hit_inside,
+// compacted query entries (16), occlusion bytes (4), 6 queues (24), rng (4), seeds (8), hit_inside,
 // qmask, active (3).  Textured scenes add a resolved material per slot.
-constexpr size_t PATH_BYTES = 8 * 16 + 32 + sizeof(NeeRec) + 128 + 16 + 4 + 24 + 4 + 3;
+constexpr size_t PATH_BYTES = 8 * 16 + 32 + sizeof(NeeRec) + 128 + 16 + 4 + 24 + 4 + 8 + 3;
 
 void release_batch(MptContext* c) {
-    release_all(c->ray_o, c->ray_d, c->hit, c->hit_inside, c->rng, c->thr, c->col, c->vsA, c->vsB, c->alb, c->nrmv,
+    release_all(c->ray_o, c->ray_d, c->hit, c->hit_inside, c->rng, c->seeds, c->thr, c->col, c->vsA, c->vsB, c->alb, c->nrmv,
                 c->q0, c->q1, c->qh, c->qm, c->qf, c->nq_light, c->nee, c->nq_o, c->nq_d, c->nq_tgt, c->occ, c->nhit, c->qmask, c->active,
                 c->mat_slot);
     c->batch_cap = 0;
@@ -337,7 +339,7 @@ int ensure_batch(MptContext* c, int batch, bool mat_slot) {
     Allocs A;
     if (!have) {
         c->batch_cap = 0;
-        A(c->ray_o, N); A(c->ray_d, N); A(c->hit, N); A(c->hit_inside, N); A(c->rng, N); A(c->thr, N); A(c->col, N);
+        A(c->ray_o, N); A(c->ray_d, N); A(c->hit, N); A(c->hit_inside, N); A(c->rng, N); A(c->seeds, N); A(c->thr, N); A(c->col, N);
         A(c->vsA, N); A(c->vsB, N); A(c->alb, N); A(c->nrmv, N); A(c->q0, N); A(c->q1, N); A(c->qh, N); A(c->qm, N); A(c->qf, N); A(c->nq_light, N);
         A(c->nee, N); A(c->nq_o, 4 * N); A(c->nq_d, 4 * N); A(c->nq_tgt, 4 * N); A(c->occ, 4 * N); A(c->nhit, N);
         A(c->qmask, N); A(c->active, N);
@@ -980,7 +982,7 @@ static int ensure_overlap(MptContext* c) {
 // Moves every per-slot pointer of P by `off` slots (the second half of an overlapped batch
 // owns slots [off, off + P.n) of the path state; per-pixel buffers stay shared).
 static void offset_slots(DevPaths& P, size_t off) {
-    P.ray_o += off; P.ray_d += off; P.hit += off; P.hit_inside += off; P.rng += off; P.thr += off; P.col += off;
+    P.ray_o += off; P.ray_d += off; P.hit += off; P.hit_inside += off; P.rng += off; P.seeds += off; P.thr += off; P.col += off;
     P.vsA += off; P.vsB += off; P.alb += off; P.nrm += off;
     P.q0 += off; P.q1 += off; P.qh += off; P.qm += off; P.qf += off; P.nq_light += off;
     P.nee += off; P.nq_o += 4 * off; P.nq_d += 4 * off; P.nq_tgt += 4 * off; P.occ += 4 * off;

@@ -103,6 +103,7 @@ struct DevPaths {
     float4* hit;              // t, u, v, prim bits
     uint8_t* hit_inside;      // "inside a volume" before the last stack push (trace_ray normal flip)
     uint32_t* rng;
+    uint2* seeds;             // per slot: the camera launch's and the path tracing launch's pixel seeds (k_camera)
     float4* thr;
     float4* col;
     uint4* vsA;

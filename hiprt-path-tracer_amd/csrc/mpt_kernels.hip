@@ -415,7 +415,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MODE == TM_P
                         skips = 0;
                         was_inside = false;
                         if (A.alpha)     // bounce 0: the camera launch's seed (CameraRays traces the camera ray)
-                            pseed = path_seed(A.F, P, ray, A.bounce == 0);
+                            pseed = A.bounce == 0 ? P.seeds[ray].x : P.seeds[ray].y;   // path_seed (k_camera)
                         tr.init(mk3(ro.x, ro.y, ro.z), mk3(rd.x, rd.y, rd.z), (int)__float_as_uint(ro.w), INFINITY,
                                 A.alpha != 0, A.alpha ? alpha_key(pseed, A.bounce, 0, 0) : 0u);
                     } else if (MODE == TM_NEE_ANY || MODE == TM_NEE_CLOSEST || MODE == TM_NEE_LIGHT || MODE == TM_NEE_LIGHT_OCC) {
@@ -427,7 +427,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MODE == TM_P
                         qmax = rd.w;
                         const bool al = A.alpha != 0;
                         uint32_t akey = 0u;
-                        if (al) akey = alpha_key(path_seed(A.F, P, ray >> 2, false), A.bounce, (ray & 3) + 1, 0);
+                        if (al) akey = alpha_key(P.seeds[ray >> 2].y, A.bounce, (ray & 3) + 1, 0);
                         float tmax = ANY ? rd.w : INFINITY;
                         if (TIE) {
                             // the light candidate of TM_NEE_LIGHT: anything nearer, or as near with a
@@ -832,7 +832,11 @@ __global__ __launch_bounds__(TB) void k_camera(DevPaths P, const MptFrame* __res
     if (rs.do_update_status_buffers) P.status[1] = 1u;
     int x, y;
     uint32_t pix = slot_pixel(F, pslot, x, y);
-    Rng rng = make_rng(camera_seed(F, pix));
+    const uint32_t cseed = camera_seed(F, pix);
+    // the path's seeds for the later stages (path_seed of the camera launch / of the path
+    // tracing launch), computed once here instead of per traversal query
+    P.seeds[slot] = make_uint2(cseed, pixel_seed(F, pix));
+    Rng rng = make_rng(cseed);
     float xd = (float)x + 0.5f, yd = (float)y + 0.5f;
     if (F.current_camera.do_jittering) { xd += rng() - 0.5f; yd += rng() - 0.5f; }
     float xn = xd / (float)F.res_x * 2.0f - 1.0f;
@@ -1143,7 +1147,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_
             gn = normalize(gn);
             sn = normalize(sn);
             d = normalize(d);
-            rng = make_rng(path_seed(A.F, P, slot, false));
+            rng = make_rng(P.seeds[slot].y);   // path_seed(F, P, slot, false), from k_camera
         }
         if (PLAIN) {
             // principled_eval_pre's 'outside' with the normal the vertex is shaded with
