@@ -11,6 +11,9 @@ Workloads (BASELINE.json configs):
 * c5: the glass-dispersion stress scene (multi-dispersion.gltf; --scene
   nested-dielectrics-complex for the nested-dielectrics one) at 3840x2160, 16 bounces,
   Principled + RIS, K = 1024.
+* c1: the Cornell box at 256x256, 1 spp, Lambert override (BSDFOverride = BSDF_LAMBERTIAN),
+  reference-default RIS: the configuration BASELINE.json quotes for the CPU megakernel; the
+  line's cpu_baseline is the oracle over the whole C1 frame, its parity the whole frame.
 All: 3 bounces unless stated, reference defaults otherwise (adaptive sampling off so that every step
 samples every pixel).  One *step* = one sample per pixel over the frame (one
 mpt_render_frame); K steps = the config's spp.  Multi-GPU: one process per GPU, the framebuffer is split into
@@ -19,10 +22,17 @@ buffers are gathered with RCCL (all_gather over xGMI) inside the timed region.
 
 value = whole-job Mray/s (every closest + any-hit query: camera, continuation, NEE
 shadow, MIS BSDF ray) = rays of all ranks / max-over-ranks wall time.
-roofline: the dominant traversal stage's algorithmic bytes (SURVEY.md §8d,
-B_ray = 32 + 16 + 80 N_node + 48 N_tri, N counted by an instrumented calibration
-pass) over its HIP-event-timed launches in the timed region.
-cpu_baseline: the CPU oracle (a port, test infrastructure) on a bounded band sample.
+roofline: the kernel with the largest HIP-event time in the timed region among the
+traversal stages (SURVEY.md §8d B_ray = 32 + 16 + 80 N_node + 48 N_tri, N counted by an
+instrumented calibration pass), the shading kernel (556 B per path vertex) and the ReSTIR DI
+kernels (bytes per pixel); achieved = units per launch x bytes per unit / the
+average launch time.  roofline_traversal adds the traversal's VALU issue rate and the PMC
+HBM fraction from the committed profile of the same command (profiles/).
+cpu_baseline: the CPU oracle (a port, test infrastructure) on a bounded sample of the same
+frame, on every core the process may use (cores stated).
+parity_vs_oracle: the GPU's 256-spp radiance against the oracle on one 8-row band (the
+metric's "RMSE vs ref @256spp"); C4 (ReSTIR DI reuses the whole frame): whole frames, as
+many as the oracle renders in its budget; C1: the whole frame at K spp.
 """
 import argparse
 import json
@@ -40,6 +50,7 @@ from mpt import abi, scene  # noqa: E402
 
 METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
 HBM_PEAK_GBS = 8000.0
+VALU_PEAK = 256 * 4 * 2.4e9 / 2    # wave64 VALU instructions / s (MI355X_MICROARCH.md: 2 cycles per wave instruction)
 S_NODE, S_TRI = 80, 48
 BAND_H = 8
 TARGET_PATHS = 16 * 1920 * 1080  # paths per wavefront launch (mpt_render_frames batch x rank pixels)
@@ -49,8 +60,8 @@ MAX_BATCH = 128    # MPT_MAX_BATCH
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--workload", default="c3", choices=["c2", "c3", "c4", "c5"])
-    ap.add_argument("--steps", type=int, default=None, help="default: the workload's spp (c3/c4 256, c2 64, c5 1024)")
+    ap.add_argument("--workload", default="c3", choices=["c1", "c2", "c3", "c4", "c5"])
+    ap.add_argument("--steps", type=int, default=None, help="default: the workload's spp (c3/c4 256, c2 64, c5 1024, c1 1)")
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--width", type=int, default=None, help="default 1920 (c5: 3840)")
     ap.add_argument("--height", type=int, default=None, help="default 1080 (c5: 2160)")
@@ -60,6 +71,8 @@ def parse():
     ap.add_argument("--bounces", type=int, default=None, help="default 3 (c5: 16)")
     ap.add_argument("--bsdf", default="principled", choices=["principled", "lambert"])
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="target CPU-baseline sample duration")
+    ap.add_argument("--parity-spp", type=int, default=256, help="spp of the RMSE-vs-oracle band (the metric's 256)")
+    ap.add_argument("--parity-seconds", type=float, default=90.0, help="oracle budget of the parity leg")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true", help="skip the RMSE-vs-oracle band check")
     ap.add_argument("--batch", type=int, default=0,
@@ -94,14 +107,40 @@ def frames_for(cam, W, H, opt, band, n, first=0, bounces=3, world=None, alpha=Fa
     return out
 
 
+def host_cores():
+    """CPU threads the oracle may run on here: the process's CPU affinity, capped by the
+    cgroup CPU quota when one is set (the GPU box grants a share of a larger machine), or
+    OMP_NUM_THREADS when the harness pins it.  Returns (threads, nproc, how)."""
+    nproc = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = nproc
+    n, how = aff, "affinity"
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(per)))
+            if quota < n:
+                n, how = quota, "cgroup quota"
+    except (OSError, ValueError):
+        pass
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    if 0 < omp < n:
+        n, how = omp, "OMP_NUM_THREADS"
+    return n, nproc, how
+
+
 def cpu_baseline(sd, luts, cam, W, H, opt, bounces, target_s, env=None, world=None, alpha=False):
     """Oracle (CPU port) timed on a bounded sample of the same frame: a subset of the
-    8-row bands at 1 spp, or the whole frame at several spp, sized to ~target_s."""
+    8-row bands at 1 spp, or the whole frame at several spp, sized to ~target_s.  ReSTIR DI
+    reuses the whole frame, so C4 times whole frames."""
     sys.path.insert(0, ROOT)
     from oracle import oracle as orc
-    cores = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    cores, nproc, how = host_cores()
     o = orc.Oracle(sd, luts, envmap=env)
-    bc = 64
+    restir = opt.direct_light_sampling == abi.LSS_RESTIR_DI
+    bc = 1 if restir else 64
     t0 = time.perf_counter()
     o.render(frames_for(cam, W, H, opt, (BAND_H, 0, bc), 1, bounces=bounces, world=world, alpha=alpha), nthreads=cores)
     dt = max(time.perf_counter() - t0, 1e-3)
@@ -110,6 +149,8 @@ def cpu_baseline(sd, luts, cam, W, H, opt, bounces, target_s, env=None, world=No
         bc2, spp = 1, max(1, int(round(scale / bc)))
     else:
         bc2, spp = max(1, int(round(bc / scale))), 1
+    if restir:
+        bc2, spp = 1, max(1, min(8, int(scale)))
     t0 = time.perf_counter()
     o.render(frames_for(cam, W, H, opt, (BAND_H, 0, bc2), spp, bounces=bounces, world=world, alpha=alpha),
              nthreads=cores)
@@ -118,31 +159,49 @@ def cpu_baseline(sd, luts, cam, W, H, opt, bounces, target_s, env=None, world=No
     rays = o.last_rays[0] + o.last_rays[1]
     o.close()
     return {"value": round(rays / dt / 1e6, 4), "unit": "Mray/s", "cores": cores, "kind": "port",
+            "host_cpus": nproc, "cores_from": how,
             "msample_per_s": round(rows * W * spp / dt / 1e6, 5),
-            "sample": f"oracle (C++ CPU port, OpenMP, {cores} threads): {spp} spp over {rows} of {H} rows "
+            "sample": f"oracle (C++ CPU port, OpenMP, {cores} threads = the host cores this process may use "
+                      f"({how}; the machine reports {nproc})): {spp} spp over {rows} of {H} rows "
                       f"({BAND_H}-row bands, 1 of every {bc2}) of the same {W}x{H} frame, {dt:.1f} s"}
 
 
-def parity_band(sd, luts, cam, W, H, opt, bounces, K, env=None, world=None, alpha=False, max_s=20.0):
-    """RMSE of the GPU's K-spp radiance (sum / K) against the CPU oracle on the same frames,
-    over one 8-row band through the middle of the frame (the metric's "RMSE vs ref @256spp";
-    the oracle is the pinned CPU restatement).  The spp of the check is
-    cut down (prefix of the same frame sequence) if the oracle would take longer than max_s."""
+def parity_check(r, sd, luts, cam, W, H, opt, bounces, spp, workload, env=None, world=None, alpha=False,
+                 max_s=90.0, batch=0):
+    """RMSE of the GPU's spp-sample radiance (sum / spp) against the CPU oracle on the same
+    frames (the metric's "RMSE vs ref @256spp"; the oracle is the pinned CPU restatement,
+    DESIGN.md §2), through the same batched path as the timed region.  Region: one 8-row
+    band through the middle of the frame; C1 the whole frame; C4 whole frames (ReSTIR DI
+    reuses neighbours across the frame), as many as the oracle renders in max_s."""
     sys.path.insert(0, ROOT)
     from oracle import oracle as orc
-    cores = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
-    bc = H // BAND_H
-    bi = bc // 2
+    cores, _, _ = host_cores()
+    restir = opt.direct_light_sampling == abi.LSS_RESTIR_DI
+    whole = restir or workload == "c1"
+    bc = 1 if whole else H // BAND_H
+    bi = 0 if whole else bc // 2
+    band = (BAND_H, bi, bc)
     o = orc.Oracle(sd, luts, envmap=env)
     t0 = time.perf_counter()
-    probe = o.render(frames_for(cam, W, H, opt, (BAND_H, bi, bc), 1, bounces=bounces, world=world, alpha=alpha),
-                     nthreads=cores)
+    probe = o.render(frames_for(cam, W, H, opt, band, 1, bounces=bounces, world=world, alpha=alpha), nthreads=cores)
     dt1 = max(time.perf_counter() - t0, 1e-4)
-    k = K if dt1 * K <= max_s else max(1, int(max_s / dt1))
-    ref = o.render(frames_for(cam, W, H, opt, (BAND_H, bi, bc), k, bounces=bounces, world=world, alpha=alpha),
+    k = spp if dt1 * spp <= max_s else max(1, int(max_s / dt1))
+    frs = frames_for(cam, W, H, opt, (BAND_H, 0, 1), k, bounces=bounces, world=world, alpha=alpha)
+    ref = o.render(frames_for(cam, W, H, opt, band, k, bounces=bounces, world=world, alpha=alpha),
                    nthreads=cores) if k > 1 else probe
     o.close()
-    return k, bi, ref
+    r.enable_stats(timing=False, instrumented=False)
+    r.render_samples(frs, max_batch=batch)
+    r.synchronize_kernel()
+    gpu = r.framebuffer(abi.FB_COLOR)
+    if not whole:
+        gpu = gpu[bi * BAND_H:(bi + 1) * BAND_H]
+    d = (gpu.astype(np.float64) - ref.astype(np.float64)) / k
+    return {"oracle": "CPU restatement (oracle/, DESIGN.md §2)",
+            "rows": "all" if whole else f"{bi * BAND_H}-{(bi + 1) * BAND_H - 1}", "spp": k,
+            "rmse": float(np.sqrt(np.mean(d * d))), "max_abs": float(np.abs(d).max()),
+            "bit_exact": bool(np.array_equal(gpu, ref)), "tolerance_rmse": 1e-3,
+            "note": (None if k == spp else f"{k} of {spp} spp: the oracle's budget ({max_s:.0f} s) on the whole frame")}
 
 
 def load_traffic(workload, W, H):
@@ -181,8 +240,8 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
-    W = a.width or (3840 if a.workload == "c5" else 1920)
-    H = a.height or (2160 if a.workload == "c5" else 1080)
+    W = a.width or (3840 if a.workload == "c5" else 256 if a.workload == "c1" else 1920)
+    H = a.height or (2160 if a.workload == "c5" else 256 if a.workload == "c1" else 1080)
     default_bounces = a.bounces is None
     a.bounces = a.bounces if a.bounces is not None else (16 if a.workload == "c5" else 3)
     if a.workload in ("c3", "c4"):
@@ -205,6 +264,16 @@ def main():
         K = a.steps or 1024
         alpha = False
         desc = f"C5: {sd.name or a.scene or 'multi-dispersion'} (glass dispersion, nested dielectrics)"
+    elif a.workload == "c1":
+        # C1: Cornell 256x256, 1 spp, Lambert override, reference-default RIS,
+        # uniform ambient, alpha testing and adaptive sampling off, CPU seed schedule
+        sd = scene.load_scene(a.scene or "cornell_pbr")
+        env, wset = None, None
+        strategy = a.strategy or "ris"
+        K = a.steps or 1
+        alpha = False
+        a.bsdf = "lambert"
+        desc = f"C1: {sd.name or a.scene or 'cornell_pbr'}"
     else:
         sd = scene.load_scene(a.scene or "cornell_pbr")
         env, wset = None, None
@@ -328,13 +397,40 @@ def main():
                   "total_ms": st.shade_ms, "avg_launch_ms": s_avg, "bytes_per_unit": b_vtx, "unit_of_work": "path vertex (hit)",
                   "units_per_launch": hits / sl,
                   "achieved": hits * b_vtx / sl / (s_avg * 1e-3) / 1e9 if s_avg > 0 else 0.0})
+    # ReSTIR DI kernels (C4): per pixel of the band, the G-buffer / reservoir / presampled-light
+    # bytes each one reads and writes; their visibility rays are traced inline
+    rk = [("k_gbuffer (CameraRays G-buffer write)", "void mpt::k_gbuffer(", 64 + 176),
+          ("k_restir_presample (lights presampling)", "void mpt::k_restir_presample(", 0),
+          ("k_restir_initial (initial candidates)", "void mpt::k_restir_initial<", 112 + 4 * 64 + 48),
+          ("k_restir_spatiotemporal / k_restir_temporal (temporal reuse)", "void mpt::k_restir_spatiotemporal<",
+           112 + 160 + 2 * 160 + 48 + 48),
+          ("k_restir_spatial (spatial reuse pass)", "void mpt::k_restir_spatial<", 112 + 48 + 2 * 160 + 48)]
+    n_pix = rows_rank * W
+    for k, (name, sym, bpp) in enumerate(rk):
+        ms, nl = st.restir_kernel_ms[k], st.restir_kernel_launches[k]
+        if nl == 0 or bpp == 0:
+            continue
+        avg = ms / nl
+        lines.append({"kernel": name, "symbol": sym, "total_ms": ms, "avg_launch_ms": avg, "bytes_per_unit": bpp,
+                      "unit_of_work": "pixel", "units_per_launch": n_pix,
+                      "achieved": n_pix * bpp / (avg * 1e-3) / 1e9 if avg > 0 else 0.0})
     dom = max(lines, key=lambda x: x["total_ms"])
 
     default_cfg = a.strategy is None and default_bounces and a.bsdf == "principled" and a.scene is None
     pmc = load_traffic(a.workload, W, H) if default_cfg else None
 
+    def pmc_entry(sym):
+        if not pmc:
+            return {}
+        if sym in pmc["kernels"]:
+            return pmc["kernels"][sym]
+        for k2, v in pmc["kernels"].items():     # template kernels: match the name prefix
+            if k2.startswith(sym):
+                return v
+        return {}
+
     def roof(x):
-        tr = pmc["kernels"].get(x["symbol"], {}) if pmc else {}
+        tr = pmc_entry(x["symbol"])
         r = {"bound": "hbm", "achieved": round(x["achieved"], 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
              "frac": round(x["achieved"] / HBM_PEAK_GBS, 5),
              "traffic": round(tr["traffic_bytes"]) if tr.get("traffic_bytes") else None,
@@ -345,24 +441,26 @@ def main():
             r.update(traffic_read=round(tr["read_bytes"]), traffic_write=round(tr["write_bytes"]),
                      traffic_per_unit=round(tr["traffic_bytes"] / max(1.0, x["units_per_launch"]), 1),
                      traffic_source=pmc["file"])
+        if r["traffic"]:
+            # the kernel's measured HBM bytes over its live launch time: the bandwidth it really draws
+            r["pmc_hbm_frac"] = round(tr["traffic_bytes"] / (x["avg_launch_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+        if tr.get("valu_insts"):
+            # VALU issue roofline: wave-level VALU instructions per launch over the chip's issue
+            # rate (256 CUs x 4 SIMDs, one wave64 VALU instruction per 2 cycles at 2.4 GHz)
+            rate = tr["valu_insts"] / (x["avg_launch_ms"] * 1e-3)
+            r["valu"] = {"insts_per_launch": round(tr["valu_insts"]), "achieved_tinst_s": round(rate / 1e12, 4),
+                         "peak_tinst_s": VALU_PEAK / 1e12, "frac": round(rate / VALU_PEAK, 4),
+                         "per_unit": round(tr["valu_insts"] / max(1.0, x["units_per_launch"]), 2)}
         if "nodes_per_ray" in x:
             r.update(nodes_per_ray=round(x["nodes_per_ray"], 3), tris_per_ray=round(x["tris_per_ray"], 3),
                      node_simd_util=round(x["node_simd_util"], 3), tri_simd_util=round(x["tri_simd_util"], 3))
         return r
 
     parity = None
-    if rank == 0 and world == 1 and not a.no_parity and a.workload != "c4":
-        # the GPU leg of the check: a fresh K'-spp accumulation restarting at sample 0 over
-        # the same frames (sample 0 overwrites the sums)
-        k, bi, ref = parity_band(sd, luts, cam, W, H, opt, a.bounces, K, env=env, world=wset, alpha=alpha)
-        r.enable_stats(timing=False, instrumented=False)
-        r.render_samples(frames[:k], max_batch=batch)   # the same batched path as the timed region
-        r.synchronize_kernel()
-        gpu = r.framebuffer(abi.FB_COLOR)[bi * BAND_H:(bi + 1) * BAND_H]
-        d = (gpu.astype(np.float64) - ref.astype(np.float64)) / k
-        parity = {"oracle": "CPU restatement (oracle/, pinned: DESIGN.md §2)", "rows": f"{bi * BAND_H}-{(bi + 1) * BAND_H - 1}",
-                  "spp": k, "rmse": float(np.sqrt(np.mean(d * d))), "max_abs": float(np.abs(d).max()),
-                  "bit_exact": bool(np.array_equal(gpu, ref)), "tolerance_rmse": 1e-3}
+    if rank == 0 and world == 1 and not a.no_parity:
+        # the GPU leg: a fresh accumulation restarting at sample 0 (sample 0 overwrites the sums)
+        parity = parity_check(r, sd, luts, cam, W, H, opt, a.bounces, K if a.workload == "c1" else a.parity_spp,
+                              a.workload, env=env, world=wset, alpha=alpha, max_s=a.parity_seconds, batch=batch)
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
@@ -384,7 +482,8 @@ def main():
             "scaling": "strong",   # fixed frame split over the ranks
             "vs_baseline": None,
             "dtype": "f32",
-            "data": ("synthetic (seeded procedural city + sky standing in for Bistro + its HDR, CPU seed schedule)"
+            "data": ("synthetic (seeded procedural city + sky standing in for Bistro + its HDR, "
+                     + ("GPURenderer seed schedule)" if a.workload == "c4" else "CPU seed schedule)")
                      if a.workload in ("c3", "c4") else f"synthetic (reference glTF {sd.name}, seeded CPU seed schedule)"),
             "msample_per_s": round(W * H * K / elapsed / 1e6, 3),
             "samples_per_launch": round(st.frames / max(1, st.shade_launches / (a.bounces + 1)), 3),
@@ -410,6 +509,9 @@ def main():
                                    "accumulate": round(st.accumulate_ms / K, 4),
                                    "compact": round(st.compact_ms / K, 4), "split": round(st.split_ms / K, 4),
                                    "miss": round(st.miss_ms / K, 4), "restir": round(st.restir_ms / K, 4),
+                                   "restir_kernels": {n: round(st.restir_kernel_ms[i] / K, 4) for i, n in
+                                                      enumerate(["gbuffer", "presample", "initial", "temporal_reuse",
+                                                                 "spatial_reuse"])},
                                    "frame_gpu": round(st.frame_ms / max(1, st.frames), 4)},
             "cpu_baseline": cpu,
             "parity_vs_oracle": parity,

@@ -69,7 +69,8 @@ constexpr int FRAME_RING = 256;   // >= 2 x MPT_MAX_BATCH
 // timing events per frame: one pair per timed launch, 10 per bounce (path, any-hit and two
 // light-hit traversals, split, plain and generic shade, miss, compact, resolve) for up to 65
 // bounces (validate_frame), + camera, ReSTIR, accumulate
-constexpr int EV_POOL = 2 * 2 * (10 * 65 + 3);   // x2: the two halves of an overlapped batch
+// + the ReSTIR DI kernels (G-buffer, presampling, initial, temporal / spatiotemporal, 4 spatial)
+constexpr int EV_POOL = 2 * 2 * (10 * 65 + 3 + 8);   // x2: the two halves of an overlapped batch
 #ifndef MPT_TRACE_BLOCKS_PER_CU
 #define MPT_TRACE_BLOCKS_PER_CU 5
 #endif
@@ -107,6 +108,7 @@ struct MptContext {
     float box_pad = 0.0f;
     int light_bvh = 1;                    // MPT_LIGHT_BVH at mpt_create: 0 = one closest-hit traversal per light-hit query
     bool light_bvh_ok = false;            // the light BVH matches the materials (else: the exact closest-hit path)
+    int light_bvh_max_stack = 1 << 30;    // test hook (MPT_LIGHT_BVH_MAX_STACK): a lower traversal-stack limit
     DBuf<int32_t> idx, mat_idx, mat_prio, emissive, tex_dims;
     DBuf<float> pos, nrm, uv;
     DBuf<uint8_t> has_n, tex;
@@ -422,7 +424,7 @@ int upload_alpha_flags(MptContext* c) {
 // for a nearer (or equally near, lower-index) triangle, equals the whole-scene closest hit
 // whenever that one is a light, and every other outcome contributes nothing.  Rebuilt when
 // a material edit changes the set; alpha-test flags as upload_alpha_flags.
-int build_light_bvh(MptContext* c) {
+static int build_light_bvh_impl(MptContext* c) {
     std::vector<uint8_t> lit(c->h_mats.size()), aflag(c->h_mats.size());
     for (size_t i = 0; i < c->h_mats.size(); i++) {
         const MptMaterial& m = c->h_mats[i];
@@ -447,7 +449,7 @@ int build_light_bvh(MptContext* c) {
             for (size_t k = 0; k < prims.size(); k++)
                 for (int j = 0; j < 3; j++) sub[3 * k + j] = c->h_idx[3 * (size_t)prims[k] + j];
             build_bvh8(c->h_pos.data(), sub.data(), (int32_t)prims.size(), c->bvh_light, 3, c->box_pad);
-            if (2 * c->bvh_light.depth + 2 > MAX_STACK) {
+            if (2 * c->bvh_light.depth + 2 > std::min(MAX_STACK, c->light_bvh_max_stack)) {
                 // too deep for the traversal stack: light-hit queries take the (exact)
                 // whole-scene closest-hit path instead
                 c->h_light_prims.clear();
@@ -472,6 +474,21 @@ int build_light_bvh(MptContext* c) {
     }
     HIPCHK(hipStreamSynchronize(st));
     c->light_bvh_ok = true;
+    return MPT_OK;
+}
+
+// A light BVH that cannot be built or uploaded is an optimisation lost, not an error: the
+// light-hit queries then take the exact whole-scene closest-hit path (light_bvh_ok false),
+// so a material edit never fails half-applied because of it.
+int build_light_bvh(MptContext* c) {
+    if (build_light_bvh_impl(c) == MPT_OK) return MPT_OK;
+    (void)hipGetLastError();
+    (void)hipStreamSynchronize(c->stream);
+    c->nodes_light.release();
+    c->tris_light.release();
+    c->h_light_prims.clear();
+    c->light_bvh_ok = false;
+    g_err.clear();
     return MPT_OK;
 }
 
@@ -649,10 +666,18 @@ static int create_context(MptContext* c, int device, void* hip_stream) {
     HIPCHK(c->spill.alloc((size_t)c->grid * TRAV_BLOCK * SPILL_WORDS));
     HIPCHK(c->srgb.alloc(256));
     HIPCHK(launch_srgb_table(c->srgb.p, c->stream));
+    return MPT_OK;
+}
+
+// The timing events (two pools of EV_POOL), created on the first mpt_enable_stats that
+// turns timing on: a context that never times its kernels holds none.  Handles already
+// created are kept, so a retry after a failure resumes where it stopped.
+static int ensure_events(MptContext* c) {
     for (int p = 0; p < 2; p++) {
-        for (int i = 0; i < EV_POOL; i++) HIPCHK(hipEventCreate(&c->ev[p][i]));
-        HIPCHK(hipEventCreate(&c->ev_frame[p][0]));
-        HIPCHK(hipEventCreate(&c->ev_frame[p][1]));
+        for (int i = 0; i < EV_POOL; i++)
+            if (!c->ev[p][i]) HIPCHK(hipEventCreate(&c->ev[p][i]));
+        for (int k = 0; k < 2; k++)
+            if (!c->ev_frame[p][k]) HIPCHK(hipEventCreate(&c->ev_frame[p][k]));
     }
     return MPT_OK;
 }
@@ -666,6 +691,7 @@ int mpt_create(int device, void* hip_stream, MptContext** out) {
     if (const char* e = std::getenv("MPT_SHADE_CLASSES")) c->shade_classes = std::atoi(e);
     if (const char* e = std::getenv("MPT_LIGHT_BVH")) c->light_bvh = std::atoi(e);
     if (const char* e = std::getenv("MPT_OVERLAP")) c->overlap = std::atoi(e);
+    if (const char* e = std::getenv("MPT_LIGHT_BVH_MAX_STACK")) c->light_bvh_max_stack = std::atoi(e);
     int r = create_context(c, device, hip_stream);
     if (r != MPT_OK) {
         const std::string msg = g_err;
@@ -972,9 +998,9 @@ static int prepare_batch(MptContext* c, const MptFrame* f, int batch) {
 // The second stream, its events and traversal spill area (overlapped batches), on first use.
 static int ensure_overlap(MptContext* c) {
     if (c->stream2) return MPT_OK;
-    HIPCHK(c->spill2.alloc(c->spill.n));
+    if (c->spill2.n != c->spill.n) HIPCHK(c->spill2.alloc(c->spill.n));
     for (hipEvent_t* e : {&c->ev_fork, &c->ev_first, &c->ev_acc, &c->ev_join})
-        HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+        if (!*e) HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));   // kept across a failed attempt
     HIPCHK(hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking));
     return MPT_OK;
 }
@@ -1115,6 +1141,7 @@ static bool batchable(const MptFrame& a, const MptFrame& b) {
 int mpt_render_frames(MptContext* c, const MptFrame* frames, int32_t count, int32_t max_batch) {
     if (!c || !frames || count < 0) return fail(MPT_ERR_INVALID_ARGUMENT, "NULL argument or negative count");
     if (count == 0) return MPT_OK;
+    HIPCHK(hipSetDevice(c->device));   // default_batch sizes the wavefront from this device's free memory
     if (max_batch <= 0) max_batch = default_batch(c, frames[0]);
     max_batch = std::min<int32_t>(max_batch, MPT_MAX_BATCH);
     int i = 0;
@@ -1206,6 +1233,10 @@ int mpt_enable_stats(MptContext* c, int enable, int instrumented) {
     if (!c) return fail(MPT_ERR_INVALID_ARGUMENT, "NULL context");
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipStreamSynchronize(c->stream));
+    if (enable) {
+        int r = ensure_events(c);
+        if (r != MPT_OK) { c->timing = false; return r; }
+    }
     c->timing = enable != 0;
     c->instrumented = instrumented != 0;
     c->ev_pending[0] = c->ev_pending[1] = false;
@@ -1259,6 +1290,10 @@ int mpt_get_stats(MptContext* c, MptStats* out) {
     out->shade_generic_vertices = rc[4];
     out->shade_generic_ms = c->stage_ms[KT_SHADE_GENERIC];
     out->shade_launches = c->stage_launches[KT_SHADE];
+    for (int k = 0; k < 5; k++) {
+        out->restir_kernel_ms[k] = c->stage_ms[KT_GBUFFER + k];
+        out->restir_kernel_launches[k] = c->stage_launches[KT_GBUFFER + k];
+    }
     out->trace_launches = c->trace_launches;
     out->frames = c->frames;
     out->frame_ms = c->frame_ms;

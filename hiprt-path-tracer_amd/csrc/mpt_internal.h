@@ -167,7 +167,10 @@ constexpr int N_TRACE_MODES = 5;
 constexpr int N_RAY_COUNTS = 5;   // DevPaths::ray_counts
 // timed kernel kinds: 0..2 = traversal stages (trace modes), then the others
 enum { KT_CAMERA = 3, KT_SHADE = 4, KT_RESOLVE = 5, KT_ACCUMULATE = 6, KT_COMPACT = 7, KT_RESTIR = 8, KT_SPLIT = 9,
-       KT_MISS = 10, KT_SHADE_GENERIC = 11, KT_COUNT = 12 };
+       KT_MISS = 10, KT_SHADE_GENERIC = 11,
+       // the ReSTIR DI kernels one by one (inside KT_RESTIR's span): G-buffer, presampling,
+       // initial candidates, temporal / fused spatiotemporal reuse, spatial reuse
+       KT_GBUFFER = 12, KT_RS_PRESAMPLE = 13, KT_RS_INITIAL = 14, KT_RS_REUSE = 15, KT_RS_SPATIAL = 16, KT_COUNT = 17 };
 constexpr uint32_t QM_CONT = 16u;
 // mat_tex bits: a texture feeds the resolved material; the material is outside the
 // plain-dielectric class (coat, sheen, metallic, transmission or thin film may be non-zero)

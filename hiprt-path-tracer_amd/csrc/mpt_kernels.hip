@@ -1433,9 +1433,15 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_
                     }
                 } else if (op == OP_CONT) {
                     // continuation (FullPathTracer.h:221-247)
+#ifdef MPT_DEBUG_SLOT
+                    if (slot == MPT_DEBUG_SLOT) printf("GPU b%d cont mi %d vs %d %d %d %d st %x %x %x L %a %a %a f %a %a %a pdf %a\n", bounce, (int)(mp - S.mats_res), tv.incident, tv.outgoing, (int)tv.inside, tv.pos, tv.st[0], tv.st[1], tv.st[2], L.x, L.y, L.z, f.r, f.g, f.b, pdf);
+#endif
                     vs = tv;
                     Col att = f * absr(dot(L, sn)) / pdf;
-                    if (pdf > 0.0f) {
+                    // 'if (bsdf_pdf <= 0.0f) break' (FullPathTracer.h:228): a NaN pdf (e.g. a
+                    // thin-film glass lobe sampled from inside, TIR in the film) continues, and the
+                    // NaN ray ends as a sample the sanity check discards
+                    if (!(pdf <= 0.0f)) {
                         bool alive = true;
                         if (bounce >= rs.russian_roulette_min_depth && rs.use_russian_roulette) {
                             float sp;
@@ -1891,15 +1897,21 @@ static void launch_trace_mode(const TraceArgs& a, int grid, bool stats, hipStrea
 }
 
 // event pair around a non-traversal kernel (KT_* id), when timing is enabled
+// (the pair is reserved at construction, so scopes may nest: the ReSTIR DI span and its kernels)
 struct TimedScope {
     LaunchCfg& cfg;
     hipStream_t st;
-    bool on;
-    TimedScope(LaunchCfg& c, hipStream_t s, int kind) : cfg(c), st(s), on(c.ev_pool && c.ev_used + 2 <= c.ev_cap) {
-        if (on) { cfg.ev_mode[cfg.ev_used / 2] = kind; hipEventRecord(cfg.ev_pool[cfg.ev_used], st); }
+    int idx;
+    TimedScope(LaunchCfg& c, hipStream_t s, int kind) : cfg(c), st(s), idx(-1) {
+        if (c.ev_pool && c.ev_used + 2 <= c.ev_cap) {
+            idx = cfg.ev_used;
+            cfg.ev_used += 2;
+            cfg.ev_mode[idx / 2] = kind;
+            hipEventRecord(cfg.ev_pool[idx], st);
+        }
     }
     ~TimedScope() {
-        if (on) { hipEventRecord(cfg.ev_pool[cfg.ev_used + 1], st); cfg.ev_used += 2; }
+        if (idx >= 0) hipEventRecord(cfg.ev_pool[idx + 1], st);
     }
 };
 
@@ -1985,10 +1997,15 @@ static void launch_restir(const DevScene& S, DevPaths& P, const MptFrame* d_fram
                           {{P.pgb_pos, 16}, {P.pgb_sn, 16}, {P.pgb_gn, 16}, {P.pgb_view, 16}, {P.pgb_meta, 16},
                            {P.pgb_vsA, 16}, {P.pgb_vsB, 16}, {P.pgb_mat, MS}});
     }
-    if (hf.options.restir_di_do_lights_presampling)   // ReSTIRDIRenderPass::launch (.cpp:241-242)
+    if (hf.options.restir_di_do_lights_presampling) {   // ReSTIRDIRenderPass::launch (.cpp:241-242)
+        TimedScope tk(cfg, st, KT_RS_PRESAMPLE);
         hipLaunchKernelGGL(k_restir_presample, dim3((n_pl + TB - 1) / TB), dim3(TB), 0, st, S, P, d_frame);
+    }
     const dim3 g(cfg.grid_persistent);
-    launch_ovr<KInitial>(ovr, g, st, S, P, d_frame);
+    {
+        TimedScope tk(cfg, st, KT_RS_INITIAL);
+        launch_ovr<KInitial>(ovr, g, st, S, P, d_frame);
+    }
     float4* last_out = restir_buffer(P, cfg.restir_out_sp2);
     // the reference-default weights run a kernel variant with the mode compiled in
     const bool def_bias = hf.options.restir_di_bias_correction_weights == MPT_RESTIR_DI_BIAS_PAIRWISE_MIS_DEFENSIVE &&
@@ -1997,12 +2014,16 @@ static void launch_restir(const DevScene& S, DevPaths& P, const MptFrame* d_fram
         P.rs_tin = last_out;
         P.rs_out = last_out == P.rs_sp1 ? P.rs_sp2 : P.rs_sp1;
         halo_exchange(hf, cfg, st, MPT_HALO_RESERVOIRS, 0, cfg.halo_rows, {{P.rs_tin, RB}});
-        if (def_bias) launch_ovr<KSpatiotemporal>(ovr, g, st, S, P, d_frame);
-        else launch_ovr<KSpatiotemporalAny>(ovr, g, st, S, P, d_frame);
+        {
+            TimedScope tk(cfg, st, KT_RS_REUSE);
+            if (def_bias) launch_ovr<KSpatiotemporal>(ovr, g, st, S, P, d_frame);
+            else launch_ovr<KSpatiotemporalAny>(ovr, g, st, S, P, d_frame);
+        }
         for (int pass = 1; pass < rd.number_of_passes; pass++) {
             float4* in = P.rs_out;
             float4* out = in == P.rs_sp1 ? P.rs_sp2 : P.rs_sp1;
             halo_exchange(hf, cfg, st, MPT_HALO_RESERVOIRS, pass, cfg.halo_rows, {{in, RB}});
+            TimedScope tk(cfg, st, KT_RS_SPATIAL);
             if (def_bias) launch_ovr<KSpatial>(ovr, g, st, S, P, d_frame, pass, (const float4*)in, out);
             else launch_ovr<KSpatialAny>(ovr, g, st, S, P, d_frame, pass, (const float4*)in, out);
             P.rs_out = out;
@@ -2017,6 +2038,7 @@ static void launch_restir(const DevScene& S, DevPaths& P, const MptFrame* d_fram
             P.rs_tin = last_out;
             float4* tout = rd.do_spatial_reuse_pass ? P.rs_init : (last_out == P.rs_sp1 ? P.rs_sp2 : P.rs_sp1);
             halo_exchange(hf, cfg, st, MPT_HALO_RESERVOIRS, 0, cfg.halo_rows, {{P.rs_tin, RB}});
+            TimedScope tk(cfg, st, KT_RS_REUSE);
             launch_ovr<KTemporal>(ovr, g, st, S, P, d_frame, (const float4*)P.rs_tin, tout);
             cur = tout;
         }
@@ -2025,6 +2047,7 @@ static void launch_restir(const DevScene& S, DevPaths& P, const MptFrame* d_fram
                 float4* in = pass == 0 ? cur : ((pass & 1) ? P.rs_sp1 : P.rs_sp2);
                 float4* out = pass == 0 ? P.rs_sp1 : ((pass & 1) ? P.rs_sp2 : P.rs_sp1);
                 halo_exchange(hf, cfg, st, MPT_HALO_RESERVOIRS, pass + 1, cfg.halo_rows, {{in, RB}});
+                TimedScope tk(cfg, st, KT_RS_SPATIAL);
                 if (def_bias) launch_ovr<KSpatial>(ovr, g, st, S, P, d_frame, pass, (const float4*)in, out);
                 else launch_ovr<KSpatialAny>(ovr, g, st, S, P, d_frame, pass, (const float4*)in, out);
                 cur = out;
@@ -2069,7 +2092,10 @@ hipError_t launch_frame(const DevScene& S, const DevPaths& P0, const MptFrame* d
         if (b == 0 && cfg.ev_first_trace) hipEventRecord(cfg.ev_first_trace, st);
         if (restir && b == 0) {
             if (cfg.halo_fn) hipMemsetAsync(&P.counters[CTR_REPROJ], 0, sizeof(int32_t), st);
-            hipLaunchKernelGGL(k_gbuffer, dim3(blocks_for(n)), dim3(TB), 0, st, S, P, d_frame);
+            {
+                TimedScope tk(cfg, st, KT_GBUFFER);
+                hipLaunchKernelGGL(k_gbuffer, dim3(blocks_for(n)), dim3(TB), 0, st, S, P, d_frame);
+            }
             launch_restir(S, P, d_frame, hf, cfg, st);
         }
         hipMemsetAsync(&P.counters[c_next], 0, sizeof(int32_t), st);

@@ -295,3 +295,137 @@ def with_alpha_cards(sd: SceneData, opacity: float = 0.5, tex_size: int = 16, al
     out.camera_info = sd.camera_info
     out.name = sd.name + "+alpha_cards"
     return out.finalize()
+
+
+def _panel_grid(x0, x1, y0, y1, z, n=4, flip=False):
+    """n x n grid of quads on the plane z = const facing +z (toward the Cornell camera):
+    vertices [(n+1)^2, 3], texcoords in [0, 1]^2, triangles [2 n^2, 3]."""
+    xs, ys = np.linspace(x0, x1, n + 1), np.linspace(y0, y1, n + 1)
+    yy, xx = np.meshgrid(ys, xs, indexing="ij")
+    V = np.stack([xx, yy, np.full_like(xx, z)], -1).reshape(-1, 3)
+    uv = np.stack([(xx - x0) / (x1 - x0), (yy - y0) / (y1 - y0)], -1).reshape(-1, 2)
+    I = []
+    for j in range(n):
+        for i in range(n):
+            a, b, c, d = j * (n + 1) + i, j * (n + 1) + i + 1, (j + 1) * (n + 1) + i + 1, (j + 1) * (n + 1) + i
+            I += [[a, b, c], [a, c, d]] if not flip else [[a, c, b], [a, d, c]]
+    return V.astype(np.float32), uv.astype(np.float32), np.array(I, np.int64)
+
+
+def _tex(rng, size, lo=0, hi=256, channels=(0, 1, 2), alpha=255):
+    t = np.zeros((size, size, 4), np.uint8)
+    for c in channels:
+        t[..., c] = rng.integers(lo, hi, (size, size))
+    t[..., 3] = alpha
+    return t
+
+
+def with_textured_panels(sd: SceneData, seed: int = 3) -> SceneData:
+    """Adds three textured panels in front of the Cornell box's back wall that drive every
+    texture slot of RendererMaterial (Material.h:140-159, read by get_intersection_material,
+    Device/includes/Material.h:47-159):
+    * panel 0 (flat normals): base colour (sRGB), normal map (Texture.h:209-222),
+      roughness-metallic (G roughness, B metallic);
+    * panel 1 (smooth, tilted vertex normals): base colour, emission texture (index > 0, so
+      emissive_texture_used, Material.h:109), specular, specular tint, specular colour;
+    * panel 2 (flat): separate metallic and roughness textures, coat, coat roughness, sheen,
+      sheen roughness, sheen colour, anisotropy, anisotropy rotation, Oren-Nayar sigma, and a
+      normal map.
+    Textures are seeded RGBA8 noise of a few levels (alpha 255)."""
+    rng = np.random.default_rng(seed)
+    S = 16
+    texs = list(sd.textures)
+    t0 = len(texs)
+
+    def add(t):
+        texs.append(t)
+        return len(texs) - 1
+
+    def normal_map():
+        n = rng.normal(size=(S, S, 3)) * np.array([0.35, 0.35, 0.0]) + np.array([0.0, 0.0, 1.0])
+        n /= np.linalg.norm(n, axis=-1, keepdims=True)
+        t = np.zeros((S, S, 4), np.uint8)
+        t[..., :3] = np.clip(np.round((n * 0.5 + 0.5) * 255.0), 0, 255).astype(np.uint8)
+        t[..., 3] = 255
+        return t
+
+    def levels(vals, chans=(0,)):
+        t = np.zeros((S, S, 4), np.uint8)
+        pick = np.asarray(vals, np.uint8)[rng.integers(0, len(vals), (S, S))]
+        for c in chans:
+            t[..., c] = pick
+        t[..., 3] = 255
+        return t
+
+    mats = []
+    # panel 0
+    m0 = abi.Material.from_buffer_copy(_mat((0.7, 0.7, 0.7), rough=0.5))
+    if t0 == 0:
+        add(_tex(rng, S, 200, 256))           # texture 0: never an emission texture (index > 0 rule)
+    m0.base_color_texture_index = add(_tex(rng, S, 40, 256))
+    m0.normal_map_texture_index = add(normal_map())
+    rm = np.zeros((S, S, 4), np.uint8)
+    rm[..., 1] = rng.choice([40, 120, 220], (S, S))           # roughness
+    rm[..., 2] = rng.choice([0, 0, 128, 255], (S, S))         # metallic
+    rm[..., 3] = 255
+    m0.roughness_metallic_texture_index = add(rm)
+    mats.append(m0)
+    # panel 1
+    m1 = abi.Material.from_buffer_copy(_mat((0.5, 0.6, 0.7), rough=0.35))
+    m1.base_color_texture_index = add(_tex(rng, S, 60, 256))
+    em = np.zeros((S, S, 4), np.uint8)
+    em[..., :3] = np.where(rng.random((S, S, 1)) < 0.3, rng.integers(128, 256, (S, S, 3)), 0)
+    em[..., 3] = 255
+    m1.emission_texture_index = add(em)
+    m1.emissive_texture_used = True
+    m1.emission = abi.Color(1.0, 1.0, 1.0)
+    m1.emission_strength = 3.0
+    m1.specular_texture_index = add(levels([60, 160, 255]))
+    m1.specular_tint_texture_index = add(levels([0, 128, 255]))
+    m1.specular_color_texture_index = add(_tex(rng, S, 100, 256))
+    mats.append(m1)
+    # panel 2
+    m2 = abi.Material.from_buffer_copy(_mat((0.6, 0.45, 0.3), rough=0.4))
+    m2.base_color_texture_index = add(_tex(rng, S, 60, 256))
+    m2.metallic_texture_index = add(levels([0, 90, 255]))
+    m2.roughness_texture_index = add(levels([30, 110, 200]))
+    m2.coat_texture_index = add(levels([0, 160, 255]))
+    m2.coat_roughness_texture_index = add(levels([10, 90]))
+    m2.sheen_texture_index = add(levels([0, 200]))
+    m2.sheen_roughness_texture_index = add(levels([60, 180]))
+    m2.sheen_color_texture_index = add(_tex(rng, S, 80, 256))
+    m2.anisotropic_texture_index = add(levels([0, 120, 230]))
+    m2.anisotropic_rotation_texture_index = add(levels([0, 64, 190]))
+    m2.oren_sigma_texture_index = add(levels([20, 90]))
+    m2.normal_map_texture_index = add(normal_map())
+    mats.append(m2)
+
+    nm = len(sd.materials)
+    out = SceneData()
+    V, N, HN, UV, I, MI = [sd.vertices], [sd.normals], [sd.has_normals], [sd.texcoords], [sd.triangle_indices.reshape(-1, 3)], \
+        [sd.material_indices]
+    nv = len(sd.vertices)
+    z = -1.0
+    for k, (x0, x1) in enumerate([(-0.95, -0.35), (-0.3, 0.3), (0.35, 0.95)]):
+        pv, puv, pi = _panel_grid(x0, x1, 1.25, 1.85, z)
+        if k == 1:   # smooth, tilted vertex normals
+            pn = np.stack([0.25 * (puv[:, 0] - 0.5), 0.2 * (puv[:, 1] - 0.5), np.ones(len(pv))], -1)
+            pn /= np.linalg.norm(pn, axis=1, keepdims=True)
+            hn = np.ones(len(pv), np.uint8)
+        else:
+            pn = np.zeros_like(pv)
+            hn = np.zeros(len(pv), np.uint8)
+        V.append(pv); N.append(pn.astype(np.float32)); HN.append(hn); UV.append(puv)
+        I.append(pi + nv); MI.append(np.full(len(pi), nm + k, np.int32))
+        nv += len(pv)
+    out.vertices = np.concatenate(V).astype(np.float32)
+    out.normals = np.concatenate(N).astype(np.float32)
+    out.has_normals = np.concatenate(HN).astype(np.uint8)
+    out.texcoords = np.concatenate(UV).astype(np.float32)
+    out.triangle_indices = np.concatenate(I).astype(np.int32).ravel()
+    out.material_indices = np.concatenate(MI).astype(np.int32)
+    out.materials = list(sd.materials) + mats
+    out.textures = texs
+    out.camera_info = sd.camera_info
+    out.name = sd.name + "+textured_panels"
+    return out.finalize()

@@ -431,6 +431,11 @@ typedef struct MptStats {
      * generic-material kernel and the vertices it shaded */
     double shade_generic_ms;
     uint64_t shade_generic_vertices;
+    /* the ReSTIR DI kernels one by one (timing enabled): 0 G-buffer (k_gbuffer), 1 lights
+     * presampling, 2 initial candidates, 3 temporal or fused spatiotemporal reuse, 4 spatial
+     * reuse passes; summed time and launches */
+    double restir_kernel_ms[5];
+    uint32_t restir_kernel_launches[5];
 } MptStats;
 
 #define MPT_FB_COLOR 0        /* 'pixels': running SUM of samples (RenderData.h:34-36) */

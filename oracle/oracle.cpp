@@ -18,21 +18,29 @@
  *                           FilterFunction.h:19-48 with alpha testing off)
  *   frame loop / seeds .... src/Renderer/CPURenderer.cpp:264-296 (driven by the caller)
  *
- * Differences from the reference, all deliberate and documented in DESIGN.md:
+ *   adaptive sampling ..... src/Device/includes/AdaptiveSampling.h:11-104, CameraRays.h:88-125
+ *   alpha testing ......... FilterFunction.h:19-48 (accept probability alpha_opacity x base-colour
+ *                           alpha, the candidate's uniform hashed from (query, primitive))
+ *   ReSTIR DI ............. kernels/ReSTIR/DI/*.h, includes/ReSTIR/DI/*.h (oracle_restir.h)
+ *   BSDFs ................. includes/BSDFs/*.h (oracle_bsdf.h)
+ *
+ * Differences from the reference, all deliberate and documented in DESIGN.md §2:
  *   * the octree/k-DOP BVH is replaced by a binned-SAH BVH2 (same closest-hit
  *     semantics; exact-t ties, which the reference resolves by octree visit order,
  *     are resolved to the lower primitive index so the answer is BVH-independent);
- *   * transcendentals through double libm (oracle_math.h);
- *   * alpha testing, adaptive sampling, low-resolution mode and ReSTIR DI are not
- *     restated here (they are rejected with an error);
+ *   * transcendentals through double libm (oracle_math.h, sharing the parity layer
+ *     csrc/tmath.h with the product; pinned against double libm by tests/test_tmath.py);
+ *   * alpha testing draws the candidate's uniform from a hash of (query, primitive)
+ *     instead of the path's RNG inside HIPRT's traversal (same accept probability);
+ *   * the low-resolution interactive mode is rejected (a data race in the reference);
  *   * undefined behaviour of the reference (uninitialised locals) is given a fixed value.
  *
  * PARITY STATUS: "parity unpinned" against the reference itself -- the reference's
  * CPU megakernel cannot be built here without writing stand-ins for the absent
  * HIPRT/Orochi headers (un-vendored submodules), and the reference ships no test
  * vectors.  The pieces that ARE pinned to reference data: the BSDF layers against the
- * reference's own baked directional-albedo LUTs (tests/test_oracle_luts.py), and the
- * white-furnace energy check (BSDFsData.h:26).
+ * reference's own baked directional-albedo LUTs (white furnace, tests/test_oracle.py and
+ * tests/test_lobes.py), and the LUT baker against the shipped LUTs (tests/test_bake.py).
  */
 #include <algorithm>
 #include <cmath>
@@ -1052,6 +1060,7 @@ PixelOut path_pixel(Ctx& c, int x, int y, GB& gb) {
             f3 bd;
             Col bc = bsdf_sample(c.bc, c.override_, pl.material, pl.vs, -rd, hi.shading_normal, hi.geometric_normal, bd, bpdf, rng);
             Col att = bc * absf(dot(bd, hi.shading_normal)) / bpdf;
+            if (g_dbg) printf("CPU b%d cont vs %d %d %d L %a %a %a f %a %a %a pdf %a\n", bounce, pl.vs.incident_mat_index, pl.vs.outgoing_mat_index, (int)pl.vs.inside_material, bd.x, bd.y, bd.z, bc.r, bc.g, bc.b, bpdf);
             if (bpdf <= 0.0f) break;
             if (!russian_roulette(rs, bounce, pl.throughput, att, rng)) break;
             pl.throughput *= get_dispersion_ray_color(pl.vs.sampled_wavelength, pl.material.dispersion_scale);

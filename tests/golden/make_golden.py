@@ -5,6 +5,8 @@
   (the seed 42 sequence is also the one CPURenderer.cpp:90,284 produces).
 * cornell_32x18_mis_2spp.npz -- the CPU oracle's Cornell image (regression fixture of
   the restated algorithm; not a reference output -- see DESIGN.md "parity unpinned").
+* c1_cornell_256_lambert_1spp.npz -- the oracle's whole C1 frame (BASELINE.json config 1:
+  Cornell 256x256, 1 spp, Lambert override, RIS, 3 bounces; tests/test_configs.py).
 """
 import json
 import os
@@ -30,6 +32,9 @@ def main():
     o = orc.Oracle(sd, scene.load_luts())
     img, alb, nrm = o.render(_frames(sd, 32, 18, 2), aov=True)
     np.savez_compressed(os.path.join(HERE, "cornell_32x18_mis_2spp.npz"), color=img, albedo=alb, normals=nrm)
+    from test_configs import c1_frames
+    img, alb, nrm = o.render(c1_frames(sd), aov=True)
+    np.savez_compressed(os.path.join(HERE, "c1_cornell_256_lambert_1spp.npz"), color=img, albedo=alb, normals=nrm)
     print("ok")
 
 

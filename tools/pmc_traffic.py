@@ -5,7 +5,9 @@ Corrections (MI355X_MICROARCH.md, HBM / rocprofv3): on gfx950 FETCH_SIZE tallies
 counters, 128 * TCC_EA0_RDREQ_128B + 64 * TCC_EA0_RDREQ_64B + 32 * TCC_EA0_RDREQ_32B
 (cross-checked against 2 x FETCH_SIZE); write bytes are WRITE_SIZE (KiB, exact for
 streaming stores).  Calibration in the same run: k_accumulate moves a known byte count
-(reads 100 B / pixel, writes 36 B / pixel).
+(reads 100 B / pixel, writes 36 B / pixel).  Pass 5: SQ_INSTS_VALU (wave-level VALU
+instructions, the traversal's issue roofline), SQ_WAVES, GRBM_GUI_ACTIVE (summed over the
+8 XCDs: effective clock = GRBM_GUI_ACTIVE / 8 / kernel time).
 usage: python tools/pmc_traffic.py gpurun_out/prof_<tag> profiles/<name>.json
 """
 import collections
@@ -30,7 +32,7 @@ def mean(x):
 
 
 def main(src, dst):
-    passes = [load(os.path.join(src, f"pmc{i}")) for i in (1, 2, 3, 4)]
+    passes = [load(os.path.join(src, f"pmc{i}")) for i in (1, 2, 3, 4, 5)]
     names = set().union(*[set(p) for p in passes])
     out = {}
     for k in sorted(names):
@@ -43,7 +45,12 @@ def main(src, dst):
         wr = 1024 * mean(w) if w else None
         hm = passes[3].get(k, {})
         hit, miss = mean(hm.get("TCC_HIT_sum", [])), mean(hm.get("TCC_MISS_sum", []))
+        sq = passes[4].get(k, {})
+        valu = mean(sq.get("SQ_INSTS_VALU", []))
+        grbm = mean(sq.get("GRBM_GUI_ACTIVE", []))
         out[k] = {"launches": len(f) or len(w), "read_bytes": rd, "write_bytes": wr,
+                  "valu_insts": valu, "waves": mean(sq.get("SQ_WAVES", [])),
+                  "grbm_gui_active": grbm,
                   "traffic_bytes": (rd or 0.0) + (wr or 0.0) if rd is not None and wr is not None else None,
                   "fetch_size_x2_bytes": 2 * 1024 * mean(f) if f else None,
                   "l2_hit_rate": hit / (hit + miss) if hit is not None and hit + miss > 0 else None}
