@@ -191,6 +191,26 @@ DEV Col lambert_sample(const Mat& m, v3 n, v3& dir, float& pdf, Rng& rng) {
     dir = cosine_sample_around(n, rng);
     return lambert_eval(m, dot(n, dir), pdf);
 }
+// Oren-Nayar (BSDFs/OrenNayar.h:49-90) on local directions (z = the shading normal); like
+// the reference, no hemisphere test: a light below the surface gets a negative pdf.
+// A, B: SimplifiedRendererMaterial::get_oren_nayar_AB (Material.h:73-78)
+DEV Col oren_nayar_eval(const Mat& m, v3 lv, v3 ll, float& pdf) {
+    const float sti = sqrtf(1.0f - ll.z * ll.z), sto = sqrtf(1.0f - lv.z * lv.z);
+    float max_cos = 0.0f;
+    if (sti > 1.0e-4f && sto > 1.0e-4f) {
+        const float spi = ll.y / sti, cpi = ll.x / sti;
+        const float spo = lv.y / sto, cpo = lv.x / sto;
+        max_cos = maxr(0.0f, cpi * cpo + spi * spo);
+    }
+    float sa, tb;
+    if (absr(ll.z) > absr(lv.z)) { sa = sto; tb = sti / absr(ll.z); }
+    else { sa = sti; tb = sto / absr(lv.z); }
+    const float s2 = m.oren_nayar_sigma * m.oren_nayar_sigma;
+    const float A = 1.0f - s2 / (2.0f * (s2 + 0.33f));
+    const float B = 0.45f * s2 / (s2 + 0.09f);
+    pdf = ll.z * INV_PI;
+    return C3(m.base_color) * INV_PI * (A + B * max_cos * sa * tb);
+}
 
 // ----------------------------------------------------------------------------------
 // Fresnel + thin film
@@ -848,25 +868,39 @@ DEV Col principled_sample(const BCtx& c, const Mat& m, VState& vs, v3 view, v3 s
     return principled_eval(c, m, vs, view, sn, out, pdf);
 }
 
+// bsdf_dispatcher_eval / _sample (Dispatcher.h:18-68).  BSDF_OREN_NAYAR: the reference's
+// dispatcher line calls 'oren_nayar_brdf_eval<0>(material, view, normal, light, pdf)' on a
+// function that is not a template (Dispatcher.h:38), so that override does not compile there;
+// this is the evident intent, the world-space overload of OrenNayar.h:92-103 (local frame
+// from build_ONB around the shading normal) and its cosine-weighted sampler (:105-110).
 template <int OVERRIDE>
 DEV Col bsdf_eval(const BCtx& c, const Mat& m, VState& vs, v3 view, v3 sn, v3 L, float& pdf) {
     if (OVERRIDE == MPT_BSDF_LAMBERTIAN) return lambert_eval(m, dot(L, sn), pdf);
+    if (OVERRIDE == MPT_BSDF_OREN_NAYAR) {
+        v3 T, B;
+        build_onb(sn, T, B);
+        return oren_nayar_eval(m, to_local(T, B, sn, view), to_local(T, B, sn, L), pdf);
+    }
     return principled_eval(c, m, vs, view, sn, L, pdf);
 }
 // evaluation split into a per-vertex part and a per-light-direction part (see PEval)
 template <int OVERRIDE, bool FULL = true>
 DEV void bsdf_eval_pre(const BCtx& c, const Mat& m, const VState& vs, v3 view, v3 sn, PEval& e) {
-    if (OVERRIDE != MPT_BSDF_LAMBERTIAN) principled_eval_pre<FULL>(c, m, vs, view, sn, e);
+    if (OVERRIDE == MPT_BSDF_OREN_NAYAR) {
+        build_onb(sn, e.T, e.B);
+        e.lv = to_local(e.T, e.B, sn, view);
+    } else if (OVERRIDE != MPT_BSDF_LAMBERTIAN) principled_eval_pre<FULL>(c, m, vs, view, sn, e);
 }
 template <int OVERRIDE, bool FULL = true>
 DEV Col bsdf_eval_post(const BCtx& c, const Mat& m, VState& vs, const PEval& e, v3 sn, v3 L, float& pdf) {
     if (OVERRIDE == MPT_BSDF_LAMBERTIAN) return lambert_eval(m, dot(L, sn), pdf);
+    if (OVERRIDE == MPT_BSDF_OREN_NAYAR) return oren_nayar_eval(m, e.lv, to_local(e.T, e.B, sn, L), pdf);
     return principled_eval_post<FULL>(c, m, vs, e, sn, L, pdf);
 }
 // sample = sample_dir + bsdf_eval on the updated state (eval skipped when sample_dir is false)
 template <int OVERRIDE, bool FULL = true>
 DEV bool bsdf_sample_dir(const BCtx& c, const Mat& m, VState& vs, v3 view, v3 sn, v3 gn, v3& dir, Rng& rng) {
-    if (OVERRIDE == MPT_BSDF_LAMBERTIAN) { dir = cosine_sample_around(sn, rng); return true; }
+    if (OVERRIDE == MPT_BSDF_LAMBERTIAN || OVERRIDE == MPT_BSDF_OREN_NAYAR) { dir = cosine_sample_around(sn, rng); return true; }
     return principled_sample_dir<FULL>(c, m, vs, view, sn, gn, dir, rng);
 }
 template <int OVERRIDE>

@@ -597,8 +597,9 @@ int validate_frame(const MptFrame* f) {
         if (rs.wants_render_low_resolution && rs.allow_render_low_resolution)
             return fail(MPT_ERR_UNSUPPORTED, "ReSTIR DI with low-resolution rendering");
     }
-    if (f->options.bsdf_override != MPT_BSDF_NONE && f->options.bsdf_override != MPT_BSDF_LAMBERTIAN)
-        return fail(MPT_ERR_UNSUPPORTED, "only BSDF_NONE (Principled) and BSDF_LAMBERTIAN are implemented");
+    if (f->options.bsdf_override != MPT_BSDF_NONE && f->options.bsdf_override != MPT_BSDF_LAMBERTIAN &&
+        f->options.bsdf_override != MPT_BSDF_OREN_NAYAR)
+        return fail(MPT_ERR_INVALID_ARGUMENT, "bsdf_override must be BSDF_NONE, BSDF_LAMBERTIAN or BSDF_OREN_NAYAR");
     if (f->options.ris_use_visibility) return fail(MPT_ERR_UNSUPPORTED, "RISUseVisiblityTargetFunction not implemented");
     return MPT_OK;
 }

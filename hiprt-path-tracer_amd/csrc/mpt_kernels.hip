@@ -1927,6 +1927,7 @@ static void timed_trace(const TraceArgs& a, LaunchCfg& cfg, hipStream_t st) {
 template <template <int> class K, typename... Args>
 static void launch_ovr(int ovr, dim3 g, hipStream_t st, Args... args) {
     if (ovr == MPT_BSDF_LAMBERTIAN) hipLaunchKernelGGL(K<MPT_BSDF_LAMBERTIAN>::fn, g, dim3(TB), 0, st, args...);
+    else if (ovr == MPT_BSDF_OREN_NAYAR) hipLaunchKernelGGL(K<MPT_BSDF_OREN_NAYAR>::fn, g, dim3(TB), 0, st, args...);
     else hipLaunchKernelGGL(K<MPT_BSDF_NONE>::fn, g, dim3(TB), 0, st, args...);
 }
 template <int OVR> struct KInitial { static constexpr auto fn = k_restir_initial<OVR>; };
@@ -2081,7 +2082,7 @@ hipError_t launch_frame(const DevScene& S, const DevPaths& P0, const MptFrame* d
     int c_cur = CTR_Q0, c_next = CTR_Q1;
     const int nb = hf.render_settings.nb_bounces;
     // material classes (k_split / k_shade): Principled BSDF only (the Lambert override has one class)
-    const int classes = hf.options.bsdf_override == MPT_BSDF_LAMBERTIAN ? 0 : (cfg.shade_classes != 0 ? 1 : 0);
+    const int classes = hf.options.bsdf_override != MPT_BSDF_NONE ? 0 : (cfg.shade_classes != 0 ? 1 : 0);
     for (int b = 0; b <= nb; b++) {
         // continuation / camera rays
         hipMemsetAsync(&P.counters[CTR_FETCH], 0, sizeof(int32_t), st);
@@ -2114,6 +2115,8 @@ hipError_t launch_frame(const DevScene& S, const DevPaths& P0, const MptFrame* d
             TimedScope ts(cfg, st, KT_SHADE);
             if (hf.options.bsdf_override == MPT_BSDF_LAMBERTIAN) {
                 hipLaunchKernelGGL((k_shade<MPT_BSDF_LAMBERTIAN, false>), dim3(blocks_for(n)), dim3(TB), 0, st, sa);
+            } else if (hf.options.bsdf_override == MPT_BSDF_OREN_NAYAR) {
+                hipLaunchKernelGGL((k_shade<MPT_BSDF_OREN_NAYAR, false>), dim3(blocks_for(n)), dim3(TB), 0, st, sa);
             } else if (!classes) {
                 hipLaunchKernelGGL((k_shade<MPT_BSDF_NONE, false>), dim3(blocks_for(n)), dim3(TB), 0, st, sa);
             } else {

@@ -136,8 +136,9 @@ DEV float restir_target(const DevScene& S, const MptFrame& F, const BCtx& bc, RR
     if (cosv == 0.0f) return 0.0f;
     float bp;
     VState tv = s.vs;
-    Col f = ovr == MPT_BSDF_LAMBERTIAN ? bsdf_eval<MPT_BSDF_LAMBERTIAN>(bc, *s.m, tv, s.view, s.sn, dir, bp)
-                                       : bsdf_eval<MPT_BSDF_NONE>(bc, *s.m, tv, s.view, s.sn, dir, bp);
+    Col f = ovr == MPT_BSDF_LAMBERTIAN   ? bsdf_eval<MPT_BSDF_LAMBERTIAN>(bc, *s.m, tv, s.view, s.sn, dir, bp)
+            : ovr == MPT_BSDF_OREN_NAYAR ? bsdf_eval<MPT_BSDF_OREN_NAYAR>(bc, *s.m, tv, s.view, s.sn, dir, bp)
+                                         : bsdf_eval<MPT_BSDF_NONE>(bc, *s.m, tv, s.view, s.sn, dir, bp);
     Col e;
     if (flags & RF_ENVMAP) { float ep; e = env_eval(S, F, dir, ep); }
     else e = emission_of(S.mats[S.mat_idx[tri]]);

@@ -373,7 +373,7 @@ OK, ERR_INVALID_ARGUMENT, ERR_HIP, ERR_NO_SCENE, ERR_UNSUPPORTED, ERR_OUT_OF_MEM
 MAX_BATCH = 128
 DEFAULT_WAVEFRONT_PATHS = 1 << 25
 MAX_WAVEFRONT_PATHS = 1 << 29
-BSDF_NONE, BSDF_LAMBERTIAN = 0, 1
+BSDF_NONE, BSDF_LAMBERTIAN, BSDF_OREN_NAYAR = 0, 1, 2
 (BAKE_GGX_CONDUCTOR, BAKE_GGX_FRESNEL, BAKE_GLOSSY_DIELECTRIC, BAKE_GGX_GLASS, BAKE_GGX_GLASS_INVERSE,
  BAKE_GGX_THIN_GLASS) = range(6)
 (LSS_NO_DIRECT_LIGHT_SAMPLING, LSS_UNIFORM_ONE_LIGHT, LSS_BSDF, LSS_MIS_LIGHT_BSDF,

@@ -72,6 +72,7 @@ extern "C" {
 /* ------------------------------------------------------------------------- */
 #define MPT_BSDF_NONE 0        /* BSDF_NONE: Principled BSDF  (KernelOptions.h:21) */
 #define MPT_BSDF_LAMBERTIAN 1  /* BSDF_LAMBERTIAN                                   */
+#define MPT_BSDF_OREN_NAYAR 2  /* BSDF_OREN_NAYAR (OrenNayar.h; see dev_bsdf.h bsdf_eval) */
 
 #define MPT_LSS_NO_DIRECT_LIGHT_SAMPLING 0 /* KernelOptions.h:50-56 */
 #define MPT_LSS_UNIFORM_ONE_LIGHT 1

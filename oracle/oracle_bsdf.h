@@ -216,6 +216,40 @@ inline Col lambertian_sample(const Material& m, f3 n, f3& dir, float& pdf, Rng& 
 }
 
 // --------------------------------------------------------------------------------
+// Oren-Nayar (OrenNayar.h:49-110; A, B: Material.h:73-78).  The reference's dispatcher calls
+// 'oren_nayar_brdf_eval<0>(...)' on a non-template (Dispatcher.h:38): BSDF_OREN_NAYAR does not
+// compile there, and this restates the evident intent, the world-space overload.
+// --------------------------------------------------------------------------------
+inline Col oren_nayar_eval_local(const Material& m, f3 local_view, f3 local_light, float& pdf) {
+    float sin_theta_i = psqrt(1.0f - local_light.z * local_light.z);
+    float sin_theta_o = psqrt(1.0f - local_view.z * local_view.z);
+    float max_cos = 0.0f;
+    if (sin_theta_i > 1.0e-4f && sin_theta_o > 1.0e-4f) {
+        float sin_phi_i = local_light.y / sin_theta_i, cos_phi_i = local_light.x / sin_theta_i;
+        float sin_phi_o = local_view.y / sin_theta_o, cos_phi_o = local_view.x / sin_theta_o;
+        float d_cos = cos_phi_i * cos_phi_o + sin_phi_i * sin_phi_o;
+        max_cos = fmaxr(0.0f, d_cos);
+    }
+    float sin_alpha, tan_beta;
+    if (absf(local_light.z) > absf(local_view.z)) { sin_alpha = sin_theta_o; tan_beta = sin_theta_i / absf(local_light.z); }
+    else { sin_alpha = sin_theta_i; tan_beta = sin_theta_o / absf(local_view.z); }
+    float sigma2 = m.oren_nayar_sigma * m.oren_nayar_sigma;
+    float A = 1.0f - sigma2 / (2.0f * (sigma2 + 0.33f));
+    float B = 0.45f * sigma2 / (sigma2 + 0.09f);
+    pdf = local_light.z * INV_PI;
+    return Col(m.base_color.r, m.base_color.g, m.base_color.b) * INV_PI * (A + B * max_cos * sin_alpha * tan_beta);
+}
+inline Col oren_nayar_eval(const Material& m, f3 view, f3 n, f3 light, float& pdf) {
+    f3 t, b;
+    build_onb(n, t, b);
+    return oren_nayar_eval_local(m, world_to_local(t, b, n, view), world_to_local(t, b, n, light), pdf);
+}
+inline Col oren_nayar_sample(const Material& m, f3 view, f3 n, f3& dir, float& pdf, Rng& rng) {
+    dir = cosine_weighted_sample_around_normal(n, rng);
+    return oren_nayar_eval(m, view, n, dir, pdf);
+}
+
+// --------------------------------------------------------------------------------
 // Fresnel (Fresnel.h)
 // --------------------------------------------------------------------------------
 inline float F0_from_eta(float eta_t, float eta_i) {
@@ -919,10 +953,12 @@ inline Col principled_sample(const BsdfCtx& c, const Material& m, VolumeState& v
 inline Col bsdf_eval(const BsdfCtx& c, int override_, const Material& m, VolumeState& vs, f3 view, f3 sn, f3 gn, f3 L, float& pdf) {
     (void)gn;
     if (override_ == MPT_BSDF_LAMBERTIAN) return lambertian_eval(m, dot(L, sn), pdf);
+    if (override_ == MPT_BSDF_OREN_NAYAR) return oren_nayar_eval(m, view, sn, L, pdf);
     return principled_eval(c, m, vs, view, sn, L, pdf);
 }
 inline Col bsdf_sample(const BsdfCtx& c, int override_, const Material& m, VolumeState& vs, f3 view, f3 sn, f3 gn, f3& dir, float& pdf, Rng& rng) {
     if (override_ == MPT_BSDF_LAMBERTIAN) return lambertian_sample(m, sn, dir, pdf, rng);
+    if (override_ == MPT_BSDF_OREN_NAYAR) return oren_nayar_sample(m, view, sn, dir, pdf, rng);
     return principled_sample(c, m, vs, view, sn, gn, dir, pdf, rng);
 }
 

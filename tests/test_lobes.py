@@ -82,18 +82,15 @@ def _same(a, b, what):
     assert not bad.any(), f"{what}: {int(bad.sum())} values differ, first at {np.argwhere(bad)[:3].tolist()}"
 
 
-_gpu_cache = {}
-
-
 def _gpu(sd, luts):
+    """A fresh context per case: a sample whose sanity check fails writes nothing, not even
+    at sample 0 (FullPathTracer.h:293-294), so a reused context would show the previous
+    case's sums where the oracle starts from zero."""
     import mpt
-    key = id(sd)
-    if key not in _gpu_cache:
-        r = mpt.GPURenderer(0)
-        r.set_scene(sd)
-        r.set_luts(luts)
-        _gpu_cache[key] = r
-    return _gpu_cache[key]
+    r = mpt.GPURenderer(0)
+    r.set_scene(sd)
+    r.set_luts(luts)
+    return r
 
 
 def _render(r, frs, batched=False):
@@ -115,11 +112,11 @@ def test_principled_lobe_bit_exact(cornell, luts, case, strategy):
     lss = abi.LSS_MIS_LIGHT_BSDF if strategy == "mis" else abi.LSS_RIS_BSDF_AND_LIGHT
     frs = frames(cornell, lss)
     r = _gpu(cornell, luts)
-    r.update_materials(mats)
     try:
+        r.update_materials(mats)
         got = _render(r, frs, batched=strategy == "ris")
     finally:
-        r.update_materials(cornell.materials)
+        r.close()
     sd = copy.copy(cornell)
     sd.materials = mats
     o = orc.Oracle(sd, luts)

@@ -137,6 +137,8 @@ def test_oracle_restir_rejects_unsupported(cornell, luts, oracle_lib):
 CASES = {
     "principled": dict(),
     "lambert": dict(ovr=abi.BSDF_LAMBERTIAN),
+    "oren_nayar": dict(ovr=abi.BSDF_OREN_NAYAR),
+    "oren_nayar_unfused": dict(ovr=abi.BSDF_OREN_NAYAR, do_fused_spatiotemporal=False),
     "three_passes": dict(passes=3),
     "no_temporal_g_buffer": dict(do_temporal_reuse_pass=False),
     "permutation_sampling": dict(use_permutation_sampling=True),

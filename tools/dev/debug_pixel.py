@@ -3,7 +3,7 @@ usage: MPT_LIB_PATH=<debug lib> ORACLE_DBG_PIX=<pixel> python tests/dev/debug_pi
 import copy
 import os
 import sys
-sys.path.insert(0, os.path.join(os.path.dirname(__file__), ".."))
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "..", "tests"))
 sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "..", "hiprt-path-tracer_amd"))
 sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", ".."))
 import numpy as np

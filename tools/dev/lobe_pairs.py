@@ -3,7 +3,7 @@ import copy
 import itertools
 import sys
 import os
-sys.path.insert(0, os.path.join(os.path.dirname(__file__), ".."))
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "..", "tests"))
 sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "..", "hiprt-path-tracer_amd"))
 sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", ".."))
 import numpy as np
