@@ -162,6 +162,11 @@ struct MptContext {
     int halo_prev = 0;                     // halo agreed in the previous frame
     int32_t* h_reproj = nullptr;           // pinned readback of the reprojection offset
     DBuf<MptMaterial> mat_slot;
+    // extended light sampling (ensure_ext): x_per entries per path slot of the current batch
+    DBuf<float4> xq_o, xq_d, xq_hit, xrec;
+    DBuf<uint8_t> xq_occ, xq_flag;
+    DBuf<int32_t> xl_any, xl_cl, xl_light;
+    int x_per = 0, x_iter = 0;
     DBuf<uint64_t> stats;
     DBuf<uint64_t> ray_counts;
     // frames
@@ -292,6 +297,10 @@ DevPaths dev_paths(MptContext* c) {
     P.rs_lo = P.pix_off;
     P.rs_hi = P.pix_off + c->n_slots;
     P.rs_conv = part ? c->rs_conv.p : c->as_conv.p;
+    P.x_per = c->x_per;
+    P.x_iter = c->x_iter;
+    P.xq_o = c->xq_o.p; P.xq_d = c->xq_d.p; P.xq_hit = c->xq_hit.p; P.xq_occ = c->xq_occ.p; P.xq_flag = c->xq_flag.p;
+    P.xrec = c->xrec.p; P.xl_any = c->xl_any.p; P.xl_cl = c->xl_cl.p; P.xl_light = c->xl_light.p;
     return P;
 }
 
@@ -353,6 +362,36 @@ int ensure_batch(MptContext* c, int batch, bool mat_slot) {
         return alloc_fail(A.e, "path state for " + std::to_string(N) + " paths");
     }
     c->batch_cap = cap;
+    return MPT_OK;
+}
+
+// Bytes per ext entry: query ray (32), result (16), records (32), occlusion + flag (2), list
+// entries (12).
+constexpr size_t EXT_ENTRY_BYTES = 32 + 16 + 32 + 2 + 12;
+
+// Extended light sampling buffers for `batch` samples per pixel at `per` entries per slot
+// (ext_layout); per == 0 leaves them unused (released).  A failure releases the group.
+int ensure_ext(MptContext* c, int batch, int per, int iter) {
+    c->x_per = 0;
+    c->x_iter = 0;
+    if (per == 0) {
+        release_all(c->xq_o, c->xq_d, c->xq_hit, c->xrec, c->xq_occ, c->xq_flag, c->xl_any, c->xl_cl, c->xl_light);
+        return MPT_OK;
+    }
+    const size_t E = (size_t)std::max(c->n_slots, 1) * (size_t)batch * (size_t)per;
+    if (E >= ((size_t)1 << 31)) return fail(MPT_ERR_OUT_OF_MEMORY, "extended light sampling: more than 2^31 entries");
+    if (c->xq_o.n < E) {
+        HIPCHK(hipStreamSynchronize(c->stream));
+        Allocs A;
+        A(c->xq_o, E); A(c->xq_d, E); A(c->xq_hit, E); A(c->xrec, 2 * E); A(c->xq_occ, E); A(c->xq_flag, E);
+        A(c->xl_any, E); A(c->xl_cl, E); A(c->xl_light, E);
+        if (A.e != hipSuccess) {
+            release_all(c->xq_o, c->xq_d, c->xq_hit, c->xrec, c->xq_occ, c->xq_flag, c->xl_any, c->xl_cl, c->xl_light);
+            return alloc_fail(A.e, "extended light sampling: " + std::to_string(E) + " entries");
+        }
+    }
+    c->x_per = per;
+    c->x_iter = iter;
     return MPT_OK;
 }
 
@@ -561,6 +600,33 @@ int resolve_materials(MptContext* c) {
     return MPT_OK;
 }
 
+// Extended light sampling (mpt_internal.h): entries per light sample (*iter) and per path
+// slot (returned), 0 when the frame's light sampling fits the four staged queries of a slot
+// (one light sample; RIS with at most one BSDF candidate and no visibility target function).
+constexpr int MAX_EXT_PER_SLOT = 2048;
+int ext_layout(const MptFrame& f, int* iter) {
+    const MptRenderSettings& rs = f.render_settings;
+    int lss = f.options.direct_light_sampling;
+    if (lss == MPT_LSS_RESTIR_DI) {   // later bounces (Lights.h:243-275); bounce 0 uses the reservoir
+        switch (f.options.restir_di_later_bounces_sampling_strategy) {
+        case MPT_RESTIR_DI_LATER_BOUNCES_UNIFORM_ONE_LIGHT: lss = MPT_LSS_UNIFORM_ONE_LIGHT; break;
+        case MPT_RESTIR_DI_LATER_BOUNCES_BSDF: lss = MPT_LSS_BSDF; break;
+        case MPT_RESTIR_DI_LATER_BOUNCES_MIS_LIGHT_BSDF: lss = MPT_LSS_MIS_LIGHT_BSDF; break;
+        default: lss = MPT_LSS_RIS_BSDF_AND_LIGHT; break;
+        }
+    }
+    const int nl = std::max(0, rs.ris_number_of_light_candidates), nb = std::max(0, rs.ris_number_of_bsdf_candidates);
+    int it = 0;
+    if (lss == MPT_LSS_UNIFORM_ONE_LIGHT || lss == MPT_LSS_BSDF) it = 1;
+    else if (lss == MPT_LSS_MIS_LIGHT_BSDF) it = 2;
+    else if (lss == MPT_LSS_RIS_BSDF_AND_LIGHT) it = 2 * nl + nb;
+    const bool ext = rs.number_of_light_samples > 1 ||
+                     (lss == MPT_LSS_RIS_BSDF_AND_LIGHT && (nb > 1 || f.options.ris_use_visibility));
+    if (!ext || it == 0) it = 0;
+    if (iter) *iter = it;
+    return it * std::max(1, rs.number_of_light_samples);
+}
+
 int validate_frame(const MptFrame* f) {
     const MptRenderSettings& rs = f->render_settings;
     if (f->res_x <= 0 || f->res_y <= 0) return fail(MPT_ERR_INVALID_ARGUMENT, "resolution must be positive");
@@ -571,10 +637,15 @@ int validate_frame(const MptFrame* f) {
     if (rs.nb_bounces < 0 || rs.nb_bounces > 64) return fail(MPT_ERR_INVALID_ARGUMENT, "nb_bounces out of range");
     if (rs.wants_render_low_resolution && rs.allow_render_low_resolution && rs.accumulate)
         return fail(MPT_ERR_UNSUPPORTED, "low-resolution interactive mode not implemented");
-    if (rs.number_of_light_samples != 1) return fail(MPT_ERR_UNSUPPORTED, "number_of_light_samples must be 1");
-    if (rs.ris_number_of_bsdf_candidates < 0 || rs.ris_number_of_bsdf_candidates > 1)
-        return fail(MPT_ERR_UNSUPPORTED, "ris_number_of_bsdf_candidates must be 0 or 1");
-    if (rs.ris_number_of_light_candidates < 0) return fail(MPT_ERR_INVALID_ARGUMENT, "negative RIS light candidates");
+    // sample_many_lights / RIS (Lights.h:222-241, RIS.h:82-289); the UI ranges are 1-8 light
+    // samples and 0-16 candidates (ImGuiSettingsWindow.cpp:787, 833), the bounds here 64
+    if (rs.number_of_light_samples < 1 || rs.number_of_light_samples > 64)
+        return fail(MPT_ERR_INVALID_ARGUMENT, "number_of_light_samples must be in [1, 64]");
+    if (rs.ris_number_of_bsdf_candidates < 0 || rs.ris_number_of_bsdf_candidates > 64 ||
+        rs.ris_number_of_light_candidates < 0 || rs.ris_number_of_light_candidates > 64)
+        return fail(MPT_ERR_INVALID_ARGUMENT, "RIS candidate counts must be in [0, 64]");
+    if (ext_layout(*f, nullptr) > MAX_EXT_PER_SLOT)
+        return fail(MPT_ERR_UNSUPPORTED, "extended light sampling needs more than MAX_EXT_PER_SLOT entries per path");
     int lss = f->options.direct_light_sampling;
     if (lss < 0 || lss > MPT_LSS_RESTIR_DI) return fail(MPT_ERR_INVALID_ARGUMENT, "bad direct_light_sampling");
     if (lss == MPT_LSS_RESTIR_DI) {
@@ -600,7 +671,6 @@ int validate_frame(const MptFrame* f) {
     if (f->options.bsdf_override != MPT_BSDF_NONE && f->options.bsdf_override != MPT_BSDF_LAMBERTIAN &&
         f->options.bsdf_override != MPT_BSDF_OREN_NAYAR)
         return fail(MPT_ERR_INVALID_ARGUMENT, "bsdf_override must be BSDF_NONE, BSDF_LAMBERTIAN or BSDF_OREN_NAYAR");
-    if (f->options.ris_use_visibility) return fail(MPT_ERR_UNSUPPORTED, "RISUseVisiblityTargetFunction not implemented");
     return MPT_OK;
 }
 
@@ -956,12 +1026,16 @@ static int default_batch(MptContext* c, const MptFrame& f) {
     if (f.band_height <= 0 || f.band_count <= 0 || f.band_index < 0 || f.band_index >= f.band_count || f.res_x <= 0)
         return 1;
     const size_t pix = (size_t)std::max(1, rows_of(f.res_y, f.band_height, f.band_index, f.band_count)) * (size_t)f.res_x;
-    const size_t per = PATH_BYTES + ((c->any_tex || f.bsdf_flags.white_furnace_mode) ? sizeof(MptMaterial) : 0);
+    const size_t per = PATH_BYTES + ((c->any_tex || f.bsdf_flags.white_furnace_mode) ? sizeof(MptMaterial) : 0) +
+                       EXT_ENTRY_BYTES * (size_t)ext_layout(f, nullptr);
     size_t fr = 0, tot = 0;
     if (hipMemGetInfo(&fr, &tot) != hipSuccess) { (void)hipGetLastError(); fr = 0; }
     const size_t held = (size_t)c->batch_cap * (size_t)std::max(c->n_slots, 1) * per;
     const size_t paths = std::min<size_t>(MPT_DEFAULT_WAVEFRONT_PATHS, (fr + held) / 2 / per);
-    return (int)std::max<size_t>(1, std::min<size_t>(MPT_MAX_BATCH, paths / pix));
+    size_t b = std::max<size_t>(1, std::min<size_t>(MPT_MAX_BATCH, paths / pix));
+    const int xp = ext_layout(f, nullptr);   // ext entries of a launch stay below 2^31
+    if (xp > 0) b = std::max<size_t>(1, std::min<size_t>(b, (((size_t)1 << 31) - 1) / (pix * (size_t)xp)));
+    return (int)b;
 }
 
 // Validation and every allocation of a wavefront of `batch` consecutive samples
@@ -993,7 +1067,11 @@ static int prepare_batch(MptContext* c, const MptFrame* f, int batch) {
                                          "triangles picks from an empty list in the reference (Lights.h:22-220)");
     if ((int64_t)std::max(c->n_slots, 1) * batch > MPT_MAX_WAVEFRONT_PATHS)
         return fail(MPT_ERR_OUT_OF_MEMORY, "wavefront above MPT_MAX_WAVEFRONT_PATHS paths");
-    return ensure_batch(c, batch, c->any_tex || f->bsdf_flags.white_furnace_mode);
+    r = ensure_batch(c, batch, c->any_tex || f->bsdf_flags.white_furnace_mode);
+    if (r != MPT_OK) return r;
+    int iter = 0;
+    const int per = ext_layout(*f, &iter);
+    return ensure_ext(c, batch, per, iter);
 }
 
 // The second stream, its events and traversal spill area (overlapped batches), on first use.
@@ -1063,7 +1141,7 @@ static int launch_batch(MptContext* c, const MptFrame* f, int batch) {
         P.rs_lo = std::max(0, cfg.own_y0 - cfg.halo_prev) * f->res_x;
         P.rs_hi = std::min(f->res_y, cfg.own_y1 + cfg.halo_prev) * f->res_x;
     }
-    const bool ovl = c->overlap && batch >= 2 && f->options.direct_light_sampling != MPT_LSS_RESTIR_DI;
+    const bool ovl = c->overlap && batch >= 2 && f->options.direct_light_sampling != MPT_LSS_RESTIR_DI && c->x_per == 0;
     hipError_t e = hipSuccess;
     if (ovl) {
         int rr = ensure_overlap(c);

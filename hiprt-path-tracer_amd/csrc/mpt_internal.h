@@ -90,7 +90,22 @@ enum : uint32_t {
     NF_NOADD = 1u << 8,      // LSS_NO_DIRECT_LIGHT_SAMPLING: nothing to add at resolve
     NF_L = 1u << 9,          // the light-sampling strategy ran at this vertex
     NF_AQ = 1u << 10,        // ReSTIR DI final shading: the light term waits for occlusion slot 0
+    NF_EXT = 1u << 11,       // extended light sampling: the light term is in the slot's ext entries
 };
+
+// Extended light sampling (number_of_light_samples > 1, RIS with more than one BSDF
+// candidate, RISUseVisiblityTargetFunction; Lights.h:222-241, RIS.h:82-289): every light
+// sample of a vertex gets its own queries and records, x_per entries per slot (entry
+// e = slot * x_per + j), laid out per light sample `it` from j = it * x_iter:
+//   uniform: [0] shadow ray + radiance        bsdf: [0] light-hit ray + BSDF value
+//   MIS:     [0] shadow ray + weighted light radiance, [1] light-hit ray + BSDF value
+//   RIS:     [c] light candidate c: {cw, random, target, triangle} + its visibility ray
+//            (visibility target function), [L + c]: {f, cos} at the final shading
+//            direction + the final shadow ray, [2L + b]: BSDF candidate b: {f, pdf},
+//            {cos, random, refraction} + its light-hit ray
+// Records: 2 float4 per entry (xrec); queries xq_o / xq_d; results xq_hit (closest) and
+// xq_occ (any hit); xq_flag per entry: XQ_ANY / XQ_CL (a query was staged), XQ_REC.
+enum : uint8_t { XQ_ANY = 1, XQ_CL = 2, XQ_REC = 4 };
 
 struct DevPaths {
     int32_t n;                // path slots of the launch = batch samples x n_pix
@@ -161,6 +176,18 @@ struct DevPaths {
     int32_t pix_off;
     int32_t rs_lo, rs_hi;
     int32_t* rs_conv;         // pixel_converged_sample_count by pixel (== as_conv when unpartitioned)
+    // extended light sampling (NF_EXT), sized by the frame's options; NULL / 0 otherwise
+    int32_t x_per;            // entries per slot
+    int32_t x_iter;           // entries per light sample
+    float4* xq_o;
+    float4* xq_d;
+    float4* xq_hit;
+    uint8_t* xq_occ;
+    uint8_t* xq_flag;
+    float4* xrec;             // 2 per entry
+    int32_t* xl_any;          // compacted ext query lists (entries), CTR_XANY / CTR_XCL / CTR_XLIGHT
+    int32_t* xl_cl;
+    int32_t* xl_light;
 };
 
 constexpr int N_TRACE_MODES = 5;
@@ -185,6 +212,7 @@ enum {
     CTR_FULL = 8,             // length of the generic-material hit queue (k_split + k_shade deferrals)
     CTR_DEFER = 9,            // plain-class hits deferred to the generic queue (tombstones in qh)
     CTR_LIGHT = 10,           // length of nq_light (k_trace TM_NEE_LIGHT)
+    CTR_XANY = 11, CTR_XCL = 12, CTR_XLIGHT = 13,   // ext query lists (extended light sampling)
     CTR_COUNT = 16
 };
 

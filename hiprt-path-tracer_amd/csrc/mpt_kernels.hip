@@ -329,6 +329,7 @@ struct TraceArgs {
     int bounce;
     int alpha;                 // render_settings.do_alpha_testing
     int static_grid;           // TM_NEE_LIGHT: one query per lane (the light BVH's stack fits in LDS)
+    int ext;                   // NEE modes: the extended-light-sampling queries (P.xq_*, P.xl_*)
 };
 DEV uint32_t slot_pixel(const MptFrame& F, int slot, int& x, int& y);
 DEV uint32_t pixel_seed(const MptFrame& F, uint32_t pix);
@@ -419,20 +420,24 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MODE == TM_P
                         tr.init(mk3(ro.x, ro.y, ro.z), mk3(rd.x, rd.y, rd.z), (int)__float_as_uint(ro.w), INFINITY,
                                 A.alpha != 0, A.alpha ? alpha_key(pseed, A.bounce, 0, 0) : 0u);
                     } else if (MODE == TM_NEE_ANY || MODE == TM_NEE_CLOSEST || MODE == TM_NEE_LIGHT || MODE == TM_NEE_LIGHT_OCC) {
-                        // compacted list of staged queries (entry = slot * 4 + kind), see k_compact
-                        ray = MODE == TM_NEE_LIGHT_OCC ? P.nq_light[i]
-                                                       : P.nq_tgt[MODE == TM_NEE_ANY ? (size_t)i : (size_t)P.n * 3 + i];
-                        ro = P.nq_o[ray];
-                        rd = P.nq_d[ray];
+                        // compacted list of staged queries (entry = slot * 4 + kind), see k_compact;
+                        // extended light sampling: entries slot * x_per + j (shadow rays alpha kind 1,
+                        // light-hit rays kind 4, as their standard counterparts)
+                        if (A.ext) ray = MODE == TM_NEE_LIGHT_OCC ? P.xl_light[i] : MODE == TM_NEE_ANY ? P.xl_any[i] : P.xl_cl[i];
+                        else ray = MODE == TM_NEE_LIGHT_OCC ? P.nq_light[i]
+                                                            : P.nq_tgt[MODE == TM_NEE_ANY ? (size_t)i : (size_t)P.n * 3 + i];
+                        ro = A.ext ? P.xq_o[ray] : P.nq_o[ray];
+                        rd = A.ext ? P.xq_d[ray] : P.nq_d[ray];
                         qmax = rd.w;
                         const bool al = A.alpha != 0;
                         uint32_t akey = 0u;
-                        if (al) akey = alpha_key(P.seeds[ray >> 2].y, A.bounce, (ray & 3) + 1, 0);
+                        if (al) akey = A.ext ? alpha_key(P.seeds[ray / P.x_per].y, A.bounce, MODE == TM_NEE_ANY ? 1 : 4, 0)
+                                             : alpha_key(P.seeds[ray >> 2].y, A.bounce, (ray & 3) + 1, 0);
                         float tmax = ANY ? rd.w : INFINITY;
                         if (TIE) {
                             // the light candidate of TM_NEE_LIGHT: anything nearer, or as near with a
                             // lower index, is the closest hit instead
-                            const float4 h = P.nhit[ray >> 2];
+                            const float4 h = A.ext ? P.xq_hit[ray] : P.nhit[ray >> 2];
                             tmax = h.x;
                             tr.tie = (int)__float_as_uint(h.w);
                         }
@@ -481,15 +486,19 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MODE == TM_P
             P.hit[ray] = make_float4(tr.best, tr.bu, tr.bv, __uint_as_float((uint32_t)(found ? tr.bprim : -1)));
             P.hit_inside[ray] = was_inside ? 1 : 0;
         } else if (MODE == TM_NEE_ANY) {
-            P.occ[ray] = found ? 1 : 0;
+            (A.ext ? P.xq_occ : P.occ)[ray] = found ? 1 : 0;
         } else if (MODE == TM_NEE_CLOSEST || MODE == TM_NEE_LIGHT) {
             // evaluate_shadow_light_ray: a hit counts only below t_max - 1e-4 (Intersect.h:337-343)
             bool ok = found && tr.best < qmax;
-            P.nhit[ray >> 2] = make_float4(tr.best, tr.bu, tr.bv, __uint_as_float((uint32_t)(ok ? tr.bprim : -1)));
-            if (MODE == TM_NEE_LIGHT && ok) P.nq_light[atomicAdd(&P.counters[CTR_LIGHT], 1)] = ray;
+            (A.ext ? P.xq_hit[ray] : P.nhit[ray >> 2]) =
+                make_float4(tr.best, tr.bu, tr.bv, __uint_as_float((uint32_t)(ok ? tr.bprim : -1)));
+            if (MODE == TM_NEE_LIGHT && ok) {
+                if (A.ext) P.xl_light[atomicAdd(&P.counters[CTR_XLIGHT], 1)] = ray;
+                else P.nq_light[atomicAdd(&P.counters[CTR_LIGHT], 1)] = ray;
+            }
         } else if (MODE == TM_NEE_LIGHT_OCC) {
             // a nearer triangle is not a light: the query contributes nothing, as a miss
-            if (found) P.nhit[ray >> 2].w = __uint_as_float(0xffffffffu);
+            if (found) (A.ext ? P.xq_hit[ray] : P.nhit[ray >> 2]).w = __uint_as_float(0xffffffffu);
         } else if (MODE == TM_RAW_ANY) {
             A.raw_occ[ray] = found ? 1 : 0;
         } else {
@@ -669,6 +678,7 @@ DEV HitAttr hit_attributes(const DevScene& S, int prim, v2 uv) {
     h.sn = n;
     return h;
 }
+#ifndef MPT_TU_PART   // k_tri_attr (main translation unit)
 __global__ void k_tri_attr(DevScene S, float4* out) {
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= S.n_tris) return;
@@ -684,6 +694,7 @@ __global__ void k_tri_attr(DevScene S, float4* out) {
     r[4] = make_float4(g.x, g.y, g.z, __int_as_float(S.mat_idx[p]));
 }
 
+#endif
 // slot -> pixel of the band partition (rows y with (y / bh) % bc == bi, increasing y)
 DEV uint32_t slot_pixel(const MptFrame& F, int slot, int& x, int& y) {
     int r = slot / F.res_x;
@@ -784,6 +795,7 @@ DEV bool adaptive_sampling(const DevPaths& P, const MptRenderSettings& rs, int s
     return true;
 }
 
+#ifndef MPT_TU_PART   // k_camera
 __global__ __launch_bounds__(TB) void k_camera(DevPaths P, const MptFrame* __restrict__ Fp) {
     int slot = blockIdx.x * TB + threadIdx.x;
     int pslot = slot, sub = 0;   // pixel of the partition, sample of the batch
@@ -855,6 +867,7 @@ __global__ __launch_bounds__(TB) void k_camera(DevPaths P, const MptFrame* __res
     P.nrm[slot] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
 }
 
+#endif
 // ----------------------------------------------------------------------------------
 // light sampling helpers (LightUtils.h)
 // ----------------------------------------------------------------------------------
@@ -864,6 +877,7 @@ struct LightInfo { int tri; v3 normal; float area; Col emission; };
 // -- the values uniform_sample_one_emissive_triangle (LightUtils.h:15-58) derives from
 // the triangle's vertices and material, computed with the same operations, so a sample
 // costs one dependent 80-byte load instead of a chain of index / vertex / material loads.
+#ifndef MPT_TU_PART   // k_emissive_table
 __global__ void k_emissive_table(DevScene S, float4* tab) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= S.n_emissive) return;
@@ -883,6 +897,7 @@ __global__ void k_emissive_table(DevScene S, float4* tab) {
     tab[5 * i + 4] = make_float4(e.r, e.g, e.b, 0.0f);
 }
 
+#endif
 DEV v3 sample_emissive_triangle(const DevScene& S, Rng& rng, float& pdf, LightInfo& li) {
     int ri = rng.random_index(S.n_emissive);
     const float4* e = S.em_tab + 5 * (size_t)ri;
@@ -985,6 +1000,180 @@ DEV void stage_query(const DevPaths& P, int slot, int kind, uint32_t& qm, v3 o, 
     qm |= 1u << kind;
 }
 
+// ----------------------------------------------------------------------------------
+// Extended light sampling (number_of_light_samples > 1, RIS with several BSDF candidates,
+// RISUseVisiblityTargetFunction): sample_many_lights' loop (Lights.h:222-241) with every
+// RNG draw of every light sample here, in the reference's order, and one record + query per
+// candidate in the slot's ext entries (layout: mpt_internal.h).  k_resolve<true> replays
+// the reservoirs / MIS sums with the trace results.  Only the EXT instantiation of k_shade
+// carries this code.
+// ----------------------------------------------------------------------------------
+DEV void x_query(const DevPaths& P, size_t e, bool any, v3 o, int last_hit, v3 d, float tmax, uint8_t& flag) {
+    P.xq_o[e] = make_float4(o.x, o.y, o.z, __uint_as_float((uint32_t)last_hit));
+    P.xq_d[e] = make_float4(d.x, d.y, d.z, tmax);
+    if (any) P.xl_any[atomicAdd(&P.counters[CTR_XANY], 1)] = (int32_t)e;
+    else P.xl_cl[atomicAdd(&P.counters[CTR_XCL], 1)] = (int32_t)e;
+    flag |= any ? XQ_ANY : XQ_CL;
+}
+DEV void x_rec(const DevPaths& P, size_t e, float4 a, float4 b) {
+    P.xrec[2 * e] = a;
+    P.xrec[2 * e + 1] = b;
+}
+// a BSDF-sampled light-hit candidate: sample (draws), evaluate, stage the light-hit ray;
+// origin as sample_one_light_bsdf / _MIS / the RIS BSDF candidates pick it
+template <int OVR, bool FULL>
+DEV float x_bsdf_cand(const DevPaths& P, const BCtx& bc, const Mat& m, const VState& vs, const PEval& pe, size_t e, int prim,
+                      v3 ip, v3 sn, v3 gn, v3 view, float ism, v3 o_refl, bool abs_cos, float r_add_slot, Rng& rng, uint8_t& fl) {
+    VState tv = vs;
+    v3 L = mk3(0.0f, 0.0f, 0.0f);
+    float pdf = 0.0f;
+    Col f = col(0.0f);
+    if (bsdf_sample_dir<OVR, FULL>(bc, m, tv, view, sn, gn, L, rng)) f = bsdf_eval_post<OVR, FULL>(bc, m, tv, pe, sn, L, pdf);
+    const bool refr = dot(L, sn * ism) < 0;
+    if (pdf > 0.0f) {
+        const v3 o = refr ? ip + sn * 1.0e-4f * ism * -1.0f : o_refl;
+        const float c = abs_cos ? absr(dot(sn, L)) : maxr(0.0f, dot(sn, L));
+        x_rec(P, e, make_float4(f.r, f.g, f.b, pdf), make_float4(c, r_add_slot, refr ? 1.0f : 0.0f, 0.0f));
+        fl |= XQ_REC;
+        x_query(P, e, false, o, prim, L, 1.0e35f - 1.0e-4f, fl);
+    }
+    return pdf;
+}
+template <int OVR, bool FULL>
+DEV void ext_light(const DevScene& S, const DevPaths& P, const MptFrame& F, const BCtx& bc, const Mat& m, const VState& vs,
+                   const PEval& pe, int slot, int prim, v3 ip, v3 sn, v3 gn, v3 view, float ism, v3 ep, int lssb, Rng& rng) {
+    const MptRenderSettings& rs = F.render_settings;
+    const int nl = rs.ris_number_of_light_candidates, nbc = rs.ris_number_of_bsdf_candidates;
+    const bool vis = F.options.ris_use_visibility != 0;
+    const size_t base = (size_t)slot * P.x_per;
+    for (int it = 0; it < rs.number_of_light_samples; it++) {
+        const size_t e0 = base + (size_t)it * P.x_iter;
+        for (int j = 0; j < P.x_iter; j++) P.xq_flag[e0 + j] = 0;
+        if (lssb == MPT_LSS_UNIFORM_ONE_LIGHT || lssb == MPT_LSS_MIS_LIGHT_BSDF) {
+            // sample_one_light_no_MIS (Lights.h:22-65) / sample_one_light_MIS (Lights.h:115-220)
+            const bool mis = lssb == MPT_LSS_MIS_LIGHT_BSDF;
+            float lpdf;
+            LightInfo li;
+            const v3 lp = sample_emissive_triangle(S, rng, lpdf, li);
+            if (!(lpdf > 0.0f)) continue;   // both return before any further draw
+            uint8_t f0 = 0, f1 = 0;
+            const v3 so = mis ? ep : ip + sn * 1.0e-4f;
+            const v3 sd = lp - so;
+            const float dist = length(sd);
+            const v3 L = sd / dist;
+            const float geo = absr(dot(li.normal, -L));
+            if (geo > 0.0f) {
+                VState tv = vs;
+                float pdf;
+                const Col f = bsdf_eval_post<OVR, FULL>(bc, m, tv, pe, sn, L, pdf);
+                if (pdf != 0.0f) {
+                    float lp2 = lpdf;
+                    lp2 *= dist * dist;
+                    lp2 /= geo;
+                    const float cosv = maxr(dot(sn, L), 0.0f);
+                    const Col rad = mis ? f * cosv * li.emission * balance(lp2, pdf) / lp2 : li.emission * cosv * f / lp2;
+                    x_rec(P, e0, make_float4(rad.r, rad.g, rad.b, 0.0f), make_float4(0.0f, 0.0f, 0.0f, 0.0f));
+                    f0 |= XQ_REC;
+                    x_query(P, e0, true, so, prim, L, dist - 1.0e-4f, f0);
+                }
+            }
+            if (mis) x_bsdf_cand<OVR, FULL>(P, bc, m, vs, pe, e0 + 1, prim, ip, sn, gn, view, ism, ep, true, 0.0f, rng, f1);
+            P.xq_flag[e0] = f0;
+            if (mis) P.xq_flag[e0 + 1] = f1;
+        } else if (lssb == MPT_LSS_BSDF) {
+            // sample_one_light_bsdf (Lights.h:67-113)
+            uint8_t f0 = 0;
+            x_bsdf_cand<OVR, FULL>(P, bc, m, vs, pe, e0, prim, ip, sn, gn, view, ism, ip + sn * 1.0e-4f, false, 0.0f, rng, f0);
+            P.xq_flag[e0] = f0;
+        } else {
+            // sample_bsdf_and_lights_RIS_reservoir (RIS.h:82-289): the light candidates' draws and
+            // weights (without visibility: final), the BSDF candidates' draws; the reservoir
+            // itself is replayed by k_resolve with the trace results
+            const v3 ep2 = ip + sn * 1.0e-4f;   // evaluate_reservoir_sample's shadow-ray origin (RIS.h:31)
+            float wsum = 0.0f;                  // without the visibility target function: the light
+            int win = -1;                       // winner is final here, only its shadow ray is traced
+            v3 win_L = mk3(0.0f, 0.0f, 0.0f);
+            float win_d = 0.0f;
+            for (int c = 0; c < nl; c++) {
+                float lpdf;
+                LightInfo li;
+                const v3 lp = sample_emissive_triangle(S, rng, lpdf, li);
+                float target = 0.0f, w = 0.0f, bp = 0.0f;
+                bool inner = false;
+                Col fc = col(0.0f);
+                v3 tl = mk3(0.0f, 0.0f, 0.0f);
+                float dist = 0.0f;
+                if (lpdf > 0.0f) {
+                    tl = lp - ep;
+                    dist = length(tl);
+                    tl = tl / dist;
+                    const float cl = absr(dot(li.normal, -tl));
+                    const float geo = maxr(0.0f, dot(sn * ism, tl));
+                    if (geo > 0.0f && cl > 1.0e-6f) {
+                        inner = true;
+                        lpdf *= dist * dist;
+                        lpdf /= cl;
+                        if (min_contrib(rs.minimum_light_contribution, li.emission / lpdf)) {
+                            VState tv = vs;
+                            fc = bsdf_eval_post<OVR, FULL>(bc, m, tv, pe, sn, tl, bp);
+                            const Col lc = fc * li.emission * geo;
+                            target = min_contrib(rs.minimum_light_contribution, lc / bp / lpdf) ? lum(lc) : 0.0f;
+                        }
+                        w = balance(lpdf, (float)nl, bp, (float)nbc);
+                    }
+                }
+                const float r = rng();   // RISReservoir::add_one_candidate (RIS_Reservoir.h:29-38)
+                const size_t e = e0 + c, ew = e0 + nl + c;
+                uint8_t f0 = XQ_REC, fw = 0;
+                x_rec(P, e, make_float4(w, lpdf, target, __int_as_float(li.tri)), make_float4(r, inner ? 1.0f : 0.0f, 0.0f, 0.0f));
+                if (inner && vis && target > 0.0f) x_query(P, e, true, ep, prim, tl, dist - 1.0e-4f, f0);
+                v3 Lw = mk3(0.0f, 0.0f, 0.0f);
+                float dw = 0.0f;
+                if (inner && target > 0.0f) {
+                    // this candidate's final shading as the winner (RIS.h:18-80): direction from ep2,
+                    // a fresh evaluation unless that is the candidate's own origin (outside)
+                    const v3 sd = lp - ep2;
+                    dw = length(sd);
+                    Lw = sd / dw;
+                    Col fw_ = fc;
+                    if (ism != 1.0f) {
+                        VState tv = vs;
+                        float bpw;
+                        fw_ = bsdf_eval_post<OVR, FULL>(bc, m, tv, pe, sn, Lw, bpw);
+                    }
+                    x_rec(P, ew, make_float4(fw_.r, fw_.g, fw_.b, maxr(0.0f, dot(sn, Lw))), make_float4(0.0f, 0.0f, 0.0f, 0.0f));
+                    fw |= XQ_REC;
+                    // with the visibility target function any candidate may win: its final shadow
+                    // ray is its visibility ray outside, a ray of its own inside
+                    if (vis && ism != 1.0f) x_query(P, ew, true, ep2, prim, Lw, dw - 1.0e-4f, fw);
+                }
+                if (!vis) {
+                    const float cw = inner ? w * target / lpdf : 0.0f;
+                    wsum += cw;
+                    if (r < cw / wsum) { win = c; win_L = Lw; win_d = dw; }
+                }
+                P.xq_flag[e] = f0;
+                P.xq_flag[ew] = fw;
+            }
+            if (!vis && win >= 0) {
+                uint8_t fw = XQ_REC;
+                x_query(P, e0 + nl + win, true, ep2, prim, win_L, win_d - 1.0e-4f, fw);
+                P.xq_flag[e0 + nl + win] = fw;
+            }
+            for (int b = 0; b < nbc; b++) {
+                uint8_t fb = 0;
+                // the candidate's random is drawn after its BSDF sample (add_one_candidate)
+                const size_t e = e0 + 2 * nl + b;
+                const float pdf = x_bsdf_cand<OVR, FULL>(P, bc, m, vs, pe, e, prim, ip, sn, gn, view, ism, ep, true, 0.0f, rng, fb);
+                const float r = rng();
+                if (pdf > 0.0f) P.xrec[2 * e + 1].y = r;
+                else x_rec(P, e, make_float4(0.0f, 0.0f, 0.0f, 0.0f), make_float4(0.0f, r, 0.0f, 0.0f));
+                P.xq_flag[e] = fb | XQ_REC;
+            }
+        }
+    }
+}
+
 DEV void store3(float* p, Col c) { p[0] = c.r; p[1] = c.g; p[2] = c.b; }
 DEV void store3(float* p, v3 c) { p[0] = c.x; p[1] = c.y; p[2] = c.z; }
 DEV Col load3c(const float* p) { return col(p[0], p[1], p[2]); }
@@ -997,7 +1186,7 @@ DEV v3 load3v(const float* p) { return mk3(p[0], p[1], p[2]); }
 // section (0 hit processing, 1 op pre, 2 BSDF eval, 3 op post, 4 finish), summed over
 // lanes into g_sect; read with mpt_debug_sections.
 #ifdef MPT_SECTION_TIMING
-__device__ unsigned long long g_sect[8];
+static __device__ unsigned long long g_sect[8];
 #define SECT_BEGIN() uint64_t sect_[6] = {0, 0, 0, 0, 0, 0}; uint64_t tprev_ = __builtin_amdgcn_s_memtime()
 #define SECT(k) do { uint64_t now_ = __builtin_amdgcn_s_memtime(); sect_[k] += now_ - tprev_; tprev_ = now_; } while (0)
 #define SECT_END() do { if (sect_[1]) for (int k_ = 0; k_ < 6; k_++) atomicAdd(&g_sect[k_], (unsigned long long)sect_[k_]); atomicAdd(&g_sect[7], 1ull); } while (0)
@@ -1078,7 +1267,7 @@ struct ShadeArgs {
 #ifndef MPT_SHADE_WAVES_PLAIN
 #define MPT_SHADE_WAVES_PLAIN MPT_SHADE_WAVES
 #endif
-template <int OVR, bool PLAIN>
+template <int OVR, bool PLAIN, bool EXT = false>
 __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_SHADE_WAVES_PLAIN : MPT_SHADE_WAVES))) void k_shade(ShadeArgs A) {
     const DevScene& S = A.S;
     const DevPaths& P = A.P;
@@ -1220,6 +1409,12 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_
             SECT(0);
             bsdf_eval_pre<OVR, !PLAIN>(bc, m, vs, view, sn, pe);
             SECT(5);
+            if (EXT && do_light && !(restir && bounce == 0)) {
+                // extended light sampling: every light sample's draws, records and queries
+                ext_light<OVR, !PLAIN>(S, P, F, bc, m, vs, pe, slot, prim, ip, sn, gn, view, ism, ep, lssb, rng);
+                fl |= NF_EXT;
+                op = do_env ? OP_ENV_LIGHT : (do_cont ? OP_CONT : OP_DONE);
+            }
             Col fW = col(0.0f);                // BSDF value / pdf at the RIS light winner
             float pdfW = 0.0f;
             // One BSDF evaluation site for every operation of the vertex: each iteration
@@ -1501,6 +1696,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_
 // camera ray of bounce 0 is re-normalised as FullPathTracer's re-read of the G-buffer does
 // (FullPathTracer.h:131-150, see k_shade).
 // ----------------------------------------------------------------------------------
+#ifndef MPT_TU_PART   // k_miss
 __global__ __launch_bounds__(TB) void k_miss(DevScene S, DevPaths P, const MptFrame* __restrict__ Fp, int bounce) {
     const int i = blockIdx.x * TB + threadIdx.x;
     if (i >= P.counters[CTR_MISS]) return;
@@ -1512,6 +1708,7 @@ __global__ __launch_bounds__(TB) void k_miss(DevScene S, DevPaths P, const MptFr
     P.col[slot] = make_float4(rc.r, rc.g, rc.b, 0.0f);
 }
 
+#endif
 // ----------------------------------------------------------------------------------
 // Queue compaction (k_split, k_compact): thread t of a block takes the CP_ITEMS
 // consecutive entries [b0 + t * CP_ITEMS, +CP_ITEMS) of the input queue, so the output
@@ -1572,6 +1769,7 @@ DEV int load_items(const int32_t* q, int b0, int count, int slots[CP_ITEMS]) {
 // has a vertex to shade instead of idling through the light-sampling loop beside a miss.
 // With `classes`, the hits are further sorted by material class (see k_shade): plain
 // dielectrics into qh (CTR_HIT), every other material into qf (CTR_FULL).
+#ifndef MPT_TU_PART   // k_split
 __global__ __launch_bounds__(CP_NT) void k_split(DevScene S, DevPaths P, const int32_t* q, const int32_t* count_q,
                                                  int classes) {
     __shared__ int tmp[CP_NT / 64 + 1];
@@ -1613,12 +1811,14 @@ __global__ __launch_bounds__(CP_NT) void k_split(DevScene S, DevPaths P, const i
     }
 }
 
+#endif
 // The bounce's shaded vertices: qh[0, CTR_HIT) followed by qf[0, CTR_FULL); entries that
 // k_shade<PLAIN> deferred to qf are -1 in qh.
 DEV int shaded_count(const DevPaths& P) { return P.counters[CTR_HIT] + P.counters[CTR_FULL]; }
 DEV int shaded_entry(const DevPaths& P, int nh, int i) { return i < nh ? P.qh[i] : P.qf[i - nh]; }
 
 // k_compact: next path queue + NEE query lists from the per-path masks of the shaded paths
+#ifndef MPT_TU_PART   // k_compact
 __global__ __launch_bounds__(CP_NT) void k_compact(DevPaths P, int32_t* q_next, int32_t* count_next) {
     __shared__ int tmp[CP_NT / 64 + 1];
     __shared__ int base[5];
@@ -1676,6 +1876,7 @@ __global__ __launch_bounds__(CP_NT) void k_compact(DevPaths P, int32_t* q_next, 
     }
 }
 
+#endif
 // ----------------------------------------------------------------------------------
 // k_resolve: finish the vertex's direct lighting with the NEE trace results
 // ----------------------------------------------------------------------------------
@@ -1711,7 +1912,101 @@ DEV float pdf_emissive_hit(const DevScene& S, const ShadowLightHit& h, v3 d) {
 
 #include "restir_di.h"
 
+// Extended light sampling (ext_light): each light sample's contribution from its records and
+// trace results, summed in sample order and divided by their count (sample_many_lights,
+// Lights.h:222-241).
+DEV Col ext_resolve(const DevScene& S, const DevPaths& P, const MptFrame& F, int slot, int lssb) {
+    const MptRenderSettings& rs = F.render_settings;
+    const int nl = rs.ris_number_of_light_candidates, nbc = rs.ris_number_of_bsdf_candidates;
+    const bool vis = F.options.ris_use_visibility != 0;
+    const size_t base = (size_t)slot * P.x_per;
+    Col dl = col(0.0f);
+    for (int it = 0; it < rs.number_of_light_samples; it++) {
+        const size_t e0 = base + (size_t)it * P.x_iter;
+        Col ld = col(0.0f);
+        if (lssb == MPT_LSS_UNIFORM_ONE_LIGHT || lssb == MPT_LSS_MIS_LIGHT_BSDF) {
+            Col lrad = col(0.0f), brad = col(0.0f);
+            if ((P.xq_flag[e0] & XQ_ANY) && !P.xq_occ[e0]) { const float4 a = P.xrec[2 * e0]; lrad = col(a.x, a.y, a.z); }
+            if (lssb == MPT_LSS_MIS_LIGHT_BSDF && (P.xq_flag[e0 + 1] & XQ_CL)) {
+                const size_t e = e0 + 1;
+                ShadowLightHit sh;
+                if (shadow_light_hit(S, P.xq_hit[e], sh) && !is_black(sh.em)) {
+                    const float4 a = P.xrec[2 * e], b = P.xrec[2 * e + 1], d = P.xq_d[e];
+                    const float lp2 = pdf_emissive_hit(S, sh, mk3(d.x, d.y, d.z));
+                    brad = col(a.x, a.y, a.z) * b.x * sh.em * balance(a.w, lp2) / a.w;
+                }
+            }
+            ld = lrad + brad;
+        } else if (lssb == MPT_LSS_BSDF) {
+            if (P.xq_flag[e0] & XQ_CL) {
+                ShadowLightHit sh;
+                if (shadow_light_hit(S, P.xq_hit[e0], sh) && !is_black(sh.em)) {
+                    const float4 a = P.xrec[2 * e0], b = P.xrec[2 * e0 + 1];
+                    ld = col(a.x, a.y, a.z) * b.x * sh.em / a.w;
+                }
+            }
+        } else {
+            // the RIS reservoir (RIS.h:82-289, RISReservoir RIS_Reservoir.h:20-51): light
+            // candidates (their visibility with the visibility target function), then the BSDF
+            // candidates with their light-hit results, in the reference's order
+            float wsum = 0.0f, tw = 0.0f;
+            int win = -1;        // light candidate, or nl + BSDF candidate
+            int win_tri = -1;
+            for (int c = 0; c < nl; c++) {
+                const float4 a = P.xrec[2 * (e0 + c)], b = P.xrec[2 * (e0 + c) + 1];
+                float target = a.z, cw = 0.0f;
+                if (b.y != 0.0f) {   // inner
+                    if (vis && target > 0.0f) target *= P.xq_occ[e0 + c] ? 0.0f : 1.0f;
+                    cw = a.x * target / a.y;
+                }
+                wsum += cw;
+                if (b.x < cw / wsum) { win = c; tw = target; win_tri = __float_as_int(a.w); }
+            }
+            for (int k = 0; k < nbc; k++) {
+                const size_t e = e0 + 2 * nl + k;
+                const float4 b = P.xrec[2 * e + 1];
+                float cw = 0.0f, target = 0.0f;
+                int tri = -1;
+                if (P.xq_flag[e] & XQ_CL) {
+                    ShadowLightHit sh;
+                    if (shadow_light_hit(S, P.xq_hit[e], sh) && !is_black(sh.em)) {
+                        const float4 a = P.xrec[2 * e], d = P.xq_d[e];
+                        const Col lc = col(a.x, a.y, a.z) * sh.em * b.x;
+                        target = lum(lc);
+                        float lpdf = pdf_emissive_hit(S, sh, mk3(d.x, d.y, d.z));
+                        lpdf *= b.z != 0.0f ? 0.0f : 1.0f;
+                        if (!min_contrib(rs.minimum_light_contribution, lc / lpdf / a.w)) target = 0.0f;
+                        cw = balance(a.w, (float)nbc, lpdf, (float)nl) * target / a.w;
+                        tri = sh.prim;
+                    }
+                }
+                wsum += cw;
+                if (b.y < cw / wsum) { win = nl + k; tw = target; win_tri = tri; }
+            }
+            // RISReservoir::end + evaluate_reservoir_sample (RIS.h:18-80)
+            const float ucw = wsum == 0.0f ? 0.0f : 1.0f / tw * wsum;
+            if (ucw > 0.0f && win >= 0) {
+                if (win >= nl) {
+                    const size_t e = e0 + 2 * nl + (win - nl);
+                    const float4 a = P.xrec[2 * e], b = P.xrec[2 * e + 1];
+                    if (b.x > 0.0f) ld = col(a.x, a.y, a.z) * ucw * emission_of(S.mats[S.mat_idx[win_tri]]) * b.x;
+                } else {
+                    const size_t ew = e0 + nl + win;
+                    // the final shadow ray: its own (inside / without the visibility target
+                    // function), else the candidate's visibility ray
+                    const bool occ = (P.xq_flag[ew] & XQ_ANY) ? P.xq_occ[ew] != 0 : P.xq_occ[e0 + win] != 0;
+                    const float4 a = P.xrec[2 * ew];
+                    if (!occ && a.w > 0.0f) ld = col(a.x, a.y, a.z) * ucw * emission_of(S.mats[S.mat_idx[win_tri]]) * a.w;
+                }
+            }
+        }
+        dl += ld;
+    }
+    return dl / (float)rs.number_of_light_samples;
+}
+
 // over the bounce's hit queue (the shaded paths); count_paths: the bounce's path rays
+template <bool EXT>
 __global__ __launch_bounds__(TB) void k_resolve(DevScene S, DevPaths P, const MptFrame* __restrict__ Fp, int bounce,
                                                 const int32_t* count_paths) {
     const MptFrame& F = *Fp;
@@ -1722,8 +2017,8 @@ __global__ __launch_bounds__(TB) void k_resolve(DevScene S, DevPaths P, const Mp
         // (atomic: the two halves of an overlapped batch resolve concurrently)
         unsigned long long* rc = (unsigned long long*)P.ray_counts;
         atomicAdd(rc + 0, (unsigned long long)*count_paths);
-        atomicAdd(rc + 1, (unsigned long long)P.counters[CTR_ANY]);
-        atomicAdd(rc + 2, (unsigned long long)P.counters[CTR_CL]);
+        atomicAdd(rc + 1, (unsigned long long)P.counters[CTR_ANY] + (EXT ? (unsigned long long)P.counters[CTR_XANY] : 0ull));
+        atomicAdd(rc + 2, (unsigned long long)P.counters[CTR_CL] + (EXT ? (unsigned long long)P.counters[CTR_XCL] : 0ull));
         atomicAdd(rc + 3, (unsigned long long)(shaded_count(P) - P.counters[CTR_DEFER]));
         atomicAdd(rc + 4, (unsigned long long)P.counters[CTR_FULL]);
     }
@@ -1746,6 +2041,7 @@ __global__ __launch_bounds__(TB) void k_resolve(DevScene S, DevPaths P, const Mp
     const uint8_t* occ = P.occ + (size_t)slot * 4;
     if (fl & NF_IMM) ld = load3c(nr.imm);
     else if (!(fl & NF_L)) ld = col(0.0f);
+    else if (EXT && (fl & NF_EXT)) ld = ext_resolve(S, P, F, slot, lssb);   // already / number_of_light_samples
     else if (lss == MPT_LSS_RESTIR_DI && bounce == 0) {
         if ((fl & NF_A) && !((fl & NF_AQ) && occ[0])) ld = load3c(nr.a);
     } else if (lssb == MPT_LSS_RIS_BSDF_AND_LIGHT) {
@@ -1805,8 +2101,10 @@ __global__ __launch_bounds__(TB) void k_resolve(DevScene S, DevPaths P, const Mp
                 ld = load3c(nr.b) * nr.b_cos * sh.em / nr.b_pdf;
         }
     }
-    // sample_many_lights: / number_of_light_samples (= 1, validated on the host)
-    if ((fl & NF_L) && !(fl & NF_IMM)) ld = ld / (float)rs.number_of_light_samples;
+    // sample_many_lights: / number_of_light_samples (1 outside extended light sampling); not the
+    // ReSTIR DI reservoir of bounce 0 (sample_one_light_ReSTIR_DI, Lights.h:243-275)
+    if ((fl & NF_L) && !(fl & NF_IMM) && !(EXT && (fl & NF_EXT)) && !(lss == MPT_LSS_RESTIR_DI && bounce == 0))
+        ld = ld / (float)rs.number_of_light_samples;
     {
         Col e2 = col(0.0f), e1 = col(0.0f);
         if ((fl & NF_E2) && !occ[2]) e2 = load3c(nr.e2);
@@ -1872,16 +2170,37 @@ DEV void accumulate_sample(const DevPaths& P, const MptRenderSettings& rs, int p
 }
 // one pixel per lane; the samples of a batch are added in sample order, exactly as
 // consecutive single-sample frames would add them
+#ifndef MPT_TU_PART   // k_accumulate
 __global__ __launch_bounds__(TB) void k_accumulate(DevPaths P, const MptFrame* __restrict__ Fp) {
     const int pixel = blockIdx.x * TB + threadIdx.x;
     if (pixel >= P.n_pix) return;
     for (int sub = 0; sub < P.batch; sub++) accumulate_sample(P, Fp[sub].render_settings, pixel, batch_slot(P, pixel, sub));
 }
 
+#endif
+// k_shade and the ReSTIR DI reuse kernels are instantiated in their own translation units
+// (mpt_part.hip, compiled once per MPT_TU_PART value) so that the build compiles them in
+// parallel; these launch them.
+void part_shade_generic(dim3 g, hipStream_t st, const ShadeArgs& a);          // k_shade<NONE, false>
+void part_shade_plain(dim3 g, hipStream_t st, const ShadeArgs& a);            // k_shade<NONE, true>
+void part_shade_ext(dim3 g, hipStream_t st, const ShadeArgs& a);              // k_shade<NONE, false, true>
+void part_shade_override(int ovr, bool ext, dim3 g, hipStream_t st, const ShadeArgs& a);   // Lambert, Oren-Nayar
+enum RestirKernel { RK_INITIAL, RK_SPATIOTEMPORAL, RK_SPATIOTEMPORAL_ANY, RK_SPATIAL, RK_SPATIAL_ANY, RK_TEMPORAL };
+void part_restir_principled(int kind, dim3 g, hipStream_t st, const DevScene& S, const DevPaths& P, const MptFrame* F,
+                            int pass, const float4* in, float4* out);
+void part_restir_override(int ovr, int kind, dim3 g, hipStream_t st, const DevScene& S, const DevPaths& P,
+                          const MptFrame* F, int pass, const float4* in, float4* out);
+#ifndef MPT_TU_PART   // host launch glue and the remaining kernels: main translation unit only
 // ----------------------------------------------------------------------------------
 // host launch glue
 // ----------------------------------------------------------------------------------
 static int blocks_for(int n) { return (n + TB - 1) / TB; }
+
+static void launch_restir_kernel(int ovr, int kind, dim3 g, hipStream_t st, const DevScene& S, const DevPaths& P,
+                                 const MptFrame* F, int pass = 0, const float4* in = nullptr, float4* out = nullptr) {
+    if (ovr == MPT_BSDF_NONE) part_restir_principled(kind, g, st, S, P, F, pass, in, out);
+    else part_restir_override(ovr, kind, g, st, S, P, F, pass, in, out);
+}
 
 template <int MODE>
 static void launch_trace_mode(const TraceArgs& a, int grid, bool stats, hipStream_t st) {
@@ -1923,19 +2242,6 @@ static void timed_trace(const TraceArgs& a, LaunchCfg& cfg, hipStream_t st) {
     if (timed) { hipEventRecord(cfg.ev_pool[cfg.ev_used + 1], st); cfg.ev_used += 2; }
     cfg.launches++;
 }
-
-template <template <int> class K, typename... Args>
-static void launch_ovr(int ovr, dim3 g, hipStream_t st, Args... args) {
-    if (ovr == MPT_BSDF_LAMBERTIAN) hipLaunchKernelGGL(K<MPT_BSDF_LAMBERTIAN>::fn, g, dim3(TB), 0, st, args...);
-    else if (ovr == MPT_BSDF_OREN_NAYAR) hipLaunchKernelGGL(K<MPT_BSDF_OREN_NAYAR>::fn, g, dim3(TB), 0, st, args...);
-    else hipLaunchKernelGGL(K<MPT_BSDF_NONE>::fn, g, dim3(TB), 0, st, args...);
-}
-template <int OVR> struct KInitial { static constexpr auto fn = k_restir_initial<OVR>; };
-template <int OVR> struct KSpatiotemporal { static constexpr auto fn = k_restir_spatiotemporal<OVR, MPT_RESTIR_DI_BIAS_PAIRWISE_MIS_DEFENSIVE>; };
-template <int OVR> struct KSpatial { static constexpr auto fn = k_restir_spatial<OVR, MPT_RESTIR_DI_BIAS_PAIRWISE_MIS_DEFENSIVE>; };
-template <int OVR> struct KSpatiotemporalAny { static constexpr auto fn = k_restir_spatiotemporal<OVR, -1>; };
-template <int OVR> struct KSpatialAny { static constexpr auto fn = k_restir_spatial<OVR, -1>; };
-template <int OVR> struct KTemporal { static constexpr auto fn = k_restir_temporal<OVR>; };
 
 // restir_output_reservoirs of a frame, as a code kept by the context between frames
 static float4* restir_buffer(const DevPaths& P, int code) { return code == 1 ? P.rs_sp2 : code == 2 ? P.rs_init : P.rs_sp1; }
@@ -2005,7 +2311,7 @@ static void launch_restir(const DevScene& S, DevPaths& P, const MptFrame* d_fram
     const dim3 g(cfg.grid_persistent);
     {
         TimedScope tk(cfg, st, KT_RS_INITIAL);
-        launch_ovr<KInitial>(ovr, g, st, S, P, d_frame);
+        launch_restir_kernel(ovr, RK_INITIAL, g, st, S, P, d_frame);
     }
     float4* last_out = restir_buffer(P, cfg.restir_out_sp2);
     // the reference-default weights run a kernel variant with the mode compiled in
@@ -2017,16 +2323,14 @@ static void launch_restir(const DevScene& S, DevPaths& P, const MptFrame* d_fram
         halo_exchange(hf, cfg, st, MPT_HALO_RESERVOIRS, 0, cfg.halo_rows, {{P.rs_tin, RB}});
         {
             TimedScope tk(cfg, st, KT_RS_REUSE);
-            if (def_bias) launch_ovr<KSpatiotemporal>(ovr, g, st, S, P, d_frame);
-            else launch_ovr<KSpatiotemporalAny>(ovr, g, st, S, P, d_frame);
+            launch_restir_kernel(ovr, def_bias ? RK_SPATIOTEMPORAL : RK_SPATIOTEMPORAL_ANY, g, st, S, P, d_frame);
         }
         for (int pass = 1; pass < rd.number_of_passes; pass++) {
             float4* in = P.rs_out;
             float4* out = in == P.rs_sp1 ? P.rs_sp2 : P.rs_sp1;
             halo_exchange(hf, cfg, st, MPT_HALO_RESERVOIRS, pass, cfg.halo_rows, {{in, RB}});
             TimedScope tk(cfg, st, KT_RS_SPATIAL);
-            if (def_bias) launch_ovr<KSpatial>(ovr, g, st, S, P, d_frame, pass, (const float4*)in, out);
-            else launch_ovr<KSpatialAny>(ovr, g, st, S, P, d_frame, pass, (const float4*)in, out);
+            launch_restir_kernel(ovr, def_bias ? RK_SPATIAL : RK_SPATIAL_ANY, g, st, S, P, d_frame, pass, in, out);
             P.rs_out = out;
         }
     } else {
@@ -2040,7 +2344,7 @@ static void launch_restir(const DevScene& S, DevPaths& P, const MptFrame* d_fram
             float4* tout = rd.do_spatial_reuse_pass ? P.rs_init : (last_out == P.rs_sp1 ? P.rs_sp2 : P.rs_sp1);
             halo_exchange(hf, cfg, st, MPT_HALO_RESERVOIRS, 0, cfg.halo_rows, {{P.rs_tin, RB}});
             TimedScope tk(cfg, st, KT_RS_REUSE);
-            launch_ovr<KTemporal>(ovr, g, st, S, P, d_frame, (const float4*)P.rs_tin, tout);
+            launch_restir_kernel(ovr, RK_TEMPORAL, g, st, S, P, d_frame, 0, P.rs_tin, tout);
             cur = tout;
         }
         if (rd.do_spatial_reuse_pass) {
@@ -2049,8 +2353,7 @@ static void launch_restir(const DevScene& S, DevPaths& P, const MptFrame* d_fram
                 float4* out = pass == 0 ? P.rs_sp1 : ((pass & 1) ? P.rs_sp2 : P.rs_sp1);
                 halo_exchange(hf, cfg, st, MPT_HALO_RESERVOIRS, pass + 1, cfg.halo_rows, {{in, RB}});
                 TimedScope tk(cfg, st, KT_RS_SPATIAL);
-                if (def_bias) launch_ovr<KSpatial>(ovr, g, st, S, P, d_frame, pass, (const float4*)in, out);
-                else launch_ovr<KSpatialAny>(ovr, g, st, S, P, d_frame, pass, (const float4*)in, out);
+                launch_restir_kernel(ovr, def_bias ? RK_SPATIAL : RK_SPATIAL_ANY, g, st, S, P, d_frame, pass, in, out);
                 cur = out;
             }
         }
@@ -2082,7 +2385,9 @@ hipError_t launch_frame(const DevScene& S, const DevPaths& P0, const MptFrame* d
     int c_cur = CTR_Q0, c_next = CTR_Q1;
     const int nb = hf.render_settings.nb_bounces;
     // material classes (k_split / k_shade): Principled BSDF only (the Lambert override has one class)
-    const int classes = hf.options.bsdf_override != MPT_BSDF_NONE ? 0 : (cfg.shade_classes != 0 ? 1 : 0);
+    // extended light sampling (DevPaths::x_per > 0): the EXT shading / resolve kernels, one class
+    const bool ext = P.x_per > 0;
+    const int classes = (hf.options.bsdf_override != MPT_BSDF_NONE || ext) ? 0 : (cfg.shade_classes != 0 ? 1 : 0);
     for (int b = 0; b <= nb; b++) {
         // continuation / camera rays
         hipMemsetAsync(&P.counters[CTR_FETCH], 0, sizeof(int32_t), st);
@@ -2102,6 +2407,7 @@ hipError_t launch_frame(const DevScene& S, const DevPaths& P0, const MptFrame* d
         hipMemsetAsync(&P.counters[c_next], 0, sizeof(int32_t), st);
         hipMemsetAsync(&P.counters[CTR_ANY], 0, 2 * sizeof(int32_t), st);
         hipMemsetAsync(&P.counters[CTR_HIT], 0, 4 * sizeof(int32_t), st);   // HIT, MISS, FULL, DEFER
+        if (ext) hipMemsetAsync(&P.counters[CTR_XANY], 0, 3 * sizeof(int32_t), st);   // XANY, XCL, XLIGHT
         const dim3 cp_grid((n + CP_NT * CP_ITEMS - 1) / (CP_NT * CP_ITEMS));
         {
             TimedScope ts(cfg, st, KT_SPLIT);
@@ -2113,21 +2419,17 @@ hipError_t launch_frame(const DevScene& S, const DevPaths& P0, const MptFrame* d
         sa.force_defer = cfg.shade_classes == 2 ? 1 : 0;
         {
             TimedScope ts(cfg, st, KT_SHADE);
-            if (hf.options.bsdf_override == MPT_BSDF_LAMBERTIAN) {
-                hipLaunchKernelGGL((k_shade<MPT_BSDF_LAMBERTIAN, false>), dim3(blocks_for(n)), dim3(TB), 0, st, sa);
-            } else if (hf.options.bsdf_override == MPT_BSDF_OREN_NAYAR) {
-                hipLaunchKernelGGL((k_shade<MPT_BSDF_OREN_NAYAR, false>), dim3(blocks_for(n)), dim3(TB), 0, st, sa);
-            } else if (!classes) {
-                hipLaunchKernelGGL((k_shade<MPT_BSDF_NONE, false>), dim3(blocks_for(n)), dim3(TB), 0, st, sa);
-            } else {
-                hipLaunchKernelGGL((k_shade<MPT_BSDF_NONE, true>), dim3(blocks_for(n)), dim3(TB), 0, st, sa);
-            }
+            const dim3 sg(blocks_for(n));
+            if (hf.options.bsdf_override != MPT_BSDF_NONE) part_shade_override(hf.options.bsdf_override, ext, sg, st, sa);
+            else if (ext) part_shade_ext(sg, st, sa);
+            else if (!classes) part_shade_generic(sg, st, sa);
+            else part_shade_plain(sg, st, sa);
         }
         if (classes) {
             TimedScope ts(cfg, st, KT_SHADE_GENERIC);
             ShadeArgs sf = sa;
             sf.q_cur = P.qf; sf.count_cur = &P.counters[CTR_FULL]; sf.q_defer = nullptr; sf.count_defer = nullptr;
-            hipLaunchKernelGGL((k_shade<MPT_BSDF_NONE, false>), dim3(blocks_for(n)), dim3(TB), 0, st, sf);
+            part_shade_generic(dim3(blocks_for(n)), st, sf);
         }
         {
             TimedScope ts(cfg, st, KT_MISS);
@@ -2158,10 +2460,30 @@ hipError_t launch_frame(const DevScene& S, const DevPaths& P0, const MptFrame* d
         } else {
             timed_trace<TM_NEE_CLOSEST>(tn, cfg, st);
         }
+        if (ext) {
+            // the extended light sampling's shadow and light-hit rays (same stages, own lists)
+            TraceArgs tx = tn;
+            tx.ext = 1;
+            tx.static_grid = 0;
+            hipMemsetAsync(&P.counters[CTR_FETCH], 0, sizeof(int32_t), st);
+            tx.count_ptr = &P.counters[CTR_XANY];
+            timed_trace<TM_NEE_ANY>(tx, cfg, st);
+            hipMemsetAsync(&P.counters[CTR_FETCH], 0, sizeof(int32_t), st);
+            tx.count_ptr = &P.counters[CTR_XCL];
+            if (cfg.light_bvh) {
+                timed_trace<TM_NEE_LIGHT>(tx, cfg, st);
+                hipMemsetAsync(&P.counters[CTR_FETCH], 0, sizeof(int32_t), st);
+                tx.count_ptr = &P.counters[CTR_XLIGHT];
+                timed_trace<TM_NEE_LIGHT_OCC>(tx, cfg, st);
+            } else {
+                timed_trace<TM_NEE_CLOSEST>(tx, cfg, st);
+            }
+        }
         {
             TimedScope ts(cfg, st, KT_RESOLVE);
-            hipLaunchKernelGGL(k_resolve, dim3(blocks_for(classes ? 2 * n : n)), dim3(TB), 0, st, S, P, d_frame, b,
-                               &P.counters[c_cur]);
+            if (ext) hipLaunchKernelGGL(k_resolve<true>, dim3(blocks_for(n)), dim3(TB), 0, st, S, P, d_frame, b, &P.counters[c_cur]);
+            else hipLaunchKernelGGL(k_resolve<false>, dim3(blocks_for(classes ? 2 * n : n)), dim3(TB), 0, st, S, P, d_frame, b,
+                                    &P.counters[c_cur]);
         }
         // swap queues
         int32_t* tq = q_cur; q_cur = q_next; q_next = tq;
@@ -2202,13 +2524,6 @@ __global__ void k_resolve_materials(DevScene S, MptMaterial* out, int32_t* tex, 
     tex[i] = (textured ? MT_TEXTURED : 0) | (plain ? 0 : MT_FULL);
 }
 
-#ifdef MPT_SECTION_TIMING
-extern "C" int mpt_debug_sections(unsigned long long* out, int reset) {
-    hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sect), sizeof(unsigned long long) * 8);
-    if (reset) { unsigned long long z[8] = {0}; hipMemcpyToSymbol(HIP_SYMBOL(g_sect), z, sizeof(z)); }
-    return 0;
-}
-#endif
 
 // Development check of the transcendental layer (fn: 0 sin 1 cos 2 exp 3 log 4 pow
 // 5 atan2 6 asin 7 acos); host pointers, synchronous.
@@ -2290,4 +2605,5 @@ hipError_t launch_trace_raw(const DevScene& S, const float4* o, const float4* d,
     return hipGetLastError();
 }
 
+#endif
 }  // namespace mpt

@@ -1,0 +1,72 @@
+// mpt_part.hip -- the large kernel instantiations of mpt_kernels.hip, one group per
+// translation unit: the build compiles this file once per MPT_TU_PART value (mpt/_build.py)
+// so that the shading and ReSTIR DI kernels compile in parallel.  mpt_kernels.hip's host glue
+// launches them through these functions.
+#ifndef MPT_TU_PART
+#error "compile with -DMPT_TU_PART=<1..6>"
+#endif
+#include "mpt_kernels.hip"
+
+namespace mpt {
+
+#if MPT_TU_PART == 1
+void part_shade_generic(dim3 g, hipStream_t st, const ShadeArgs& a) {
+    hipLaunchKernelGGL((k_shade<MPT_BSDF_NONE, false>), g, dim3(TB), 0, st, a);
+}
+#elif MPT_TU_PART == 2
+void part_shade_plain(dim3 g, hipStream_t st, const ShadeArgs& a) {
+    hipLaunchKernelGGL((k_shade<MPT_BSDF_NONE, true>), g, dim3(TB), 0, st, a);
+}
+#ifdef MPT_SECTION_TIMING
+extern "C" int mpt_debug_sections(unsigned long long* out, int reset) {   // k_shade<NONE, true>'s section clocks
+    hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sect), sizeof(unsigned long long) * 8);
+    if (reset) { unsigned long long z[8] = {0}; hipMemcpyToSymbol(HIP_SYMBOL(g_sect), z, sizeof(z)); }
+    return 0;
+}
+#endif
+#elif MPT_TU_PART == 3
+void part_shade_ext(dim3 g, hipStream_t st, const ShadeArgs& a) {
+    hipLaunchKernelGGL((k_shade<MPT_BSDF_NONE, false, true>), g, dim3(TB), 0, st, a);
+}
+#elif MPT_TU_PART == 4
+void part_shade_override(int ovr, bool ext, dim3 g, hipStream_t st, const ShadeArgs& a) {
+    if (ovr == MPT_BSDF_LAMBERTIAN) {
+        if (ext) hipLaunchKernelGGL((k_shade<MPT_BSDF_LAMBERTIAN, false, true>), g, dim3(TB), 0, st, a);
+        else hipLaunchKernelGGL((k_shade<MPT_BSDF_LAMBERTIAN, false>), g, dim3(TB), 0, st, a);
+    } else {
+        if (ext) hipLaunchKernelGGL((k_shade<MPT_BSDF_OREN_NAYAR, false, true>), g, dim3(TB), 0, st, a);
+        else hipLaunchKernelGGL((k_shade<MPT_BSDF_OREN_NAYAR, false>), g, dim3(TB), 0, st, a);
+    }
+}
+#elif MPT_TU_PART == 5 || MPT_TU_PART == 6
+// ReSTIR DI reuse kernels of one BSDF override (5: Principled, 6: Lambert + Oren-Nayar); the
+// reference-default bias correction (pairwise MIS defensive with visibility) has its own
+// variant with the mode compiled in, the others read it from the frame (-1)
+template <int OVR>
+static void restir_kernel(int kind, dim3 g, hipStream_t st, const DevScene& S, const DevPaths& P, const MptFrame* F, int pass,
+                          const float4* in, float4* out) {
+    constexpr int DEF = MPT_RESTIR_DI_BIAS_PAIRWISE_MIS_DEFENSIVE;
+    switch (kind) {
+    case RK_INITIAL: hipLaunchKernelGGL(k_restir_initial<OVR>, g, dim3(TB), 0, st, S, P, F); break;
+    case RK_SPATIOTEMPORAL: hipLaunchKernelGGL((k_restir_spatiotemporal<OVR, DEF>), g, dim3(TB), 0, st, S, P, F); break;
+    case RK_SPATIOTEMPORAL_ANY: hipLaunchKernelGGL((k_restir_spatiotemporal<OVR, -1>), g, dim3(TB), 0, st, S, P, F); break;
+    case RK_SPATIAL: hipLaunchKernelGGL((k_restir_spatial<OVR, DEF>), g, dim3(TB), 0, st, S, P, F, pass, in, out); break;
+    case RK_SPATIAL_ANY: hipLaunchKernelGGL((k_restir_spatial<OVR, -1>), g, dim3(TB), 0, st, S, P, F, pass, in, out); break;
+    default: hipLaunchKernelGGL(k_restir_temporal<OVR>, g, dim3(TB), 0, st, S, P, F, in, out); break;
+    }
+}
+#if MPT_TU_PART == 5
+void part_restir_principled(int kind, dim3 g, hipStream_t st, const DevScene& S, const DevPaths& P, const MptFrame* F, int pass,
+                            const float4* in, float4* out) {
+    restir_kernel<MPT_BSDF_NONE>(kind, g, st, S, P, F, pass, in, out);
+}
+#else
+void part_restir_override(int ovr, int kind, dim3 g, hipStream_t st, const DevScene& S, const DevPaths& P, const MptFrame* F,
+                          int pass, const float4* in, float4* out) {
+    if (ovr == MPT_BSDF_LAMBERTIAN) restir_kernel<MPT_BSDF_LAMBERTIAN>(kind, g, st, S, P, F, pass, in, out);
+    else restir_kernel<MPT_BSDF_OREN_NAYAR>(kind, g, st, S, P, F, pass, in, out);
+}
+#endif
+#endif
+
+}  // namespace mpt

@@ -300,6 +300,7 @@ DEV void restir_reproject(const MptFrame& F, v3 p, float& fx, float& fy) {
 }
 
 // ---- G-buffer write: CameraRays (CameraRays.h:144-166) over the camera queue ----------
+#ifndef MPT_TU_PART   // k_gbuffer
 __global__ __launch_bounds__(TB) void k_gbuffer(DevScene S, DevPaths P, const MptFrame* __restrict__ Fp) {
     const MptFrame& F = *Fp;
     int i = blockIdx.x * TB + threadIdx.x;
@@ -365,8 +366,10 @@ __global__ __launch_bounds__(TB) void k_gbuffer(DevScene S, DevPaths P, const Mp
     P.gb_meta[gp] = meta;
     P.gb_view[gp] = make_float4(-d.x, -d.y, -d.z, 0.0f);
 }
+#endif
 
 // ---- ReSTIR_DI_LightsPresampling (LightsPresampling.h:22-130) ------------------------
+#ifndef MPT_TU_PART   // k_restir_presample
 __global__ __launch_bounds__(TB) void k_restir_presample(DevScene S, DevPaths P, const MptFrame* __restrict__ Fp) {
     const MptFrame& F = *Fp;
     const MptReSTIRDISettings& rd = F.render_settings.restir_di_settings;
@@ -416,6 +419,7 @@ __global__ __launch_bounds__(TB) void k_restir_presample(DevScene S, DevPaths P,
     o[1] = make_float4(nrm.x, nrm.y, nrm.z, pdf);
     o[2] = make_float4(rad.r, rad.g, rad.b, __uint_as_float(flags));
 }
+#endif
 
 // ---- ReSTIR_DI_InitialCandidates (InitialCandidates.h:24-508) ------------------------
 template <int OVR>
@@ -1058,6 +1062,7 @@ RESTIR_KERNEL void k_restir_spatial(DevScene S, DevPaths P, const MptFrame* __re
 }
 
 // CameraRays' reset / previous-frame G-buffer copy for LSS_RESTIR_DI (CameraRays.h:19-34, 78-91)
+#ifndef MPT_TU_PART   // k_restir_frame_begin
 __global__ __launch_bounds__(TB) void k_restir_frame_begin(DevPaths P, const MptFrame* __restrict__ Fp) {
     const MptFrame& F = *Fp;
     const MptRenderSettings& rs = F.render_settings;
@@ -1076,18 +1081,24 @@ __global__ __launch_bounds__(TB) void k_restir_frame_begin(DevPaths P, const Mpt
         rr_store(P.rs_sp2, i, rr_default());
     }
 }
+#endif
 
 // pixel_converged_sample_count by pixel for the neighbour tests of a partitioned context
 // (restir_spatial_neighbor reads it at neighbouring pixels; exchanged with the G-buffer)
+#ifndef MPT_TU_PART   // k_restir_conv
 __global__ __launch_bounds__(TB) void k_restir_conv(DevPaths P) {
     int s = blockIdx.x * TB + threadIdx.x;
     if (s < P.n) P.rs_conv[s + P.pix_off] = P.as_conv[s];
 }
+#endif
 
+#ifndef MPT_TU_PART   // k_restir_fill
 __global__ void k_restir_fill(float4* r, int n) {   // default reservoirs (Reservoir.h:166-170)
     int i = blockIdx.x * TB + threadIdx.x;
     if (i < n) rr_store(r, i, rr_default());
 }
+#endif
+#ifndef MPT_TU_PART   // k_restir_fill_lights
 __global__ void k_restir_fill_lights(float4* l, int n) {   // default presampled lights
     int i = blockIdx.x * TB + threadIdx.x;
     if (i < n) {
@@ -1097,3 +1108,4 @@ __global__ void k_restir_fill_lights(float4* l, int n) {   // default presampled
         l[4 * (size_t)i + 3] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     }
 }
+#endif

@@ -20,6 +20,9 @@ LIB_PATH = PKG_DIR / "libmpt.so"
 OBJ_DIR = CSRC / "build"
 
 SOURCES = ["bvh8.cpp", "mpt_kernels.hip", "bake.hip", "mpt_api.cpp"]
+# mpt_part.hip is compiled once per part (-DMPT_TU_PART=k): the shading and ReSTIR DI kernel
+# instantiations, so that they compile in parallel with the rest
+PARTS = [1, 2, 3, 4, 5, 6]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 CXXFLAGS = [
@@ -29,7 +32,7 @@ CXXFLAGS = [
 
 
 def _deps() -> list[Path]:
-    return [CSRC / s for s in SOURCES] + sorted(CSRC.glob("*.h")) + sorted(INCLUDE.glob("*.h"))
+    return [CSRC / s for s in SOURCES] + [CSRC / "mpt_part.hip"] + sorted(CSRC.glob("*.h")) + sorted(INCLUDE.glob("*.h"))
 
 
 def up_to_date() -> bool:
@@ -48,13 +51,14 @@ def build(force: bool = False, verbose: bool = True, defines=(), out: Path | Non
     obj_dir.mkdir(parents=True, exist_ok=True)
     procs = []
     objs = []
-    for s in SOURCES:
-        obj = obj_dir / (Path(s).stem + ".o")
+    units = [(s, [], Path(s).stem) for s in SOURCES] + [("mpt_part.hip", [f"-DMPT_TU_PART={k}"], f"mpt_part{k}") for k in PARTS]
+    for s, extra, stem in units:
+        obj = obj_dir / (stem + ".o")
         objs.append(obj)
-        cmd = [HIPCC, *CXXFLAGS, *defines, "-c", str(CSRC / s), "-o", str(obj)]
+        cmd = [HIPCC, *CXXFLAGS, *defines, *extra, "-c", str(CSRC / s), "-o", str(obj)]
         if verbose:
             print("[mpt build]", " ".join(cmd), file=sys.stderr)
-        procs.append((s, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))
+        procs.append((stem, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))
     errors = []
     for s, p in procs:
         out, _ = p.communicate()

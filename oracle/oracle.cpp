@@ -1215,8 +1215,7 @@ int oracle_render(OracleScene* sc, const MptFrame* frames, int nframes, float* s
     const bool restir = f0.options.direct_light_sampling == MPT_LSS_RESTIR_DI;
     if ((has_adaptive_buffers(f0.render_settings) && !(as_count && as_sqlum && as_conv && status)) ||
         f0.render_settings.wants_render_low_resolution ||
-        (restir && (f0.band_count != 1 || f0.render_settings.number_of_light_samples != 1 ||
-                    f0.render_settings.restir_di_settings.number_of_passes > 4)) ||
+        (restir && (f0.band_count != 1 || f0.render_settings.restir_di_settings.number_of_passes > 4)) ||
         (f0.options.envmap_sampling == MPT_ESS_BINARY_SEARCH && s.env_rgba && !s.env_cdf))
         return -4;
     std::vector<int> rows;
