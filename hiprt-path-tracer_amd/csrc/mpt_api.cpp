@@ -143,7 +143,7 @@ struct MptContext {
     DBuf<uint2> seeds;
     DBuf<uint4> vsA, vsB;
     DBuf<int32_t> q0, q1, qh, qm, qf, nq_light, counters, nq_tgt, fetch_raw;
-    DBuf<NeeRec> nee;
+    DBuf<float4> nthr, na, nb, ndir, nris, ne1, ne2;   // NEE record planes (mpt_internal.h)
     DBuf<float> fb_color, fb_albedo, fb_normal;
     DBuf<int32_t> as_count, as_conv;
     DBuf<float> as_sqlum;
@@ -265,7 +265,9 @@ DevPaths dev_paths(MptContext* c) {
     P.qf = c->qf.p;
     P.nq_light = c->nq_light.p;
     P.counters = c->counters.p;
-    P.nee = c->nee.p;
+    P.nthr = c->nthr.p; P.na = c->na.p; P.nb = c->nb.p; P.ndir = c->ndir.p; P.nris = c->nris.p; P.ne1 = c->ne1.p;
+    P.ne2 = c->ne2.p;
+    P.nq_stride = (int64_t)std::max(c->n_slots, 1) * (int64_t)std::max(c->batch_cap, 1);
     P.nq_o = c->nq_o.p;
     P.nq_d = c->nq_d.p;
     P.nq_tgt = c->nq_tgt.p;
@@ -324,14 +326,15 @@ struct Allocs {
 };
 
 // Bytes of path state per path slot (ensure_batch): ray_o, ray_d, hit, thr, col, alb, nrmv,
-// nhit (8 x 16), vsA + vsB (32), the NEE record, 4 staged NEE query rays (2 x 64), the
+// nhit (8 x 16), vsA + vsB (32), the NEE record planes (7 x 16), 4 staged NEE query rays (2 x 64), the
 // compacted query entries (16), occlusion bytes (4), 6 queues (24), rng (4), seeds (8), hit_inside,
 // qmask, active (3).  Textured scenes add a resolved material per slot.
-constexpr size_t PATH_BYTES = 8 * 16 + 32 + sizeof(NeeRec) + 128 + 16 + 4 + 24 + 4 + 8 + 3;
+constexpr size_t PATH_BYTES = 8 * 16 + 32 + 7 * 16 + 128 + 16 + 4 + 24 + 4 + 8 + 3;
 
 void release_batch(MptContext* c) {
     release_all(c->ray_o, c->ray_d, c->hit, c->hit_inside, c->rng, c->seeds, c->thr, c->col, c->vsA, c->vsB, c->alb, c->nrmv,
-                c->q0, c->q1, c->qh, c->qm, c->qf, c->nq_light, c->nee, c->nq_o, c->nq_d, c->nq_tgt, c->occ, c->nhit, c->qmask, c->active,
+                c->q0, c->q1, c->qh, c->qm, c->qf, c->nq_light, c->nthr, c->na, c->nb, c->ndir, c->nris, c->ne1, c->ne2, c->nq_o,
+                c->nq_d, c->nq_tgt, c->occ, c->nhit, c->qmask, c->active,
                 c->mat_slot);
     c->batch_cap = 0;
 }
@@ -352,7 +355,8 @@ int ensure_batch(MptContext* c, int batch, bool mat_slot) {
         c->batch_cap = 0;
         A(c->ray_o, N); A(c->ray_d, N); A(c->hit, N); A(c->hit_inside, N); A(c->rng, N); A(c->seeds, N); A(c->thr, N); A(c->col, N);
         A(c->vsA, N); A(c->vsB, N); A(c->alb, N); A(c->nrmv, N); A(c->q0, N); A(c->q1, N); A(c->qh, N); A(c->qm, N); A(c->qf, N); A(c->nq_light, N);
-        A(c->nee, N); A(c->nq_o, 4 * N); A(c->nq_d, 4 * N); A(c->nq_tgt, 4 * N); A(c->occ, 4 * N); A(c->nhit, N);
+        A(c->nthr, N); A(c->na, N); A(c->nb, N); A(c->ndir, N); A(c->nris, N); A(c->ne1, N); A(c->ne2, N);
+        A(c->nq_o, 4 * N); A(c->nq_d, 4 * N); A(c->nq_tgt, 4 * N); A(c->occ, 4 * N); A(c->nhit, N);
         A(c->qmask, N); A(c->active, N);
         if (A.e == hipSuccess) A(hipMemsetAsync(c->active.p, 0, N, c->stream));
     }
@@ -1090,7 +1094,9 @@ static void offset_slots(DevPaths& P, size_t off) {
     P.ray_o += off; P.ray_d += off; P.hit += off; P.hit_inside += off; P.rng += off; P.seeds += off; P.thr += off; P.col += off;
     P.vsA += off; P.vsB += off; P.alb += off; P.nrm += off;
     P.q0 += off; P.q1 += off; P.qh += off; P.qm += off; P.qf += off; P.nq_light += off;
-    P.nee += off; P.nq_o += 4 * off; P.nq_d += 4 * off; P.nq_tgt += 4 * off; P.occ += 4 * off;
+    // NEE record planes, and the kind-major query / occlusion planes (stride = the allocation)
+    P.nthr += off; P.na += off; P.nb += off; P.ndir += off; P.nris += off; P.ne1 += off; P.ne2 += off;
+    P.nq_o += off; P.nq_d += off; P.occ += off; P.nq_tgt += 4 * off;
     P.nhit += off; P.qmask += off; P.active += off;
     if (P.mat_slot) P.mat_slot += off;
 }

@@ -65,19 +65,18 @@ struct DevScene {
     float env_cdf_sum;            // its last element (OrochiEnvmap::compute_cdf)
 };
 
-// NEE record written by the shade stage and consumed by the resolve stage (128 B / slot)
-struct alignas(16) NeeRec {
-    float thr[3]; uint32_t flags;
-    float a[3]; float a_cos;        // light sample: MIS/uniform pending radiance, RIS winner bsdf*; cos
-    float b[3]; float b_pdf;        // BSDF sample / candidate: bsdf colour, pdf
-    float dir[3]; float b_cos;      // BSDF sample direction, cosine
-    float e1[3]; float ris_wsum;    // envmap light-sampled contribution; RIS weight sum of light candidates
-    float e2[3]; float ris_target;  // envmap BSDF-sampled contribution; RIS target of the light winner
-    float r_add; int32_t ris_tri; float imm[3];   // RIS random of the BSDF candidate; light winner triangle; immediate light term
-    float pad[3];
-};
-static_assert(sizeof(NeeRec) == 128, "NeeRec is 128 bytes");
-
+// NEE record written by the shade stage and consumed by the resolve stage: seven float4
+// planes indexed by slot (SoA, so that a wave's stores of one field cover 1 KiB of
+// consecutive bytes), each written whole, and only when the vertex uses it:
+//   nthr  throughput at the vertex (rgb) + NF_* flags
+//   na    light-sample term (rgb: MIS / uniform pending radiance, RIS winner BSDF value,
+//         ReSTIR DI final shading, or the immediate emission of NF_IMM) + RIS winner cosine
+//   nb    BSDF sample / candidate: BSDF value (rgb) + pdf
+//   ndir  BSDF sample direction + cosine
+//   nris  RIS: light-candidate weight sum, winner target, the BSDF candidate's random,
+//         winner triangle
+//   ne1   envmap light-sampled contribution (rgb)
+//   ne2   envmap BSDF-sampled contribution (rgb)
 enum : uint32_t {
     NF_SHADED = 1u << 0,     // the path had a hit at this bounce -> resolve adds NEE
     NF_A = 1u << 1,          // light-sample contribution pending occlusion slot 0
@@ -132,12 +131,19 @@ struct DevPaths {
     int32_t* qf;              // hits on materials outside the plain-dielectric class (k_split, k_shade)
     int32_t* nq_light;        // light-hit queries whose light candidate needs the whole-scene check (slot * 4 + 3)
     int32_t* counters;        // see CTR_*
-    NeeRec* nee;
-    float4* nq_o;             // staged NEE query rays, slot * 4 + kind (kinds 0..2 any hit, 3 closest)
-    float4* nq_d;
+    float4* nthr;             // NEE record planes (above)
+    float4* na;
+    float4* nb;
+    float4* ndir;
+    float4* nris;
+    float4* ne1;
+    float4* ne2;
+    float4* nq_o;             // staged NEE query rays of query id slot * 4 + kind (kinds 0..2 any hit, 3
+    float4* nq_d;             // closest), stored kind-major: [kind * nq_stride + slot] (nq_index)
+    int64_t nq_stride;        // path slots the query / occlusion planes are sized for
     int32_t* nq_tgt;          // compacted query lists: [0, 3n) any hit, [3n, 4n) closest; entries slot * 4 + kind
     uint8_t* qmask;           // per slot: staged queries (bits 0..3), continuation (QM_CONT)
-    uint8_t* occ;             // any-hit results, slot * 4 + kind
+    uint8_t* occ;             // any-hit results, kind-major like nq_o
     float4* nhit;             // closest NEE result per slot
     MptMaterial* mat_slot;    // per-slot resolved material (textured materials, white furnace)
     float* fb_color;          // 3 per slot (sum)

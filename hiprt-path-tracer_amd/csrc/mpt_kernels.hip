@@ -63,6 +63,8 @@ constexpr int SPILL_DEPTH = TRAV_SPILL_DEPTH;
 // wave64 helpers
 // ----------------------------------------------------------------------------------
 DEV int lane_id() { return __lane_id(); }
+// storage index of staged NEE query id (slot * 4 + kind): kind-major planes (DevPaths::nq_o)
+DEV size_t nq_index(const DevPaths& P, int id) { return (size_t)(id & 3) * (size_t)P.nq_stride + (size_t)(id >> 2); }
 DEV int wave_append(int32_t* counter, bool pred) {
     unsigned long long m = __ballot(pred);
     unsigned long long act = __ballot(1);
@@ -426,8 +428,8 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MODE == TM_P
                         if (A.ext) ray = MODE == TM_NEE_LIGHT_OCC ? P.xl_light[i] : MODE == TM_NEE_ANY ? P.xl_any[i] : P.xl_cl[i];
                         else ray = MODE == TM_NEE_LIGHT_OCC ? P.nq_light[i]
                                                             : P.nq_tgt[MODE == TM_NEE_ANY ? (size_t)i : (size_t)P.n * 3 + i];
-                        ro = A.ext ? P.xq_o[ray] : P.nq_o[ray];
-                        rd = A.ext ? P.xq_d[ray] : P.nq_d[ray];
+                        ro = A.ext ? P.xq_o[ray] : P.nq_o[nq_index(P, ray)];
+                        rd = A.ext ? P.xq_d[ray] : P.nq_d[nq_index(P, ray)];
                         qmax = rd.w;
                         const bool al = A.alpha != 0;
                         uint32_t akey = 0u;
@@ -486,7 +488,8 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MODE == TM_P
             P.hit[ray] = make_float4(tr.best, tr.bu, tr.bv, __uint_as_float((uint32_t)(found ? tr.bprim : -1)));
             P.hit_inside[ray] = was_inside ? 1 : 0;
         } else if (MODE == TM_NEE_ANY) {
-            (A.ext ? P.xq_occ : P.occ)[ray] = found ? 1 : 0;
+            if (A.ext) P.xq_occ[ray] = found ? 1 : 0;
+            else P.occ[nq_index(P, ray)] = found ? 1 : 0;
         } else if (MODE == TM_NEE_CLOSEST || MODE == TM_NEE_LIGHT) {
             // evaluate_shadow_light_ray: a hit counts only below t_max - 1e-4 (Intersect.h:337-343)
             bool ok = found && tr.best < qmax;
@@ -994,7 +997,7 @@ DEV Col env_eval(const DevScene& S, const MptFrame& F, v3 d, float& pdf) {
 // compacted lists afterwards, so k_shade itself issues no atomics (an atomic with a
 // return value would wait for all of the lane's outstanding stores).
 DEV void stage_query(const DevPaths& P, int slot, int kind, uint32_t& qm, v3 o, int last_hit, v3 d, float tmax) {
-    size_t e = (size_t)slot * 4 + kind;
+    const size_t e = (size_t)kind * (size_t)P.nq_stride + (size_t)slot;
     P.nq_o[e] = make_float4(o.x, o.y, o.z, __uint_as_float((uint32_t)last_hit));
     P.nq_d[e] = make_float4(d.x, d.y, d.z, tmax);
     qm |= 1u << kind;
@@ -1294,6 +1297,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_
         VState vs = vs_load(P.vsA, P.vsB, slot);
         Rng rng = make_rng(P.rng[slot]);
         Col thr = col(P.thr[slot].x, P.thr[slot].y, P.thr[slot].z);
+        const Col thr_vertex = thr;        // the NEE terms' throughput (k_resolve)
         float4 cv = P.col[slot];
         Col rcol = col(cv.x, cv.y, cv.z);
         v3 ip = mk3(0, 0, 0), gn = mk3(0, 0, 0), sn = mk3(0, 0, 0);
@@ -1348,7 +1352,6 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_
                 return;             // nothing written (no block-wide operation follows)
             }
         }
-        NeeRec& nr = P.nee[slot];   // written field by field, straight to HBM
         uint32_t fl = 0;
         uint32_t qm = 0;            // staged NEE queries (bits 0..3) + continuation (bit 4)
         if (found) {
@@ -1370,7 +1373,11 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_
                             !(F.bsdf_flags.white_furnace_mode && F.bsdf_flags.white_furnace_mode_turn_off_emissives);
             if (do_light && is_emissive(m)) {
                 do_light = false;
-                if (m.emissive_texture_used && bounce > 0) { fl |= NF_IMM; store3(nr.imm, emission_of(m)); }
+                if (m.emissive_texture_used && bounce > 0) {
+                    fl |= NF_IMM;
+                    const Col e = emission_of(m);
+                    P.na[slot] = make_float4(e.r, e.g, e.b, 0.0f);
+                }
             }
             do_light = do_light && lss != MPT_LSS_NO_DIRECT_LIGHT_SAMPLING;
             const int lssb = bounce_lss(F, bounce);
@@ -1399,7 +1406,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_
             v3 pointW = mk3(0, 0, 0);
             int triW = -1, ris_c = 0;
             bool hasW = false;
-            const Col thr_vertex = thr;
+            float r_add = 0.0f;                // the RIS BSDF candidate's random (add_one_candidate)
             // per-vertex half of every BSDF evaluation below, one LDS record per lane (55
             // dwords: an odd stride, so lane-parallel accesses are bank-conflict free).  Held
             // in registers it pushed the kernel into ~140 spilled VGPRs; in LDS it costs one
@@ -1520,23 +1527,18 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_
                     if (pdf > 0.0f) {
                         fl |= NF_B | (refr ? NF_B_REFR : 0u);
                         stage_query(P, slot, 3, qm, so, prim, L, 1.0e35f - 1.0e-4f);
-                        store3(nr.b, f);
-                        nr.b_pdf = pdf;
-                        store3(nr.dir, L);
-                        nr.b_cos = absr(dot(sn, L));
+                        P.nb[slot] = make_float4(f.r, f.g, f.b, pdf);
+                        P.ndir[slot] = make_float4(L.x, L.y, L.z, absr(dot(sn, L)));
                     }
-                    nr.r_add = rng();
+                    r_add = rng();
                     next = OP_RIS_WIN;
                 } else if (op == OP_RIS_WIN) {
                     if (!do_eval) { f = fW; pdf = pdfW; }
-                    nr.ris_wsum = wsum;
+                    P.nris[slot] = make_float4(wsum, targetW, r_add, __int_as_float(triW));
                     if (hasW) {
                         fl |= NF_RIS_W;
                         stage_query(P, slot, 0, qm, lp, prim, L, dist - 1.0e-4f);
-                        store3(nr.a, f);
-                        nr.a_cos = maxr(0.0f, dot(sn, L));
-                        nr.ris_target = targetW;
-                        nr.ris_tri = triW;
+                        P.na[slot] = make_float4(f.r, f.g, f.b, maxr(0.0f, dot(sn, L)));
                     }
                     next = OP_DONE;
                 } else if (op == OP_MIS_LIGHT) {
@@ -1546,7 +1548,8 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_
                         lp2 /= geo;
                         float w = balance(lp2, pdf);
                         float cosv = maxr(dot(sn, L), 0.0f);
-                        store3(nr.a, f * cosv * li.emission * w / lp2);
+                        const Col a = f * cosv * li.emission * w / lp2;
+                        P.na[slot] = make_float4(a.r, a.g, a.b, 0.0f);
                         fl |= NF_A;
                         stage_query(P, slot, 0, qm, lp, prim, L, dist - 1.0e-4f);
                     }
@@ -1557,10 +1560,8 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_
                     if (pdf > 0) {
                         fl |= NF_B;
                         stage_query(P, slot, 3, qm, bo, prim, L, 1.0e35f - 1.0e-4f);
-                        store3(nr.b, f);
-                        nr.b_pdf = pdf;
-                        store3(nr.dir, L);
-                        nr.b_cos = absr(dot(sn, L));
+                        P.nb[slot] = make_float4(f.r, f.g, f.b, pdf);
+                        P.ndir[slot] = make_float4(L.x, L.y, L.z, absr(dot(sn, L)));
                     }
                 } else if (op == OP_UNI_LIGHT) {
                     if (do_eval && pdf != 0.0f) {
@@ -1568,7 +1569,8 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_
                         lp2 *= dist * dist;
                         lp2 /= geo;
                         float cosv = maxr(dot(sn, L), 0.0f);
-                        store3(nr.a, li.emission * cosv * f / lp2);
+                        const Col a = li.emission * cosv * f / lp2;
+                        P.na[slot] = make_float4(a.r, a.g, a.b, 0.0f);
                         fl |= NF_A;
                         stage_query(P, slot, 0, qm, lp, prim, L, dist - 1.0e-4f);
                     }
@@ -1579,10 +1581,8 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_
                         v3 no = refr ? ip + sn * 1.0e-4f * ism * -1.0f : ip + sn * 1.0e-4f;
                         fl |= NF_B;
                         stage_query(P, slot, 3, qm, no, prim, L, 1.0e35f - 1.0e-4f);
-                        store3(nr.b, f);
-                        nr.b_pdf = pdf;
-                        store3(nr.dir, L);
-                        nr.b_cos = maxr(0.0f, dot(sn, L));
+                        P.nb[slot] = make_float4(f.r, f.g, f.b, pdf);
+                        P.ndir[slot] = make_float4(L.x, L.y, L.z, maxr(0.0f, dot(sn, L)));
                     }
                 } else if (op == OP_RESTIR) {
                     if (do_eval) {
@@ -1592,7 +1592,8 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_
                             Col e;
                             if (rres.flags & RF_ENVMAP) { float ep_; e = env_eval(S, F, L, ep_); }
                             else e = emission_of(S.mats[S.mat_idx[rres.tri]]);
-                            store3(nr.a, f * rres.UCW * e * c);
+                            const Col a = f * rres.UCW * e * c;
+                            P.na[slot] = make_float4(a.r, a.g, a.b, 0.0f);
                             fl |= NF_A;
                             if (!(rres.flags & RF_UNOCCLUDED) && rs.restir_di_settings.do_final_shading_visibility) {
                                 fl |= NF_AQ;
@@ -1604,7 +1605,8 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_
                     // Envmap.h:151-246
                     if (do_eval) {
                         float mw = F.options.envmap_bsdf_mis ? balance(lpdf, pdf) : 1.0f;
-                        store3(nr.e1, f * geo * mw * ec / lpdf);
+                        const Col e1 = f * geo * mw * ec / lpdf;
+                        P.ne1[slot] = make_float4(e1.r, e1.g, e1.b, 0.0f);
 #ifdef MPT_DEBUG_SLOT
                         if (slot == MPT_DEBUG_SLOT) { Col e1_ = f * geo * mw * ec / lpdf; printf("GPU env f %a %a %a bp %a mw %a e1 %a %a %a\n", f.r, f.g, f.b, pdf, mw, e1_.r, e1_.g, e1_.b); }
 #endif
@@ -1621,7 +1623,8 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_
                         Col er = env_eval(S, F, L, epdf);
                         if (epdf > 0.0f && env_use) {
                             float mw = balance(pdf, epdf);
-                            store3(nr.e2, er * mw * c2 * f / pdf);
+                            const Col e2 = er * mw * c2 * f / pdf;
+                            P.ne2[slot] = make_float4(e2.r, e2.g, e2.b, 0.0f);
                             fl |= NF_E2;
                             stage_query(P, slot, 2, qm, ip, prim, L, 1.0e35f - 1.0e-4f);
                         }
@@ -1675,11 +1678,10 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_
             } else if (bounce == 0) {
                 rcol += emission_of(m);
             }
-            store3(nr.thr, thr_vertex);
         } else {
             rcol += miss_radiance(S, F, bounce, d, thr);   // not reached: k_split sends misses to k_miss
         }
-        nr.flags = fl;
+        P.nthr[slot] = make_float4(thr_vertex.r, thr_vertex.g, thr_vertex.b, __uint_as_float(fl));
         P.qmask[slot] = (uint8_t)(qm | (cont ? QM_CONT : 0u));
         P.rng[slot] = rng.s;
         P.thr[slot] = make_float4(thr.r, thr.g, thr.b, 0.0f);
@@ -2026,79 +2028,80 @@ __global__ __launch_bounds__(TB) void k_resolve(DevScene S, DevPaths P, const Mp
     if (i >= nh + P.counters[CTR_FULL]) return;
     const int slot = shaded_entry(P, nh, i);
     if (slot < 0) return;   // deferred to the generic shading list
-#ifdef MPT_RESOLVE_BYREF
-    const NeeRec& nr = P.nee[slot];
-#else
-    // the whole 128-B record in eight back-to-back 16-B loads: each cache line is consumed
-    // while it is resident (field-by-field loads re-fetched lines from HBM, PMC)
-    const NeeRec nr = P.nee[slot];
-#endif
-    uint32_t fl = nr.flags;
+    // the NEE record planes the vertex wrote (flags in nthr.w), each read whole
+    const float4 t4 = P.nthr[slot];
+    const uint32_t fl = __float_as_uint(t4.w);
     if (!(fl & NF_SHADED) || (fl & NF_NOADD)) return;
     const int lss = F.options.direct_light_sampling;
     const int lssb = bounce_lss(F, bounce);
     Col ld = col(0.0f), ed = col(0.0f);
-    const uint8_t* occ = P.occ + (size_t)slot * 4;
-    if (fl & NF_IMM) ld = load3c(nr.imm);
+    auto occ = [&](int k) { return P.occ[(size_t)k * (size_t)P.nq_stride + (size_t)slot] != 0; };
+    if (fl & NF_IMM) { const float4 a = P.na[slot]; ld = col(a.x, a.y, a.z); }
     else if (!(fl & NF_L)) ld = col(0.0f);
     else if (EXT && (fl & NF_EXT)) ld = ext_resolve(S, P, F, slot, lssb);   // already / number_of_light_samples
     else if (lss == MPT_LSS_RESTIR_DI && bounce == 0) {
-        if ((fl & NF_A) && !((fl & NF_AQ) && occ[0])) ld = load3c(nr.a);
+        if ((fl & NF_A) && !((fl & NF_AQ) && occ(0))) { const float4 a = P.na[slot]; ld = col(a.x, a.y, a.z); }
     } else if (lssb == MPT_LSS_RIS_BSDF_AND_LIGHT) {
-        float wsum = nr.ris_wsum;
+        const float4 ris = P.nris[slot];
+        float wsum = ris.x;
         float cwb = 0.0f, targetb = 0.0f;
         int trib = -1;
+        float4 b = make_float4(0.0f, 0.0f, 0.0f, 0.0f), dr = b;
         if (fl & NF_B) {
+            b = P.nb[slot];
+            dr = P.ndir[slot];
             ShadowLightHit sh;
-            v3 dir = load3v(nr.dir);
             if (shadow_light_hit(S, P.nhit[slot], sh) && !is_black(sh.em)) {
-                Col lc = load3c(nr.b) * sh.em * nr.b_cos;
+                Col lc = col(b.x, b.y, b.z) * sh.em * dr.w;
                 targetb = lum(lc);
-                float lpdf = pdf_emissive_hit(S, sh, dir);
+                float lpdf = pdf_emissive_hit(S, sh, mk3(dr.x, dr.y, dr.z));
                 lpdf *= (fl & NF_B_REFR) ? 0.0f : 1.0f;
-                if (!min_contrib(rs.minimum_light_contribution, lc / lpdf / nr.b_pdf)) targetb = 0.0f;
-                float w = balance(nr.b_pdf, (float)rs.ris_number_of_bsdf_candidates, lpdf, (float)rs.ris_number_of_light_candidates);
-                cwb = w * targetb / nr.b_pdf;
+                if (!min_contrib(rs.minimum_light_contribution, lc / lpdf / b.w)) targetb = 0.0f;
+                float w = balance(b.w, (float)rs.ris_number_of_bsdf_candidates, lpdf, (float)rs.ris_number_of_light_candidates);
+                cwb = w * targetb / b.w;
                 trib = sh.prim;
             }
         }
         bool bsdf_wins = false;
         if (rs.ris_number_of_bsdf_candidates > 0) {
             wsum += cwb;
-            bsdf_wins = nr.r_add < cwb / wsum;
+            bsdf_wins = ris.z < cwb / wsum;
         }
         // RISReservoir::end (RIS_Reservoir.h:45-51); wsum > 0 implies a winner exists
-        float target = bsdf_wins ? targetb : ((fl & NF_RIS_W) ? nr.ris_target : 0.0f);
+        float target = bsdf_wins ? targetb : ((fl & NF_RIS_W) ? ris.y : 0.0f);
         float ucw = wsum == 0.0f ? 0.0f : 1.0f / target * wsum;
         if (ucw > 0.0f) {
             if (bsdf_wins) {
-                float c = nr.b_cos;
-                if (c > 0.0f) ld = load3c(nr.b) * ucw * emission_of(S.mats[S.mat_idx[trib]]) * c;
-            } else if (!occ[0]) {
-                float c = nr.a_cos;
-                if (c > 0.0f) ld = load3c(nr.a) * ucw * emission_of(S.mats[S.mat_idx[nr.ris_tri]]) * c;
+                float c = dr.w;
+                if (c > 0.0f) ld = col(b.x, b.y, b.z) * ucw * emission_of(S.mats[S.mat_idx[trib]]) * c;
+            } else if (!occ(0)) {
+                const float4 a = P.na[slot];
+                float c = a.w;
+                if (c > 0.0f) ld = col(a.x, a.y, a.z) * ucw * emission_of(S.mats[S.mat_idx[__float_as_int(ris.w)]]) * c;
             }
         }
     } else if (lssb == MPT_LSS_MIS_LIGHT_BSDF) {
         Col lrad = col(0.0f), brad = col(0.0f);
-        if ((fl & NF_A) && !occ[0]) lrad = load3c(nr.a);
+        if ((fl & NF_A) && !occ(0)) { const float4 a = P.na[slot]; lrad = col(a.x, a.y, a.z); }
         if (fl & NF_B) {
             ShadowLightHit sh;
-            v3 dir = load3v(nr.dir);
             if (shadow_light_hit(S, P.nhit[slot], sh) && !is_black(sh.em)) {
-                float lp2 = pdf_emissive_hit(S, sh, dir);
-                float w = balance(nr.b_pdf, lp2);
-                brad = load3c(nr.b) * nr.b_cos * sh.em * w / nr.b_pdf;
+                const float4 b = P.nb[slot], dr = P.ndir[slot];
+                float lp2 = pdf_emissive_hit(S, sh, mk3(dr.x, dr.y, dr.z));
+                float w = balance(b.w, lp2);
+                brad = col(b.x, b.y, b.z) * dr.w * sh.em * w / b.w;
             }
         }
         ld = lrad + brad;
     } else if (lssb == MPT_LSS_UNIFORM_ONE_LIGHT) {
-        if ((fl & NF_A) && !occ[0]) ld = load3c(nr.a);
+        if ((fl & NF_A) && !occ(0)) { const float4 a = P.na[slot]; ld = col(a.x, a.y, a.z); }
     } else if (lssb == MPT_LSS_BSDF) {
         if (fl & NF_B) {
             ShadowLightHit sh;
-            if (shadow_light_hit(S, P.nhit[slot], sh) && !is_black(sh.em))
-                ld = load3c(nr.b) * nr.b_cos * sh.em / nr.b_pdf;
+            if (shadow_light_hit(S, P.nhit[slot], sh) && !is_black(sh.em)) {
+                const float4 b = P.nb[slot], dr = P.ndir[slot];
+                ld = col(b.x, b.y, b.z) * dr.w * sh.em / b.w;
+            }
         }
     }
     // sample_many_lights: / number_of_light_samples (1 outside extended light sampling); not the
@@ -2107,21 +2110,18 @@ __global__ __launch_bounds__(TB) void k_resolve(DevScene S, DevPaths P, const Mp
         ld = ld / (float)rs.number_of_light_samples;
     {
         Col e2 = col(0.0f), e1 = col(0.0f);
-        if ((fl & NF_E2) && !occ[2]) e2 = load3c(nr.e2);
-        if ((fl & NF_E1) && !occ[1]) e1 = load3c(nr.e1);
-#ifdef MPT_DEBUG_SLOT
-        if (slot == MPT_DEBUG_SLOT) printf("GPU resolve fl %x occ %d %d %d\n", fl, occ[0], occ[1], occ[2]);
-#endif
+        if ((fl & NF_E2) && !occ(2)) { const float4 e = P.ne2[slot]; e2 = col(e.x, e.y, e.z); }
+        if ((fl & NF_E1) && !occ(1)) { const float4 e = P.ne1[slot]; e1 = col(e.x, e.y, e.z); }
         ed = e2 + e1;
     }
     ld = clamp_contrib(ld, rs.direct_contribution_clamp, bounce == 0);
     ed = clamp_contrib(ed, rs.envmap_contribution_clamp, bounce == 0);
-    Col ind = (ld + ed) * load3c(nr.thr);
+    Col ind = (ld + ed) * col(t4.x, t4.y, t4.z);
     float4 cv = P.col[slot];
     Col rc = col(cv.x, cv.y, cv.z) + clamp_contrib(ind, rs.indirect_contribution_clamp, bounce > 0);
     P.col[slot] = make_float4(rc.r, rc.g, rc.b, 0.0f);
 #ifdef MPT_DEBUG_SLOT
-    if (slot == MPT_DEBUG_SLOT) { Col t_ = load3c(nr.thr); printf("GPU b%d ld %a %a %a ed %a %a %a thr %a %a %a rc %a %a %a\n", bounce, ld.r, ld.g, ld.b, ed.r, ed.g, ed.b, t_.r, t_.g, t_.b, rc.r, rc.g, rc.b); }
+    if (slot == MPT_DEBUG_SLOT) { Col t_ = col(t4.x, t4.y, t4.z); printf("GPU b%d ld %a %a %a ed %a %a %a thr %a %a %a rc %a %a %a\n", bounce, ld.r, ld.g, ld.b, ed.r, ed.g, ed.b, t_.r, t_.g, t_.b, rc.r, rc.g, rc.b); }
 #endif
 }
 
