@@ -393,7 +393,7 @@ def main():
     hits = (st.path_hits or st.stage_rays[0]) - st.shade_generic_vertices
     lines.append({"kernel": "k_shade<BSDF_NONE, plain> (path vertex of a plain-dielectric material: hit, NEE sampling, "
                             "BSDF sampling, RR)",
-                  "symbol": "void mpt::k_shade<0, true>(mpt::ShadeArgs)",
+                  "symbol": "void mpt::k_shade<0, true",   # k_shade<OVR, plain, RIS visibility>
                   "total_ms": st.shade_ms, "avg_launch_ms": s_avg, "bytes_per_unit": b_vtx, "unit_of_work": "path vertex (hit)",
                   "units_per_launch": hits / sl,
                   "achieved": hits * b_vtx / sl / (s_avg * 1e-3) / 1e9 if s_avg > 0 else 0.0})

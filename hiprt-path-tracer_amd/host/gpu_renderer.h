@@ -8,6 +8,7 @@
 #define MPT_HOST_GPU_RENDERER_H
 
 #include <cstdint>
+#include <string>
 #include <vector>
 
 #include "mpt.h"
@@ -27,6 +28,17 @@ struct Xorshift32 {
     }
 };
 
+// Device destinations of the displayed buffers: the HIP pointers an OpenGL interop map
+// returns (OpenGLInteropBuffer<T>::map, OpenGLInteropBuffer.h), W*H float3 each; nullptr =
+// that buffer is not displayed.  The reference renders straight into them between
+// map_buffers_for_render and unmap_buffers; libmpt owns its sums, so unmap_buffers copies
+// them in (device to device, on the renderer's stream) before OpenGL takes the buffers back.
+struct DisplayBuffers {
+    float* color = nullptr;      // 'pixels' (a sum over the samples, RenderData.h:32)
+    float* albedo = nullptr;     // denoiser albedo AOV
+    float* normals = nullptr;    // denoiser normals AOV
+};
+
 class GPURenderer {
 public:
     // GPURenderer::GPURenderer (GPURenderer.cpp:48-86): m_rng seeded 42
@@ -38,51 +50,89 @@ public:
     // set_scene (GPURenderer.cpp:1041-1134): the arrays are copied, the BVH8 built on upload
     void set_scene(const MptScene& scene);
     // set_envmap (GPURenderer.cpp:1136-1174): RGBA32F equirect; alias table and CDF built here
-    void set_envmap(const float* rgba, int width, int height);
+    void set_envmap(const float* rgba, int width, int height, const std::string& envmap_filepath = "");
+    bool has_envmap() const { return m_has_envmap; }
+    const std::string& get_envmap_filepath() const { return m_envmap_path; }
     // setup_brdfs_data (GPURenderer.cpp:88-175)
     void setup_brdfs_data(const MptLuts& luts);
     // resize (GPURenderer.h:172)
     void resize(int width, int height);
-    // set_camera: the camera of the next frame; the previous one becomes prev_camera
+    // set_camera (GPURenderer.h:218): the camera of the next frames; each sample's previous
+    // camera is the one of the sample before it (GPURenderer.cpp:424-449)
     void set_camera(const MptCamera& camera);
+    const MptCamera& get_camera() const { return m_camera; }
+
+    // update_materials (GPURenderer.h:228, .cpp:1196-1200): material edits of the front-end's
+    // editor; re-uploaded and re-resolved (texture flags, material classes, light BVH)
+    void update_materials(std::vector<MptMaterial>& materials);
+    const std::vector<MptMaterial>& get_original_materials() const { return m_original_materials; }
+    const std::vector<MptMaterial>& get_current_materials() const { return m_current_materials; }
 
     // update (GPURenderer.cpp:236-262): one m_rng draw per displayed frame
     // (update_render_data, GPURenderer.cpp:980-983); resets sample_number when not accumulating
     void update();
-    // render (GPURenderer.cpp:408-456): the samples_per_frame loop of CameraRays, ReSTIR DI and
-    // FullPathTracer with the reference's seed draws; traced as batched wavefronts (mpt_render_frames)
+    // render (GPURenderer.cpp:408-456): per sample launch_camera_rays, launch_ReSTIR_DI,
+    // launch_path_tracing with the reference's seed draws; the samples_per_frame samples of one
+    // call are traced as batched wavefronts (mpt_render_frames)
     void render();
+    // The three launches of one sample (GPURenderer.cpp:465-486).  libmpt runs a sample's
+    // CameraRays, ReSTIR DI passes and path tracing as one launch set, so the first two draw
+    // their seeds into the render data and launch_path_tracing enqueues the whole sample (inside
+    // render(), the samples of the call are enqueued together at its end).
+    void launch_camera_rays();
+    void launch_ReSTIR_DI();
+    void launch_path_tracing();
     // reset (GPURenderer.cpp:953-973): restart the accumulation, m_rng re-seeded 42
     void reset();
     void synchronize_kernel();
     bool frame_render_done();
 
-    MptRenderSettings& get_render_settings() { return m_settings; }
-    MptWorldSettings& get_world_settings() { return m_world; }
-    MptKernelOptions& get_kernel_options() { return m_options; }   // KernelOptions.h macros, at run time
-    MptBSDFFlags& get_bsdf_flags() { return m_bsdf_flags; }
+    // map_buffers_for_render / unmap_buffers (GPURenderer.cpp:583-598) over the display
+    // buffers registered here (see DisplayBuffers)
+    void set_display_buffers(const DisplayBuffers& buffers) { m_display = buffers; }
+    void map_buffers_for_render();
+    void unmap_buffers();
+
+    MptRenderSettings& get_render_settings() { return m_render_data.render_settings; }
+    MptWorldSettings& get_world_settings() { return m_render_data.world_settings; }
+    MptKernelOptions& get_kernel_options() { return m_render_data.options; }   // KernelOptions.h macros, at run time
+    MptBSDFFlags& get_bsdf_flags() { return m_render_data.bsdf_flags; }
+    // get_render_data (GPURenderer.h:211): HIPRTRenderData's host-visible part -- settings,
+    // cameras, seeds, resolution -- as the frame record libmpt consumes (device buffers are
+    // libmpt's own; read them with get_framebuffer / get_aux_buffer)
+    MptFrame& get_render_data() { return m_render_data; }
     // copy_status_buffers / get_status_buffer_values (GPURenderer.cpp:269-283)
-    MptStatus get_status_buffer_values();
+    void copy_status_buffers();
+    const MptStatus& get_status_buffer_values() const { return m_status; }
     // the 'pixels' sum buffer and the denoiser AOVs (RenderData.h:32-36), host copy
     void get_framebuffer(int kind, float* dst_rgb);
+    // pixel_sample_count / pixel_converged_sample_count / pixel_squared_luminance
+    // (RenderData.h:62-84; get_pixels_converged_sample_count_buffer, GPURenderer.h:193), host copy
+    void get_aux_buffer(int kind, void* dst);
     int render_width() const { return m_width; }
     int render_height() const { return m_height; }
-    // the frames of the last render() (tests)
+    // the frames enqueued by the last render() / launch_path_tracing() (tests)
     const std::vector<MptFrame>& last_frames() const { return m_last_frames; }
 
 private:
     void check(int rc) const;
+    void flush();
 
     MptContext* m_ctx = nullptr;
     Xorshift32 m_rng{42};
     int m_width = 0, m_height = 0;
-    MptRenderSettings m_settings{};
-    MptWorldSettings m_world{};
-    MptKernelOptions m_options{};
-    MptBSDFFlags m_bsdf_flags{};
+    MptFrame m_render_data{};
     MptCamera m_camera{};
     MptCamera m_previous_frame_camera{};
     bool m_has_camera = false;
+    bool m_in_render = false;
+    bool m_has_envmap = false;
+    bool m_mapped = false;
+    std::string m_envmap_path;
+    DisplayBuffers m_display;
+    MptStatus m_status{};
+    std::vector<MptMaterial> m_original_materials, m_current_materials;
+    std::vector<MptFrame> m_pending;        // samples enqueued by the launches of this render()
     std::vector<MptFrame> m_last_frames;
 };
 

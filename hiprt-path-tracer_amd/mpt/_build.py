@@ -87,8 +87,10 @@ def build_host_test(verbose: bool = True) -> Path:
     deps = HOST_SOURCES + sorted(HOST_DIR.glob("*.h")) + [lib]
     if HOST_TEST.exists() and all(p.stat().st_mtime <= HOST_TEST.stat().st_mtime for p in deps):
         return HOST_TEST
-    cmd = ["g++", "-O2", "-std=c++17", f"-I{INCLUDE}", f"-I{HOST_DIR}", *map(str, HOST_SOURCES),
-           f"-L{PKG_DIR}", "-lmpt", "-Wl,-rpath,$ORIGIN/../mpt", "-Wl,-rpath,/opt/rocm/lib",
+    # the driver also calls the HIP runtime API itself (hipMalloc'd display buffers)
+    cmd = ["g++", "-O2", "-std=c++17", "-D__HIP_PLATFORM_AMD__", f"-I{INCLUDE}", f"-I{HOST_DIR}", "-I/opt/rocm/include",
+           *map(str, HOST_SOURCES), f"-L{PKG_DIR}", "-lmpt", "-L/opt/rocm/lib", "-lamdhip64",
+           "-Wl,-rpath,$ORIGIN/../mpt", "-Wl,-rpath,/opt/rocm/lib",
            "-Wl,-rpath-link,/opt/rocm/lib", "-o", str(HOST_TEST)]
     if verbose:
         print("[mpt build]", " ".join(cmd), file=sys.stderr)

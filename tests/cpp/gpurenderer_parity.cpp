@@ -1,7 +1,16 @@
 // Test driver (tests/test_host_cpp.py): the C++ GPURenderer mirror (hiprt-path-tracer_amd/host)
 // rendering a scene handed over as a raw blob by the test, through libmpt.
 // usage: gpurenderer_parity <in.blob> <out.bin>
-//   out.bin = int32 n_frames, MptFrame[n_frames] (every frame render() built), float sums[W*H*3]
+//   blob mode 0: RenderWindow's loop (update() then render()); mode 1: the same samples through
+//   the three launches called one by one (launch_camera_rays / launch_ReSTIR_DI /
+//   launch_path_tracing, the driver doing render()'s per-sample bookkeeping).  M2 > 0:
+//   update_materials with the blob's edited materials before rendering.  The colour comes back
+//   through the display-buffer path (map_buffers_for_render / unmap_buffers into hipMalloc'd
+//   destinations, as an OpenGL interop map would hand them over) and is checked against
+//   get_framebuffer; the per-pixel sample counts against the frames rendered.
+//   out.bin = int32 n_frames, MptFrame[n_frames] (every frame enqueued), float sums[W*H*3]
+#include <hip/hip_runtime_api.h>
+
 #include <cstdio>
 #include <cstring>
 #include <stdexcept>
@@ -35,6 +44,7 @@ int main(int argc, char** argv) {
         const auto camera = r.get<MptCamera>();
         const int W = r.get<int32_t>(), H = r.get<int32_t>(), n_updates = r.get<int32_t>();
         const int T = r.get<int32_t>(), V = r.get<int32_t>(), M = r.get<int32_t>(), E = r.get<int32_t>();
+        const int mode = r.get<int32_t>(), M2 = r.get<int32_t>();
         auto idx = r.arr<int32_t>(3 * (size_t)T);
         auto pos = r.arr<float>(3 * (size_t)V);
         auto nrm = r.arr<float>(3 * (size_t)V);
@@ -46,6 +56,7 @@ int main(int argc, char** argv) {
         const size_t lut_n[6] = {128 * 128, 128 * 64 * 128, 256 * 16 * 128, 256 * 16 * 128, 32 * 32 * 96, 32 * 32 * 3};
         std::vector<float> lut[6];
         for (int k = 0; k < 6; k++) lut[k] = r.arr<float>(lut_n[k]);
+        auto mats2 = r.arr<MptMaterial>((size_t)M2);
         fclose(fin);
 
         mpt_host::GPURenderer gr(0);
@@ -67,15 +78,57 @@ int main(int argc, char** argv) {
         gr.get_bsdf_flags() = flags;
         gr.set_camera(camera);
         gr.reset();
+        if (M2 > 0) {
+            gr.update_materials(mats2);
+            if (gr.get_current_materials().size() != (size_t)M2 || gr.get_original_materials().size() != (size_t)M)
+                throw std::runtime_error("material lists");
+        }
+        const size_t px = (size_t)W * H;
+        float* display = nullptr;
+        if (hipMalloc(&display, px * 3 * sizeof(float)) != hipSuccess) throw std::runtime_error("hipMalloc");
+        mpt_host::DisplayBuffers db;
+        db.color = display;
+        gr.set_display_buffers(db);
         std::vector<MptFrame> frames;
         for (int u = 0; u < n_updates; u++) {   // RenderWindow::render: update() then render() per displayed frame
             gr.update();
-            gr.render();
-            frames.insert(frames.end(), gr.last_frames().begin(), gr.last_frames().end());
+            if (mode == 0) {
+                gr.render();
+                frames.insert(frames.end(), gr.last_frames().begin(), gr.last_frames().end());
+            } else {
+                MptRenderSettings& rs = gr.get_render_settings();
+                const int spf = rs.samples_per_frame > 0 ? rs.samples_per_frame : 1;
+                gr.map_buffers_for_render();
+                for (int i = 1; i <= spf; i++) {
+                    if (i == spf) rs.do_update_status_buffers = true;
+                    gr.launch_camera_rays();
+                    gr.launch_ReSTIR_DI();
+                    gr.launch_path_tracing();
+                    frames.insert(frames.end(), gr.last_frames().begin(), gr.last_frames().end());
+                    rs.sample_number++;
+                    rs.denoiser_AOV_accumulation_counter++;
+                    rs.need_to_reset = false;
+                    rs.restir_di_settings.temporal_buffer_clear_requested = false;
+                }
+            }
+            gr.unmap_buffers();
         }
         gr.synchronize_kernel();
-        std::vector<float> img((size_t)W * H * 3);
-        gr.get_framebuffer(MPT_FB_COLOR, img.data());
+        if (gr.get_render_data().render_settings.sample_number != (int)frames.size())
+            throw std::runtime_error("render data sample_number");
+        std::vector<float> img(px * 3), direct(px * 3);
+        if (hipMemcpy(img.data(), display, px * 3 * sizeof(float), hipMemcpyDeviceToHost) != hipSuccess)
+            throw std::runtime_error("hipMemcpy");
+        (void)hipFree(display);
+        gr.get_framebuffer(MPT_FB_COLOR, direct.data());
+        if (std::memcmp(img.data(), direct.data(), px * 3 * sizeof(float)) != 0)
+            throw std::runtime_error("display buffer differs from get_framebuffer");
+        std::vector<int32_t> cnt(px);
+        gr.get_aux_buffer(MPT_AUX_SAMPLE_COUNT, cnt.data());
+        if (!gr.get_render_settings().enable_adaptive_sampling)
+            for (size_t i = 0; i < px; i++)
+                if (cnt[i] != (int32_t)frames.size()) throw std::runtime_error("pixel sample count");
+        gr.copy_status_buffers();
         MptStatus st = gr.get_status_buffer_values();
         FILE* fo = fopen(argv[2], "wb");
         if (!fo) throw std::runtime_error("cannot open output");

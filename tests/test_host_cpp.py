@@ -3,9 +3,11 @@ launch surface (GPURenderer.h:75-300) over the C ABI.  The test hands a scene + 
 front-end's settings to the C++ driver (tests/cpp/gpurenderer_parity.cpp) as a raw blob; the
 driver runs RenderWindow's loop (update() then render() per displayed frame, render()
 drawing the reference's seeds and tracing samples_per_frame samples through
-mpt_render_frames).  Checked: the frames it built carry exactly the seeds of
-mpt.scene.gpu_seed_schedule (the reference's m_rng order), and its image equals the CPU
-oracle's on those frames bit for bit."""
+mpt_render_frames), or the same samples through launch_camera_rays / launch_ReSTIR_DI /
+launch_path_tracing called one by one, optionally after update_materials; the image comes
+back through map_buffers_for_render / unmap_buffers into device buffers.  Checked: the
+frames it built carry exactly the seeds of mpt.scene.gpu_seed_schedule (the reference's m_rng
+order), and its image equals the CPU oracle's on those frames bit for bit."""
 import ctypes as C
 import os
 import struct
@@ -19,13 +21,13 @@ from mpt import _build, abi, scene
 W, H = 48, 32
 
 
-def _blob(path, sd, luts, settings, world, options, camera, n_updates):
+def _blob(path, sd, luts, settings, world, options, camera, n_updates, mode=0, mats2=()):
     with open(path, "wb") as f:
         f.write(struct.pack("<I", 0x4254504D))
         for s in (settings, world, options, abi.BSDFFlags.default(), camera):
             f.write(bytes(s))
         T, V = sd.num_triangles, len(sd.vertices)
-        f.write(struct.pack("<7i", W, H, n_updates, T, V, len(sd.materials), len(sd.emissive)))
+        f.write(struct.pack("<9i", W, H, n_updates, T, V, len(sd.materials), len(sd.emissive), mode, len(mats2)))
         f.write(np.ascontiguousarray(sd.triangle_indices, np.int32).tobytes())
         for a, t in ((sd.vertices, np.float32), (sd.normals, np.float32), (sd.has_normals, np.uint8),
                      (sd.texcoords, np.float32), (sd.material_indices, np.int32)):
@@ -34,6 +36,7 @@ def _blob(path, sd, luts, settings, world, options, camera, n_updates):
         f.write(np.ascontiguousarray(sd.emissive if len(sd.emissive) else np.zeros(1), np.int32).tobytes())
         for k in ("ggx_conductor", "glossy_dielectric", "ggx_glass", "ggx_glass_inverse", "ggx_thin_glass", "sheen_ltc"):
             f.write(np.ascontiguousarray(luts[k], np.float32).tobytes())
+        f.write(b"".join(bytes(m) for m in mats2))
 
 
 def _read_out(path):
@@ -57,7 +60,27 @@ CASES = {
     "ris_spf1": dict(lss=abi.LSS_RIS_BSDF_AND_LIGHT, spf=1, updates=3),
     "restir_fused": dict(lss=abi.LSS_RESTIR_DI, spf=1, updates=3),
     "restir_unfused_spf2": dict(lss=abi.LSS_RESTIR_DI, spf=2, updates=2, fused=False),
+    "split_launches_mis": dict(lss=abi.LSS_MIS_LIGHT_BSDF, spf=2, updates=2, mode=1),
+    "split_launches_restir": dict(lss=abi.LSS_RESTIR_DI, spf=1, updates=3, mode=1),
+    "update_materials_ris": dict(lss=abi.LSS_RIS_BSDF_AND_LIGHT, spf=2, updates=2, edit=True),
 }
+
+
+def _edited(sd):
+    """A material edit as the front-end's editor makes one: a wall turned glossy red metal, the
+    light brighter."""
+    mats = [abi.Material.from_buffer_copy(m) for m in sd.materials]
+    wall = int(sd.material_indices[0])
+    mats[wall].base_color = abi.Color(0.8, 0.1, 0.1)
+    mats[wall].metallic = 1.0
+    mats[wall].roughness = 0.3
+    for m in mats:
+        if m.emission_strength > 0:
+            m.emission_strength *= 1.5
+    for m in mats:
+        m.make_safe()
+        m.precompute_properties()
+    return mats
 
 
 @pytest.mark.gpu
@@ -72,7 +95,8 @@ def test_cpp_gpurenderer_matches_oracle(cornell, luts, tmp_path, case):
     opt.direct_light_sampling = c["lss"]
     cam = scene.make_camera(cornell.camera_info, W, H)
     blob, out = tmp_path / "in.blob", tmp_path / "out.bin"
-    _blob(blob, cornell, luts, st, abi.WorldSettings.default(), opt, cam, c["updates"])
+    mats2 = _edited(cornell) if c.get("edit") else []
+    _blob(blob, cornell, luts, st, abi.WorldSettings.default(), opt, cam, c["updates"], c.get("mode", 0), mats2)
     r = subprocess.run([str(_build.HOST_TEST), str(blob), str(out)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     frames, img = _read_out(out)
@@ -85,6 +109,11 @@ def test_cpp_gpurenderer_matches_oracle(cornell, luts, tmp_path, case):
         assert f.render_settings.sample_number == d["sample_number"]
         assert f.camera_random_seed == d["camera_random_seed"] and f.random_seed == d["random_seed"]
         assert list(f.restir_di_seeds) == list(d["restir_di_seeds"])
-    ref = orc.Oracle(cornell, luts).render(frames)
+    sd = cornell
+    if mats2:
+        import copy
+        sd = copy.copy(cornell)
+        sd.materials = mats2
+    ref = orc.Oracle(sd, luts).render(frames)
     assert np.array_equal(img, ref), f"{case}: {(img != ref).sum()} values differ"
     assert img.mean() > 0

@@ -77,3 +77,34 @@ def test_light_bvh_material_edit_and_no_lights(monkeypatch, luts):
             finally:
                 r.close()
         _assert_modes_equal(out, ref, "material edit")
+
+
+def test_light_bvh_too_deep_fallback(monkeypatch, luts):
+    """A light BVH too deep for the traversal stack (forced by the MPT_LIGHT_BVH_MAX_STACK
+    test hook) is dropped: light-hit queries take the exact whole-scene closest-hit path, so
+    the render is bit-exact against MPT_LIGHT_BVH=0 and the oracle, and a material edit in that
+    state still succeeds (and still falls back)."""
+    sd = scene.load_scene("cornell_pbr")
+    frs = frames(sd, 40, 24, 2, lss=abi.LSS_MIS_LIGHT_BSDF)
+    monkeypatch.setenv("MPT_LIGHT_BVH_MAX_STACK", "2")
+    out = _render_modes(monkeypatch, sd, luts, frs, var="MPT_LIGHT_BVH", modes=(0, 1))
+    _assert_modes_equal(out, oracle_for(sd, luts).render(frs, aov=True), "too-deep light BVH")
+    mats = [abi.Material.from_buffer_copy(m) for m in sd.materials]
+    wall = int(sd.material_indices[0])
+    mats[wall].emission = abi.Color(0.3, 0.2, 0.1)
+    mats[wall].emission_strength = 2.0
+    import copy
+    sd2 = copy.copy(sd)
+    sd2.materials = mats
+    r = mpt.GPURenderer(0)
+    try:
+        r.set_scene(sd)
+        r.set_luts(luts)
+        r.update_materials(mats)
+        for f in frs:
+            r.render(f)
+        r.synchronize_kernel()
+        img = r.framebuffer(abi.FB_COLOR)
+    finally:
+        r.close()
+    assert np.array_equal(img, oracle_for(sd2, luts).render(frs)), "material edit with a too-deep light BVH"
