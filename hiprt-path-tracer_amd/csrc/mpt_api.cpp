@@ -27,6 +27,14 @@ int fail(int code, const std::string& msg) {
     return code;
 }
 
+}  // namespace
+
+namespace mpt {
+int api_fail(int code, const char* msg) { return fail(code, msg); }   // for the library's other host files
+}  // namespace mpt
+
+namespace {
+
 #define HIPCHK(expr)                                                                                  \
     do {                                                                                              \
         hipError_t e_ = (expr);                                                                       \

@@ -29,7 +29,7 @@ SYMBOLS = [
     "mpt_render_frame", "mpt_render_frames", "mpt_synchronize", "mpt_query_done", "mpt_get_framebuffer", "mpt_partition_rows",
     "mpt_enable_stats", "mpt_get_stats", "mpt_trace_closest", "mpt_trace_any", "mpt_clear_status",
     "mpt_query_status", "mpt_get_aux_buffer", "mpt_build_envmap_cdf", "mpt_set_envmap_cdf", "mpt_set_halo_exchange",
-    "mpt_bake_lut",
+    "mpt_bake_lut", "mpt_png_unfilter",
 ]
 
 
@@ -81,6 +81,7 @@ def lib() -> C.CDLL:
     L.mpt_get_stats.argtypes = [vp, C.POINTER(abi.Stats)]
     L.mpt_trace_closest.argtypes = [vp, vp, vp, i32, vp, vp, vp, vp, C.c_int]
     L.mpt_trace_any.argtypes = [vp, vp, vp, i32, vp, C.c_int]
+    L.mpt_png_unfilter.argtypes = [vp, C.c_int64, vp, i32, i32, i32]
     L.mpt_build_envmap_cdf.argtypes = [vp, i32, i32, vp, vp]
     L.mpt_set_envmap_cdf.argtypes = [vp, vp, f32]
     L.mpt_clear_status.argtypes = [vp]

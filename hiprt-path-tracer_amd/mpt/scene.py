@@ -13,18 +13,33 @@ importer that the reference consumes:
   ``make_safe`` + ``precompute_properties`` (HostDeviceCommon/Material.h:44-71);
 * the emissive triangle list of ``ThreadFunctions::load_scene_parse_emissive_triangles``
   (Threads/ThreadFunctions.cpp:116-143);
+* the textures of ``SceneParser::prepare_textures`` / ``get_textures_paths_and_indices`` /
+  ``assign_material_texture_indices`` (SceneParser.cpp:278-347, 409-455) and
+  ``ThreadFunctions::load_scene_texture`` (ThreadFunctions.cpp:30-97): per material, in the
+  order base colour, emission, roughness-metallic, specular, coat, sheen, transmission,
+  normal map, each decoded (mpt/image.py: PNG) with the channel count the reference asks
+  stb_image for, and a constant emissive texture folded into the material's emission
+  (``CONSTANT_EMISSIVE_TEXTURE``);
 * the camera of ``SceneParser::parse_camera`` (SceneParser.cpp:222-276) and
   ``Camera::to_hiprt`` / ``get_view_matrix`` (Scene/Camera.cpp:9-45), including the
   reference's '+0.425 rad' vertical-FOV term and its matrix conventions.
 
 ASSIMP's own conversions (glTF yfov -> mHorizontalFOV = yfov * aspect, default
-material values) are assumptions of this restatement; they only
+material values, the glTF2 importer's texture types: baseColorTexture -> BASE_COLOR,
+metallicRoughnessTexture -> METALNESS and DIFFUSE_ROUGHNESS with one path,
+KHR_materials_specular.specularTexture -> SPECULAR, clearcoatTexture -> CLEARCOAT,
+sheenColorTexture -> SHEEN, transmissionTexture -> TRANSMISSION, its V flip of texture
+coordinates, v -> 1 - v) are assumptions of this restatement; they only
 decide which scene is rendered, not the renderer's parity, since the oracle and the
-HIP path consume the same arrays.
+HIP path consume the same arrays.  One deliberate superset: embedded images (data URIs,
+bufferViews, .glb) are decoded; the reference hands ASSIMP's '*N' embedded-texture names to
+stb_image as file paths, which fails and leaves an empty texture.
 """
+import base64
 import json
 import math
 import os
+import struct
 
 import numpy as np
 
@@ -145,9 +160,13 @@ def _accessor(g, bins, idx):
     return np.array(arr)
 
 
-def _material_from_gltf(gm):
-    """SceneParser::read_material_properties on ASSIMP's glTF2 material keys."""
+def _material_from_gltf(gm, tex=None):
+    """SceneParser::read_material_properties on ASSIMP's glTF2 material keys.  tex: the
+    material's texture indices (assigned before the properties are read, SceneParser.cpp:73-80,
+    so a material with an emission texture keeps the default black emission)."""
     m = abi.Material.default()
+    for k, v in (tex or {}).items():
+        setattr(m, k, v)
     pbr = gm.get("pbrMetallicRoughness", {})
     bc = pbr.get("baseColorFactor", [1.0, 1.0, 1.0, 1.0])
     m.base_color = abi.Color(*bc[:3])
@@ -190,15 +209,119 @@ def _material_from_gltf(gm):
     return m
 
 
+# Texture slots in the order SceneParser::get_textures_paths_and_indices reads them
+# (SceneParser.cpp:409-455), with the glTF texture that ASSIMP's glTF2 importer files under
+# that aiTextureType and the channel count load_scene_texture asks stb_image for
+# (ThreadFunctions.cpp:44-83; roughness + metallic share one path -> the packed 3-channel slot).
+_TEX_SLOTS = [
+    ("base_color_texture_index", lambda gm, e: gm.get("pbrMetallicRoughness", {}).get("baseColorTexture"), 4),
+    ("emission_texture_index", lambda gm, e: gm.get("emissiveTexture"), 4),
+    ("roughness_metallic_texture_index", lambda gm, e: gm.get("pbrMetallicRoughness", {}).get("metallicRoughnessTexture"), 3),
+    ("specular_texture_index", lambda gm, e: e.get("KHR_materials_specular", {}).get("specularTexture"), 1),
+    ("coat_texture_index", lambda gm, e: e.get("KHR_materials_clearcoat", {}).get("clearcoatTexture"), 1),
+    ("sheen_texture_index", lambda gm, e: e.get("KHR_materials_sheen", {}).get("sheenColorTexture"), 1),
+    ("specular_transmission_texture_index", lambda gm, e: e.get("KHR_materials_transmission", {}).get("transmissionTexture"), 1),
+    ("normal_map_texture_index", lambda gm, e: gm.get("normalTexture"), 4),
+]
+CONSTANT_EMISSIVE_TEXTURE = -2   # RendererMaterial::CONSTANT_EMISSIVE_TEXTURE (Material.h:236-237)
+
+
+def _read_glb(path):
+    """Binary glTF: the JSON chunk and the BIN chunk (buffer 0)."""
+    with open(path, "rb") as f:
+        data = f.read()
+    magic, version, length = struct.unpack_from("<4sII", data, 0)
+    if magic != b"glTF" or version != 2:
+        raise ValueError(f"{path}: not a glTF 2 binary")
+    pos, g, binchunk = 12, None, None
+    while pos + 8 <= min(length, len(data)):
+        n, kind = struct.unpack_from("<I4s", data, pos)
+        body = data[pos + 8:pos + 8 + n]
+        if kind == b"JSON":
+            g = json.loads(body.decode("utf-8"))
+        elif kind == b"BIN\x00":
+            binchunk = body
+        pos += 8 + n
+    if g is None:
+        raise ValueError(f"{path}: GLB without a JSON chunk")
+    return g, binchunk
+
+
+def _uri_bytes(base, uri):
+    if uri.startswith("data:"):
+        return base64.b64decode(uri.split(",", 1)[1])
+    # SceneParser::normalize_texture_paths (SceneParser.cpp:476-494): '%20' -> ' '
+    with open(os.path.join(base, uri.replace("%20", " ")), "rb") as f:
+        return f.read()
+
+
+def _image_bytes(g, bins, base, image_index):
+    im = g["images"][image_index]
+    if "uri" in im:
+        return _uri_bytes(base, im["uri"])
+    bv = g["bufferViews"][im["bufferView"]]
+    off = bv.get("byteOffset", 0)
+    return bytes(bins[bv["buffer"]][off:off + bv["byteLength"]])
+
+
+def _load_textures(g, bins, base, materials_json):
+    """SceneParser::prepare_textures + assign_material_texture_indices + the texture-loading
+    threads (ThreadFunctions::load_scene_texture): per material, its textures in slot order
+    (global index = the material's offset + its local index), decoded with the slot's channel
+    count, an emission texture of constant colour (stb values within 5 of the first texel,
+    Image8Bit::is_constant_color(5), Image.cpp:250-271) folded into the material (emission =
+    its texel sampled at uv (0, 0), i.e. the bottom-left texel / 255, Image.cpp:161-193) and
+    replaced by CONSTANT_EMISSIVE_TEXTURE.  Returns (per-material {slot: index},
+    per-material constant emission or None, textures as RGBA8, per-material texture count)."""
+    from . import image
+    tex_idx, const_em, textures, per_mat = [], [], [], []
+    cache = {}
+    for gm in materials_json:
+        ext = gm.get("extensions", {})
+        slots, em = {}, None
+        n0 = len(textures)
+        for slot, get, channels in _TEX_SLOTS:
+            info = get(gm, ext)
+            if not info or "index" not in info:
+                continue
+            src = g["textures"][info["index"]].get("source")
+            if src is None:
+                continue
+            key = (src, channels)
+            if key not in cache:
+                try:
+                    cache[key] = image.read_image(_image_bytes(g, bins, base, src), channels)
+                except (OSError, ValueError) as e:
+                    raise ValueError(f"texture {g['images'][src].get('uri', src)!r} ({slot}): {e}") from None
+            img = cache[key]
+            if slot == "emission_texture_index":
+                first = img[0, 0].astype(np.int32)
+                if np.all(np.abs(img.astype(np.int32) - first) <= 5):
+                    slots[slot] = CONSTANT_EMISSIVE_TEXTURE
+                    em = img[-1, 0, :3].astype(np.float32) / np.float32(255.0)
+                    textures.append(np.array([[[0, 0, 0, 255]]], np.uint8))   # the slot stays, never read
+                    continue
+            slots[slot] = len(textures)
+            textures.append(image.to_rgba8(img))
+        tex_idx.append(slots)
+        const_em.append(em)
+        per_mat.append(len(textures) - n0)
+    return tex_idx, const_em, textures, per_mat
+
+
 def load_gltf(path, aspect_override=None):
-    """Loads a .gltf (+ .bin) into SceneData."""
-    with open(path) as f:
-        g = json.load(f)
+    """Loads a .gltf (+ .bin, + textures) or a .glb into SceneData."""
     base = os.path.dirname(path)
     bins = []
-    for b in g.get("buffers", []):
-        with open(os.path.join(base, b["uri"]), "rb") as f:
-            bins.append(f.read())
+    if path.endswith(".glb"):
+        g, binchunk = _read_glb(path)
+        for k, b in enumerate(g.get("buffers", [])):
+            bins.append(binchunk if "uri" not in b and k == 0 else _uri_bytes(base, b["uri"]))
+    else:
+        with open(path) as f:
+            g = json.load(f)
+        for b in g.get("buffers", []):
+            bins.append(_uri_bytes(base, b["uri"]))
 
     # world transforms
     world = {}
@@ -249,9 +372,14 @@ def load_gltf(path, aspect_override=None):
             inst.append((mi, pos, nrm, uv, idx.reshape(-1, 3)))
 
     total_mats = n_mat + (1 if need_default else 0)
-    mats = [_material_from_gltf(gm) for gm in materials_json]
+    tex_idx, const_em, textures, tex_count = _load_textures(g, bins, base, materials_json)
+    mats = [_material_from_gltf(gm, t) for gm, t in zip(materials_json, tex_idx)]
+    for m, em in zip(mats, const_em):
+        if em is not None:      # Material::set_emission after the texture thread (ThreadFunctions.cpp:87-93)
+            m.emission = abi.Color(*[float(x) for x in em])
     if need_default:
         mats.append(_material_from_gltf({}))
+        tex_count.append(0)
 
     sd = SceneData()
     sd.name = os.path.splitext(os.path.basename(path))[0]
@@ -266,8 +394,12 @@ def load_gltf(path, aspect_override=None):
             verts.append(pos)
             nrms.append(nrm if nrm is not None else np.zeros_like(pos))
             hasn.append(np.full(len(pos), 1 if nrm is not None else 0, np.uint8))
-            # texcoords only kept when the material has textures (SceneParser.cpp:136-141)
-            uvs.append(np.zeros((len(pos), 2), np.float32))
+            # texcoords only kept when the material has textures (SceneParser.cpp:136-141),
+            # V flipped by ASSIMP's glTF2 importer
+            if uv is not None and tex_count[mi] > 0:
+                uvs.append(np.stack([uv[:, 0], np.float32(1.0) - uv[:, 1]], 1).astype(np.float32))
+            else:
+                uvs.append(np.zeros((len(pos), 2), np.float32))
             mids.append(np.full(len(idx), mi, np.int32))
             voff += len(pos)
     sd.triangle_indices = np.concatenate(tri).astype(np.int32).ravel()
@@ -277,6 +409,7 @@ def load_gltf(path, aspect_override=None):
     sd.texcoords = np.concatenate(uvs)
     sd.material_indices = np.concatenate(mids)
     sd.materials = mats
+    sd.textures = textures
 
     cams = [(ni, n) for ni, n in enumerate(g["nodes"]) if "camera" in n and ni in world]
     if cams:
@@ -294,7 +427,8 @@ def load_gltf(path, aspect_override=None):
 
 def load_scene(name):
     """Loads a scene shipped in data/scenes (copied from the reference's data/GLTFs)."""
-    return load_gltf(os.path.join(DATA_DIR, "scenes", name + ".gltf"))
+    p = os.path.join(DATA_DIR, "scenes", name + ".gltf")
+    return load_gltf(p if os.path.exists(p) else p[:-5] + ".glb")
 
 
 # ----------------------------------------------------------------------------------

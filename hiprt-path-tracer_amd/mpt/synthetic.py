@@ -429,3 +429,160 @@ def with_textured_panels(sd: SceneData, seed: int = 3) -> SceneData:
     out.camera_info = sd.camera_info
     out.name = sd.name + "+textured_panels"
     return out.finalize()
+
+
+def write_textured_gltf(dirpath: str, seed: int = 5, glb: bool = False) -> str:
+    """Writes a small textured glTF 2 scene (the ingestion test asset: the reference's one
+    textured scene, the-white-room-low.gltf, ships without its geometry) and returns its path.
+
+    A floor and a back wall under an emissive ceiling quad, two panels in front:
+    * floor: base colour (RGB PNG in a file whose name has a space, referenced as '%20'),
+      metallicRoughnessTexture (RGB), normalTexture (RGBA, Adam7-interlaced);
+    * back wall: untextured (its texture coordinates are dropped, SceneParser.cpp:136-141);
+    * left panel: an emission texture with texel variation (emissiveFactor 1, strength 2),
+      KHR_materials_specular.specularTexture (RGB: stb's grey conversion), clearcoatTexture
+      (grey + alpha);
+    * right panel: a near-constant emission texture (every texel within 5 of the first: folded
+      into the material's emission, Image8Bit::is_constant_color(5)), sheenColorTexture in a
+      data: URI, transmissionTexture as a palette PNG with tRNS;
+    * ceiling: emissiveFactor 5, no texture.
+    glb=True writes one .glb with every image in a bufferView."""
+    import base64
+    import json
+    import os
+    import struct
+
+    from . import image
+    rng = np.random.default_rng(seed)
+    S = 16
+
+    def noise(c, lo=0, hi=256, size=S):
+        return rng.integers(lo, hi, (size, size, c)).astype(np.uint8)
+
+    nrm = rng.normal(size=(S, S, 3)) * np.array([0.3, 0.3, 0.0]) + np.array([0.0, 0.0, 1.0])
+    nrm /= np.linalg.norm(nrm, axis=-1, keepdims=True)
+    nrm_img = np.concatenate([np.clip(np.round((nrm * 0.5 + 0.5) * 255), 0, 255).astype(np.uint8),
+                              np.full((S, S, 1), 255, np.uint8)], -1)
+    em_const = np.clip(np.array([200, 150, 90], np.int32) + rng.integers(-2, 3, (S, S, 3)), 0, 255).astype(np.uint8)
+    em_var = np.where(rng.random((S, S, 1)) < 0.4, noise(3, 100, 256), 0).astype(np.uint8)
+    pal = np.concatenate([rng.integers(0, 256, (6, 3)), np.array([[255], [128], [0], [255], [60], [255]])], 1)
+    images = {
+        "floor base.png": image.encode_png(noise(3, 40, 256)),
+        "floor_mr.png": image.encode_png(np.concatenate([noise(1), noise(1, 20, 230), noise(1, 0, 256)], -1)),
+        "floor_normal.png": image.encode_png(nrm_img, interlace=True),
+        "left_emission.png": image.encode_png(em_var),
+        "left_specular.png": image.encode_png(noise(3, 30, 256)),
+        "left_coat.png": image.encode_png(noise(2, 0, 256)),
+        "right_emission.png": image.encode_png(em_const),
+        "right_sheen.png": image.encode_png(noise(3, 0, 256)),
+        "right_transmission.png": image.encode_png(rng.integers(0, 6, (S, S)).astype(np.uint8), palette=pal),
+    }
+    names = list(images)
+
+    # geometry: quads (4 vertices, 2 triangles), positions / normals / uvs
+    quads = [
+        # (corner, edge u, edge v, normal, material)
+        ((-1.0, 0.0, 1.0), (2.0, 0.0, 0.0), (0.0, 0.0, -2.0), (0, 1, 0), 0),     # floor
+        ((-1.0, 0.0, -1.0), (2.0, 0.0, 0.0), (0.0, 2.0, 0.0), (0, 0, 1), 1),     # back wall
+        ((-0.9, 0.3, -0.4), (0.7, 0.0, 0.2), (0.0, 0.9, 0.0), (-0.275, 0, 0.962), 2),  # left panel
+        ((0.2, 0.3, -0.3), (0.7, 0.0, -0.2), (0.0, 0.9, 0.0), (0.275, 0, 0.962), 3),   # right panel
+        ((-0.3, 1.99, -0.3), (0.6, 0.0, 0.0), (0.0, 0.0, 0.6), (0, -1, 0), 4),   # ceiling light
+    ]
+    bin_parts, views, accessors, meshes, nodes = [], [], [], [], []
+
+    def add_view(data: bytes, target=None):
+        off = sum(len(b) for b in bin_parts)
+        pad = (-off) % 4
+        if pad:
+            bin_parts.append(b"\0" * pad)
+            off += pad
+        bin_parts.append(data)
+        v = {"buffer": 0, "byteOffset": off, "byteLength": len(data)}
+        if target:
+            v["target"] = target
+        views.append(v)
+        return len(views) - 1
+
+    def add_acc(arr, ctype, typ, target):
+        arr = np.ascontiguousarray(arr)
+        a = {"bufferView": add_view(arr.tobytes(), target), "componentType": ctype, "count": int(arr.shape[0]), "type": typ}
+        if typ == "VEC3" and ctype == 5126:
+            a["min"], a["max"] = arr.min(0).tolist(), arr.max(0).tolist()
+        accessors.append(a)
+        return len(accessors) - 1
+
+    for k, (p0, eu, ev, n, mat) in enumerate(quads):
+        p0, eu, ev = np.array(p0), np.array(eu), np.array(ev)
+        P = np.array([p0, p0 + eu, p0 + eu + ev, p0 + ev], np.float32)
+        N = np.tile(np.array(n, np.float64) / np.linalg.norm(n), (4, 1)).astype(np.float32)
+        UV = np.array([[0, 1], [1, 1], [1, 0], [0, 0]], np.float32) * np.float32(1.5 if k == 0 else 1.0)
+        I = np.array([0, 1, 2, 0, 2, 3], np.uint16)
+        prim = {"attributes": {"POSITION": add_acc(P, 5126, "VEC3", 34962), "NORMAL": add_acc(N, 5126, "VEC3", 34962),
+                               "TEXCOORD_0": add_acc(UV, 5126, "VEC2", 34962)},
+                "indices": add_acc(I, 5123, "SCALAR", 34963), "material": mat}
+        meshes.append({"primitives": [prim]})
+        nodes.append({"mesh": k})
+    nodes.append({"camera": 0, "translation": [0.0, 1.0, 3.2]})
+
+    def tex(name):
+        return {"index": names.index(name)}
+    materials = [
+        {"name": "floor", "pbrMetallicRoughness": {"baseColorTexture": tex("floor base.png"), "metallicRoughnessTexture":
+                                                  tex("floor_mr.png"), "roughnessFactor": 0.6, "metallicFactor": 0.5},
+         "normalTexture": tex("floor_normal.png")},
+        {"name": "wall", "pbrMetallicRoughness": {"baseColorFactor": [0.7, 0.65, 0.6, 1.0], "metallicFactor": 0.0,
+                                                 "roughnessFactor": 0.8}},
+        {"name": "left", "pbrMetallicRoughness": {"baseColorFactor": [0.5, 0.6, 0.7, 1.0], "metallicFactor": 0.0,
+                                                 "roughnessFactor": 0.4},
+         "emissiveTexture": tex("left_emission.png"), "emissiveFactor": [1.0, 1.0, 1.0],
+         "extensions": {"KHR_materials_emissive_strength": {"emissiveStrength": 2.0},
+                        "KHR_materials_specular": {"specularFactor": 0.8, "specularTexture": tex("left_specular.png")},
+                        "KHR_materials_clearcoat": {"clearcoatFactor": 0.7, "clearcoatRoughnessFactor": 0.2,
+                                                    "clearcoatTexture": tex("left_coat.png")}}},
+        {"name": "right", "pbrMetallicRoughness": {"baseColorFactor": [0.8, 0.5, 0.4, 1.0], "metallicFactor": 0.0,
+                                                  "roughnessFactor": 0.5},
+         "emissiveTexture": tex("right_emission.png"), "emissiveFactor": [1.0, 1.0, 1.0],
+         "extensions": {"KHR_materials_sheen": {"sheenColorFactor": [0.9, 0.8, 0.7], "sheenRoughnessFactor": 0.4,
+                                                "sheenColorTexture": tex("right_sheen.png")},
+                        "KHR_materials_transmission": {"transmissionFactor": 0.3,
+                                                       "transmissionTexture": tex("right_transmission.png")}}},
+        {"name": "light", "pbrMetallicRoughness": {"baseColorFactor": [1, 1, 1, 1], "metallicFactor": 0.0},
+         "emissiveFactor": [1.0, 1.0, 1.0], "extensions": {"KHR_materials_emissive_strength": {"emissiveStrength": 5.0}}},
+    ]
+    imgs = []
+    for nm in names:
+        if glb:
+            imgs.append({"bufferView": add_view(images[nm]), "mimeType": "image/png"})
+        elif nm == "right_sheen.png":
+            imgs.append({"uri": "data:image/png;base64," + base64.b64encode(images[nm]).decode()})
+        else:
+            imgs.append({"uri": nm.replace(" ", "%20")})
+    binary = b"".join(bin_parts)
+    g = {"asset": {"version": "2.0"}, "scene": 0, "scenes": [{"nodes": list(range(len(nodes)))}], "nodes": nodes,
+         "meshes": meshes, "materials": materials, "accessors": accessors, "bufferViews": views,
+         "textures": [{"source": i} for i in range(len(names))], "images": imgs,
+         "cameras": [{"type": "perspective", "perspective": {"yfov": 0.75, "aspectRatio": 1.0, "znear": 0.05, "zfar": 50.0}}],
+         "extensionsUsed": ["KHR_materials_emissive_strength", "KHR_materials_specular", "KHR_materials_clearcoat",
+                            "KHR_materials_sheen", "KHR_materials_transmission"]}
+    os.makedirs(dirpath, exist_ok=True)
+    if glb:
+        g["buffers"] = [{"byteLength": len(binary)}]
+        js = json.dumps(g).encode()
+        js += b" " * ((-len(js)) % 4)
+        binary += b"\0" * ((-len(binary)) % 4)
+        body = struct.pack("<I4s", len(js), b"JSON") + js + struct.pack("<I4s", len(binary), b"BIN\0") + binary
+        path = os.path.join(dirpath, "textured_room.glb")
+        with open(path, "wb") as f:
+            f.write(struct.pack("<4sII", b"glTF", 2, 12 + len(body)) + body)
+        return path
+    g["buffers"] = [{"uri": "textured_room.bin", "byteLength": len(binary)}]
+    with open(os.path.join(dirpath, "textured_room.bin"), "wb") as f:
+        f.write(binary)
+    for nm in names:
+        if nm != "right_sheen.png":
+            with open(os.path.join(dirpath, nm), "wb") as f:
+                f.write(images[nm])
+    path = os.path.join(dirpath, "textured_room.gltf")
+    with open(path, "w") as f:
+        json.dump(g, f)
+    return path

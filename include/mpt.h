@@ -589,6 +589,14 @@ int mpt_trace_closest(MptContext* ctx, const float* rays, const int32_t* last_hi
 int mpt_trace_any(MptContext* ctx, const float* rays, const int32_t* last_hit, int32_t n,
                   uint8_t* out_occluded, int pointers_are_device);
 
+/* Host helper of the glTF texture loader (mpt/image.py; the reference decodes textures with
+ * stb_image in Image8Bit::read_image, Image.cpp:33-61): reverses the PNG scanline filters
+ * (None / Sub / Up / Average / Paeth) of `rows` inflated rows, each a filter-type byte
+ * followed by row_bytes bytes, into out (rows * row_bytes).  bpp = bytes per complete pixel
+ * (rounded up to 1).  No context, no GPU. */
+int mpt_png_unfilter(const uint8_t* filtered, int64_t filtered_size, uint8_t* out, int32_t rows, int32_t row_bytes,
+                     int32_t bpp);
+
 #ifdef __cplusplus
 }
 #endif

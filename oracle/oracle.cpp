@@ -21,8 +21,8 @@
  *   adaptive sampling ..... src/Device/includes/AdaptiveSampling.h:11-104, CameraRays.h:88-125
  *   alpha testing ......... FilterFunction.h:19-48 (accept probability alpha_opacity x base-colour
  *                           alpha, the candidate's uniform hashed from (query, primitive))
- *   ReSTIR DI ............. kernels/ReSTIR/DI/*.h, includes/ReSTIR/DI/*.h (oracle_restir.h)
- *   BSDFs ................. includes/BSDFs/*.h (oracle_bsdf.h)
+ *   ReSTIR DI ............. the headers of kernels/ReSTIR/DI/ and includes/ReSTIR/DI/ (oracle_restir.h)
+ *   BSDFs ................. the headers of includes/BSDFs/ (oracle_bsdf.h)
  *
  * Differences from the reference, all deliberate and documented in DESIGN.md §2:
  *   * the octree/k-DOP BVH is replaced by a binned-SAH BVH2 (same closest-hit
