@@ -129,6 +129,7 @@ struct MptContext {
     // material-class shading (k_split / k_shade): 1 on (default), 0 off, 2 on with every
     // plain vertex deferred to the generic kernel (test hook); MPT_SHADE_CLASSES at mpt_create
     int shade_classes = 1;
+    int restir_staged = 1;                // ReSTIR DI reuse passes staged around their rays (MPT_RESTIR_STAGED)
     std::vector<MptMaterial> h_mats;
     std::vector<int32_t> h_mat_idx;       // per triangle (alpha flags of the triangle records)
     std::vector<uint8_t> h_tex_alpha;     // per texture: some texel has alpha < 255
@@ -164,6 +165,12 @@ struct MptContext {
     DBuf<MptMaterial> gb_mat, pgb_mat;
     DBuf<float4> rs_init, rs_sp1, rs_sp2, rs_plights;
     DBuf<int32_t> rs_conv;
+    // staged ReSTIR DI passes (DevPaths::rq_*): RS_RPP ray positions per pixel slot
+    DBuf<float4> rq_o, rq_d, rq_rec;
+    DBuf<uint32_t> rq_key;
+    DBuf<uint8_t> rq_occ;
+    DBuf<int32_t> rq_list;
+    DBuf<int4> rq_meta;
     int restir_out_sp2 = 0;
     MptHaloExchangeFn halo_fn = nullptr;   // ReSTIR DI across a row partition
     void* halo_user = nullptr;
@@ -311,6 +318,8 @@ DevPaths dev_paths(MptContext* c) {
     P.x_iter = c->x_iter;
     P.xq_o = c->xq_o.p; P.xq_d = c->xq_d.p; P.xq_hit = c->xq_hit.p; P.xq_occ = c->xq_occ.p; P.xq_flag = c->xq_flag.p;
     P.xrec = c->xrec.p; P.xl_any = c->xl_any.p; P.xl_cl = c->xl_cl.p; P.xl_light = c->xl_light.p;
+    P.rq_o = c->rq_o.p; P.rq_d = c->rq_d.p; P.rq_key = c->rq_key.p; P.rq_occ = c->rq_occ.p; P.rq_list = c->rq_list.p;
+    P.rq_meta = c->rq_meta.p; P.rq_rec = c->rq_rec.p;
     return P;
 }
 
@@ -549,7 +558,7 @@ int build_light_bvh(MptContext* c) {
 void release_restir(MptContext* c) {
     release_all(c->gb_pos, c->gb_sn, c->gb_gn, c->gb_view, c->pgb_pos, c->pgb_sn, c->pgb_gn, c->pgb_view, c->gb_meta,
                 c->pgb_meta, c->gb_vsA, c->gb_vsB, c->pgb_vsA, c->pgb_vsB, c->gb_mat, c->pgb_mat, c->rs_init, c->rs_sp1,
-                c->rs_sp2, c->rs_plights, c->rs_conv);
+                c->rs_sp2, c->rs_plights, c->rs_conv, c->rq_o, c->rq_d, c->rq_rec, c->rq_key, c->rq_occ, c->rq_list, c->rq_meta);
     c->restir_out_sp2 = 0;
 }
 
@@ -586,6 +595,15 @@ int ensure_restir(MptContext* c, const MptFrame* f) {
     if (c->band_c > 1 && c->rs_conv.n != N) {
         A(c->rs_conv, N);
         if (A.e == hipSuccess) A(hipMemsetAsync(c->rs_conv.p, 0xff, N * sizeof(int32_t), st));
+    }
+    if (c->restir_staged) {
+        // staged reuse passes: per pixel slot of the partition (ReSTIR frames trace one sample)
+        const size_t ns = (size_t)std::max(c->n_slots, 1);
+        if (c->rq_meta.n != ns) {
+            A(c->rq_o, ns * RS_RPP_HOST); A(c->rq_d, ns * RS_RPP_HOST); A(c->rq_key, ns * RS_RPP_HOST);
+            A(c->rq_occ, ns * RS_RPP_HOST); A(c->rq_list, ns * RS_RPP_HOST);
+            A(c->rq_meta, ns); A(c->rq_rec, ns * RS_KMAX_HOST);
+        }
     }
     if (c->rs_plights.n != 4 * npl) {
         A(c->rs_plights, 4 * npl);
@@ -772,6 +790,7 @@ int mpt_create(int device, void* hip_stream, MptContext** out) {
     if (device < 0 || device >= ndev) return fail(MPT_ERR_INVALID_ARGUMENT, "device index out of range");
     MptContext* c = new MptContext();   // value-initialised: every handle starts null
     if (const char* e = std::getenv("MPT_SHADE_CLASSES")) c->shade_classes = std::atoi(e);
+    if (const char* e = std::getenv("MPT_RESTIR_STAGED")) c->restir_staged = std::atoi(e);
     if (const char* e = std::getenv("MPT_LIGHT_BVH")) c->light_bvh = std::atoi(e);
     if (const char* e = std::getenv("MPT_OVERLAP")) c->overlap = std::atoi(e);
     if (const char* e = std::getenv("MPT_LIGHT_BVH_MAX_STACK")) c->light_bvh_max_stack = std::atoi(e);
@@ -1135,6 +1154,7 @@ static int launch_batch(MptContext* c, const MptFrame* f, int batch) {
     cfg.ev_used = 0;
     cfg.restir_out_sp2 = c->restir_out_sp2;
     cfg.shade_classes = c->shade_classes;
+    cfg.restir_staged = c->restir_staged;
     cfg.light_bvh = c->light_bvh && c->light_bvh_ok;
     cfg.light_static = !c->h_light_prims.empty() && 2 * c->bvh_light.depth + 2 <= TRAV_LDS_STACK;
     if (restir_part) {

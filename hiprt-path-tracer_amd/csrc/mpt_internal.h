@@ -194,9 +194,22 @@ struct DevPaths {
     int32_t* xl_any;          // compacted ext query lists (entries), CTR_XANY / CTR_XCL / CTR_XLIGHT
     int32_t* xl_cl;
     int32_t* xl_light;
+    // staged ReSTIR DI reuse passes (restir_di.h, RS_RPP ray positions per pixel slot): rays
+    // (xyz + last hit bits / xyz + t_max), their alpha keys and any-hit results, the compacted
+    // ray list (CTR_RQ, then the visibility-reuse rays CTR_RQV), per-pixel pass metadata and
+    // per-neighbour records
+    float4* rq_o;
+    float4* rq_d;
+    uint32_t* rq_key;
+    uint8_t* rq_occ;
+    int32_t* rq_list;
+    int4* rq_meta;
+    float4* rq_rec;
 };
 
 constexpr int N_TRACE_MODES = 5;
+// staged ReSTIR DI reuse passes (restir_di.h RS_KMAX / RS_RPP): neighbours per pass, ray positions per pixel
+constexpr int RS_KMAX_HOST = 5, RS_RPP_HOST = 2 * RS_KMAX_HOST;
 constexpr int N_RAY_COUNTS = 5;   // DevPaths::ray_counts
 // timed kernel kinds: 0..2 = traversal stages (trace modes), then the others
 enum { KT_CAMERA = 3, KT_SHADE = 4, KT_RESOLVE = 5, KT_ACCUMULATE = 6, KT_COMPACT = 7, KT_RESTIR = 8, KT_SPLIT = 9,
@@ -219,7 +232,8 @@ enum {
     CTR_DEFER = 9,            // plain-class hits deferred to the generic queue (tombstones in qh)
     CTR_LIGHT = 10,           // length of nq_light (k_trace TM_NEE_LIGHT)
     CTR_XANY = 11, CTR_XCL = 12, CTR_XLIGHT = 13,   // ext query lists (extended light sampling)
-    CTR_COUNT = 16
+    CTR_RQ = 14, CTR_RQV = 15,                      // staged ReSTIR DI rays / visibility-reuse rays
+    CTR_COUNT = 20
 };
 
 // launch glue (mpt_kernels.hip)
@@ -243,6 +257,7 @@ struct LaunchCfg {
     int shade_classes;        // material-class shading: 0 off, 1 on, 2 on + defer every plain vertex (test hook)
     int light_bvh;            // light-hit queries through the light BVH (1) or one closest-hit traversal (0)
     int light_static;         // the light BVH's traversal stack fits in LDS (one query per lane, no spill)
+    int restir_staged;        // ReSTIR DI reuse passes staged around their rays (restir_di.h), when supported
     // overlapped batch halves (mpt_api.cpp launch_batch): recorded after the bounce-0 path
     // traversal / after k_accumulate; waited for before k_accumulate (all optional)
     hipEvent_t ev_first_trace;

@@ -306,9 +306,12 @@ DEV bool traverse(const DevScene& S, v3 o, v3 d, int last_hit, float tmax, THit&
 // TM_NEE_CLOSEST in two steps (build_light_bvh in mpt_api.cpp): the closest hit among the
 // triangles that can emit, then an any-hit query over the whole scene up to that hit for
 // the candidates found; they report in TM_NEE_CLOSEST's stage (timing, counters).
+// TM_LIST_ANY: any-hit queries staged by the ReSTIR DI reuse passes (raw_o / raw_d / raw_key
+// at the positions of a compacted list; results in raw_occ), reported in the raw any-hit
+// stage's instrumentation counters (raw queries never run inside a render).
 enum TraceMode { TM_PATH = 0, TM_NEE_ANY = 1, TM_NEE_CLOSEST = 2, TM_RAW_CLOSEST = 3, TM_RAW_ANY = 4, TM_NEE_LIGHT = 5,
-                 TM_NEE_LIGHT_OCC = 6 };
-constexpr int trace_stage(int mode) { return mode >= TM_NEE_LIGHT ? TM_NEE_CLOSEST : mode; }
+                 TM_NEE_LIGHT_OCC = 6, TM_LIST_ANY = 7 };
+constexpr int trace_stage(int mode) { return mode == TM_LIST_ANY ? TM_RAW_ANY : mode >= TM_NEE_LIGHT ? TM_NEE_CLOSEST : mode; }
 // Short traversals (the light BVH: ~1.5 nodes per query) run one query per lane over a grid
 // covering the list instead of persistent waves: with so little work per query the shared
 // work counter of the persistent kernel (one device-scope atomic per wave refill) is what
@@ -327,6 +330,7 @@ struct TraceArgs {
     const float4* raw_d;
     float4* raw_hit;
     uint8_t* raw_occ;
+    const uint32_t* raw_key;   // TM_LIST_ANY: alpha key per ray (alpha testing on)
     const MptFrame* F;         // frame constants (alpha keys); NULL for raw queries
     int bounce;
     int alpha;                 // render_settings.do_alpha_testing
@@ -354,7 +358,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MODE == TM_P
     uint32_t* spill = P.stack_spill + (MODE == TM_NEE_LIGHT && A.static_grid ? 0 : ((size_t)blockIdx.x * TB + threadIdx.x) * (2 * SPILL_DEPTH));
     uint32_t n_nodes = 0, n_tris = 0, n_rays = 0;
     uint32_t n_slots[2] = {0u, 0u};
-    constexpr bool ANY = (MODE == TM_NEE_ANY || MODE == TM_RAW_ANY || MODE == TM_NEE_LIGHT_OCC);
+    constexpr bool ANY = (MODE == TM_NEE_ANY || MODE == TM_RAW_ANY || MODE == TM_NEE_LIGHT_OCC || MODE == TM_LIST_ANY);
     constexpr bool TIE = MODE == TM_NEE_LIGHT_OCC;
     const Node8* bvh_nodes = MODE == TM_NEE_LIGHT ? S.nodes_light : S.nodes;
     const TriRec* bvh_tris = MODE == TM_NEE_LIGHT ? S.tris_light : S.tris;
@@ -445,6 +449,12 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MODE == TM_P
                         }
                         tr.init(mk3(ro.x, ro.y, ro.z), mk3(rd.x, rd.y, rd.z), (int)__float_as_uint(ro.w), tmax, al, akey);
                         if (MODE == TM_NEE_LIGHT && S.n_light_tris == 0) tr.gk = 0u;   // no light: nothing to traverse
+                    } else if (MODE == TM_LIST_ANY) {
+                        ray = A.queue[i];
+                        ro = A.raw_o[ray];
+                        rd = A.raw_d[ray];
+                        tr.init(mk3(ro.x, ro.y, ro.z), mk3(rd.x, rd.y, rd.z), (int)__float_as_uint(ro.w), rd.w, A.alpha != 0,
+                                A.alpha ? A.raw_key[ray] : 0u);
                     } else {
                         ray = i;
                         ro = A.raw_o[i];
@@ -502,7 +512,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MODE == TM_P
         } else if (MODE == TM_NEE_LIGHT_OCC) {
             // a nearer triangle is not a light: the query contributes nothing, as a miss
             if (found) (A.ext ? P.xq_hit[ray] : P.nhit[ray >> 2]).w = __uint_as_float(0xffffffffu);
-        } else if (MODE == TM_RAW_ANY) {
+        } else if (MODE == TM_RAW_ANY || MODE == TM_LIST_ANY) {
             A.raw_occ[ray] = found ? 1 : 0;
         } else {
             A.raw_hit[ray] = make_float4(tr.best, tr.bu, tr.bv, __uint_as_float((uint32_t)(found ? tr.bprim : -1)));
@@ -2185,7 +2195,8 @@ void part_shade_generic(dim3 g, hipStream_t st, const ShadeArgs& a);          //
 void part_shade_plain(dim3 g, hipStream_t st, const ShadeArgs& a);            // k_shade<NONE, true>
 void part_shade_ext(dim3 g, hipStream_t st, const ShadeArgs& a);              // k_shade<NONE, false, true>
 void part_shade_override(int ovr, bool ext, dim3 g, hipStream_t st, const ShadeArgs& a);   // Lambert, Oren-Nayar
-enum RestirKernel { RK_INITIAL, RK_SPATIOTEMPORAL, RK_SPATIOTEMPORAL_ANY, RK_SPATIAL, RK_SPATIAL_ANY, RK_TEMPORAL };
+enum RestirKernel { RK_INITIAL, RK_SPATIOTEMPORAL, RK_SPATIOTEMPORAL_ANY, RK_SPATIAL, RK_SPATIAL_ANY, RK_TEMPORAL, RK_SP_GATHER,
+                   RK_SP_COMBINE };
 void part_restir_principled(int kind, dim3 g, hipStream_t st, const DevScene& S, const DevPaths& P, const MptFrame* F,
                             int pass, const float4* in, float4* out);
 void part_restir_override(int ovr, int kind, dim3 g, hipStream_t st, const DevScene& S, const DevPaths& P,
@@ -2271,6 +2282,35 @@ static int halo_exchange(const MptFrame& hf, LaunchCfg& cfg, hipStream_t st, int
     return x.halo_rows;
 }
 
+// One spatial reuse pass: staged (gather, traced rays, combine, visibility reuse;
+// restir_di.h) when the reference-default weights are selected and the neighbour counts fit
+// RS_KMAX, else the monolithic kernel.
+static void launch_spatial_pass(int ovr, bool def_bias, const MptFrame& hf, LaunchCfg& cfg, dim3 g, hipStream_t st,
+                                const DevScene& S, const DevPaths& P, const MptFrame* d_frame, int pass, const float4* in,
+                                float4* out) {
+    const MptReSTIRDISettings& rd = hf.render_settings.restir_di_settings;
+    const bool staged = def_bias && cfg.restir_staged && P.rq_o && rd.reuse_neighbor_count <= RS_KMAX &&
+                        (!rd.do_disocclusion_reuse_boost || rd.disocclusion_reuse_count <= RS_KMAX);
+    if (!staged) {
+        launch_restir_kernel(ovr, def_bias ? RK_SPATIAL : RK_SPATIAL_ANY, g, st, S, P, d_frame, pass, in, out);
+        return;
+    }
+    const dim3 gp(blocks_for(P.n));
+    hipMemsetAsync(&P.counters[CTR_RQ], 0, 2 * sizeof(int32_t), st);   // CTR_RQ, CTR_RQV
+    launch_restir_kernel(ovr, RK_SP_GATHER, gp, st, S, P, d_frame, pass, in, out);
+    TraceArgs ta{};
+    ta.S = S; ta.P = P; ta.queue = P.rq_list; ta.count_ptr = &P.counters[CTR_RQ]; ta.fetch = &P.counters[CTR_FETCH];
+    ta.raw_o = P.rq_o; ta.raw_d = P.rq_d; ta.raw_key = P.rq_key; ta.raw_occ = P.rq_occ;
+    ta.F = d_frame; ta.alpha = hf.render_settings.do_alpha_testing ? 1 : 0;
+    hipMemsetAsync(&P.counters[CTR_FETCH], 0, sizeof(int32_t), st);
+    launch_trace_mode<TM_LIST_ANY>(ta, cfg.grid_persistent, cfg.stats, st);
+    launch_restir_kernel(ovr, RK_SP_COMBINE, gp, st, S, P, d_frame, pass, in, out);
+    ta.count_ptr = &P.counters[CTR_RQV];
+    hipMemsetAsync(&P.counters[CTR_FETCH], 0, sizeof(int32_t), st);
+    launch_trace_mode<TM_LIST_ANY>(ta, cfg.grid_persistent, cfg.stats, st);
+    hipLaunchKernelGGL(k_rs_visapply, gp, dim3(TB), 0, st, P, out);
+}
+
 // ReSTIRDIRenderPass::launch (ReSTIRDIRenderPass.cpp:233-264) for the fused configuration:
 // presampling, initial candidates, fused spatiotemporal, (number_of_passes - 1) spatial
 // passes ping-ponging between the two spatial buffers; returns the output buffer in P.rs_out.
@@ -2330,7 +2370,7 @@ static void launch_restir(const DevScene& S, DevPaths& P, const MptFrame* d_fram
             float4* out = in == P.rs_sp1 ? P.rs_sp2 : P.rs_sp1;
             halo_exchange(hf, cfg, st, MPT_HALO_RESERVOIRS, pass, cfg.halo_rows, {{in, RB}});
             TimedScope tk(cfg, st, KT_RS_SPATIAL);
-            launch_restir_kernel(ovr, def_bias ? RK_SPATIAL : RK_SPATIAL_ANY, g, st, S, P, d_frame, pass, in, out);
+            launch_spatial_pass(ovr, def_bias, hf, cfg, g, st, S, P, d_frame, pass, in, out);
             P.rs_out = out;
         }
     } else {
@@ -2353,7 +2393,7 @@ static void launch_restir(const DevScene& S, DevPaths& P, const MptFrame* d_fram
                 float4* out = pass == 0 ? P.rs_sp1 : ((pass & 1) ? P.rs_sp2 : P.rs_sp1);
                 halo_exchange(hf, cfg, st, MPT_HALO_RESERVOIRS, pass + 1, cfg.halo_rows, {{in, RB}});
                 TimedScope tk(cfg, st, KT_RS_SPATIAL);
-                launch_restir_kernel(ovr, def_bias ? RK_SPATIAL : RK_SPATIAL_ANY, g, st, S, P, d_frame, pass, in, out);
+                launch_spatial_pass(ovr, def_bias, hf, cfg, g, st, S, P, d_frame, pass, in, out);
                 cur = out;
             }
         }

@@ -50,8 +50,15 @@ static void restir_kernel(int kind, dim3 g, hipStream_t st, const DevScene& S, c
     case RK_INITIAL: hipLaunchKernelGGL(k_restir_initial<OVR>, g, dim3(TB), 0, st, S, P, F); break;
     case RK_SPATIOTEMPORAL: hipLaunchKernelGGL((k_restir_spatiotemporal<OVR, DEF>), g, dim3(TB), 0, st, S, P, F); break;
     case RK_SPATIOTEMPORAL_ANY: hipLaunchKernelGGL((k_restir_spatiotemporal<OVR, -1>), g, dim3(TB), 0, st, S, P, F); break;
-    case RK_SPATIAL: hipLaunchKernelGGL((k_restir_spatial<OVR, DEF>), g, dim3(TB), 0, st, S, P, F, pass, in, out); break;
-    case RK_SPATIAL_ANY: hipLaunchKernelGGL((k_restir_spatial<OVR, -1>), g, dim3(TB), 0, st, S, P, F, pass, in, out); break;
+    case RK_SPATIAL:
+        hipLaunchKernelGGL((k_restir_spatial<OVR, DEF>), g, dim3(TB), 0, st, S, P, F, pass, in, out);
+        break;
+    case RK_SPATIAL_ANY:
+        hipLaunchKernelGGL((k_restir_spatial<OVR, -1>), g, dim3(TB), 0, st, S, P, F, pass, in, out);
+        break;
+    // the staged spatial pass (restir_di.h): gather and combine
+    case RK_SP_GATHER: hipLaunchKernelGGL(k_rsp_gather<OVR>, g, dim3(TB), 0, st, S, P, F, pass, in); break;
+    case RK_SP_COMBINE: hipLaunchKernelGGL(k_rsp_combine<OVR>, g, dim3(TB), 0, st, S, P, F, pass, in, out); break;
     default: hipLaunchKernelGGL(k_restir_temporal<OVR>, g, dim3(TB), 0, st, S, P, F, in, out); break;
     }
 }

@@ -42,7 +42,19 @@ DEV RSurf gb_surface(const DevScene& S, const DevPaths& P, int i, bool prev) {
     return s;
 }
 
-// ---- traced rays of a pass (alpha keys: pass pixel seed, 0, 5 + pass, ray counter) ----
+// ---- traced rays of a pass --------------------------------------------------------------
+// Alpha keys (alpha_key: pass pixel seed, bounce 0, kind 5 + pass, position): the position
+// names the ray's site in the pass, not its rank among the rays traced so far, so a key does
+// not depend on which earlier rays were skipped and a pass can stage its rays (k_rsp_*).  The
+// oracle (oracle_restir.h) uses the same positions.
+DEV constexpr int RP_TFC(int k) { return 2 * k; }           // neighbour k's sample at the center
+DEV constexpr int RP_TCN(int k) { return 2 * k + 1; }       // the canonical sample at neighbour k (pairwise MIS)
+constexpr int RP_T_TFC = 4000, RP_T_TCN = 4001;             // the temporal neighbour's pair
+DEV constexpr int RP_GBH(int cur, int j) { return 10000 + cur * 1000 + j; }   // j = 999 / 998: temporal / center terms
+DEV constexpr int RP_NORM(int j) { return 20000 + j; }
+DEV constexpr int RP_LIGHT(int i) { return 100 + i; }       // initial candidates: light candidate i (target visibility)
+DEV constexpr int RP_BSDF(int i) { return 200 + i; }        // initial candidates: BSDF candidate i
+constexpr int RP_VISREUSE = 30000;                          // restir_visibility_reuse
 struct RRays {
     const DevScene* S;
     uint2* lds;
@@ -52,6 +64,7 @@ struct RRays {
     int kind;
     int n;
     uint32_t n_any, n_closest;
+    DEV RRays& at(int pos) { n = pos; return *this; }
     DEV bool any(v3 o, v3 d, float tmax, int last) {
         n_any++;
         uint32_t key = alpha ? alpha_key(pseed, 0, kind, n++) : 0u;
@@ -123,9 +136,13 @@ DEV void rr_end_norm(RResv& r, float nume, float denom) {   // end_with_normaliz
 }
 DEV void rr_end_normalized(RResv& r) { rr_end_norm(r, 1.0f, 1.0f); }   // the pairwise weights' 1 / 1
 
-// ReSTIR_DI_evaluate_target_function<vis> (Utils.h:20-128)
-DEV float restir_target(const DevScene& S, const MptFrame& F, const BCtx& bc, RRays& rr, int tri, v3 point, uint32_t flags,
-                        const RSurf& s, bool vis, int ovr) {
+// ReSTIR_DI_evaluate_target_function<vis> (Utils.h:20-128), split at the visibility test:
+// restir_target_unocc returns the target before it (0 = no ray would be traced) and the
+// shadow ray the test traces (its distance; evaluate_shadow_ray traces to distance - 1e-4,
+// Intersect.h:227)
+struct TgtRay { v3 o, d; float dist; };
+DEV float restir_target_unocc(const DevScene& S, const MptFrame& F, const BCtx& bc, int tri, v3 point, uint32_t flags,
+                              const RSurf& s, bool vis, int ovr, TgtRay& ray) {
     if (tri == -1 && !(flags & RF_ENVMAP)) return 0.0f;
     float dist = 0.0f;
     v3 dir;
@@ -143,8 +160,17 @@ DEV float restir_target(const DevScene& S, const MptFrame& F, const BCtx& bc, RR
     if (flags & RF_ENVMAP) { float ep; e = env_eval(S, F, dir, ep); }
     else e = emission_of(S.mats[S.mat_idx[tri]]);
     float t = lum(f * e * cosv);
+    ray.o = s.sp;
+    ray.d = dir;
+    ray.dist = dist;
+    return t;
+}
+DEV float restir_target(const DevScene& S, const MptFrame& F, const BCtx& bc, RRays& rr, int tri, v3 point, uint32_t flags,
+                        const RSurf& s, bool vis, int ovr) {
+    TgtRay ray;
+    float t = restir_target_unocc(S, F, bc, tri, point, flags, s, vis, ovr, ray);
     if (t == 0.0f) return 0.0f;
-    if (vis) t *= rr.any(s.sp, dir, dist, s.last) ? 0.0f : 1.0f;
+    if (vis) t *= rr.any(s.sp, ray.d, ray.dist, s.last) ? 0.0f : 1.0f;
     return t;
 }
 
@@ -156,7 +182,7 @@ DEV void restir_visibility_reuse(const MptFrame& F, RRays& rr, RResv& r, v3 sp, 
     v3 dir;
     if (r.flags & RF_ENVMAP) { dir = mat_x_vec(F.world_settings.envmap_to_world_matrix.m, r.point); dist = 1.0e35f; }
     else { dir = r.point - sp; dist = length(dir); dir = dir / dist; }
-    if (rr.any(sp, dir, dist, last)) r.UCW = -1.0f;
+    if (rr.at(RP_VISREUSE).any(sp, dir, dist, last)) r.UCW = -1.0f;
     else r.flags |= RF_UNOCCLUDED;
 }
 
@@ -215,7 +241,9 @@ DEV int restir_spatial_neighbor(const DevPaths& P, const MptFrame& F, int k, int
     return ni;
 }
 
-// pairwise MIS defensive (SpatiotemporalMISWeight.h:193-291, SpatialMISWeight.h:167-262)
+// pairwise MIS defensive (SpatiotemporalMISWeight.h:193-291, SpatialMISWeight.h:167-262).
+// weight() evaluates the canonical sample's target at the neighbour (tcn, with visibility when
+// bvis) and hands it to weight_tcn, which the staged passes call with the stored value.
 struct PairwiseMIS {
     float mc;
     bool defensive;   // PAIRWISE_MIS_DEFENSIVE (else PAIRWISE_MIS, SpatialMISWeight.h:95-165)
@@ -223,6 +251,12 @@ struct PairwiseMIS {
     DEV float weight(const DevScene& S, const MptFrame& F, const BCtx& bc, RRays& rr, const MptReSTIRDISettings& rd,
                      const RResv& res, const RResv& center, float tf_center, const RSurf& nsurf, int vcount, int vM,
                      bool update_mc, bool canonical, int ovr) {
+        float tcn = 0.0f;
+        if (!canonical && update_mc) tcn = restir_target(S, F, bc, rr, center.tri, center.point, center.flags, nsurf, bvis, ovr);
+        return weight_tcn(rd, res, center, tf_center, tcn, vcount, vM, update_mc, canonical);
+    }
+    DEV float weight_tcn(const MptReSTIRDISettings& rd, const RResv& res, const RResv& center, float tf_center, float tcn,
+                         int vcount, int vM, bool update_mc, bool canonical) {
         if (!defensive) {
             const bool cw = rd.use_confidence_weights;
             if (canonical) return mc == 0.0f ? 1.0f : mc;
@@ -233,7 +267,6 @@ struct PairwiseMIS {
             float denom = tfn * nsum + tf_center / div * cM;
             float mi = denom == 0.0f ? 0.0f : (nume / denom);
             if (update_mc) {
-                float tcn = restir_target(S, F, bc, rr, center.tri, center.point, center.flags, nsurf, bvis, ovr);
                 float tcc = center.target;
                 float nume_mc = tcc / div * cM;
                 float denom_mc = tcn * nsum + tcc / div * cM;
@@ -254,7 +287,6 @@ struct PairwiseMIS {
             if (denom != 0.0f) mi = nume / denom;
             if (rd.use_confidence_weights) mi *= nsum / (nsum + cM);
             if (update_mc) {
-                float tcn = restir_target(S, F, bc, rr, center.tri, center.point, center.flags, nsurf, bvis, ovr);
                 float tcc = center.target;
                 float nume_mc = tcc / div * cM;
                 float denom_mc = tcn * nsum + tcc / div * cM;
@@ -524,7 +556,7 @@ RESTIR_KERNEL void k_restir_initial(DevScene S, DevPaths P, const MptFrame* __re
             }
             // ReSTIR_DI_InitialTargetFunctionVisibility (InitialCandidates.h:248-264)
             if (F.options.restir_di_initial_target_visibility && target > 0.0f) {
-                if (rr.any(ep, tl, dist, g.last)) { r.M++; continue; }
+                if (rr.at(RP_LIGHT(i)).any(ep, tl, dist, g.last)) { r.M++; continue; }
                 flags |= RF_UNOCCLUDED;
             }
             rr_add(r, tri, point, target, flags, weight, rng);
@@ -538,7 +570,7 @@ RESTIR_KERNEL void k_restir_initial(DevScene S, DevPaths P, const MptFrame* __re
             bool refr = dot(dir, g.view) < 0.0f;   // the reference tests against the view direction
             if (!(bpdf > 0.0f)) continue;
             THit h;
-            bool found = rr.closest(g.p, dir, g.last, h) && h.t < 1.0e35f - 1.0e-4f;
+            bool found = rr.at(RP_BSDF(i)).closest(g.p, dir, g.last, h) && h.t < 1.0e35f - 1.0e-4f;
             ShadowLightHit sh;
             if (found) found = shadow_light_hit(S, make_float4(h.t, h.u, h.v, __uint_as_float((uint32_t)h.prim)), sh);
             if (found && !is_black(sh.em)) {
@@ -681,13 +713,13 @@ RESTIR_KERNEL void k_restir_spatiotemporal(DevScene S, DevPaths P, const MptFram
                 int nj = valid_nb(j);
                 if (nj == -1) continue;
                 RSurf js = j == reuse ? cs : gb_surface(S, P, nj, use_prev);
-                float tj = restir_target(S, F, bc, rr, r.tri, r.point, r.flags, js, bvis, OVR);
+                float tj = restir_target(S, F, bc, rr.at(RP_GBH(current, j)), r.tri, r.point, r.flags, js, bvis, OVR);
                 int M = 1;
                 if (cw) M = j == reuse ? ic.M : rr_load(tin, nj).M;
                 denom += tj * (float)M;
                 if (j + 1 == current) nume = tj * (float)M;
             }
-            float tt = restir_target(S, F, bc, rr, r.tri, r.point, r.flags, ts, bvis, OVR);
+            float tt = restir_target(S, F, bc, rr.at(RP_GBH(current, 999)), r.tri, r.point, r.flags, ts, bvis, OVR);
             int M = cw ? tres.M : 1;
             denom += tt * (float)M;
             if (current == 0) nume = tt * (float)M;
@@ -696,7 +728,7 @@ RESTIR_KERNEL void k_restir_spatiotemporal(DevScene S, DevPaths P, const MptFram
         int selected = 0;   // MIS-like: 0 temporal, k + 1 spatial k
         if (temporal_ok) {
             float tfc = 0.0f;
-            if (tres.UCW > 0.0f) tfc = restir_target(S, F, bc, rr, tres.tri, tres.point, tres.flags, cs, bvis, OVR);
+            if (tres.UCW > 0.0f) tfc = restir_target(S, F, bc, rr.at(RP_T_TFC), tres.tri, tres.point, tres.flags, cs, bvis, OVR);
             float jac = 1.0f;
             if (tfc > 0.0f && tres.UCW > 0.0f && !(tres.flags & RF_ENVMAP)) {
                 jac = restir_jacobian(S, tres, cs.sp, ts.sp - ts.sn * 1.0e-4f);
@@ -708,7 +740,7 @@ RESTIR_KERNEL void k_restir_spatiotemporal(DevScene S, DevPaths P, const MptFram
             else if (mode == MPT_RESTIR_DI_BIAS_MIS_GBH) wgt = gbh(tres, 0);
             else {
                 bool update_mc = ic.M > 0 && ic.UCW > 0.0f;
-                wgt = mis.weight(S, F, bc, rr, rd, tres, ic, tfc, ts, vcount, vM, update_mc, false, OVR);
+                wgt = mis.weight(S, F, bc, rr.at(RP_T_TCN), rd, tres, ic, tfc, ts, vcount, vM, update_mc, false, OVR);
             }
             if (rr_combine(o, tres, wgt, tfc, jac, rng)) {
                 selected = 0;
@@ -727,7 +759,7 @@ RESTIR_KERNEL void k_restir_spatiotemporal(DevScene S, DevPaths P, const MptFram
             bool vis = spatial_visibility(F, rd, k, reuse);
             if (nr.UCW > 0.0f) {
                 if (k == reuse) tfc = nr.target;
-                else tfc = restir_target(S, F, bc, rr, nr.tri, nr.point, nr.flags, cs, vis, OVR);
+                else tfc = restir_target(S, F, bc, rr.at(RP_TFC(k)), nr.tri, nr.point, nr.flags, cs, vis, OVR);
             }
             float jac = 1.0f;
             if (tfc > 0.0f && nr.UCW > 0.0f && k != reuse && !(nr.flags & RF_ENVMAP)) {
@@ -744,7 +776,7 @@ RESTIR_KERNEL void k_restir_spatiotemporal(DevScene S, DevPaths P, const MptFram
                 if (nr.UCW == 0.0f && !update_mc) wgt = 1.0f;
                 else {
                     RSurf ns = gb_surface(S, P, ni, use_prev);
-                    wgt = mis.weight(S, F, bc, rr, rd, nr, ic, tfc, ns, vcount, vM, update_mc, k == reuse, OVR);
+                    wgt = mis.weight(S, F, bc, rr.at(RP_TCN(k)), rd, nr, ic, tfc, ns, vcount, vM, update_mc, k == reuse, OVR);
                 }
             }
             if (rr_combine(o, nr, wgt, tfc, jac, rng)) {
@@ -769,7 +801,7 @@ RESTIR_KERNEL void k_restir_spatiotemporal(DevScene S, DevPaths P, const MptFram
                 }
                 // the MIS-like loop reads the current frame's G-buffer (SpatiotemporalNormalizationWeight.h:130)
                 RSurf js = j == reuse ? cs : gb_surface(S, P, nj, mode == MPT_RESTIR_DI_BIAS_MIS_LIKE ? false : use_prev);
-                float tj = restir_target(S, F, bc, rr, o.tri, o.point, o.flags, js, bvis, OVR);
+                float tj = restir_target(S, F, bc, rr.at(RP_NORM(j)), o.tri, o.point, o.flags, js, bvis, OVR);
                 if (tj > 0.0f) {
                     if (mode == MPT_RESTIR_DI_BIAS_1_OVER_Z) nd += (float)(j == reuse ? ic.M : rr_load(tin, nj).M);
                     else {
@@ -782,7 +814,7 @@ RESTIR_KERNEL void k_restir_spatiotemporal(DevScene S, DevPaths P, const MptFram
             }
             if (mode == MPT_RESTIR_DI_BIAS_1_OVER_M) nd += (float)tres.M;
             else {
-                float tt = restir_target(S, F, bc, rr, o.tri, o.point, o.flags, ts, bvis, OVR);
+                float tt = restir_target(S, F, bc, rr.at(RP_NORM(999)), o.tri, o.point, o.flags, ts, bvis, OVR);
                 if (mode == MPT_RESTIR_DI_BIAS_1_OVER_Z) { if (tt > 0.0f) nd += (float)tres.M; }
                 else {
                     if (selected == 0) nn += tt;
@@ -843,9 +875,10 @@ RESTIR_KERNEL void k_restir_temporal(DevScene S, DevPaths P, const MptFrame* __r
         int selected = 0;   // MIS-like: TEMPORAL_NEIGHBOR_ID 0 / INITIAL_CANDIDATES_ID 1
         // GBH weight of a reservoir's sample between the temporal neighbour and the center (TemporalMISWeight.h:62-110)
         auto gbh = [&](const RResv& r, bool temporal_id) -> float {
-            float tt = restir_target(S, F, bc, rr, r.tri, r.point, r.flags, ts, bvis, OVR);   // temporal M != 0 here
+            const int cur = temporal_id ? 0 : 1;
+            float tt = restir_target(S, F, bc, rr.at(RP_GBH(cur, 999)), r.tri, r.point, r.flags, ts, bvis, OVR);   // temporal M != 0 here
             if (temporal_id && tt == 0.0f) return 0.0f;
-            float tc = restir_target(S, F, bc, rr, r.tri, r.point, r.flags, cs, bvis, OVR);
+            float tc = restir_target(S, F, bc, rr.at(RP_GBH(cur, 998)), r.tri, r.point, r.flags, cs, bvis, OVR);
             int tM = cw ? tres.M : 1, cM = cw ? ic.M : 1;
             float nume = temporal_id ? tt * (float)tM : tc * (float)cM;
             float denom = tt * (float)tM + tc * (float)cM;
@@ -853,7 +886,7 @@ RESTIR_KERNEL void k_restir_temporal(DevScene S, DevPaths P, const MptFrame* __r
         };
         {
             float tfc = 0.0f;
-            if (tres.UCW > 0.0f) tfc = restir_target(S, F, bc, rr, tres.tri, tres.point, tres.flags, cs, bvis, OVR);
+            if (tres.UCW > 0.0f) tfc = restir_target(S, F, bc, rr.at(RP_T_TFC), tres.tri, tres.point, tres.flags, cs, bvis, OVR);
             float jac = 1.0f;
             if (tfc > 0.0f && tres.UCW > 0.0f && !(tres.flags & RF_ENVMAP)) {
                 jac = restir_jacobian(S, tres, cs.sp, ts.sp - ts.sn * 1.0e-4f);
@@ -872,7 +905,7 @@ RESTIR_KERNEL void k_restir_temporal(DevScene S, DevPaths P, const MptFrame* __r
                 float denom = tfn * nsum + tfc * cM;
                 float mi = denom == 0.0f ? 0.0f : (nume / denom);
                 if (def && cw) mi *= nsum / (nsum + cM);
-                float tcn = restir_target(S, F, bc, rr, ic.tri, ic.point, ic.flags, ts, bvis, OVR);
+                float tcn = restir_target(S, F, bc, rr.at(RP_T_TCN), ic.tri, ic.point, ic.flags, ts, bvis, OVR);
                 float tcc = ic.target;
                 float nume_mc = tcc * cM;
                 float denom_mc = tcn * nsum + tcc * cM;
@@ -906,13 +939,13 @@ RESTIR_KERNEL void k_restir_temporal(DevScene S, DevPaths P, const MptFrame* __r
             if (mode == MPT_RESTIR_DI_BIAS_1_OVER_M) nd = (float)(ic.M + tres.M);
             else if (mode == MPT_RESTIR_DI_BIAS_1_OVER_Z) {
                 nd = 0.0f;
-                float tc = restir_target(S, F, bc, rr, o.tri, o.point, o.flags, cs, bvis, OVR);
+                float tc = restir_target(S, F, bc, rr.at(RP_NORM(998)), o.tri, o.point, o.flags, cs, bvis, OVR);
                 nd += (float)((tc > 0.0f) * ic.M);
-                float tt = restir_target(S, F, bc, rr, o.tri, o.point, o.flags, ts, bvis, OVR);   // temporal M > 0
+                float tt = restir_target(S, F, bc, rr.at(RP_NORM(999)), o.tri, o.point, o.flags, ts, bvis, OVR);   // temporal M > 0
                 nd += (float)((tt > 0.0f) * tres.M);
             } else if (mode == MPT_RESTIR_DI_BIAS_MIS_LIKE) {
-                float tc = restir_target(S, F, bc, rr, o.tri, o.point, o.flags, cs, bvis, OVR);
-                float tt = restir_target(S, F, bc, rr, o.tri, o.point, o.flags, ts, bvis, OVR);
+                float tc = restir_target(S, F, bc, rr.at(RP_NORM(998)), o.tri, o.point, o.flags, cs, bvis, OVR);
+                float tt = restir_target(S, F, bc, rr.at(RP_NORM(999)), o.tri, o.point, o.flags, ts, bvis, OVR);
                 nn = selected == 1 ? tc : tt;
                 int icM = cw ? ic.M : 1, tM = cw ? tres.M : 1;
                 nd = tc * (float)icM + tt * (float)tM;
@@ -986,7 +1019,7 @@ RESTIR_KERNEL void k_restir_spatial(DevScene S, DevPaths P, const MptFrame* __re
             bool vis = spatial_visibility(F, rd, k, reuse);
             if (nr.UCW > 0.0f) {
                 if (k == reuse) tfc = nr.target;
-                else tfc = restir_target(S, F, bc, rr, nr.tri, nr.point, nr.flags, cs, vis, OVR);
+                else tfc = restir_target(S, F, bc, rr.at(RP_TFC(k)), nr.tri, nr.point, nr.flags, cs, vis, OVR);
             }
             float jac = 1.0f;
             if (tfc > 0.0f && nr.UCW > 0.0f && k != reuse && !(nr.flags & RF_ENVMAP)) {
@@ -1006,7 +1039,7 @@ RESTIR_KERNEL void k_restir_spatial(DevScene S, DevPaths P, const MptFrame* __re
                         int nj = valid_nb(j);
                         if (nj == -1) continue;
                         RSurf js = gb_surface(S, P, nj, false);
-                        float tj = restir_target(S, F, bc, rr, nr.tri, nr.point, nr.flags, js, bvis, OVR);
+                        float tj = restir_target(S, F, bc, rr.at(RP_GBH(k, j)), nr.tri, nr.point, nr.flags, js, bvis, OVR);
                         int M = cw ? rr_load(in, nj).M : 1;
                         denom += tj * (float)M;
                         if (j == k) nume = tj * (float)M;
@@ -1016,7 +1049,7 @@ RESTIR_KERNEL void k_restir_spatial(DevScene S, DevPaths P, const MptFrame* __re
             } else {
                 bool update_mc = cres.M > 0 && cres.UCW > 0.0f;
                 RSurf ns = gb_surface(S, P, ni, false);
-                wgt = mis.weight(S, F, bc, rr, rd, nr, cres, tfc, ns, vcount, vM, update_mc, k == reuse, OVR);
+                wgt = mis.weight(S, F, bc, rr.at(RP_TCN(k)), rd, nr, cres, tfc, ns, vcount, vM, update_mc, k == reuse, OVR);
             }
             if (rr_combine(o, nr, wgt, tfc, jac, rng)) {
                 selected = k;
@@ -1036,7 +1069,7 @@ RESTIR_KERNEL void k_restir_spatial(DevScene S, DevPaths P, const MptFrame* __re
                 if (nj == -1) continue;
                 if (mode == MPT_RESTIR_DI_BIAS_1_OVER_M) { nd += (float)rr_load(in, nj).M; continue; }
                 RSurf js = gb_surface(S, P, nj, false);
-                float tj = restir_target(S, F, bc, rr, o.tri, o.point, o.flags, js, bvis, OVR);
+                float tj = restir_target(S, F, bc, rr.at(RP_NORM(j)), o.tri, o.point, o.flags, js, bvis, OVR);
                 if (tj > 0.0f) {
                     int M = rr_load(in, nj).M;
                     if (mode == MPT_RESTIR_DI_BIAS_1_OVER_Z) nd += (float)M;
@@ -1060,6 +1093,253 @@ RESTIR_KERNEL void k_restir_spatial(DevScene S, DevPaths P, const MptFrame* __re
     }
     count_pass_rays(P, rr.n_any, rr.n_closest);
 }
+
+// ---- staged spatial reuse (the reference-default weights) -----------------------------
+// k_restir_spatial traces its visibility rays inline, inside a kernel whose BSDF evaluations
+// hold every register (256 VGPRs and scratch spills at 2 waves / SIMD), so the traversal
+// runs slowly and lanes wait on each other's rays.  The staged pass splits it at the rays:
+//  * k_rsp_gather: per pixel, the neighbour selection and the quantities that do not depend
+//    on any ray -- each neighbour's unoccluded target functions (the BSDF evaluations) and
+//    Jacobian -- and the visibility rays the monolithic kernel would trace, staged at fixed
+//    positions (pixel slot, 2k + which) with the alpha keys of their position in its order;
+//  * k_trace<TM_LIST_ANY> over the staged rays (persistent, chunked, LDS stack);
+//  * k_rsp_combine: the resampling from the stored values and the occlusion bytes, with the
+//    RNG draws of the monolithic kernel; the visibility-reuse ray of the result is staged
+//    again, traced, and applied by k_rs_visapply.
+// Alpha keys are positional (RP_*), so a staged ray has the key the monolithic kernel gives
+// it, including the bias-correction ray of a neighbour that a Jacobian rejection then drops
+// (staged and traced, never used).
+constexpr int RS_KMAX = RS_KMAX_HOST, RS_RPP = RS_RPP_HOST;   // neighbours a staged pass supports; ray positions per pixel
+enum : int { RSM_SKIP = 1 };                      // rq_meta.x: the pixel is not resampled (output untouched)
+
+// exclusive scan of one int per thread over a TB-thread block; total to `total`
+DEV int rs_block_scan(int v, int* tmp, int& total) {
+    const int lane = lane_id(), wid = threadIdx.x >> 6;
+    constexpr int NW = TB / 64;
+    int x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        int y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) tmp[wid] = x;
+    __syncthreads();
+    int before = 0, all = 0;
+#pragma unroll
+    for (int w = 0; w < NW; w++) {
+        const int tw = tmp[w];
+        if (w < wid) before += tw;
+        all += tw;
+    }
+    __syncthreads();
+    total = all;
+    return before + x - v;
+}
+
+DEV void rs_stage_ray(const DevPaths& P, size_t id, const TgtRay& r, int last, uint32_t key) {
+    P.rq_o[id] = make_float4(r.o.x, r.o.y, r.o.z, __uint_as_float((uint32_t)last));
+    P.rq_d[id] = make_float4(r.d.x, r.d.y, r.d.z, r.dist - 1.0e-4f);
+    P.rq_key[id] = key;
+}
+
+// appends the ray positions in `mask` of slot s to the list behind `counter` (one atomic per block)
+DEV void rs_append(const DevPaths& P, int32_t* counter, int s, uint32_t mask, int* tmp, int* base) {
+    int tot;
+    const int off = rs_block_scan(__popc(mask), tmp, tot);
+    if (threadIdx.x == 0) *base = tot ? atomicAdd(counter, tot) : 0;
+    __syncthreads();
+    int o = *base + off;
+    while (mask) {
+        const int j = __builtin_ctz(mask);
+        mask &= mask - 1u;
+        P.rq_list[o++] = s * RS_RPP + j;
+    }
+}
+
+template <int OVR>
+RESTIR_KERNEL void k_rsp_gather(DevScene S, DevPaths P, const MptFrame* __restrict__ Fp, int pass, const float4* __restrict__ in) {
+    __shared__ int tmp[TB / 64];
+    __shared__ int base;
+    const MptFrame& F = *Fp;
+    const BCtx bc = make_bctx(S, F);
+    const int W = F.res_x;
+    const uint32_t pass_rs = F.restir_di_seeds[4 + pass];
+    const bool alpha = F.render_settings.do_alpha_testing;
+    const int s = blockIdx.x * TB + threadIdx.x;
+    uint32_t rmask = 0u;
+    if (s < P.n) {
+        const int center = s + P.pix_off;
+        int4 meta = make_int4(RSM_SKIP, 0, 0, 0);
+        MptReSTIRDISettings rd = F.render_settings.restir_di_settings;
+        rd.spatial_pass_index = pass;
+        if (P.active[s] && P.gb_meta[center].z) {
+            const uint32_t seed = pass_seed(F, (uint32_t)center, pass_rs);
+            Rng rng = make_rng(seed);
+            const RSurf cs = gb_surface(S, P, center, false);
+            if (!is_emissive(*cs.m)) {
+                const int x = center % W, y = center / W;
+                float rot = rd.do_neighbor_rotation ? TWO_PI * rng() : 0.0f;
+                float cr = pcos(rot), sr = psin(rot);
+                const RResv cres = rr_load(in, center);
+                if (cres.M <= 1 && rd.do_disocclusion_reuse_boost) rd.reuse_neighbor_count = rd.disocclusion_reuse_count;
+                const int reuse = rd.reuse_neighbor_count;
+                int cache = 0, vcount = 0, vM = 0;
+                for (int k = 0; k < reuse; k++) {
+                    int ni = restir_spatial_neighbor(P, F, k, reuse, rd.reuse_radius, x, y, cr, sr, pass_rs);
+                    if (ni == -1) continue;
+                    if (!restir_similar(S, P, rd, ni, *cs.m, cs.sp, cs.sn, false)) continue;
+                    vM += rr_load(in, ni).M;
+                    vcount++;
+                    cache |= 1 << k;
+                }
+                meta = make_int4(0, cache, vM, vcount);
+                const bool update_mc = cres.M > 0 && cres.UCW > 0.0f;
+                for (int k = 0; k < reuse && vM != 0; k++) {
+                    if (!((cache >> k) & 1)) continue;
+                    const int ni = restir_spatial_neighbor(P, F, k, reuse, rd.reuse_radius, x, y, cr, sr, pass_rs);
+                    const RResv nr = rr_load(in, ni);
+                    const bool vis = spatial_visibility(F, rd, k, reuse);
+                    float tfc = 0.0f, tcn = 0.0f, jac = 1.0f;
+                    TgtRay ray;
+                    if (nr.UCW > 0.0f) {
+                        tfc = restir_target_unocc(S, F, bc, nr.tri, nr.point, nr.flags, cs, vis, OVR, ray);
+                        if (vis && tfc > 0.0f) {
+                            rs_stage_ray(P, (size_t)s * RS_RPP + 2 * k, ray, cs.last, alpha ? alpha_key(seed, 0, 7, RP_TFC(k)) : 0u);
+                            rmask |= 1u << (2 * k);
+                        }
+                        if (tfc > 0.0f && !(nr.flags & RF_ENVMAP)) {
+                            float4 np = P.gb_pos[ni];
+                            jac = restir_jacobian(S, nr, cs.sp, mk3(np.x, np.y, np.z));
+                        }
+                    }
+                    if (update_mc) {
+                        const RSurf ns = gb_surface(S, P, ni, false);
+                        tcn = restir_target_unocc(S, F, bc, cres.tri, cres.point, cres.flags, ns, true, OVR, ray);
+                        if (tcn > 0.0f) {
+                            rs_stage_ray(P, (size_t)s * RS_RPP + 2 * k + 1, ray, ns.last, alpha ? alpha_key(seed, 0, 7, RP_TCN(k)) : 0u);
+                            rmask |= 1u << (2 * k + 1);
+                        }
+                    }
+                    P.rq_rec[(size_t)s * RS_KMAX + k] = make_float4(__int_as_float(ni), tfc, tcn, jac);
+                }
+            }
+        }
+        P.rq_meta[s] = meta;
+    }
+    rs_append(P, &P.counters[CTR_RQ], s, rmask, tmp, &base);
+}
+
+template <int OVR>
+RESTIR_KERNEL void k_rsp_combine(DevScene S, DevPaths P, const MptFrame* __restrict__ Fp, int pass, const float4* __restrict__ in,
+                                 float4* out) {
+    __shared__ int tmp[TB / 64];
+    __shared__ int base;
+    const MptFrame& F = *Fp;
+    const uint32_t pass_rs = F.restir_di_seeds[4 + pass];
+    const bool alpha = F.render_settings.do_alpha_testing;
+    const int s = blockIdx.x * TB + threadIdx.x;
+    uint32_t vmask = 0u, n_any = 0u;
+    if (s < P.n && !(P.rq_meta[s].x & RSM_SKIP)) {
+        const int4 meta = P.rq_meta[s];
+        const int center = s + P.pix_off;
+        MptReSTIRDISettings rd = F.render_settings.restir_di_settings;
+        rd.spatial_pass_index = pass;
+        const uint32_t seed = pass_seed(F, (uint32_t)center, pass_rs);
+        Rng rng = make_rng(seed);
+        if (rd.do_neighbor_rotation) (void)rng();   // the neighbour rotation (used by k_rsp_gather)
+        const RResv cres = rr_load(in, center);
+        if (cres.M <= 1 && rd.do_disocclusion_reuse_boost) rd.reuse_neighbor_count = rd.disocclusion_reuse_count;
+        const int reuse = rd.reuse_neighbor_count;
+        const int cache = meta.y, vM = meta.z, vcount = meta.w;
+        const bool update_mc = cres.M > 0 && cres.UCW > 0.0f;
+        RResv o = rr_default();
+        PairwiseMIS mis{0.0f, true, true};
+        int ntr = 0;   // rays the monolithic kernel traces (the ray counters)
+        const size_t r0 = (size_t)s * RS_RPP;
+        for (int k = vM == 0 ? reuse : 0; k < reuse + 1; k++) {
+            if (k < reuse && !((cache >> k) & 1)) continue;
+            RResv nr;
+            float4 rec = make_float4(0.0f, 0.0f, 0.0f, 1.0f);
+            if (k == reuse) nr = cres;
+            else {
+                rec = P.rq_rec[(size_t)s * RS_KMAX + k];
+                nr = rr_load(in, __float_as_int(rec.x));
+            }
+            const bool vis = spatial_visibility(F, rd, k, reuse);
+            float tfc = 0.0f;
+            if (nr.UCW > 0.0f) {
+                if (k == reuse) tfc = nr.target;
+                else {
+                    tfc = rec.y;
+                    if (vis && tfc > 0.0f) {
+                        if (P.rq_occ[r0 + 2 * k]) tfc = 0.0f;
+                        ntr++;
+                    }
+                }
+            }
+            float jac = 1.0f;
+            if (tfc > 0.0f && nr.UCW > 0.0f && k != reuse && !(nr.flags & RF_ENVMAP)) {
+                jac = rec.w;
+                if (jac == -1.0f) {   // (its staged bias-correction ray is not used)
+                    o.M += nr.M;
+                    continue;
+                }
+            }
+            float tcn = 0.0f;
+            if (k != reuse && update_mc) {
+                tcn = rec.z;
+                if (tcn > 0.0f) {
+                    if (P.rq_occ[r0 + 2 * k + 1]) tcn = 0.0f;
+                    ntr++;
+                }
+            }
+            const float wgt = mis.weight_tcn(rd, nr, cres, tfc, tcn, vcount, vM, update_mc, k == reuse);
+            if (rr_combine(o, nr, wgt, tfc, jac, rng)) {
+                if (vis) o.flags |= RF_UNOCCLUDED;
+                else if (k == reuse) o.flags |= nr.flags & RF_UNOCCLUDED;
+                else o.flags &= ~RF_UNOCCLUDED;
+            }
+        }
+        {
+            rr_end_normalized(o);
+            const bool vreuse = (F.options.restir_di_do_visibility_reuse ||
+                                 (F.options.restir_di_initial_target_visibility && F.options.restir_di_spatial_target_visibility)) &&
+                                (rd.do_temporal_reuse_pass || rd.number_of_passes - 1 != rd.spatial_pass_index);
+            if (vreuse && o.UCW > 0.0f && !(o.flags & RF_UNOCCLUDED)) {
+                // restir_visibility_reuse's ray, staged at position 0 (its first-pass result is consumed)
+                const float4 gp = P.gb_pos[center], gs = P.gb_sn[center];
+                const v3 sp = mk3(gp.x, gp.y, gp.z) + mk3(gs.x, gs.y, gs.z) * 1.0e-4f;
+                TgtRay ray;
+                ray.o = sp;
+                if (o.flags & RF_ENVMAP) { ray.d = mat_x_vec(F.world_settings.envmap_to_world_matrix.m, o.point); ray.dist = 1.0e35f; }
+                else { v3 dir = o.point - sp; ray.dist = length(dir); ray.d = dir / ray.dist; }
+                rs_stage_ray(P, r0, ray, P.gb_meta[center].x, alpha ? alpha_key(seed, 0, 7, RP_VISREUSE) : 0u);
+                vmask = 1u;
+                ntr++;
+            }
+            if (rd.m_cap > 0) o.M = imin(o.M, rd.m_cap);
+            rr_store(out, center, o);
+            n_any = (uint32_t)ntr;
+        }
+    }
+    rs_append(P, &P.counters[CTR_RQV], s, vmask, tmp, &base);
+    // ray counters: one atomic per block (per wave, 32 k atomics on one word would serialise)
+    int tot;
+    (void)rs_block_scan((int)n_any, tmp, tot);
+    if (threadIdx.x == 0 && tot) atomicAdd((unsigned long long*)&P.ray_counts[1], (unsigned long long)tot);
+}
+
+#ifndef MPT_TU_PART   // k_rs_visapply
+// restir_visibility_reuse's outcome for the staged rays: occluded -> UCW = -1, else unoccluded
+__global__ __launch_bounds__(TB) void k_rs_visapply(DevPaths P, float4* out) {
+    const int i = blockIdx.x * TB + threadIdx.x;
+    if (i >= P.counters[CTR_RQV]) return;
+    const int id = P.rq_list[i];
+    const size_t c = (size_t)(id / RS_RPP + P.pix_off);
+    if (P.rq_occ[id]) out[3 * c].z = -1.0f;
+    else out[3 * c + 2].x = __uint_as_float(__float_as_uint(out[3 * c + 2].x) | RF_UNOCCLUDED);
+}
+#endif
 
 // CameraRays' reset / previous-frame G-buffer copy for LSS_RESTIR_DI (CameraRays.h:19-34, 78-91)
 #ifndef MPT_TU_PART   // k_restir_frame_begin

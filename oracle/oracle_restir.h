@@ -91,11 +91,22 @@ inline uint32_t pass_seed(const MptFrame& f, uint32_t pix, uint32_t seed) {
     return f.render_settings.freeze_random ? wang_hash(pix + 1u) : wang_hash((pix + 1u) * (uint32_t)(f.render_settings.sample_number + 1) * seed);
 }
 
-// Traced rays of the ReSTIR passes use alpha keys (pass pixel seed, 0, 5 + pass, ray counter)
+// Traced rays of the ReSTIR passes use alpha keys (pass pixel seed, 0, 5 + pass, position):
+// the position names the ray's site in the pass (not its rank among the rays traced so far),
+// the same positions as the GPU passes (restir_di.h RP_*)
+inline int RP_TFC(int k) { return 2 * k; }           // neighbour k's sample at the center
+inline int RP_TCN(int k) { return 2 * k + 1; }       // the canonical sample at neighbour k (pairwise MIS)
+constexpr int RP_T_TFC = 4000, RP_T_TCN = 4001;      // the temporal neighbour's pair
+inline int RP_GBH(int cur, int j) { return 10000 + cur * 1000 + j; }   // j = 999 / 998: temporal / center terms
+inline int RP_NORM(int j) { return 20000 + j; }
+inline int RP_LIGHT(int i) { return 100 + i; }
+inline int RP_BSDF(int i) { return 200 + i; }
+constexpr int RP_VISREUSE = 30000;
 struct RestirRays {
     Ctx& c;
     int kind;
     int n = 0;
+    RestirRays& at(int pos) { n = pos; return *this; }
     bool any(f3 o, f3 d, float tmax, int last) {
         c.rays_any++;
         uint32_t ak = c.alpha ? alpha_key(c.pseed, 0, kind, n++) : 0u;
@@ -136,7 +147,7 @@ void restir_visibility_reuse(Ctx& c, RestirRays& rr, OResv& r, f3 sp, int last) 
     f3 dir;
     if (r.flags & RF_ENVMAP) { dir = mat_x_vec(c.f->world_settings.envmap_to_world_matrix, r.point); dist = 1.0e35f; }
     else { dir = r.point - sp; dir = dir / (dist = length(dir)); }
-    if (rr.any(sp, dir, dist, last)) r.UCW = -1.0f;
+    if (rr.at(RP_VISREUSE).any(sp, dir, dist, last)) r.UCW = -1.0f;
     else r.flags |= RF_UNOCCLUDED;
 }
 
@@ -339,7 +350,7 @@ void restir_initial(Ctx& c, RestirPassCtx& R, int x, int y) {
         }
         // ReSTIR_DI_InitialTargetFunctionVisibility (InitialCandidates.h:248-264)
         if (f.options.restir_di_initial_target_visibility && target > 0.0f) {
-            if (rr.any(ep, tl, dist, g.prim)) { r.M++; continue; }
+            if (rr.at(RP_LIGHT(i)).any(ep, tl, dist, g.prim)) { r.M++; continue; }
             flags |= RF_UNOCCLUDED;
         }
         r.add_one_candidate(tri, point, target, flags, weight, rng);
@@ -354,7 +365,7 @@ void restir_initial(Ctx& c, RestirPassCtx& R, int x, int y) {
         if (!(bpdf > 0.0f)) continue;
         ShadowLightHit sh;
         c.rays_closest++;
-        uint32_t ak = c.alpha ? alpha_key(c.pseed, 0, rr.kind, rr.n++) : 0u;
+        uint32_t ak = c.alpha ? alpha_key(c.pseed, 0, rr.kind, RP_BSDF(i)) : 0u;
         Hit h = closest(s, g.first_hit, dir, g.prim, c.alpha ? &ak : nullptr);
         bool found = h.prim >= 0 && h.t < 1.0e35f - 1.0e-4f;
         if (found) {
@@ -578,13 +589,13 @@ void restir_spatiotemporal(Ctx& c, RestirPassCtx& R, int x, int y, std::vector<O
             int nj = valid_nb(j);
             if (nj == -1) continue;
             RSurface js = j == reuse ? cs : surface_of(nb_gb(nj, use_prev));
-            float tj = restir_target(c, rr, r.tri, r.point, r.flags, js, bvis);
+            float tj = restir_target(c, rr.at(RP_GBH(current, j)), r.tri, r.point, r.flags, js, bvis);
             int M = 1;
             if (cw) M = j == reuse ? ic.M : tin[(size_t)nj].M;
             denom += tj * (float)M;
             if (j + 1 == current) nume = tj * (float)M;
         }
-        float tt = restir_target(c, rr, r.tri, r.point, r.flags, ts, bvis);
+        float tt = restir_target(c, rr.at(RP_GBH(current, 999)), r.tri, r.point, r.flags, ts, bvis);
         int M = cw ? tres.M : 1;
         denom += tt * (float)M;
         if (current == 0) nume = tt * (float)M;
@@ -593,7 +604,7 @@ void restir_spatiotemporal(Ctx& c, RestirPassCtx& R, int x, int y, std::vector<O
     int selected = 0;
     if (tidx != -1 && tres.M > 0) {
         float tfc = 0.0f;
-        if (tres.UCW > 0.0f) tfc = restir_target(c, rr, tres.tri, tres.point, tres.flags, cs, bvis);
+        if (tres.UCW > 0.0f) tfc = restir_target(c, rr.at(RP_T_TFC), tres.tri, tres.point, tres.flags, cs, bvis);
         float jac = 1.0f;
         if (tfc > 0.0f && tres.UCW > 0.0f && !(tres.flags & RF_ENVMAP)) {
             const GB& tg = use_prev ? R.prev[(size_t)tidx] : R.cur[(size_t)tidx];
@@ -607,7 +618,7 @@ void restir_spatiotemporal(Ctx& c, RestirPassCtx& R, int x, int y, std::vector<O
         else if (mode == MPT_RESTIR_DI_BIAS_MIS_GBH) w = gbh(tres, 0);
         else {
             bool update_mc = ic.M > 0 && ic.UCW > 0.0f;
-            w = mis.weight(c, rr, rd, tres, ic, tfc, *tgb, vcount, vM, update_mc, false);
+            w = mis.weight(c, rr.at(RP_T_TCN), rd, tres, ic, tfc, *tgb, vcount, vM, update_mc, false);
         }
         if (o.combine_with(tres, w, tfc, jac, rng)) {
             selected = 0;
@@ -626,7 +637,7 @@ void restir_spatiotemporal(Ctx& c, RestirPassCtx& R, int x, int y, std::vector<O
         bool vis = spatial_visibility(f, rd, k, reuse);
         if (nr.UCW > 0.0f) {
             if (k == reuse) tfc = nr.target;
-            else tfc = restir_target(c, rr, nr.tri, nr.point, nr.flags, cs, vis);
+            else tfc = restir_target(c, rr.at(RP_TFC(k)), nr.tri, nr.point, nr.flags, cs, vis);
         }
         float jac = 1.0f;
         if (tfc > 0.0f && nr.UCW > 0.0f && k != reuse && !(nr.flags & RF_ENVMAP)) {
@@ -643,7 +654,7 @@ void restir_spatiotemporal(Ctx& c, RestirPassCtx& R, int x, int y, std::vector<O
             if (nr.UCW == 0.0f && !update_mc) w = 1.0f;
             else {
                 const GB& ng = use_prev ? R.prev[(size_t)ni] : R.cur[(size_t)ni];
-                w = mis.weight(c, rr, rd, nr, ic, tfc, ng, vcount, vM, update_mc, k == reuse);
+                w = mis.weight(c, rr.at(RP_TCN(k)), rd, nr, ic, tfc, ng, vcount, vM, update_mc, k == reuse);
             }
         }
         if (o.combine_with(nr, w, tfc, jac, rng)) {
@@ -668,7 +679,7 @@ void restir_spatiotemporal(Ctx& c, RestirPassCtx& R, int x, int y, std::vector<O
             }
             // the MIS-like loop reads the current frame's G-buffer (SpatiotemporalNormalizationWeight.h:130)
             RSurface js = j == reuse ? cs : surface_of(nb_gb(nj, mode == MPT_RESTIR_DI_BIAS_MIS_LIKE ? false : use_prev));
-            float tj = restir_target(c, rr, o.tri, o.point, o.flags, js, bvis);
+            float tj = restir_target(c, rr.at(RP_NORM(j)), o.tri, o.point, o.flags, js, bvis);
             if (tj > 0.0f) {
                 if (mode == MPT_RESTIR_DI_BIAS_1_OVER_Z) nd += (float)(j == reuse ? ic.M : tin[(size_t)nj].M);
                 else {
@@ -681,7 +692,7 @@ void restir_spatiotemporal(Ctx& c, RestirPassCtx& R, int x, int y, std::vector<O
         }
         if (mode == MPT_RESTIR_DI_BIAS_1_OVER_M) nd += (float)tres.M;
         else {
-            float tt = restir_target(c, rr, o.tri, o.point, o.flags, ts, bvis);
+            float tt = restir_target(c, rr.at(RP_NORM(999)), o.tri, o.point, o.flags, ts, bvis);
             if (mode == MPT_RESTIR_DI_BIAS_1_OVER_Z) { if (tt > 0.0f) nd += (float)tres.M; }
             else {
                 if (selected == 0) nn += tt;
@@ -736,9 +747,10 @@ void restir_temporal(Ctx& c, RestirPassCtx& R, int x, int y, std::vector<OResv>&
     int selected = 0;   // MIS-like: TEMPORAL_NEIGHBOR_ID 0 / INITIAL_CANDIDATES_ID 1
     // ReSTIRDITemporalResamplingMISWeight<MIS_GBH> (TemporalMISWeight.h:62-110)
     auto gbh = [&](const OResv& r, bool temporal_id) -> float {
-        float tt = restir_target(c, rr, r.tri, r.point, r.flags, ts, bvis);
+        const int cur = temporal_id ? 0 : 1;
+        float tt = restir_target(c, rr.at(RP_GBH(cur, 999)), r.tri, r.point, r.flags, ts, bvis);
         if (temporal_id && tt == 0.0f) return 0.0f;
-        float tc = restir_target(c, rr, r.tri, r.point, r.flags, cs, bvis);
+        float tc = restir_target(c, rr.at(RP_GBH(cur, 998)), r.tri, r.point, r.flags, cs, bvis);
         int tM = cw ? tres.M : 1, cM = cw ? ic.M : 1;
         float nume = temporal_id ? tt * (float)tM : tc * (float)cM;
         float denom = tt * (float)tM + tc * (float)cM;
@@ -746,7 +758,7 @@ void restir_temporal(Ctx& c, RestirPassCtx& R, int x, int y, std::vector<OResv>&
     };
     {
         float tfc = 0.0f;
-        if (tres.UCW > 0.0f) tfc = restir_target(c, rr, tres.tri, tres.point, tres.flags, cs, bvis);
+        if (tres.UCW > 0.0f) tfc = restir_target(c, rr.at(RP_T_TFC), tres.tri, tres.point, tres.flags, cs, bvis);
         float jac = 1.0f;
         if (tfc > 0.0f && tres.UCW > 0.0f && !(tres.flags & RF_ENVMAP)) {
             jac = restir_jacobian(s, tres, cs.sp, ts.sp - ts.sn * 1.0e-4f);
@@ -765,7 +777,7 @@ void restir_temporal(Ctx& c, RestirPassCtx& R, int x, int y, std::vector<OResv>&
             float denom = tfn * nsum + tfc * cM;
             float mi = denom == 0.0f ? 0.0f : (nume / denom);
             if (def && cw) mi *= nsum / (nsum + cM);
-            float tcn = restir_target(c, rr, ic.tri, ic.point, ic.flags, ts, bvis);
+            float tcn = restir_target(c, rr.at(RP_T_TCN), ic.tri, ic.point, ic.flags, ts, bvis);
             float tcc = ic.target;
             float nume_mc = tcc * cM;
             float denom_mc = tcn * nsum + tcc * cM;
@@ -798,13 +810,13 @@ void restir_temporal(Ctx& c, RestirPassCtx& R, int x, int y, std::vector<OResv>&
         if (mode == MPT_RESTIR_DI_BIAS_1_OVER_M) nd = (float)(ic.M + tres.M);
         else if (mode == MPT_RESTIR_DI_BIAS_1_OVER_Z) {
             nd = 0.0f;
-            float tc = restir_target(c, rr, o.tri, o.point, o.flags, cs, bvis);
+            float tc = restir_target(c, rr.at(RP_NORM(998)), o.tri, o.point, o.flags, cs, bvis);
             nd += (float)((tc > 0.0f) * ic.M);
-            float tt = restir_target(c, rr, o.tri, o.point, o.flags, ts, bvis);
+            float tt = restir_target(c, rr.at(RP_NORM(999)), o.tri, o.point, o.flags, ts, bvis);
             nd += (float)((tt > 0.0f) * tres.M);
         } else if (mode == MPT_RESTIR_DI_BIAS_MIS_LIKE) {
-            float tc = restir_target(c, rr, o.tri, o.point, o.flags, cs, bvis);
-            float tt = restir_target(c, rr, o.tri, o.point, o.flags, ts, bvis);
+            float tc = restir_target(c, rr.at(RP_NORM(998)), o.tri, o.point, o.flags, cs, bvis);
+            float tt = restir_target(c, rr.at(RP_NORM(999)), o.tri, o.point, o.flags, ts, bvis);
             nn = selected == 1 ? tc : tt;
             int icM = cw ? ic.M : 1, tM = cw ? tres.M : 1;
             nd = tc * (float)icM + tt * (float)tM;
@@ -872,7 +884,7 @@ void restir_spatial(Ctx& c, RestirPassCtx& R, int x, int y, int pass, std::vecto
         bool vis = spatial_visibility(f, rd, k, reuse);
         if (nr.UCW > 0.0f) {
             if (k == reuse) tfc = nr.target;
-            else tfc = restir_target(c, rr, nr.tri, nr.point, nr.flags, cs, vis);
+            else tfc = restir_target(c, rr.at(RP_TFC(k)), nr.tri, nr.point, nr.flags, cs, vis);
         }
         float jac = 1.0f;
         if (tfc > 0.0f && nr.UCW > 0.0f && k != reuse && !(nr.flags & RF_ENVMAP)) {
@@ -892,7 +904,7 @@ void restir_spatial(Ctx& c, RestirPassCtx& R, int x, int y, int pass, std::vecto
                     int nj = valid_nb(j);
                     if (nj == -1) continue;
                     RSurface js = surface_of(R.cur[(size_t)nj]);
-                    float tj = restir_target(c, rr, nr.tri, nr.point, nr.flags, js, bvis);
+                    float tj = restir_target(c, rr.at(RP_GBH(k, j)), nr.tri, nr.point, nr.flags, js, bvis);
                     int M = cw ? in[(size_t)nj].M : 1;
                     denom += tj * (float)M;
                     if (j == k) nume = tj * (float)M;
@@ -901,7 +913,7 @@ void restir_spatial(Ctx& c, RestirPassCtx& R, int x, int y, int pass, std::vecto
             }
         } else {
             bool update_mc = cres.M > 0 && cres.UCW > 0.0f;
-            w = mis.weight(c, rr, rd, nr, cres, tfc, R.cur[(size_t)ni], vcount, vM, update_mc, k == reuse);
+            w = mis.weight(c, rr.at(RP_TCN(k)), rd, nr, cres, tfc, R.cur[(size_t)ni], vcount, vM, update_mc, k == reuse);
         }
         if (o.combine_with(nr, w, tfc, jac, rng)) {
             selected = k;
@@ -921,7 +933,7 @@ void restir_spatial(Ctx& c, RestirPassCtx& R, int x, int y, int pass, std::vecto
             if (nj == -1) continue;
             if (mode == MPT_RESTIR_DI_BIAS_1_OVER_M) { nd += (float)in[(size_t)nj].M; continue; }
             RSurface js = surface_of(R.cur[(size_t)nj]);
-            float tj = restir_target(c, rr, o.tri, o.point, o.flags, js, bvis);
+            float tj = restir_target(c, rr.at(RP_NORM(j)), o.tri, o.point, o.flags, js, bvis);
             if (tj > 0.0f) {
                 int M = in[(size_t)nj].M;
                 if (mode == MPT_RESTIR_DI_BIAS_1_OVER_Z) nd += (float)M;

@@ -159,3 +159,25 @@ def test_c5_16_bounces_4k_crop_bit_exact(luts, name, strategy):
     for k, what in enumerate(["color", "albedo", "normals"]):
         _same(got[k], ref[k], f"C5 {name} {strategy} {what}")
     assert got[0].mean() > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fused", [True, False], ids=["fused", "unfused"])
+def test_c4_restir_staged_equals_monolithic(city, luts, city_oracle, fused, monkeypatch):
+    """The staged spatial pass (gather, traced ray list, combine, staged visibility reuse;
+    restir_di.h) against the monolithic kernel (MPT_RESTIR_STAGED=0) on the C4 city frame with
+    alpha testing: the same sums and the same ray counts, bit for bit."""
+    _, env = city_oracle
+    frs = c4_frames(city, 3, fused=fused, passes=2 if fused else 1)
+    out = {}
+    for mode in ("monolithic", "staged"):
+        monkeypatch.setenv("MPT_RESTIR_STAGED", "0" if mode == "monolithic" else "1")
+        r = _gpu(city, luts, env)
+        r.render_samples(frs)
+        r.synchronize_kernel()
+        out[mode] = r.framebuffer(abi.FB_COLOR)
+        st = r.stats()
+        out[mode + "_rays"] = (st.rays_any, st.rays_closest)
+        r.close()
+    _same(out["staged"], out["monolithic"], "C4 staged vs monolithic")
+    assert out["staged_rays"] == out["monolithic_rays"], (out["staged_rays"], out["monolithic_rays"])

@@ -45,7 +45,8 @@ def _read_out(path):
     fs = C.sizeof(abi.Frame)
     frames = [abi.Frame.from_buffer_copy(raw, 4 + i * fs) for i in range(n)]
     img = np.frombuffer(raw, np.float32, W * H * 3, 4 + n * fs).reshape(H, W, 3)
-    return frames, img
+    cnt = np.frombuffer(raw, np.int32, W * H, 4 + n * fs + W * H * 12).reshape(H, W)
+    return frames, img, cnt
 
 
 def test_host_driver_built():
@@ -99,7 +100,7 @@ def test_cpp_gpurenderer_matches_oracle(cornell, luts, tmp_path, case):
     _blob(blob, cornell, luts, st, abi.WorldSettings.default(), opt, cam, c["updates"], c.get("mode", 0), mats2)
     r = subprocess.run([str(_build.HOST_TEST), str(blob), str(out)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
-    frames, img = _read_out(out)
+    frames, img, cnt = _read_out(out)
     n = c["spf"] * c["updates"]
     assert len(frames) == n
     restir = c["lss"] == abi.LSS_RESTIR_DI
@@ -114,6 +115,8 @@ def test_cpp_gpurenderer_matches_oracle(cornell, luts, tmp_path, case):
         import copy
         sd = copy.copy(cornell)
         sd.materials = mats2
-    ref = orc.Oracle(sd, luts).render(frames)
+    o = orc.Oracle(sd, luts)
+    ref = o.render(frames)
     assert np.array_equal(img, ref), f"{case}: {(img != ref).sum()} values differ"
+    assert np.array_equal(cnt, o.last_aux["sample_count"]), f"{case}: pixel_sample_count differs"
     assert img.mean() > 0
