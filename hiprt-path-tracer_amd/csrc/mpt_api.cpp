@@ -169,7 +169,7 @@ struct MptContext {
     DBuf<float4> rq_o, rq_d, rq_rec;
     DBuf<uint32_t> rq_key;
     DBuf<uint8_t> rq_occ;
-    DBuf<int32_t> rq_list;
+    DBuf<int32_t> rq_list, rq_items;
     DBuf<int4> rq_meta;
     int restir_out_sp2 = 0;
     MptHaloExchangeFn halo_fn = nullptr;   // ReSTIR DI across a row partition
@@ -319,7 +319,7 @@ DevPaths dev_paths(MptContext* c) {
     P.xq_o = c->xq_o.p; P.xq_d = c->xq_d.p; P.xq_hit = c->xq_hit.p; P.xq_occ = c->xq_occ.p; P.xq_flag = c->xq_flag.p;
     P.xrec = c->xrec.p; P.xl_any = c->xl_any.p; P.xl_cl = c->xl_cl.p; P.xl_light = c->xl_light.p;
     P.rq_o = c->rq_o.p; P.rq_d = c->rq_d.p; P.rq_key = c->rq_key.p; P.rq_occ = c->rq_occ.p; P.rq_list = c->rq_list.p;
-    P.rq_meta = c->rq_meta.p; P.rq_rec = c->rq_rec.p;
+    P.rq_items = c->rq_items.p; P.rq_meta = c->rq_meta.p; P.rq_rec = c->rq_rec.p;
     return P;
 }
 
@@ -558,7 +558,7 @@ int build_light_bvh(MptContext* c) {
 void release_restir(MptContext* c) {
     release_all(c->gb_pos, c->gb_sn, c->gb_gn, c->gb_view, c->pgb_pos, c->pgb_sn, c->pgb_gn, c->pgb_view, c->gb_meta,
                 c->pgb_meta, c->gb_vsA, c->gb_vsB, c->pgb_vsA, c->pgb_vsB, c->gb_mat, c->pgb_mat, c->rs_init, c->rs_sp1,
-                c->rs_sp2, c->rs_plights, c->rs_conv, c->rq_o, c->rq_d, c->rq_rec, c->rq_key, c->rq_occ, c->rq_list, c->rq_meta);
+                c->rs_sp2, c->rs_plights, c->rs_conv, c->rq_o, c->rq_d, c->rq_rec, c->rq_key, c->rq_occ, c->rq_list, c->rq_items, c->rq_meta);
     c->restir_out_sp2 = 0;
 }
 
@@ -601,7 +601,7 @@ int ensure_restir(MptContext* c, const MptFrame* f) {
         const size_t ns = (size_t)std::max(c->n_slots, 1);
         if (c->rq_meta.n != ns) {
             A(c->rq_o, ns * RS_RPP_HOST); A(c->rq_d, ns * RS_RPP_HOST); A(c->rq_key, ns * RS_RPP_HOST);
-            A(c->rq_occ, ns * RS_RPP_HOST); A(c->rq_list, ns * RS_RPP_HOST);
+            A(c->rq_occ, ns * RS_RPP_HOST); A(c->rq_list, ns * RS_RPP_HOST); A(c->rq_items, 2 * ns * RS_RPP_HOST);
             A(c->rq_meta, ns); A(c->rq_rec, ns * RS_KMAX_HOST);
         }
     }

@@ -203,6 +203,7 @@ struct DevPaths {
     uint32_t* rq_key;
     uint8_t* rq_occ;
     int32_t* rq_list;
+    int32_t* rq_items;        // target-evaluation items by class (2 x RS_RPP per pixel slot)
     int4* rq_meta;
     float4* rq_rec;
 };
@@ -233,6 +234,7 @@ enum {
     CTR_LIGHT = 10,           // length of nq_light (k_trace TM_NEE_LIGHT)
     CTR_XANY = 11, CTR_XCL = 12, CTR_XLIGHT = 13,   // ext query lists (extended light sampling)
     CTR_RQ = 14, CTR_RQV = 15,                      // staged ReSTIR DI rays / visibility-reuse rays
+    CTR_RQE0 = 16, CTR_RQE1 = 17,                   // staged ReSTIR DI target evaluations: plain / generic class
     CTR_COUNT = 20
 };
 

@@ -309,9 +309,12 @@ DEV bool traverse(const DevScene& S, v3 o, v3 d, int last_hit, float tmax, THit&
 // TM_LIST_ANY: any-hit queries staged by the ReSTIR DI reuse passes (raw_o / raw_d / raw_key
 // at the positions of a compacted list; results in raw_occ), reported in the raw any-hit
 // stage's instrumentation counters (raw queries never run inside a render).
+// TM_LIST_CLOSEST: the same for closest-hit queries (hit written to raw_hit at the ray's position).
 enum TraceMode { TM_PATH = 0, TM_NEE_ANY = 1, TM_NEE_CLOSEST = 2, TM_RAW_CLOSEST = 3, TM_RAW_ANY = 4, TM_NEE_LIGHT = 5,
-                 TM_NEE_LIGHT_OCC = 6, TM_LIST_ANY = 7 };
-constexpr int trace_stage(int mode) { return mode == TM_LIST_ANY ? TM_RAW_ANY : mode >= TM_NEE_LIGHT ? TM_NEE_CLOSEST : mode; }
+                 TM_NEE_LIGHT_OCC = 6, TM_LIST_ANY = 7, TM_LIST_CLOSEST = 8 };
+constexpr int trace_stage(int mode) {
+    return mode == TM_LIST_ANY ? TM_RAW_ANY : mode == TM_LIST_CLOSEST ? TM_RAW_CLOSEST : mode >= TM_NEE_LIGHT ? TM_NEE_CLOSEST : mode;
+}
 // Short traversals (the light BVH: ~1.5 nodes per query) run one query per lane over a grid
 // covering the list instead of persistent waves: with so little work per query the shared
 // work counter of the persistent kernel (one device-scope atomic per wave refill) is what
@@ -449,12 +452,12 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MODE == TM_P
                         }
                         tr.init(mk3(ro.x, ro.y, ro.z), mk3(rd.x, rd.y, rd.z), (int)__float_as_uint(ro.w), tmax, al, akey);
                         if (MODE == TM_NEE_LIGHT && S.n_light_tris == 0) tr.gk = 0u;   // no light: nothing to traverse
-                    } else if (MODE == TM_LIST_ANY) {
+                    } else if (MODE == TM_LIST_ANY || MODE == TM_LIST_CLOSEST) {
                         ray = A.queue[i];
                         ro = A.raw_o[ray];
                         rd = A.raw_d[ray];
-                        tr.init(mk3(ro.x, ro.y, ro.z), mk3(rd.x, rd.y, rd.z), (int)__float_as_uint(ro.w), rd.w, A.alpha != 0,
-                                A.alpha ? A.raw_key[ray] : 0u);
+                        tr.init(mk3(ro.x, ro.y, ro.z), mk3(rd.x, rd.y, rd.z), (int)__float_as_uint(ro.w), ANY ? rd.w : INFINITY,
+                                A.alpha != 0, A.alpha ? A.raw_key[ray] : 0u);
                     } else {
                         ray = i;
                         ro = A.raw_o[i];
@@ -2195,8 +2198,8 @@ void part_shade_generic(dim3 g, hipStream_t st, const ShadeArgs& a);          //
 void part_shade_plain(dim3 g, hipStream_t st, const ShadeArgs& a);            // k_shade<NONE, true>
 void part_shade_ext(dim3 g, hipStream_t st, const ShadeArgs& a);              // k_shade<NONE, false, true>
 void part_shade_override(int ovr, bool ext, dim3 g, hipStream_t st, const ShadeArgs& a);   // Lambert, Oren-Nayar
-enum RestirKernel { RK_INITIAL, RK_SPATIOTEMPORAL, RK_SPATIOTEMPORAL_ANY, RK_SPATIAL, RK_SPATIAL_ANY, RK_TEMPORAL, RK_SP_GATHER,
-                   RK_SP_COMBINE };
+enum RestirKernel { RK_INITIAL, RK_SPATIOTEMPORAL, RK_SPATIOTEMPORAL_ANY, RK_SPATIAL, RK_SPATIAL_ANY, RK_TEMPORAL, RK_SP_SELECT,
+                   RK_SP_EVAL_PLAIN, RK_SP_EVAL_GENERIC, RK_SP_COMBINE, RK_INITIAL_STAGED_PLAIN, RK_INITIAL_STAGED_GENERIC };
 void part_restir_principled(int kind, dim3 g, hipStream_t st, const DevScene& S, const DevPaths& P, const MptFrame* F,
                             int pass, const float4* in, float4* out);
 void part_restir_override(int ovr, int kind, dim3 g, hipStream_t st, const DevScene& S, const DevPaths& P,
@@ -2282,8 +2285,8 @@ static int halo_exchange(const MptFrame& hf, LaunchCfg& cfg, hipStream_t st, int
     return x.halo_rows;
 }
 
-// One spatial reuse pass: staged (gather, traced rays, combine, visibility reuse;
-// restir_di.h) when the reference-default weights are selected and the neighbour counts fit
+// One spatial reuse pass: staged (selection, class-sorted target evaluations, traced rays,
+// combine, visibility reuse; restir_di.h) when the reference-default weights are selected and the neighbour counts fit
 // RS_KMAX, else the monolithic kernel.
 static void launch_spatial_pass(int ovr, bool def_bias, const MptFrame& hf, LaunchCfg& cfg, dim3 g, hipStream_t st,
                                 const DevScene& S, const DevPaths& P, const MptFrame* d_frame, int pass, const float4* in,
@@ -2296,8 +2299,10 @@ static void launch_spatial_pass(int ovr, bool def_bias, const MptFrame& hf, Laun
         return;
     }
     const dim3 gp(blocks_for(P.n));
-    hipMemsetAsync(&P.counters[CTR_RQ], 0, 2 * sizeof(int32_t), st);   // CTR_RQ, CTR_RQV
-    launch_restir_kernel(ovr, RK_SP_GATHER, gp, st, S, P, d_frame, pass, in, out);
+    hipMemsetAsync(&P.counters[CTR_RQ], 0, 4 * sizeof(int32_t), st);   // CTR_RQ, CTR_RQV, CTR_RQE0, CTR_RQE1
+    launch_restir_kernel(ovr, RK_SP_SELECT, gp, st, S, P, d_frame, pass, in, out);
+    launch_restir_kernel(ovr, RK_SP_EVAL_PLAIN, g, st, S, P, d_frame, pass, in, out);
+    launch_restir_kernel(ovr, RK_SP_EVAL_GENERIC, g, st, S, P, d_frame, pass, in, out);
     TraceArgs ta{};
     ta.S = S; ta.P = P; ta.queue = P.rq_list; ta.count_ptr = &P.counters[CTR_RQ]; ta.fetch = &P.counters[CTR_FETCH];
     ta.raw_o = P.rq_o; ta.raw_d = P.rq_d; ta.raw_key = P.rq_key; ta.raw_occ = P.rq_occ;
@@ -2351,7 +2356,30 @@ static void launch_restir(const DevScene& S, DevPaths& P, const MptFrame* d_fram
     const dim3 g(cfg.grid_persistent);
     {
         TimedScope tk(cfg, st, KT_RS_INITIAL);
-        launch_restir_kernel(ovr, RK_INITIAL, g, st, S, P, d_frame);
+        // staged (the BSDF candidate's ray through k_trace<TM_LIST_CLOSEST>) for the reference
+        // defaults: at most one BSDF candidate, no visibility in the initial target function
+        const bool staged = cfg.restir_staged && P.rq_o && rd.number_of_initial_bsdf_candidates <= 1 &&
+                            !hf.options.restir_di_initial_target_visibility;
+        if (!staged) launch_restir_kernel(ovr, RK_INITIAL, g, st, S, P, d_frame);
+        else {
+            const dim3 gp(blocks_for(P.n));
+            hipMemsetAsync(&P.counters[CTR_RQ], 0, 4 * sizeof(int32_t), st);   // CTR_RQ, CTR_RQV, CTR_RQE0, CTR_RQE1
+            hipLaunchKernelGGL(k_rsi_classify, gp, dim3(TB), 0, st, S, P, d_frame, ovr == MPT_BSDF_NONE ? 1 : 0);
+            launch_restir_kernel(ovr, RK_INITIAL_STAGED_PLAIN, g, st, S, P, d_frame);
+            launch_restir_kernel(ovr, RK_INITIAL_STAGED_GENERIC, g, st, S, P, d_frame);
+            TraceArgs ta{};
+            ta.S = S; ta.P = P; ta.queue = P.rq_list; ta.count_ptr = &P.counters[CTR_RQ]; ta.fetch = &P.counters[CTR_FETCH];
+            ta.raw_o = P.rq_o; ta.raw_d = P.rq_d; ta.raw_key = P.rq_key; ta.raw_occ = P.rq_occ;
+            ta.raw_hit = P.rq_o;   // each hit written over its own (already read) ray origin
+            ta.F = d_frame; ta.alpha = hf.render_settings.do_alpha_testing ? 1 : 0;
+            hipMemsetAsync(&P.counters[CTR_FETCH], 0, sizeof(int32_t), st);
+            launch_trace_mode<TM_LIST_CLOSEST>(ta, cfg.grid_persistent, cfg.stats, st);
+            hipLaunchKernelGGL(k_rsi_finish, gp, dim3(TB), 0, st, S, P, d_frame);
+            ta.count_ptr = &P.counters[CTR_RQV];
+            hipMemsetAsync(&P.counters[CTR_FETCH], 0, sizeof(int32_t), st);
+            launch_trace_mode<TM_LIST_ANY>(ta, cfg.grid_persistent, cfg.stats, st);
+            hipLaunchKernelGGL(k_rs_visapply, gp, dim3(TB), 0, st, P, P.rs_init);
+        }
     }
     float4* last_out = restir_buffer(P, cfg.restir_out_sp2);
     // the reference-default weights run a kernel variant with the mode compiled in

@@ -47,7 +47,16 @@ static void restir_kernel(int kind, dim3 g, hipStream_t st, const DevScene& S, c
                           const float4* in, float4* out) {
     constexpr int DEF = MPT_RESTIR_DI_BIAS_PAIRWISE_MIS_DEFENSIVE;
     switch (kind) {
-    case RK_INITIAL: hipLaunchKernelGGL(k_restir_initial<OVR>, g, dim3(TB), 0, st, S, P, F); break;
+    case RK_INITIAL: hipLaunchKernelGGL((k_restir_initial<OVR, false>), g, dim3(TB), 0, st, S, P, F, nullptr, nullptr); break;
+    // staged initial candidates over k_rsi_classify's lists (the plain class: Principled only)
+    case RK_INITIAL_STAGED_PLAIN:
+        if (OVR == MPT_BSDF_NONE)
+            hipLaunchKernelGGL((k_restir_initial<OVR, true, true>), g, dim3(TB), 0, st, S, P, F, P.rq_items, &P.counters[CTR_RQE0]);
+        break;
+    case RK_INITIAL_STAGED_GENERIC:
+        hipLaunchKernelGGL((k_restir_initial<OVR, true, false>), g, dim3(TB), 0, st, S, P, F, P.rq_items + P.n,
+                           &P.counters[CTR_RQE1]);
+        break;
     case RK_SPATIOTEMPORAL: hipLaunchKernelGGL((k_restir_spatiotemporal<OVR, DEF>), g, dim3(TB), 0, st, S, P, F); break;
     case RK_SPATIOTEMPORAL_ANY: hipLaunchKernelGGL((k_restir_spatiotemporal<OVR, -1>), g, dim3(TB), 0, st, S, P, F); break;
     case RK_SPATIAL:
@@ -56,8 +65,16 @@ static void restir_kernel(int kind, dim3 g, hipStream_t st, const DevScene& S, c
     case RK_SPATIAL_ANY:
         hipLaunchKernelGGL((k_restir_spatial<OVR, -1>), g, dim3(TB), 0, st, S, P, F, pass, in, out);
         break;
-    // the staged spatial pass (restir_di.h): gather and combine
-    case RK_SP_GATHER: hipLaunchKernelGGL(k_rsp_gather<OVR>, g, dim3(TB), 0, st, S, P, F, pass, in); break;
+    // the staged spatial pass (restir_di.h): selection, class-sorted evaluations, combine
+    case RK_SP_SELECT: hipLaunchKernelGGL(k_rsp_select<OVR>, g, dim3(TB), 0, st, S, P, F, pass, in); break;
+    case RK_SP_EVAL_PLAIN:   // (only the Principled BSDF has the plain class)
+        if (OVR == MPT_BSDF_NONE)
+            hipLaunchKernelGGL((k_rsp_eval<OVR, true>), g, dim3(TB), 0, st, S, P, F, pass, in, P.rq_items, &P.counters[CTR_RQE0]);
+        break;
+    case RK_SP_EVAL_GENERIC:
+        hipLaunchKernelGGL((k_rsp_eval<OVR, false>), g, dim3(TB), 0, st, S, P, F, pass, in, P.rq_items + (size_t)P.n * RS_RPP,
+                           &P.counters[CTR_RQE1]);
+        break;
     case RK_SP_COMBINE: hipLaunchKernelGGL(k_rsp_combine<OVR>, g, dim3(TB), 0, st, S, P, F, pass, in, out); break;
     default: hipLaunchKernelGGL(k_restir_temporal<OVR>, g, dim3(TB), 0, st, S, P, F, in, out); break;
     }

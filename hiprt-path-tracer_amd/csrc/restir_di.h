@@ -94,6 +94,55 @@ DEV void count_pass_rays(const DevPaths& P, uint32_t n_any, uint32_t n_closest) 
     }
 }
 
+// ---- staged passes: ray positions, block-aggregated list appends ----------------------
+struct TgtRay { v3 o, d; float dist; };   // a shadow ray of a target function / visibility test
+constexpr int RS_KMAX = RS_KMAX_HOST, RS_RPP = RS_RPP_HOST;   // neighbours a staged pass supports; ray positions per pixel
+enum : int { RSM_SKIP = 1 };                      // rq_meta.x: the pixel is not resampled (output untouched)
+
+// exclusive scan of one int per thread over a TB-thread block; total to `total`
+DEV int rs_block_scan(int v, int* tmp, int& total) {
+    const int lane = lane_id(), wid = threadIdx.x >> 6;
+    constexpr int NW = TB / 64;
+    int x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        int y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) tmp[wid] = x;
+    __syncthreads();
+    int before = 0, all = 0;
+#pragma unroll
+    for (int w = 0; w < NW; w++) {
+        const int tw = tmp[w];
+        if (w < wid) before += tw;
+        all += tw;
+    }
+    __syncthreads();
+    total = all;
+    return before + x - v;
+}
+
+DEV void rs_stage_ray(const DevPaths& P, size_t id, const TgtRay& r, int last, uint32_t key) {
+    P.rq_o[id] = make_float4(r.o.x, r.o.y, r.o.z, __uint_as_float((uint32_t)last));
+    P.rq_d[id] = make_float4(r.d.x, r.d.y, r.d.z, r.dist - 1.0e-4f);
+    P.rq_key[id] = key;
+}
+
+// appends the ray positions in `mask` of slot s to the list behind `counter` (one atomic per block)
+DEV void rs_append(const DevPaths& P, int32_t* counter, int s, uint32_t mask, int* tmp, int* base) {
+    int tot;
+    const int off = rs_block_scan(__popc(mask), tmp, tot);
+    if (threadIdx.x == 0) *base = tot ? atomicAdd(counter, tot) : 0;
+    __syncthreads();
+    int o = *base + off;
+    while (mask) {
+        const int j = __builtin_ctz(mask);
+        mask &= mask - 1u;
+        P.rq_list[o++] = s * RS_RPP + j;
+    }
+}
+
 DEV float power_heuristic(float a, int na, float b, int nb) {   // Sampling.h:75-87
     float pa = ((float)na * a) * ((float)na * a);
     float pb = ((float)nb * b) * ((float)nb * b);
@@ -138,9 +187,11 @@ DEV void rr_end_normalized(RResv& r) { rr_end_norm(r, 1.0f, 1.0f); }   // the pa
 
 // ReSTIR_DI_evaluate_target_function<vis> (Utils.h:20-128), split at the visibility test:
 // restir_target_unocc returns the target before it (0 = no ray would be traced) and the
-// shadow ray the test traces (its distance; evaluate_shadow_ray traces to distance - 1e-4,
-// Intersect.h:227)
-struct TgtRay { v3 o, d; float dist; };
+// shadow ray the test traces (TgtRay: its distance; evaluate_shadow_ray traces to
+// distance - 1e-4, Intersect.h:227)
+// PLAIN: the surface is a plain dielectric seen from outside (rs_plain): the Principled BSDF
+// with the zero-weight lobes compiled out (dev_bsdf.h FULL = false), bit for bit the same
+template <bool PLAIN = false>
 DEV float restir_target_unocc(const DevScene& S, const MptFrame& F, const BCtx& bc, int tri, v3 point, uint32_t flags,
                               const RSurf& s, bool vis, int ovr, TgtRay& ray) {
     if (tri == -1 && !(flags & RF_ENVMAP)) return 0.0f;
@@ -153,9 +204,16 @@ DEV float restir_target_unocc(const DevScene& S, const MptFrame& F, const BCtx& 
     if (cosv == 0.0f) return 0.0f;
     float bp;
     VState tv = s.vs;
-    Col f = ovr == MPT_BSDF_LAMBERTIAN   ? bsdf_eval<MPT_BSDF_LAMBERTIAN>(bc, *s.m, tv, s.view, s.sn, dir, bp)
+    Col f;
+    if (PLAIN) {
+        PEval pe;
+        bsdf_eval_pre<MPT_BSDF_NONE, false>(bc, *s.m, tv, s.view, s.sn, pe);
+        f = bsdf_eval_post<MPT_BSDF_NONE, false>(bc, *s.m, tv, pe, s.sn, dir, bp);
+    } else {
+        f = ovr == MPT_BSDF_LAMBERTIAN   ? bsdf_eval<MPT_BSDF_LAMBERTIAN>(bc, *s.m, tv, s.view, s.sn, dir, bp)
             : ovr == MPT_BSDF_OREN_NAYAR ? bsdf_eval<MPT_BSDF_OREN_NAYAR>(bc, *s.m, tv, s.view, s.sn, dir, bp)
                                          : bsdf_eval<MPT_BSDF_NONE>(bc, *s.m, tv, s.view, s.sn, dir, bp);
+    }
     Col e;
     if (flags & RF_ENVMAP) { float ep; e = env_eval(S, F, dir, ep); }
     else e = emission_of(S.mats[S.mat_idx[tri]]);
@@ -453,19 +511,89 @@ __global__ __launch_bounds__(TB) void k_restir_presample(DevScene S, DevPaths P,
 }
 #endif
 
+// the evaluation class of a G-buffer surface: plain dielectric seen from outside (the
+// condition k_shade<PLAIN> checks before it shades, principled_eval_pre's 'outside')
+DEV bool rs_plain(const DevScene& S, const DevPaths& P, int pix, const RSurf& g) {
+    const int mi = P.gb_meta[pix].y - 1;
+    return mi >= 0 && !(S.mat_tex[mi] & MT_FULL) && (dot(g.view, g.sn) > 0.0f || g.m->thin_walled);
+}
+
 // ---- ReSTIR_DI_InitialCandidates (InitialCandidates.h:24-508) ------------------------
-template <int OVR>
-RESTIR_KERNEL void k_restir_initial(DevScene S, DevPaths P, const MptFrame* __restrict__ Fp) {
-    __shared__ uint2 lds[LDS_STACK * TB];
+// The BSDF candidate once its ray is traced (InitialCandidates.h:296-394): found = a closest
+// hit below 1e35 - 1e-4 with hit record h (t, u, v, prim).
+DEV void initial_bsdf_candidate(const DevScene& S, const MptFrame& F, v3 gp, v3 gsn, v3 dir, Col f, float bpdf, bool refr,
+                                bool found, float4 h, float env_p, int nl, int nb, RResv& r, Rng& rng) {
+    const MptWorldSettings& w = F.world_settings;
+    ShadowLightHit sh;
+    if (found) found = shadow_light_hit(S, h, sh);
+    if (found && !is_black(sh.em)) {
+        float ce = absr(dot(gsn, dir));
+        Col lc = f * sh.em * ce;
+        float tf = lum(lc);
+        float lpdf = 0.0f;
+        if (!refr) lpdf = pdf_emissive_hit(S, sh, dir);
+        if (!min_contrib(F.render_settings.minimum_light_contribution, lc / lpdf / bpdf)) { r.M++; return; }
+        lpdf *= (1.0f - env_p);
+        float mis = power_heuristic(bpdf, nb, lpdf, nl);
+        float weight = mis * tf / bpdf;
+        rr_add(r, sh.prim, gp + dir * sh.dist, tf, RF_UNOCCLUDED | (refr ? RF_BSDF_REFRACTION : 0u), weight, rng);
+    } else if (!found && w.ambient_light_type == MPT_AMBIENT_ENVMAP) {
+        float ce = maxr(0.0f, dot(gsn, dir));
+        if (ce > 0.0f) {
+            float epdf;
+            Col er = env_eval(S, F, dir, epdf);
+            Col ec = f * er * ce;
+            if (!min_contrib(F.render_settings.minimum_light_contribution, ec / epdf / bpdf)) { r.M++; return; }
+            float tf = lum(ec);
+            epdf *= env_p;
+            float mis = power_heuristic(bpdf, nb, epdf, nl);
+            float weight = mis * tf / bpdf;
+            rr_add(r, -1, mat_x_vec(w.world_to_envmap_matrix.m, dir), tf, RF_ENVMAP | RF_UNOCCLUDED, weight, rng);
+        }
+    }
+}
+
+// Staged variant (STAGED = true; the host uses it with at most one BSDF candidate and no
+// initial target visibility, the reference defaults): the kernel stops at the BSDF
+// candidate's ray, stages it (k_trace<TM_LIST_CLOSEST>) and leaves the partial reservoir in
+// rs_init, the RNG state in rq_meta and the candidate in rq_rec for k_rsi_finish.  It runs
+// over the pixel lists k_rsi_classify sorts by the material class of the G-buffer surface:
+// PLAIN = plain dielectric seen from outside (the BSDF with the zero-weight lobes compiled
+// out, dev_bsdf.h FULL = false, bit for bit the generic code's result for it).
+enum : int { RSI_RAY = 2 };   // rq_meta.x: a BSDF-candidate ray was staged
+// bsdf_sample with the class's code: the direction, then the evaluation on the updated state
+template <int OVR, bool FULL>
+DEV Col bsdf_sample_cls(const BCtx& bc, const Mat& m, VState& vs, v3 view, v3 sn, v3 gn, v3& dir, float& pdf, Rng& rng) {
+    if (FULL) return bsdf_sample<OVR>(bc, m, vs, view, sn, gn, dir, pdf, rng);
+    pdf = 0.0f;
+    if (!bsdf_sample_dir<OVR, false>(bc, m, vs, view, sn, gn, dir, rng)) return col(0.0f);
+    PEval pe;
+    bsdf_eval_pre<OVR, false>(bc, m, vs, view, sn, pe);
+    return bsdf_eval_post<OVR, false>(bc, m, vs, pe, sn, dir, pdf);
+}
+template <int OVR, bool STAGED, bool PLAIN = false>
+RESTIR_KERNEL void k_restir_initial(DevScene S, DevPaths P, const MptFrame* __restrict__ Fp, const int32_t* __restrict__ list,
+                                    const int32_t* __restrict__ list_count) {
+    __shared__ uint2 lds[STAGED ? 1 : LDS_STACK * TB];
+    __shared__ int tmp[TB / 64];
+    __shared__ int sbase;
     const MptFrame& F = *Fp;
     const MptReSTIRDISettings& rd = F.render_settings.restir_di_settings;
     const MptWorldSettings& w = F.world_settings;
-    if (S.n_emissive == 0 && w.ambient_light_type != MPT_AMBIENT_ENVMAP) return;
+    if (S.n_emissive == 0 && w.ambient_light_type != MPT_AMBIENT_ENVMAP) return;   // (block-uniform)
     const BCtx bc = make_bctx(S, F);
     RRays rr{&S, lds, P.stack_spill + ((size_t)blockIdx.x * TB + threadIdx.x) * (2 * SPILL_DEPTH),
              F.render_settings.do_alpha_testing, 0u, 5, 0, 0u, 0u};
     const int W = F.res_x;
-    for (int s = blockIdx.x * TB + threadIdx.x; s < P.n; s += gridDim.x * TB) {
+    // staged: over the class list, with a block-uniform trip count (the block appends its rays)
+    const int count = STAGED ? *list_count : P.n;
+    const int b_end = STAGED ? count : (int)(blockIdx.x * TB + 1);
+    for (int b0 = blockIdx.x * TB; b0 < b_end; b0 += gridDim.x * TB) {
+    uint32_t rmask = 0u;
+    int s_lane = 0;
+    for (int t = STAGED ? b0 + (int)threadIdx.x : blockIdx.x * TB + threadIdx.x; t < count; t += STAGED ? count : gridDim.x * TB) {
+        const int s = STAGED ? list[t] : t;
+        s_lane = s;
         const int pix = s + P.pix_off;
         RSurf g = gb_surface(S, P, pix, false);
         if (is_emissive(*g.m)) continue;
@@ -481,7 +609,7 @@ RESTIR_KERNEL void k_restir_initial(DevScene S, DevPaths P, const MptFrame* __re
         RResv r = rr_default();
         v3 ep = g.p + g.sn * 1.0e-4f * 1.0f;
         PEval pe;
-        bsdf_eval_pre<OVR>(bc, *g.m, g.vs, g.view, g.sn, pe);
+        bsdf_eval_pre<OVR, !PLAIN>(bc, *g.m, g.vs, g.view, g.sn, pe);
         for (int i = 0; i < nl; i++) {
             int tri;
             v3 point, tl;
@@ -545,7 +673,7 @@ RESTIR_KERNEL void k_restir_initial(DevScene S, DevPaths P, const MptFrame* __re
             if (cosv > 0.0f && pdf > 0.0f) {
                 float bp;
                 VState tv = g.vs;
-                Col f = bsdf_eval_post<OVR>(bc, *g.m, tv, pe, g.sn, tl, bp);
+                Col f = bsdf_eval_post<OVR, !PLAIN>(bc, *g.m, tv, pe, g.sn, tl, bp);
                 Col lc = f * rad * cosv;
                 float tf = lum(lc);
                 if (min_contrib(F.render_settings.minimum_light_contribution, lc / pdf / bp)) {
@@ -566,46 +694,129 @@ RESTIR_KERNEL void k_restir_initial(DevScene S, DevPaths P, const MptFrame* __re
             float bpdf = 0.0f;
             v3 dir;
             VState tv = g.vs;
-            Col f = bsdf_sample<OVR>(bc, *g.m, tv, g.view, g.sn, g.gn, dir, bpdf, rng);
+            Col f = bsdf_sample_cls<OVR, !PLAIN>(bc, *g.m, tv, g.view, g.sn, g.gn, dir, bpdf, rng);
             bool refr = dot(dir, g.view) < 0.0f;   // the reference tests against the view direction
             if (!(bpdf > 0.0f)) continue;
+            if (STAGED) {
+                const size_t id = (size_t)s * RS_RPP;
+                P.rq_o[id] = make_float4(g.p.x, g.p.y, g.p.z, __uint_as_float((uint32_t)g.last));
+                P.rq_d[id] = make_float4(dir.x, dir.y, dir.z, INFINITY);
+                P.rq_key[id] = F.render_settings.do_alpha_testing ? alpha_key(seed, 0, 5, RP_BSDF(i)) : 0u;
+                P.rq_rec[(size_t)s * RS_KMAX] = make_float4(f.r, f.g, f.b, bpdf);
+                P.rq_rec[(size_t)s * RS_KMAX + 1] = make_float4(dir.x, dir.y, dir.z, refr ? 1.0f : 0.0f);
+                rmask = 1u;
+                continue;
+            }
             THit h;
             bool found = rr.at(RP_BSDF(i)).closest(g.p, dir, g.last, h) && h.t < 1.0e35f - 1.0e-4f;
-            ShadowLightHit sh;
-            if (found) found = shadow_light_hit(S, make_float4(h.t, h.u, h.v, __uint_as_float((uint32_t)h.prim)), sh);
-            if (found && !is_black(sh.em)) {
-                float ce = absr(dot(g.sn, dir));
-                Col lc = f * sh.em * ce;
-                float tf = lum(lc);
-                float lpdf = 0.0f;
-                if (!refr) lpdf = pdf_emissive_hit(S, sh, dir);
-                if (!min_contrib(F.render_settings.minimum_light_contribution, lc / lpdf / bpdf)) { r.M++; continue; }
-                lpdf *= (1.0f - env_p);
-                float mis = power_heuristic(bpdf, nb, lpdf, nl);
-                float weight = mis * tf / bpdf;
-                rr_add(r, sh.prim, g.p + dir * sh.dist, tf, RF_UNOCCLUDED | (refr ? RF_BSDF_REFRACTION : 0u), weight, rng);
-            } else if (!found && w.ambient_light_type == MPT_AMBIENT_ENVMAP) {
-                float ce = maxr(0.0f, dot(g.sn, dir));
-                if (ce > 0.0f) {
-                    float epdf;
-                    Col er = env_eval(S, F, dir, epdf);
-                    Col ec = f * er * ce;
-                    if (!min_contrib(F.render_settings.minimum_light_contribution, ec / epdf / bpdf)) { r.M++; continue; }
-                    float tf = lum(ec);
-                    epdf *= env_p;
-                    float mis = power_heuristic(bpdf, nb, epdf, nl);
-                    float weight = mis * tf / bpdf;
-                    rr_add(r, -1, mat_x_vec(w.world_to_envmap_matrix.m, dir), tf, RF_ENVMAP | RF_UNOCCLUDED, weight, rng);
-                }
-            }
+            initial_bsdf_candidate(S, F, g.p, g.sn, dir, f, bpdf, refr, found,
+                                   make_float4(h.t, h.u, h.v, __uint_as_float((uint32_t)h.prim)), env_p, nl, nb, r, rng);
+        }
+        if (STAGED) {
+            rr_store(P.rs_init, pix, r);   // partial: k_rsi_finish adds the BSDF candidate and ends it
+            P.rq_meta[s] = make_int4(rmask ? RSI_RAY : 0, (int)rng.s, 0, 0);
+            continue;
         }
         r.UCW = r.wsum == 0.0f ? 0.0f : 1.0f / r.target * r.wsum;   // end()
         r.M = 1;
         if (F.options.restir_di_do_visibility_reuse) restir_visibility_reuse(F, rr, r, g.p + g.sn * 1.0e-4f, g.last);
         rr_store(P.rs_init, pix, r);
     }
-    count_pass_rays(P, rr.n_any, rr.n_closest);
+    if (STAGED) {
+        rs_append(P, &P.counters[CTR_RQ], s_lane, rmask, tmp, &sbase);
+        __syncthreads();
+    }
+    }
+    if (!STAGED) count_pass_rays(P, rr.n_any, rr.n_closest);
 }
+
+#ifndef MPT_TU_PART   // k_rsi_classify
+// The staged initial pass's pixel lists: pixels that run the pass (not emissive, active, a
+// camera hit), by the class of their G-buffer surface (rs_plain): plain at [0, n), generic at
+// [n, 2n) of rq_items; every other pixel is marked skipped for k_rsi_finish.
+__global__ __launch_bounds__(TB) void k_rsi_classify(DevScene S, DevPaths P, const MptFrame* __restrict__ Fp, int principled) {
+    __shared__ int tmp[TB / 64];
+    __shared__ int base;
+    const MptFrame& F = *Fp;
+    if (S.n_emissive == 0 && F.world_settings.ambient_light_type != MPT_AMBIENT_ENVMAP) return;   // (grid-uniform)
+    const int s = blockIdx.x * TB + threadIdx.x;
+    int cls = -1;
+    if (s < P.n) {
+        const int pix = s + P.pix_off;
+        const RSurf g = gb_surface(S, P, pix, false);
+        if (!is_emissive(*g.m) && P.active[s] && P.gb_meta[pix].z) cls = principled && rs_plain(S, P, pix, g) ? 0 : 1;
+        else P.rq_meta[s] = make_int4(RSM_SKIP, 0, 0, 0);
+    }
+    for (int c = 0; c < 2; c++) {
+        int tot;
+        const int off = rs_block_scan(cls == c ? 1 : 0, tmp, tot);
+        if (threadIdx.x == 0) base = tot ? atomicAdd(&P.counters[CTR_RQE0 + c], tot) : 0;
+        __syncthreads();
+        if (cls == c) P.rq_items[(size_t)c * P.n + base + off] = s;
+        __syncthreads();
+    }
+}
+#endif
+
+#ifndef MPT_TU_PART   // k_rsi_finish
+// Staged initial candidates, second half: the BSDF candidate from its traced ray (closest
+// hit in rq_o, written over the staged ray by k_trace<TM_LIST_CLOSEST>), end(), and the
+// visibility-reuse ray staged for k_rs_visapply.
+RESTIR_KERNEL void k_rsi_finish(DevScene S, DevPaths P, const MptFrame* __restrict__ Fp) {
+    __shared__ int tmp[TB / 64];
+    __shared__ int sbase;
+    const MptFrame& F = *Fp;
+    const MptReSTIRDISettings& rd = F.render_settings.restir_di_settings;
+    const MptWorldSettings& w = F.world_settings;
+    if (S.n_emissive == 0 && w.ambient_light_type != MPT_AMBIENT_ENVMAP) return;   // as k_restir_initial (grid-uniform)
+    const int s = blockIdx.x * TB + threadIdx.x;
+    uint32_t vmask = 0u, n_any = 0u, n_cl = 0u;
+    if (s < P.n && !(P.rq_meta[s].x & RSM_SKIP)) {
+        const int4 meta = P.rq_meta[s];
+        const int pix = s + P.pix_off;
+        RResv r = rr_load(P.rs_init, pix);
+        Rng rng = make_rng((uint32_t)meta.y);
+        const float4 gp4 = P.gb_pos[pix], gs4 = P.gb_sn[pix];
+        const v3 gp = mk3(gp4.x, gp4.y, gp4.z), gsn = mk3(gs4.x, gs4.y, gs4.z);
+        const size_t id = (size_t)s * RS_RPP;
+        if (meta.x & RSI_RAY) {
+            const int nl = rd.number_of_initial_light_candidates, nb = rd.number_of_initial_bsdf_candidates;
+            float env_p = 0.0f;
+            if (w.ambient_light_type == MPT_AMBIENT_ENVMAP) env_p = S.n_emissive == 0 ? 1.0f : rd.envmap_candidate_probability;
+            const float4 fr = P.rq_rec[(size_t)s * RS_KMAX], dr = P.rq_rec[(size_t)s * RS_KMAX + 1];
+            const float4 h = P.rq_o[id];
+            const bool found = (int)__float_as_uint(h.w) >= 0 && h.x < 1.0e35f - 1.0e-4f;
+            initial_bsdf_candidate(S, F, gp, gsn, mk3(dr.x, dr.y, dr.z), col(fr.x, fr.y, fr.z), fr.w, dr.w != 0.0f, found, h,
+                                   env_p, nl, nb, r, rng);
+            n_cl = 1u;
+        }
+        r.UCW = r.wsum == 0.0f ? 0.0f : 1.0f / r.target * r.wsum;   // end()
+        r.M = 1;
+        if (F.options.restir_di_do_visibility_reuse && r.UCW > 0.0f && !(r.flags & RF_UNOCCLUDED)) {
+            const v3 sp = gp + gsn * 1.0e-4f;
+            TgtRay ray;
+            ray.o = sp;
+            if (r.flags & RF_ENVMAP) { ray.d = mat_x_vec(w.envmap_to_world_matrix.m, r.point); ray.dist = 1.0e35f; }
+            else { v3 dir = r.point - sp; ray.dist = length(dir); ray.d = dir / ray.dist; }
+            rs_stage_ray(P, id, ray, P.gb_meta[pix].x,
+                         F.render_settings.do_alpha_testing ? alpha_key(pass_seed(F, (uint32_t)pix, F.restir_di_seeds[1]), 0, 5,
+                                                                        RP_VISREUSE)
+                                                            : 0u);
+            vmask = 1u;
+            n_any = 1u;
+        }
+        rr_store(P.rs_init, pix, r);
+    }
+    rs_append(P, &P.counters[CTR_RQV], s, vmask, tmp, &sbase);
+    int ta, tc;
+    (void)rs_block_scan((int)n_any, tmp, ta);
+    (void)rs_block_scan((int)n_cl, tmp, tc);
+    if (threadIdx.x == 0) {
+        if (ta) atomicAdd((unsigned long long*)&P.ray_counts[1], (unsigned long long)ta);
+        if (tc) atomicAdd((unsigned long long*)&P.ray_counts[2], (unsigned long long)tc);
+    }
+}
+#endif
 
 // find_temporal_neighbor_index (Utils.h:371-421)
 DEV int restir_temporal_neighbor(const DevScene& S, const DevPaths& P, const MptFrame& F, v3 p, v3 n, const Mat& cm,
@@ -1097,11 +1308,16 @@ RESTIR_KERNEL void k_restir_spatial(DevScene S, DevPaths P, const MptFrame* __re
 // ---- staged spatial reuse (the reference-default weights) -----------------------------
 // k_restir_spatial traces its visibility rays inline, inside a kernel whose BSDF evaluations
 // hold every register (256 VGPRs and scratch spills at 2 waves / SIMD), so the traversal
-// runs slowly and lanes wait on each other's rays.  The staged pass splits it at the rays:
-//  * k_rsp_gather: per pixel, the neighbour selection and the quantities that do not depend
-//    on any ray -- each neighbour's unoccluded target functions (the BSDF evaluations) and
-//    Jacobian -- and the visibility rays the monolithic kernel would trace, staged at fixed
-//    positions (pixel slot, 2k + which) with the alpha keys of their position in its order;
+// runs slowly and lanes wait on each other's rays.  The staged pass splits it into
+// material-sorted stages:
+//  * k_rsp_select (per pixel, no BSDF code): the neighbour selection, the similarity tests,
+//    each neighbour's reservoir and Jacobian, and the target-function evaluations the pass
+//    needs -- neighbour k's sample at the center (TFC) and the canonical sample at neighbour k
+//    (TCN) -- appended as items to the plain-dielectric list or the generic list by the
+//    material class of the surface they are evaluated at (as k_split sorts the shading);
+//  * k_rsp_eval<PLAIN> per list: the unoccluded target function (dev_bsdf.h FULL = false for
+//    the plain list) and the visibility ray the monolithic kernel would trace, staged at the
+//    item's position (pixel slot, 2k + which);
 //  * k_trace<TM_LIST_ANY> over the staged rays (persistent, chunked, LDS stack);
 //  * k_rsp_combine: the resampling from the stored values and the occlusion bytes, with the
 //    RNG draws of the monolithic kernel; the visibility-reuse ray of the result is staged
@@ -1109,124 +1325,135 @@ RESTIR_KERNEL void k_restir_spatial(DevScene S, DevPaths P, const MptFrame* __re
 // Alpha keys are positional (RP_*), so a staged ray has the key the monolithic kernel gives
 // it, including the bias-correction ray of a neighbour that a Jacobian rejection then drops
 // (staged and traced, never used).
-constexpr int RS_KMAX = RS_KMAX_HOST, RS_RPP = RS_RPP_HOST;   // neighbours a staged pass supports; ray positions per pixel
-enum : int { RSM_SKIP = 1 };                      // rq_meta.x: the pixel is not resampled (output untouched)
-
-// exclusive scan of one int per thread over a TB-thread block; total to `total`
-DEV int rs_block_scan(int v, int* tmp, int& total) {
-    const int lane = lane_id(), wid = threadIdx.x >> 6;
-    constexpr int NW = TB / 64;
-    int x = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        int y = __shfl_up(x, o);
-        if (lane >= o) x += y;
-    }
-    if (lane == 63) tmp[wid] = x;
-    __syncthreads();
-    int before = 0, all = 0;
-#pragma unroll
-    for (int w = 0; w < NW; w++) {
-        const int tw = tmp[w];
-        if (w < wid) before += tw;
-        all += tw;
-    }
-    __syncthreads();
-    total = all;
-    return before + x - v;
-}
-
-DEV void rs_stage_ray(const DevPaths& P, size_t id, const TgtRay& r, int last, uint32_t key) {
-    P.rq_o[id] = make_float4(r.o.x, r.o.y, r.o.z, __uint_as_float((uint32_t)last));
-    P.rq_d[id] = make_float4(r.d.x, r.d.y, r.d.z, r.dist - 1.0e-4f);
-    P.rq_key[id] = key;
-}
-
-// appends the ray positions in `mask` of slot s to the list behind `counter` (one atomic per block)
-DEV void rs_append(const DevPaths& P, int32_t* counter, int s, uint32_t mask, int* tmp, int* base) {
-    int tot;
-    const int off = rs_block_scan(__popc(mask), tmp, tot);
-    if (threadIdx.x == 0) *base = tot ? atomicAdd(counter, tot) : 0;
-    __syncthreads();
-    int o = *base + off;
-    while (mask) {
-        const int j = __builtin_ctz(mask);
-        mask &= mask - 1u;
-        P.rq_list[o++] = s * RS_RPP + j;
-    }
-}
+constexpr uint32_t RSE_VIS = 0x80000000u;   // eval item flag: the target is evaluated with visibility
 
 template <int OVR>
-RESTIR_KERNEL void k_rsp_gather(DevScene S, DevPaths P, const MptFrame* __restrict__ Fp, int pass, const float4* __restrict__ in) {
+__global__ __launch_bounds__(TB) void k_rsp_select(DevScene S, DevPaths P, const MptFrame* __restrict__ Fp, int pass,
+                                                   const float4* __restrict__ in) {
     __shared__ int tmp[TB / 64];
     __shared__ int base;
     const MptFrame& F = *Fp;
-    const BCtx bc = make_bctx(S, F);
     const int W = F.res_x;
     const uint32_t pass_rs = F.restir_di_seeds[4 + pass];
-    const bool alpha = F.render_settings.do_alpha_testing;
     const int s = blockIdx.x * TB + threadIdx.x;
-    uint32_t rmask = 0u;
+    uint32_t m_plain = 0u, m_gen = 0u, vis_bits = 0u;   // items by position (2k + which)
     if (s < P.n) {
         const int center = s + P.pix_off;
         int4 meta = make_int4(RSM_SKIP, 0, 0, 0);
         MptReSTIRDISettings rd = F.render_settings.restir_di_settings;
         rd.spatial_pass_index = pass;
         if (P.active[s] && P.gb_meta[center].z) {
-            const uint32_t seed = pass_seed(F, (uint32_t)center, pass_rs);
-            Rng rng = make_rng(seed);
+            Rng rng = make_rng(pass_seed(F, (uint32_t)center, pass_rs));
             const RSurf cs = gb_surface(S, P, center, false);
             if (!is_emissive(*cs.m)) {
                 const int x = center % W, y = center / W;
-                float rot = rd.do_neighbor_rotation ? TWO_PI * rng() : 0.0f;
-                float cr = pcos(rot), sr = psin(rot);
+                float cr = 1.0f, sr = 0.0f;
+                if (rd.do_neighbor_rotation) {
+                    const float2 sc = psincos(TWO_PI * rng());
+                    sr = sc.x;
+                    cr = sc.y;
+                }
                 const RResv cres = rr_load(in, center);
                 if (cres.M <= 1 && rd.do_disocclusion_reuse_boost) rd.reuse_neighbor_count = rd.disocclusion_reuse_count;
                 const int reuse = rd.reuse_neighbor_count;
                 int cache = 0, vcount = 0, vM = 0;
+                int nis[RS_KMAX];
                 for (int k = 0; k < reuse; k++) {
-                    int ni = restir_spatial_neighbor(P, F, k, reuse, rd.reuse_radius, x, y, cr, sr, pass_rs);
-                    if (ni == -1) continue;
-                    if (!restir_similar(S, P, rd, ni, *cs.m, cs.sp, cs.sn, false)) continue;
-                    vM += rr_load(in, ni).M;
+                    nis[k] = restir_spatial_neighbor(P, F, k, reuse, rd.reuse_radius, x, y, cr, sr, pass_rs);
+                    if (nis[k] == -1) continue;
+                    if (!restir_similar(S, P, rd, nis[k], *cs.m, cs.sp, cs.sn, false)) continue;
+                    vM += rr_load(in, nis[k]).M;
                     vcount++;
                     cache |= 1 << k;
                 }
                 meta = make_int4(0, cache, vM, vcount);
                 const bool update_mc = cres.M > 0 && cres.UCW > 0.0f;
+                const bool c_plain = OVR == MPT_BSDF_NONE && rs_plain(S, P, center, cs);
                 for (int k = 0; k < reuse && vM != 0; k++) {
                     if (!((cache >> k) & 1)) continue;
-                    const int ni = restir_spatial_neighbor(P, F, k, reuse, rd.reuse_radius, x, y, cr, sr, pass_rs);
+                    const int ni = nis[k];
                     const RResv nr = rr_load(in, ni);
-                    const bool vis = spatial_visibility(F, rd, k, reuse);
-                    float tfc = 0.0f, tcn = 0.0f, jac = 1.0f;
-                    TgtRay ray;
+                    float jac = 1.0f;
                     if (nr.UCW > 0.0f) {
-                        tfc = restir_target_unocc(S, F, bc, nr.tri, nr.point, nr.flags, cs, vis, OVR, ray);
-                        if (vis && tfc > 0.0f) {
-                            rs_stage_ray(P, (size_t)s * RS_RPP + 2 * k, ray, cs.last, alpha ? alpha_key(seed, 0, 7, RP_TFC(k)) : 0u);
-                            rmask |= 1u << (2 * k);
-                        }
-                        if (tfc > 0.0f && !(nr.flags & RF_ENVMAP)) {
-                            float4 np = P.gb_pos[ni];
+                        (c_plain ? m_plain : m_gen) |= 1u << (2 * k);
+                        if (spatial_visibility(F, rd, k, reuse)) vis_bits |= 1u << (2 * k);
+                        // used only when the target turns out positive (the monolithic kernel's order)
+                        if (!(nr.flags & RF_ENVMAP)) {
+                            const float4 np = P.gb_pos[ni];
                             jac = restir_jacobian(S, nr, cs.sp, mk3(np.x, np.y, np.z));
                         }
                     }
                     if (update_mc) {
-                        const RSurf ns = gb_surface(S, P, ni, false);
-                        tcn = restir_target_unocc(S, F, bc, cres.tri, cres.point, cres.flags, ns, true, OVR, ray);
-                        if (tcn > 0.0f) {
-                            rs_stage_ray(P, (size_t)s * RS_RPP + 2 * k + 1, ray, ns.last, alpha ? alpha_key(seed, 0, 7, RP_TCN(k)) : 0u);
-                            rmask |= 1u << (2 * k + 1);
-                        }
+                        const bool n_plain = OVR == MPT_BSDF_NONE && rs_plain(S, P, ni, gb_surface(S, P, ni, false));
+                        (n_plain ? m_plain : m_gen) |= 1u << (2 * k + 1);
+                        vis_bits |= 1u << (2 * k + 1);   // ReSTIR_DI_BiasCorrectionUseVisibility
                     }
-                    P.rq_rec[(size_t)s * RS_KMAX + k] = make_float4(__int_as_float(ni), tfc, tcn, jac);
+                    P.rq_rec[(size_t)s * RS_KMAX + k] = make_float4(__int_as_float(ni), 0.0f, 0.0f, jac);
                 }
             }
         }
         P.rq_meta[s] = meta;
     }
-    rs_append(P, &P.counters[CTR_RQ], s, rmask, tmp, &base);
+    // item lists: plain at [0, n * RS_RPP), generic at [n * RS_RPP, 2 n * RS_RPP)
+    for (int c = 0; c < 2; c++) {
+        uint32_t mask = c == 0 ? m_plain : m_gen;
+        int tot;
+        const int off = rs_block_scan(__popc(mask), tmp, tot);
+        if (threadIdx.x == 0) base = tot ? atomicAdd(&P.counters[CTR_RQE0 + c], tot) : 0;
+        __syncthreads();
+        int32_t* list = P.rq_items + (size_t)c * P.n * RS_RPP;
+        int o = base + off;
+        while (mask) {
+            const int j = __builtin_ctz(mask);
+            mask &= mask - 1u;
+            list[o++] = (s * RS_RPP + j) | (((vis_bits >> j) & 1u) ? (int)RSE_VIS : 0);
+        }
+        __syncthreads();
+    }
+}
+
+// One target-function evaluation per item of a class list (count in the device counter);
+// grid-stride with a block-uniform trip count (the block appends its rays each round).
+template <int OVR, bool PLAIN>
+RESTIR_KERNEL void k_rsp_eval(DevScene S, DevPaths P, const MptFrame* __restrict__ Fp, int pass, const float4* __restrict__ in,
+                              const int32_t* __restrict__ items, const int32_t* __restrict__ count_ptr) {
+    __shared__ int tmp[TB / 64];
+    __shared__ int base;
+    const MptFrame& F = *Fp;
+    const BCtx bc = make_bctx(S, F);
+    const uint32_t pass_rs = F.restir_di_seeds[4 + pass];
+    const bool alpha = F.render_settings.do_alpha_testing;
+    const int count = *count_ptr;
+    for (int b0 = blockIdx.x * TB; b0 < count; b0 += gridDim.x * TB) {
+        const int i = b0 + (int)threadIdx.x;
+        uint32_t rmask = 0u;
+        int s = 0;
+        if (i < count) {
+            const uint32_t it = (uint32_t)items[i];
+            const bool vis = (it & RSE_VIS) != 0;
+            const int id = (int)(it & ~RSE_VIS);
+            s = id / RS_RPP;
+            const int j = id - s * RS_RPP, k = j >> 1, which = j & 1;
+            const int center = s + P.pix_off;
+            float* rec = reinterpret_cast<float*>(&P.rq_rec[(size_t)s * RS_KMAX + k]);
+            const int ni = __float_as_int(rec[0]);
+            const int at = which ? ni : center;
+            const RSurf g = gb_surface(S, P, at, false);
+            const RResv smp = rr_load(in, which ? center : ni);
+            TgtRay ray;
+            float t;
+            if (PLAIN) t = restir_target_unocc<true>(S, F, bc, smp.tri, smp.point, smp.flags, g, vis, OVR, ray);
+            else t = restir_target_unocc<false>(S, F, bc, smp.tri, smp.point, smp.flags, g, vis, OVR, ray);
+            rec[1 + which] = t;
+            if (vis && t > 0.0f) {
+                const uint32_t key = alpha ? alpha_key(pass_seed(F, (uint32_t)center, pass_rs), 0, 7, which ? RP_TCN(k) : RP_TFC(k)) : 0u;
+                rs_stage_ray(P, (size_t)id, ray, g.last, key);
+                rmask = 1u << j;
+            }
+        }
+        rs_append(P, &P.counters[CTR_RQ], s, rmask, tmp, &base);
+        __syncthreads();
+    }
 }
 
 template <int OVR>
@@ -1246,7 +1473,7 @@ RESTIR_KERNEL void k_rsp_combine(DevScene S, DevPaths P, const MptFrame* __restr
         rd.spatial_pass_index = pass;
         const uint32_t seed = pass_seed(F, (uint32_t)center, pass_rs);
         Rng rng = make_rng(seed);
-        if (rd.do_neighbor_rotation) (void)rng();   // the neighbour rotation (used by k_rsp_gather)
+        if (rd.do_neighbor_rotation) (void)rng();   // the neighbour rotation (used by k_rsp_select)
         const RResv cres = rr_load(in, center);
         if (cres.M <= 1 && rd.do_disocclusion_reuse_boost) rd.reuse_neighbor_count = rd.disocclusion_reuse_count;
         const int reuse = rd.reuse_neighbor_count;

@@ -177,6 +177,11 @@ CASES = {
     "no_presampling_unfused": dict(do_fused_spatiotemporal=False, kopt=dict(restir_di_do_lights_presampling=0)),
     "no_visibility_reuse_target_vis": dict(do_fused_spatiotemporal=False,
                                            kopt=dict(restir_di_do_visibility_reuse=0, restir_di_initial_target_visibility=1)),
+    # the staged initial pass takes at most one BSDF candidate; 0 and 2 run the monolithic kernel
+    "no_bsdf_candidate": dict(number_of_initial_bsdf_candidates=0),
+    "two_bsdf_candidates": dict(number_of_initial_bsdf_candidates=2),
+    # the staged spatial pass takes at most RS_KMAX (5) neighbours; 7 runs the monolithic kernel
+    "seven_neighbours": dict(reuse_neighbor_count=7, disocclusion_reuse_count=7),
 }
 
 
