@@ -602,7 +602,7 @@ int ensure_restir(MptContext* c, const MptFrame* f) {
         if (c->rq_meta.n != ns) {
             A(c->rq_o, ns * RS_RPP_HOST); A(c->rq_d, ns * RS_RPP_HOST); A(c->rq_key, ns * RS_RPP_HOST);
             A(c->rq_occ, ns * RS_RPP_HOST); A(c->rq_list, ns * RS_RPP_HOST); A(c->rq_items, 2 * ns * RS_RPP_HOST);
-            A(c->rq_meta, ns); A(c->rq_rec, ns * RS_KMAX_HOST);
+            A(c->rq_meta, ns); A(c->rq_rec, ns * RS_REC_HOST);
         }
     }
     if (c->rs_plights.n != 4 * npl) {

@@ -210,7 +210,7 @@ struct DevPaths {
 
 constexpr int N_TRACE_MODES = 5;
 // staged ReSTIR DI reuse passes (restir_di.h RS_KMAX / RS_RPP): neighbours per pass, ray positions per pixel
-constexpr int RS_KMAX_HOST = 5, RS_RPP_HOST = 2 * RS_KMAX_HOST;
+constexpr int RS_KMAX_HOST = 5, RS_RPP_HOST = 2 * RS_KMAX_HOST + 2, RS_REC_HOST = RS_KMAX_HOST + 2;
 constexpr int N_RAY_COUNTS = 5;   // DevPaths::ray_counts
 // timed kernel kinds: 0..2 = traversal stages (trace modes), then the others
 enum { KT_CAMERA = 3, KT_SHADE = 4, KT_RESOLVE = 5, KT_ACCUMULATE = 6, KT_COMPACT = 7, KT_RESTIR = 8, KT_SPLIT = 9,

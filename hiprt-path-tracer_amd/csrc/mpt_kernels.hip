@@ -2199,7 +2199,8 @@ void part_shade_plain(dim3 g, hipStream_t st, const ShadeArgs& a);            //
 void part_shade_ext(dim3 g, hipStream_t st, const ShadeArgs& a);              // k_shade<NONE, false, true>
 void part_shade_override(int ovr, bool ext, dim3 g, hipStream_t st, const ShadeArgs& a);   // Lambert, Oren-Nayar
 enum RestirKernel { RK_INITIAL, RK_SPATIOTEMPORAL, RK_SPATIOTEMPORAL_ANY, RK_SPATIAL, RK_SPATIAL_ANY, RK_TEMPORAL, RK_SP_SELECT,
-                   RK_SP_EVAL_PLAIN, RK_SP_EVAL_GENERIC, RK_SP_COMBINE, RK_INITIAL_STAGED_PLAIN, RK_INITIAL_STAGED_GENERIC };
+                   RK_SP_EVAL_PLAIN, RK_SP_EVAL_GENERIC, RK_SP_COMBINE, RK_INITIAL_STAGED_PLAIN, RK_INITIAL_STAGED_GENERIC,
+                   RK_ST_SELECT, RK_ST_EVAL_PLAIN, RK_ST_EVAL_GENERIC, RK_ST_COMBINE };
 void part_restir_principled(int kind, dim3 g, hipStream_t st, const DevScene& S, const DevPaths& P, const MptFrame* F,
                             int pass, const float4* in, float4* out);
 void part_restir_override(int ovr, int kind, dim3 g, hipStream_t st, const DevScene& S, const DevPaths& P,
@@ -2316,6 +2317,37 @@ static void launch_spatial_pass(int ovr, bool def_bias, const MptFrame& hf, Laun
     hipLaunchKernelGGL(k_rs_visapply, gp, dim3(TB), 0, st, P, out);
 }
 
+// The fused spatiotemporal pass: staged (k_rst_select, class-sorted evaluations, traced rays,
+// k_rst_combine, visibility reuse; restir_di.h) under the same conditions as a spatial pass and
+// no temporal-buffer clear this frame, else the monolithic kernel.
+static void launch_fused_pass(int ovr, bool def_bias, const MptFrame& hf, LaunchCfg& cfg, dim3 g, hipStream_t st,
+                              const DevScene& S, const DevPaths& P, const MptFrame* d_frame) {
+    const MptReSTIRDISettings& rd = hf.render_settings.restir_di_settings;
+    const bool staged = def_bias && cfg.restir_staged && P.rq_o && rd.reuse_neighbor_count <= RS_KMAX &&
+                        (!rd.do_disocclusion_reuse_boost || rd.disocclusion_reuse_count <= RS_KMAX) &&
+                        !rd.temporal_buffer_clear_requested;
+    if (!staged) {
+        launch_restir_kernel(ovr, def_bias ? RK_SPATIOTEMPORAL : RK_SPATIOTEMPORAL_ANY, g, st, S, P, d_frame);
+        return;
+    }
+    const dim3 gp(blocks_for(P.n));
+    hipMemsetAsync(&P.counters[CTR_RQ], 0, 4 * sizeof(int32_t), st);   // CTR_RQ, CTR_RQV, CTR_RQE0, CTR_RQE1
+    launch_restir_kernel(ovr, RK_ST_SELECT, gp, st, S, P, d_frame);
+    launch_restir_kernel(ovr, RK_ST_EVAL_PLAIN, g, st, S, P, d_frame);
+    launch_restir_kernel(ovr, RK_ST_EVAL_GENERIC, g, st, S, P, d_frame);
+    TraceArgs ta{};
+    ta.S = S; ta.P = P; ta.queue = P.rq_list; ta.count_ptr = &P.counters[CTR_RQ]; ta.fetch = &P.counters[CTR_FETCH];
+    ta.raw_o = P.rq_o; ta.raw_d = P.rq_d; ta.raw_key = P.rq_key; ta.raw_occ = P.rq_occ;
+    ta.F = d_frame; ta.alpha = hf.render_settings.do_alpha_testing ? 1 : 0;
+    hipMemsetAsync(&P.counters[CTR_FETCH], 0, sizeof(int32_t), st);
+    launch_trace_mode<TM_LIST_ANY>(ta, cfg.grid_persistent, cfg.stats, st);
+    launch_restir_kernel(ovr, RK_ST_COMBINE, gp, st, S, P, d_frame);
+    ta.count_ptr = &P.counters[CTR_RQV];
+    hipMemsetAsync(&P.counters[CTR_FETCH], 0, sizeof(int32_t), st);
+    launch_trace_mode<TM_LIST_ANY>(ta, cfg.grid_persistent, cfg.stats, st);
+    hipLaunchKernelGGL(k_rs_visapply, gp, dim3(TB), 0, st, P, P.rs_out);
+}
+
 // ReSTIRDIRenderPass::launch (ReSTIRDIRenderPass.cpp:233-264) for the fused configuration:
 // presampling, initial candidates, fused spatiotemporal, (number_of_passes - 1) spatial
 // passes ping-ponging between the two spatial buffers; returns the output buffer in P.rs_out.
@@ -2391,7 +2423,7 @@ static void launch_restir(const DevScene& S, DevPaths& P, const MptFrame* d_fram
         halo_exchange(hf, cfg, st, MPT_HALO_RESERVOIRS, 0, cfg.halo_rows, {{P.rs_tin, RB}});
         {
             TimedScope tk(cfg, st, KT_RS_REUSE);
-            launch_restir_kernel(ovr, def_bias ? RK_SPATIOTEMPORAL : RK_SPATIOTEMPORAL_ANY, g, st, S, P, d_frame);
+            launch_fused_pass(ovr, def_bias, hf, cfg, g, st, S, P, d_frame);
         }
         for (int pass = 1; pass < rd.number_of_passes; pass++) {
             float4* in = P.rs_out;

@@ -69,12 +69,24 @@ static void restir_kernel(int kind, dim3 g, hipStream_t st, const DevScene& S, c
     case RK_SP_SELECT: hipLaunchKernelGGL(k_rsp_select<OVR>, g, dim3(TB), 0, st, S, P, F, pass, in); break;
     case RK_SP_EVAL_PLAIN:   // (only the Principled BSDF has the plain class)
         if (OVR == MPT_BSDF_NONE)
-            hipLaunchKernelGGL((k_rsp_eval<OVR, true>), g, dim3(TB), 0, st, S, P, F, pass, in, P.rq_items, &P.counters[CTR_RQE0]);
+            hipLaunchKernelGGL((k_rsp_eval<OVR, true, false>), g, dim3(TB), 0, st, S, P, F, pass, in, P.rq_items, &P.counters[CTR_RQE0]);
         break;
     case RK_SP_EVAL_GENERIC:
-        hipLaunchKernelGGL((k_rsp_eval<OVR, false>), g, dim3(TB), 0, st, S, P, F, pass, in, P.rq_items + (size_t)P.n * RS_RPP,
+        hipLaunchKernelGGL((k_rsp_eval<OVR, false, false>), g, dim3(TB), 0, st, S, P, F, pass, in, P.rq_items + (size_t)P.n * RS_RPP,
                            &P.counters[CTR_RQE1]);
         break;
+    // the staged fused spatiotemporal pass: selection, class-sorted evaluations, combine
+    case RK_ST_SELECT: hipLaunchKernelGGL(k_rst_select<OVR>, g, dim3(TB), 0, st, S, P, F); break;
+    case RK_ST_EVAL_PLAIN:
+        if (OVR == MPT_BSDF_NONE)
+            hipLaunchKernelGGL((k_rsp_eval<OVR, true, true>), g, dim3(TB), 0, st, S, P, F, 0, P.rs_tin, P.rq_items,
+                               &P.counters[CTR_RQE0]);
+        break;
+    case RK_ST_EVAL_GENERIC:
+        hipLaunchKernelGGL((k_rsp_eval<OVR, false, true>), g, dim3(TB), 0, st, S, P, F, 0, P.rs_tin,
+                           P.rq_items + (size_t)P.n * RS_RPP, &P.counters[CTR_RQE1]);
+        break;
+    case RK_ST_COMBINE: hipLaunchKernelGGL(k_rst_combine<OVR>, g, dim3(TB), 0, st, S, P, F); break;
     case RK_SP_COMBINE: hipLaunchKernelGGL(k_rsp_combine<OVR>, g, dim3(TB), 0, st, S, P, F, pass, in, out); break;
     default: hipLaunchKernelGGL(k_restir_temporal<OVR>, g, dim3(TB), 0, st, S, P, F, in, out); break;
     }

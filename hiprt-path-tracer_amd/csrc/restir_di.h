@@ -96,7 +96,10 @@ DEV void count_pass_rays(const DevPaths& P, uint32_t n_any, uint32_t n_closest) 
 
 // ---- staged passes: ray positions, block-aggregated list appends ----------------------
 struct TgtRay { v3 o, d; float dist; };   // a shadow ray of a target function / visibility test
-constexpr int RS_KMAX = RS_KMAX_HOST, RS_RPP = RS_RPP_HOST;   // neighbours a staged pass supports; ray positions per pixel
+// neighbours a staged pass supports; ray positions per pixel slot (spatial neighbour k: 2k, 2k + 1;
+// fused pass: temporal 0, 1, spatial k 2 + 2k, 3 + 2k); records per pixel slot (rq_rec)
+constexpr int RS_KMAX = RS_KMAX_HOST, RS_RPP = RS_RPP_HOST, RS_REC = RS_REC_HOST;
+constexpr uint32_t RSE_PREV = 0x40000000u;   // eval item flag: the surface is in the previous frame's G-buffer
 enum : int { RSM_SKIP = 1 };                      // rq_meta.x: the pixel is not resampled (output untouched)
 
 // exclusive scan of one int per thread over a TB-thread block; total to `total`
@@ -513,8 +516,8 @@ __global__ __launch_bounds__(TB) void k_restir_presample(DevScene S, DevPaths P,
 
 // the evaluation class of a G-buffer surface: plain dielectric seen from outside (the
 // condition k_shade<PLAIN> checks before it shades, principled_eval_pre's 'outside')
-DEV bool rs_plain(const DevScene& S, const DevPaths& P, int pix, const RSurf& g) {
-    const int mi = P.gb_meta[pix].y - 1;
+DEV bool rs_plain(const DevScene& S, const DevPaths& P, int pix, const RSurf& g, bool prev = false) {
+    const int mi = (prev ? P.pgb_meta[pix].y : P.gb_meta[pix].y) - 1;
     return mi >= 0 && !(S.mat_tex[mi] & MT_FULL) && (dot(g.view, g.sn) > 0.0f || g.m->thin_walled);
 }
 
@@ -702,8 +705,8 @@ RESTIR_KERNEL void k_restir_initial(DevScene S, DevPaths P, const MptFrame* __re
                 P.rq_o[id] = make_float4(g.p.x, g.p.y, g.p.z, __uint_as_float((uint32_t)g.last));
                 P.rq_d[id] = make_float4(dir.x, dir.y, dir.z, INFINITY);
                 P.rq_key[id] = F.render_settings.do_alpha_testing ? alpha_key(seed, 0, 5, RP_BSDF(i)) : 0u;
-                P.rq_rec[(size_t)s * RS_KMAX] = make_float4(f.r, f.g, f.b, bpdf);
-                P.rq_rec[(size_t)s * RS_KMAX + 1] = make_float4(dir.x, dir.y, dir.z, refr ? 1.0f : 0.0f);
+                P.rq_rec[(size_t)s * RS_REC] = make_float4(f.r, f.g, f.b, bpdf);
+                P.rq_rec[(size_t)s * RS_REC + 1] = make_float4(dir.x, dir.y, dir.z, refr ? 1.0f : 0.0f);
                 rmask = 1u;
                 continue;
             }
@@ -783,7 +786,7 @@ RESTIR_KERNEL void k_rsi_finish(DevScene S, DevPaths P, const MptFrame* __restri
             const int nl = rd.number_of_initial_light_candidates, nb = rd.number_of_initial_bsdf_candidates;
             float env_p = 0.0f;
             if (w.ambient_light_type == MPT_AMBIENT_ENVMAP) env_p = S.n_emissive == 0 ? 1.0f : rd.envmap_candidate_probability;
-            const float4 fr = P.rq_rec[(size_t)s * RS_KMAX], dr = P.rq_rec[(size_t)s * RS_KMAX + 1];
+            const float4 fr = P.rq_rec[(size_t)s * RS_REC], dr = P.rq_rec[(size_t)s * RS_REC + 1];
             const float4 h = P.rq_o[id];
             const bool found = (int)__float_as_uint(h.w) >= 0 && h.x < 1.0e35f - 1.0e-4f;
             initial_bsdf_candidate(S, F, gp, gsn, mk3(dr.x, dr.y, dr.z), col(fr.x, fr.y, fr.z), fr.w, dr.w != 0.0f, found, h,
@@ -1327,6 +1330,26 @@ RESTIR_KERNEL void k_restir_spatial(DevScene S, DevPaths P, const MptFrame* __re
 // (staged and traced, never used).
 constexpr uint32_t RSE_VIS = 0x80000000u;   // eval item flag: the target is evaluated with visibility
 
+// appends items (positions in `mask` of slot s, flags per position) to the two class lists
+DEV void rs_append_items(const DevPaths& P, int s, uint32_t m_plain, uint32_t m_gen, uint32_t vis_bits, uint32_t prev_bits,
+                         int* tmp, int* base) {
+    for (int c = 0; c < 2; c++) {
+        uint32_t mask = c == 0 ? m_plain : m_gen;
+        int tot;
+        const int off = rs_block_scan(__popc(mask), tmp, tot);
+        if (threadIdx.x == 0) *base = tot ? atomicAdd(&P.counters[CTR_RQE0 + c], tot) : 0;
+        __syncthreads();
+        int32_t* list = P.rq_items + (size_t)c * P.n * RS_RPP;
+        int o = *base + off;
+        while (mask) {
+            const int j = __builtin_ctz(mask);
+            mask &= mask - 1u;
+            list[o++] = (s * RS_RPP + j) | (((vis_bits >> j) & 1u) ? (int)RSE_VIS : 0) | (((prev_bits >> j) & 1u) ? (int)RSE_PREV : 0);
+        }
+        __syncthreads();
+    }
+}
+
 template <int OVR>
 __global__ __launch_bounds__(TB) void k_rsp_select(DevScene S, DevPaths P, const MptFrame* __restrict__ Fp, int pass,
                                                    const float4* __restrict__ in) {
@@ -1388,40 +1411,29 @@ __global__ __launch_bounds__(TB) void k_rsp_select(DevScene S, DevPaths P, const
                         (n_plain ? m_plain : m_gen) |= 1u << (2 * k + 1);
                         vis_bits |= 1u << (2 * k + 1);   // ReSTIR_DI_BiasCorrectionUseVisibility
                     }
-                    P.rq_rec[(size_t)s * RS_KMAX + k] = make_float4(__int_as_float(ni), 0.0f, 0.0f, jac);
+                    P.rq_rec[(size_t)s * RS_REC + k] = make_float4(__int_as_float(ni), 0.0f, 0.0f, jac);
                 }
             }
         }
         P.rq_meta[s] = meta;
     }
     // item lists: plain at [0, n * RS_RPP), generic at [n * RS_RPP, 2 n * RS_RPP)
-    for (int c = 0; c < 2; c++) {
-        uint32_t mask = c == 0 ? m_plain : m_gen;
-        int tot;
-        const int off = rs_block_scan(__popc(mask), tmp, tot);
-        if (threadIdx.x == 0) base = tot ? atomicAdd(&P.counters[CTR_RQE0 + c], tot) : 0;
-        __syncthreads();
-        int32_t* list = P.rq_items + (size_t)c * P.n * RS_RPP;
-        int o = base + off;
-        while (mask) {
-            const int j = __builtin_ctz(mask);
-            mask &= mask - 1u;
-            list[o++] = (s * RS_RPP + j) | (((vis_bits >> j) & 1u) ? (int)RSE_VIS : 0);
-        }
-        __syncthreads();
-    }
+    rs_append_items(P, s, m_plain, m_gen, vis_bits, 0u, tmp, &base);
 }
 
 // One target-function evaluation per item of a class list (count in the device counter);
 // grid-stride with a block-uniform trip count (the block appends its rays each round).
-template <int OVR, bool PLAIN>
+// FUSED: an item of the fused spatiotemporal pass (positions 0 / 1: the temporal neighbour,
+// record RS_KMAX; 2 + 2k + which: spatial neighbour k; the canonical sample is the initial
+// candidates' reservoir), else of a spatial pass.
+template <int OVR, bool PLAIN, bool FUSED>
 RESTIR_KERNEL void k_rsp_eval(DevScene S, DevPaths P, const MptFrame* __restrict__ Fp, int pass, const float4* __restrict__ in,
                               const int32_t* __restrict__ items, const int32_t* __restrict__ count_ptr) {
     __shared__ int tmp[TB / 64];
     __shared__ int base;
     const MptFrame& F = *Fp;
     const BCtx bc = make_bctx(S, F);
-    const uint32_t pass_rs = F.restir_di_seeds[4 + pass];
+    const uint32_t pass_rs = FUSED ? F.restir_di_seeds[2] : F.restir_di_seeds[4 + pass];
     const bool alpha = F.render_settings.do_alpha_testing;
     const int count = *count_ptr;
     for (int b0 = blockIdx.x * TB; b0 < count; b0 += gridDim.x * TB) {
@@ -1430,23 +1442,26 @@ RESTIR_KERNEL void k_rsp_eval(DevScene S, DevPaths P, const MptFrame* __restrict
         int s = 0;
         if (i < count) {
             const uint32_t it = (uint32_t)items[i];
-            const bool vis = (it & RSE_VIS) != 0;
-            const int id = (int)(it & ~RSE_VIS);
+            const bool vis = (it & RSE_VIS) != 0, prev = (it & RSE_PREV) != 0;
+            const int id = (int)(it & ~(RSE_VIS | RSE_PREV));
             s = id / RS_RPP;
-            const int j = id - s * RS_RPP, k = j >> 1, which = j & 1;
+            const int j = id - s * RS_RPP;
+            const bool temporal = FUSED && j < 2;
+            const int jj = FUSED ? (temporal ? j : j - 2) : j;
+            const int k = temporal ? RS_KMAX : jj >> 1, which = jj & 1;
             const int center = s + P.pix_off;
-            float* rec = reinterpret_cast<float*>(&P.rq_rec[(size_t)s * RS_KMAX + k]);
+            float* rec = reinterpret_cast<float*>(&P.rq_rec[(size_t)s * RS_REC + k]);
             const int ni = __float_as_int(rec[0]);
-            const int at = which ? ni : center;
-            const RSurf g = gb_surface(S, P, at, false);
-            const RResv smp = rr_load(in, which ? center : ni);
+            const RSurf g = gb_surface(S, P, which ? ni : center, which && prev);
+            const RResv smp = which ? rr_load(FUSED ? P.rs_init : in, center) : rr_load(in, ni);
             TgtRay ray;
             float t;
             if (PLAIN) t = restir_target_unocc<true>(S, F, bc, smp.tri, smp.point, smp.flags, g, vis, OVR, ray);
             else t = restir_target_unocc<false>(S, F, bc, smp.tri, smp.point, smp.flags, g, vis, OVR, ray);
             rec[1 + which] = t;
             if (vis && t > 0.0f) {
-                const uint32_t key = alpha ? alpha_key(pass_seed(F, (uint32_t)center, pass_rs), 0, 7, which ? RP_TCN(k) : RP_TFC(k)) : 0u;
+                const int pos = temporal ? (which ? RP_T_TCN : RP_T_TFC) : (which ? RP_TCN(k) : RP_TFC(k));
+                const uint32_t key = alpha ? alpha_key(pass_seed(F, (uint32_t)center, pass_rs), 0, FUSED ? 6 : 7, pos) : 0u;
                 rs_stage_ray(P, (size_t)id, ray, g.last, key);
                 rmask = 1u << j;
             }
@@ -1489,7 +1504,7 @@ RESTIR_KERNEL void k_rsp_combine(DevScene S, DevPaths P, const MptFrame* __restr
             float4 rec = make_float4(0.0f, 0.0f, 0.0f, 1.0f);
             if (k == reuse) nr = cres;
             else {
-                rec = P.rq_rec[(size_t)s * RS_KMAX + k];
+                rec = P.rq_rec[(size_t)s * RS_REC + k];
                 nr = rr_load(in, __float_as_int(rec.x));
             }
             const bool vis = spatial_visibility(F, rd, k, reuse);
@@ -1551,6 +1566,237 @@ RESTIR_KERNEL void k_rsp_combine(DevScene S, DevPaths P, const MptFrame* __restr
     }
     rs_append(P, &P.counters[CTR_RQV], s, vmask, tmp, &base);
     // ray counters: one atomic per block (per wave, 32 k atomics on one word would serialise)
+    int tot;
+    (void)rs_block_scan((int)n_any, tmp, tot);
+    if (threadIdx.x == 0 && tot) atomicAdd((unsigned long long*)&P.ray_counts[1], (unsigned long long)tot);
+}
+
+// ---- staged fused spatiotemporal pass (the reference-default weights) -------------------
+// As the staged spatial pass: k_rst_select (the temporal neighbour search with its RNG
+// draws, the spatial neighbours around the reprojected position, similarity, Jacobians,
+// class-sorted evaluation items), k_rsp_eval<PLAIN, FUSED>, the traced list, k_rst_combine.
+// Record RS_KMAX holds the temporal neighbour (index, targets, Jacobian), record RS_KMAX + 1
+// the RNG state after the neighbour rotation and the reprojected position.
+template <int OVR>
+__global__ __launch_bounds__(TB) void k_rst_select(DevScene S, DevPaths P, const MptFrame* __restrict__ Fp) {
+    __shared__ int tmp[TB / 64];
+    __shared__ int base;
+    const MptFrame& F = *Fp;
+    float4* tin = P.rs_tin;
+    const int s = blockIdx.x * TB + threadIdx.x;
+    uint32_t m_plain = 0u, m_gen = 0u, vis_bits = 0u, prev_bits = 0u;
+    if (s < P.n) {
+        const int center = s + P.pix_off;
+        int4 meta = make_int4(RSM_SKIP, 0, 0, 0);
+        MptReSTIRDISettings rd = F.render_settings.restir_di_settings;
+        rd.spatial_pass_index = 0;   // configure_spatial_pass_for_fused_spatiotemporal(0)
+        if (P.active[s] && P.gb_meta[center].z) {
+            Rng rng = make_rng(pass_seed(F, (uint32_t)center, F.restir_di_seeds[2]));
+            const RSurf cs = gb_surface(S, P, center, false);
+            if (!is_emissive(*cs.m)) {
+                const bool use_prev = rd.do_temporal_reuse_pass;
+                int tpx, tpy;
+                const int tidx = restir_temporal_neighbor(S, P, F, cs.p, cs.sn, *cs.m, rng, tpx, tpy);
+                RResv tres = rr_default();
+                tres.tri = -1;
+                if (tidx != -1 && !F.render_settings.freeze_random) tres = rr_load(tin, tidx);
+                if ((tidx == -1 || tres.M <= 1) && rd.do_disocclusion_reuse_boost) rd.reuse_neighbor_count = rd.disocclusion_reuse_count;
+                float cr = 1.0f, sr = 0.0f;
+                if (rd.do_neighbor_rotation) {
+                    const float2 sc = psincos(TWO_PI * rng());
+                    sr = sc.x;
+                    cr = sc.y;
+                }
+                const int reuse = rd.reuse_neighbor_count;
+                int cache = 0, vcount = 0, vM = 0;
+                int nis[RS_KMAX];
+                for (int k = 0; k < reuse; k++) {
+                    nis[k] = restir_spatial_neighbor(P, F, k, reuse, rd.reuse_radius, tpx, tpy, cr, sr, F.restir_di_seeds[2]);
+                    if (nis[k] == -1) continue;
+                    if (!restir_similar(S, P, rd, nis[k], *cs.m, cs.sp, cs.sn, use_prev)) continue;
+                    vM += rr_load(tin, nis[k]).M;
+                    vcount++;
+                    cache |= 1 << k;
+                }
+                const bool temporal_ok = tidx != -1 && tres.M > 0;
+                if (temporal_ok) { vcount++; vM += tres.M; }
+                meta = make_int4(0, cache, vM, vcount);
+                const RResv ic = rr_load(P.rs_init, center);
+                const bool update_mc = ic.M > 0 && ic.UCW > 0.0f;
+                const bool c_plain = OVR == MPT_BSDF_NONE && rs_plain(S, P, center, cs);
+                const uint32_t pv = use_prev ? 1u : 0u;
+                if (temporal_ok) {
+                    float jac = 1.0f;
+                    if (tres.UCW > 0.0f) {
+                        (c_plain ? m_plain : m_gen) |= 1u << 0;
+                        vis_bits |= 1u << 0;   // bias-correction visibility
+                        if (!(tres.flags & RF_ENVMAP)) {
+                            const RSurf ts = gb_surface(S, P, tidx, use_prev);
+                            jac = restir_jacobian(S, tres, cs.sp, ts.sp - ts.sn * 1.0e-4f);
+                        }
+                    }
+                    if (update_mc) {
+                        const bool t_plain = OVR == MPT_BSDF_NONE && rs_plain(S, P, tidx, gb_surface(S, P, tidx, use_prev), use_prev);
+                        (t_plain ? m_plain : m_gen) |= 1u << 1;
+                        vis_bits |= 1u << 1;
+                        prev_bits |= pv << 1;
+                    }
+                    P.rq_rec[(size_t)s * RS_REC + RS_KMAX] = make_float4(__int_as_float(tidx), 0.0f, 0.0f, jac);
+                }
+                for (int k = 0; k < reuse && vM != 0; k++) {
+                    if (!((cache >> k) & 1)) continue;
+                    const int ni = nis[k];
+                    const RResv nr = rr_load(tin, ni);
+                    float jac = 1.0f;
+                    if (nr.UCW > 0.0f) {
+                        (c_plain ? m_plain : m_gen) |= 1u << (2 + 2 * k);
+                        if (spatial_visibility(F, rd, k, reuse)) vis_bits |= 1u << (2 + 2 * k);
+                        if (!(nr.flags & RF_ENVMAP)) {
+                            const RSurf ns = gb_surface(S, P, ni, use_prev);
+                            jac = restir_jacobian(S, nr, cs.sp, ns.sp);
+                        }
+                    }
+                    if (update_mc) {
+                        const bool n_plain = OVR == MPT_BSDF_NONE && rs_plain(S, P, ni, gb_surface(S, P, ni, use_prev), use_prev);
+                        (n_plain ? m_plain : m_gen) |= 1u << (3 + 2 * k);
+                        vis_bits |= 1u << (3 + 2 * k);
+                        prev_bits |= pv << (3 + 2 * k);
+                    }
+                    P.rq_rec[(size_t)s * RS_REC + k] = make_float4(__int_as_float(ni), 0.0f, 0.0f, jac);
+                }
+                P.rq_rec[(size_t)s * RS_REC + RS_KMAX + 1] = make_float4(__uint_as_float(rng.s), __int_as_float(tidx), 0.0f, 0.0f);
+            }
+        }
+        P.rq_meta[s] = meta;
+    }
+    rs_append_items(P, s, m_plain, m_gen, vis_bits, prev_bits, tmp, &base);
+}
+
+template <int OVR>
+RESTIR_KERNEL void k_rst_combine(DevScene S, DevPaths P, const MptFrame* __restrict__ Fp) {
+    __shared__ int tmp[TB / 64];
+    __shared__ int base;
+    const MptFrame& F = *Fp;
+    const bool alpha = F.render_settings.do_alpha_testing;
+    float4* tin = P.rs_tin;
+    const int s = blockIdx.x * TB + threadIdx.x;
+    uint32_t vmask = 0u, n_any = 0u;
+    if (s < P.n && !(P.rq_meta[s].x & RSM_SKIP)) {
+        const int4 meta = P.rq_meta[s];
+        const int center = s + P.pix_off;
+        MptReSTIRDISettings rd = F.render_settings.restir_di_settings;
+        rd.spatial_pass_index = 0;
+        const float4 st4 = P.rq_rec[(size_t)s * RS_REC + RS_KMAX + 1];
+        Rng rng = make_rng(__float_as_uint(st4.x));   // after the temporal search and the rotation
+        const int tidx = __float_as_int(st4.y);
+        RResv tres = rr_default();
+        tres.tri = -1;
+        if (tidx != -1 && !F.render_settings.freeze_random) tres = rr_load(tin, tidx);
+        if ((tidx == -1 || tres.M <= 1) && rd.do_disocclusion_reuse_boost) rd.reuse_neighbor_count = rd.disocclusion_reuse_count;
+        const int reuse = rd.reuse_neighbor_count;
+        const int cache = meta.y, vM = meta.z, vcount = meta.w;
+        const bool temporal_ok = tidx != -1 && tres.M > 0;
+        const RResv ic = rr_load(P.rs_init, center);
+        const bool update_mc = ic.M > 0 && ic.UCW > 0.0f;
+        RResv o = rr_default();
+        PairwiseMIS mis{0.0f, true, true};
+        int ntr = 0;
+        const size_t r0 = (size_t)s * RS_RPP;
+        if (temporal_ok) {
+            const float4 rec = P.rq_rec[(size_t)s * RS_REC + RS_KMAX];
+            float tfc = 0.0f;
+            if (tres.UCW > 0.0f) {
+                tfc = rec.y;
+                if (tfc > 0.0f) {
+                    if (P.rq_occ[r0]) tfc = 0.0f;
+                    ntr++;
+                }
+            }
+            float jac = 1.0f;
+            if (tfc > 0.0f && tres.UCW > 0.0f && !(tres.flags & RF_ENVMAP)) {
+                jac = rec.w;
+                if (jac == -1.0f) jac = 0.0f;
+            }
+            float tcn = 0.0f;
+            if (update_mc) {
+                tcn = rec.z;
+                if (tcn > 0.0f) {
+                    if (P.rq_occ[r0 + 1]) tcn = 0.0f;
+                    ntr++;
+                }
+            }
+            const float wgt = mis.weight_tcn(rd, tres, ic, tfc, tcn, vcount, vM, update_mc, false);
+            if (rr_combine(o, tres, wgt, tfc, jac, rng)) o.flags |= RF_UNOCCLUDED;
+        }
+        for (int k = vM == 0 ? reuse : 0; k < reuse + 1; k++) {
+            if (k < reuse && !((cache >> k) & 1)) continue;
+            RResv nr;
+            float4 rec = make_float4(0.0f, 0.0f, 0.0f, 1.0f);
+            if (k == reuse) nr = ic;
+            else {
+                rec = P.rq_rec[(size_t)s * RS_REC + k];
+                nr = rr_load(tin, __float_as_int(rec.x));
+            }
+            const bool vis = spatial_visibility(F, rd, k, reuse);
+            float tfc = 0.0f;
+            if (nr.UCW > 0.0f) {
+                if (k == reuse) tfc = nr.target;
+                else {
+                    tfc = rec.y;
+                    if (vis && tfc > 0.0f) {
+                        if (P.rq_occ[r0 + 2 + 2 * k]) tfc = 0.0f;
+                        ntr++;
+                    }
+                }
+            }
+            float jac = 1.0f;
+            if (tfc > 0.0f && nr.UCW > 0.0f && k != reuse && !(nr.flags & RF_ENVMAP)) {
+                jac = rec.w;
+                if (jac == -1.0f) {   // (its staged bias-correction ray is not used)
+                    o.M += nr.M;
+                    continue;
+                }
+            }
+            float wgt;
+            if (nr.UCW == 0.0f && !update_mc) wgt = 1.0f;
+            else {
+                float tcn = 0.0f;
+                if (k != reuse && update_mc) {
+                    tcn = rec.z;
+                    if (tcn > 0.0f) {
+                        if (P.rq_occ[r0 + 3 + 2 * k]) tcn = 0.0f;
+                        ntr++;
+                    }
+                }
+                wgt = mis.weight_tcn(rd, nr, ic, tfc, tcn, vcount, vM, update_mc, k == reuse);
+            }
+            if (rr_combine(o, nr, wgt, tfc, jac, rng)) {
+                if (vis) o.flags |= RF_UNOCCLUDED;
+                else if (k == reuse) o.flags |= nr.flags & RF_UNOCCLUDED;
+                else o.flags &= ~RF_UNOCCLUDED;
+            }
+        }
+        rr_end_normalized(o);
+        const bool vreuse = (F.options.restir_di_do_visibility_reuse ||
+                             (F.options.restir_di_initial_target_visibility && F.options.restir_di_spatial_target_visibility)) &&
+                            (rd.do_temporal_reuse_pass || rd.number_of_passes - 1 != rd.spatial_pass_index);
+        if (vreuse && o.UCW > 0.0f && !(o.flags & RF_UNOCCLUDED)) {
+            const float4 gp = P.gb_pos[center], gs = P.gb_sn[center];
+            const v3 sp = mk3(gp.x, gp.y, gp.z) + mk3(gs.x, gs.y, gs.z) * 1.0e-4f;
+            TgtRay ray;
+            ray.o = sp;
+            if (o.flags & RF_ENVMAP) { ray.d = mat_x_vec(F.world_settings.envmap_to_world_matrix.m, o.point); ray.dist = 1.0e35f; }
+            else { v3 dir = o.point - sp; ray.dist = length(dir); ray.d = dir / ray.dist; }
+            const uint32_t seed = pass_seed(F, (uint32_t)center, F.restir_di_seeds[2]);
+            rs_stage_ray(P, r0, ray, P.gb_meta[center].x, alpha ? alpha_key(seed, 0, 6, RP_VISREUSE) : 0u);
+            vmask = 1u;
+            ntr++;
+        }
+        if (rd.m_cap > 0) o.M = imin(o.M, rd.m_cap);
+        rr_store(P.rs_out, center, o);
+        n_any = (uint32_t)ntr;
+    }
+    rs_append(P, &P.counters[CTR_RQV], s, vmask, tmp, &base);
     int tot;
     (void)rs_block_scan((int)n_any, tmp, tot);
     if (threadIdx.x == 0 && tot) atomicAdd((unsigned long long*)&P.ray_counts[1], (unsigned long long)tot);
