@@ -1,12 +1,20 @@
-// bvh8.cpp -- host BVH8 builder: binned-SAH BVH2, greedy collapse to 8-wide nodes
-// (expand the child with the largest surface area), octant-ordered child slots
-// (so that a ray visits slot k ^ (octant ^ 7) first, front to back), conservative
-// 8-bit quantisation of child boxes.  See bvh8.h for the node format.
+// bvh8.cpp -- host BVH8 builder: binned-SAH BVH2, collapsed to 8-wide nodes, octant-ordered
+// child slots (so that a ray visits slot k ^ (octant ^ 7) first, front to back),
+// conservative 8-bit quantisation of child boxes.  See bvh8.h for the node format.
+// Collapse: greedy (expand the child with the largest surface area, BVH2 leaves of
+// max_leaf triangles), or with MPT_BVH_COLLAPSE=cost a surface-area cost minimisation over
+// the whole BVH2 built down to single triangles (the dynamic programme of compressed wide
+// BVH builders: each subtree takes the cheapest way to stand as 1..8 child slots -- one leaf
+// of up to max_leaf triangles, one internal node, or its two children's slots).  Measured on
+// the C3 city (tools/bvh_check.py, 100 k camera + bounce rays): greedy 7.37 nodes / 2.33
+// triangles per ray, cost 7.57 / 2.43 (triangle / node cost 0.1 - 1.0: no better), so greedy
+// stays the default; 64 / 128 SAH bins instead of 32 gain < 1 %.
 #include "bvh8.h"
 
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 
 namespace mpt {
@@ -31,6 +39,7 @@ struct Builder {
     const int32_t* idx;
     int n;
     int max_leaf;
+    int sah_depth = 40;   // deeper than this, only balanced (median) splits
     std::vector<AABB> tbox;
     std::vector<float> cen;
     std::vector<int> order;
@@ -44,15 +53,15 @@ struct Builder {
         nodes[id].box = b;
         int cnt = end - begin;
         if (cnt <= max_leaf) { nodes[id].first = begin; nodes[id].count = cnt; return id; }
-        const int NB = 32;
+        const int NB = std::getenv("MPT_BVH_BINS") ? std::atoi(std::getenv("MPT_BVH_BINS")) : 32;
         int best_axis = -1, best_split = 0;
         float best_cost = FLT_MAX;
-        // past depth 40 only balanced splits, so the tree depth stays below 64 (traversal stack)
-        for (int ax = 0; ax < 3 && depth < 40; ax++) {
+        // past sah_depth only balanced splits, so that the tree depth stays bounded (traversal stack)
+        for (int ax = 0; ax < 3 && depth < sah_depth; ax++) {
             float ext = cb.hi[ax] - cb.lo[ax];
             if (!(ext > 0.0f)) continue;
-            AABB bb[NB];
-            int bc[NB] = {0};
+            AABB bb[256];
+            int bc[256] = {0};
             float k = NB / ext;
             for (int i = begin; i < end; i++) {
                 int t = order[i];
@@ -60,8 +69,8 @@ struct Builder {
                 bb[bi].grow(tbox[t]);
                 bc[bi]++;
             }
-            float la[NB];
-            int lc[NB];
+            float la[256];
+            int lc[256];
             AABB acc;
             int ac = 0;
             for (int i = 0; i < NB; i++) { acc.grow(bb[i]); ac += bc[i]; la[i] = acc.valid() ? acc.area() : 0.0f; lc[i] = ac; }
@@ -117,7 +126,7 @@ float scene_box_pad(const float* vertices, int num_triangles, const int32_t* ind
 }
 
 void build_bvh8(const float* vertices, const int32_t* indices, int32_t num_triangles, BVH8& out, int max_leaf,
-                float pad_in) {
+                float pad_in, int sah_depth) {
     out.nodes.clear();
     out.tris.clear();
     if (num_triangles <= 0) return;
@@ -127,6 +136,7 @@ void build_bvh8(const float* vertices, const int32_t* indices, int32_t num_trian
     b.idx = indices;
     b.n = num_triangles;
     b.max_leaf = max_leaf;
+    b.sah_depth = sah_depth;
     b.tbox.resize(num_triangles);
     b.cen.resize(3 * (size_t)num_triangles);
     b.order.resize(num_triangles);
@@ -143,8 +153,93 @@ void build_bvh8(const float* vertices, const int32_t* indices, int32_t num_trian
     const float pad = pad_in >= 0.0f ? pad_in : scene_box_pad(vertices, num_triangles, indices);
     for (int t = 0; t < num_triangles; t++)
         for (int i = 0; i < 3; i++) { b.tbox[t].lo[i] -= pad; b.tbox[t].hi[i] += pad; }
+    const char* cm = std::getenv("MPT_BVH_COLLAPSE");
+    const bool greedy = !(cm && std::strcmp(cm, "cost") == 0);
+    const int leaf_max = max_leaf;
+    if (!greedy) b.max_leaf = 1;   // the cost collapse forms leaves from BVH2 subtrees itself
     b.nodes.reserve(2 * (size_t)num_triangles);
     int root = b.build2(0, num_triangles, 0);
+
+    // ---- cost collapse: cost[n][i-1] = cheapest representation of subtree n as at most i
+    // child slots; how[n][i-1]: 0 = as i - 1 slots, 1..7 = split (k slots left, i - k right),
+    // for i = 1: 8 = one leaf slot, 9 = one internal node
+    const size_t N2n = b.nodes.size();
+    std::vector<float> cost;
+    std::vector<uint8_t> how, split8;   // split8[n]: slots of n's left child when n is an internal BVH8 node
+    std::vector<int> tri_count;
+    if (!greedy) {
+        const float C_NODE = 1.0f;
+        const char* ct = std::getenv("MPT_BVH_CTRI");   // development A/B: triangle test cost / node test cost
+        const float C_TRI = ct ? (float)std::atof(ct) : 0.3f;
+        cost.assign(N2n * 8, 0.0f);
+        how.assign(N2n * 8, 0);
+        split8.assign(N2n, 0);
+        tri_count.assign(N2n, 0);
+        // children have larger indices than their parent (pre-order build): reverse order is post-order
+        for (size_t ni = N2n; ni-- > 0;) {
+            const N2& nd = b.nodes[ni];
+            const float A = nd.box.area();
+            float* c = &cost[ni * 8];
+            uint8_t* h = &how[ni * 8];
+            if (nd.count > 0) {
+                tri_count[ni] = nd.count;
+                for (int i = 0; i < 8; i++) { c[i] = A * C_TRI * (float)nd.count; h[i] = i == 0 ? 8 : 0; }
+                continue;
+            }
+            const int l = nd.left, r = nd.right;
+            tri_count[ni] = tri_count[l] + tri_count[r];
+            const float* cl = &cost[(size_t)l * 8];
+            const float* cr = &cost[(size_t)r * 8];
+            float dist[9];
+            uint8_t dk[9];
+            for (int j = 2; j <= 8; j++) {
+                dist[j] = FLT_MAX;
+                dk[j] = 1;
+                for (int k = 1; k < j; k++) {
+                    const float v = cl[k - 1] + cr[j - k - 1];
+                    if (v < dist[j]) { dist[j] = v; dk[j] = (uint8_t)k; }
+                }
+            }
+            const float c_internal = A * C_NODE + dist[8];
+            split8[ni] = dk[8];
+            const float c_leaf = tri_count[ni] <= leaf_max ? A * C_TRI * (float)tri_count[ni] : FLT_MAX;
+            c[0] = std::min(c_leaf, c_internal);
+            h[0] = c_leaf <= c_internal ? 8 : 9;
+            for (int i = 2; i <= 8; i++) {
+                if (dist[i] < c[i - 2]) { c[i - 1] = dist[i]; h[i - 1] = dk[i]; }
+                else { c[i - 1] = c[i - 2]; h[i - 1] = 0; }
+            }
+        }
+    }
+    // the child slots of a BVH8 node made from BVH2 node n: n's subtree distributed over 8
+    // slots as the cost choices say; each slot is a BVH2 node (a leaf slot if its choice is
+    // 'leaf' or it is a BVH2 leaf, else an internal BVH8 node)
+    auto distribute = [&](int n) {
+        std::vector<int> out_slots;
+        std::vector<std::pair<int, int>> work{{b.nodes[n].left, split8[n]}, {b.nodes[n].right, 8 - split8[n]}};
+        while (!work.empty()) {
+            auto [x, j] = work.back();
+            work.pop_back();
+            while (j > 1 && how[(size_t)x * 8 + j - 1] == 0) j--;
+            if (j == 1 || b.nodes[x].count > 0) { out_slots.push_back(x); continue; }
+            const int k = how[(size_t)x * 8 + j - 1];
+            work.push_back({b.nodes[x].left, k});
+            work.push_back({b.nodes[x].right, j - k});
+        }
+        return out_slots;
+    };
+    auto is_leaf_slot = [&](int x) { return b.nodes[x].count > 0 || (!greedy && how[(size_t)x * 8] == 8); };
+    // the triangles of a leaf slot: the BVH2 subtree's triangles, in order
+    auto leaf_tris = [&](int x, std::vector<int>& tris) {
+        std::vector<int> stk{x};
+        while (!stk.empty()) {
+            int y = stk.back();
+            stk.pop_back();
+            const N2& ny = b.nodes[y];
+            if (ny.count > 0) { for (int k = 0; k < ny.count; k++) tris.push_back(b.order[ny.first + k]); }
+            else { stk.push_back(ny.right); stk.push_back(ny.left); }
+        }
+    };
 
     // BFS over BVH8 nodes; each entry names the BVH2 node it collapses
     struct Item { int n2; int n8; int depth; };
@@ -159,19 +254,23 @@ void build_bvh8(const float* vertices, const int32_t* indices, int32_t num_trian
         // gather up to 8 children
         std::vector<int> ch;
         const N2& r2 = b.nodes[it.n2];
-        if (r2.count > 0) ch.push_back(it.n2);
-        else { ch.push_back(r2.left); ch.push_back(r2.right); }
-        while (ch.size() < 8) {
-            int best = -1;
-            float ba = -1.0f;
-            for (int i = 0; i < (int)ch.size(); i++) {
-                const N2& c = b.nodes[ch[i]];
-                if (c.count == 0 && c.box.area() > ba) { ba = c.box.area(); best = i; }
+        if (r2.count > 0 || (!greedy && how[(size_t)it.n2 * 8] == 8)) ch.push_back(it.n2);   // the root is one leaf
+        else if (!greedy) ch = distribute(it.n2);
+        else {
+            ch.push_back(r2.left);
+            ch.push_back(r2.right);
+            while (ch.size() < 8) {
+                int best = -1;
+                float ba = -1.0f;
+                for (int i = 0; i < (int)ch.size(); i++) {
+                    const N2& c = b.nodes[ch[i]];
+                    if (c.count == 0 && c.box.area() > ba) { ba = c.box.area(); best = i; }
+                }
+                if (best < 0) break;
+                int nb = ch[best];
+                ch[best] = b.nodes[nb].left;
+                ch.push_back(b.nodes[nb].right);
             }
-            if (best < 0) break;
-            int nb = ch[best];
-            ch[best] = b.nodes[nb].left;
-            ch.push_back(b.nodes[nb].right);
         }
         // node box and slot assignment (octant heuristic)
         AABB nb;
@@ -232,16 +331,17 @@ void build_bvh8(const float* vertices, const int32_t* indices, int32_t num_trian
             }
             nd.qlox[s] = qlo[0]; nd.qloy[s] = qlo[1]; nd.qloz[s] = qlo[2];
             nd.qhix[s] = qhi[0]; nd.qhiy[s] = qhi[1]; nd.qhiz[s] = qhi[2];
-            if (c.count == 0) {
+            if (!is_leaf_slot(ch[ci])) {
                 nd.imask |= (uint8_t)(1u << s);
                 nd.meta[s] = (uint8_t)internal_rank++;
                 out.nodes.emplace_back();
                 queue.push_back({ch[ci], (int)out.nodes.size() - 1, it.depth + 1});
             } else {
                 int off = (int)out.tris.size() - (int)nd.tri_base;
-                nd.meta[s] = (uint8_t)((c.count << 5) | off);
-                for (int k = 0; k < c.count; k++) {
-                    int t = b.order[c.first + k];
+                std::vector<int> lt;
+                leaf_tris(ch[ci], lt);
+                nd.meta[s] = (uint8_t)(((int)lt.size() << 5) | off);
+                for (int t : lt) {
                     const float* A = vertices + 3 * (size_t)indices[3 * (size_t)t + 0];
                     const float* B = vertices + 3 * (size_t)indices[3 * (size_t)t + 1];
                     const float* C = vertices + 3 * (size_t)indices[3 * (size_t)t + 2];

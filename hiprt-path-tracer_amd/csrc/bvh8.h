@@ -46,8 +46,10 @@ struct BVH8 {
 // Builds the BVH8 over indexed triangles.  max_leaf: triangles per leaf child (<= 4).
 // pad: triangle-box padding (< 0: 2^-20 of the largest coordinate of these triangles; a
 // BVH over a subset of a scene passes the whole scene's pad, scene_box_pad).
+// sah_depth: BVH2 depth below which SAH splits are used, balanced splits beyond (a smaller
+// value gives a shallower tree: the rebuild of a BVH too deep for the traversal stack).
 void build_bvh8(const float* vertices, const int32_t* indices, int32_t num_triangles, BVH8& out, int max_leaf = 3,
-                float pad = -1.0f);
+                float pad = -1.0f, int sah_depth = 40);
 float scene_box_pad(const float* vertices, int num_triangles, const int32_t* indices);
 
 }  // namespace mpt

@@ -847,15 +847,22 @@ int mpt_upload_scene(MptContext* c, const MptScene* s) {
     // triangles per leaf child: 3 (MPT_BVH_LEAF, 1..4, development A/B)
     int max_leaf = 3;
     if (const char* e = std::getenv("MPT_BVH_LEAF")) max_leaf = std::max(1, std::min(4, std::atoi(e)));
-    build_bvh8(s->vertices, s->triangle_indices, s->num_triangles, c->bvh, max_leaf);
+    // per level: at most one node group and one postponed triangle group on the stack; a
+    // tree too deep for the traversal stack is rebuilt with balanced splits from a smaller
+    // depth on (test hook MPT_BVH_MAX_STACK: a lower limit)
+    int stack_cap = MAX_STACK;
+    if (const char* e = std::getenv("MPT_BVH_MAX_STACK")) stack_cap = std::max(4, std::min(MAX_STACK, std::atoi(e)));
+    for (int sah_depth = 40;; sah_depth = sah_depth * 2 / 3) {
+        build_bvh8(s->vertices, s->triangle_indices, s->num_triangles, c->bvh, max_leaf, -1.0f, sah_depth);
+        if (2 * c->bvh.depth + 2 <= stack_cap || sah_depth == 0) break;
+    }
     c->box_pad = scene_box_pad(s->vertices, s->num_triangles, s->triangle_indices);
     c->h_idx.assign(s->triangle_indices, s->triangle_indices + 3 * (size_t)s->num_triangles);
     c->h_pos.assign(s->vertices, s->vertices + 3 * (size_t)s->num_vertices);
     c->h_light_prims.clear();
     c->nodes_light.release();
     c->tris_light.release();
-    // per level: at most one node group and one postponed triangle group on the stack
-    if (2 * c->bvh.depth + 2 > MAX_STACK) return fail(MPT_ERR_UNSUPPORTED, "BVH8 deeper than the traversal stack");
+    if (2 * c->bvh.depth + 2 > stack_cap) return fail(MPT_ERR_UNSUPPORTED, "BVH8 deeper than the traversal stack");
     hipStream_t st = c->stream;
     HIPCHK(c->nodes.upload(c->bvh.nodes.data(), c->bvh.nodes.size(), st));
     HIPCHK(c->tris.upload(c->bvh.tris.data(), c->bvh.tris.size(), st));

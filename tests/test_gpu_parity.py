@@ -371,3 +371,29 @@ def test_city_full_frame_batched_equals_sequential(city, luts):
     for k, what in enumerate(["color", "albedo", "normals"]):
         assert_same(bat[k], seq[k], f"full-frame batched vs sequential {what}")
     assert np.isfinite(bat[0]).all() and bat[0].mean() > 0
+
+
+@pytest.mark.parametrize("mode", ["shallow_rebuild", "cost_collapse"])
+def test_traversal_bvh_variants_bit_exact(scenes, luts, monkeypatch, mode):
+    """BVH variants give the same hits (traversal results never depend on the BVH): a tree
+    rebuilt shallower because it is too deep for the traversal stack (forced by the
+    MPT_BVH_MAX_STACK test hook: balanced splits from a smaller depth on, instead of refusing
+    the scene) and the surface-area cost collapse (MPT_BVH_COLLAPSE=cost), against the oracle."""
+    import mpt
+    if mode == "shallow_rebuild":
+        monkeypatch.setenv("MPT_BVH_MAX_STACK", "16")   # Cornell: depth 8 (SAH) -> 7 (balanced)
+    else:
+        monkeypatch.setenv("MPT_BVH_COLLAPSE", "cost")
+    sd = scenes["cornell_pbr"]
+    r = mpt.GPURenderer(0)
+    try:
+        r.set_scene(sd)
+        r.set_luts(luts)
+        o = oracle_for(sd, luts)
+        rays = random_rays(sd, 100000, 11)
+        gp, gt, _, _ = r.trace_closest(rays)
+        op, ot, _, _ = o.trace_closest(rays)
+        assert_same(gp, op, f"{mode}: prim")
+        assert_same(gt[op >= 0], ot[op >= 0], f"{mode}: t")
+    finally:
+        r.close()
