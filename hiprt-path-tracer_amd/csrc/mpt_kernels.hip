@@ -371,8 +371,18 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MODE == TM_P
     // most TRACE_BUDGET nodes.  A wave claims TRACE_CHUNK consecutive rays per atomic on
     // the shared counter and serves its refills from that chunk: the device-scope atomic
     // is a serial point for all 5k waves (one per refill put the short light-BVH
-    // traversals at 12 ns per refill, the counter's throughput).
+    // traversals at 12 ns per refill, the counter's throughput).  The first chunk of every
+    // wave is static -- wave w serves rays [w * sc, (w + 1) * sc) of the first n_waves * sc,
+    // sc = count / n_waves rounded up to 64 (at most TRACE_CHUNK) -- so that a launch starts
+    // without 20 k waves queueing on the counter, and a launch of fewer rays than
+    // n_waves * TRACE_CHUNK (the 1-spp ReSTIR DI wavefronts, the staged ReSTIR rays) takes no
+    // atomic at all; later chunks come from the counter, offset by the static part.
     Trav<ANY, STATS, TIE> tr;
+    const int n_waves = (int)gridDim.x * (TB / 64);
+    const int wave_id = (int)blockIdx.x * (TB / 64) + (int)(threadIdx.x >> 6);
+    int sc = (count + n_waves - 1) / max(1, n_waves);
+    sc = min(TRACE_CHUNK, max(64, (sc + 63) & ~63));
+    const int n_static = (int)min((long long)count, (long long)sc * n_waves);
     bool alive = false;
     bool exhausted = false;   // wave-uniform: the ray counter has passed `count`
     int ray = 0;              // RAW: ray index; NEE: staged query (slot * 4 + kind); PATH: slot
@@ -380,8 +390,9 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MODE == TM_P
     uint32_t pseed = 0u;      // PATH: pixel seed of the alpha keys
     bool was_inside = false;  // PATH: kept over re-traces, as in trace_ray's loop
     float qmax = 0.0f;        // NEE closest: the query's t_max
-    int chunk_next = 0, chunk_end = 0;   // wave-uniform: the unserved part of the wave's chunk
-    bool counter_done = false;           // wave-uniform: the shared counter has passed `count`
+    int chunk_next = min(wave_id * sc, n_static);                // wave-uniform: the unserved part of the wave's chunk
+    int chunk_end = min(chunk_next + sc, n_static);
+    bool counter_done = n_static >= count;                        // wave-uniform: the shared counter has passed `count`
     while (true) {
         const unsigned long long idle = __ballot(!alive);
         if (!exhausted && __popcll(idle) >= (unsigned)TRACE_REFILL) {
@@ -400,14 +411,14 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MODE == TM_P
                 chunk_next += take0;
                 if (take0 < need && !counter_done) {
                     int b = 0;
-                    if (lane_id() == 0) b = atomicAdd(A.fetch, TRACE_CHUNK);
+                    if (lane_id() == 0) b = n_static + atomicAdd(A.fetch, TRACE_CHUNK);
                     b = __shfl(b, 0);
                     counter_done = b + TRACE_CHUNK >= count;
                     chunk_end = min(b + TRACE_CHUNK, count);
                     base1 = b;
                     chunk_next = min(b + (need - take0), chunk_end);
                 } else {
-                    base1 = chunk_end;   // nothing left: the remaining lanes get i >= count
+                    base1 = count;   // nothing left for this wave: the remaining lanes get i >= count
                 }
                 exhausted = counter_done && chunk_next >= chunk_end;
             }
