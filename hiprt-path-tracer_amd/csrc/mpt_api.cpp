@@ -79,6 +79,7 @@ constexpr int FRAME_RING = 256;   // >= 2 x MPT_MAX_BATCH
 // bounces (validate_frame), + camera, ReSTIR, accumulate
 // + the ReSTIR DI kernels (G-buffer, presampling, initial, temporal / spatiotemporal, 4 spatial)
 constexpr int EV_POOL = 2 * 2 * (10 * 65 + 3 + 8);   // x2: the two halves of an overlapped batch
+constexpr int RESTIR_MAX_BATCH = 32;                    // ~45 timed scopes per batched ReSTIR DI sample
 #ifndef MPT_TRACE_BLOCKS_PER_CU
 #define MPT_TRACE_BLOCKS_PER_CU 5
 #endif
@@ -130,6 +131,7 @@ struct MptContext {
     // plain vertex deferred to the generic kernel (test hook); MPT_SHADE_CLASSES at mpt_create
     int shade_classes = 1;
     int restir_staged = 1;                // ReSTIR DI reuse passes staged around their rays (MPT_RESTIR_STAGED)
+    int restir_batch = 1;                 // ReSTIR DI samples batched after bounce 0 (MPT_RESTIR_BATCH)
     std::vector<MptMaterial> h_mats;
     std::vector<int32_t> h_mat_idx;       // per triangle (alpha flags of the triangle records)
     std::vector<uint8_t> h_tex_alpha;     // per texture: some texel has alpha < 255
@@ -791,6 +793,7 @@ int mpt_create(int device, void* hip_stream, MptContext** out) {
     MptContext* c = new MptContext();   // value-initialised: every handle starts null
     if (const char* e = std::getenv("MPT_SHADE_CLASSES")) c->shade_classes = std::atoi(e);
     if (const char* e = std::getenv("MPT_RESTIR_STAGED")) c->restir_staged = std::atoi(e);
+    if (const char* e = std::getenv("MPT_RESTIR_BATCH")) c->restir_batch = std::atoi(e);
     if (const char* e = std::getenv("MPT_LIGHT_BVH")) c->light_bvh = std::atoi(e);
     if (const char* e = std::getenv("MPT_OVERLAP")) c->overlap = std::atoi(e);
     if (const char* e = std::getenv("MPT_LIGHT_BVH_MAX_STACK")) c->light_bvh_max_stack = std::atoi(e);
@@ -1122,19 +1125,6 @@ static int ensure_overlap(MptContext* c) {
     return MPT_OK;
 }
 
-// Moves every per-slot pointer of P by `off` slots (the second half of an overlapped batch
-// owns slots [off, off + P.n) of the path state; per-pixel buffers stay shared).
-static void offset_slots(DevPaths& P, size_t off) {
-    P.ray_o += off; P.ray_d += off; P.hit += off; P.hit_inside += off; P.rng += off; P.seeds += off; P.thr += off; P.col += off;
-    P.vsA += off; P.vsB += off; P.alb += off; P.nrm += off;
-    P.q0 += off; P.q1 += off; P.qh += off; P.qm += off; P.qf += off; P.nq_light += off;
-    // NEE record planes, and the kind-major query / occlusion planes (stride = the allocation)
-    P.nthr += off; P.na += off; P.nb += off; P.ndir += off; P.nris += off; P.ne1 += off; P.ne2 += off;
-    P.nq_o += off; P.nq_d += off; P.occ += off; P.nq_tgt += 4 * off;
-    P.nhit += off; P.qmask += off; P.active += off;
-    if (P.mat_slot) P.mat_slot += off;
-}
-
 // Enqueues a prepared wavefront (prepare_batch).
 static int launch_batch(MptContext* c, const MptFrame* f, int batch) {
     const bool restir_part = f->options.direct_light_sampling == MPT_LSS_RESTIR_DI && f->band_count > 1;
@@ -1216,6 +1206,9 @@ static int launch_batch(MptContext* c, const MptFrame* f, int batch) {
         HIPCHK(hipStreamWaitEvent(c->stream, c->ev_join, 0));
         cfg.ev_used = cfg1.ev_used;
         cfg.launches = cfg0.launches + cfg1.launches;
+    } else if (f->options.direct_light_sampling == MPT_LSS_RESTIR_DI && batch > 1) {
+        P.group = std::max(c->n_slots, 1);   // slot = sample * pixels + pixel
+        e = launch_frames_restir(dev_scene(c), P, c->d_frames + slot, c->h_frames + slot, batch, cfg, c->stream);
     } else {
         e = launch_frame(dev_scene(c), P, c->d_frames + slot, *f, cfg, c->stream);
     }
@@ -1241,11 +1234,16 @@ int mpt_render_frame(MptContext* c, const MptFrame* f) {
 }
 
 // Frames that differ only in what GPURenderer::render changes between the samples of one
-// call (GPURenderer.cpp:424-449: sample number, seeds, AOV counter, reset / status flags)
-// and need no per-sample feedback (adaptive sampling, the stop-noise threshold and ReSTIR
-// DI read the previous sample's results) are rendered as one wavefront.
-static bool batchable(const MptFrame& a, const MptFrame& b) {
-    if (a.options.direct_light_sampling == MPT_LSS_RESTIR_DI) return false;
+// call (GPURenderer.cpp:424-449: sample number, seeds, AOV counter, reset / status flags;
+// ReSTIRDIRenderPass::launch's seeds and temporal-buffer clear, ReSTIRDIRenderPass.cpp:233-264)
+// and need no per-sample feedback on the host (adaptive sampling and the stop-noise
+// threshold gate each sample's camera rays on the previous ones) are rendered as one
+// wavefront.  ReSTIR DI samples, whose reuse passes read the previous sample's reservoirs,
+// run their first bounce one sample after the other (launch_frames_restir) and share the
+// later bounces' wavefront; not across a partition (the halo exchange is per sample).
+static bool batchable(const MptContext* c, const MptFrame& a, const MptFrame& b) {
+    const bool restir = a.options.direct_light_sampling == MPT_LSS_RESTIR_DI;
+    if (restir && (!c->restir_batch || a.band_count > 1)) return false;
     const MptRenderSettings& rs = a.render_settings;
     if ((rs.stop_pixel_noise_threshold > 0.0f || rs.enable_adaptive_sampling) && rs.accumulate) return false;
     MptFrame t = b;
@@ -1255,6 +1253,13 @@ static bool batchable(const MptFrame& a, const MptFrame& b) {
     t.render_settings.do_update_status_buffers = a.render_settings.do_update_status_buffers;
     t.random_seed = a.random_seed;
     t.camera_random_seed = a.camera_random_seed;
+    if (restir) {
+        MptReSTIRDISettings& rd = t.render_settings.restir_di_settings;
+        const MptReSTIRDISettings& ra = a.render_settings.restir_di_settings;
+        rd.permutation_sampling_random_bits = ra.permutation_sampling_random_bits;
+        rd.temporal_buffer_clear_requested = ra.temporal_buffer_clear_requested;
+        std::memcpy(t.restir_di_seeds, a.restir_di_seeds, sizeof(t.restir_di_seeds));
+    }
     return std::memcmp(&t, &a, sizeof(MptFrame)) == 0;
 }
 
@@ -1264,10 +1269,12 @@ int mpt_render_frames(MptContext* c, const MptFrame* frames, int32_t count, int3
     HIPCHK(hipSetDevice(c->device));   // default_batch sizes the wavefront from this device's free memory
     if (max_batch <= 0) max_batch = default_batch(c, frames[0]);
     max_batch = std::min<int32_t>(max_batch, MPT_MAX_BATCH);
+    // batched ReSTIR DI runs each sample's first bounce in turn (its timing events per sample)
+    if (frames[0].options.direct_light_sampling == MPT_LSS_RESTIR_DI) max_batch = std::min(max_batch, RESTIR_MAX_BATCH);
     int i = 0;
     while (i < count) {
         int b = 1;
-        while (i + b < count && b < max_batch && batchable(frames[i], frames[i + b])) b++;
+        while (i + b < count && b < max_batch && batchable(c, frames[i], frames[i + b])) b++;
         int r = prepare_batch(c, frames + i, b);
         // a wavefront that does not fit in device memory is halved (bit-identical result),
         // and the smaller size is kept for the rest of the call

@@ -235,6 +235,7 @@ enum {
     CTR_XANY = 11, CTR_XCL = 12, CTR_XLIGHT = 13,   // ext query lists (extended light sampling)
     CTR_RQ = 14, CTR_RQV = 15,                      // staged ReSTIR DI rays / visibility-reuse rays
     CTR_RQE0 = 16, CTR_RQE1 = 17,                   // staged ReSTIR DI target evaluations: plain / generic class
+    CTR_QG = 18,                                    // batched ReSTIR DI: the later bounces' path queue
     CTR_COUNT = 20
 };
 
@@ -267,8 +268,27 @@ struct LaunchCfg {
     hipEvent_t ev_acc_wait;
 };
 
+// Moves every per-slot pointer of P by `off` slots: a view of slots [off, off + P.n) of the
+// path state (the second half of an overlapped batch, one sample of a batched ReSTIR DI
+// wavefront); per-pixel buffers stay shared.
+inline void offset_slots(DevPaths& P, size_t off) {
+    P.ray_o += off; P.ray_d += off; P.hit += off; P.hit_inside += off; P.rng += off; P.seeds += off; P.thr += off; P.col += off;
+    P.vsA += off; P.vsB += off; P.alb += off; P.nrm += off;
+    P.q0 += off; P.q1 += off; P.qh += off; P.qm += off; P.qf += off; P.nq_light += off;
+    // NEE record planes, and the kind-major query / occlusion planes (stride = the allocation)
+    P.nthr += off; P.na += off; P.nb += off; P.ndir += off; P.nris += off; P.ne1 += off; P.ne2 += off;
+    P.nq_o += off; P.nq_d += off; P.occ += off; P.nq_tgt += 4 * off;
+    P.nhit += off; P.qmask += off; P.active += off;
+    if (P.mat_slot) P.mat_slot += off;
+}
+
 hipError_t launch_frame(const DevScene& S, const DevPaths& P, const MptFrame* d_frame, const MptFrame& h_frame,
                         LaunchCfg& cfg, hipStream_t st);
+// A batch of `batch` ReSTIR DI samples (P: batch samples, slot = sample * pixels + pixel):
+// each sample's camera rays, ReSTIR DI passes and first bounce in turn (each reads the
+// previous sample's reservoirs), then the later bounces of all samples as one wavefront.
+hipError_t launch_frames_restir(const DevScene& S, const DevPaths& P, const MptFrame* d_frames, const MptFrame* h_frames,
+                                int batch, LaunchCfg& cfg, hipStream_t st);
 hipError_t launch_resolve_materials(const DevScene& S, MptMaterial* out_res, int32_t* out_tex, int n, float4* em_tab,
                                    hipStream_t st);
 hipError_t launch_restir_fill(float4* reservoirs, int n, hipStream_t st);

@@ -2473,33 +2473,21 @@ static void launch_restir(const DevScene& S, DevPaths& P, const MptFrame* d_fram
     cfg.restir_out_sp2 = restir_code(P, P.rs_out);
 }
 
-hipError_t launch_frame(const DevScene& S, const DevPaths& P0, const MptFrame* d_frame, const MptFrame& hf, LaunchCfg& cfg,
-                        hipStream_t st) {
-    DevPaths P = P0;
+// Bounces [b_first, b_last] of the paths in q_cur (count counters[c_cur]): trace, G-buffer and
+// ReSTIR DI passes (bounce 0 of a ReSTIR DI frame), split, shade, miss, compact into q_next,
+// NEE rays, resolve.  Leaves the continuation list of the last bounce in the buffer passed
+// as q_next for an odd number of bounces, as q_cur for an even one.
+static void frame_bounces(const DevScene& S, DevPaths& P, const MptFrame* d_frame, const MptFrame& hf, LaunchCfg& cfg,
+                          hipStream_t st, int b_first, int b_last, int32_t* q_cur, int c_cur, int32_t* q_next,
+                          int c_next) {
     const int n = P.n;
-    if (n == 0) return hipSuccess;
-    const MptRenderSettings& hrs = hf.render_settings;
-    const bool as = (hrs.stop_pixel_noise_threshold > 0.0f || hrs.enable_adaptive_sampling) && hrs.accumulate;
     const bool restir = hf.options.direct_light_sampling == MPT_LSS_RESTIR_DI;
-    if (restir) {
-        hipLaunchKernelGGL(k_restir_frame_begin, dim3(blocks_for(P.rs_hi - P.rs_lo)), dim3(TB), 0, st, P, d_frame);
-        P.rs_out = restir_buffer(P, cfg.restir_out_sp2);
-    }
-    // all pixels start a path, unless adaptive sampling compacts the camera queue
-    hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(&P.counters[CTR_Q0]), as ? 0 : n, 1, st);
-    {
-        TimedScope ts(cfg, st, KT_CAMERA);
-        hipLaunchKernelGGL(k_camera, dim3(blocks_for(n)), dim3(TB), 0, st, P, d_frame);
-    }
-    int32_t* q_cur = P.q0;
-    int32_t* q_next = P.q1;
-    int c_cur = CTR_Q0, c_next = CTR_Q1;
     const int nb = hf.render_settings.nb_bounces;
     // material classes (k_split / k_shade): Principled BSDF only (the Lambert override has one class)
     // extended light sampling (DevPaths::x_per > 0): the EXT shading / resolve kernels, one class
     const bool ext = P.x_per > 0;
     const int classes = (hf.options.bsdf_override != MPT_BSDF_NONE || ext) ? 0 : (cfg.shade_classes != 0 ? 1 : 0);
-    for (int b = 0; b <= nb; b++) {
+    for (int b = b_first; b <= b_last; b++) {
         // continuation / camera rays
         hipMemsetAsync(&P.counters[CTR_FETCH], 0, sizeof(int32_t), st);
         TraceArgs ta{};
@@ -2600,6 +2588,26 @@ hipError_t launch_frame(const DevScene& S, const DevPaths& P0, const MptFrame* d
         int32_t* tq = q_cur; q_cur = q_next; q_next = tq;
         int tc = c_cur; c_cur = c_next; c_next = tc;
     }
+}
+
+hipError_t launch_frame(const DevScene& S, const DevPaths& P0, const MptFrame* d_frame, const MptFrame& hf, LaunchCfg& cfg,
+                        hipStream_t st) {
+    DevPaths P = P0;
+    const int n = P.n;
+    if (n == 0) return hipSuccess;
+    const MptRenderSettings& hrs = hf.render_settings;
+    const bool as = (hrs.stop_pixel_noise_threshold > 0.0f || hrs.enable_adaptive_sampling) && hrs.accumulate;
+    if (hf.options.direct_light_sampling == MPT_LSS_RESTIR_DI) {
+        hipLaunchKernelGGL(k_restir_frame_begin, dim3(blocks_for(P.rs_hi - P.rs_lo)), dim3(TB), 0, st, P, d_frame);
+        P.rs_out = restir_buffer(P, cfg.restir_out_sp2);
+    }
+    // all pixels start a path, unless adaptive sampling compacts the camera queue
+    hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(&P.counters[CTR_Q0]), as ? 0 : n, 1, st);
+    {
+        TimedScope ts(cfg, st, KT_CAMERA);
+        hipLaunchKernelGGL(k_camera, dim3(blocks_for(n)), dim3(TB), 0, st, P, d_frame);
+    }
+    frame_bounces(S, P, d_frame, hf, cfg, st, 0, hf.render_settings.nb_bounces, P.q0, CTR_Q0, P.q1, CTR_Q1);
     // an overlapped batch's second half adds its samples after the first half's (sample order)
     if (cfg.ev_acc_wait) hipStreamWaitEvent(st, cfg.ev_acc_wait, 0);
     {
@@ -2607,6 +2615,58 @@ hipError_t launch_frame(const DevScene& S, const DevPaths& P0, const MptFrame* d
         hipLaunchKernelGGL(k_accumulate, dim3(blocks_for(P.n_pix)), dim3(TB), 0, st, P, d_frame);
     }
     if (cfg.ev_acc_done) hipEventRecord(cfg.ev_acc_done, st);
+    return hipGetLastError();
+}
+
+
+// batched ReSTIR DI: sample s's continuation list (view slots) appended to the later
+// bounces' queue (slot = s * pixels + pixel); the queue length is added by k_add_count
+__global__ __launch_bounds__(TB) void k_append_queue(int32_t* __restrict__ dst, const int32_t* dst_count,
+                                                     const int32_t* __restrict__ src, const int32_t* src_count,
+                                                     int32_t off) {
+    const int i = blockIdx.x * TB + threadIdx.x;
+    if (i < *src_count) dst[*dst_count + i] = src[i] + off;
+}
+__global__ void k_add_count(int32_t* dst_count, const int32_t* src_count) {
+    if (threadIdx.x == 0) dst_count[0] += src_count[0];
+}
+
+hipError_t launch_frames_restir(const DevScene& S, const DevPaths& PF, const MptFrame* d_frames, const MptFrame* hf,
+                                int batch, LaunchCfg& cfg, hipStream_t st) {
+    const int n = PF.n_pix;
+    if (n == 0 || batch <= 0) return hipSuccess;
+    const int nb = hf[0].render_settings.nb_bounces;
+    hipMemsetAsync(&PF.counters[CTR_QG], 0, sizeof(int32_t), st);
+    for (int s = 0; s < batch; s++) {
+        // sample s over its own slots [s * n, (s + 1) * n): frame_begin, camera rays, bounce 0
+        // with the ReSTIR DI passes (which read sample s - 1's reservoirs and G-buffer)
+        DevPaths P = PF;
+        offset_slots(P, (size_t)s * n);
+        P.n = n; P.batch = 1; P.group = 1;
+        hipLaunchKernelGGL(k_restir_frame_begin, dim3(blocks_for(P.rs_hi - P.rs_lo)), dim3(TB), 0, st, P, d_frames + s);
+        P.rs_out = restir_buffer(P, cfg.restir_out_sp2);
+        hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(&P.counters[CTR_Q0]), n, 1, st);
+        {
+            TimedScope ts(cfg, st, KT_CAMERA);
+            hipLaunchKernelGGL(k_camera, dim3(blocks_for(n)), dim3(TB), 0, st, P, d_frames + s);
+        }
+        frame_bounces(S, P, d_frames + s, hf[s], cfg, st, 0, 0, P.q0, CTR_Q0, P.q1, CTR_Q1);
+        if (nb > 0) {
+            // the global queue's first entries never reach the next sample's slots: after
+            // sample s it holds at most (s + 1) * n entries
+            hipLaunchKernelGGL(k_append_queue, dim3(blocks_for(n)), dim3(TB), 0, st, PF.q0, &PF.counters[CTR_QG], P.q1,
+                               &PF.counters[CTR_Q1], (int32_t)((size_t)s * n));
+            hipLaunchKernelGGL(k_add_count, dim3(1), dim3(64), 0, st, &PF.counters[CTR_QG], &PF.counters[CTR_Q1]);
+        }
+    }
+    // bounces 1..nb of every sample as one wavefront (slot = sample * n + pixel: group = n)
+    DevPaths G = PF;
+    G.group = n;
+    if (nb > 0) frame_bounces(S, G, d_frames, hf[0], cfg, st, 1, nb, G.q0, CTR_QG, G.q1, CTR_Q1);
+    {
+        TimedScope ts(cfg, st, KT_ACCUMULATE);
+        hipLaunchKernelGGL(k_accumulate, dim3(blocks_for(n)), dim3(TB), 0, st, G, d_frames);
+    }
     return hipGetLastError();
 }
 

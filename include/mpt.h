@@ -528,9 +528,12 @@ int mpt_render_frame(MptContext* ctx, const MptFrame* frame);
  * GPURenderer.cpp:424-449): frames[k] is the frame of the k-th sample, each with its own
  * sample_number / seeds.  Runs of frames that differ only in sample_number, random_seed,
  * camera_random_seed, denoiser_AOV_accumulation_counter, need_to_reset and
- * do_update_status_buffers, and need no per-sample feedback (no adaptive sampling or
- * stop-noise threshold, not ReSTIR DI), are traced as ONE wavefront of up to max_batch
- * (<= MPT_MAX_BATCH; <= 0: see MPT_DEFAULT_WAVEFRONT_PATHS) samples per pixel; the result is bit-identical
+ * do_update_status_buffers (and, for ReSTIR DI, restir_di_seeds, the permutation bits and
+ * temporal_buffer_clear_requested), and need no per-sample feedback (no adaptive sampling or
+ * stop-noise threshold), are traced as ONE wavefront of up to max_batch
+ * (<= MPT_MAX_BATCH; <= 0: see MPT_DEFAULT_WAVEFRONT_PATHS) samples per pixel -- ReSTIR DI
+ * samples (at most 32, not across a partition) run their camera rays, reuse passes and
+ * first bounce one after the other and share the later bounces; the result is bit-identical
  * to count mpt_render_frame calls (samples are added to the sums in order).  Other frames
  * are rendered one by one.  Asynchronous. */
 #define MPT_MAX_BATCH 128

@@ -207,6 +207,40 @@ def test_gpu_restir_bit_exact(cornell, luts, case):
     r.close()
 
 
+BATCH_CASES = ["principled", "lambert", "three_passes", "permutation_sampling", "adaptive", "unfused",
+               "unfused_temporal_only", "bias_gbh", "fused_mis_like_moving", "later_bounces_mis",
+               "initial_target_visibility", "no_presampling", "two_bsdf_candidates", "seven_neighbours"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("max_batch", [2, 7])
+@pytest.mark.parametrize("case", BATCH_CASES + ["zero_bounces", "alpha_cards"])
+def test_gpu_restir_batched_bit_exact(cornell, luts, case, max_batch):
+    """mpt_render_frames over ReSTIR DI frames: each sample's camera rays, reuse passes and
+    first bounce in turn, the later bounces of the batch as one wavefront (slot = sample *
+    pixels + pixel) -- equal to the oracle's sample-by-sample render; adaptive sampling and
+    the moved camera (a frame that differs) fall back to smaller runs."""
+    import mpt
+    from oracle import oracle as orc
+    sd = synthetic.with_alpha_cards(cornell) if case == "alpha_cards" else cornell
+    kw = dict(bounces=0) if case == "zero_bounces" else dict(alpha=True) if case == "alpha_cards" else CASES[case]
+    frs = frames(sd, abi.LSS_RESTIR_DI, 7, **kw)
+    r = mpt.GPURenderer(0)
+    r.set_scene(sd)
+    r.set_luts(luts)
+    r.render_samples(frs, max_batch=max_batch)
+    r.synchronize_kernel()
+    o = orc.Oracle(sd, luts)
+    c, ca, cn = o.render(frs, aov=True)
+    g = r.framebuffer(abi.FB_COLOR)
+    assert np.array_equal(g, c), f"{case}: {(g != c).sum()} values differ"
+    assert np.array_equal(r.framebuffer(abi.FB_ALBEDO), ca)
+    assert np.array_equal(r.framebuffer(abi.FB_NORMALS), cn)
+    assert np.isfinite(g).all() and g.mean() > 0
+    o.close()
+    r.close()
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("case", ["envmap", "envmap_only", "alpha_cards", "alpha_cards_unfused", "envmap_unfused",
                                   "alpha_cards_gbh", "envmap_mis_like", "envmap_no_presampling", "envmap_only_no_presampling"])
