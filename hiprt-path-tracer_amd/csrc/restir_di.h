@@ -42,6 +42,17 @@ DEV RSurf gb_surface(const DevScene& S, const DevPaths& P, int i, bool prev) {
     return s;
 }
 
+// XCD-aware block order for the passes that read neighbouring pixels: the hardware hands
+// block b to XCD b % 8, so logical block (b % 8) * (G / 8) + b / 8 gives each XCD one
+// contiguous run of rows, whose neighbours then stay in that XCD's L2 (the G % 8 tail
+// blocks keep their index).  Measured on C4: k_rsp_select 0.78 -> 0.65 ms, k_rsp_combine
+// 0.32 -> 0.27 ms; the evaluation kernels keep the append order (per-XCD item lists, tried
+// with work stealing, were slower: the image regions differ in work).
+DEV int xcd_block() {
+    const int G = (int)gridDim.x, b = (int)blockIdx.x, per = G >> 3;
+    return b < (per << 3) ? (b & 7) * per + (b >> 3) : b;
+}
+
 // ---- traced rays of a pass --------------------------------------------------------------
 // Alpha keys (alpha_key: pass pixel seed, bounce 0, kind 5 + pass, position): the position
 // names the ray's site in the pass, not its rank among the rays traced so far, so a key does
@@ -1358,7 +1369,7 @@ __global__ __launch_bounds__(TB) void k_rsp_select(DevScene S, DevPaths P, const
     const MptFrame& F = *Fp;
     const int W = F.res_x;
     const uint32_t pass_rs = F.restir_di_seeds[4 + pass];
-    const int s = blockIdx.x * TB + threadIdx.x;
+    const int s = xcd_block() * TB + threadIdx.x;
     uint32_t m_plain = 0u, m_gen = 0u, vis_bits = 0u;   // items by position (2k + which)
     if (s < P.n) {
         const int center = s + P.pix_off;
@@ -1479,7 +1490,7 @@ RESTIR_KERNEL void k_rsp_combine(DevScene S, DevPaths P, const MptFrame* __restr
     const MptFrame& F = *Fp;
     const uint32_t pass_rs = F.restir_di_seeds[4 + pass];
     const bool alpha = F.render_settings.do_alpha_testing;
-    const int s = blockIdx.x * TB + threadIdx.x;
+    const int s = xcd_block() * TB + threadIdx.x;
     uint32_t vmask = 0u, n_any = 0u;
     if (s < P.n && !(P.rq_meta[s].x & RSM_SKIP)) {
         const int4 meta = P.rq_meta[s];
@@ -1583,7 +1594,7 @@ __global__ __launch_bounds__(TB) void k_rst_select(DevScene S, DevPaths P, const
     __shared__ int base;
     const MptFrame& F = *Fp;
     float4* tin = P.rs_tin;
-    const int s = blockIdx.x * TB + threadIdx.x;
+    const int s = xcd_block() * TB + threadIdx.x;
     uint32_t m_plain = 0u, m_gen = 0u, vis_bits = 0u, prev_bits = 0u;
     if (s < P.n) {
         const int center = s + P.pix_off;
@@ -1679,7 +1690,7 @@ RESTIR_KERNEL void k_rst_combine(DevScene S, DevPaths P, const MptFrame* __restr
     const MptFrame& F = *Fp;
     const bool alpha = F.render_settings.do_alpha_testing;
     float4* tin = P.rs_tin;
-    const int s = blockIdx.x * TB + threadIdx.x;
+    const int s = xcd_block() * TB + threadIdx.x;
     uint32_t vmask = 0u, n_any = 0u;
     if (s < P.n && !(P.rq_meta[s].x & RSM_SKIP)) {
         const int4 meta = P.rq_meta[s];
