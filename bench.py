@@ -397,14 +397,19 @@ def main():
                   "total_ms": st.shade_ms, "avg_launch_ms": s_avg, "bytes_per_unit": b_vtx, "unit_of_work": "path vertex (hit)",
                   "units_per_launch": hits / sl,
                   "achieved": hits * b_vtx / sl / (s_avg * 1e-3) / 1e9 if s_avg > 0 else 0.0})
-    # ReSTIR DI kernels (C4): per pixel of the band, the G-buffer / reservoir / presampled-light
-    # bytes each one reads and writes; their visibility rays are traced inline
+    # ReSTIR DI passes (C4), timed as a whole (HIP events around each pass): per pixel of the
+    # band, the G-buffer / reservoir / presampled-light bytes the pass reads and writes
+    # (DESIGN.md §4).  With the reference-default weights a pass is staged (restir_di.h:
+    # selection, class-sorted evaluations, its rays through k_trace<TM_LIST_*>, combine,
+    # visibility reuse), else one monolithic kernel tracing inline
     rk = [("k_gbuffer (CameraRays G-buffer write)", "void mpt::k_gbuffer(", 64 + 176),
           ("k_restir_presample (lights presampling)", "void mpt::k_restir_presample(", 0),
-          ("k_restir_initial (initial candidates)", "void mpt::k_restir_initial<", 112 + 4 * 64 + 48),
-          ("k_restir_spatiotemporal / k_restir_temporal (temporal reuse)", "void mpt::k_restir_spatiotemporal<",
-           112 + 160 + 2 * 160 + 48 + 48),
-          ("k_restir_spatial (spatial reuse pass)", "void mpt::k_restir_spatial<", 112 + 48 + 2 * 160 + 48)]
+          ("ReSTIR DI initial candidates pass (k_rsi_classify, k_restir_initial<STAGED>, k_trace<LIST_CLOSEST>, "
+           "k_rsi_finish, k_trace<LIST_ANY>, k_rs_visapply)", "void mpt::k_restir_initial<", 112 + 4 * 64 + 48),
+          ("ReSTIR DI fused spatiotemporal pass (k_rst_select, k_rsp_eval<FUSED>, k_trace<LIST_ANY>, k_rst_combine, "
+           "k_rs_visapply)", "void mpt::k_rst_", 112 + 160 + 2 * 160 + 48 + 48),
+          ("ReSTIR DI spatial reuse pass (k_rsp_select, k_rsp_eval, k_trace<LIST_ANY>, k_rsp_combine, k_rs_visapply)",
+           "void mpt::k_rsp_", 112 + 48 + 2 * 160 + 48)]
     n_pix = rows_rank * W
     for k, (name, sym, bpp) in enumerate(rk):
         ms, nl = st.restir_kernel_ms[k], st.restir_kernel_launches[k]

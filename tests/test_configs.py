@@ -124,7 +124,7 @@ def test_c4_city_restir_full_frame_bit_exact(city, luts, city_oracle, fused):
     o, env = city_oracle
     frs = c4_frames(city, 3, fused=fused, passes=2 if fused else 1)
     r = _gpu(city, luts, env)
-    r.render_samples(frs)            # the bench's entry point (ReSTIR frames run one by one)
+    r.render_samples(frs)            # the bench's entry point (batched: per-sample bounce 0, shared later bounces)
     r.synchronize_kernel()
     got = r.framebuffer(abi.FB_COLOR)
     r.close()
@@ -181,3 +181,23 @@ def test_c4_restir_staged_equals_monolithic(city, luts, city_oracle, fused, monk
         r.close()
     _same(out["staged"], out["monolithic"], "C4 staged vs monolithic")
     assert out["staged_rays"] == out["monolithic_rays"], (out["staged_rays"], out["monolithic_rays"])
+
+
+@pytest.mark.gpu
+def test_c4_restir_batched_equals_unbatched(city, luts, city_oracle, monkeypatch):
+    """Batched ReSTIR DI samples (launch_frames_restir) against one wavefront per sample
+    (MPT_RESTIR_BATCH=0) on the C4 city frame: the same sums and the same ray counts."""
+    _, env = city_oracle
+    frs = c4_frames(city, 4)
+    out = {}
+    for mode in ("unbatched", "batched"):
+        monkeypatch.setenv("MPT_RESTIR_BATCH", "0" if mode == "unbatched" else "1")
+        r = _gpu(city, luts, env)
+        r.render_samples(frs)
+        r.synchronize_kernel()
+        out[mode] = r.framebuffer(abi.FB_COLOR)
+        st = r.stats()
+        out[mode + "_rays"] = (st.rays_any, st.rays_closest)
+        r.close()
+    _same(out["batched"], out["unbatched"], "C4 batched vs unbatched")
+    assert out["batched_rays"] == out["unbatched_rays"], (out["batched_rays"], out["unbatched_rays"])
