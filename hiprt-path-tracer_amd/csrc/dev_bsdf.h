@@ -512,19 +512,27 @@ DEV float thin_walled_roughness(bool thin, float r, float eta) {
     float rem = r * sqrtf(3.7f * (eta - 1.0f) * sq(eta - 0.5f) / pow3(eta));
     return clampr(0.0f, 1.0f, rem / 1.39f);
 }
-// FULL = false: the material is of the plain-dielectric class (MC_PLAIN below: no coat,
-// sheen, metal, transmission or thin film), so the lobes and terms that are exactly zero for
-// it are not compiled in.  Same result as FULL = true for such a material, bit for bit.
-template <bool FULL = true>
+// Material classes of the BSDF code (template parameter FULL): BC_FULL (1) the whole
+// Principled BSDF; BC_PLAIN (0) a plain dielectric (no coat, sheen, metal, transmission or
+// thin film: MT_FULL clear, see k_resolve_materials) and BC_GLASS (2) a dielectric that may
+// transmit but has no coat, sheen, metal or thin film (MT_GLASS): the lobes and terms that are
+// exactly zero for the class are not compiled in.  Same result as BC_FULL for a material of
+// the class, bit for bit (the glass class keeps the coat block, which a refracting direction
+// enters whatever the coat weight).
+enum : int { BC_PLAIN = 0, BC_FULL = 1, BC_GLASS = 2 };
+DEV constexpr bool bc_extra(int cls) { return cls == BC_FULL; }    // sheen, metal, thin film, coat / sheen sampling
+DEV constexpr bool bc_layers(int cls) { return cls != BC_PLAIN; }  // coat evaluation, glass lobe
+template <int FULL = BC_FULL>
 DEV Col spec_fresnel(const Mat& m, float rel, float ci) {
     float above = m.ior / rel;
     Col Fs = col(0.0f), Ft = col(0.0f);
     if (m.thin_film < 1.0f) Fs = col(fresnel_dielectric(ci, rel));
-    if (FULL && m.thin_film > 0.0f) Ft = thin_film_fresnel(m, above, ci);
+    if (bc_extra(FULL) && m.thin_film > 0.0f) Ft = thin_film_fresnel(m, above, ci);
     return lerpc(Fs, Ft, m.thin_film);
 }
 DEV float ior_or_air(const BCtx& c, int idx) { return idx == MAX_MAT ? 1.0f : c.mats[idx].ior; }
 
+template <int FULL = BC_FULL>
 DEV Col glass_eval(const BCtx& c, const Mat& m, VState& vs, v3 V, v3 L, float& pdf) {
     pdf = 0.0f;
     float NoV = V.z, NoL = L.z;
@@ -544,7 +552,7 @@ DEV Col glass_eval(const BCtx& c, const Mat& m, VState& vs, v3 V, v3 L, float& p
     if (HoL * NoL < 0.0f || HoV * NoV < 0.0f) return col(0.0f);
     float comp = dielectric_comp(c, m, vs, et, ei, rel, V.z);
     Col Ft = col(0.0f), Fn = col(0.0f);
-    if (m.thin_film > 0.0f) Ft = thin_film_fresnel(m, ei, HoV);
+    if (bc_extra(FULL) && m.thin_film > 0.0f) Ft = thin_film_fresnel(m, ei, HoV);
     if (m.thin_film < 1.0f) Fn = col(fresnel_dielectric(HoV, rel));
     Col F = lerpc(Fn, Ft, m.thin_film);
     float frp = lum(F);
@@ -580,6 +588,7 @@ DEV Col glass_eval(const BCtx& c, const Mat& m, VState& vs, v3 V, v3 L, float& p
     }
     return out;
 }
+template <int FULL = BC_FULL>
 DEV v3 glass_sample(const BCtx& c, const Mat& m, VState& vs, v3 V, Rng& rng) {
     float ei = dispersion_ior(m.dispersion_abbe_number, m.dispersion_scale, ior_or_air(c, vs.incident), absr(vs.wl));
     float et = dispersion_ior(m.dispersion_abbe_number, m.dispersion_scale, ior_or_air(c, vs.outgoing), absr(vs.wl));
@@ -591,7 +600,7 @@ DEV v3 glass_sample(const BCtx& c, const Mat& m, VState& vs, v3 V, Rng& rng) {
     v3 mn = ggx_vndf(V, ax, ay, rng);
     float HoV = dot(V, mn);
     Col Ft = col(0.0f), Fn = col(0.0f);
-    if (m.thin_film > 0.0f) Ft = thin_film_fresnel(m, ei, HoV);
+    if (bc_extra(FULL) && m.thin_film > 0.0f) Ft = thin_film_fresnel(m, ei, HoV);
     if (m.thin_film < 1.0f) Fn = col(fresnel_dielectric(HoV, rel));
     Col F = lerpc(Fn, Ft, m.thin_film);
     float frp = lum(F);
@@ -657,7 +666,7 @@ struct PEval {
     float gbc, ccc;
 };
 
-template <bool FULL = true>
+template <int FULL = BC_FULL>
 DEV void principled_eval_pre(const BCtx& c, const Mat& m, const VState& vs, v3 view, v3 sn, PEval& e) {
     v3 n = sn;
     e.outside = dot(view, n) > 0 || m.thin_walled;
@@ -673,7 +682,7 @@ DEV void principled_eval_pre(const BCtx& c, const Mat& m, const VState& vs, v3 v
     // coat, view side (entered when the coat has weight or the light refracts, which
     // needs 'outside')
     e.coat_vdf = 0.0f; e.coat_oa = 0.0f; e.coat_dark = col(1.0f);
-    if (FULL && (e.w[0] > 0.0f || e.outside)) {
+    if (bc_layers(FULL) && (e.w[0] > 0.0f || e.outside)) {
         e.coat_vdf = fresnel_dielectric(absr(e.lv.z), e.inc, m.coat_ior);
         if (!is_white(C3(m.coat_medium_absorption)))
             e.coat_oa = maxr(1.0e-6f, sqrtf(1.0f - (1.0f - e.lv.z * e.lv.z) / (m.coat_ior * m.coat_ior)));
@@ -700,7 +709,7 @@ DEV void principled_eval_pre(const BCtx& c, const Mat& m, const VState& vs, v3 v
 // the generic code skips those lobes too, except the coat block on a refracting direction,
 // which then only scales the throughput of lobes that are all skipped (nr = 0, w[6] = 0),
 // and adds cp * p[0] = 0 to the pdf and a zero colour to fc -- no effect on the result.
-template <bool FULL = true>
+template <int FULL = BC_FULL>
 DEV Col principled_eval_post(const BCtx& c, const Mat& m, VState& vs, const PEval& e, v3 sn, v3 L, float& pdf) {
     pdf = 0.0f;
     const bool refracting = dot(sn, L) < 0.0f && e.outside;
@@ -714,7 +723,7 @@ DEV Col principled_eval_post(const BCtx& c, const Mat& m, VState& vs, const PEva
     Col thr = col(1.0f), fc = col(0.0f);
     float nr = refracting ? 0.0f : 1.0f;
     // coat (Principled.h:493-593)
-    if (FULL && (e.w[0] > 0.0f || refracting)) {
+    if (bc_layers(FULL) && (e.w[0] > 0.0f || refracting)) {
         float cp = 0.0f;
         Col ct = col(0.0f);
         if (!refracting) {
@@ -738,7 +747,7 @@ DEV Col principled_eval_post(const BCtx& c, const Mat& m, VState& vs, const PEva
         fc += ct;
     }
     // sheen
-    if (FULL && e.w[1] > 0.0f) {
+    if (bc_extra(FULL) && e.w[1] > 0.0f) {
         float refl, sp;
         Col ct = sheen_eval(c, m, ll, lv, sp, refl);
         ct *= e.w[1];
@@ -751,7 +760,7 @@ DEV Col principled_eval_post(const BCtx& c, const Mat& m, VState& vs, const PEva
 #pragma unroll
     for (int k = 0; k < 2; k++) {
         float wk = e.w[2 + k] * nr;
-        if (FULL && wk > 0.0f) {
+        if (bc_extra(FULL) && wk > 0.0f) {
             float mp;
             float HoL = clampr(1.0e-8f, 1.0f, dot(lhr, llr));
             Col Fm = f82_tint(C3(m.base_color), C3(m.metallic_F82), C3(m.metallic_F90), m.metallic_F90_falloff_exponent, HoL);
@@ -764,9 +773,9 @@ DEV Col principled_eval_post(const BCtx& c, const Mat& m, VState& vs, const PEva
         }
     }
     // glass
-    if (FULL && e.w[6] > 0.0f) {
+    if (bc_layers(FULL) && e.w[6] > 0.0f) {
         float gp;
-        Col ct = glass_eval(c, m, vs, lvr, llr, gp);
+        Col ct = glass_eval<FULL>(c, m, vs, lvr, llr, gp);
         ct *= e.w[6];
         ct *= thr;
         pdf += gp * e.p[6];
@@ -820,7 +829,7 @@ DEV Col principled_eval(const BCtx& c, const Mat& m, VState& vs, v3 view, v3 n, 
 // FULL = false (plain dielectric): p[0] = p[1] = 0, so r1 < c0 and r1 < c1 never hold (r1 >= 0)
 // and the coat / sheen samplers are not compiled in; the glass branch stays (r1 > c5 can
 // hold by rounding when p[6] = 0).
-template <bool FULL = true>
+template <int FULL = BC_FULL>
 DEV bool principled_sample_dir(const BCtx& c, const Mat& m, VState& vs, v3 view, v3 sn, v3 gn, v3& out, Rng& rng) {
     v3 n = sn;
     bool outside = dot(view, n) > 0 || m.thin_walled;
@@ -842,11 +851,11 @@ DEV bool principled_sample_dir(const BCtx& c, const Mat& m, VState& vs, v3 view,
     v3 TR, BR;
     build_rotated_onb(n, TR, BR, m.anisotropy_rotation * PI);
     v3 lvr = to_local(TR, BR, n, view);
-    if (FULL && r1 < c0) {
+    if (bc_extra(FULL) && r1 < c0) {
         v3 TC, BC;
         build_rotated_onb(n, TC, BC, m.coat_anisotropy_rotation * PI);
         out = to_world(TC, BC, n, ggx_sample_reflection(m.coat_roughness, m.coat_anisotropy, to_local(TC, BC, n, view), rng));
-    } else if (FULL && r1 < c1) {
+    } else if (bc_extra(FULL) && r1 < c1) {
         v3 T, B;
         build_onb(n, T, B);
         out = to_world(T, B, n, sheen_sample(c, m, to_local(T, B, n, view), rng));
@@ -857,7 +866,7 @@ DEV bool principled_sample_dir(const BCtx& c, const Mat& m, VState& vs, v3 view,
     } else if (r1 < c5) {
         out = cosine_sample_around(n, rng);
     } else {
-        out = to_world(TR, BR, n, glass_sample(c, m, vs, lvr, rng));
+        out = to_world(TR, BR, n, glass_sample<FULL>(c, m, vs, lvr, rng));
     }
     return !(dot(out, sn) < 0 && !glass);
 }
@@ -884,21 +893,21 @@ DEV Col bsdf_eval(const BCtx& c, const Mat& m, VState& vs, v3 view, v3 sn, v3 L,
     return principled_eval(c, m, vs, view, sn, L, pdf);
 }
 // evaluation split into a per-vertex part and a per-light-direction part (see PEval)
-template <int OVERRIDE, bool FULL = true>
+template <int OVERRIDE, int FULL = BC_FULL>
 DEV void bsdf_eval_pre(const BCtx& c, const Mat& m, const VState& vs, v3 view, v3 sn, PEval& e) {
     if (OVERRIDE == MPT_BSDF_OREN_NAYAR) {
         build_onb(sn, e.T, e.B);
         e.lv = to_local(e.T, e.B, sn, view);
     } else if (OVERRIDE != MPT_BSDF_LAMBERTIAN) principled_eval_pre<FULL>(c, m, vs, view, sn, e);
 }
-template <int OVERRIDE, bool FULL = true>
+template <int OVERRIDE, int FULL = BC_FULL>
 DEV Col bsdf_eval_post(const BCtx& c, const Mat& m, VState& vs, const PEval& e, v3 sn, v3 L, float& pdf) {
     if (OVERRIDE == MPT_BSDF_LAMBERTIAN) return lambert_eval(m, dot(L, sn), pdf);
     if (OVERRIDE == MPT_BSDF_OREN_NAYAR) return oren_nayar_eval(m, e.lv, to_local(e.T, e.B, sn, L), pdf);
     return principled_eval_post<FULL>(c, m, vs, e, sn, L, pdf);
 }
 // sample = sample_dir + bsdf_eval on the updated state (eval skipped when sample_dir is false)
-template <int OVERRIDE, bool FULL = true>
+template <int OVERRIDE, int FULL = BC_FULL>
 DEV bool bsdf_sample_dir(const BCtx& c, const Mat& m, VState& vs, v3 view, v3 sn, v3 gn, v3& dir, Rng& rng) {
     if (OVERRIDE == MPT_BSDF_LAMBERTIAN || OVERRIDE == MPT_BSDF_OREN_NAYAR) { dir = cosine_sample_around(sn, rng); return true; }
     return principled_sample_dir<FULL>(c, m, vs, view, sn, gn, dir, rng);

@@ -132,6 +132,7 @@ struct MptContext {
     int shade_classes = 1;
     int restir_staged = 1;                // ReSTIR DI reuse passes staged around their rays (MPT_RESTIR_STAGED)
     int restir_batch = 1;                 // ReSTIR DI samples batched after bounce 0 (MPT_RESTIR_BATCH)
+    int shade_glass = 1;                  // glass-class shading kernel (MPT_SHADE_GLASS)
     std::vector<MptMaterial> h_mats;
     std::vector<int32_t> h_mat_idx;       // per triangle (alpha flags of the triangle records)
     std::vector<uint8_t> h_tex_alpha;     // per texture: some texel has alpha < 255
@@ -794,6 +795,7 @@ int mpt_create(int device, void* hip_stream, MptContext** out) {
     if (const char* e = std::getenv("MPT_SHADE_CLASSES")) c->shade_classes = std::atoi(e);
     if (const char* e = std::getenv("MPT_RESTIR_STAGED")) c->restir_staged = std::atoi(e);
     if (const char* e = std::getenv("MPT_RESTIR_BATCH")) c->restir_batch = std::atoi(e);
+    if (const char* e = std::getenv("MPT_SHADE_GLASS")) c->shade_glass = std::atoi(e);
     if (const char* e = std::getenv("MPT_LIGHT_BVH")) c->light_bvh = std::atoi(e);
     if (const char* e = std::getenv("MPT_OVERLAP")) c->overlap = std::atoi(e);
     if (const char* e = std::getenv("MPT_LIGHT_BVH_MAX_STACK")) c->light_bvh_max_stack = std::atoi(e);
@@ -1152,6 +1154,7 @@ static int launch_batch(MptContext* c, const MptFrame* f, int batch) {
     cfg.restir_out_sp2 = c->restir_out_sp2;
     cfg.shade_classes = c->shade_classes;
     cfg.restir_staged = c->restir_staged;
+    cfg.shade_glass = c->shade_glass;
     cfg.light_bvh = c->light_bvh && c->light_bvh_ok;
     cfg.light_static = !c->h_light_prims.empty() && 2 * c->bvh_light.depth + 2 <= TRAV_LDS_STACK;
     if (restir_part) {

@@ -221,7 +221,7 @@ enum { KT_CAMERA = 3, KT_SHADE = 4, KT_RESOLVE = 5, KT_ACCUMULATE = 6, KT_COMPAC
 constexpr uint32_t QM_CONT = 16u;
 // mat_tex bits: a texture feeds the resolved material; the material is outside the
 // plain-dielectric class (coat, sheen, metallic, transmission or thin film may be non-zero)
-constexpr int32_t MT_TEXTURED = 1, MT_FULL = 2;
+constexpr int32_t MT_TEXTURED = 1, MT_FULL = 2, MT_GLASS = 4;   // MT_GLASS: k_resolve_materials
 constexpr int STATS_STRIDE = 6;   // per mode: traversals, nodes, tris, (unused), node slots, tri slots
 constexpr int N_STATS = N_TRACE_MODES * STATS_STRIDE;
 
@@ -236,6 +236,7 @@ enum {
     CTR_RQ = 14, CTR_RQV = 15,                      // staged ReSTIR DI rays / visibility-reuse rays
     CTR_RQE0 = 16, CTR_RQE1 = 17,                   // staged ReSTIR DI target evaluations: plain / generic class
     CTR_QG = 18,                                    // batched ReSTIR DI: the later bounces' path queue
+    CTR_GLASS = 19,                                 // length of the glass-class list (top of qf, k_split)
     CTR_COUNT = 20
 };
 
@@ -261,6 +262,7 @@ struct LaunchCfg {
     int light_bvh;            // light-hit queries through the light BVH (1) or one closest-hit traversal (0)
     int light_static;         // the light BVH's traversal stack fits in LDS (one query per lane, no spill)
     int restir_staged;        // ReSTIR DI reuse passes staged around their rays (restir_di.h), when supported
+    int shade_glass;          // k_split's glass class (MPT_SHADE_GLASS)
     // overlapped batch halves (mpt_api.cpp launch_batch): recorded after the bounce-0 path
     // traversal / after k_accumulate; waited for before k_accumulate (all optional)
     hipEvent_t ev_first_trace;

@@ -1048,7 +1048,7 @@ DEV void x_rec(const DevPaths& P, size_t e, float4 a, float4 b) {
 }
 // a BSDF-sampled light-hit candidate: sample (draws), evaluate, stage the light-hit ray;
 // origin as sample_one_light_bsdf / _MIS / the RIS BSDF candidates pick it
-template <int OVR, bool FULL>
+template <int OVR, int FULL>
 DEV float x_bsdf_cand(const DevPaths& P, const BCtx& bc, const Mat& m, const VState& vs, const PEval& pe, size_t e, int prim,
                       v3 ip, v3 sn, v3 gn, v3 view, float ism, v3 o_refl, bool abs_cos, float r_add_slot, Rng& rng, uint8_t& fl) {
     VState tv = vs;
@@ -1066,7 +1066,7 @@ DEV float x_bsdf_cand(const DevPaths& P, const BCtx& bc, const Mat& m, const VSt
     }
     return pdf;
 }
-template <int OVR, bool FULL>
+template <int OVR, int FULL>
 DEV void ext_light(const DevScene& S, const DevPaths& P, const MptFrame& F, const BCtx& bc, const Mat& m, const VState& vs,
                    const PEval& pe, int slot, int prim, v3 ip, v3 sn, v3 gn, v3 view, float ism, v3 ep, int lssb, Rng& rng) {
     const MptRenderSettings& rs = F.render_settings;
@@ -1279,6 +1279,7 @@ struct ShadeArgs {
     int32_t* q_defer;          // PLAIN: vertices handed to the generic kernel (seen from inside)
     int32_t* count_defer;
     int force_defer;           // test hook (MPT_SHADE_CLASSES=2): defer every plain vertex
+    int rev;                   // the list grows downward from q_cur (the glass class, stored at the top of qf)
 };
 
 #ifndef MPT_SHADE_WAVES
@@ -1294,16 +1295,21 @@ struct ShadeArgs {
 #ifndef MPT_SHADE_WAVES_PLAIN
 #define MPT_SHADE_WAVES_PLAIN MPT_SHADE_WAVES
 #endif
-template <int OVR, bool PLAIN, bool EXT = false>
+template <int OVR, bool PLAIN, bool EXT = false, bool GLASS = false>
 __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_SHADE_WAVES_PLAIN : MPT_SHADE_WAVES))) void k_shade(ShadeArgs A) {
+    constexpr int CLS = PLAIN ? BC_PLAIN : (GLASS ? BC_GLASS : BC_FULL);   // the BSDF code's class (dev_bsdf.h)
     const DevScene& S = A.S;
     const DevPaths& P = A.P;
     const MptFrame& F = *A.F;
     const MptRenderSettings& rs = F.render_settings;
     const int bounce = A.bounce;
+    // the grid covers the whole wavefront, a class list is often much shorter: blocks past its
+    // end leave at once (an empty 4K x 4-sample launch otherwise costs ~0.2 ms)
+    const int count = *A.count_cur;
+    if ((int)(blockIdx.x * TB) >= count) return;
     int i = blockIdx.x * TB + threadIdx.x;
-    bool valid = i < *A.count_cur;
-    int slot = valid ? A.q_cur[i] : 0;
+    bool valid = i < count;
+    int slot = valid ? (A.rev ? A.q_cur[-1 - i] : A.q_cur[i]) : 0;
 
     BCtx bc;
     bc.mats = S.mats;
@@ -1438,11 +1444,11 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_
             __shared__ PEval pe_lds[TB];
             PEval& pe = pe_lds[threadIdx.x];
             SECT(0);
-            bsdf_eval_pre<OVR, !PLAIN>(bc, m, vs, view, sn, pe);
+            bsdf_eval_pre<OVR, CLS>(bc, m, vs, view, sn, pe);
             SECT(5);
             if (EXT && do_light && !(restir && bounce == 0)) {
                 // extended light sampling: every light sample's draws, records and queries
-                ext_light<OVR, !PLAIN>(S, P, F, bc, m, vs, pe, slot, prim, ip, sn, gn, view, ism, ep, lssb, rng);
+                ext_light<OVR, CLS>(S, P, F, bc, m, vs, pe, slot, prim, ip, sn, gn, view, ism, ep, lssb, rng);
                 fl |= NF_EXT;
                 op = do_env ? OP_ENV_LIGHT : (do_cont ? OP_CONT : OP_DONE);
             }
@@ -1464,7 +1470,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_
                 Col ec = col(0.0f);
                 bool inner = false;
                 if (op == OP_RIS_BSDF || op == OP_MIS_BSDF || op == OP_BSDF_LIGHT || op == OP_ENV_BSDF || op == OP_CONT) {
-                    do_eval = bsdf_sample_dir<OVR, !PLAIN>(bc, m, tv, view, sn, gn, L, rng);
+                    do_eval = bsdf_sample_dir<OVR, CLS>(bc, m, tv, view, sn, gn, L, rng);
                 } else if (op == OP_RIS_LIGHT) {
                     lp = sample_emissive_triangle(S, rng, lpdf, li);
                     if (lpdf > 0.0f) {
@@ -1527,7 +1533,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_
                 float pdf = 0.0f;
                 Col f = col(0.0f);
                 SECT(1);
-                if (do_eval) f = bsdf_eval_post<OVR, !PLAIN>(bc, m, tv, pe, sn, L, pdf);
+                if (do_eval) f = bsdf_eval_post<OVR, CLS>(bc, m, tv, pe, sn, L, pdf);
                 SECT(2);
                 int next = OP_DONE;
                 if (op == OP_RIS_LIGHT) {
@@ -1794,54 +1800,67 @@ DEV int load_items(const int32_t* q, int b0, int count, int slots[CP_ITEMS]) {
 // k_resolve) and those that left the scene (k_miss), so that every lane of a shading wave
 // has a vertex to shade instead of idling through the light-sampling loop beside a miss.
 // With `classes`, the hits are further sorted by material class (see k_shade): plain
-// dielectrics into qh (CTR_HIT), every other material into qf (CTR_FULL).
+// dielectrics into qh (CTR_HIT), every other material into qf (CTR_FULL) -- with classes = 2
+// the glass class (MT_GLASS) into the top of qf, growing downward (CTR_GLASS).
 #ifndef MPT_TU_PART   // k_split
 __global__ __launch_bounds__(CP_NT) void k_split(DevScene S, DevPaths P, const int32_t* q, const int32_t* count_q,
                                                  int classes) {
     __shared__ int tmp[CP_NT / 64 + 1];
-    __shared__ int base[3];
+    __shared__ int base[4];
     const int count = *count_q;
     const int b0 = blockIdx.x * CP_NT * CP_ITEMS;
     if (b0 >= count) return;
     int slots[CP_ITEMS];
     const int n = load_items(q, b0, count, slots);
-    uint32_t hm = 0u, fm = 0u;
-    int nh = 0, nf = 0;
+    uint32_t hm = 0u, fm = 0u, gm = 0u;
+    int nh = 0, nf = 0, ng = 0;
 #pragma unroll
     for (int j = 0; j < CP_ITEMS; j++) {
         const int prim = j < n ? __float_as_int(P.hit[slots[j]].w) : -1;
         if (prim >= 0) {
-            if (classes && (S.mat_tex[S.mat_idx[prim]] & MT_FULL)) { fm |= 1u << j; nf++; }
+            const int32_t mt = classes ? S.mat_tex[S.mat_idx[prim]] : 0;
+            if (classes == 2 && (mt & MT_GLASS)) { gm |= 1u << j; ng++; }
+            else if (mt & MT_FULL) { fm |= 1u << j; nf++; }
             else { hm |= 1u << j; nh++; }
         }
     }
-    int th, tm, tf;
+    int th, tm, tf, tg;
     int oh = block_scan_excl(nh, tmp, th);
-    int om = block_scan_excl(n - nh - nf, tmp, tm);
+    int om = block_scan_excl(n - nh - nf - ng, tmp, tm);
     int of = block_scan_excl(nf, tmp, tf);
+    int og = classes == 2 ? block_scan_excl(ng, tmp, tg) : (tg = 0);
     if (threadIdx.x == 0) {
         base[0] = th ? atomicAdd(&P.counters[CTR_HIT], th) : 0;
         base[1] = tm ? atomicAdd(&P.counters[CTR_MISS], tm) : 0;
         base[2] = tf ? atomicAdd(&P.counters[CTR_FULL], tf) : 0;
+        base[3] = tg ? atomicAdd(&P.counters[CTR_GLASS], tg) : 0;
     }
     __syncthreads();
     oh += base[0];
     om += base[1];
     of += base[2];
+    og += base[3];
+    int32_t* const qg = P.qf + P.n - 1;   // the glass list: qg[-k]
 #pragma unroll
     for (int j = 0; j < CP_ITEMS; j++) {
         if (j >= n) break;
         if ((hm >> j) & 1u) P.qh[oh++] = slots[j];
         else if ((fm >> j) & 1u) P.qf[of++] = slots[j];
+        else if ((gm >> j) & 1u) qg[-(og++)] = slots[j];
         else P.qm[om++] = slots[j];
     }
 }
 
 #endif
-// The bounce's shaded vertices: qh[0, CTR_HIT) followed by qf[0, CTR_FULL); entries that
-// k_shade<PLAIN> deferred to qf are -1 in qh.
-DEV int shaded_count(const DevPaths& P) { return P.counters[CTR_HIT] + P.counters[CTR_FULL]; }
-DEV int shaded_entry(const DevPaths& P, int nh, int i) { return i < nh ? P.qh[i] : P.qf[i - nh]; }
+// The bounce's shaded vertices: qh[0, CTR_HIT), then qf[0, CTR_FULL), then the glass list
+// at the top of qf (qf[n - 1 - k], k < CTR_GLASS); entries that k_shade<PLAIN> deferred to qf
+// are -1 in qh.
+DEV int shaded_count(const DevPaths& P) { return P.counters[CTR_HIT] + P.counters[CTR_FULL] + P.counters[CTR_GLASS]; }
+DEV int shaded_entry(const DevPaths& P, int nh, int i) {
+    if (i < nh) return P.qh[i];
+    const int nf = P.counters[CTR_FULL];
+    return i - nh < nf ? P.qf[i - nh] : P.qf[P.n - 1 - (i - nh - nf)];
+}
 
 // k_compact: next path queue + NEE query lists from the per-path masks of the shaded paths
 #ifndef MPT_TU_PART   // k_compact
@@ -1849,7 +1868,7 @@ __global__ __launch_bounds__(CP_NT) void k_compact(DevPaths P, int32_t* q_next, 
     __shared__ int tmp[CP_NT / 64 + 1];
     __shared__ int base[5];
     const int nh = P.counters[CTR_HIT];
-    const int count = nh + P.counters[CTR_FULL];
+    const int count = shaded_count(P);
     const int b0 = blockIdx.x * CP_NT * CP_ITEMS;
     if (b0 >= count) return;
     int slots[CP_ITEMS];
@@ -2046,10 +2065,10 @@ __global__ __launch_bounds__(TB) void k_resolve(DevScene S, DevPaths P, const Mp
         atomicAdd(rc + 1, (unsigned long long)P.counters[CTR_ANY] + (EXT ? (unsigned long long)P.counters[CTR_XANY] : 0ull));
         atomicAdd(rc + 2, (unsigned long long)P.counters[CTR_CL] + (EXT ? (unsigned long long)P.counters[CTR_XCL] : 0ull));
         atomicAdd(rc + 3, (unsigned long long)(shaded_count(P) - P.counters[CTR_DEFER]));
-        atomicAdd(rc + 4, (unsigned long long)P.counters[CTR_FULL]);
+        atomicAdd(rc + 4, (unsigned long long)(P.counters[CTR_FULL] + P.counters[CTR_GLASS]));
     }
     const int nh = P.counters[CTR_HIT];
-    if (i >= nh + P.counters[CTR_FULL]) return;
+    if (i >= shaded_count(P)) return;
     const int slot = shaded_entry(P, nh, i);
     if (slot < 0) return;   // deferred to the generic shading list
     // the NEE record planes the vertex wrote (flags in nthr.w), each read whole
@@ -2207,6 +2226,7 @@ __global__ __launch_bounds__(TB) void k_accumulate(DevPaths P, const MptFrame* _
 // parallel; these launch them.
 void part_shade_generic(dim3 g, hipStream_t st, const ShadeArgs& a);          // k_shade<NONE, false>
 void part_shade_plain(dim3 g, hipStream_t st, const ShadeArgs& a);            // k_shade<NONE, true>
+void part_shade_glass(dim3 g, hipStream_t st, const ShadeArgs& a);            // k_shade<NONE, false, false, true>
 void part_shade_ext(dim3 g, hipStream_t st, const ShadeArgs& a);              // k_shade<NONE, false, true>
 void part_shade_override(int ovr, bool ext, dim3 g, hipStream_t st, const ShadeArgs& a);   // Lambert, Oren-Nayar
 enum RestirKernel { RK_INITIAL, RK_SPATIOTEMPORAL, RK_SPATIOTEMPORAL_ANY, RK_SPATIAL, RK_SPATIAL_ANY, RK_TEMPORAL, RK_SP_SELECT,
@@ -2486,7 +2506,7 @@ static void frame_bounces(const DevScene& S, DevPaths& P, const MptFrame* d_fram
     // material classes (k_split / k_shade): Principled BSDF only (the Lambert override has one class)
     // extended light sampling (DevPaths::x_per > 0): the EXT shading / resolve kernels, one class
     const bool ext = P.x_per > 0;
-    const int classes = (hf.options.bsdf_override != MPT_BSDF_NONE || ext) ? 0 : (cfg.shade_classes != 0 ? 1 : 0);
+    const int classes = (hf.options.bsdf_override != MPT_BSDF_NONE || ext) ? 0 : (cfg.shade_classes != 0 ? (cfg.shade_glass ? 2 : 1) : 0);
     for (int b = b_first; b <= b_last; b++) {
         // continuation / camera rays
         hipMemsetAsync(&P.counters[CTR_FETCH], 0, sizeof(int32_t), st);
@@ -2506,13 +2526,14 @@ static void frame_bounces(const DevScene& S, DevPaths& P, const MptFrame* d_fram
         hipMemsetAsync(&P.counters[c_next], 0, sizeof(int32_t), st);
         hipMemsetAsync(&P.counters[CTR_ANY], 0, 2 * sizeof(int32_t), st);
         hipMemsetAsync(&P.counters[CTR_HIT], 0, 4 * sizeof(int32_t), st);   // HIT, MISS, FULL, DEFER
+        hipMemsetAsync(&P.counters[CTR_GLASS], 0, sizeof(int32_t), st);
         if (ext) hipMemsetAsync(&P.counters[CTR_XANY], 0, 3 * sizeof(int32_t), st);   // XANY, XCL, XLIGHT
         const dim3 cp_grid((n + CP_NT * CP_ITEMS - 1) / (CP_NT * CP_ITEMS));
         {
             TimedScope ts(cfg, st, KT_SPLIT);
             hipLaunchKernelGGL(k_split, cp_grid, dim3(CP_NT), 0, st, S, P, q_cur, &P.counters[c_cur], classes);
         }
-        ShadeArgs sa;
+        ShadeArgs sa{};
         sa.S = S; sa.P = P; sa.F = d_frame; sa.bounce = b; sa.last_bounce = nb;
         sa.q_cur = P.qh; sa.count_cur = &P.counters[CTR_HIT]; sa.q_defer = P.qf; sa.count_defer = &P.counters[CTR_FULL];
         sa.force_defer = cfg.shade_classes == 2 ? 1 : 0;
@@ -2529,6 +2550,11 @@ static void frame_bounces(const DevScene& S, DevPaths& P, const MptFrame* d_fram
             ShadeArgs sf = sa;
             sf.q_cur = P.qf; sf.count_cur = &P.counters[CTR_FULL]; sf.q_defer = nullptr; sf.count_defer = nullptr;
             part_shade_generic(dim3(blocks_for(n)), st, sf);
+            if (classes == 2) {   // the glass class, at the top of qf
+                ShadeArgs sg2 = sf;
+                sg2.q_cur = P.qf + P.n; sg2.count_cur = &P.counters[CTR_GLASS]; sg2.rev = 1;
+                part_shade_glass(dim3(blocks_for(n)), st, sg2);
+            }
         }
         {
             TimedScope ts(cfg, st, KT_MISS);
@@ -2692,7 +2718,12 @@ __global__ void k_resolve_materials(DevScene S, MptMaterial* out, int32_t* tex, 
                        m.sheen_texture_index == MPT_NO_TEXTURE && m.metallic_texture_index == MPT_NO_TEXTURE &&
                        m.roughness_metallic_texture_index == MPT_NO_TEXTURE &&
                        m.specular_transmission_texture_index == MPT_NO_TEXTURE;
-    tex[i] = (textured ? MT_TEXTURED : 0) | (plain ? 0 : MT_FULL);
+    // glass class (k_shade<GLASS>): as plain, but transmission allowed (the glass lobe and the
+    // coat block stay compiled in, dev_bsdf.h BC_GLASS)
+    const bool glass = !plain && r.coat == 0.0f && r.sheen == 0.0f && r.metallic == 0.0f && r.thin_film == 0.0f &&
+                       m.coat_texture_index == MPT_NO_TEXTURE && m.sheen_texture_index == MPT_NO_TEXTURE &&
+                       m.metallic_texture_index == MPT_NO_TEXTURE && m.roughness_metallic_texture_index == MPT_NO_TEXTURE;
+    tex[i] = (textured ? MT_TEXTURED : 0) | (plain ? 0 : MT_FULL) | (glass ? MT_GLASS : 0);
 }
 
 

@@ -28,6 +28,9 @@ extern "C" int mpt_debug_sections(unsigned long long* out, int reset) {   // k_s
 void part_shade_ext(dim3 g, hipStream_t st, const ShadeArgs& a) {
     hipLaunchKernelGGL((k_shade<MPT_BSDF_NONE, false, true>), g, dim3(TB), 0, st, a);
 }
+void part_shade_glass(dim3 g, hipStream_t st, const ShadeArgs& a) {
+    hipLaunchKernelGGL((k_shade<MPT_BSDF_NONE, false, false, true>), g, dim3(TB), 0, st, a);
+}
 #elif MPT_TU_PART == 4
 void part_shade_override(int ovr, bool ext, dim3 g, hipStream_t st, const ShadeArgs& a) {
     if (ovr == MPT_BSDF_LAMBERTIAN) {

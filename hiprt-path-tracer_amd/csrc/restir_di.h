@@ -576,7 +576,7 @@ DEV void initial_bsdf_candidate(const DevScene& S, const MptFrame& F, v3 gp, v3 
 // out, dev_bsdf.h FULL = false, bit for bit the generic code's result for it).
 enum : int { RSI_RAY = 2 };   // rq_meta.x: a BSDF-candidate ray was staged
 // bsdf_sample with the class's code: the direction, then the evaluation on the updated state
-template <int OVR, bool FULL>
+template <int OVR, int FULL>
 DEV Col bsdf_sample_cls(const BCtx& bc, const Mat& m, VState& vs, v3 view, v3 sn, v3 gn, v3& dir, float& pdf, Rng& rng) {
     if (FULL) return bsdf_sample<OVR>(bc, m, vs, view, sn, gn, dir, pdf, rng);
     pdf = 0.0f;

@@ -70,3 +70,15 @@ def test_classes_city_band_batched(monkeypatch, luts):
     out = _render_modes(monkeypatch, city, luts, frs, env=env, batch=2)
     _assert_modes_equal(out, oracle_for(city, luts, env).render(frs, aov=True), "city band")
     assert np.isfinite(out[1][0]).all() and out[1][0].mean() > 0
+
+
+@pytest.mark.parametrize("name,strategy,bounces", [("multi-dispersion", "ris", 16), ("nested-dielectrics-complex", "mis", 8),
+                                                   ("cornell_pbr", "ris", 4)])
+def test_glass_class(monkeypatch, luts, name, strategy, bounces):
+    """The glass class (MT_GLASS: transmission without coat / sheen / metal / thin film, shaded
+    by k_shade<GLASS> with dev_bsdf.h BC_GLASS from the top of the generic list) against the
+    generic kernel (MPT_SHADE_GLASS=0) and the oracle, incl. dispersion and nested dielectrics."""
+    sd = scene.load_scene(name)
+    frs = frames(sd, 40, 30, 2, lss=STRATEGIES[strategy], bounces=bounces)
+    out = _render_modes(monkeypatch, sd, luts, frs, var="MPT_SHADE_GLASS", modes=(0, 1))
+    _assert_modes_equal(out, oracle_for(sd, luts).render(frs, aov=True), f"{name} glass class")
