@@ -1730,14 +1730,15 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_
 // ----------------------------------------------------------------------------------
 #ifndef MPT_TU_PART   // k_miss
 __global__ __launch_bounds__(TB) void k_miss(DevScene S, DevPaths P, const MptFrame* __restrict__ Fp, int bounce) {
-    const int i = blockIdx.x * TB + threadIdx.x;
-    if (i >= P.counters[CTR_MISS]) return;
-    const int slot = P.qm[i];
-    const float4 rdv = P.ray_d[slot], t4 = P.thr[slot], cv = P.col[slot];
-    v3 d = mk3(rdv.x, rdv.y, rdv.z);
-    if (bounce == 0) d = normalize(d);
-    const Col rc = col(cv.x, cv.y, cv.z) + miss_radiance(S, *Fp, bounce, d, col(t4.x, t4.y, t4.z));
-    P.col[slot] = make_float4(rc.r, rc.g, rc.b, 0.0f);
+    const int nm = P.counters[CTR_MISS];   // grid-stride, as k_resolve
+    for (int i = blockIdx.x * TB + threadIdx.x; i < nm; i += gridDim.x * TB) {
+        const int slot = P.qm[i];
+        const float4 rdv = P.ray_d[slot], t4 = P.thr[slot], cv = P.col[slot];
+        v3 d = mk3(rdv.x, rdv.y, rdv.z);
+        if (bounce == 0) d = normalize(d);
+        const Col rc = col(cv.x, cv.y, cv.z) + miss_radiance(S, *Fp, bounce, d, col(t4.x, t4.y, t4.z));
+        P.col[slot] = make_float4(rc.r, rc.g, rc.b, 0.0f);
+    }
 }
 
 #endif
@@ -2050,25 +2051,10 @@ DEV Col ext_resolve(const DevScene& S, const DevPaths& P, const MptFrame& F, int
     return dl / (float)rs.number_of_light_samples;
 }
 
-// over the bounce's hit queue (the shaded paths); count_paths: the bounce's path rays
+// one entry of the bounce's shaded list
 template <bool EXT>
-__global__ __launch_bounds__(TB) void k_resolve(DevScene S, DevPaths P, const MptFrame* __restrict__ Fp, int bounce,
-                                                const int32_t* count_paths) {
-    const MptFrame& F = *Fp;
+DEV void resolve_entry(const DevScene& S, const DevPaths& P, const MptFrame& F, int bounce, int nh, int i) {
     const MptRenderSettings& rs = F.render_settings;
-    int i = blockIdx.x * TB + threadIdx.x;
-    if (i == 0) {
-        // always-on ray accounting: path rays + NEE any-hit + NEE closest of this bounce, path hits
-        // (atomic: the two halves of an overlapped batch resolve concurrently)
-        unsigned long long* rc = (unsigned long long*)P.ray_counts;
-        atomicAdd(rc + 0, (unsigned long long)*count_paths);
-        atomicAdd(rc + 1, (unsigned long long)P.counters[CTR_ANY] + (EXT ? (unsigned long long)P.counters[CTR_XANY] : 0ull));
-        atomicAdd(rc + 2, (unsigned long long)P.counters[CTR_CL] + (EXT ? (unsigned long long)P.counters[CTR_XCL] : 0ull));
-        atomicAdd(rc + 3, (unsigned long long)(shaded_count(P) - P.counters[CTR_DEFER]));
-        atomicAdd(rc + 4, (unsigned long long)(P.counters[CTR_FULL] + P.counters[CTR_GLASS]));
-    }
-    const int nh = P.counters[CTR_HIT];
-    if (i >= shaded_count(P)) return;
     const int slot = shaded_entry(P, nh, i);
     if (slot < 0) return;   // deferred to the generic shading list
     // the NEE record planes the vertex wrote (flags in nthr.w), each read whole
@@ -2166,6 +2152,26 @@ __global__ __launch_bounds__(TB) void k_resolve(DevScene S, DevPaths P, const Mp
 #ifdef MPT_DEBUG_SLOT
     if (slot == MPT_DEBUG_SLOT) { Col t_ = col(t4.x, t4.y, t4.z); printf("GPU b%d ld %a %a %a ed %a %a %a thr %a %a %a rc %a %a %a\n", bounce, ld.r, ld.g, ld.b, ed.r, ed.g, ed.b, t_.r, t_.g, t_.b, rc.r, rc.g, rc.b); }
 #endif
+}
+
+// over the bounce's shaded list (grid-stride: the grid is sized for the wavefront, the list
+// shrinks bounce by bounce); count_paths: the bounce's path rays
+template <bool EXT>
+__global__ __launch_bounds__(TB) void k_resolve(DevScene S, DevPaths P, const MptFrame* __restrict__ Fp, int bounce,
+                                                const int32_t* count_paths) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        // always-on ray accounting: path rays + NEE any-hit + NEE closest of this bounce, path hits
+        // (atomic: the two halves of an overlapped batch resolve concurrently)
+        unsigned long long* rc = (unsigned long long*)P.ray_counts;
+        atomicAdd(rc + 0, (unsigned long long)*count_paths);
+        atomicAdd(rc + 1, (unsigned long long)P.counters[CTR_ANY] + (EXT ? (unsigned long long)P.counters[CTR_XANY] : 0ull));
+        atomicAdd(rc + 2, (unsigned long long)P.counters[CTR_CL] + (EXT ? (unsigned long long)P.counters[CTR_XCL] : 0ull));
+        atomicAdd(rc + 3, (unsigned long long)(shaded_count(P) - P.counters[CTR_DEFER]));
+        atomicAdd(rc + 4, (unsigned long long)(P.counters[CTR_FULL] + P.counters[CTR_GLASS]));
+    }
+    const int nh = P.counters[CTR_HIT];
+    const int total = shaded_count(P);
+    for (int i = blockIdx.x * TB + threadIdx.x; i < total; i += gridDim.x * TB) resolve_entry<EXT>(S, P, *Fp, bounce, nh, i);
 }
 
 // ----------------------------------------------------------------------------------
@@ -2558,7 +2564,7 @@ static void frame_bounces(const DevScene& S, DevPaths& P, const MptFrame* d_fram
         }
         {
             TimedScope ts(cfg, st, KT_MISS);
-            hipLaunchKernelGGL(k_miss, dim3(blocks_for(n)), dim3(TB), 0, st, S, P, d_frame, b);
+            hipLaunchKernelGGL(k_miss, dim3(std::min(blocks_for(n), 8 * cfg.grid_persistent)), dim3(TB), 0, st, S, P, d_frame, b);
         }
         {
             TimedScope ts(cfg, st, KT_COMPACT);
@@ -2606,9 +2612,10 @@ static void frame_bounces(const DevScene& S, DevPaths& P, const MptFrame* d_fram
         }
         {
             TimedScope ts(cfg, st, KT_RESOLVE);
-            if (ext) hipLaunchKernelGGL(k_resolve<true>, dim3(blocks_for(n)), dim3(TB), 0, st, S, P, d_frame, b, &P.counters[c_cur]);
-            else hipLaunchKernelGGL(k_resolve<false>, dim3(blocks_for(classes ? 2 * n : n)), dim3(TB), 0, st, S, P, d_frame, b,
-                                    &P.counters[c_cur]);
+            // grid-stride over the shaded list (up to 2n entries with classes: deferred vertices appear twice)
+            const dim3 rg(std::min(blocks_for(classes ? 2 * n : n), 8 * cfg.grid_persistent));
+            if (ext) hipLaunchKernelGGL(k_resolve<true>, rg, dim3(TB), 0, st, S, P, d_frame, b, &P.counters[c_cur]);
+            else hipLaunchKernelGGL(k_resolve<false>, rg, dim3(TB), 0, st, S, P, d_frame, b, &P.counters[c_cur]);
         }
         // swap queues
         int32_t* tq = q_cur; q_cur = q_next; q_next = tq;
