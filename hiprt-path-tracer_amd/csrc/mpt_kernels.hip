@@ -357,6 +357,8 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MODE == TM_P
     const DevScene& S = A.S;
     const DevPaths& P = A.P;
     const int count = (MODE == TM_RAW_CLOSEST || MODE == TM_RAW_ANY) ? A.count_const : *A.count_ptr;
+    // a static grid covers the wavefront; blocks past the query list leave at once
+    if (MODE == TM_NEE_LIGHT && A.static_grid && (int)(blockIdx.x * TB) >= count) return;
     // (a static grid never spills: static_grid requires the stack to fit in LDS)
     uint32_t* spill = P.stack_spill + (MODE == TM_NEE_LIGHT && A.static_grid ? 0 : ((size_t)blockIdx.x * TB + threadIdx.x) * (2 * SPILL_DEPTH));
     uint32_t n_nodes = 0, n_tris = 0, n_rays = 0;
