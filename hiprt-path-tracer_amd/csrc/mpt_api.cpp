@@ -1351,10 +1351,20 @@ int mpt_get_aux_buffer(MptContext* c, int kind, void* dst, int dst_is_device) {
     const void* src = kind == MPT_AUX_SAMPLE_COUNT ? (const void*)c->as_count.p
                     : kind == MPT_AUX_CONVERGED_SAMPLE_COUNT ? (const void*)c->as_conv.p
                     : kind == MPT_AUX_SQUARED_LUMINANCE ? (const void*)c->as_sqlum.p : nullptr;
+    size_t bytes = (size_t)c->n_slots * 4;
+    if (kind >= MPT_AUX_RESTIR_OUTPUT && kind <= MPT_AUX_RESTIR_INITIAL && c->rs_init.p) {
+        // the frame-sized ReSTIR DI reservoir buffers: the last frame's output, the other
+        // spatial buffer (the fused pass's output when a spatial pass followed it), the
+        // initial candidates
+        const int o = c->restir_out_sp2;
+        const float4* out = o == 1 ? c->rs_sp2.p : o == 2 ? c->rs_init.p : c->rs_sp1.p;
+        src = kind == MPT_AUX_RESTIR_OUTPUT ? (const void*)out
+            : kind == MPT_AUX_RESTIR_OTHER ? (const void*)(o == 1 ? c->rs_sp1.p : c->rs_sp2.p) : (const void*)c->rs_init.p;
+        bytes = c->rs_init.n * sizeof(float4);
+    }
     if (!src) return fail(MPT_ERR_INVALID_ARGUMENT, "bad aux buffer kind or no frame rendered");
     HIPCHK(hipSetDevice(c->device));
-    HIPCHK(hipMemcpyAsync(dst, src, (size_t)c->n_slots * 4, dst_is_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost,
-                          c->stream));
+    HIPCHK(hipMemcpyAsync(dst, src, bytes, dst_is_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     return MPT_OK;
 }

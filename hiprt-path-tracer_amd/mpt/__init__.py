@@ -255,7 +255,11 @@ class GPURenderer:
     def aux_buffer(self, kind):
         """MPT_AUX_* buffer of the partition -> [rows, W] (int32, or float32 for squared luminance)."""
         f = self.frame
-        out = np.zeros((self.rows(), f.res_x), np.float32 if kind == abi.AUX_SQUARED_LUMINANCE else np.int32)
+        if kind in (abi.AUX_RESTIR_OUTPUT, abi.AUX_RESTIR_OTHER, abi.AUX_RESTIR_INITIAL):
+            # frame-sized reservoirs -> [H, W, 12] float32 (M and triangle as int bits in 0 / 3)
+            out = np.zeros((f.res_y, f.res_x, 12), np.float32)
+        else:
+            out = np.zeros((self.rows(), f.res_x), np.float32 if kind == abi.AUX_SQUARED_LUMINANCE else np.int32)
         _check(lib().mpt_get_aux_buffer(self.h, kind, _p(out), 0))
         return out
 

@@ -382,6 +382,7 @@ ESS_NO_SAMPLING, ESS_BINARY_SEARCH, ESS_ALIAS_TABLE = range(3)
 AMBIENT_NONE, AMBIENT_UNIFORM, AMBIENT_ENVMAP = range(3)
 FB_COLOR, FB_ALBEDO, FB_NORMALS = range(3)
 AUX_SAMPLE_COUNT, AUX_CONVERGED_SAMPLE_COUNT, AUX_SQUARED_LUMINANCE = range(3)
+AUX_RESTIR_OUTPUT, AUX_RESTIR_OTHER, AUX_RESTIR_INITIAL = 3, 4, 5
 
 
 class Status(C.Structure):

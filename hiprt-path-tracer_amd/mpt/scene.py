@@ -480,7 +480,11 @@ def make_camera(camera_info, width, height, jitter=True):
     inv_view_rowmajor = np.linalg.inv(view)
     # glm stores P column-major; inverse(P) reinterpreted row-major == inverse(P)^T
     inv_proj_reinterpreted = np.linalg.inv(P).T
-    view_proj = (view.T @ P.T)  # glm view_matrix * projection_matrix, column-major storage
+    # Camera.cpp:20-21: glm's view_matrix (already the transposed world->view matrix,
+    # Camera.cpp:50) times projection_matrix, stored column-major and reinterpreted row-major:
+    # (view^T P)^T = P^T view.  With the transposed inverse projection of the camera rays this
+    # reprojects a first hit onto its own pixel (Utils.h:426-437, restir_reproject).
+    view_proj = P.T @ view
     cam = abi.Camera()
     for i in range(4):
         for j in range(4):

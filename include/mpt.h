@@ -447,6 +447,12 @@ typedef struct MptStats {
 #define MPT_AUX_SAMPLE_COUNT 0            /* pixel_sample_count (int32) */
 #define MPT_AUX_CONVERGED_SAMPLE_COUNT 1  /* pixel_converged_sample_count (int32, -1 = not converged) */
 #define MPT_AUX_SQUARED_LUMINANCE 2       /* pixel_squared_luminance (float) */
+/* ReSTIR DI reservoirs of the whole frame (3 float4 per pixel: {M, weight_sum, UCW, triangle},
+ * {point, target_function}, {flags}): the last frame's output, the other spatial buffer (the
+ * fused pass's output when a spatial pass followed it) and the initial candidates */
+#define MPT_AUX_RESTIR_OUTPUT 3
+#define MPT_AUX_RESTIR_OTHER 4
+#define MPT_AUX_RESTIR_INITIAL 5
 
 /* StatusBuffersValues (Renderer/StatusBuffersValues.h:9-21) */
 typedef struct MptStatus {
@@ -560,7 +566,7 @@ int mpt_partition_rows(int32_t res_y, int32_t band_height, int32_t band_index, i
  * render_settings.do_update_status_buffers; mpt_query_status <- copy_status_buffers (.cpp:269-273). */
 int mpt_clear_status(MptContext* ctx);
 int mpt_query_status(MptContext* ctx, MptStatus* out);
-/* Copies an MPT_AUX_* buffer of the partition (n_slots * 4 bytes) to dst (host or device). */
+/* Copies an MPT_AUX_* buffer of the partition (n_slots * 4 bytes; the ReSTIR DI kinds: frame pixels * 48 bytes) to dst (host or device). */
 int mpt_get_aux_buffer(MptContext* ctx, int kind, void* dst, int dst_is_device);
 int mpt_enable_stats(MptContext* ctx, int enable, int instrumented);
 int mpt_get_stats(MptContext* ctx, MptStats* out);
