@@ -190,10 +190,23 @@ def parity_check(r, sd, luts, cam, W, H, opt, bounces, spp, workload, env=None, 
     ref = o.render(frames_for(cam, W, H, opt, band, k, bounces=bounces, world=world, alpha=alpha),
                    nthreads=cores) if k > 1 else probe
     o.close()
+    own = None
+    if restir:
+        # ReSTIR DI keeps state across samples (G-buffers, reservoirs): a context fresh like
+        # the oracle's, not the timed run's (whose last G-buffer a sample-0 reset keeps as the
+        # previous frame's, as the reference's renderer would)
+        import mpt
+        own = r = mpt.GPURenderer(r.device)
+        r.set_scene(sd)
+        r.set_luts(luts)
+        if env is not None:
+            r.set_envmap(env)
     r.enable_stats(timing=False, instrumented=False)
     r.render_samples(frs, max_batch=batch)
     r.synchronize_kernel()
     gpu = r.framebuffer(abi.FB_COLOR)
+    if own is not None:
+        own.close()
     if not whole:
         gpu = gpu[bi * BAND_H:(bi + 1) * BAND_H]
     d = (gpu.astype(np.float64) - ref.astype(np.float64)) / k
