@@ -7,7 +7,8 @@ CPU: the oracle's estimators keep their expectation (more light samples or candi
 lower the variance; the visibility target function is unbiased too).
 GPU: bit-exact against the oracle, for every light-sampling strategy, inside dielectrics
 (the RIS final shadow ray then differs from the candidate's), with alpha testing, under an
-envmap, with ReSTIR DI's later bounces and through the batched wavefronts."""
+envmap, with ReSTIR DI's later bounces and through the batched wavefronts (ReSTIR DI: each
+sample's first bounce in turn, the later bounces' extended light sampling batched)."""
 import numpy as np
 import pytest
 
@@ -107,8 +108,6 @@ def test_gpu_light_sampling_options_bit_exact(cornell, luts, case, batched):
     from oracle import oracle as orc
     kind, kw = CASES[case]
     kw = dict(kw)
-    if batched and kw["lss"] == "restir":
-        pytest.skip("ReSTIR DI frames are rendered one by one")
     sd, env, world = _scene(kind, cornell)
     frs = frames(sd, LSS[kw.pop("lss")], 3, world=world, **kw)
     r = mpt.GPURenderer(0)
