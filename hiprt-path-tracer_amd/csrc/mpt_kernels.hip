@@ -432,7 +432,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MODE == TM_P
                     n_rays++;
                     float4 ro, rd;
                     if (MODE == TM_PATH) {
-                        ray = A.queue[i];
+                        ray = A.queue ? A.queue[i] : i;   // no queue: every slot (batched ReSTIR DI camera rays)
                         ro = P.ray_o[ray];
                         rd = P.ray_d[ray];
                         skips = 0;
@@ -2507,7 +2507,7 @@ static void launch_restir(const DevScene& S, DevPaths& P, const MptFrame* d_fram
 // as q_next for an odd number of bounces, as q_cur for an even one.
 static void frame_bounces(const DevScene& S, DevPaths& P, const MptFrame* d_frame, const MptFrame& hf, LaunchCfg& cfg,
                           hipStream_t st, int b_first, int b_last, int32_t* q_cur, int c_cur, int32_t* q_next,
-                          int c_next) {
+                          int c_next, bool first_traced = false) {
     const int n = P.n;
     const bool restir = hf.options.direct_light_sampling == MPT_LSS_RESTIR_DI;
     const int nb = hf.render_settings.nb_bounces;
@@ -2516,12 +2516,15 @@ static void frame_bounces(const DevScene& S, DevPaths& P, const MptFrame* d_fram
     const bool ext = P.x_per > 0;
     const int classes = (hf.options.bsdf_override != MPT_BSDF_NONE || ext) ? 0 : (cfg.shade_classes != 0 ? (cfg.shade_glass ? 2 : 1) : 0);
     for (int b = b_first; b <= b_last; b++) {
-        // continuation / camera rays
-        hipMemsetAsync(&P.counters[CTR_FETCH], 0, sizeof(int32_t), st);
-        TraceArgs ta{};
-        ta.S = S; ta.P = P; ta.queue = q_cur; ta.count_ptr = &P.counters[c_cur]; ta.fetch = &P.counters[CTR_FETCH];
-        ta.F = d_frame; ta.bounce = b; ta.alpha = hf.render_settings.do_alpha_testing ? 1 : 0;
-        timed_trace<TM_PATH>(ta, cfg, st);
+        // continuation / camera rays (first_traced: the first bounce's rays were traced already)
+        const int alpha = hf.render_settings.do_alpha_testing ? 1 : 0;
+        if (!(first_traced && b == b_first)) {
+            hipMemsetAsync(&P.counters[CTR_FETCH], 0, sizeof(int32_t), st);
+            TraceArgs ta{};
+            ta.S = S; ta.P = P; ta.queue = q_cur; ta.count_ptr = &P.counters[c_cur]; ta.fetch = &P.counters[CTR_FETCH];
+            ta.F = d_frame; ta.bounce = b; ta.alpha = alpha;
+            timed_trace<TM_PATH>(ta, cfg, st);
+        }
         if (b == 0 && cfg.ev_first_trace) hipEventRecord(cfg.ev_first_trace, st);
         if (restir && b == 0) {
             if (cfg.halo_fn) hipMemsetAsync(&P.counters[CTR_REPROJ], 0, sizeof(int32_t), st);
@@ -2578,7 +2581,7 @@ static void frame_bounces(const DevScene& S, DevPaths& P, const MptFrame* d_fram
         hipMemsetAsync(&P.counters[CTR_FETCH], 0, sizeof(int32_t), st);
         TraceArgs tn{};
         tn.S = S; tn.P = P; tn.count_ptr = &P.counters[CTR_ANY]; tn.fetch = &P.counters[CTR_FETCH];
-        tn.F = d_frame; tn.bounce = b; tn.alpha = ta.alpha;
+        tn.F = d_frame; tn.bounce = b; tn.alpha = alpha;
         timed_trace<TM_NEE_ANY>(tn, cfg, st);
         hipMemsetAsync(&P.counters[CTR_FETCH], 0, sizeof(int32_t), st);
         tn.count_ptr = &P.counters[CTR_CL];
@@ -2671,21 +2674,37 @@ hipError_t launch_frames_restir(const DevScene& S, const DevPaths& PF, const Mpt
     const int n = PF.n_pix;
     if (n == 0 || batch <= 0) return hipSuccess;
     const int nb = hf[0].render_settings.nb_bounces;
+    // the camera rays of every sample over its own slots [s * n, (s + 1) * n) (their seeds,
+    // jitter and alpha keys are the sample's; nothing of the ReSTIR DI state is read), then
+    // one traversal of all of them: a launch of batch x n rays instead of `batch` of n
+    for (int s = 0; s < batch; s++) {
+        DevPaths P = PF;
+        offset_slots(P, (size_t)s * n);
+        P.n = n; P.batch = 1; P.group = 1;
+        TimedScope ts(cfg, st, KT_CAMERA);
+        hipLaunchKernelGGL(k_camera, dim3(blocks_for(n)), dim3(TB), 0, st, P, d_frames + s);
+    }
+    {
+        DevPaths G = PF;
+        G.group = n;
+        hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(&PF.counters[CTR_QG]), batch * n, 1, st);
+        hipMemsetAsync(&PF.counters[CTR_FETCH], 0, sizeof(int32_t), st);
+        TraceArgs ta{};
+        ta.S = S; ta.P = G; ta.queue = nullptr; ta.count_ptr = &PF.counters[CTR_QG]; ta.fetch = &PF.counters[CTR_FETCH];
+        ta.F = d_frames; ta.bounce = 0; ta.alpha = hf[0].render_settings.do_alpha_testing ? 1 : 0;
+        timed_trace<TM_PATH>(ta, cfg, st);
+    }
     hipMemsetAsync(&PF.counters[CTR_QG], 0, sizeof(int32_t), st);
     for (int s = 0; s < batch; s++) {
-        // sample s over its own slots [s * n, (s + 1) * n): frame_begin, camera rays, bounce 0
-        // with the ReSTIR DI passes (which read sample s - 1's reservoirs and G-buffer)
+        // sample s: frame_begin, G-buffer, the ReSTIR DI passes (which read sample s - 1's
+        // reservoirs and G-buffer) and the rest of bounce 0 over its own slots
         DevPaths P = PF;
         offset_slots(P, (size_t)s * n);
         P.n = n; P.batch = 1; P.group = 1;
         hipLaunchKernelGGL(k_restir_frame_begin, dim3(blocks_for(P.rs_hi - P.rs_lo)), dim3(TB), 0, st, P, d_frames + s);
         P.rs_out = restir_buffer(P, cfg.restir_out_sp2);
-        hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(&P.counters[CTR_Q0]), n, 1, st);
-        {
-            TimedScope ts(cfg, st, KT_CAMERA);
-            hipLaunchKernelGGL(k_camera, dim3(blocks_for(n)), dim3(TB), 0, st, P, d_frames + s);
-        }
-        frame_bounces(S, P, d_frames + s, hf[s], cfg, st, 0, 0, P.q0, CTR_Q0, P.q1, CTR_Q1);
+        hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(&P.counters[CTR_Q0]), n, 1, st);   // the camera queue
+        frame_bounces(S, P, d_frames + s, hf[s], cfg, st, 0, 0, P.q0, CTR_Q0, P.q1, CTR_Q1, true);
         if (nb > 0) {
             // the global queue's first entries never reach the next sample's slots: after
             // sample s it holds at most (s + 1) * n entries
