@@ -167,6 +167,7 @@ struct MptContext {
     DBuf<uint4> gb_vsA, gb_vsB, pgb_vsA, pgb_vsB;
     DBuf<MptMaterial> gb_mat, pgb_mat;
     DBuf<float4> rs_init, rs_sp1, rs_sp2, rs_plights;
+    DBuf<float4> rs_keep;                 // batched ReSTIR DI: the final reservoirs of each sample of a batch
     DBuf<int32_t> rs_conv;
     // staged ReSTIR DI passes (DevPaths::rq_*): RS_RPP ray positions per pixel slot
     DBuf<float4> rq_o, rq_d, rq_rec;
@@ -309,6 +310,7 @@ DevPaths dev_paths(MptContext* c) {
     P.pgb_pos = c->pgb_pos.p; P.pgb_sn = c->pgb_sn.p; P.pgb_gn = c->pgb_gn.p; P.pgb_view = c->pgb_view.p; P.pgb_meta = c->pgb_meta.p;
     P.pgb_vsA = c->pgb_vsA.p; P.pgb_vsB = c->pgb_vsB.p; P.pgb_mat = c->pgb_mat.p;
     P.rs_init = c->rs_init.p; P.rs_sp1 = c->rs_sp1.p; P.rs_sp2 = c->rs_sp2.p; P.rs_plights = c->rs_plights.p;
+    P.rs_keep = c->rs_keep.p; P.rs_keep_n = (int64_t)c->rs_init.n / 3; P.rs_keep_on = 0;
     P.rs_out = c->restir_out_sp2 == 1 ? c->rs_sp2.p : c->restir_out_sp2 == 2 ? c->rs_init.p : c->rs_sp1.p;
     P.rs_tin = P.rs_out;
     // contiguous band (ReSTIR DI across a partition) or the whole frame: slot s = pixel s + pix_off
@@ -561,7 +563,7 @@ int build_light_bvh(MptContext* c) {
 void release_restir(MptContext* c) {
     release_all(c->gb_pos, c->gb_sn, c->gb_gn, c->gb_view, c->pgb_pos, c->pgb_sn, c->pgb_gn, c->pgb_view, c->gb_meta,
                 c->pgb_meta, c->gb_vsA, c->gb_vsB, c->pgb_vsA, c->pgb_vsB, c->gb_mat, c->pgb_mat, c->rs_init, c->rs_sp1,
-                c->rs_sp2, c->rs_plights, c->rs_conv, c->rq_o, c->rq_d, c->rq_rec, c->rq_key, c->rq_occ, c->rq_list, c->rq_items, c->rq_meta);
+                c->rs_sp2, c->rs_plights, c->rs_keep, c->rs_conv, c->rq_o, c->rq_d, c->rq_rec, c->rq_key, c->rq_occ, c->rq_list, c->rq_items, c->rq_meta);
     c->restir_out_sp2 = 0;
 }
 
@@ -1112,6 +1114,15 @@ static int prepare_batch(MptContext* c, const MptFrame* f, int batch) {
         return fail(MPT_ERR_OUT_OF_MEMORY, "wavefront above MPT_MAX_WAVEFRONT_PATHS paths");
     r = ensure_batch(c, batch, c->any_tex || f->bsdf_flags.white_furnace_mode);
     if (r != MPT_OK) return r;
+    if (f->options.direct_light_sampling == MPT_LSS_RESTIR_DI && batch > 1 &&
+        c->rs_keep.n < c->rs_init.n * (size_t)batch) {
+        // each sample's final reservoirs, for the batch's bounce-0 shading (launch_frames_restir)
+        c->rs_keep.release();
+        if (c->rs_keep.alloc(c->rs_init.n * (size_t)batch) != hipSuccess) {
+            (void)hipGetLastError();
+            return fail(MPT_ERR_OUT_OF_MEMORY, "ReSTIR DI batch reservoirs");
+        }
+    }
     int iter = 0;
     const int per = ext_layout(*f, &iter);
     return ensure_ext(c, batch, per, iter);

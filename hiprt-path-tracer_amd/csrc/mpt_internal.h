@@ -175,6 +175,9 @@ struct DevPaths {
     float4* rs_sp2;
     float4* rs_out;           // restir_output_reservoirs of this frame (rs_sp1 or rs_sp2)
     float4* rs_tin;           // temporal input of this frame (last frame's output)
+    float4* rs_keep;          // batched ReSTIR DI: each sample's final reservoirs (sample-major, rs_keep_n pixels each)
+    int64_t rs_keep_n;
+    int rs_keep_on;           // k_shade's final shading reads rs_keep by (sample, pixel) instead of rs_out
     float4* rs_plights;       // presampled lights (4 float4 each)
     // The G-buffer / reservoir / rs_conv arrays are frame-sized and indexed by the global
     // pixel index; path-state slot s of this context is pixel s + pix_off (contiguous band).

@@ -1511,13 +1511,21 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_
                         do_eval = geo > 0.0f;
                     }
                 } else if (op == OP_RESTIR) {
-                    // sample_light_ReSTIR_DI + evaluate_ReSTIR_DI_reservoir (FinalShading.h:16-115)
-                    const size_t rpix = (size_t)slot + P.pix_off;
-                    rres = rr_load(P.rs_out, (int)rpix);
+                    // sample_light_ReSTIR_DI + evaluate_ReSTIR_DI_reservoir (FinalShading.h:16-115);
+                    // a batched ReSTIR DI launch reads the sample's kept final reservoirs
+                    float4* rsb = P.rs_out;
+                    size_t rpix = (size_t)slot + P.pix_off;
+                    if (P.rs_keep_on) {
+                        int kpix, ksub;
+                        batch_split(P, slot, kpix, ksub);
+                        rsb = P.rs_keep + (size_t)ksub * 3 * (size_t)P.rs_keep_n;
+                        rpix = (size_t)kpix + P.pix_off;
+                    }
+                    rres = rr_load(rsb, (int)rpix);
                     if ((rres.flags & RF_ENVMAP) && ws.ambient_light_type != MPT_AMBIENT_ENVMAP) {
                         rres.UCW = 0.0f;   // validate_reservoir writes through to the buffer
-                        float4 a = P.rs_out[3 * rpix];
-                        P.rs_out[3 * rpix] = make_float4(a.x, a.y, 0.0f, a.w);
+                        float4 a = rsb[3 * rpix];
+                        rsb[3 * rpix] = make_float4(a.x, a.y, 0.0f, a.w);
                     }
                     if (rres.UCW > 0.0f) {
                         if (rres.flags & RF_ENVMAP) { L = mat_x_vec(ws.envmap_to_world_matrix.m, rres.point); dist = 1.0e35f; }
@@ -2501,13 +2509,24 @@ static void launch_restir(const DevScene& S, DevPaths& P, const MptFrame* d_fram
     cfg.restir_out_sp2 = restir_code(P, P.rs_out);
 }
 
+// CameraRays' G-buffer write and the ReSTIR DI passes of a frame (P.rs_out: their output)
+static void restir_first_bounce(const DevScene& S, DevPaths& P, const MptFrame* d_frame, const MptFrame& hf, LaunchCfg& cfg,
+                                hipStream_t st) {
+    if (cfg.halo_fn) hipMemsetAsync(&P.counters[CTR_REPROJ], 0, sizeof(int32_t), st);
+    {
+        TimedScope tk(cfg, st, KT_GBUFFER);
+        hipLaunchKernelGGL(k_gbuffer, dim3(blocks_for(P.n)), dim3(TB), 0, st, S, P, d_frame);
+    }
+    launch_restir(S, P, d_frame, hf, cfg, st);
+}
+
 // Bounces [b_first, b_last] of the paths in q_cur (count counters[c_cur]): trace, G-buffer and
 // ReSTIR DI passes (bounce 0 of a ReSTIR DI frame), split, shade, miss, compact into q_next,
 // NEE rays, resolve.  Leaves the continuation list of the last bounce in the buffer passed
 // as q_next for an odd number of bounces, as q_cur for an even one.
 static void frame_bounces(const DevScene& S, DevPaths& P, const MptFrame* d_frame, const MptFrame& hf, LaunchCfg& cfg,
                           hipStream_t st, int b_first, int b_last, int32_t* q_cur, int c_cur, int32_t* q_next,
-                          int c_next, bool first_traced = false) {
+                          int c_next, bool first_traced = false, bool restir_done = false) {
     const int n = P.n;
     const bool restir = hf.options.direct_light_sampling == MPT_LSS_RESTIR_DI;
     const int nb = hf.render_settings.nb_bounces;
@@ -2526,14 +2545,7 @@ static void frame_bounces(const DevScene& S, DevPaths& P, const MptFrame* d_fram
             timed_trace<TM_PATH>(ta, cfg, st);
         }
         if (b == 0 && cfg.ev_first_trace) hipEventRecord(cfg.ev_first_trace, st);
-        if (restir && b == 0) {
-            if (cfg.halo_fn) hipMemsetAsync(&P.counters[CTR_REPROJ], 0, sizeof(int32_t), st);
-            {
-                TimedScope tk(cfg, st, KT_GBUFFER);
-                hipLaunchKernelGGL(k_gbuffer, dim3(blocks_for(n)), dim3(TB), 0, st, S, P, d_frame);
-            }
-            launch_restir(S, P, d_frame, hf, cfg, st);
-        }
+        if (restir && b == 0 && !restir_done) restir_first_bounce(S, P, d_frame, hf, cfg, st);
         hipMemsetAsync(&P.counters[c_next], 0, sizeof(int32_t), st);
         hipMemsetAsync(&P.counters[CTR_ANY], 0, 2 * sizeof(int32_t), st);
         hipMemsetAsync(&P.counters[CTR_HIT], 0, 4 * sizeof(int32_t), st);   // HIT, MISS, FULL, DEFER
@@ -2668,6 +2680,10 @@ __global__ __launch_bounds__(TB) void k_append_queue(int32_t* __restrict__ dst, 
 __global__ void k_add_count(int32_t* dst_count, const int32_t* src_count) {
     if (threadIdx.x == 0) dst_count[0] += src_count[0];
 }
+__global__ __launch_bounds__(TB) void k_iota(int32_t* q, int n) {
+    const int i = blockIdx.x * TB + threadIdx.x;
+    if (i < n) q[i] = i;
+}
 
 hipError_t launch_frames_restir(const DevScene& S, const DevPaths& PF, const MptFrame* d_frames, const MptFrame* hf,
                                 int batch, LaunchCfg& cfg, hipStream_t st) {
@@ -2695,15 +2711,26 @@ hipError_t launch_frames_restir(const DevScene& S, const DevPaths& PF, const Mpt
         timed_trace<TM_PATH>(ta, cfg, st);
     }
     hipMemsetAsync(&PF.counters[CTR_QG], 0, sizeof(int32_t), st);
+    // With an envmap the final shading never writes through to a reservoir (validate_reservoir
+    // only drops envmap samples without one), so no sample's passes depend on an earlier
+    // sample's shading: each sample's final reservoirs are kept (rs_keep) and bounce 0 runs
+    // once over the batch, like the later bounces
+    const bool defer = PF.rs_keep && hf[0].world_settings.ambient_light_type == MPT_AMBIENT_ENVMAP;
     for (int s = 0; s < batch; s++) {
         // sample s: frame_begin, G-buffer, the ReSTIR DI passes (which read sample s - 1's
-        // reservoirs and G-buffer) and the rest of bounce 0 over its own slots
+        // reservoirs and G-buffer) and, unless deferred, the rest of bounce 0 over its own slots
         DevPaths P = PF;
         offset_slots(P, (size_t)s * n);
         P.n = n; P.batch = 1; P.group = 1;
         hipLaunchKernelGGL(k_restir_frame_begin, dim3(blocks_for(P.rs_hi - P.rs_lo)), dim3(TB), 0, st, P, d_frames + s);
         P.rs_out = restir_buffer(P, cfg.restir_out_sp2);
         hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(&P.counters[CTR_Q0]), n, 1, st);   // the camera queue
+        if (defer) {
+            restir_first_bounce(S, P, d_frames + s, hf[s], cfg, st);
+            const size_t rn = 3 * (size_t)PF.rs_keep_n;
+            hipMemcpyAsync(PF.rs_keep + (size_t)s * rn, P.rs_out, rn * sizeof(float4), hipMemcpyDeviceToDevice, st);
+            continue;
+        }
         frame_bounces(S, P, d_frames + s, hf[s], cfg, st, 0, 0, P.q0, CTR_Q0, P.q1, CTR_Q1, true);
         if (nb > 0) {
             // the global queue's first entries never reach the next sample's slots: after
@@ -2713,10 +2740,18 @@ hipError_t launch_frames_restir(const DevScene& S, const DevPaths& PF, const Mpt
             hipLaunchKernelGGL(k_add_count, dim3(1), dim3(64), 0, st, &PF.counters[CTR_QG], &PF.counters[CTR_Q1]);
         }
     }
-    // bounces 1..nb of every sample as one wavefront (slot = sample * n + pixel: group = n)
+    // bounces 1..nb (deferred: 0..nb) of every sample as one wavefront (slot = sample * n + pixel:
+    // group = n)
     DevPaths G = PF;
     G.group = n;
-    if (nb > 0) frame_bounces(S, G, d_frames, hf[0], cfg, st, 1, nb, G.q0, CTR_QG, G.q1, CTR_Q1);
+    if (defer) {
+        G.rs_keep_on = 1;
+        hipLaunchKernelGGL(k_iota, dim3(blocks_for(batch * n)), dim3(TB), 0, st, G.q0, batch * n);
+        hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(&G.counters[CTR_Q0]), batch * n, 1, st);
+        frame_bounces(S, G, d_frames, hf[0], cfg, st, 0, nb, G.q0, CTR_Q0, G.q1, CTR_Q1, true, true);
+    } else if (nb > 0) {
+        frame_bounces(S, G, d_frames, hf[0], cfg, st, 1, nb, G.q0, CTR_QG, G.q1, CTR_Q1);
+    }
     {
         TimedScope ts(cfg, st, KT_ACCUMULATE);
         hipLaunchKernelGGL(k_accumulate, dim3(blocks_for(n)), dim3(TB), 0, st, G, d_frames);

@@ -214,23 +214,38 @@ BATCH_CASES = ["principled", "lambert", "three_passes", "permutation_sampling", 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("max_batch", [2, 7])
-@pytest.mark.parametrize("case", BATCH_CASES + ["zero_bounces", "alpha_cards"])
+@pytest.mark.parametrize("case", BATCH_CASES + ["zero_bounces", "alpha_cards", "envmap", "envmap_alpha_cards",
+                                               "envmap_unfused", "envmap_zero_bounces", "envmap_moving"])
 def test_gpu_restir_batched_bit_exact(cornell, luts, case, max_batch):
     """mpt_render_frames over ReSTIR DI frames: each sample's camera rays, reuse passes and
     first bounce in turn, the later bounces of the batch as one wavefront (slot = sample *
     pixels + pixel) -- equal to the oracle's sample-by-sample render; adaptive sampling and
-    the moved camera (a frame that differs) fall back to smaller runs."""
+    the moved camera (a frame that differs) fall back to smaller runs.  Under an envmap the
+    first bounce is deferred too (the kept final reservoirs of every sample, rs_keep)."""
     import mpt
     from oracle import oracle as orc
-    sd = synthetic.with_alpha_cards(cornell) if case == "alpha_cards" else cornell
-    kw = dict(bounces=0) if case == "zero_bounces" else dict(alpha=True) if case == "alpha_cards" else CASES[case]
+    sd = synthetic.with_alpha_cards(cornell) if case.endswith("alpha_cards") else cornell
+    env = mpt.build_envmap(scene.procedural_sky(128, 64, seed=7)) if case.startswith("envmap") else None
+    base = case[len("envmap_"):] if case.startswith("envmap_") else ("" if case == "envmap" else case)
+    if base == "zero_bounces":
+        kw = dict(bounces=0)
+    elif base == "alpha_cards":
+        kw = dict(alpha=True)
+    elif base == "moving":
+        kw = dict(move_at=3)
+    else:
+        kw = dict(CASES[base]) if base else {}
+    if env is not None:
+        kw["world"] = scene.envmap_world(1.0)
     frs = frames(sd, abi.LSS_RESTIR_DI, 7, **kw)
     r = mpt.GPURenderer(0)
     r.set_scene(sd)
     r.set_luts(luts)
+    if env is not None:
+        r.set_envmap(env)
     r.render_samples(frs, max_batch=max_batch)
     r.synchronize_kernel()
-    o = orc.Oracle(sd, luts)
+    o = orc.Oracle(sd, luts, envmap=env)
     c, ca, cn = o.render(frs, aov=True)
     g = r.framebuffer(abi.FB_COLOR)
     assert np.array_equal(g, c), f"{case}: {(g != c).sum()} values differ"
