@@ -65,6 +65,15 @@ constexpr int SPILL_DEPTH = TRAV_SPILL_DEPTH;
 DEV int lane_id() { return __lane_id(); }
 // storage index of staged NEE query id (slot * 4 + kind): kind-major planes (DevPaths::nq_o)
 DEV size_t nq_index(const DevPaths& P, int id) { return (size_t)(id & 3) * (size_t)P.nq_stride + (size_t)(id >> 2); }
+// storage index of staged ReSTIR DI ray id (slot * RS_RPP + position): position-major planes
+// (DevPaths::rq_o / rq_d / rq_key / rq_occ), so that a block's lanes (consecutive slots) staging
+// the same position write one contiguous run
+DEV size_t rq_phys(const DevPaths& P, int id) {
+    const int s = id / RS_RPP_HOST;
+    return (size_t)(id - s * RS_RPP_HOST) * (size_t)P.n + (size_t)s;
+}
+// record k of slot s (DevPaths::rq_rec): record-major planes
+DEV size_t rq_rec_at(const DevPaths& P, int s, int k) { return (size_t)k * (size_t)P.n + (size_t)s; }
 DEV int wave_append(int32_t* counter, bool pred) {
     unsigned long long m = __ballot(pred);
     unsigned long long act = __ballot(1);
@@ -466,7 +475,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MODE == TM_P
                         tr.init(mk3(ro.x, ro.y, ro.z), mk3(rd.x, rd.y, rd.z), (int)__float_as_uint(ro.w), tmax, al, akey);
                         if (MODE == TM_NEE_LIGHT && S.n_light_tris == 0) tr.gk = 0u;   // no light: nothing to traverse
                     } else if (MODE == TM_LIST_ANY || MODE == TM_LIST_CLOSEST) {
-                        ray = A.queue[i];
+                        ray = (int)rq_phys(P, A.queue[i]);   // the staged ray's storage index
                         ro = A.raw_o[ray];
                         rd = A.raw_d[ray];
                         tr.init(mk3(ro.x, ro.y, ro.z), mk3(rd.x, rd.y, rd.z), (int)__float_as_uint(ro.w), ANY ? rd.w : INFINITY,

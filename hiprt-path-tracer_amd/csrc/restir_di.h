@@ -138,9 +138,10 @@ DEV int rs_block_scan(int v, int* tmp, int& total) {
 }
 
 DEV void rs_stage_ray(const DevPaths& P, size_t id, const TgtRay& r, int last, uint32_t key) {
-    P.rq_o[id] = make_float4(r.o.x, r.o.y, r.o.z, __uint_as_float((uint32_t)last));
-    P.rq_d[id] = make_float4(r.d.x, r.d.y, r.d.z, r.dist - 1.0e-4f);
-    P.rq_key[id] = key;
+    const size_t q = rq_phys(P, (int)id);
+    P.rq_o[q] = make_float4(r.o.x, r.o.y, r.o.z, __uint_as_float((uint32_t)last));
+    P.rq_d[q] = make_float4(r.d.x, r.d.y, r.d.z, r.dist - 1.0e-4f);
+    P.rq_key[q] = key;
 }
 
 // appends the ray positions in `mask` of slot s to the list behind `counter` (one atomic per block)
@@ -712,12 +713,12 @@ RESTIR_KERNEL void k_restir_initial(DevScene S, DevPaths P, const MptFrame* __re
             bool refr = dot(dir, g.view) < 0.0f;   // the reference tests against the view direction
             if (!(bpdf > 0.0f)) continue;
             if (STAGED) {
-                const size_t id = (size_t)s * RS_RPP;
+                const size_t id = rq_phys(P, s * RS_RPP);
                 P.rq_o[id] = make_float4(g.p.x, g.p.y, g.p.z, __uint_as_float((uint32_t)g.last));
                 P.rq_d[id] = make_float4(dir.x, dir.y, dir.z, INFINITY);
                 P.rq_key[id] = F.render_settings.do_alpha_testing ? alpha_key(seed, 0, 5, RP_BSDF(i)) : 0u;
-                P.rq_rec[(size_t)s * RS_REC] = make_float4(f.r, f.g, f.b, bpdf);
-                P.rq_rec[(size_t)s * RS_REC + 1] = make_float4(dir.x, dir.y, dir.z, refr ? 1.0f : 0.0f);
+                P.rq_rec[rq_rec_at(P, s, 0)] = make_float4(f.r, f.g, f.b, bpdf);
+                P.rq_rec[rq_rec_at(P, s, 1)] = make_float4(dir.x, dir.y, dir.z, refr ? 1.0f : 0.0f);
                 rmask = 1u;
                 continue;
             }
@@ -797,8 +798,8 @@ RESTIR_KERNEL void k_rsi_finish(DevScene S, DevPaths P, const MptFrame* __restri
             const int nl = rd.number_of_initial_light_candidates, nb = rd.number_of_initial_bsdf_candidates;
             float env_p = 0.0f;
             if (w.ambient_light_type == MPT_AMBIENT_ENVMAP) env_p = S.n_emissive == 0 ? 1.0f : rd.envmap_candidate_probability;
-            const float4 fr = P.rq_rec[(size_t)s * RS_REC], dr = P.rq_rec[(size_t)s * RS_REC + 1];
-            const float4 h = P.rq_o[id];
+            const float4 fr = P.rq_rec[rq_rec_at(P, s, 0)], dr = P.rq_rec[rq_rec_at(P, s, 1)];
+            const float4 h = P.rq_o[rq_phys(P, (int)id)];
             const bool found = (int)__float_as_uint(h.w) >= 0 && h.x < 1.0e35f - 1.0e-4f;
             initial_bsdf_candidate(S, F, gp, gsn, mk3(dr.x, dr.y, dr.z), col(fr.x, fr.y, fr.z), fr.w, dr.w != 0.0f, found, h,
                                    env_p, nl, nb, r, rng);
@@ -1422,7 +1423,7 @@ __global__ __launch_bounds__(TB) void k_rsp_select(DevScene S, DevPaths P, const
                         (n_plain ? m_plain : m_gen) |= 1u << (2 * k + 1);
                         vis_bits |= 1u << (2 * k + 1);   // ReSTIR_DI_BiasCorrectionUseVisibility
                     }
-                    P.rq_rec[(size_t)s * RS_REC + k] = make_float4(__int_as_float(ni), 0.0f, 0.0f, jac);
+                    P.rq_rec[rq_rec_at(P, s, k)] = make_float4(__int_as_float(ni), 0.0f, 0.0f, jac);
                 }
             }
         }
@@ -1461,7 +1462,7 @@ RESTIR_KERNEL void k_rsp_eval(DevScene S, DevPaths P, const MptFrame* __restrict
             const int jj = FUSED ? (temporal ? j : j - 2) : j;
             const int k = temporal ? RS_KMAX : jj >> 1, which = jj & 1;
             const int center = s + P.pix_off;
-            float* rec = reinterpret_cast<float*>(&P.rq_rec[(size_t)s * RS_REC + k]);
+            float* rec = reinterpret_cast<float*>(&P.rq_rec[rq_rec_at(P, s, k)]);
             const int ni = __float_as_int(rec[0]);
             const RSurf g = gb_surface(S, P, which ? ni : center, which && prev);
             const RResv smp = which ? rr_load(FUSED ? P.rs_init : in, center) : rr_load(in, ni);
@@ -1515,7 +1516,7 @@ RESTIR_KERNEL void k_rsp_combine(DevScene S, DevPaths P, const MptFrame* __restr
             float4 rec = make_float4(0.0f, 0.0f, 0.0f, 1.0f);
             if (k == reuse) nr = cres;
             else {
-                rec = P.rq_rec[(size_t)s * RS_REC + k];
+                rec = P.rq_rec[rq_rec_at(P, s, k)];
                 nr = rr_load(in, __float_as_int(rec.x));
             }
             const bool vis = spatial_visibility(F, rd, k, reuse);
@@ -1525,7 +1526,7 @@ RESTIR_KERNEL void k_rsp_combine(DevScene S, DevPaths P, const MptFrame* __restr
                 else {
                     tfc = rec.y;
                     if (vis && tfc > 0.0f) {
-                        if (P.rq_occ[r0 + 2 * k]) tfc = 0.0f;
+                        if (P.rq_occ[rq_phys(P, (int)r0 + 2 * k)]) tfc = 0.0f;
                         ntr++;
                     }
                 }
@@ -1542,7 +1543,7 @@ RESTIR_KERNEL void k_rsp_combine(DevScene S, DevPaths P, const MptFrame* __restr
             if (k != reuse && update_mc) {
                 tcn = rec.z;
                 if (tcn > 0.0f) {
-                    if (P.rq_occ[r0 + 2 * k + 1]) tcn = 0.0f;
+                    if (P.rq_occ[rq_phys(P, (int)r0 + 2 * k + 1)]) tcn = 0.0f;
                     ntr++;
                 }
             }
@@ -1652,7 +1653,7 @@ __global__ __launch_bounds__(TB) void k_rst_select(DevScene S, DevPaths P, const
                         vis_bits |= 1u << 1;
                         prev_bits |= pv << 1;
                     }
-                    P.rq_rec[(size_t)s * RS_REC + RS_KMAX] = make_float4(__int_as_float(tidx), 0.0f, 0.0f, jac);
+                    P.rq_rec[rq_rec_at(P, s, RS_KMAX)] = make_float4(__int_as_float(tidx), 0.0f, 0.0f, jac);
                 }
                 for (int k = 0; k < reuse && vM != 0; k++) {
                     if (!((cache >> k) & 1)) continue;
@@ -1673,9 +1674,9 @@ __global__ __launch_bounds__(TB) void k_rst_select(DevScene S, DevPaths P, const
                         vis_bits |= 1u << (3 + 2 * k);
                         prev_bits |= pv << (3 + 2 * k);
                     }
-                    P.rq_rec[(size_t)s * RS_REC + k] = make_float4(__int_as_float(ni), 0.0f, 0.0f, jac);
+                    P.rq_rec[rq_rec_at(P, s, k)] = make_float4(__int_as_float(ni), 0.0f, 0.0f, jac);
                 }
-                P.rq_rec[(size_t)s * RS_REC + RS_KMAX + 1] = make_float4(__uint_as_float(rng.s), __int_as_float(tidx), 0.0f, 0.0f);
+                P.rq_rec[rq_rec_at(P, s, RS_KMAX + 1)] = make_float4(__uint_as_float(rng.s), __int_as_float(tidx), 0.0f, 0.0f);
             }
         }
         P.rq_meta[s] = meta;
@@ -1697,7 +1698,7 @@ RESTIR_KERNEL void k_rst_combine(DevScene S, DevPaths P, const MptFrame* __restr
         const int center = s + P.pix_off;
         MptReSTIRDISettings rd = F.render_settings.restir_di_settings;
         rd.spatial_pass_index = 0;
-        const float4 st4 = P.rq_rec[(size_t)s * RS_REC + RS_KMAX + 1];
+        const float4 st4 = P.rq_rec[rq_rec_at(P, s, RS_KMAX + 1)];
         Rng rng = make_rng(__float_as_uint(st4.x));   // after the temporal search and the rotation
         const int tidx = __float_as_int(st4.y);
         RResv tres = rr_default();
@@ -1714,12 +1715,12 @@ RESTIR_KERNEL void k_rst_combine(DevScene S, DevPaths P, const MptFrame* __restr
         int ntr = 0;
         const size_t r0 = (size_t)s * RS_RPP;
         if (temporal_ok) {
-            const float4 rec = P.rq_rec[(size_t)s * RS_REC + RS_KMAX];
+            const float4 rec = P.rq_rec[rq_rec_at(P, s, RS_KMAX)];
             float tfc = 0.0f;
             if (tres.UCW > 0.0f) {
                 tfc = rec.y;
                 if (tfc > 0.0f) {
-                    if (P.rq_occ[r0]) tfc = 0.0f;
+                    if (P.rq_occ[rq_phys(P, (int)r0)]) tfc = 0.0f;
                     ntr++;
                 }
             }
@@ -1732,7 +1733,7 @@ RESTIR_KERNEL void k_rst_combine(DevScene S, DevPaths P, const MptFrame* __restr
             if (update_mc) {
                 tcn = rec.z;
                 if (tcn > 0.0f) {
-                    if (P.rq_occ[r0 + 1]) tcn = 0.0f;
+                    if (P.rq_occ[rq_phys(P, (int)r0 + 1)]) tcn = 0.0f;
                     ntr++;
                 }
             }
@@ -1745,7 +1746,7 @@ RESTIR_KERNEL void k_rst_combine(DevScene S, DevPaths P, const MptFrame* __restr
             float4 rec = make_float4(0.0f, 0.0f, 0.0f, 1.0f);
             if (k == reuse) nr = ic;
             else {
-                rec = P.rq_rec[(size_t)s * RS_REC + k];
+                rec = P.rq_rec[rq_rec_at(P, s, k)];
                 nr = rr_load(tin, __float_as_int(rec.x));
             }
             const bool vis = spatial_visibility(F, rd, k, reuse);
@@ -1755,7 +1756,7 @@ RESTIR_KERNEL void k_rst_combine(DevScene S, DevPaths P, const MptFrame* __restr
                 else {
                     tfc = rec.y;
                     if (vis && tfc > 0.0f) {
-                        if (P.rq_occ[r0 + 2 + 2 * k]) tfc = 0.0f;
+                        if (P.rq_occ[rq_phys(P, (int)r0 + 2 + 2 * k)]) tfc = 0.0f;
                         ntr++;
                     }
                 }
@@ -1775,7 +1776,7 @@ RESTIR_KERNEL void k_rst_combine(DevScene S, DevPaths P, const MptFrame* __restr
                 if (k != reuse && update_mc) {
                     tcn = rec.z;
                     if (tcn > 0.0f) {
-                        if (P.rq_occ[r0 + 3 + 2 * k]) tcn = 0.0f;
+                        if (P.rq_occ[rq_phys(P, (int)r0 + 3 + 2 * k)]) tcn = 0.0f;
                         ntr++;
                     }
                 }
@@ -1820,7 +1821,7 @@ __global__ __launch_bounds__(TB) void k_rs_visapply(DevPaths P, float4* out) {
     if (i >= P.counters[CTR_RQV]) return;
     const int id = P.rq_list[i];
     const size_t c = (size_t)(id / RS_RPP + P.pix_off);
-    if (P.rq_occ[id]) out[3 * c].z = -1.0f;
+    if (P.rq_occ[rq_phys(P, id)]) out[3 * c].z = -1.0f;
     else out[3 * c + 2].x = __uint_as_float(__float_as_uint(out[3 * c + 2].x) | RF_UNOCCLUDED);
 }
 #endif
