@@ -150,7 +150,7 @@ struct MptContext {
     int batch_cap = 0;      // samples per pixel the path state is sized for (mpt_render_frames)
     int batch = 1;          // samples of the launch being set up
     DBuf<float4> ray_o, ray_d, hit, thr, col, alb, nrmv, nq_o, nq_d, nhit;
-    DBuf<uint8_t> hit_inside, occ, qmask;
+    DBuf<uint8_t> hit_inside, hit_cls, occ, qmask;
     DBuf<uint32_t> rng, spill, spill2;
     DBuf<uint2> seeds;
     DBuf<uint4> vsA, vsB;
@@ -269,6 +269,7 @@ DevPaths dev_paths(MptContext* c) {
     P.ray_d = c->ray_d.p;
     P.hit = c->hit.p;
     P.hit_inside = c->hit_inside.p;
+    P.hit_cls = c->hit_cls.p;
     P.rng = c->rng.p;
     P.seeds = c->seeds.p;
     P.thr = c->thr.p;
@@ -354,7 +355,7 @@ struct Allocs {
 constexpr size_t PATH_BYTES = 8 * 16 + 32 + 7 * 16 + 128 + 16 + 4 + 24 + 4 + 8 + 3;
 
 void release_batch(MptContext* c) {
-    release_all(c->ray_o, c->ray_d, c->hit, c->hit_inside, c->rng, c->seeds, c->thr, c->col, c->vsA, c->vsB, c->alb, c->nrmv,
+    release_all(c->ray_o, c->ray_d, c->hit, c->hit_inside, c->hit_cls, c->rng, c->seeds, c->thr, c->col, c->vsA, c->vsB, c->alb, c->nrmv,
                 c->q0, c->q1, c->qh, c->qm, c->qf, c->nq_light, c->nthr, c->na, c->nb, c->ndir, c->nris, c->ne1, c->ne2, c->nq_o,
                 c->nq_d, c->nq_tgt, c->occ, c->nhit, c->qmask, c->active,
                 c->mat_slot);
@@ -375,7 +376,7 @@ int ensure_batch(MptContext* c, int batch, bool mat_slot) {
     Allocs A;
     if (!have) {
         c->batch_cap = 0;
-        A(c->ray_o, N); A(c->ray_d, N); A(c->hit, N); A(c->hit_inside, N); A(c->rng, N); A(c->seeds, N); A(c->thr, N); A(c->col, N);
+        A(c->ray_o, N); A(c->ray_d, N); A(c->hit, N); A(c->hit_inside, N); A(c->hit_cls, N); A(c->rng, N); A(c->seeds, N); A(c->thr, N); A(c->col, N);
         A(c->vsA, N); A(c->vsB, N); A(c->alb, N); A(c->nrmv, N); A(c->q0, N); A(c->q1, N); A(c->qh, N); A(c->qm, N); A(c->qf, N); A(c->nq_light, N);
         A(c->nthr, N); A(c->na, N); A(c->nb, N); A(c->ndir, N); A(c->nris, N); A(c->ne1, N); A(c->ne2, N);
         A(c->nq_o, 4 * N); A(c->nq_d, 4 * N); A(c->nq_tgt, 4 * N); A(c->occ, 4 * N); A(c->nhit, N);
@@ -632,6 +633,21 @@ int resolve_materials(MptContext* c) {
     HIPCHK(hipStreamSynchronize(c->stream));
     c->any_tex = false;
     for (int32_t v : t) c->any_tex |= (v & MT_TEXTURED) != 0;
+    // each triangle's material class in its BVH record (TriRec::pad1): the path traversal
+    // reports it with the hit (DevPaths::hit_cls), so k_split needs no material lookups
+    bool changed = false;
+    for (TriRec& tr : c->bvh.tris) {
+        int32_t prim;
+        std::memcpy(&prim, &tr.prim_bits, 4);
+        const uint32_t cls = (prim >= 0 && (size_t)prim < c->h_mat_idx.size()) ? (uint32_t)(t[c->h_mat_idx[prim]] & 0x7f) : 0u;
+        uint32_t old;
+        std::memcpy(&old, &tr.pad1, 4);
+        if (old != cls) { std::memcpy(&tr.pad1, &cls, 4); changed = true; }
+    }
+    if (changed) {
+        HIPCHK(c->tris.upload(c->bvh.tris.data(), c->bvh.tris.size(), c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+    }
     return MPT_OK;
 }
 

@@ -116,6 +116,7 @@ struct DevPaths {
     float4* ray_d;            // xyz + tmax
     float4* hit;              // t, u, v, prim bits
     uint8_t* hit_inside;      // "inside a volume" before the last stack push (trace_ray normal flip)
+    uint8_t* hit_cls;         // the hit triangle's material class (MT_* bits, TriRec::pad1), 0xff: miss
     uint32_t* rng;
     uint2* seeds;             // per slot: the camera launch's and the path tracing launch's pixel seeds (k_camera)
     float4* thr;
@@ -277,7 +278,7 @@ struct LaunchCfg {
 // path state (the second half of an overlapped batch, one sample of a batched ReSTIR DI
 // wavefront); per-pixel buffers stay shared.
 inline void offset_slots(DevPaths& P, size_t off) {
-    P.ray_o += off; P.ray_d += off; P.hit += off; P.hit_inside += off; P.rng += off; P.seeds += off; P.thr += off; P.col += off;
+    P.ray_o += off; P.ray_d += off; P.hit += off; P.hit_inside += off; P.hit_cls += off; P.rng += off; P.seeds += off; P.thr += off; P.col += off;
     P.vsA += off; P.vsB += off; P.alb += off; P.nrm += off;
     P.q0 += off; P.q1 += off; P.qh += off; P.qm += off; P.qf += off; P.nq_light += off;
     // NEE record planes, and the kind-major query / occlusion planes (stride = the allocation)

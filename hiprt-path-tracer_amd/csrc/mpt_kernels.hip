@@ -125,6 +125,7 @@ struct Trav {
     float best;          // closest: current closest t; any: t_max (unchanged until the hit)
     int bprim;
     float bu, bv;
+    uint32_t bcls;       // closest: the material class of the hit (TriRec::pad1)
     uint32_t gbase, gimask, gk;   // current node group: child base, internal mask, remaining hits
     int sp;
     int last_hit;
@@ -144,6 +145,7 @@ struct Trav {
         bprim = -1;
         bu = 0.0f;
         bv = 0.0f;
+        bcls = 0u;
         gbase = 0;
         gimask = 1u;
         gk = 1u << (0 ^ xr);
@@ -290,7 +292,7 @@ struct Trav {
                         return true;
                     }
                 } else if (t < best || (t == best && prim < bprim)) {
-                    best = t; bprim = prim; bu = u; bv = v;
+                    best = t; bprim = prim; bu = u; bv = v; bcls = __float_as_uint(t2.w);
                 }
             }
         }
@@ -522,6 +524,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MODE == TM_P
             P.ray_o[ray] = make_float4(tr.o.x, tr.o.y, tr.o.z, __uint_as_float((uint32_t)tr.last_hit));
             P.hit[ray] = make_float4(tr.best, tr.bu, tr.bv, __uint_as_float((uint32_t)(found ? tr.bprim : -1)));
             P.hit_inside[ray] = was_inside ? 1 : 0;
+            P.hit_cls[ray] = found ? (uint8_t)tr.bcls : (uint8_t)0xffu;
         } else if (MODE == TM_NEE_ANY) {
             if (A.ext) P.xq_occ[ray] = found ? 1 : 0;
             else P.occ[nq_index(P, ray)] = found ? 1 : 0;
@@ -1836,9 +1839,10 @@ __global__ __launch_bounds__(CP_NT) void k_split(DevScene S, DevPaths P, const i
     int nh = 0, nf = 0, ng = 0;
 #pragma unroll
     for (int j = 0; j < CP_ITEMS; j++) {
-        const int prim = j < n ? __float_as_int(P.hit[slots[j]].w) : -1;
-        if (prim >= 0) {
-            const int32_t mt = classes ? S.mat_tex[S.mat_idx[prim]] : 0;
+        // the hit's material class as the traversal reported it (0xff: a miss)
+        const uint32_t hc = j < n ? (uint32_t)P.hit_cls[slots[j]] : 0xffu;
+        if (hc != 0xffu) {
+            const int32_t mt = classes ? (int32_t)hc : 0;
             if (classes == 2 && (mt & MT_GLASS)) { gm |= 1u << j; ng++; }
             else if (mt & MT_FULL) { fm |= 1u << j; nf++; }
             else { hm |= 1u << j; nh++; }
