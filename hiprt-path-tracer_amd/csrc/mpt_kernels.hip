@@ -2200,7 +2200,13 @@ __global__ __launch_bounds__(TB) void k_resolve(DevScene S, DevPaths P, const Mp
 // ----------------------------------------------------------------------------------
 // k_accumulate (FullPathTracer.h:292-327)
 // ----------------------------------------------------------------------------------
-DEV void accumulate_sample(const DevPaths& P, const MptRenderSettings& rs, int pixel, int slot) {
+// the pixel's framebuffer values, held in registers over the samples of a batch
+struct PixAcc {
+    Col c;
+    v3 a, n;
+    float sq;
+};
+DEV void accumulate_sample(const DevPaths& P, const MptRenderSettings& rs, int slot, PixAcc& f, bool& any) {
     if (!P.active[slot]) return;          // FullPathTracer.h:114-115
     float4 cv = P.col[slot];
     Col c = col(cv.x, cv.y, cv.z);
@@ -2208,45 +2214,61 @@ DEV void accumulate_sample(const DevPaths& P, const MptRenderSettings& rs, int p
     bool invalid = false;
     if (wl == 0.0f) invalid |= (c.r < 0 || c.g < 0 || c.b < 0);
     invalid |= has_nan(c);
-    float* fb = P.fb_color + 3 * (size_t)pixel;
     if (invalid) {
         if (rs.display_NaNs) {
             Col dc = col(1.0e30f, 0.0f, 1.0e30f);
             if (rs.sample_number != 0) dc = dc * (float)rs.sample_number;
-            fb[0] = dc.r; fb[1] = dc.g; fb[2] = dc.b;
+            f.c = dc;
         }
         return;
     }
-    P.status[1] = 1u;                     // still_one_ray_active (FullPathTracer.h:299)
+    any = true;                           // still_one_ray_active (FullPathTracer.h:299)
     if (has_adaptive_buffers(rs)) {
         float l = lum(c);
-        P.as_sqlum[pixel] += l * l;
+        f.sq += l * l;
     }
-    if (rs.sample_number == 0) { fb[0] = c.r; fb[1] = c.g; fb[2] = c.b; }
-    else { fb[0] += c.r; fb[1] += c.g; fb[2] += c.b; }
+    if (rs.sample_number == 0) f.c = c;
+    else { f.c.r += c.r; f.c.g += c.g; f.c.b += c.b; }
     float cnt = (float)rs.denoiser_AOV_accumulation_counter;
     float4 a = P.alb[slot], n = P.nrm[slot];
-    float* fa = P.fb_albedo + 3 * (size_t)pixel;
-    float* fn = P.fb_normal + 3 * (size_t)pixel;
     if (rs.sample_number == 0) {
-        fa[0] = a.x; fa[1] = a.y; fa[2] = a.z;
-        fn[0] = n.x; fn[1] = n.y; fn[2] = n.z;
+        f.a = mk3(a.x, a.y, a.z);
+        f.n = mk3(n.x, n.y, n.z);
     } else {
-        fa[0] = (fa[0] * cnt + a.x) / (cnt + 1.0f);
-        fa[1] = (fa[1] * cnt + a.y) / (cnt + 1.0f);
-        fa[2] = (fa[2] * cnt + a.z) / (cnt + 1.0f);
-        v3 acc = (mk3(fn[0], fn[1], fn[2]) * cnt + mk3(n.x, n.y, n.z)) / (cnt + 1.0f);
+        f.a.x = (f.a.x * cnt + a.x) / (cnt + 1.0f);
+        f.a.y = (f.a.y * cnt + a.y) / (cnt + 1.0f);
+        f.a.z = (f.a.z * cnt + a.z) / (cnt + 1.0f);
+        v3 acc = (f.n * cnt + mk3(n.x, n.y, n.z)) / (cnt + 1.0f);
         float len = length(acc);
-        if (!is_zero(len)) { acc = acc / len; fn[0] = acc.x; fn[1] = acc.y; fn[2] = acc.z; }
+        if (!is_zero(len)) f.n = acc / len;
     }
 }
 // one pixel per lane; the samples of a batch are added in sample order, exactly as
-// consecutive single-sample frames would add them
+// consecutive single-sample frames would add them, on register copies of the pixel's
+// framebuffer values (read once, written once per launch); the still-active flag is
+// written once per wave instead of once per path
 #ifndef MPT_TU_PART   // k_accumulate
 __global__ __launch_bounds__(TB) void k_accumulate(DevPaths P, const MptFrame* __restrict__ Fp) {
     const int pixel = blockIdx.x * TB + threadIdx.x;
-    if (pixel >= P.n_pix) return;
-    for (int sub = 0; sub < P.batch; sub++) accumulate_sample(P, Fp[sub].render_settings, pixel, batch_slot(P, pixel, sub));
+    bool any = false;
+    if (pixel < P.n_pix) {
+        float* fb = P.fb_color + 3 * (size_t)pixel;
+        float* fa = P.fb_albedo + 3 * (size_t)pixel;
+        float* fn = P.fb_normal + 3 * (size_t)pixel;
+        PixAcc f;
+        f.c = col(fb[0], fb[1], fb[2]);
+        f.a = mk3(fa[0], fa[1], fa[2]);
+        f.n = mk3(fn[0], fn[1], fn[2]);
+        bool adaptive = false;
+        for (int sub = 0; sub < P.batch; sub++) adaptive |= has_adaptive_buffers(Fp[sub].render_settings);
+        f.sq = adaptive ? P.as_sqlum[pixel] : 0.0f;
+        for (int sub = 0; sub < P.batch; sub++) accumulate_sample(P, Fp[sub].render_settings, batch_slot(P, pixel, sub), f, any);
+        fb[0] = f.c.r; fb[1] = f.c.g; fb[2] = f.c.b;
+        fa[0] = f.a.x; fa[1] = f.a.y; fa[2] = f.a.z;
+        fn[0] = f.n.x; fn[1] = f.n.y; fn[2] = f.n.z;
+        if (adaptive) P.as_sqlum[pixel] = f.sq;
+    }
+    if (__ballot(any) != 0ull && lane_id() == 0) P.status[1] = 1u;
 }
 
 #endif
