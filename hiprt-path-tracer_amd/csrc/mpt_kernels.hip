@@ -2478,7 +2478,8 @@ static void launch_restir(const DevScene& S, DevPaths& P, const MptFrame* d_fram
         else {
             const dim3 gp(blocks_for(P.n));
             hipMemsetAsync(&P.counters[CTR_RQ], 0, 4 * sizeof(int32_t), st);   // CTR_RQ, CTR_RQV, CTR_RQE0, CTR_RQE1
-            hipLaunchKernelGGL(k_rsi_classify, gp, dim3(TB), 0, st, S, P, d_frame, ovr == MPT_BSDF_NONE ? 1 : 0);
+            hipLaunchKernelGGL(k_rsi_classify, dim3((P.n + TB * RSI_PPT - 1) / (TB * RSI_PPT)), dim3(TB), 0, st, S, P, d_frame,
+                               ovr == MPT_BSDF_NONE ? 1 : 0);
             launch_restir_kernel(ovr, RK_INITIAL_STAGED_PLAIN, g, st, S, P, d_frame);
             launch_restir_kernel(ovr, RK_INITIAL_STAGED_GENERIC, g, st, S, P, d_frame);
             TraceArgs ta{};

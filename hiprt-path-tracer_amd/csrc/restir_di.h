@@ -749,25 +749,32 @@ RESTIR_KERNEL void k_restir_initial(DevScene S, DevPaths P, const MptFrame* __re
 // The staged initial pass's pixel lists: pixels that run the pass (not emissive, active, a
 // camera hit), by the class of their G-buffer surface (rs_plain): plain at [0, n), generic at
 // [n, 2n) of rq_items; every other pixel is marked skipped for k_rsi_finish.
+// RSI_PPT pixels per thread (s, s + TB, ...): the list appends take one device-scope atomic
+// per class and block, and one word serialises them (~90 per us), so fewer, larger blocks
+constexpr int RSI_PPT = 4;
 __global__ __launch_bounds__(TB) void k_rsi_classify(DevScene S, DevPaths P, const MptFrame* __restrict__ Fp, int principled) {
     __shared__ int tmp[TB / 64];
     __shared__ int base;
     const MptFrame& F = *Fp;
     if (S.n_emissive == 0 && F.world_settings.ambient_light_type != MPT_AMBIENT_ENVMAP) return;   // (grid-uniform)
-    const int s = blockIdx.x * TB + threadIdx.x;
-    int cls = -1;
-    if (s < P.n) {
+    const int s0 = blockIdx.x * (TB * RSI_PPT) + threadIdx.x;
+    uint32_t cm[2] = {0u, 0u};   // bit k: pixel s0 + k * TB in class 0 / 1
+#pragma unroll
+    for (int k = 0; k < RSI_PPT; k++) {
+        const int s = s0 + k * TB;
+        if (s >= P.n) break;
         const int pix = s + P.pix_off;
         const RSurf g = gb_surface(S, P, pix, false);
-        if (!is_emissive(*g.m) && P.active[s] && P.gb_meta[pix].z) cls = principled && rs_plain(S, P, pix, g) ? 0 : 1;
+        if (!is_emissive(*g.m) && P.active[s] && P.gb_meta[pix].z) cm[principled && rs_plain(S, P, pix, g) ? 0 : 1] |= 1u << k;
         else P.rq_meta[s] = make_int4(RSM_SKIP, 0, 0, 0);
     }
     for (int c = 0; c < 2; c++) {
         int tot;
-        const int off = rs_block_scan(cls == c ? 1 : 0, tmp, tot);
+        const int off = rs_block_scan(__popc(cm[c]), tmp, tot);
         if (threadIdx.x == 0) base = tot ? atomicAdd(&P.counters[CTR_RQE0 + c], tot) : 0;
         __syncthreads();
-        if (cls == c) P.rq_items[(size_t)c * P.n + base + off] = s;
+        int o = base + off;
+        for (uint32_t m = cm[c]; m; m &= m - 1u) P.rq_items[(size_t)c * P.n + o++] = s0 + __builtin_ctz(m) * TB;
         __syncthreads();
     }
 }
