@@ -2489,7 +2489,7 @@ static void launch_restir(const DevScene& S, DevPaths& P, const MptFrame* d_fram
             ta.F = d_frame; ta.alpha = hf.render_settings.do_alpha_testing ? 1 : 0;
             hipMemsetAsync(&P.counters[CTR_FETCH], 0, sizeof(int32_t), st);
             launch_trace_mode<TM_LIST_CLOSEST>(ta, cfg.grid_persistent, cfg.stats, st);
-            hipLaunchKernelGGL(k_rsi_finish, gp, dim3(TB), 0, st, S, P, d_frame);
+            hipLaunchKernelGGL(k_rsi_finish, dim3((P.n + TB * RSI_PPT - 1) / (TB * RSI_PPT)), dim3(TB), 0, st, S, P, d_frame);
             ta.count_ptr = &P.counters[CTR_RQV];
             hipMemsetAsync(&P.counters[CTR_FETCH], 0, sizeof(int32_t), st);
             launch_trace_mode<TM_LIST_ANY>(ta, cfg.grid_persistent, cfg.stats, st);

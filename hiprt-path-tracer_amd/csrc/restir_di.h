@@ -791,8 +791,11 @@ RESTIR_KERNEL void k_rsi_finish(DevScene S, DevPaths P, const MptFrame* __restri
     const MptReSTIRDISettings& rd = F.render_settings.restir_di_settings;
     const MptWorldSettings& w = F.world_settings;
     if (S.n_emissive == 0 && w.ambient_light_type != MPT_AMBIENT_ENVMAP) return;   // as k_restir_initial (grid-uniform)
-    const int s = blockIdx.x * TB + threadIdx.x;
-    uint32_t vmask = 0u, n_any = 0u, n_cl = 0u;
+    const int s0 = blockIdx.x * (TB * RSI_PPT) + threadIdx.x;   // RSI_PPT pixels per thread, as k_rsi_classify
+    uint32_t vbits = 0u, n_any = 0u, n_cl = 0u;
+#pragma unroll
+    for (int kk = 0; kk < RSI_PPT; kk++) {
+    const int s = s0 + kk * TB;
     if (s < P.n && !(P.rq_meta[s].x & RSM_SKIP)) {
         const int4 meta = P.rq_meta[s];
         const int pix = s + P.pix_off;
@@ -810,7 +813,7 @@ RESTIR_KERNEL void k_rsi_finish(DevScene S, DevPaths P, const MptFrame* __restri
             const bool found = (int)__float_as_uint(h.w) >= 0 && h.x < 1.0e35f - 1.0e-4f;
             initial_bsdf_candidate(S, F, gp, gsn, mk3(dr.x, dr.y, dr.z), col(fr.x, fr.y, fr.z), fr.w, dr.w != 0.0f, found, h,
                                    env_p, nl, nb, r, rng);
-            n_cl = 1u;
+            n_cl++;
         }
         r.UCW = r.wsum == 0.0f ? 0.0f : 1.0f / r.target * r.wsum;   // end()
         r.M = 1;
@@ -824,12 +827,20 @@ RESTIR_KERNEL void k_rsi_finish(DevScene S, DevPaths P, const MptFrame* __restri
                          F.render_settings.do_alpha_testing ? alpha_key(pass_seed(F, (uint32_t)pix, F.restir_di_seeds[1]), 0, 5,
                                                                         RP_VISREUSE)
                                                             : 0u);
-            vmask = 1u;
-            n_any = 1u;
+            vbits |= 1u << kk;
+            n_any++;
         }
         rr_store(P.rs_init, pix, r);
     }
-    rs_append(P, &P.counters[CTR_RQV], s, vmask, tmp, &sbase);
+    }
+    {   // the visibility-reuse rays (position 0 of their slots) to the CTR_RQV list
+        int tot;
+        const int off = rs_block_scan(__popc(vbits), tmp, tot);
+        if (threadIdx.x == 0) sbase = tot ? atomicAdd(&P.counters[CTR_RQV], tot) : 0;
+        __syncthreads();
+        int o = sbase + off;
+        for (uint32_t m = vbits; m; m &= m - 1u) P.rq_list[o++] = (s0 + __builtin_ctz(m) * TB) * RS_RPP;
+    }
     int ta, tc;
     (void)rs_block_scan((int)n_any, tmp, ta);
     (void)rs_block_scan((int)n_cl, tmp, tc);
