@@ -223,8 +223,6 @@ def load_traffic(workload, W, H):
     tools/pmc_traffic.py from separate rocprofv3 --pmc passes of this same command).
     PMC counters need rocprofv3 around the process, so they cannot be read live here."""
     import glob
-    if (W, H) not in ((1920, 1080), (3840, 2160)):
-        return None
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{workload}_pmc_traffic.json")))
     if not files:
         return None
@@ -395,7 +393,7 @@ def main():
                       "bytes_per_unit": b_ray, "unit_of_work": "ray", "nodes_per_ray": n_node, "tris_per_ray": n_tri,
                       "node_simd_util": cal.stage_nodes[m] / max(1, cal.stage_node_slots[m]),
                       "tri_simd_util": cal.stage_tris[m] / max(1, cal.stage_tri_slots[m]),
-                      "units_per_launch": st.stage_rays[m] / launches})
+                      "units_per_launch": st.stage_rays[m] / launches, "launches": st.stage_launches[m]})
     # shade: per path vertex (a path ray that hit a surface: k_split sends the misses to
     # k_miss) = material 256 + vertex gathers 12+36+36+24 + path state 2x96 (§8d); the
     # plain-dielectric kernel (material classes) shades all but the generic
@@ -408,8 +406,24 @@ def main():
                             "BSDF sampling, RR)",
                   "symbol": "void mpt::k_shade<0, true",   # k_shade<OVR, plain, RIS visibility>
                   "total_ms": st.shade_ms, "avg_launch_ms": s_avg, "bytes_per_unit": b_vtx, "unit_of_work": "path vertex (hit)",
-                  "units_per_launch": hits / sl,
+                  "units_per_launch": hits / sl, "launches": st.shade_launches,
                   "achieved": hits * b_vtx / sl / (s_avg * 1e-3) / 1e9 if s_avg > 0 else 0.0})
+    # ReSTIR DI (C4): the staged reuse passes' plain-class target-function evaluations, timed on
+    # their own (HIP events around every k_rsp_eval<OVR, true, *> launch, fused and spatial); per
+    # evaluation item: item 4 + its record 16 read + 4 written + the evaluated
+    # surface's G-buffer entry 7 x 16 + the sample's reservoir 48 + the material 256 + the
+    # light's emissive-table record 80 + the staged ray 36 = 556 B
+    B_EVAL = 4 + 16 + 4 + 112 + 48 + 256 + 80 + 36
+    if st.restir_eval_launches:
+        el = st.restir_eval_launches
+        e_avg = st.restir_eval_ms / el
+        lines.append({"kernel": "k_rsp_eval<BSDF_NONE, plain> (ReSTIR DI target-function evaluations at plain-dielectric "
+                                "surfaces, fused spatiotemporal + spatial passes)",
+                      "symbol": "void mpt::k_rsp_eval<0, true", "total_ms": st.restir_eval_ms, "avg_launch_ms": e_avg,
+                      "bytes_per_unit": B_EVAL, "unit_of_work": "target-function evaluation",
+                      "units_per_launch": st.restir_eval_items / el, "launches": el,
+                      "achieved": st.restir_eval_items * B_EVAL / el / (e_avg * 1e-3) / 1e9 if e_avg > 0 else 0.0})
+    n_kernel_lines = len(lines)
     # ReSTIR DI passes (C4), timed as a whole (HIP events around each pass): per pixel of the
     # band, the G-buffer / reservoir / presampled-light bytes the pass reads and writes
     # (DESIGN.md §4).  With the reference-default weights a pass is staged (restir_di.h:
@@ -430,9 +444,10 @@ def main():
             continue
         avg = ms / nl
         lines.append({"kernel": name, "symbol": sym, "total_ms": ms, "avg_launch_ms": avg, "bytes_per_unit": bpp,
-                      "unit_of_work": "pixel", "units_per_launch": n_pix,
+                      "unit_of_work": "pixel", "units_per_launch": n_pix, "launches": nl,
                       "achieved": n_pix * bpp / (avg * 1e-3) / 1e9 if avg > 0 else 0.0})
-    dom = max(lines, key=lambda x: x["total_ms"])
+    # the dominant KERNEL (the ReSTIR DI pass lines above span several kernels: reported, not candidates)
+    dom = max(lines[:n_kernel_lines], key=lambda x: x["total_ms"])
 
     default_cfg = a.strategy is None and default_bounces and a.bsdf == "principled" and a.scene is None
     pmc = load_traffic(a.workload, W, H) if default_cfg else None
@@ -448,31 +463,39 @@ def main():
         return {}
 
     def roof(x):
-        tr = pmc_entry(x["symbol"])
+        # counter fields come from the committed profile of this command (profiles/), each
+        # normalised by THAT run's own launches: its units per launch (the bench line of the
+        # profiled run) and its kernel-trace launch time -- so per-unit bytes and fractions do not
+        # depend on this run's --steps; `traffic` is those bytes per unit x this run's units
+        tr = pmc_entry(x["symbol"]).get("timed") or {}
         r = {"bound": "hbm", "achieved": round(x["achieved"], 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-             "frac": round(x["achieved"] / HBM_PEAK_GBS, 5),
-             "traffic": round(tr["traffic_bytes"]) if tr.get("traffic_bytes") else None,
+             "frac": round(x["achieved"] / HBM_PEAK_GBS, 5), "traffic": None,
              "kernel": x["kernel"],
              "avg_launch_ms": round(x["avg_launch_ms"], 5), "bytes_per_unit": round(x["bytes_per_unit"], 2),
              "unit_of_work": x["unit_of_work"], "units_per_launch": round(x["units_per_launch"], 1)}
-        if r["traffic"]:
-            r.update(traffic_read=round(tr["read_bytes"]), traffic_write=round(tr["write_bytes"]),
-                     traffic_per_unit=round(tr["traffic_bytes"] / max(1.0, x["units_per_launch"]), 1),
-                     traffic_source=pmc["file"])
-        if r["traffic"]:
-            # the kernel's measured HBM bytes over its live launch time: the bandwidth it really draws
-            r["pmc_hbm_frac"] = round(tr["traffic_bytes"] / (x["avg_launch_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+        if tr.get("traffic_per_unit"):
+            r.update(traffic=round(tr["traffic_per_unit"] * x["units_per_launch"]),
+                     traffic_per_unit=round(tr["traffic_per_unit"], 1),
+                     traffic_read_per_unit=round(tr["read_per_unit"], 1), traffic_write_per_unit=round(tr["write_per_unit"], 1),
+                     traffic_source=pmc["file"],
+                     profiled={"units_per_launch": round(tr["units_per_launch"], 1), "launches": tr["launches"],
+                               "avg_launch_ms": round(tr["avg_ns"] / 1e6, 5), "traffic_per_launch": round(tr["traffic_bytes"])},
+                     # the kernel's measured HBM bytes over its own profiled launch time
+                     pmc_hbm_frac=round(tr["hbm_frac"], 4))
         if tr.get("valu_insts"):
             # VALU issue roofline: wave-level VALU instructions per launch over the chip's issue
-            # rate (256 CUs x 4 SIMDs, one wave64 VALU instruction per 2 cycles at 2.4 GHz)
-            rate = tr["valu_insts"] / (x["avg_launch_ms"] * 1e-3)
-            r["valu"] = {"insts_per_launch": round(tr["valu_insts"]), "achieved_tinst_s": round(rate / 1e12, 4),
-                         "peak_tinst_s": VALU_PEAK / 1e12, "frac": round(rate / VALU_PEAK, 4),
-                         "per_unit": round(tr["valu_insts"] / max(1.0, x["units_per_launch"]), 2)}
+            # rate (256 CUs x 4 SIMDs, one wave64 VALU instruction per 2 cycles at 2.4 GHz), both
+            # from the profiled run
+            r["valu"] = {"insts_per_launch": round(tr["valu_insts"]), "achieved_tinst_s": round(tr["valu_rate"] / 1e12, 4),
+                         "peak_tinst_s": VALU_PEAK / 1e12, "frac": round(tr["valu_rate"] / VALU_PEAK, 4),
+                         "per_unit": round(tr["valu_insts"] / max(1.0, tr["units_per_launch"]), 2)}
         if "nodes_per_ray" in x:
             r.update(nodes_per_ray=round(x["nodes_per_ray"], 3), tris_per_ray=round(x["tris_per_ray"], 3),
                      node_simd_util=round(x["node_simd_util"], 3), tri_simd_util=round(x["tri_simd_util"], 3))
         return r
+
+    dname, darch, dcus = mpt.device_info(local)
+    device = {"name": dname, "arch": darch, "compute_units": dcus, "libmpt_sha256_16": mpt.build_id()}
 
     parity = None
     if rank == 0 and world == 1 and not a.no_parity:
@@ -517,6 +540,15 @@ def main():
                                      f"interleaved {BAND_H}-row bands over {world} rank(s), RCCL all_gather")},
             "roofline": roof(dom),
             "roofline_traversal": roof(max(lines[:3], key=lambda x: x["total_ms"])),
+            "roofline_restir": roof(lines[n_kernel_lines - 1]) if st.restir_eval_launches else None,
+            # every timed kernel line of this run (tools/pmc_traffic.py normalises the profile of
+            # this command by them: the last `launches` dispatches of `symbol` are the timed ones)
+            "kernel_lines": [{"symbol": x["symbol"], "launches": x["launches"], "units_per_launch": x["units_per_launch"],
+                              "avg_launch_ms": round(x["avg_launch_ms"], 5), "bytes_per_unit": round(x["bytes_per_unit"], 2)}
+                             for x in lines[:n_kernel_lines]],
+            "restir_passes": [{"kernel": x["kernel"], "ms_per_step": round(x["total_ms"] / K, 4), "model_bytes_per_pixel": x["bytes_per_unit"],
+                               "model_achieved_gbs": round(x["achieved"], 2)} for x in lines[n_kernel_lines:]] or None,
+            "device": device,
             "traversal_stages": [{"kernel": x["kernel"].split(" ")[0], "nodes_per_ray": round(x["nodes_per_ray"], 3),
                                   "tris_per_ray": round(x["tris_per_ray"], 3), "node_simd_util": round(x["node_simd_util"], 3),
                                   "tri_simd_util": round(x["tri_simd_util"], 3)} for x in lines[:3]],

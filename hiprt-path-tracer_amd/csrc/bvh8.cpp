@@ -40,6 +40,7 @@ struct Builder {
     int n;
     int max_leaf;
     int sah_depth = 40;   // deeper than this, only balanced (median) splits
+    int n_bins = 32;      // SAH bins per axis (MPT_BVH_BINS, read once per build, clamped to [2, 256])
     std::vector<AABB> tbox;
     std::vector<float> cen;
     std::vector<int> order;
@@ -53,7 +54,7 @@ struct Builder {
         nodes[id].box = b;
         int cnt = end - begin;
         if (cnt <= max_leaf) { nodes[id].first = begin; nodes[id].count = cnt; return id; }
-        const int NB = std::getenv("MPT_BVH_BINS") ? std::atoi(std::getenv("MPT_BVH_BINS")) : 32;
+        const int NB = n_bins;
         int best_axis = -1, best_split = 0;
         float best_cost = FLT_MAX;
         // past sah_depth only balanced splits, so that the tree depth stays bounded (traversal stack)
@@ -137,6 +138,7 @@ void build_bvh8(const float* vertices, const int32_t* indices, int32_t num_trian
     b.n = num_triangles;
     b.max_leaf = max_leaf;
     b.sah_depth = sah_depth;
+    if (const char* nb = std::getenv("MPT_BVH_BINS")) b.n_bins = std::max(2, std::min(256, std::atoi(nb)));
     b.tbox.resize(num_triangles);
     b.cen.resize(3 * (size_t)num_triangles);
     b.order.resize(num_triangles);

@@ -78,8 +78,9 @@ constexpr int FRAME_RING = 256;   // >= 2 x MPT_MAX_BATCH
 // light-hit traversals, split, plain and generic shade, miss, compact, resolve) for up to 65
 // bounces (validate_frame), + camera, ReSTIR, accumulate
 // + the ReSTIR DI kernels (G-buffer, presampling, initial, temporal / spatiotemporal, 4 spatial)
-constexpr int EV_POOL = 2 * 2 * (10 * 65 + 3 + 8);   // x2: the two halves of an overlapped batch
-constexpr int RESTIR_MAX_BATCH = 32;                    // ~45 timed scopes per batched ReSTIR DI sample
+constexpr int RESTIR_MAX_BATCH = 32;                    // <= 50 timed scopes per batched ReSTIR DI sample
+// x2: the two halves of an overlapped batch
+constexpr int EV_POOL = 2 * 2 * ((10 * 65 + 3 + 8) > 50 * RESTIR_MAX_BATCH ? (10 * 65 + 3 + 8) : 50 * RESTIR_MAX_BATCH);
 #ifndef MPT_TRACE_BLOCKS_PER_CU
 #define MPT_TRACE_BLOCKS_PER_CU 5
 #endif
@@ -490,7 +491,12 @@ int upload_alpha_flags(MptContext* c) {
 // for a nearer (or equally near, lower-index) triangle, equals the whole-scene closest hit
 // whenever that one is a light, and every other outcome contributes nothing.  Rebuilt when
 // a material edit changes the set; alpha-test flags as upload_alpha_flags.
-static int build_light_bvh_impl(MptContext* c) {
+#define LBCHK(expr)                                                                                   \
+    do {                                                                                              \
+        hipError_t e_ = (expr);                                                                       \
+        if (e_ != hipSuccess) { herr = e_; return fail(MPT_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); } \
+    } while (0)
+static int build_light_bvh_impl(MptContext* c, hipError_t& herr) {
     std::vector<uint8_t> lit(c->h_mats.size()), aflag(c->h_mats.size());
     for (size_t i = 0; i < c->h_mats.size(); i++) {
         const MptMaterial& m = c->h_mats[i];
@@ -526,7 +532,7 @@ static int build_light_bvh_impl(MptContext* c) {
                 std::memcpy(&k, &tr.prim_bits, 4);
                 std::memcpy(&tr.prim_bits, &prims[k], 4);
             }
-            HIPCHK(c->nodes_light.upload(c->bvh_light.nodes.data(), c->bvh_light.nodes.size(), st));
+            LBCHK(c->nodes_light.upload(c->bvh_light.nodes.data(), c->bvh_light.nodes.size(), st));
         }
     }
     if (!prims.empty()) {
@@ -536,24 +542,31 @@ static int build_light_bvh_impl(MptContext* c) {
             uint32_t f = aflag[c->h_mat_idx[prim]];
             std::memcpy(&tr.pad0, &f, 4);
         }
-        HIPCHK(c->tris_light.upload(c->bvh_light.tris.data(), c->bvh_light.tris.size(), st));
+        LBCHK(c->tris_light.upload(c->bvh_light.tris.data(), c->bvh_light.tris.size(), st));
     }
-    HIPCHK(hipStreamSynchronize(st));
+    LBCHK(hipStreamSynchronize(st));
     c->light_bvh_ok = true;
     return MPT_OK;
 }
 
-// A light BVH that cannot be built or uploaded is an optimisation lost, not an error: the
-// light-hit queries then take the exact whole-scene closest-hit path (light_bvh_ok false),
-// so a material edit never fails half-applied because of it.
+#undef LBCHK
+// A light BVH that cannot be allocated is an optimisation lost, not an error: the light-hit
+// queries then take the exact whole-scene closest-hit path (light_bvh_ok false), so a
+// material edit never fails half-applied because device memory is short.  Any other HIP
+// error (a sticky fault of an earlier launch surfacing at the synchronize, a failed copy) is
+// returned to the caller.
 int build_light_bvh(MptContext* c) {
-    if (build_light_bvh_impl(c) == MPT_OK) return MPT_OK;
-    (void)hipGetLastError();
-    (void)hipStreamSynchronize(c->stream);
+    hipError_t herr = hipSuccess;
+    const int rc = build_light_bvh_impl(c, herr);
+    if (rc == MPT_OK) return MPT_OK;
     c->nodes_light.release();
     c->tris_light.release();
     c->h_light_prims.clear();
     c->light_bvh_ok = false;
+    if (herr != hipErrorOutOfMemory) return rc;
+    (void)hipGetLastError();
+    const hipError_t se = hipStreamSynchronize(c->stream);
+    if (se != hipSuccess) return fail(MPT_ERR_HIP, std::string("build_light_bvh: ") + hipGetErrorString(se));
     g_err.clear();
     return MPT_OK;
 }
@@ -749,9 +762,20 @@ const char* mpt_last_error(void) { return g_err.c_str(); }
 int mpt_version(void) { return 1; }
 
 int mpt_abi_sizes(int32_t* out, int n) {
-    int32_t s[6] = {(int32_t)sizeof(MptMaterial), (int32_t)sizeof(MptRenderSettings), (int32_t)sizeof(MptWorldSettings),
-                    (int32_t)sizeof(MptCamera), (int32_t)sizeof(MptFrame), (int32_t)sizeof(MptScene)};
-    for (int i = 0; i < n && i < 6; i++) out[i] = s[i];
+    int32_t s[7] = {(int32_t)sizeof(MptMaterial), (int32_t)sizeof(MptRenderSettings), (int32_t)sizeof(MptWorldSettings),
+                    (int32_t)sizeof(MptCamera), (int32_t)sizeof(MptFrame), (int32_t)sizeof(MptScene),
+                    (int32_t)sizeof(MptStats)};
+    if (!out) return fail(MPT_ERR_INVALID_ARGUMENT, "NULL argument");
+    for (int i = 0; i < n && i < 7; i++) out[i] = s[i];
+    return MPT_OK;
+}
+
+int mpt_device_info(int device, char* name, int32_t name_cap, char* arch, int32_t arch_cap, int32_t* out_cus) {
+    hipDeviceProp_t p;
+    HIPCHK(hipGetDeviceProperties(&p, device));
+    if (name && name_cap > 0) { std::strncpy(name, p.name, (size_t)name_cap - 1); name[name_cap - 1] = 0; }
+    if (arch && arch_cap > 0) { std::strncpy(arch, p.gcnArchName, (size_t)arch_cap - 1); arch[arch_cap - 1] = 0; }
+    if (out_cus) *out_cus = p.multiProcessorCount;
     return MPT_OK;
 }
 
@@ -1087,8 +1111,12 @@ static int default_batch(MptContext* c, const MptFrame& f) {
     if (f.band_height <= 0 || f.band_count <= 0 || f.band_index < 0 || f.band_index >= f.band_count || f.res_x <= 0)
         return 1;
     const size_t pix = (size_t)std::max(1, rows_of(f.res_y, f.band_height, f.band_index, f.band_count)) * (size_t)f.res_x;
+    // + the kept final reservoirs of a batched ReSTIR DI wavefront under an envmap (rs_keep: 3 float4
+    // per pixel and sample, see prepare_batch)
+    const bool keep = f.options.direct_light_sampling == MPT_LSS_RESTIR_DI &&
+                      f.world_settings.ambient_light_type == MPT_AMBIENT_ENVMAP;
     const size_t per = PATH_BYTES + ((c->any_tex || f.bsdf_flags.white_furnace_mode) ? sizeof(MptMaterial) : 0) +
-                       EXT_ENTRY_BYTES * (size_t)ext_layout(f, nullptr);
+                       EXT_ENTRY_BYTES * (size_t)ext_layout(f, nullptr) + (keep ? 3 * sizeof(float4) : 0);
     size_t fr = 0, tot = 0;
     if (hipMemGetInfo(&fr, &tot) != hipSuccess) { (void)hipGetLastError(); fr = 0; }
     const size_t held = (size_t)c->batch_cap * (size_t)std::max(c->n_slots, 1) * per;
@@ -1130,9 +1158,12 @@ static int prepare_batch(MptContext* c, const MptFrame* f, int batch) {
         return fail(MPT_ERR_OUT_OF_MEMORY, "wavefront above MPT_MAX_WAVEFRONT_PATHS paths");
     r = ensure_batch(c, batch, c->any_tex || f->bsdf_flags.white_furnace_mode);
     if (r != MPT_OK) return r;
-    if (f->options.direct_light_sampling == MPT_LSS_RESTIR_DI && batch > 1 &&
-        c->rs_keep.n < c->rs_init.n * (size_t)batch) {
-        // each sample's final reservoirs, for the batch's bounce-0 shading (launch_frames_restir)
+    // each sample's final reservoirs, for the batch's bounce-0 shading (launch_frames_restir):
+    // only read when the envmap is the ambient light (the deferred first bounce), so only held then
+    const bool keep = f->options.direct_light_sampling == MPT_LSS_RESTIR_DI &&
+                      f->world_settings.ambient_light_type == MPT_AMBIENT_ENVMAP;
+    if (!keep) c->rs_keep.release();
+    if (keep && batch > 1 && c->rs_keep.n < c->rs_init.n * (size_t)batch) {
         c->rs_keep.release();
         if (c->rs_keep.alloc(c->rs_init.n * (size_t)batch) != hipSuccess) {
             (void)hipGetLastError();
@@ -1461,6 +1492,9 @@ int mpt_get_stats(MptContext* c, MptStats* out) {
         out->restir_kernel_ms[k] = c->stage_ms[KT_GBUFFER + k];
         out->restir_kernel_launches[k] = c->stage_launches[KT_GBUFFER + k];
     }
+    out->restir_eval_ms = c->stage_ms[KT_RS_EVAL];
+    out->restir_eval_launches = c->stage_launches[KT_RS_EVAL];
+    out->restir_eval_items = rc[5];
     out->trace_launches = c->trace_launches;
     out->frames = c->frames;
     out->frame_ms = c->frame_ms;

@@ -152,7 +152,8 @@ struct DevPaths {
     float* fb_normal;
     uint32_t* stack_spill;    // global spill area of the traversal stacks
     uint64_t* stats;          // [trace mode][rays, nodes, tris, -] (instrumented traversal)
-    uint64_t* ray_counts;     // path rays, NEE any-hit rays, NEE closest rays, path hits, generic-class vertices (always on)
+    uint64_t* ray_counts;     // path rays, NEE any-hit rays, NEE closest rays, path hits, generic-class vertices,
+                              // plain-class ReSTIR DI target evaluations (always on)
     // adaptive sampling / stop-noise threshold (AuxiliaryBuffers, RenderData.h:62-84)
     int32_t* as_count;        // pixel_sample_count
     float* as_sqlum;          // pixel_squared_luminance
@@ -215,13 +216,15 @@ struct DevPaths {
 constexpr int N_TRACE_MODES = 5;
 // staged ReSTIR DI reuse passes (restir_di.h RS_KMAX / RS_RPP): neighbours per pass, ray positions per pixel
 constexpr int RS_KMAX_HOST = 5, RS_RPP_HOST = 2 * RS_KMAX_HOST + 2, RS_REC_HOST = RS_KMAX_HOST + 2;
-constexpr int N_RAY_COUNTS = 5;   // DevPaths::ray_counts
+constexpr int N_RAY_COUNTS = 6;   // DevPaths::ray_counts
 // timed kernel kinds: 0..2 = traversal stages (trace modes), then the others
 enum { KT_CAMERA = 3, KT_SHADE = 4, KT_RESOLVE = 5, KT_ACCUMULATE = 6, KT_COMPACT = 7, KT_RESTIR = 8, KT_SPLIT = 9,
        KT_MISS = 10, KT_SHADE_GENERIC = 11,
        // the ReSTIR DI kernels one by one (inside KT_RESTIR's span): G-buffer, presampling,
        // initial candidates, temporal / fused spatiotemporal reuse, spatial reuse
-       KT_GBUFFER = 12, KT_RS_PRESAMPLE = 13, KT_RS_INITIAL = 14, KT_RS_REUSE = 15, KT_RS_SPATIAL = 16, KT_COUNT = 17 };
+       KT_GBUFFER = 12, KT_RS_PRESAMPLE = 13, KT_RS_INITIAL = 14, KT_RS_REUSE = 15, KT_RS_SPATIAL = 16,
+       // the plain-class target-function evaluations of the staged reuse passes (k_rsp_eval<OVR, true, *>)
+       KT_RS_EVAL = 17, KT_COUNT = 18 };
 constexpr uint32_t QM_CONT = 16u;
 // mat_tex bits: a texture feeds the resolved material; the material is outside the
 // plain-dielectric class (coat, sheen, metallic, transmission or thin film may be non-zero)

@@ -2293,6 +2293,11 @@ void part_restir_override(int ovr, int kind, dim3 g, hipStream_t st, const DevSc
 // ----------------------------------------------------------------------------------
 static int blocks_for(int n) { return (n + TB - 1) / TB; }
 
+// adds a device list length to a 64-bit statistics counter (units of a timed kernel)
+__global__ void k_count_add64(uint64_t* dst, const int32_t* src) {
+    if (threadIdx.x == 0) atomicAdd((unsigned long long*)dst, (unsigned long long)(uint32_t)*src);
+}
+
 static void launch_restir_kernel(int ovr, int kind, dim3 g, hipStream_t st, const DevScene& S, const DevPaths& P,
                                  const MptFrame* F, int pass = 0, const float4* in = nullptr, float4* out = nullptr) {
     if (ovr == MPT_BSDF_NONE) part_restir_principled(kind, g, st, S, P, F, pass, in, out);
@@ -2384,7 +2389,11 @@ static void launch_spatial_pass(int ovr, bool def_bias, const MptFrame& hf, Laun
     const dim3 gp(blocks_for(P.n));
     hipMemsetAsync(&P.counters[CTR_RQ], 0, 4 * sizeof(int32_t), st);   // CTR_RQ, CTR_RQV, CTR_RQE0, CTR_RQE1
     launch_restir_kernel(ovr, RK_SP_SELECT, gp, st, S, P, d_frame, pass, in, out);
-    launch_restir_kernel(ovr, RK_SP_EVAL_PLAIN, g, st, S, P, d_frame, pass, in, out);
+    hipLaunchKernelGGL(k_count_add64, dim3(1), dim3(64), 0, st, P.ray_counts + 5, &P.counters[CTR_RQE0]);
+    {
+        TimedScope te(cfg, st, KT_RS_EVAL);
+        launch_restir_kernel(ovr, RK_SP_EVAL_PLAIN, g, st, S, P, d_frame, pass, in, out);
+    }
     launch_restir_kernel(ovr, RK_SP_EVAL_GENERIC, g, st, S, P, d_frame, pass, in, out);
     TraceArgs ta{};
     ta.S = S; ta.P = P; ta.queue = P.rq_list; ta.count_ptr = &P.counters[CTR_RQ]; ta.fetch = &P.counters[CTR_FETCH];
@@ -2415,7 +2424,11 @@ static void launch_fused_pass(int ovr, bool def_bias, const MptFrame& hf, Launch
     const dim3 gp(blocks_for(P.n));
     hipMemsetAsync(&P.counters[CTR_RQ], 0, 4 * sizeof(int32_t), st);   // CTR_RQ, CTR_RQV, CTR_RQE0, CTR_RQE1
     launch_restir_kernel(ovr, RK_ST_SELECT, gp, st, S, P, d_frame);
-    launch_restir_kernel(ovr, RK_ST_EVAL_PLAIN, g, st, S, P, d_frame);
+    hipLaunchKernelGGL(k_count_add64, dim3(1), dim3(64), 0, st, P.ray_counts + 5, &P.counters[CTR_RQE0]);
+    {
+        TimedScope te(cfg, st, KT_RS_EVAL);
+        launch_restir_kernel(ovr, RK_ST_EVAL_PLAIN, g, st, S, P, d_frame);
+    }
     launch_restir_kernel(ovr, RK_ST_EVAL_GENERIC, g, st, S, P, d_frame);
     TraceArgs ta{};
     ta.S = S; ta.P = P; ta.queue = P.rq_list; ta.count_ptr = &P.counters[CTR_RQ]; ta.fetch = &P.counters[CTR_FETCH];

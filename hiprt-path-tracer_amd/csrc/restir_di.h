@@ -57,15 +57,19 @@ DEV int xcd_block() {
 // Alpha keys (alpha_key: pass pixel seed, bounce 0, kind 5 + pass, position): the position
 // names the ray's site in the pass, not its rank among the rays traced so far, so a key does
 // not depend on which earlier rays were skipped and a pass can stage its rays (k_rsp_*).  The
-// oracle (oracle_restir.h) uses the same positions.
+// oracle (oracle_restir.h) uses the same positions.  The families occupy disjoint ranges for
+// every configuration validate_frame accepts (<= 32 reuse neighbours, so cur, j <= 33 besides
+// the 998 / 999 terms): [0, 68) neighbour pairs, 4000-4001 temporal pair, [100000, 134000)
+// GBH terms, [200000, 201000) normalisation terms, 300000 visibility reuse, 1000000 + i / 2000000
+// + i initial light / BSDF candidates.
 DEV constexpr int RP_TFC(int k) { return 2 * k; }           // neighbour k's sample at the center
 DEV constexpr int RP_TCN(int k) { return 2 * k + 1; }       // the canonical sample at neighbour k (pairwise MIS)
 constexpr int RP_T_TFC = 4000, RP_T_TCN = 4001;             // the temporal neighbour's pair
-DEV constexpr int RP_GBH(int cur, int j) { return 10000 + cur * 1000 + j; }   // j = 999 / 998: temporal / center terms
-DEV constexpr int RP_NORM(int j) { return 20000 + j; }
-DEV constexpr int RP_LIGHT(int i) { return 100 + i; }       // initial candidates: light candidate i (target visibility)
-DEV constexpr int RP_BSDF(int i) { return 200 + i; }        // initial candidates: BSDF candidate i
-constexpr int RP_VISREUSE = 30000;                          // restir_visibility_reuse
+DEV constexpr int RP_GBH(int cur, int j) { return 100000 + cur * 1000 + j; }   // j = 999 / 998: temporal / center terms
+DEV constexpr int RP_NORM(int j) { return 200000 + j; }
+DEV constexpr int RP_LIGHT(int i) { return 1000000 + i; }       // initial candidates: light candidate i (target visibility)
+DEV constexpr int RP_BSDF(int i) { return 2000000 + i; }        // initial candidates: BSDF candidate i
+constexpr int RP_VISREUSE = 300000;                          // restir_visibility_reuse
 struct RRays {
     const DevScene* S;
     uint2* lds;

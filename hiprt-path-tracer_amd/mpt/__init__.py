@@ -29,7 +29,7 @@ SYMBOLS = [
     "mpt_render_frame", "mpt_render_frames", "mpt_synchronize", "mpt_query_done", "mpt_get_framebuffer", "mpt_partition_rows",
     "mpt_enable_stats", "mpt_get_stats", "mpt_trace_closest", "mpt_trace_any", "mpt_clear_status",
     "mpt_query_status", "mpt_get_aux_buffer", "mpt_build_envmap_cdf", "mpt_set_envmap_cdf", "mpt_set_halo_exchange",
-    "mpt_bake_lut", "mpt_png_unfilter",
+    "mpt_bake_lut", "mpt_png_unfilter", "mpt_device_info",
 ]
 
 
@@ -82,6 +82,7 @@ def lib() -> C.CDLL:
     L.mpt_trace_closest.argtypes = [vp, vp, vp, i32, vp, vp, vp, vp, C.c_int]
     L.mpt_trace_any.argtypes = [vp, vp, vp, i32, vp, C.c_int]
     L.mpt_png_unfilter.argtypes = [vp, C.c_int64, vp, i32, i32, i32]
+    L.mpt_device_info.argtypes = [C.c_int, vp, i32, vp, i32, vp]
     L.mpt_build_envmap_cdf.argtypes = [vp, i32, i32, vp, vp]
     L.mpt_set_envmap_cdf.argtypes = [vp, vp, f32]
     L.mpt_clear_status.argtypes = [vp]
@@ -103,9 +104,22 @@ def _p(a):
 
 
 def abi_sizes():
-    out = np.zeros(6, np.int32)
-    _check(lib().mpt_abi_sizes(_p(out), 6))
-    return dict(zip(["Material", "RenderSettings", "WorldSettings", "Camera", "Frame", "Scene"], out.tolist()))
+    out = np.zeros(7, np.int32)
+    _check(lib().mpt_abi_sizes(_p(out), 7))
+    return dict(zip(["Material", "RenderSettings", "WorldSettings", "Camera", "Frame", "Scene", "Stats"], out.tolist()))
+
+
+def device_info(device=0):
+    """(name, gfx arch, compute units) of a HIP device (mpt_device_info)."""
+    name, arch, cus = C.create_string_buffer(256), C.create_string_buffer(64), C.c_int32()
+    _check(lib().mpt_device_info(device, name, 256, arch, 64, C.byref(cus)))
+    return name.value.decode(errors="replace"), arch.value.decode(errors="replace"), int(cus.value)
+
+
+def build_id():
+    """First 16 hex digits of the SHA-256 of the loaded libmpt.so (identifies the build a line ran)."""
+    import hashlib
+    return hashlib.sha256(open(lib()._name, "rb").read()).hexdigest()[:16]
 
 
 def partition_rows(res_y, band_height, band_index, band_count):

@@ -437,6 +437,11 @@ typedef struct MptStats {
      * reuse passes; summed time and launches */
     double restir_kernel_ms[5];
     uint32_t restir_kernel_launches[5];
+    /* the staged reuse passes' plain-class target-function evaluations (k_rsp_eval, Principled
+     * BSDF): summed time, launches and evaluation items */
+    double restir_eval_ms;
+    uint32_t restir_eval_launches;
+    uint64_t restir_eval_items;
 } MptStats;
 
 #define MPT_FB_COLOR 0        /* 'pixels': running SUM of samples (RenderData.h:34-36) */
@@ -509,8 +514,12 @@ typedef int (*MptHaloExchangeFn)(void* user, MptHaloExchange* x);
 
 const char* mpt_last_error(void);
 int mpt_version(void);
-/* sizes of the mirrored structs as compiled into the library (ABI check) */
+/* sizes of the mirrored structs as compiled into the library (ABI check): MptMaterial,
+ * MptRenderSettings, MptWorldSettings, MptCamera, MptFrame, MptScene, MptStats */
 int mpt_abi_sizes(int32_t* out_sizes, int n);
+/* The HIP device's marketing name, its gfx architecture string and compute-unit count (the
+ * bench line's device identity); any output may be NULL. */
+int mpt_device_info(int device, char* name, int32_t name_cap, char* arch, int32_t arch_cap, int32_t* out_cus);
 
 int mpt_create(int device, void* hip_stream, MptContext** out_ctx);
 int mpt_destroy(MptContext* ctx);

@@ -97,11 +97,11 @@ inline uint32_t pass_seed(const MptFrame& f, uint32_t pix, uint32_t seed) {
 inline int RP_TFC(int k) { return 2 * k; }           // neighbour k's sample at the center
 inline int RP_TCN(int k) { return 2 * k + 1; }       // the canonical sample at neighbour k (pairwise MIS)
 constexpr int RP_T_TFC = 4000, RP_T_TCN = 4001;      // the temporal neighbour's pair
-inline int RP_GBH(int cur, int j) { return 10000 + cur * 1000 + j; }   // j = 999 / 998: temporal / center terms
-inline int RP_NORM(int j) { return 20000 + j; }
-inline int RP_LIGHT(int i) { return 100 + i; }
-inline int RP_BSDF(int i) { return 200 + i; }
-constexpr int RP_VISREUSE = 30000;
+inline int RP_GBH(int cur, int j) { return 100000 + cur * 1000 + j; }   // j = 999 / 998: temporal / center terms
+inline int RP_NORM(int j) { return 200000 + j; }
+inline int RP_LIGHT(int i) { return 1000000 + i; }
+inline int RP_BSDF(int i) { return 2000000 + i; }
+constexpr int RP_VISREUSE = 300000;
 struct RestirRays {
     Ctx& c;
     int kind;

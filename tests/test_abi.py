@@ -38,6 +38,7 @@ def test_struct_sizes_match_reference_pods():
     assert lib_sizes["Camera"] == C.sizeof(abi.Camera)
     assert lib_sizes["Frame"] == C.sizeof(abi.Frame)
     assert lib_sizes["Scene"] == C.sizeof(abi.Scene)
+    assert lib_sizes["Stats"] == C.sizeof(abi.Stats)
 
 
 def test_version_and_error_reporting_without_gpu():
