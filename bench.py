@@ -167,12 +167,16 @@ def cpu_baseline(sd, luts, cam, W, H, opt, bounces, target_s, env=None, world=No
 
 
 def parity_check(r, sd, luts, cam, W, H, opt, bounces, spp, workload, env=None, world=None, alpha=False,
-                 max_s=90.0, batch=0):
+                 max_s=90.0, batch=0, history=None):
     """RMSE of the GPU's spp-sample radiance (sum / spp) against the CPU oracle on the same
     frames (the metric's "RMSE vs ref @256spp"; the oracle is the pinned CPU restatement,
     DESIGN.md §2), through the same batched path as the timed region.  Region: one 8-row
     band through the middle of the frame; C1 the whole frame; C4 whole frames (ReSTIR DI
-    reuses neighbours across the frame), as many as the oracle renders in max_s."""
+    reuses neighbours across the frame), as many as the oracle renders in max_s.
+    ReSTIR DI keeps state across samples: the GPU leg restarts at sample 0 in the TIMED context
+    (a GPURenderer::reset in a used context: the timed run's last G-buffer becomes the first
+    frame's previous one, GPURenderer.cpp:953-973), and the oracle starts from the same state:
+    the G-buffer the timed frames (`history`) leave (oracle_gbuffer_history)."""
     sys.path.insert(0, ROOT)
     from oracle import oracle as orc
     cores, _, _ = host_cores()
@@ -181,32 +185,27 @@ def parity_check(r, sd, luts, cam, W, H, opt, bounces, spp, workload, env=None, 
     bc = 1 if whole else H // BAND_H
     bi = 0 if whole else bc // 2
     band = (BAND_H, bi, bc)
-    o = orc.Oracle(sd, luts, envmap=env)
+    o = orc.Oracle(sd, luts, envmap=env, keep_state=restir)
+    t_hist = 0.0
+    if restir:
+        t0 = time.perf_counter()
+        o.gbuffer_history(history, nthreads=cores)
+        t_hist = time.perf_counter() - t0
     t0 = time.perf_counter()
     probe = o.render(frames_for(cam, W, H, opt, band, 1, bounces=bounces, world=world, alpha=alpha), nthreads=cores)
     dt1 = max(time.perf_counter() - t0, 1e-4)
     k = spp if dt1 * spp <= max_s else max(1, int(max_s / dt1))
     frs = frames_for(cam, W, H, opt, (BAND_H, 0, 1), k, bounces=bounces, world=world, alpha=alpha)
+    if k > 1 and restir:
+        o.reset_state()                     # the probe advanced the kept state: back to the timed run's
+        o.gbuffer_history(history, nthreads=cores)
     ref = o.render(frames_for(cam, W, H, opt, band, k, bounces=bounces, world=world, alpha=alpha),
                    nthreads=cores) if k > 1 else probe
     o.close()
-    own = None
-    if restir:
-        # ReSTIR DI keeps state across samples (G-buffers, reservoirs): a context fresh like
-        # the oracle's, not the timed run's (whose last G-buffer a sample-0 reset keeps as the
-        # previous frame's, as the reference's renderer would)
-        import mpt
-        own = r = mpt.GPURenderer(r.device)
-        r.set_scene(sd)
-        r.set_luts(luts)
-        if env is not None:
-            r.set_envmap(env)
     r.enable_stats(timing=False, instrumented=False)
     r.render_samples(frs, max_batch=batch)
     r.synchronize_kernel()
     gpu = r.framebuffer(abi.FB_COLOR)
-    if own is not None:
-        own.close()
     if not whole:
         gpu = gpu[bi * BAND_H:(bi + 1) * BAND_H]
     d = (gpu.astype(np.float64) - ref.astype(np.float64)) / k
@@ -214,6 +213,8 @@ def parity_check(r, sd, luts, cam, W, H, opt, bounces, spp, workload, env=None, 
             "rows": "all" if whole else f"{bi * BAND_H}-{(bi + 1) * BAND_H - 1}", "spp": k,
             "rmse": float(np.sqrt(np.mean(d * d))), "max_abs": float(np.abs(d).max()),
             "bit_exact": bool(np.array_equal(gpu, ref)), "tolerance_rmse": 1e-3,
+            "context": ("the timed run's (restarted at sample 0; the oracle from the G-buffer of the "
+                        f"{len(history)} frames the context rendered, {t_hist:.1f} s)") if restir else "the timed run's",
             "note": (None if k == spp else f"{k} of {spp} spp: the oracle's budget ({max_s:.0f} s) on the whole frame")}
 
 
@@ -333,13 +334,13 @@ def main():
     # calibration: instrumented traversal -> nodes / triangles per query per stage
     r.enable_stats(timing=False, instrumented=True)
     # (one batch, so every launch of the run has the timed region's size)
-    r.render_samples(frames_for(cam, W, H, opt, band, max(2, batch), first=0, bounces=a.bounces, world=wset, alpha=alpha),
-                     max_batch=batch)
+    cal_frames = frames_for(cam, W, H, opt, band, max(2, batch), first=0, bounces=a.bounces, world=wset, alpha=alpha)
+    r.render_samples(cal_frames, max_batch=batch)
     cal = r.stats()
     # warmup (untimed), then the timed K-frame accumulation restarting at sample 0
     r.enable_stats(timing=False, instrumented=False)
-    r.render_samples(frames_for(cam, W, H, opt, band, a.warmup, bounces=a.bounces, world=wset, alpha=alpha),
-                     max_batch=batch)
+    warm_frames = frames_for(cam, W, H, opt, band, a.warmup, bounces=a.bounces, world=wset, alpha=alpha)
+    r.render_samples(warm_frames, max_batch=batch)
     frames = frames_for(cam, W, H, opt, band, K, bounces=a.bounces, world=wset, alpha=alpha)
     r.synchronize_kernel()
     r.enable_stats(timing=True, instrumented=False)
@@ -501,7 +502,8 @@ def main():
     if rank == 0 and world == 1 and not a.no_parity:
         # the GPU leg: a fresh accumulation restarting at sample 0 (sample 0 overwrites the sums)
         parity = parity_check(r, sd, luts, cam, W, H, opt, a.bounces, K if a.workload == "c1" else a.parity_spp,
-                              a.workload, env=env, world=wset, alpha=alpha, max_s=a.parity_seconds, batch=batch)
+                              a.workload, env=env, world=wset, alpha=alpha, max_s=a.parity_seconds, batch=batch,
+                              history=cal_frames + warm_frames + frames)
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:

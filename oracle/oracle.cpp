@@ -88,6 +88,7 @@ struct OScene {
     std::vector<Tri> tris;
     std::vector<BNode> nodes;
     std::vector<int> order;
+    struct KeptState* kept = nullptr;   // oracle_keep_state: ReSTIR DI state across oracle_render calls
 };
 
 struct Bounds {
@@ -1098,6 +1099,24 @@ PixelOut path_pixel(Ctx& c, int x, int y, GB& gb) {
 
 #include "oracle_restir.h"
 
+// The state a renderer keeps between frames (GPURenderer + ReSTIRDIRenderPass): the G-buffer
+// of the last frame, the previous frame's G-buffer and the reservoir buffers with the current
+// restir_output_reservoirs.  GPURenderer::reset (GPURenderer.cpp:953-973) keeps all of them:
+// ReSTIRDIRenderPass::reset (ReSTIRDIRenderPass.cpp:228-231) only rewinds odd_frame, and
+// the first frame after it clears the reservoirs in CameraRays' reset_render
+// (CameraRays.h:19-34, 78-91) after copying the kept G-buffer into the previous-frame one, so
+// that frame's temporal reuse sees the surfaces of the frame rendered before the reset.
+// odd_frame only picks the output buffer of a temporal pass without spatial passes
+// (ReSTIRDIRenderPass.cpp:355-364); the restatement (and the GPU) alternate that buffer with the
+// last output instead, which keeps the temporal pass from writing the buffer it reads (all three
+// were just cleared, so the choice is not visible in the image).
+struct KeptState {
+    bool keep = false;
+    int W = 0, H = 0;
+    std::vector<GB> gbuf, gprev;
+    RestirBuffers B;
+};
+
 }  // namespace
 
 // ----------------------------------------------------------------------------------
@@ -1146,7 +1165,21 @@ void oracle_set_envmap_cdf(OracleScene* sc, const float* cdf, float total_sum) {
     s->env_cdf_sum = total_sum;
 }
 
-void oracle_destroy(OracleScene* s) { delete reinterpret_cast<OScene*>(s); }
+void oracle_destroy(OracleScene* sc) {
+    OScene* s = reinterpret_cast<OScene*>(sc);
+    delete s->kept;
+    delete s;
+}
+
+/* keep != 0: ReSTIR DI renders keep their state (G-buffers, reservoirs, output buffer) from one
+ * oracle_render call to the next, like one GPU renderer context; keep == 0 drops it (every call
+ * starts from a fresh renderer, the default). */
+void oracle_keep_state(OracleScene* sc, int keep) {
+    OScene* s = reinterpret_cast<OScene*>(sc);
+    delete s->kept;
+    s->kept = nullptr;
+    if (keep) { s->kept = new KeptState(); s->kept->keep = true; }
+}
 
 int oracle_trace_closest(OracleScene* sc, const float* rays, const int32_t* last_hit, int n, int32_t* prim, float* t, float* u, float* v) {
     const OScene& s = *reinterpret_cast<OScene*>(sc);
@@ -1223,10 +1256,22 @@ int oracle_render(OracleScene* sc, const MptFrame* frames, int nframes, float* s
         if ((y / f0.band_height) % f0.band_count == f0.band_index) rows.push_back(y);
     int W = f0.res_x;
     size_t npx = (size_t)W * rows.size();
-    std::vector<GB> gbuf(npx, GB{}), gprev(npx, GB{});
+    // a fresh renderer's state, or (oracle_keep_state, ReSTIR DI) the state the last call left
+    KeptState local;
+    const bool kept = restir && s.kept && s.kept->keep;
+    KeptState& K = kept ? *s.kept : local;
+    if (!kept || K.W != W || K.H != f0.res_y || K.gbuf.size() != npx) {
+        K.W = W;
+        K.H = f0.res_y;
+        K.gbuf.assign(npx, GB{});
+        K.gprev.assign(npx, GB{});
+        K.B = RestirBuffers();
+        if (restir) { K.B.init.assign(npx, OResv()); K.B.sp1.assign(npx, OResv()); K.B.sp2.assign(npx, OResv()); K.B.output = &K.B.sp1; }
+    }
+    std::vector<GB>& gbuf = K.gbuf;
+    std::vector<GB>& gprev = K.gprev;
+    RestirBuffers& B = K.B;
     std::vector<uint8_t> active(npx, 0);
-    RestirBuffers B;
-    if (restir) { B.init.assign(npx, OResv()); B.sp1.assign(npx, OResv()); B.sp2.assign(npx, OResv()); B.output = &B.sp1; }
     uint64_t rc = 0, ra = 0;
     if (nthreads <= 0) nthreads = omp_get_max_threads();
     auto make_ctx = [&](Ctx& c, const MptFrame& f) {
@@ -1376,6 +1421,61 @@ int oracle_render(OracleScene* sc, const MptFrame* frames, int nframes, float* s
         }
     }
     if (rays) { rays[0] = rc; rays[1] = ra; }
+    return 0;
+}
+
+/* The kept ReSTIR DI state a later reset-to-sample-0 run reads after `frames` were rendered,
+ * without rendering them: the G-buffer (that run's first frame clears the reservoirs and copies
+ * the G-buffer into the previous-frame one).  CameraRays writes a pixel's prim, view direction
+ * and hit flag every frame, its normals, material, first hit and volume state only on a hit
+ * (CameraRays.h:144-166; stale entries stay), so per pixel the frames are evaluated from the
+ * last one backwards until one hits.  Needs oracle_keep_state and ReSTIR DI frames without
+ * adaptive sampling (-4 otherwise); the reservoirs are left cleared. */
+int oracle_gbuffer_history(OracleScene* sc, const MptFrame* frames, int nframes, int nthreads) {
+    OScene& s = *reinterpret_cast<OScene*>(sc);
+    if (nframes <= 0) return 0;
+    const MptFrame& f0 = frames[0];
+    if (!s.kept || f0.options.direct_light_sampling != MPT_LSS_RESTIR_DI || f0.band_count != 1 ||
+        has_adaptive_buffers(f0.render_settings))
+        return -4;
+    const int W = f0.res_x, H = f0.res_y;
+    const size_t npx = (size_t)W * H;
+    KeptState& K = *s.kept;
+    if (K.W != W || K.H != H || K.gbuf.size() != npx) {
+        K.W = W;
+        K.H = H;
+        K.gbuf.assign(npx, GB{});
+        K.gprev.assign(npx, GB{});
+    }
+    K.B = RestirBuffers();
+    K.B.init.assign(npx, OResv()); K.B.sp1.assign(npx, OResv()); K.B.sp2.assign(npx, OResv()); K.B.output = &K.B.sp1;
+    if (nthreads <= 0) nthreads = omp_get_max_threads();
+#pragma omp parallel for schedule(dynamic) num_threads(nthreads)
+    for (int y = 0; y < H; y++) {
+        std::vector<Ctx> cs(nframes);
+        for (int fi = 0; fi < nframes; fi++) {
+            const MptFrame& f = frames[fi];
+            cs[fi].s = &s;
+            cs[fi].f = &f;
+            cs[fi].bc.materials = s.mats;
+            cs[fi].bc.luts = s.luts;
+            cs[fi].bc.clearcoat_compensation = f.bsdf_flags.clearcoat_compensation_approximation;
+            cs[fi].bc.ggx_masking = f.bsdf_flags.ggx_masking_shadowing;
+            cs[fi].bc.white_furnace = f.bsdf_flags.white_furnace_mode;
+            cs[fi].override_ = f.options.bsdf_override;
+            cs[fi].lss = f.options.direct_light_sampling;
+            cs[fi].alpha = f.render_settings.do_alpha_testing;
+        }
+        for (int x = 0; x < W; x++) {
+            GB& g = K.gbuf[(size_t)y * W + x];
+            for (int fi = nframes - 1; fi >= 0; fi--) {
+                GB t = g;                       // a miss leaves g's hit fields
+                camera_pixel(cs[fi], x, y, t);
+                if (fi == nframes - 1) { g.prim = t.prim; g.view = t.view; g.hit = t.hit; }
+                if (t.hit) { g.gn = t.gn; g.sn = t.sn; g.mat = t.mat; g.first_hit = t.first_hit; g.vs = t.vs; break; }
+            }
+        }
+    }
     return 0;
 }
 

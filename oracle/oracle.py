@@ -42,6 +42,8 @@ def lib():
         L.oracle_create.argtypes = [C.POINTER(abi.Scene), C.POINTER(abi.Luts), C.c_void_p, C.c_int, C.c_int,
                                     C.c_void_p, C.c_void_p, C.c_float]
         L.oracle_destroy.argtypes = [C.c_void_p]
+        L.oracle_keep_state.argtypes = [C.c_void_p, C.c_int]
+        L.oracle_gbuffer_history.argtypes = [C.c_void_p, C.POINTER(abi.Frame), C.c_int, C.c_int]
         L.oracle_set_envmap_cdf.argtypes = [C.c_void_p, C.c_void_p, C.c_float]
         L.oracle_trace_closest.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p,
                                            C.c_void_p, C.c_void_p]
@@ -70,7 +72,7 @@ def _p(a):
 class Oracle:
     """CPU oracle bound to one scene (+ LUTs, + optional envmap)."""
 
-    def __init__(self, scene_data, luts=None, envmap=None):
+    def __init__(self, scene_data, luts=None, envmap=None, keep_state=False):
         self.sd = scene_data
         self.luts = luts if luts is not None else mscene.load_luts()
         self._abi_scene = scene_data.to_abi()
@@ -87,6 +89,19 @@ class Oracle:
         if envmap is not None and envmap.get("cdf") is not None:
             self._cdf = np.ascontiguousarray(envmap["cdf"], np.float32)
             lib().oracle_set_envmap_cdf(self.h, _p(self._cdf), envmap["cdf_sum"])
+        if keep_state:
+            lib().oracle_keep_state(self.h, 1)
+
+    def gbuffer_history(self, frames, nthreads=0):
+        """Sets the kept ReSTIR DI state to what rendering `frames` leaves for a later
+        reset-to-sample-0 run: their G-buffer (oracle_gbuffer_history), without rendering them."""
+        arr = (abi.Frame * len(frames))(*frames)
+        if lib().oracle_gbuffer_history(self.h, arr, len(frames), nthreads) != 0:
+            raise RuntimeError("oracle_gbuffer_history: needs keep_state and whole-frame ReSTIR DI frames without adaptive sampling")
+
+    def reset_state(self, keep=True):
+        """Drops the kept ReSTIR DI state (a fresh renderer); keeps state from then on if keep."""
+        lib().oracle_keep_state(self.h, 1 if keep else 0)
 
     def close(self):
         if self.h:

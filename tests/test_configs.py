@@ -201,3 +201,33 @@ def test_c4_restir_batched_equals_unbatched(city, luts, city_oracle, monkeypatch
         r.close()
     _same(out["batched"], out["unbatched"], "C4 batched vs unbatched")
     assert out["batched_rays"] == out["unbatched_rays"], (out["batched_rays"], out["unbatched_rays"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fused", [True, False], ids=["fused", "unfused"])
+def test_c4_city_restir_reset_in_used_context_bit_exact(city, luts, city_oracle, fused):
+    """The C4 timed path: frames rendered, then GPURenderer::reset (sample 0, need_to_reset, the
+    seed schedule restarted) in the SAME context, whose G-buffer the first post-reset frame
+    reads as the previous frame's (GPURenderer.cpp:953-973, ReSTIRDIRenderPass.cpp:228-231,
+    CameraRays.h:78-91).  Whole 1920x1080 city frame against the oracle keeping its ReSTIR DI
+    state across the two runs; bit-exact, fused and unfused."""
+    import mpt
+    from oracle import oracle as orc
+    _, env = city_oracle
+    passes = 2 if fused else 1
+    a = c4_frames(city, 2, fused=fused, passes=passes)
+    b = c4_frames(city, 3, fused=fused, passes=passes)
+    b[0].render_settings.need_to_reset = True
+    r = _gpu(city, luts, env)
+    o = orc.Oracle(city, luts, envmap=env, keep_state=True)
+    for run in (a, b):
+        r.render_samples(run)
+        r.synchronize_kernel()
+        got = r.framebuffer(abi.FB_COLOR)
+        ref = o.render(run)
+        _same(got, ref, f"C4 {'fused' if fused else 'unfused'} colour after a reset in a used context")
+    # the state mattered: a fresh renderer's post-reset frames differ
+    o.reset_state()
+    assert not np.array_equal(o.render(b), got)
+    o.close()
+    r.close()

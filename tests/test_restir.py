@@ -146,6 +146,40 @@ def test_oracle_restir_no_visibility_reuse_temporal_bias(cornell, luts, oracle_l
     o.close()
 
 
+def _reset_run(sd, k, m, **kw):
+    """k frames, then GPURenderer::reset (GPURenderer.cpp:953-973: m_rng re-seeded 42, sample 0,
+    need_to_reset) and m frames: the second run's frames are the first run's schedule again"""
+    a = frames(sd, abi.LSS_RESTIR_DI, k, **kw)
+    b = frames(sd, abi.LSS_RESTIR_DI, m, **kw)
+    b[0].render_settings.need_to_reset = True
+    return a, b
+
+
+def test_oracle_restir_reset_keeps_g_buffer(cornell, luts, oracle_lib):
+    """A renderer reset keeps the G-buffer (ReSTIRDIRenderPass::reset only rewinds odd_frame), so
+    the first frame after it reuses the pre-reset frame's surfaces temporally: with kept state
+    the oracle's post-reset render differs from a fresh renderer's; dropping the state makes it
+    equal again.  Of the pre-reset history only the G-buffer matters (the first post-reset frame
+    clears the reservoirs): the G-buffer history alone (oracle_gbuffer_history: the pixels' camera
+    rays from the last frame backwards to the last hit, what the bench's parity leg uses for the
+    timed run) gives the same image."""
+    a, b = _reset_run(cornell, 6, 2)
+    o = oracle_lib.Oracle(cornell, luts, keep_state=True)
+    o.render(a)
+    kept = o.render(b)
+    o.reset_state()
+    fresh = o.render(b)
+    assert not np.array_equal(kept, fresh)
+    o.reset_state()
+    o.gbuffer_history(a)
+    assert np.array_equal(o.render(b), kept)
+    o.close()
+    o2 = oracle_lib.Oracle(cornell, luts)          # default: every call a fresh renderer
+    o2.render(a)
+    assert np.array_equal(o2.render(b), fresh)
+    o2.close()
+
+
 def test_oracle_restir_rejects_unsupported(cornell, luts, oracle_lib):
     o = oracle_lib.Oracle(cornell, luts)
     fr = frames(cornell, abi.LSS_RESTIR_DI, 1, band=(8, 0, 3))   # one contiguous band per context only
@@ -461,3 +495,48 @@ def test_gpu_restir_partitioned_two_processes(cornell, luts, tmp_path):
     ref = r.framebuffer(abi.FB_COLOR)
     r.close()
     assert np.array_equal(got, ref), f"{(got != ref).sum()} values differ"
+
+
+RESET_CASES = ["principled", "unfused", "unfused_temporal_only", "three_passes", "permutation_sampling", "bias_gbh",
+               "fused_mis_like", "lambert", "adaptive"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("batched", [False, True], ids=["per_frame", "batched"])
+@pytest.mark.parametrize("case", RESET_CASES + ["envmap", "alpha_cards"])
+def test_gpu_restir_reset_in_used_context_bit_exact(cornell, luts, case, batched):
+    """The ReSTIR DI state across a GPURenderer::reset in a used context (the bench's timed
+    run): k frames, then a restart at sample 0 in the same context, against the oracle keeping
+    its state across the two calls (oracle_keep_state) -- bit-exact, sample by sample and
+    through mpt_render_frames' batched samples."""
+    import mpt
+    from oracle import oracle as orc
+    sd = synthetic.with_alpha_cards(cornell) if case == "alpha_cards" else cornell
+    env = mpt.build_envmap(scene.procedural_sky(128, 64, seed=7)) if case == "envmap" else None
+    kw = dict(CASES[case]) if case in CASES else {}
+    if case == "alpha_cards":
+        kw["alpha"] = True
+    if env is not None:
+        kw["world"] = scene.envmap_world(1.0)
+    a, b = _reset_run(sd, 3, 4, **kw)
+    r = mpt.GPURenderer(0)
+    r.set_scene(sd)
+    r.set_luts(luts)
+    if env is not None:
+        r.set_envmap(env)
+    o = orc.Oracle(sd, luts, envmap=env, keep_state=True)
+    for run in (a, b):
+        if batched:
+            r.render_samples(run, max_batch=4)
+        else:
+            for f in run:
+                r.render(f)
+        r.synchronize_kernel()
+        c, ca, cn = o.render(run, aov=True)
+        g = r.framebuffer(abi.FB_COLOR)
+        assert np.array_equal(g, c), f"{case}: {(g != c).sum()} values differ"
+        assert np.array_equal(r.framebuffer(abi.FB_ALBEDO), ca)
+        assert np.array_equal(r.framebuffer(abi.FB_NORMALS), cn)
+    assert np.isfinite(g).all() and g.mean() > 0
+    o.close()
+    r.close()
