@@ -68,6 +68,19 @@ TRANS float patan2(float y, float x) { return (float)::atan2((double)y, (double)
 TRANS float pasin(float x) { return (float)::asin((double)x); }
 TRANS float pacos(float x) { return (float)::acos((double)x); }
 TRANS float2 psincos(float x) { return make_float2((float)::sin((double)x), (float)::cos((double)x)); }
+#elif defined(MPT_TRANS_FLOAT_UB)
+// A/B experiments only (not bit-exact with the oracle): the device library's float
+// functions, inline -- an upper bound of what cheaper transcendentals could gain
+#define TRANS DEV
+TRANS float psin(float x) { return ::sinf(x); }
+TRANS float pcos(float x) { return ::cosf(x); }
+TRANS float pexp(float x) { return ::expf(x); }
+TRANS float plog(float x) { return ::logf(x); }
+TRANS float ppow(float x, float y) { return ::powf(x, y); }
+TRANS float patan2(float y, float x) { return ::atan2f(y, x); }
+TRANS float pasin(float x) { return ::asinf(x); }
+TRANS float pacos(float x) { return ::acosf(x); }
+TRANS float2 psincos(float x) { float s, c; ::sincosf(x, &s, &c); return make_float2(s, c); }
 #else
 // Out of line: inlined at their ~60 call sites they push k_shade from 272 to 1072 B of
 // scratch per lane and k_trace<PATH> (the sRGB pow of the alpha test) from 4 to 3 waves/SIMD.

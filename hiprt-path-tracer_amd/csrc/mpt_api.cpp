@@ -1,6 +1,7 @@
 // mpt_api.cpp -- the C ABI of libmpt (include/mpt.h).  Owns all device memory of a
 // context (one per GPU), builds the BVH8 on scene upload, stages per-frame settings
 // and launches the wavefront frame (mpt_kernels.hip).
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -9,6 +10,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -212,6 +214,11 @@ struct MptContext {
     // raw traces
     DBuf<float4> raw_o, raw_d, raw_hit;
     DBuf<uint8_t> raw_occ;
+    // one process per GPU (mpt_comm_*): the RCCL communicator of the frame partition and the
+    // padded staging rows of mpt_comm_gather (send: this rank's rows, recv: every rank's, root)
+    void* comm = nullptr;
+    int comm_rank = 0, comm_size = 1;
+    DBuf<uint8_t> comm_send, comm_recv;
 };
 
 namespace {
@@ -852,12 +859,17 @@ int mpt_create(int device, void* hip_stream, MptContext** out) {
     return MPT_OK;
 }
 
+namespace {
+void rccl_comm_destroy(void* comm);   // (mpt_comm_init, below)
+}  // namespace
+
 // Tolerates a partially created context (mpt_create's failure path).  Every device buffer
 // is a DBuf, released by the context's destructor on the context's device.
 int mpt_destroy(MptContext* c) {
     if (!c) return MPT_OK;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->comm) rccl_comm_destroy(c->comm);
     for (int p = 0; p < 2; p++) {
         for (int i = 0; i < EV_POOL; i++)
             if (c->ev[p][i]) (void)hipEventDestroy(c->ev[p][i]);
@@ -1382,6 +1394,215 @@ int mpt_get_framebuffer(MptContext* c, int kind, float* dst, int dst_is_device) 
     HIPCHK(hipSetDevice(c->device));
     size_t bytes = 3 * (size_t)c->n_slots * sizeof(float);
     HIPCHK(hipMemcpyAsync(dst, src, bytes, dst_is_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return MPT_OK;
+}
+
+// ---------------------------------------------------------------------------------------
+// Multi-GPU output (SURVEY.md §8b Outputs row; the reference renders on one device,
+// main.cpp:57, and hands 'pixels' to OpenGL, GPURenderer.cpp:583-598).  A context holds its
+// partition's rows band-major compact: compact row r is frame row ((r / bh) * bc + bi) * bh
+// + r % bh.  Groups of bh rows therefore land at a stride of bc * bh frame rows, so one
+// strided 2D copy moves all full groups of a band and a second one the partial last group.
+// ---------------------------------------------------------------------------------------
+namespace {
+
+// element bytes and source buffer of a gather kind (MPT_FB_* or MPT_GATHER_AUX + MPT_AUX_*)
+const void* gather_src(const MptContext* c, int kind, size_t& elem) {
+    elem = 12;
+    if (kind == MPT_FB_COLOR) return c->fb_color.p;
+    if (kind == MPT_FB_ALBEDO) return c->fb_albedo.p;
+    if (kind == MPT_FB_NORMALS) return c->fb_normal.p;
+    elem = 4;
+    if (kind == MPT_GATHER_AUX + MPT_AUX_SAMPLE_COUNT) return c->as_count.p;
+    if (kind == MPT_GATHER_AUX + MPT_AUX_CONVERGED_SAMPLE_COUNT) return c->as_conv.p;
+    if (kind == MPT_GATHER_AUX + MPT_AUX_SQUARED_LUMINANCE) return c->as_sqlum.p;
+    elem = 0;
+    return nullptr;
+}
+
+// Enqueues on `st` the copies of band (bh, bi, bc)'s compact rows `src` into the frame-sized
+// row-major `dst` (rows of row_bytes).  Same-device, peer-accessible or host destinations take
+// the strided 2D copies; otherwise one peer copy per group.
+hipError_t scatter_band_rows(uint8_t* dst, const uint8_t* src, size_t row_bytes, int res_y, int bh, int bi, int bc,
+                             hipMemcpyKind kind, bool per_group, int dst_dev, int src_dev, hipStream_t st) {
+    const int full = std::max(0, (res_y / bh - bi + bc - 1) / bc);   // groups g with (g bc + bi + 1) bh <= res_y
+    const size_t gbytes = (size_t)bh * row_bytes;
+    if (per_group) {
+        for (int g = 0; g < full; g++) {
+            hipError_t e = hipMemcpyPeerAsync(dst + (size_t)(g * bc + bi) * gbytes, dst_dev, src + (size_t)g * gbytes, src_dev,
+                                              gbytes, st);
+            if (e != hipSuccess) return e;
+        }
+    } else if (full > 0) {
+        hipError_t e = hipMemcpy2DAsync(dst + (size_t)bi * gbytes, (size_t)bc * gbytes, src, gbytes, gbytes, full, kind, st);
+        if (e != hipSuccess) return e;
+    }
+    const int y0 = (full * bc + bi) * bh;   // the partial group, if this band owns it
+    if (y0 < res_y) {
+        const size_t bytes = (size_t)std::min(bh, res_y - y0) * row_bytes;
+        hipError_t e = per_group ? hipMemcpyPeerAsync(dst + (size_t)y0 * row_bytes, dst_dev, src + (size_t)full * gbytes, src_dev, bytes, st)
+                                 : hipMemcpyAsync(dst + (size_t)y0 * row_bytes, src + (size_t)full * gbytes, bytes, kind, st);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+}  // namespace
+
+int mpt_gather(MptContext* const* ctxs, int32_t n, int32_t root, int kind, void* dst, int dst_is_device) {
+    if (!ctxs || n <= 0 || !dst) return fail(MPT_ERR_INVALID_ARGUMENT, "NULL argument or n <= 0");
+    if (root < 0 || root >= n) return fail(MPT_ERR_INVALID_ARGUMENT, "root out of range");
+    std::vector<int> seen(n, 0);
+    size_t elem = 0;
+    for (int k = 0; k < n; k++) {
+        const MptContext* c = ctxs[k];
+        if (!c) return fail(MPT_ERR_INVALID_ARGUMENT, "NULL context in ctxs");
+        size_t e;
+        if (!gather_src(c, kind, e)) return fail(MPT_ERR_INVALID_ARGUMENT, "bad gather kind or no frame rendered on a context");
+        elem = e;
+        if (c->res_x != ctxs[0]->res_x || c->res_y != ctxs[0]->res_y || c->band_h != ctxs[0]->band_h || c->band_c != n)
+            return fail(MPT_ERR_INVALID_ARGUMENT, "contexts do not partition one frame into n bands (res, band_height, band_count == n)");
+        if (c->band_i < 0 || c->band_i >= n || seen[c->band_i]++) return fail(MPT_ERR_INVALID_ARGUMENT, "band indices are not 0..n-1");
+    }
+    const int dev = ctxs[root]->device;
+    const size_t row_bytes = (size_t)ctxs[0]->res_x * elem;
+    for (int k = 0; k < n; k++) {
+        MptContext* c = ctxs[k];
+        HIPCHK(hipSetDevice(c->device));
+        bool per_group = false;
+        if (dst_is_device && c->device != dev) {
+            int can = 0;
+            HIPCHK(hipDeviceCanAccessPeer(&can, c->device, dev));
+            if (can) {
+                hipError_t e = hipDeviceEnablePeerAccess(dev, 0);
+                if (e == hipErrorPeerAccessAlreadyEnabled) (void)hipGetLastError();
+                else if (e != hipSuccess) return fail(MPT_ERR_HIP, std::string("hipDeviceEnablePeerAccess: ") + hipGetErrorString(e));
+            }
+            per_group = !can;
+        }
+        size_t e;
+        const uint8_t* src = (const uint8_t*)gather_src(c, kind, e);
+        HIPCHK(scatter_band_rows((uint8_t*)dst, src, row_bytes, c->res_y, c->band_h, c->band_i, c->band_c,
+                                 dst_is_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, per_group, dev, c->device, c->stream));
+    }
+    for (int k = 0; k < n; k++) {
+        HIPCHK(hipSetDevice(ctxs[k]->device));
+        HIPCHK(hipStreamSynchronize(ctxs[k]->stream));
+    }
+    return MPT_OK;
+}
+
+// ---- one process per GPU: RCCL, loaded on first use (libmpt itself links no RCCL) -------------
+namespace {
+
+struct Rccl {
+    bool tried = false, ok = false;
+    std::string why;
+    int (*get_unique_id)(void*) = nullptr;
+    int (*comm_init_rank)(void**, int, const void*, int) = nullptr;   // ncclUniqueId passed by value: see init below
+    int (*comm_destroy)(void*) = nullptr;
+    int (*gather)(const void*, void*, size_t, int, int, void*, hipStream_t) = nullptr;
+    const char* (*error_string)(int) = nullptr;
+};
+
+Rccl* rccl_lib() {
+    static Rccl r;
+    static std::mutex mu;
+    std::lock_guard<std::mutex> lk(mu);
+    if (r.tried) return &r;
+    r.tried = true;
+    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);   // the copy torch may already have mapped
+    if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) { r.why = std::string("cannot load librccl.so.1: ") + dlerror(); return &r; }
+    r.get_unique_id = (int (*)(void*))dlsym(h, "ncclGetUniqueId");
+    r.comm_destroy = (int (*)(void*))dlsym(h, "ncclCommDestroy");
+    r.gather = (int (*)(const void*, void*, size_t, int, int, void*, hipStream_t))dlsym(h, "ncclGather");
+    r.error_string = (const char* (*)(int))dlsym(h, "ncclGetErrorString");
+    r.comm_init_rank = (int (*)(void**, int, const void*, int))dlsym(h, "ncclCommInitRank");
+    r.ok = r.get_unique_id && r.comm_destroy && r.gather && r.error_string && r.comm_init_rank;
+    if (!r.ok) r.why = "librccl.so.1 lacks ncclGetUniqueId / ncclCommInitRank / ncclGather / ncclCommDestroy";
+    return &r;
+}
+
+constexpr int NCCL_ID_BYTES = 128;   // NCCL_UNIQUE_ID_BYTES
+struct NcclId { char internal[NCCL_ID_BYTES]; };
+constexpr int NCCL_UINT8 = 1;        // ncclUint8
+
+void rccl_comm_destroy(void* comm) {
+    if (rccl_lib()->ok) (void)rccl_lib()->comm_destroy(comm);
+}
+
+int rccl_fail(int rc, const char* what) {
+    return fail(MPT_ERR_HIP, std::string(what) + ": " + (rccl_lib()->error_string ? rccl_lib()->error_string(rc) : "rccl error"));
+}
+
+}  // namespace
+
+int mpt_comm_unique_id(uint8_t* out, int32_t cap) {
+    if (!out || cap < MPT_COMM_ID_BYTES) return fail(MPT_ERR_INVALID_ARGUMENT, "out must hold MPT_COMM_ID_BYTES bytes");
+    Rccl& r = *rccl_lib();
+    if (!r.ok) return fail(MPT_ERR_UNSUPPORTED, r.why);
+    NcclId id;
+    int rc = r.get_unique_id(&id);
+    if (rc != 0) return rccl_fail(rc, "ncclGetUniqueId");
+    std::memcpy(out, id.internal, MPT_COMM_ID_BYTES);
+    return MPT_OK;
+}
+
+int mpt_comm_init(MptContext* c, int32_t nranks, int32_t rank, const uint8_t* id) {
+    if (!c || !id) return fail(MPT_ERR_INVALID_ARGUMENT, "NULL argument");
+    if (nranks <= 0 || rank < 0 || rank >= nranks) return fail(MPT_ERR_INVALID_ARGUMENT, "rank out of range");
+    if (c->comm) return fail(MPT_ERR_INVALID_ARGUMENT, "the context already has a communicator");
+    Rccl& r = *rccl_lib();
+    if (!r.ok) return fail(MPT_ERR_UNSUPPORTED, r.why);
+    HIPCHK(hipSetDevice(c->device));
+    // ncclCommInitRank takes the 128-byte ncclUniqueId by value; on x86-64 (SysV) a struct
+    // larger than 16 bytes is passed in memory, which is what this signature describes
+    NcclId nid;
+    std::memcpy(nid.internal, id, MPT_COMM_ID_BYTES);
+    auto init = (int (*)(void**, int, NcclId, int))r.comm_init_rank;
+    void* comm = nullptr;
+    int rc = init(&comm, nranks, nid, rank);
+    if (rc != 0) return rccl_fail(rc, "ncclCommInitRank");
+    c->comm = comm;
+    c->comm_rank = rank;
+    c->comm_size = nranks;
+    return MPT_OK;
+}
+
+int mpt_comm_gather(MptContext* c, int32_t root, int kind, void* dst, int dst_is_device) {
+    if (!c) return fail(MPT_ERR_INVALID_ARGUMENT, "NULL context");
+    if (!c->comm) return fail(MPT_ERR_INVALID_ARGUMENT, "no communicator (mpt_comm_init)");
+    if (root < 0 || root >= c->comm_size) return fail(MPT_ERR_INVALID_ARGUMENT, "root out of range");
+    if (c->comm_rank == root && !dst) return fail(MPT_ERR_INVALID_ARGUMENT, "NULL dst on the root");
+    size_t elem;
+    const uint8_t* src = (const uint8_t*)gather_src(c, kind, elem);
+    if (!src) return fail(MPT_ERR_INVALID_ARGUMENT, "bad gather kind or no frame rendered");
+    const int n = c->comm_size;
+    if (c->band_c != n || c->band_i != c->comm_rank)
+        return fail(MPT_ERR_INVALID_ARGUMENT, "the frame's band partition must be (band_count, band_index) = (ranks, rank)");
+    int mr = 0;
+    for (int k = 0; k < n; k++) mr = std::max(mr, rows_of(c->res_y, c->band_h, k, n));
+    const size_t row_bytes = (size_t)c->res_x * elem, part = (size_t)mr * row_bytes;
+    HIPCHK(hipSetDevice(c->device));
+    hipError_t ae = c->comm_send.alloc(part);
+    if (ae != hipSuccess) return alloc_fail(ae, "gather staging");
+    const size_t own = (size_t)c->n_slots * elem;
+    HIPCHK(hipMemcpyAsync(c->comm_send.p, src, own, hipMemcpyDeviceToDevice, c->stream));
+    if (own < part) HIPCHK(hipMemsetAsync(c->comm_send.p + own, 0, part - own, c->stream));
+    uint8_t* recv = nullptr;
+    if (c->comm_rank == root) {
+        if ((ae = c->comm_recv.alloc(part * n)) != hipSuccess) return alloc_fail(ae, "gather staging");
+        recv = c->comm_recv.p;
+    }
+    int rc = rccl_lib()->gather(c->comm_send.p, recv, part, NCCL_UINT8, root, c->comm, c->stream);
+    if (rc != 0) return rccl_fail(rc, "ncclGather");
+    if (c->comm_rank == root)
+        for (int k = 0; k < n; k++)
+            HIPCHK(scatter_band_rows((uint8_t*)dst, recv + (size_t)k * part, row_bytes, c->res_y, c->band_h, k, n,
+                                     dst_is_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, false, c->device,
+                                     c->device, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     return MPT_OK;
 }

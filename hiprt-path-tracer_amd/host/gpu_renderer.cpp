@@ -1,34 +1,100 @@
 // gpu_renderer.cpp -- see gpu_renderer.h.  Host code only; all GPU work is libmpt's.
 #include "gpu_renderer.h"
 
+#include <hip/hip_runtime_api.h>
+
+#include <algorithm>
 #include <cstring>
 #include <stdexcept>
+#include <thread>
 
 namespace mpt_host {
 
+// ---- LocalHaloGroup ------------------------------------------------------------------------
+LocalHaloGroup::LocalHaloGroup(int band_count, int band_height, std::vector<int> devices)
+    : m_n(band_count), m_bh(band_height), m_devices(std::move(devices)), m_members(band_count),
+      m_published(band_count), m_need(band_count, 0) {
+    for (int k = 0; k < m_n; k++) m_members[k] = Member{this, k};
+}
+
+void LocalHaloGroup::wait() {
+    std::unique_lock<std::mutex> lk(m_mu);
+    const unsigned gen = m_generation;
+    if (++m_arrived == m_n) {
+        m_arrived = 0;
+        m_generation++;
+        m_cv.notify_all();
+    } else {
+        m_cv.wait(lk, [&] { return m_generation != gen; });
+    }
+}
+
+int LocalHaloGroup::exchange(void* user, MptHaloExchange* x) {
+    Member* me = (Member*)user;
+    LocalHaloGroup& g = *me->group;
+    const int k = me->rank;
+    hipStream_t st = (hipStream_t)x->stream;
+    int rc = hipSetDevice(g.m_devices[k]) == hipSuccess && hipStreamSynchronize(st) == hipSuccess ? 0 : 1;   // own rows final
+    g.m_published[k] = *x;
+    g.m_need[k] = x->halo_rows;
+    g.wait();
+    if (x->phase == MPT_HALO_GBUFFER) x->halo_rows = *std::max_element(g.m_need.begin(), g.m_need.end());
+    // rows [y0 - halo, y0) and [y1, y1 + halo) of every buffer, from the bands that own them
+    const int h = x->halo_rows;
+    const int ranges[2][2] = {{std::max(0, x->own_y0 - h), x->own_y0}, {x->own_y1, std::min(x->res_y, x->own_y1 + h)}};
+    for (int p = 0; p < g.m_n && rc == 0; p++) {
+        if (p == k) continue;
+        const int p0 = std::min(x->res_y, p * g.m_bh), p1 = std::min(x->res_y, p0 + g.m_bh);
+        for (const auto& r : ranges) {
+            const int a = std::max(r[0], p0), b = std::min(r[1], p1);
+            if (a >= b) continue;
+            for (int i = 0; i < x->n_buffers && rc == 0; i++) {
+                const size_t row = (size_t)x->res_x * (size_t)x->bytes_per_pixel[i], off = (size_t)a * row;
+                rc = hipMemcpyPeerAsync((char*)x->buffers[i] + off, g.m_devices[k], (const char*)g.m_published[p].buffers[i] + off,
+                                        g.m_devices[p], (size_t)(b - a) * row, st) == hipSuccess ? 0 : 1;
+            }
+        }
+    }
+    if (hipStreamSynchronize(st) != hipSuccess) rc = 1;
+    g.wait();   // nobody overwrites rows another member is still copying
+    return rc;
+}
+
+// ---- GPURenderer -----------------------------------------------------------------------------
 void GPURenderer::check(int rc) const {
     if (rc != MPT_OK) throw std::runtime_error(std::string("libmpt: ") + mpt_last_error());
 }
 
-GPURenderer::GPURenderer(int device) {
-    check(mpt_create(device, nullptr, &m_ctx));
+GPURenderer::GPURenderer(int device) : GPURenderer(std::vector<int>{device}) {}
+
+GPURenderer::GPURenderer(const std::vector<int>& devices) : m_devices(devices) {
+    if (devices.empty()) throw std::runtime_error("GPURenderer: no device");
+    for (int d : devices) {
+        MptContext* c = nullptr;
+        int rc = mpt_create(d, nullptr, &c);
+        if (rc != MPT_OK) {
+            for (MptContext* o : m_ctxs) mpt_destroy(o);
+            check(rc);
+        }
+        m_ctxs.push_back(c);
+    }
     m_render_data.band_height = 1;
     m_render_data.band_index = 0;
     m_render_data.band_count = 1;
 }
 
 GPURenderer::~GPURenderer() {
-    if (m_ctx) mpt_destroy(m_ctx);
+    for (MptContext* c : m_ctxs) mpt_destroy(c);
 }
 
 void GPURenderer::set_scene(const MptScene& scene) {
-    check(mpt_upload_scene(m_ctx, &scene));
+    for (MptContext* c : m_ctxs) check(mpt_upload_scene(c, &scene));
     m_original_materials.assign(scene.materials, scene.materials + scene.num_materials);
     m_current_materials = m_original_materials;
 }
 
 void GPURenderer::update_materials(std::vector<MptMaterial>& materials) {
-    check(mpt_update_materials(m_ctx, materials.data(), (int32_t)materials.size()));
+    for (MptContext* c : m_ctxs) check(mpt_update_materials(c, materials.data(), (int32_t)materials.size()));
     m_current_materials = materials;
 }
 
@@ -38,19 +104,23 @@ void GPURenderer::set_envmap(const float* rgba, int width, int height, const std
     std::vector<int32_t> alias((size_t)width * height);
     float lum_sum = 0.0f, cdf_sum = 0.0f;
     check(mpt_build_alias_table(rgba, width, height, prob.data(), alias.data(), &lum_sum));
-    check(mpt_set_envmap(m_ctx, rgba, width, height, prob.data(), alias.data(), lum_sum));
     check(mpt_build_envmap_cdf(rgba, width, height, cdf.data(), &cdf_sum));
-    check(mpt_set_envmap_cdf(m_ctx, cdf.data(), cdf_sum));
+    for (MptContext* c : m_ctxs) {
+        check(mpt_set_envmap(c, rgba, width, height, prob.data(), alias.data(), lum_sum));
+        check(mpt_set_envmap_cdf(c, cdf.data(), cdf_sum));
+    }
     m_has_envmap = true;
     m_envmap_path = envmap_filepath;
 }
 
-void GPURenderer::setup_brdfs_data(const MptLuts& luts) { check(mpt_set_luts(m_ctx, &luts)); }
+void GPURenderer::setup_brdfs_data(const MptLuts& luts) {
+    for (MptContext* c : m_ctxs) check(mpt_set_luts(c, &luts));
+}
 
 void GPURenderer::resize(int width, int height) {
     m_width = width;
     m_height = height;
-    check(mpt_resize(m_ctx, width, height));
+    for (MptContext* c : m_ctxs) check(mpt_resize(c, width, height));
     m_render_data.render_settings.need_to_reset = true;   // resizing restarts the accumulation (GPURenderer::resize)
 }
 
@@ -118,17 +188,55 @@ void GPURenderer::launch_path_tracing() {
     if (!m_in_render) flush();   // a launch outside render(): enqueued on its own
 }
 
+// Band k of the context partition: interleaved 8-row bands (path tracing: every pixel's RNG
+// stream depends only on its pixel index, and interleaving balances sky against geometry), or
+// one contiguous band per context for ReSTIR DI (halo exchange, mpt.h MptHaloExchange)
+void GPURenderer::band_fields(MptFrame& f, int k) const {
+    const int n = (int)m_ctxs.size();
+    if (n == 1) { f.band_height = 1; f.band_index = 0; f.band_count = 1; return; }
+    const bool restir = f.options.direct_light_sampling == MPT_LSS_RESTIR_DI;
+    f.band_height = restir ? (f.res_y + n - 1) / n : 8;
+    f.band_index = k;
+    f.band_count = n;
+}
+
 void GPURenderer::flush() {
     if (m_pending.empty()) return;
     m_last_frames = m_pending;
     m_pending.clear();
-    check(mpt_render_frames(m_ctx, m_last_frames.data(), (int32_t)m_last_frames.size(), 0));
+    const int n = (int)m_ctxs.size();
+    if (n == 1) {
+        check(mpt_render_frames(m_ctxs[0], m_last_frames.data(), (int32_t)m_last_frames.size(), 0));
+        return;
+    }
+    // one host thread per context: a ReSTIR DI context blocks in its halo exchange until its
+    // neighbours reach the same point
+    const bool restir = m_last_frames[0].options.direct_light_sampling == MPT_LSS_RESTIR_DI;
+    const int bh = (m_height + n - 1) / n;
+    if (restir && (!m_halo || m_halo_bh != bh)) {
+        m_halo.reset(new LocalHaloGroup(n, bh, m_devices));
+        m_halo_bh = bh;
+        for (int k = 0; k < n; k++) check(mpt_set_halo_exchange(m_ctxs[k], &LocalHaloGroup::exchange, m_halo->member(k)));
+    }
+    std::vector<int> rcs(n, MPT_OK);
+    std::vector<std::string> errs(n);
+    std::vector<std::thread> th;
+    for (int k = 0; k < n; k++)
+        th.emplace_back([&, k] {
+            std::vector<MptFrame> fr = m_last_frames;
+            for (MptFrame& f : fr) band_fields(f, k);
+            rcs[k] = mpt_render_frames(m_ctxs[k], fr.data(), (int32_t)fr.size(), 0);
+            if (rcs[k] != MPT_OK) errs[k] = mpt_last_error();   // the error text is per thread
+        });
+    for (auto& t : th) t.join();
+    for (int k = 0; k < n; k++)
+        if (rcs[k] != MPT_OK) throw std::runtime_error("libmpt (band " + std::to_string(k) + "): " + errs[k]);
 }
 
 void GPURenderer::render() {
     if (!m_has_camera) throw std::runtime_error("GPURenderer::render: no camera");
     MptRenderSettings& rs = m_render_data.render_settings;
-    check(mpt_clear_status(m_ctx));   // internal_update_clear_device_status_buffers
+    for (MptContext* c : m_ctxs) check(mpt_clear_status(c));   // internal_update_clear_device_status_buffers
     map_buffers_for_render();         // GPURenderer.cpp:419
     const int spf = rs.samples_per_frame > 0 ? rs.samples_per_frame : 1;
     m_pending.clear();
@@ -153,12 +261,17 @@ void GPURenderer::render() {
     flush();
 }
 
-void GPURenderer::synchronize_kernel() { check(mpt_synchronize(m_ctx)); }
+void GPURenderer::synchronize_kernel() {
+    for (MptContext* c : m_ctxs) check(mpt_synchronize(c));
+}
 
 bool GPURenderer::frame_render_done() {
-    int done = 0;
-    check(mpt_query_done(m_ctx, &done));
-    return done != 0;
+    for (MptContext* c : m_ctxs) {
+        int done = 0;
+        check(mpt_query_done(c, &done));
+        if (!done) return false;
+    }
+    return true;
 }
 
 void GPURenderer::map_buffers_for_render() { m_mapped = true; }
@@ -167,16 +280,37 @@ void GPURenderer::unmap_buffers() {
     // the display buffers receive the sums of everything rendered so far (device-to-device
     // copies on the renderer's stream, after the frame's launches)
     if (!m_mapped) return;
-    if (m_display.color) check(mpt_get_framebuffer(m_ctx, MPT_FB_COLOR, m_display.color, 1));
-    if (m_display.albedo) check(mpt_get_framebuffer(m_ctx, MPT_FB_ALBEDO, m_display.albedo, 1));
-    if (m_display.normals) check(mpt_get_framebuffer(m_ctx, MPT_FB_NORMALS, m_display.normals, 1));
+    // (several contexts: the bands gathered onto devices[0], peer copies over xGMI)
+    if (!m_mapped) return;
+    const int n = (int)m_ctxs.size();
+    if (m_display.color) check(mpt_gather(m_ctxs.data(), n, 0, MPT_FB_COLOR, m_display.color, 1));
+    if (m_display.albedo) check(mpt_gather(m_ctxs.data(), n, 0, MPT_FB_ALBEDO, m_display.albedo, 1));
+    if (m_display.normals) check(mpt_gather(m_ctxs.data(), n, 0, MPT_FB_NORMALS, m_display.normals, 1));
     m_mapped = false;
 }
 
-void GPURenderer::copy_status_buffers() { check(mpt_query_status(m_ctx, &m_status)); }
+void GPURenderer::copy_status_buffers() {
+    // several contexts: a ray is active if one band has one; converged pixels add up
+    MptStatus all{};
+    for (MptContext* c : m_ctxs) {
+        MptStatus s{};
+        check(mpt_query_status(c, &s));
+        all.one_ray_active = all.one_ray_active || s.one_ray_active;
+        all.pixel_converged_count += s.pixel_converged_count;
+    }
+    m_status = all;
+}
 
-void GPURenderer::get_framebuffer(int kind, float* dst_rgb) { check(mpt_get_framebuffer(m_ctx, kind, dst_rgb, 0)); }
+void GPURenderer::get_framebuffer(int kind, float* dst_rgb) {
+    check(mpt_gather(m_ctxs.data(), (int32_t)m_ctxs.size(), 0, kind, dst_rgb, 0));
+}
 
-void GPURenderer::get_aux_buffer(int kind, void* dst) { check(mpt_get_aux_buffer(m_ctx, kind, dst, 0)); }
+void GPURenderer::get_aux_buffer(int kind, void* dst) {
+    if (kind >= MPT_AUX_RESTIR_OUTPUT) {   // frame-sized reservoirs: the first context's copy
+        check(mpt_get_aux_buffer(m_ctxs[0], kind, dst, 0));
+        return;
+    }
+    check(mpt_gather(m_ctxs.data(), (int32_t)m_ctxs.size(), 0, MPT_GATHER_AUX + kind, dst, 0));
+}
 
 }  // namespace mpt_host

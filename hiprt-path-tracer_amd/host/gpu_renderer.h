@@ -7,7 +7,10 @@
 #ifndef MPT_HOST_GPU_RENDERER_H
 #define MPT_HOST_GPU_RENDERER_H
 
+#include <condition_variable>
 #include <cstdint>
+#include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -39,10 +42,46 @@ struct DisplayBuffers {
     float* normals = nullptr;    // denoiser normals AOV
 };
 
+// ReSTIR DI across the row bands of several contexts of this process (mpt.h MptHaloExchange):
+// one host thread per context renders its band; at every exchange point each member
+// publishes its buffers, waits for the others, copies its halo rows from the owners (peer
+// copies between GPUs) on its own stream and waits again, so that no owner overwrites rows
+// still being read.  (mpt.partition.LocalHaloGroup is the same protocol in Python.)
+class LocalHaloGroup {
+public:
+    LocalHaloGroup(int band_count, int band_height, std::vector<int> devices);
+    // the MptHaloExchangeFn of member `rank` (user = the Member)
+    struct Member { LocalHaloGroup* group; int rank; };
+    Member* member(int rank) { return &m_members[rank]; }
+    static int exchange(void* user, MptHaloExchange* x);
+
+private:
+    void wait();   // generation barrier over the band_count members
+    int m_n, m_bh;
+    std::vector<int> m_devices;
+    std::vector<Member> m_members;
+    std::vector<MptHaloExchange> m_published;
+    std::vector<int> m_need;
+    std::mutex m_mu;
+    std::condition_variable m_cv;
+    int m_arrived = 0;
+    unsigned m_generation = 0;
+};
+
 class GPURenderer {
 public:
     // GPURenderer::GPURenderer (GPURenderer.cpp:48-86): m_rng seeded 42
     explicit GPURenderer(int device = 0);
+    // The frame tiled across several GPUs of this process (north_star: row partition + a final
+    // gather over xGMI; the reference drives one device, main.cpp:57): one libmpt context per
+    // entry of `devices` (an index may repeat: several bands on one GPU).  Context k renders
+    // band k -- interleaved 8-row bands for path tracing, one contiguous band per context plus
+    // the halo exchange for ReSTIR DI (its reuse passes read neighbouring pixels) -- each from
+    // its own host thread; map / unmap, get_framebuffer and get_aux_buffer gather the whole
+    // frame with mpt_gather onto devices[0].  Every pixel's result is bit-identical to the
+    // single-device render.  Switching between ReSTIR DI and the other strategies changes the
+    // partition, which restarts the accumulation (the reference resets on such option edits).
+    explicit GPURenderer(const std::vector<int>& devices);
     ~GPURenderer();
     GPURenderer(const GPURenderer&) = delete;
     GPURenderer& operator=(const GPURenderer&) = delete;
@@ -111,14 +150,21 @@ public:
     void get_aux_buffer(int kind, void* dst);
     int render_width() const { return m_width; }
     int render_height() const { return m_height; }
-    // the frames enqueued by the last render() / launch_path_tracing() (tests)
+    // the frames enqueued by the last render() / launch_path_tracing() (tests; band fields of
+    // the whole frame)
     const std::vector<MptFrame>& last_frames() const { return m_last_frames; }
+    int device_count() const { return (int)m_ctxs.size(); }
 
 private:
     void check(int rc) const;
     void flush();
 
-    MptContext* m_ctx = nullptr;
+    void band_fields(MptFrame& f, int k) const;
+
+    std::vector<MptContext*> m_ctxs;
+    std::vector<int> m_devices;
+    std::unique_ptr<LocalHaloGroup> m_halo;   // ReSTIR DI over several contexts
+    int m_halo_bh = 0;
     Xorshift32 m_rng{42};
     int m_width = 0, m_height = 0;
     MptFrame m_render_data{};

@@ -29,7 +29,8 @@ SYMBOLS = [
     "mpt_render_frame", "mpt_render_frames", "mpt_synchronize", "mpt_query_done", "mpt_get_framebuffer", "mpt_partition_rows",
     "mpt_enable_stats", "mpt_get_stats", "mpt_trace_closest", "mpt_trace_any", "mpt_clear_status",
     "mpt_query_status", "mpt_get_aux_buffer", "mpt_build_envmap_cdf", "mpt_set_envmap_cdf", "mpt_set_halo_exchange",
-    "mpt_bake_lut", "mpt_png_unfilter", "mpt_device_info",
+    "mpt_bake_lut", "mpt_png_unfilter", "mpt_device_info", "mpt_gather", "mpt_comm_unique_id", "mpt_comm_init",
+    "mpt_comm_gather", "mpt_jpeg_decode", "mpt_hdr_decode",
 ]
 
 
@@ -90,6 +91,12 @@ def lib() -> C.CDLL:
     L.mpt_get_aux_buffer.argtypes = [vp, C.c_int, vp, C.c_int]
     L.mpt_set_halo_exchange.argtypes = [vp, abi.HaloExchangeFn, vp]
     L.mpt_bake_lut.argtypes = [vp, C.c_int, i32, i32, i32, i32, vp, C.c_int]
+    L.mpt_gather.argtypes = [C.POINTER(vp), i32, i32, C.c_int, vp, C.c_int]
+    L.mpt_comm_unique_id.argtypes = [vp, i32]
+    L.mpt_comm_init.argtypes = [vp, i32, i32, vp]
+    L.mpt_comm_gather.argtypes = [vp, i32, C.c_int, vp, C.c_int]
+    L.mpt_jpeg_decode.argtypes = [vp, C.c_int64, i32, vp, C.c_int64, vp, vp, vp]
+    L.mpt_hdr_decode.argtypes = [vp, C.c_int64, i32, vp, C.c_int64, vp, vp]
     _lib = L
     return L
 
@@ -124,6 +131,33 @@ def build_id():
 
 def partition_rows(res_y, band_height, band_index, band_count):
     return lib().mpt_partition_rows(res_y, band_height, band_index, band_count)
+
+
+GATHER_AUX = 16   # mpt.h MPT_GATHER_AUX: gather kind of an MPT_AUX_* buffer
+
+
+def _gather_out(f, kind):
+    if kind >= GATHER_AUX:
+        return np.zeros((f.res_y, f.res_x), np.float32 if kind == GATHER_AUX + abi.AUX_SQUARED_LUMINANCE else np.int32)
+    return np.zeros((f.res_y, f.res_x, 3), np.float32)
+
+
+def gather(renderers, root=0, kind=abi.FB_COLOR):
+    """mpt_gather: the whole frame of buffer `kind` from the renderers that render the row
+    partitions band_index = 0..n-1 of one frame (one process; peer copies between GPUs) ->
+    host array [res_y, res_x(, 3)]."""
+    f = renderers[root].frame
+    out = _gather_out(f, kind)
+    hs = (C.c_void_p * len(renderers))(*[r.h for r in renderers])
+    _check(lib().mpt_gather(hs, len(renderers), root, kind, _p(out), 0))
+    return out
+
+
+def comm_unique_id() -> bytes:
+    """mpt_comm_unique_id (rank 0; share the bytes with the other ranks out of band)."""
+    buf = (C.c_uint8 * 128)()
+    _check(lib().mpt_comm_unique_id(buf, 128))
+    return bytes(buf)
 
 
 def build_envmap(rgba):
@@ -254,6 +288,18 @@ class GPURenderer:
 
     def framebuffer_to_device(self, kind, dev_ptr: int):
         _check(lib().mpt_get_framebuffer(self.h, kind, C.c_void_p(dev_ptr), 1))
+
+    # --- one process per GPU (RCCL, mpt_comm_*) ----------------------------------------
+    def comm_init(self, nranks: int, rank: int, uid: bytes):
+        buf = (C.c_uint8 * 128).from_buffer_copy(uid)
+        _check(lib().mpt_comm_init(self.h, nranks, rank, buf))
+        self.comm_rank = rank
+
+    def comm_gather(self, root=0, kind=abi.FB_COLOR):
+        """mpt_comm_gather (collective): the whole frame on the root (host array), None elsewhere."""
+        out = _gather_out(self.frame, kind)
+        _check(lib().mpt_comm_gather(self.h, root, kind, _p(out), 0))
+        return out if self.comm_rank == root else None
 
     # --- status buffers / adaptive sampling (GPURenderer.cpp:269-283) ---------------
     def clear_status_buffers(self):

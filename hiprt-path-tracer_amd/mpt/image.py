@@ -1,7 +1,17 @@
-"""8-bit texture decoding for the glTF loader: the reference's ``Image8Bit::read_image``
-(src/Image/Image.cpp:33-61) = ``stbi_load(path, &w, &h, &n, output_channels)`` without a
-vertical flip, restated for PNG with the standard library's zlib and libmpt's scanline
-filter reversal (``mpt_png_unfilter``, csrc/image.cpp).
+"""Image decoding for the scene and envmap loaders, with the semantics of the decoder the
+reference compiles (stb_image, thirdparties/stbi/stb_image.h):
+
+* textures: ``Image8Bit::read_image`` (src/Image/Image.cpp:33-61) = ``stbi_load(path, &w, &h,
+  &n, output_channels)`` without a vertical flip -- PNG restated here with the standard
+  library's zlib and libmpt's scanline filter reversal (``mpt_png_unfilter``, csrc/image.cpp),
+  JPEG by libmpt's restatement of stb_image's decoder (``mpt_jpeg_decode``, csrc/jpeg.cpp);
+* envmaps and the baked LUTs: ``Image32Bit::read_image_hdr`` (Image.cpp:342-370) =
+  ``stbi_loadf`` with ``flipY`` -- Radiance .hdr by ``mpt_hdr_decode`` (csrc/jpeg.cpp); an 8-bit
+  file through ``stbi_loadf`` becomes ``pow(v / 255, 2.2)`` (alpha ``v / 255``).
+  ``load_envmap`` is ``RendererEnvmap``'s read (RendererEnvmap.cpp:39-48: 4 channels, flipped).
+
+Every decode is pinned byte for byte (float for float) against the reference's own stb_image.h
+compiled from its sources (oracle/_ref, tests/golden/images, tests/test_image_decode.py).
 
 What stb_image does and this module restates:
 * every PNG colour type (grey, RGB, palette, grey + alpha, RGBA), bit depths 1/2/4/8/16,
@@ -12,8 +22,8 @@ What stb_image does and this module restates:
   replicates, RGB -> grey is ``(77 r + 150 g + 29 b) >> 8`` (stbi__compute_y), a missing
   alpha is 255, an unwanted alpha is dropped.
 
-Other formats (JPEG, TGA, ...) raise ``ValueError``: the loader names the texture and fails
-loudly rather than rendering a different scene.
+Other formats (TGA, BMP, DDS, ...) raise ``ValueError``: the loader names the texture and
+fails loudly rather than rendering a different scene.
 """
 from __future__ import annotations
 
@@ -135,13 +145,82 @@ def convert_channels(img: np.ndarray, n: int) -> np.ndarray:
     return np.ascontiguousarray(out.astype(np.uint8))
 
 
+def is_jpeg(data: bytes) -> bool:
+    return data[:2] == b"\xff\xd8"
+
+
+def is_hdr(data: bytes) -> bool:
+    return data.startswith(b"#?RADIANCE\n") or data.startswith(b"#?RGBE\n")
+
+
+def decode_jpeg(data: bytes, channels: int = 0) -> np.ndarray:
+    """JPEG bytes -> uint8 [h, w, n] (n = channels, or the file's 3 / 1), stbi_load's bytes."""
+    import ctypes as C
+    from . import _check, lib
+    buf = np.frombuffer(data, np.uint8)
+    w, h, comp = C.c_int32(), C.c_int32(), C.c_int32()
+    _check(lib().mpt_jpeg_decode(buf.ctypes.data, len(buf), channels, None, 0, C.byref(w), C.byref(h), C.byref(comp)))
+    n = channels or (3 if comp.value >= 3 else 1)
+    out = np.empty((h.value, w.value, n), np.uint8)
+    _check(lib().mpt_jpeg_decode(buf.ctypes.data, len(buf), channels, out.ctypes.data, out.size, C.byref(w), C.byref(h),
+                                 C.byref(comp)))
+    return out
+
+
+def decode_hdr(data: bytes, channels: int = 0) -> np.ndarray:
+    """Radiance .hdr bytes -> float32 [h, w, n] (n = channels or 3), rows as stored."""
+    import ctypes as C
+    from . import _check, lib
+    buf = np.frombuffer(data, np.uint8)
+    w, h = C.c_int32(), C.c_int32()
+    _check(lib().mpt_hdr_decode(buf.ctypes.data, len(buf), channels, None, 0, C.byref(w), C.byref(h)))
+    out = np.empty((h.value, w.value, channels or 3), np.float32)
+    _check(lib().mpt_hdr_decode(buf.ctypes.data, len(buf), channels, out.ctypes.data, out.size, C.byref(w), C.byref(h)))
+    return out
+
+
+def _kind(data: bytes) -> str:
+    head = data[:4]
+    return "DDS" if head == b"DDS " else "TGA/BMP/other"
+
+
 def read_image(data: bytes, channels: int) -> np.ndarray:
-    """Image8Bit::read_image(path, channels, flipY = false) on the file's bytes."""
+    """Image8Bit::read_image(path, channels, flipY = false) on the file's bytes (stbi_load)."""
     if data[:8] == PNG_SIG:
         return convert_channels(decode_png(data), channels)
-    head = data[:4]
-    kind = "JPEG" if head[:3] == b"\xff\xd8\xff" else "DDS" if head == b"DDS " else "unknown"
-    raise ValueError(f"texture format {kind} is not supported (PNG only)")
+    if is_jpeg(data):
+        return decode_jpeg(data, channels)
+    raise ValueError(f"texture format {_kind(data)} is not supported (PNG and JPEG)")
+
+
+def read_image_hdr(data: bytes, channels: int, flip_y: bool = True) -> np.ndarray:
+    """Image32Bit::read_image_hdr(path, channels, flipY) on the file's bytes (stbi_loadf): float32
+    [h, w, channels], the rows flipped when flip_y (stbi_set_flip_vertically_on_load)."""
+    if is_hdr(data):
+        img = decode_hdr(data, channels)
+    elif data[:8] == PNG_SIG or is_jpeg(data):
+        # stbi__ldr_to_hdr: colour channels pow(v / 255, 2.2) * 1 in double, alpha v / 255
+        ldr = read_image(data, channels).astype(np.float32)
+        img = np.empty(ldr.shape, np.float32)
+        n = channels if channels & 1 else channels - 1
+        img[..., :n] = (np.power((ldr[..., :n] / np.float32(255.0)).astype(np.float64), float(np.float32(2.2)))
+                        * float(np.float32(1.0))).astype(np.float32)
+        if n < channels:
+            img[..., n:] = ldr[..., n:] / np.float32(255.0)
+    else:
+        raise ValueError(f"image format {_kind(data)} is not supported by read_image_hdr (.hdr, PNG, JPEG)")
+    return np.ascontiguousarray(img[::-1]) if flip_y else img
+
+
+def load_envmap(path) -> np.ndarray:
+    """The envmap as RendererEnvmap reads it (RendererEnvmap.cpp:39-48 -> ThreadFunctions::read_envmap,
+    ThreadFunctions.cpp:145-151): read_image_hdr(path, 4, flipY = true) -> float32 [h, w, 4], the
+    input of mpt.build_envmap.  (.exr envmaps, read by tinyexr in the reference, are not supported.)"""
+    path = str(path)
+    if path.endswith(".exr"):
+        raise ValueError("OpenEXR envmaps are not supported (use .hdr)")
+    with open(path, "rb") as f:
+        return read_image_hdr(f.read(), 4, True)
 
 
 def to_rgba8(img: np.ndarray) -> np.ndarray:

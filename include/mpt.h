@@ -570,6 +570,29 @@ int mpt_query_done(MptContext* ctx, int* out_done);
  * rows owned by this context in increasing y) to dst; dst may be host or device. */
 int mpt_get_framebuffer(MptContext* ctx, int kind, float* dst, int dst_is_device);
 int mpt_partition_rows(int32_t res_y, int32_t band_height, int32_t band_index, int32_t band_count);
+/* Multi-GPU output (SURVEY.md §8b Outputs row; GPURenderer.cpp:583-598 hands the one device's
+ * 'pixels' to the display).  n contexts render the n row partitions of one frame (MptFrame
+ * band_count == n, band_index 0..n-1, one band_height, same resolution; each on its own GPU or
+ * several on one).  mpt_gather assembles buffer `kind` of the whole frame, row-major
+ * (res_y x res_x), into dst on ctxs[root]'s device (dst_is_device) or in host memory: every
+ * context's compact rows go out on its own stream (after its frames) as strided 2D copies --
+ * peer copies over xGMI when the devices differ.  One host process drives all contexts.
+ * Synchronous.  kind: MPT_FB_* (3 floats per pixel) or MPT_GATHER_AUX + MPT_AUX_SAMPLE_COUNT /
+ * _CONVERGED_SAMPLE_COUNT / _SQUARED_LUMINANCE (4 bytes per pixel). */
+#define MPT_GATHER_AUX 16
+int mpt_gather(MptContext* const* ctxs, int32_t n, int32_t root, int kind, void* dst, int dst_is_device);
+/* One process per GPU: an RCCL communicator over the ranks of the partition (loaded from
+ * librccl.so.1 on first use).  Rank 0 calls mpt_comm_unique_id and shares the id out of band;
+ * every rank then calls mpt_comm_init on its context (ncclCommInitRank, collective).
+ * mpt_comm_gather is collective over the ranks: rank k's frames must carry band_count = ranks,
+ * band_index = k; each rank's compact rows (padded to the largest band) travel with one
+ * ncclGather over xGMI to the root, which re-interleaves them into dst (row-major frame; device
+ * or host).  dst is ignored on the other ranks.  The communicator is destroyed with the
+ * context.  Synchronous. */
+#define MPT_COMM_ID_BYTES 128
+int mpt_comm_unique_id(uint8_t* out_id, int32_t cap);
+int mpt_comm_init(MptContext* ctx, int32_t nranks, int32_t rank, const uint8_t* id);
+int mpt_comm_gather(MptContext* ctx, int32_t root, int kind, void* dst, int dst_is_device);
 /* Status buffers: mpt_clear_status <- GPURenderer::internal_update_clear_device_status_buffers
  * (GPURenderer.cpp:275-283, once per displayed frame); the last sample of the frame sets
  * render_settings.do_update_status_buffers; mpt_query_status <- copy_status_buffers (.cpp:269-273). */
@@ -614,6 +637,21 @@ int mpt_trace_any(MptContext* ctx, const float* rays, const int32_t* last_hit, i
  * (rounded up to 1).  No context, no GPU. */
 int mpt_png_unfilter(const uint8_t* filtered, int64_t filtered_size, uint8_t* out, int32_t rows, int32_t row_bytes,
                      int32_t bpp);
+/* JPEG decode with stb_image's semantics (stbi_load in Image8Bit::read_image, Image.cpp:33-61: the
+ * reference's textured scene ships JPEG textures): baseline / extended / progressive Huffman,
+ * 1 / 3 / 4 components, any integer sampling ratio; the islow integer IDCT, the 2:1 triangle
+ * upsampling and fixed-point YCbCr conversion of stb_image's x86-64 build, bit for bit.
+ * req_comp 0 = the file's own (3 for colour, 1 for grey), else 1..4.  out = NULL: only the
+ * header is read (w, h, the file's component count); else out_cap >= w * h * n bytes, rows top
+ * to bottom.  No context, no GPU. */
+int mpt_jpeg_decode(const uint8_t* data, int64_t size, int32_t req_comp, uint8_t* out, int64_t out_cap,
+                    int32_t* out_w, int32_t* out_h, int32_t* out_comp);
+/* Radiance .hdr (RGBE, flat or RLE scanlines) decode with stbi_loadf's semantics
+ * (Image32Bit::read_image_hdr, Image.cpp:342-370: envmaps, RendererEnvmap.cpp:39-48, and the
+ * baked LUTs, GPURenderer.cpp:122-170): float = mantissa * 2^(e - 136), req_comp 1 / 2 average the
+ * three channels, alpha 1.  out = NULL: dimensions only.  Rows top to bottom (the caller flips). */
+int mpt_hdr_decode(const uint8_t* data, int64_t size, int32_t req_comp, float* out, int64_t out_cap,
+                   int32_t* out_w, int32_t* out_h);
 
 #ifdef __cplusplus
 }

@@ -4,7 +4,8 @@
 //   blob mode 0: RenderWindow's loop (update() then render()); mode 1: the same samples through
 //   the three launches called one by one (launch_camera_rays / launch_ReSTIR_DI /
 //   launch_path_tracing, the driver doing render()'s per-sample bookkeeping).  M2 > 0:
-//   update_materials with the blob's edited materials before rendering.  The colour comes back
+//   update_materials with the blob's edited materials before rendering.  N_SPLIT > 1: the
+//   multi-device renderer with N_SPLIT row bands (contexts on device 0), gathered by mpt_gather.  The colour comes back
 //   through the display-buffer path (map_buffers_for_render / unmap_buffers into hipMalloc'd
 //   destinations, as an OpenGL interop map would hand them over) and is checked against
 //   get_framebuffer; the per-pixel sample counts are returned for the test.
@@ -45,7 +46,7 @@ int main(int argc, char** argv) {
         const auto camera = r.get<MptCamera>();
         const int W = r.get<int32_t>(), H = r.get<int32_t>(), n_updates = r.get<int32_t>();
         const int T = r.get<int32_t>(), V = r.get<int32_t>(), M = r.get<int32_t>(), E = r.get<int32_t>();
-        const int mode = r.get<int32_t>(), M2 = r.get<int32_t>();
+        const int mode = r.get<int32_t>(), M2 = r.get<int32_t>(), n_split = r.get<int32_t>();
         auto idx = r.arr<int32_t>(3 * (size_t)T);
         auto pos = r.arr<float>(3 * (size_t)V);
         auto nrm = r.arr<float>(3 * (size_t)V);
@@ -60,7 +61,9 @@ int main(int argc, char** argv) {
         auto mats2 = r.arr<MptMaterial>((size_t)M2);
         fclose(fin);
 
-        mpt_host::GPURenderer gr(0);
+        // n_split > 1: the frame tiled across n_split contexts (here all on device 0), gathered
+        // with mpt_gather
+        mpt_host::GPURenderer gr(std::vector<int>(n_split > 1 ? n_split : 1, 0));
         MptScene s{};
         s.triangle_indices = idx.data(); s.num_triangles = T;
         s.vertices = pos.data(); s.vertex_normals = nrm.data(); s.has_vertex_normals = has_n.data();

@@ -82,7 +82,12 @@ def test_stb_channel_conversion():
 
 
 def test_unsupported_format_fails_loudly():
-    with pytest.raises(ValueError, match="JPEG"):
+    """Formats the loader does not decode (DDS, TGA, ...) and corrupt JPEGs raise; JPEG itself is
+    decoded (tests/test_image_decode.py pins it against the reference's stb_image)."""
+    import mpt
+    with pytest.raises(ValueError, match="DDS"):
+        image.read_image(b"DDS " + b"\0" * 16, 4)
+    with pytest.raises(mpt.MptError, match="jpeg"):
         image.read_image(b"\xff\xd8\xff\xe0" + b"\0" * 16, 4)
 
 

@@ -21,13 +21,13 @@ from mpt import _build, abi, scene
 W, H = 48, 32
 
 
-def _blob(path, sd, luts, settings, world, options, camera, n_updates, mode=0, mats2=()):
+def _blob(path, sd, luts, settings, world, options, camera, n_updates, mode=0, mats2=(), split=1):
     with open(path, "wb") as f:
         f.write(struct.pack("<I", 0x4254504D))
         for s in (settings, world, options, abi.BSDFFlags.default(), camera):
             f.write(bytes(s))
         T, V = sd.num_triangles, len(sd.vertices)
-        f.write(struct.pack("<9i", W, H, n_updates, T, V, len(sd.materials), len(sd.emissive), mode, len(mats2)))
+        f.write(struct.pack("<10i", W, H, n_updates, T, V, len(sd.materials), len(sd.emissive), mode, len(mats2), split))
         f.write(np.ascontiguousarray(sd.triangle_indices, np.int32).tobytes())
         for a, t in ((sd.vertices, np.float32), (sd.normals, np.float32), (sd.has_normals, np.uint8),
                      (sd.texcoords, np.float32), (sd.material_indices, np.int32)):
@@ -64,6 +64,12 @@ CASES = {
     "split_launches_mis": dict(lss=abi.LSS_MIS_LIGHT_BSDF, spf=2, updates=2, mode=1),
     "split_launches_restir": dict(lss=abi.LSS_RESTIR_DI, spf=1, updates=3, mode=1),
     "update_materials_ris": dict(lss=abi.LSS_RIS_BSDF_AND_LIGHT, spf=2, updates=2, edit=True),
+    # the frame tiled across contexts (GPURenderer(devices), here all on device 0) + mpt_gather:
+    # interleaved 8-row bands for path tracing, contiguous bands + halo exchange for ReSTIR DI
+    "split2_mis": dict(lss=abi.LSS_MIS_LIGHT_BSDF, spf=4, updates=2, split=2),
+    "split3_ris_split_launches": dict(lss=abi.LSS_RIS_BSDF_AND_LIGHT, spf=2, updates=2, mode=1, split=3),
+    "split2_restir_fused": dict(lss=abi.LSS_RESTIR_DI, spf=2, updates=2, split=2),
+    "split3_restir_unfused": dict(lss=abi.LSS_RESTIR_DI, spf=1, updates=3, fused=False, split=3),
 }
 
 
@@ -97,7 +103,8 @@ def test_cpp_gpurenderer_matches_oracle(cornell, luts, tmp_path, case):
     cam = scene.make_camera(cornell.camera_info, W, H)
     blob, out = tmp_path / "in.blob", tmp_path / "out.bin"
     mats2 = _edited(cornell) if c.get("edit") else []
-    _blob(blob, cornell, luts, st, abi.WorldSettings.default(), opt, cam, c["updates"], c.get("mode", 0), mats2)
+    _blob(blob, cornell, luts, st, abi.WorldSettings.default(), opt, cam, c["updates"], c.get("mode", 0), mats2,
+          c.get("split", 1))
     r = subprocess.run([str(_build.HOST_TEST), str(blob), str(out)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     frames, img, cnt = _read_out(out)
