@@ -40,6 +40,7 @@ import json
 import math
 import os
 import struct
+import warnings
 
 import numpy as np
 
@@ -144,20 +145,63 @@ def _node_matrix(n):
     return m
 
 
-def _accessor(g, bins, idx):
-    a = g["accessors"][idx]
-    bv = g["bufferViews"][a["bufferView"]]
-    dt = np.dtype(_COMP[a["componentType"]])
-    n = _NCOMP[a["type"]]
-    off = bv.get("byteOffset", 0) + a.get("byteOffset", 0)
+def _view(g, bins, view_idx, byte_offset, dt, cnt, n):
+    """cnt elements of n components of dtype dt from a bufferView (honouring byteStride)."""
+    bv = g["bufferViews"][view_idx]
+    off = bv.get("byteOffset", 0) + byte_offset
     stride = bv.get("byteStride", 0)
     buf = bins[bv["buffer"]]
-    cnt = a["count"]
     if stride and stride != n * dt.itemsize:
-        arr = np.ndarray((cnt, n), dt, buf, off, (stride, dt.itemsize))
+        return np.array(np.ndarray((cnt, n), dt, buf, off, (stride, dt.itemsize)))
+    return np.frombuffer(buf, dt, cnt * n, off).reshape(cnt, n).copy()
+
+
+# glTF 2.0 §3.11 (accessor.normalized): integer components as fractions of their range
+_NORM = {np.dtype(np.uint8): 255.0, np.dtype(np.int8): 127.0, np.dtype(np.uint16): 65535.0, np.dtype(np.int16): 32767.0}
+
+
+def _accessor(g, bins, idx):
+    """An accessor as [count, components]: its bufferView data (zeros without one), the sparse
+    substitutions applied (glTF 2.0 §3.6.2.3), and, for a normalized integer accessor
+    (KHR_mesh_quantization positions / normals / texcoords), the components mapped to [0, 1] or
+    [-1, 1] (§3.11: c / 255, max(c / 127, -1), c / 65535, max(c / 32767, -1)) as float32."""
+    a = g["accessors"][idx]
+    dt = np.dtype(_COMP[a["componentType"]])
+    n = _NCOMP[a["type"]]
+    cnt = a["count"]
+    if "bufferView" in a:
+        arr = _view(g, bins, a["bufferView"], a.get("byteOffset", 0), dt, cnt, n)
     else:
-        arr = np.frombuffer(buf, dt, cnt * n, off).reshape(cnt, n)
-    return np.array(arr)
+        arr = np.zeros((cnt, n), dt)
+    sp = a.get("sparse")
+    if sp:
+        k = sp["count"]
+        ii, vv = sp["indices"], sp["values"]
+        where = _view(g, bins, ii["bufferView"], ii.get("byteOffset", 0), np.dtype(_COMP[ii["componentType"]]), k, 1).ravel()
+        arr[where.astype(np.int64)] = _view(g, bins, vv["bufferView"], vv.get("byteOffset", 0), dt, k, n)
+    if a.get("normalized") and dt in _NORM:
+        f = arr.astype(np.float32) / np.float32(_NORM[dt])
+        return np.maximum(f, np.float32(-1.0)) if dt.kind == "i" else f
+    return arr
+
+
+def _triangles(mode, idx):
+    """A primitive's index list as triangles: TRIANGLES as they are, TRIANGLE_STRIP with every
+    other triangle's first two vertices swapped (one winding) and TRIANGLE_FAN around its first
+    vertex -- what ASSIMP's glTF 2 importer builds before the reference reads the faces
+    (SceneParser.cpp:151-165 takes three indices per face; glTF 2.0 §3.7.2.1)."""
+    n = len(idx)
+    if mode == 4:
+        return idx[: n - n % 3].reshape(-1, 3)
+    if n < 3:
+        return np.zeros((0, 3), np.int64)
+    i = np.arange(n - 2)
+    if mode == 5:
+        odd = (i % 2) == 1
+        a = np.where(odd, idx[i + 1], idx[i])
+        b = np.where(odd, idx[i], idx[i + 1])
+        return np.stack([a, b, idx[i + 2]], 1)
+    return np.stack([np.full(n - 2, idx[0]), idx[i + 1], idx[i + 2]], 1)   # mode 6: fan
 
 
 def _material_from_gltf(gm, tex=None):
@@ -350,7 +394,11 @@ def load_gltf(path, aspect_override=None):
         R = M[:3, :3]
         RIT = np.linalg.inv(R).T
         for prim in g["meshes"][n["mesh"]]["primitives"]:
-            if prim.get("mode", 4) != 4:
+            mode = prim.get("mode", 4)
+            if mode not in (4, 5, 6):
+                # points / lines have no surface: ASSIMP hands them over as 1- or 2-index faces,
+                # which the reference's three-index face loop (SceneParser.cpp:151-165) reads past
+                warnings.warn(f"{os.path.basename(path)}: mesh {n['mesh']}: primitive mode {mode} (points / lines) skipped")
                 continue
             att = prim["attributes"]
             pos = _accessor(g, bins, att["POSITION"]).astype(np.float64)
@@ -369,7 +417,7 @@ def load_gltf(path, aspect_override=None):
             if mi is None:
                 need_default = True
                 mi = n_mat
-            inst.append((mi, pos, nrm, uv, idx.reshape(-1, 3)))
+            inst.append((mi, pos, nrm, uv, _triangles(mode, idx)))
 
     total_mats = n_mat + (1 if need_default else 0)
     tex_idx, const_em, textures, tex_count = _load_textures(g, bins, base, materials_json)
