@@ -941,7 +941,11 @@ __global__ void k_emissive_table(DevScene S, float4* tab) {
 #endif
 DEV v3 sample_emissive_triangle(const DevScene& S, Rng& rng, float& pdf, LightInfo& li) {
     int ri = rng.random_index(S.n_emissive);
+#ifdef MPT_UB_LOCAL_GATHERS   // A/B experiments only (not bit-exact): every sample reads a cache-resident record
+    const float4* e = S.em_tab + 5 * (size_t)(ri & 63);
+#else
     const float4* e = S.em_tab + 5 * (size_t)ri;
+#endif
     float4 e0 = e[0], e1 = e[1], e2 = e[2], e3 = e[3], e4 = e[4];
     float r1 = rng(), r2 = rng();
     float sr1 = sqrtf(r1);
@@ -965,7 +969,11 @@ DEV Col clamp_contrib(Col c, float mx, bool cond) { return (!has_nan(c) && mx > 
 DEV Col env_tex(const DevScene& S, const MptFrame& F, v2 uv) {
     float u = wrap01(uv.x), v = 1.0f - wrap01(uv.y);
     int x = (int)(u * (float)(S.env_w - 1)), y = (int)(v * (float)(S.env_h - 1));
+#ifdef MPT_UB_LOCAL_GATHERS
+    float4 p = S.env[(x + (size_t)y * S.env_w) & 4095];
+#else
     float4 p = S.env[x + (size_t)y * S.env_w];
+#endif
     return col(p.x, p.y, p.z) * F.world_settings.envmap_intensity;
 }
 DEV Col eval_env_no_pdf(const DevScene& S, const MptFrame& F, v3 d) {
@@ -1003,7 +1011,11 @@ DEV Col env_sample(const DevScene& S, const MptFrame& F, v3& dir, float& pdf, Rn
         env_cdf_search(S, rng() * S.env_cdf_sum, x, y);
     } else {
         int ri = rng.random_index(S.env_h * S.env_w);
+#ifdef MPT_UB_LOCAL_GATHERS
+        const int2 e = S.alias[ri & 4095];
+#else
         const int2 e = S.alias[ri];   // one 8-B load: probability bits + alias index
+#endif
         if (rng() > __int_as_float(e.x)) ri = e.y;
         y = (int)((unsigned)ri / (unsigned)S.env_w);
         x = ri - y * S.env_w;
