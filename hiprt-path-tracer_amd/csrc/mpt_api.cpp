@@ -144,6 +144,7 @@ struct MptContext {
     DBuf<float> lut_conductor, lut_glossy, lut_glass, lut_glass_inv, lut_thin, lut_sheen;
     DBuf<float4> env;
     DBuf<int2> alias;
+    DBuf<float4> env_rich;                // alias entries with their radiance texels (launch_env_rich)
     DBuf<float> env_cdf;
     float env_cdf_sum = 0.0f;
     int env_w = 0, env_h = 0;
@@ -258,6 +259,7 @@ DevScene dev_scene(MptContext* c) {
     S.lut_sheen = c->lut_sheen.p;
     S.env = c->env.p;
     S.alias = c->alias.p;
+    S.env_rich = c->env_rich.p;
     S.env_w = c->env_w;
     S.env_h = c->env_h;
     S.env_sum = c->env_sum;
@@ -1037,7 +1039,7 @@ int mpt_set_envmap(MptContext* c, const float* rgba, int32_t w, int32_t h, const
     if (!c) return fail(MPT_ERR_INVALID_ARGUMENT, "NULL context");
     HIPCHK(hipSetDevice(c->device));
     if (!rgba || w <= 0 || h <= 0) {
-        c->env.release(); c->alias.release(); c->env_cdf.release();
+        c->env.release(); c->alias.release(); c->env_cdf.release(); c->env_rich.release();
         c->env_w = c->env_h = 0;
         return MPT_OK;
     }
@@ -1058,9 +1060,16 @@ int mpt_set_envmap(MptContext* c, const float* rgba, int32_t w, int32_t h, const
     }
     HIPCHK(c->env.upload(reinterpret_cast<const float4*>(rgba), n, c->stream));
     HIPCHK(c->alias.upload(pa.data(), n, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
     c->env_w = w;
     c->env_h = h;
+    {
+        hipError_t e = c->env_rich.alloc(2 * n);
+        if (e != hipSuccess) return alloc_fail(e, "envmap alias entries");
+        DevScene S = dev_scene(c);
+        S.env_rich = nullptr;
+        HIPCHK(launch_env_rich(S, c->env_rich.p, c->stream));
+    }
+    HIPCHK(hipStreamSynchronize(c->stream));
     c->env_sum = lsum;
     c->env_cdf.release();   // a new envmap invalidates a previous CDF
     return MPT_OK;

@@ -59,6 +59,10 @@ struct DevScene {
     // envmap
     const float4* env;
     const int2* alias;            // alias table, one entry per texel: (probability bits, alias index)
+    // the alias table with the radiance texels its sampler reads (k_env_rich): per texel i two
+    // float4 {probability, alias index bits, rgb(i)}, {rgb(alias(i))}, rgb(j) = the texel env_tex
+    // reads for a sample at texel j -- one 32-B gather per envmap sample instead of two dependent
+    const float4* env_rich;
     int32_t env_w, env_h;
     float env_sum;
     const float* env_cdf;         // ESS_BINARY_SEARCH: running luminance sum per texel (Image.cpp:553-574)
@@ -305,6 +309,7 @@ hipError_t launch_restir_fill_lights(float4* lights, int n, hipStream_t st);
 hipError_t launch_bake(int kind, int w, int h, int d, int ipk, int nb_samples, int iteration, float* out, hipStream_t st);
 hipError_t launch_tri_attr(const DevScene& S, float4* out, hipStream_t st);
 hipError_t launch_srgb_table(float* out, hipStream_t st);
+hipError_t launch_env_rich(const DevScene& S, float4* out, hipStream_t st);
 hipError_t launch_trace_raw(const DevScene& S, const float4* o, const float4* d, int n, bool any, float4* out_hit,
                             uint8_t* out_occ, int32_t* fetch_ctr, uint32_t* spill, int grid, hipStream_t st);
 

@@ -939,37 +939,81 @@ __global__ void k_emissive_table(DevScene S, float4* tab) {
 }
 
 #endif
-DEV v3 sample_emissive_triangle(const DevScene& S, Rng& rng, float& pdf, LightInfo& li) {
-    int ri = rng.random_index(S.n_emissive);
-#ifdef MPT_UB_LOCAL_GATHERS   // A/B experiments only (not bit-exact): every sample reads a cache-resident record
+// uniform_sample_one_emissive_triangle in three parts, so that a caller can load a later
+// sample's record early: the index draw, the record (one 80-byte load), the rest of the draws
+struct EmRec { float4 e0, e1, e2, e3, e4; };
+DEV int emissive_index(const DevScene& S, Rng& rng) { return rng.random_index(S.n_emissive); }
+DEV EmRec emissive_record(const DevScene& S, int ri) {
+#if defined(MPT_UB_LOCAL_GATHERS) && (MPT_UB_LOCAL_GATHERS & 1)   // A/B experiments only (not bit-exact): cache-resident records
     const float4* e = S.em_tab + 5 * (size_t)(ri & 63);
 #else
     const float4* e = S.em_tab + 5 * (size_t)ri;
 #endif
-    float4 e0 = e[0], e1 = e[1], e2 = e[2], e3 = e[3], e4 = e[4];
+    EmRec r;
+    r.e0 = e[0]; r.e1 = e[1]; r.e2 = e[2]; r.e3 = e[3]; r.e4 = e[4];
+    return r;
+}
+DEV v3 emissive_point(const DevScene& S, const EmRec& r, Rng& rng, float& pdf, LightInfo& li) {
     float r1 = rng(), r2 = rng();
     float sr1 = sqrtf(r1);
     float u = 1.0f - sr1, v = (1.0f - r2) * sr1;
-    v3 A = mk3(e0.x, e0.y, e0.z), AB = mk3(e1.x, e1.y, e1.z), AC = mk3(e2.x, e2.y, e2.z);
+    v3 A = mk3(r.e0.x, r.e0.y, r.e0.z), AB = mk3(r.e1.x, r.e1.y, r.e1.z), AC = mk3(r.e2.x, r.e2.y, r.e2.z);
     v3 pt = A + AB * u + AC * v;
     li.tri = -1; li.normal = mk3(0.0f, 1.0f, 0.0f); li.area = 1.0f; li.emission = col(0.0f);
-    if (e3.w == 0.0f) { pdf = 0.0f; return mk3(0.0f, 0.0f, 0.0f); }
-    li.tri = __float_as_int(e0.w);
-    li.normal = mk3(e3.x, e3.y, e3.z);
-    li.area = e1.w;
-    li.emission = col(e4.x, e4.y, e4.z);
+    if (r.e3.w == 0.0f) { pdf = 0.0f; return mk3(0.0f, 0.0f, 0.0f); }
+    li.tri = __float_as_int(r.e0.w);
+    li.normal = mk3(r.e3.x, r.e3.y, r.e3.z);
+    li.area = r.e1.w;
+    li.emission = col(r.e4.x, r.e4.y, r.e4.z);
     pdf = 1.0f / li.area;
     pdf /= (float)S.n_emissive;
     return pt;
 }
+DEV v3 sample_emissive_triangle(const DevScene& S, Rng& rng, float& pdf, LightInfo& li) {
+    const int ri = emissive_index(S, rng);
+    return emissive_point(S, emissive_record(S, ri), rng, pdf, li);
+}
+// A light sample's record loaded ahead of its draws: valid for the RNG state `state` (the one
+// its index draw starts from), so a prediction that the draws then do not meet is just unused
+struct EmPrefetch {
+    uint32_t state;
+    bool valid;
+    EmRec r;
+    DEV void issue(const DevScene& S, Rng at) {
+        state = at.s;
+        valid = true;
+        r = emissive_record(S, emissive_index(S, at));
+    }
+    // sample_emissive_triangle from rng, with the prefetched record when it is the right one
+    DEV v3 sample(const DevScene& S, Rng& rng, float& pdf, LightInfo& li) {
+        const bool hit = valid && state == rng.s;
+        const int ri = emissive_index(S, rng);
+        valid = false;
+        return emissive_point(S, hit ? r : emissive_record(S, ri), rng, pdf, li);
+    }
+};
 DEV bool min_contrib(float mn, Col c) { return mn > 0.0f ? !(c.r < mn && c.g < mn && c.b < mn) : true; }
 DEV Col clamp_contrib(Col c, float mx, bool cond) { return (!has_nan(c) && mx > 0.0f && cond) ? clampc(c, -mx, mx) : c; }
 
 // envmap (Envmap.h)
+// the texel index env_tex reads at uv (Envmap.h: wrapped, v flipped, truncated)
+DEV size_t env_tex_index(const DevScene& S, v2 uv) {
+    float u = wrap01(uv.x), v = 1.0f - wrap01(uv.y);
+    int x = (int)(u * (float)(S.env_w - 1)), y = (int)(v * (float)(S.env_h - 1));
+    return (size_t)x + (size_t)y * S.env_w;
+}
+// the uv env_sample derives from the sampled texel index (its radiance lookup)
+DEV v2 env_sample_uv(const DevScene& S, int ri, float& u, float& v) {
+    const int y = (int)((unsigned)ri / (unsigned)S.env_w);
+    const int x = ri - y * S.env_w;
+    u = (float)x / (float)(unsigned)S.env_w;
+    v = (float)y / (float)(unsigned)S.env_h;
+    return mk2(u, 1.0f - v);
+}
 DEV Col env_tex(const DevScene& S, const MptFrame& F, v2 uv) {
     float u = wrap01(uv.x), v = 1.0f - wrap01(uv.y);
     int x = (int)(u * (float)(S.env_w - 1)), y = (int)(v * (float)(S.env_h - 1));
-#ifdef MPT_UB_LOCAL_GATHERS
+#if defined(MPT_UB_LOCAL_GATHERS) && (MPT_UB_LOCAL_GATHERS & 2)
     float4 p = S.env[(x + (size_t)y * S.env_w) & 4095];
 #else
     float4 p = S.env[x + (size_t)y * S.env_w];
@@ -1007,11 +1051,32 @@ DEV float env_total(const DevScene& S, const MptFrame& F) {
 }
 DEV Col env_sample(const DevScene& S, const MptFrame& F, v3& dir, float& pdf, Rng& rng) {
     int x, y;
+    if (F.options.envmap_sampling != MPT_ESS_BINARY_SEARCH && S.env_rich) {
+        // alias table with the texels (one 32-B gather): the same draws, texel and arithmetic
+        // as the two-load path below
+        int ri = rng.random_index(S.env_h * S.env_w);
+        const float4 a = S.env_rich[2 * (size_t)ri], b = S.env_rich[2 * (size_t)ri + 1];
+        Col tex;
+        if (rng() > a.x) { ri = __float_as_int(a.y); tex = col(b.y, b.z, b.w); }
+        else tex = col(a.z, a.w, b.x);
+        float u, v;
+        env_sample_uv(S, ri, u, v);
+        float phi = u * TWO_PI;
+        float theta = maxr(1.0e-5f, v * PI);
+        const float2 sct = psincos(theta), scp = psincos(phi);
+        float ct = sct.y, st = sct.x;
+        dir = mat_x_vec(F.world_settings.envmap_to_world_matrix.m, mk3(-st * scp.y, -ct, -st * scp.x));
+        Col rad = tex * F.world_settings.envmap_intensity;
+        pdf = lum(rad) / (env_total(S, F) * F.world_settings.envmap_intensity);
+        pdf *= (float)((unsigned)S.env_w * (unsigned)S.env_h);
+        pdf /= (TWO_PIPI * st);
+        return rad;
+    }
     if (F.options.envmap_sampling == MPT_ESS_BINARY_SEARCH) {
         env_cdf_search(S, rng() * S.env_cdf_sum, x, y);
     } else {
         int ri = rng.random_index(S.env_h * S.env_w);
-#ifdef MPT_UB_LOCAL_GATHERS
+#if defined(MPT_UB_LOCAL_GATHERS) && (MPT_UB_LOCAL_GATHERS & 2)
         const int2 e = S.alias[ri & 4095];
 #else
         const int2 e = S.alias[ri];   // one 8-B load: probability bits + alias index
@@ -1027,6 +1092,22 @@ DEV Col env_sample(const DevScene& S, const MptFrame& F, v3& dir, float& pdf, Rn
     float ct = sct.y, st = sct.x;
     dir = mat_x_vec(F.world_settings.envmap_to_world_matrix.m, mk3(-st * scp.y, -ct, -st * scp.x));
     Col rad = env_tex(S, F, mk2(u, 1.0f - v));
+    pdf = lum(rad) / (env_total(S, F) * F.world_settings.envmap_intensity);
+    pdf *= (float)((unsigned)S.env_w * (unsigned)S.env_h);
+    pdf /= (TWO_PIPI * st);
+    return rad;
+}
+// env_eval in two halves, so that a shading kernel can issue the texel load before a BSDF
+// evaluation and consume it after: env_fetch = eval_env_no_pdf's texel, env_eval_tex the rest
+DEV float4 env_fetch(const DevScene& S, const MptFrame& F, v3 d) {
+    v3 r = mat_x_vec(F.world_settings.world_to_envmap_matrix.m, d);
+    float u = 0.5f + patan2(r.z, r.x) * INV_2_PI;
+    float v = 0.5f + pasin(r.y) * INV_PI;
+    return S.env[env_tex_index(S, mk2(u, 1.0f - v))];
+}
+DEV Col env_eval_tex(const DevScene& S, const MptFrame& F, v3 d, float4 p, float& pdf) {
+    Col rad = col(p.x, p.y, p.z) * F.world_settings.envmap_intensity;
+    float st = psin(pacos(-d.y));
     pdf = lum(rad) / (env_total(S, F) * F.world_settings.envmap_intensity);
     pdf *= (float)((unsigned)S.env_w * (unsigned)S.env_h);
     pdf /= (TWO_PIPI * st);
@@ -1469,6 +1550,13 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_
             // ds_read per field per evaluation (-23% k_shade time on C3)
             __shared__ PEval pe_lds[TB];
             PEval& pe = pe_lds[threadIdx.x];
+            // the first light sample's emissive record, loaded while the per-vertex BSDF terms are
+            // computed (its index is the vertex's next draw); each RIS light candidate then loads
+            // the next one's record (the draws between them are fixed: two for the point, one for
+            // the reservoir) while it is evaluated
+            EmPrefetch pf;
+            pf.valid = false;
+            if (op == OP_RIS_LIGHT || op == OP_MIS_LIGHT || op == OP_UNI_LIGHT) pf.issue(S, rng);
             SECT(0);
             bsdf_eval_pre<OVR, CLS>(bc, m, vs, view, sn, pe);
             SECT(5);
@@ -1495,10 +1583,18 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_
                 v3 lp = mk3(0.0f, 0.0f, 0.0f);
                 Col ec = col(0.0f);
                 bool inner = false;
+                float4 etex = make_float4(0.0f, 0.0f, 0.0f, 0.0f);   // OP_ENV_BSDF: the envmap texel along L
                 if (op == OP_RIS_BSDF || op == OP_MIS_BSDF || op == OP_BSDF_LIGHT || op == OP_ENV_BSDF || op == OP_CONT) {
                     do_eval = bsdf_sample_dir<OVR, CLS>(bc, m, tv, view, sn, gn, L, rng);
+                    // the texel's load is issued here and waited for after the evaluation
+                    if (op == OP_ENV_BSDF && do_eval) etex = env_fetch(S, F, L);
                 } else if (op == OP_RIS_LIGHT) {
-                    lp = sample_emissive_triangle(S, rng, lpdf, li);
+                    lp = pf.sample(S, rng, lpdf, li);
+                    if (ris_c + 1 < nl) {   // the next candidate's index draw follows this one's reservoir draw
+                        Rng nx = rng;
+                        (void)nx();
+                        pf.issue(S, nx);
+                    }
                     if (lpdf > 0.0f) {
                         v3 tl = lp - ep;
                         dist = length(tl);
@@ -1524,7 +1620,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_
                     do_eval = hasW && ism != 1.0f;
                 } else if (op == OP_MIS_LIGHT || op == OP_UNI_LIGHT) {
                     // sample_one_light_MIS (Lights.h:115-220) / _no_MIS (Lights.h:22-65)
-                    lp = sample_emissive_triangle(S, rng, lpdf, li);
+                    lp = pf.sample(S, rng, lpdf, li);
                     if (lpdf > 0.0f) {
                         v3 so = op == OP_MIS_LIGHT ? ep : ip + sn * 1.0e-4f;
                         v3 sd = lp - so;
@@ -1684,7 +1780,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_
                     float c2 = absr(dot(sn, L));
                     if (pdf > 0.0f) {
                         float epdf;
-                        Col er = env_eval(S, F, L, epdf);
+                        Col er = env_eval_tex(S, F, L, etex, epdf);
                         if (epdf > 0.0f && env_use) {
                             float mw = balance(pdf, epdf);
                             const Col e2 = er * mw * c2 * f / pdf;
@@ -2903,6 +2999,21 @@ hipError_t launch_resolve_materials(const DevScene& S, MptMaterial* out_res, int
 __global__ void k_srgb_table(float* out) {
     const int v = threadIdx.x;
     out[v] = ppow((float)v / 255.0f, 2.2f);
+}
+__global__ void k_env_rich(DevScene S, float4* out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= S.env_w * S.env_h) return;
+    const int2 e = S.alias[i];
+    float u, v;
+    const float4 p = S.env[env_tex_index(S, env_sample_uv(S, i, u, v))];
+    const float4 q = S.env[env_tex_index(S, env_sample_uv(S, e.y, u, v))];
+    out[2 * (size_t)i] = make_float4(__int_as_float(e.x), __int_as_float(e.y), p.x, p.y);
+    out[2 * (size_t)i + 1] = make_float4(p.z, q.x, q.y, q.z);
+}
+hipError_t launch_env_rich(const DevScene& S, float4* out, hipStream_t st) {
+    const int n = S.env_w * S.env_h;
+    hipLaunchKernelGGL(k_env_rich, dim3((n + 255) / 256), dim3(256), 0, st, S, out);
+    return hipGetLastError();
 }
 hipError_t launch_srgb_table(float* out, hipStream_t st) {
     hipLaunchKernelGGL(k_srgb_table, dim3(1), dim3(256), 0, st, out);
