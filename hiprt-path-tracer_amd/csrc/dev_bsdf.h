@@ -76,7 +76,7 @@ DEV VState vs_default() {
     return v;
 }
 DEV VState vs_load(const uint4* A, const uint4* B, int i) {
-    uint4 a = A[i], b = B[i];
+    uint4 a = ld_s(A + i), b = ld_s(B + i);
     VState v;
     v.st[0] = a.x; v.st[1] = a.y; v.st[2] = a.z;
     v.pos = (int)(a.w & 3u);
@@ -86,8 +86,8 @@ DEV VState vs_load(const uint4* A, const uint4* B, int i) {
     return v;
 }
 DEV void vs_store(uint4* A, uint4* B, int i, const VState& v) {
-    A[i] = make_uint4(v.st[0], v.st[1], v.st[2], (uint32_t)v.pos | ((uint32_t)v.inside << 2));
-    B[i] = make_uint4((uint32_t)v.incident, (uint32_t)v.outgoing, __float_as_uint(v.dist), __float_as_uint(v.wl));
+    st_s(A + i, make_uint4(v.st[0], v.st[1], v.st[2], (uint32_t)v.pos | ((uint32_t)v.inside << 2)));
+    st_s(B + i, make_uint4((uint32_t)v.incident, (uint32_t)v.outgoing, __float_as_uint(v.dist), __float_as_uint(v.wl)));
 }
 DEV uint32_t& vs_entry(VState& v, int i) {   // constant-index friendly access
     return i == 0 ? v.st[0] : (i == 1 ? v.st[1] : v.st[2]);

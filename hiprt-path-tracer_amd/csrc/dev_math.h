@@ -101,6 +101,63 @@ TRANS float pasin(float x) { return tmath::asinf_(x); }
 TRANS float pacos(float x) { return tmath::acosf_(x); }
 #endif
 
+// Streaming path state -- written by one wavefront stage and read once by the next (rays,
+// hits, throughput, NEE records, staged queries): non-temporal accesses (the 'nt' bit: L2
+// evict-first) so that the data every path re-reads -- the emissive-triangle table, materials,
+// the envmap alias entries, BVH nodes -- stays in the XCDs' L2 instead of being pushed out by
+// ~15 GB of path state per shading launch.  Same values either way.
+#ifndef MPT_NT_STREAM
+#define MPT_NT_STREAM 1
+#endif
+typedef float nt_f4 __attribute__((ext_vector_type(4)));
+typedef unsigned nt_u4 __attribute__((ext_vector_type(4)));
+DEV float4 ld_s(const float4* p) {
+#if MPT_NT_STREAM
+    const nt_f4 x = __builtin_nontemporal_load(reinterpret_cast<const nt_f4*>(p));
+    return make_float4(x.x, x.y, x.z, x.w);
+#else
+    return *p;
+#endif
+}
+DEV void st_s(float4* p, float4 v) {
+#if MPT_NT_STREAM
+    const nt_f4 x = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(x, reinterpret_cast<nt_f4*>(p));
+#else
+    *p = v;
+#endif
+}
+DEV uint4 ld_s(const uint4* p) {
+#if MPT_NT_STREAM
+    const nt_u4 x = __builtin_nontemporal_load(reinterpret_cast<const nt_u4*>(p));
+    return make_uint4(x.x, x.y, x.z, x.w);
+#else
+    return *p;
+#endif
+}
+DEV void st_s(uint4* p, uint4 v) {
+#if MPT_NT_STREAM
+    const nt_u4 x = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(x, reinterpret_cast<nt_u4*>(p));
+#else
+    *p = v;
+#endif
+}
+template <typename T> DEV T ld_s(const T* p) {
+#if MPT_NT_STREAM
+    return __builtin_nontemporal_load(p);
+#else
+    return *p;
+#endif
+}
+template <typename T> DEV void st_s(T* p, T v) {
+#if MPT_NT_STREAM
+    __builtin_nontemporal_store(v, p);
+#else
+    *p = v;
+#endif
+}
+
 constexpr float PI = 3.14159265358979323846f;
 constexpr float TWO_PI = 6.28318530717958647693f;
 constexpr float INV_PI = 0.31830988618379067154f;

@@ -444,8 +444,8 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MODE == TM_P
                     float4 ro, rd;
                     if (MODE == TM_PATH) {
                         ray = A.queue ? A.queue[i] : i;   // no queue: every slot (batched ReSTIR DI camera rays)
-                        ro = P.ray_o[ray];
-                        rd = P.ray_d[ray];
+                        ro = ld_s(&P.ray_o[ray]);
+                        rd = ld_s(&P.ray_d[ray]);
                         skips = 0;
                         was_inside = false;
                         if (A.alpha)     // bounce 0: the camera launch's seed (CameraRays traces the camera ray)
@@ -459,8 +459,8 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MODE == TM_P
                         if (A.ext) ray = MODE == TM_NEE_LIGHT_OCC ? P.xl_light[i] : MODE == TM_NEE_ANY ? P.xl_any[i] : P.xl_cl[i];
                         else ray = MODE == TM_NEE_LIGHT_OCC ? P.nq_light[i]
                                                             : P.nq_tgt[MODE == TM_NEE_ANY ? (size_t)i : (size_t)P.n * 3 + i];
-                        ro = A.ext ? P.xq_o[ray] : P.nq_o[nq_index(P, ray)];
-                        rd = A.ext ? P.xq_d[ray] : P.nq_d[nq_index(P, ray)];
+                        ro = A.ext ? P.xq_o[ray] : ld_s(&P.nq_o[nq_index(P, ray)]);
+                        rd = A.ext ? P.xq_d[ray] : ld_s(&P.nq_d[nq_index(P, ray)]);
                         qmax = rd.w;
                         const bool al = A.alpha != 0;
                         uint32_t akey = 0u;
@@ -521,13 +521,13 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MODE == TM_P
                         A.alpha ? alpha_key(pseed, A.bounce, 0, skips) : 0u);
                 continue;
             }
-            P.ray_o[ray] = make_float4(tr.o.x, tr.o.y, tr.o.z, __uint_as_float((uint32_t)tr.last_hit));
-            P.hit[ray] = make_float4(tr.best, tr.bu, tr.bv, __uint_as_float((uint32_t)(found ? tr.bprim : -1)));
-            P.hit_inside[ray] = was_inside ? 1 : 0;
-            P.hit_cls[ray] = found ? (uint8_t)tr.bcls : (uint8_t)0xffu;
+            st_s(&P.ray_o[ray], make_float4(tr.o.x, tr.o.y, tr.o.z, __uint_as_float((uint32_t)tr.last_hit)));
+            st_s(&P.hit[ray], make_float4(tr.best, tr.bu, tr.bv, __uint_as_float((uint32_t)(found ? tr.bprim : -1))));
+            st_s(&P.hit_inside[ray], (uint8_t)(was_inside ? 1 : 0));
+            st_s(&P.hit_cls[ray], found ? (uint8_t)tr.bcls : (uint8_t)0xffu);
         } else if (MODE == TM_NEE_ANY) {
             if (A.ext) P.xq_occ[ray] = found ? 1 : 0;
-            else P.occ[nq_index(P, ray)] = found ? 1 : 0;
+            else st_s(&P.occ[nq_index(P, ray)], (uint8_t)(found ? 1 : 0));
         } else if (MODE == TM_NEE_CLOSEST || MODE == TM_NEE_LIGHT) {
             // evaluate_shadow_light_ray: a hit counts only below t_max - 1e-4 (Intersect.h:337-343)
             bool ok = found && tr.best < qmax;
@@ -941,6 +941,12 @@ __global__ void k_emissive_table(DevScene S, float4* tab) {
 #endif
 // uniform_sample_one_emissive_triangle in three parts, so that a caller can load a later
 // sample's record early: the index draw, the record (one 80-byte load), the rest of the draws
+#ifndef MPT_EM_PREFETCH   // A/B switches of the shading kernel's early loads (see EmPrefetch, env_fetch)
+#define MPT_EM_PREFETCH 0
+#endif
+#ifndef MPT_ENV_EARLY
+#define MPT_ENV_EARLY 0
+#endif
 struct EmRec { float4 e0, e1, e2, e3, e4; };
 DEV int emissive_index(const DevScene& S, Rng& rng) { return rng.random_index(S.n_emissive); }
 DEV EmRec emissive_record(const DevScene& S, int ri) {
@@ -1129,8 +1135,8 @@ DEV Col env_eval(const DevScene& S, const MptFrame& F, v3 d, float& pdf) {
 // return value would wait for all of the lane's outstanding stores).
 DEV void stage_query(const DevPaths& P, int slot, int kind, uint32_t& qm, v3 o, int last_hit, v3 d, float tmax) {
     const size_t e = (size_t)kind * (size_t)P.nq_stride + (size_t)slot;
-    P.nq_o[e] = make_float4(o.x, o.y, o.z, __uint_as_float((uint32_t)last_hit));
-    P.nq_d[e] = make_float4(d.x, d.y, d.z, tmax);
+    st_s(&P.nq_o[e], make_float4(o.x, o.y, o.z, __uint_as_float((uint32_t)last_hit)));
+    st_s(&P.nq_d[e], make_float4(d.x, d.y, d.z, tmax));
     qm |= 1u << kind;
 }
 
@@ -1427,15 +1433,16 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_
     bool cont = false;   // continuation ray emitted
     SECT_BEGIN();
     if (valid) {
-        float4 ro = P.ray_o[slot], rdv = P.ray_d[slot], hv = P.hit[slot];
+        float4 ro = ld_s(&P.ray_o[slot]), rdv = ld_s(&P.ray_d[slot]), hv = ld_s(&P.hit[slot]);
         v3 o = mk3(ro.x, ro.y, ro.z), d = mk3(rdv.x, rdv.y, rdv.z);
         int prim = (int)__float_as_uint(hv.w);
         bool found = prim >= 0;
         VState vs = vs_load(P.vsA, P.vsB, slot);
-        Rng rng = make_rng(P.rng[slot]);
-        Col thr = col(P.thr[slot].x, P.thr[slot].y, P.thr[slot].z);
+        Rng rng = make_rng(ld_s(&P.rng[slot]));
+        const float4 thv = ld_s(&P.thr[slot]);
+        Col thr = col(thv.x, thv.y, thv.z);
         const Col thr_vertex = thr;        // the NEE terms' throughput (k_resolve)
-        float4 cv = P.col[slot];
+        float4 cv = ld_s(&P.col[slot]);
         Col rcol = col(cv.x, cv.y, cv.z);
         v3 ip = mk3(0, 0, 0), gn = mk3(0, 0, 0), sn = mk3(0, 0, 0);
         // The material is read through a pointer (L1/L2-resident) instead of being held in
@@ -1513,7 +1520,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_
                 if (m.emissive_texture_used && bounce > 0) {
                     fl |= NF_IMM;
                     const Col e = emission_of(m);
-                    P.na[slot] = make_float4(e.r, e.g, e.b, 0.0f);
+                    st_s(&P.na[slot], make_float4(e.r, e.g, e.b, 0.0f));
                 }
             }
             do_light = do_light && lss != MPT_LSS_NO_DIRECT_LIGHT_SAMPLING;
@@ -1556,7 +1563,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_
             // the reservoir) while it is evaluated
             EmPrefetch pf;
             pf.valid = false;
-            if (op == OP_RIS_LIGHT || op == OP_MIS_LIGHT || op == OP_UNI_LIGHT) pf.issue(S, rng);
+            if (MPT_EM_PREFETCH && (op == OP_RIS_LIGHT || op == OP_MIS_LIGHT || op == OP_UNI_LIGHT)) pf.issue(S, rng);
             SECT(0);
             bsdf_eval_pre<OVR, CLS>(bc, m, vs, view, sn, pe);
             SECT(5);
@@ -1587,10 +1594,10 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_
                 if (op == OP_RIS_BSDF || op == OP_MIS_BSDF || op == OP_BSDF_LIGHT || op == OP_ENV_BSDF || op == OP_CONT) {
                     do_eval = bsdf_sample_dir<OVR, CLS>(bc, m, tv, view, sn, gn, L, rng);
                     // the texel's load is issued here and waited for after the evaluation
-                    if (op == OP_ENV_BSDF && do_eval) etex = env_fetch(S, F, L);
+                    if (MPT_ENV_EARLY && op == OP_ENV_BSDF && do_eval) etex = env_fetch(S, F, L);
                 } else if (op == OP_RIS_LIGHT) {
                     lp = pf.sample(S, rng, lpdf, li);
-                    if (ris_c + 1 < nl) {   // the next candidate's index draw follows this one's reservoir draw
+                    if (MPT_EM_PREFETCH && ris_c + 1 < nl) {   // the next candidate's index draw follows this one's reservoir draw
                         Rng nx = rng;
                         (void)nx();
                         pf.issue(S, nx);
@@ -1687,18 +1694,18 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_
                     if (pdf > 0.0f) {
                         fl |= NF_B | (refr ? NF_B_REFR : 0u);
                         stage_query(P, slot, 3, qm, so, prim, L, 1.0e35f - 1.0e-4f);
-                        P.nb[slot] = make_float4(f.r, f.g, f.b, pdf);
-                        P.ndir[slot] = make_float4(L.x, L.y, L.z, absr(dot(sn, L)));
+                        st_s(&P.nb[slot], make_float4(f.r, f.g, f.b, pdf));
+                        st_s(&P.ndir[slot], make_float4(L.x, L.y, L.z, absr(dot(sn, L))));
                     }
                     r_add = rng();
                     next = OP_RIS_WIN;
                 } else if (op == OP_RIS_WIN) {
                     if (!do_eval) { f = fW; pdf = pdfW; }
-                    P.nris[slot] = make_float4(wsum, targetW, r_add, __int_as_float(triW));
+                    st_s(&P.nris[slot], make_float4(wsum, targetW, r_add, __int_as_float(triW)));
                     if (hasW) {
                         fl |= NF_RIS_W;
                         stage_query(P, slot, 0, qm, lp, prim, L, dist - 1.0e-4f);
-                        P.na[slot] = make_float4(f.r, f.g, f.b, maxr(0.0f, dot(sn, L)));
+                        st_s(&P.na[slot], make_float4(f.r, f.g, f.b, maxr(0.0f, dot(sn, L))));
                     }
                     next = OP_DONE;
                 } else if (op == OP_MIS_LIGHT) {
@@ -1709,7 +1716,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_
                         float w = balance(lp2, pdf);
                         float cosv = maxr(dot(sn, L), 0.0f);
                         const Col a = f * cosv * li.emission * w / lp2;
-                        P.na[slot] = make_float4(a.r, a.g, a.b, 0.0f);
+                        st_s(&P.na[slot], make_float4(a.r, a.g, a.b, 0.0f));
                         fl |= NF_A;
                         stage_query(P, slot, 0, qm, lp, prim, L, dist - 1.0e-4f);
                     }
@@ -1720,8 +1727,8 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_
                     if (pdf > 0) {
                         fl |= NF_B;
                         stage_query(P, slot, 3, qm, bo, prim, L, 1.0e35f - 1.0e-4f);
-                        P.nb[slot] = make_float4(f.r, f.g, f.b, pdf);
-                        P.ndir[slot] = make_float4(L.x, L.y, L.z, absr(dot(sn, L)));
+                        st_s(&P.nb[slot], make_float4(f.r, f.g, f.b, pdf));
+                        st_s(&P.ndir[slot], make_float4(L.x, L.y, L.z, absr(dot(sn, L))));
                     }
                 } else if (op == OP_UNI_LIGHT) {
                     if (do_eval && pdf != 0.0f) {
@@ -1730,7 +1737,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_
                         lp2 /= geo;
                         float cosv = maxr(dot(sn, L), 0.0f);
                         const Col a = li.emission * cosv * f / lp2;
-                        P.na[slot] = make_float4(a.r, a.g, a.b, 0.0f);
+                        st_s(&P.na[slot], make_float4(a.r, a.g, a.b, 0.0f));
                         fl |= NF_A;
                         stage_query(P, slot, 0, qm, lp, prim, L, dist - 1.0e-4f);
                     }
@@ -1741,8 +1748,8 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_
                         v3 no = refr ? ip + sn * 1.0e-4f * ism * -1.0f : ip + sn * 1.0e-4f;
                         fl |= NF_B;
                         stage_query(P, slot, 3, qm, no, prim, L, 1.0e35f - 1.0e-4f);
-                        P.nb[slot] = make_float4(f.r, f.g, f.b, pdf);
-                        P.ndir[slot] = make_float4(L.x, L.y, L.z, maxr(0.0f, dot(sn, L)));
+                        st_s(&P.nb[slot], make_float4(f.r, f.g, f.b, pdf));
+                        st_s(&P.ndir[slot], make_float4(L.x, L.y, L.z, maxr(0.0f, dot(sn, L))));
                     }
                 } else if (op == OP_RESTIR) {
                     if (do_eval) {
@@ -1753,7 +1760,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_
                             if (rres.flags & RF_ENVMAP) { float ep_; e = env_eval(S, F, L, ep_); }
                             else e = emission_of(S.mats[S.mat_idx[rres.tri]]);
                             const Col a = f * rres.UCW * e * c;
-                            P.na[slot] = make_float4(a.r, a.g, a.b, 0.0f);
+                            st_s(&P.na[slot], make_float4(a.r, a.g, a.b, 0.0f));
                             fl |= NF_A;
                             if (!(rres.flags & RF_UNOCCLUDED) && rs.restir_di_settings.do_final_shading_visibility) {
                                 fl |= NF_AQ;
@@ -1766,7 +1773,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_
                     if (do_eval) {
                         float mw = F.options.envmap_bsdf_mis ? balance(lpdf, pdf) : 1.0f;
                         const Col e1 = f * geo * mw * ec / lpdf;
-                        P.ne1[slot] = make_float4(e1.r, e1.g, e1.b, 0.0f);
+                        st_s(&P.ne1[slot], make_float4(e1.r, e1.g, e1.b, 0.0f));
 #ifdef MPT_DEBUG_SLOT
                         if (slot == MPT_DEBUG_SLOT) { Col e1_ = f * geo * mw * ec / lpdf; printf("GPU env f %a %a %a bp %a mw %a e1 %a %a %a\n", f.r, f.g, f.b, pdf, mw, e1_.r, e1_.g, e1_.b); }
 #endif
@@ -1780,11 +1787,11 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_
                     float c2 = absr(dot(sn, L));
                     if (pdf > 0.0f) {
                         float epdf;
-                        Col er = env_eval_tex(S, F, L, etex, epdf);
+                        Col er = MPT_ENV_EARLY ? env_eval_tex(S, F, L, etex, epdf) : env_eval(S, F, L, epdf);
                         if (epdf > 0.0f && env_use) {
                             float mw = balance(pdf, epdf);
                             const Col e2 = er * mw * c2 * f / pdf;
-                            P.ne2[slot] = make_float4(e2.r, e2.g, e2.b, 0.0f);
+                            st_s(&P.ne2[slot], make_float4(e2.r, e2.g, e2.b, 0.0f));
                             fl |= NF_E2;
                             stage_query(P, slot, 2, qm, ip, prim, L, 1.0e35f - 1.0e-4f);
                         }
@@ -1816,8 +1823,8 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_
                         if (alive) {
                             thr *= dispersion_ray_color(vs.wl, m.dispersion_scale);
                             thr *= att;
-                            P.ray_o[slot] = make_float4(ip.x, ip.y, ip.z, __uint_as_float((uint32_t)prim));
-                            P.ray_d[slot] = make_float4(L.x, L.y, L.z, INFINITY);
+                            st_s(&P.ray_o[slot], make_float4(ip.x, ip.y, ip.z, __uint_as_float((uint32_t)prim)));
+                            st_s(&P.ray_d[slot], make_float4(L.x, L.y, L.z, INFINITY));
                             cont = true;
                         }
                     }
@@ -1841,11 +1848,11 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_
         } else {
             rcol += miss_radiance(S, F, bounce, d, thr);   // not reached: k_split sends misses to k_miss
         }
-        P.nthr[slot] = make_float4(thr_vertex.r, thr_vertex.g, thr_vertex.b, __uint_as_float(fl));
-        P.qmask[slot] = (uint8_t)(qm | (cont ? QM_CONT : 0u));
-        P.rng[slot] = rng.s;
-        P.thr[slot] = make_float4(thr.r, thr.g, thr.b, 0.0f);
-        P.col[slot] = make_float4(rcol.r, rcol.g, rcol.b, 0.0f);
+        st_s(&P.nthr[slot], make_float4(thr_vertex.r, thr_vertex.g, thr_vertex.b, __uint_as_float(fl)));
+        st_s(&P.qmask[slot], (uint8_t)(qm | (cont ? QM_CONT : 0u)));
+        st_s(&P.rng[slot], rng.s);
+        st_s(&P.thr[slot], make_float4(thr.r, thr.g, thr.b, 0.0f));
+        st_s(&P.col[slot], make_float4(rcol.r, rcol.g, rcol.b, 0.0f));
         vs_store(P.vsA, P.vsB, slot, vs);
     }
     // queue appends (every lane of the wave takes part in the ballots)
@@ -1863,11 +1870,11 @@ __global__ __launch_bounds__(TB) void k_miss(DevScene S, DevPaths P, const MptFr
     const int nm = P.counters[CTR_MISS];   // grid-stride, as k_resolve
     for (int i = blockIdx.x * TB + threadIdx.x; i < nm; i += gridDim.x * TB) {
         const int slot = P.qm[i];
-        const float4 rdv = P.ray_d[slot], t4 = P.thr[slot], cv = P.col[slot];
+        const float4 rdv = ld_s(&P.ray_d[slot]), t4 = ld_s(&P.thr[slot]), cv = ld_s(&P.col[slot]);
         v3 d = mk3(rdv.x, rdv.y, rdv.z);
         if (bounce == 0) d = normalize(d);
         const Col rc = col(cv.x, cv.y, cv.z) + miss_radiance(S, *Fp, bounce, d, col(t4.x, t4.y, t4.z));
-        P.col[slot] = make_float4(rc.r, rc.g, rc.b, 0.0f);
+        st_s(&P.col[slot], make_float4(rc.r, rc.g, rc.b, 0.0f));
     }
 }
 
@@ -1948,7 +1955,7 @@ __global__ __launch_bounds__(CP_NT) void k_split(DevScene S, DevPaths P, const i
 #pragma unroll
     for (int j = 0; j < CP_ITEMS; j++) {
         // the hit's material class as the traversal reported it (0xff: a miss)
-        const uint32_t hc = j < n ? (uint32_t)P.hit_cls[slots[j]] : 0xffu;
+        const uint32_t hc = j < n ? (uint32_t)ld_s(&P.hit_cls[slots[j]]) : 0xffu;
         if (hc != 0xffu) {
             const int32_t mt = classes ? (int32_t)hc : 0;
             if (classes == 2 && (mt & MT_GLASS)) { gm |= 1u << j; ng++; }
@@ -2016,7 +2023,7 @@ __global__ __launch_bounds__(CP_NT) void k_compact(DevPaths P, int32_t* q_next, 
     int c[5] = {0, 0, 0, 0, 0};
 #pragma unroll
     for (int j = 0; j < CP_ITEMS; j++) {
-        m[j] = (j < n && slots[j] >= 0) ? P.qmask[slots[j]] : 0;
+        m[j] = (j < n && slots[j] >= 0) ? ld_s(&P.qmask[slots[j]]) : (uint8_t)0;
         c[0] += (m[j] & QM_CONT) ? 1 : 0;
         c[1] += m[j] & 1u;
         c[2] += (m[j] >> 1) & 1u;
@@ -2189,29 +2196,29 @@ DEV void resolve_entry(const DevScene& S, const DevPaths& P, const MptFrame& F, 
     const int slot = shaded_entry(P, nh, i);
     if (slot < 0) return;   // deferred to the generic shading list
     // the NEE record planes the vertex wrote (flags in nthr.w), each read whole
-    const float4 t4 = P.nthr[slot];
+    const float4 t4 = ld_s(&P.nthr[slot]);
     const uint32_t fl = __float_as_uint(t4.w);
     if (!(fl & NF_SHADED) || (fl & NF_NOADD)) return;
     const int lss = F.options.direct_light_sampling;
     const int lssb = bounce_lss(F, bounce);
     Col ld = col(0.0f), ed = col(0.0f);
-    auto occ = [&](int k) { return P.occ[(size_t)k * (size_t)P.nq_stride + (size_t)slot] != 0; };
-    if (fl & NF_IMM) { const float4 a = P.na[slot]; ld = col(a.x, a.y, a.z); }
+    auto occ = [&](int k) { return ld_s(&P.occ[(size_t)k * (size_t)P.nq_stride + (size_t)slot]) != 0; };
+    if (fl & NF_IMM) { const float4 a = ld_s(&P.na[slot]); ld = col(a.x, a.y, a.z); }
     else if (!(fl & NF_L)) ld = col(0.0f);
     else if (EXT && (fl & NF_EXT)) ld = ext_resolve(S, P, F, slot, lssb);   // already / number_of_light_samples
     else if (lss == MPT_LSS_RESTIR_DI && bounce == 0) {
-        if ((fl & NF_A) && !((fl & NF_AQ) && occ(0))) { const float4 a = P.na[slot]; ld = col(a.x, a.y, a.z); }
+        if ((fl & NF_A) && !((fl & NF_AQ) && occ(0))) { const float4 a = ld_s(&P.na[slot]); ld = col(a.x, a.y, a.z); }
     } else if (lssb == MPT_LSS_RIS_BSDF_AND_LIGHT) {
-        const float4 ris = P.nris[slot];
+        const float4 ris = ld_s(&P.nris[slot]);
         float wsum = ris.x;
         float cwb = 0.0f, targetb = 0.0f;
         int trib = -1;
         float4 b = make_float4(0.0f, 0.0f, 0.0f, 0.0f), dr = b;
         if (fl & NF_B) {
-            b = P.nb[slot];
-            dr = P.ndir[slot];
+            b = ld_s(&P.nb[slot]);
+            dr = ld_s(&P.ndir[slot]);
             ShadowLightHit sh;
-            if (shadow_light_hit(S, P.nhit[slot], sh) && !is_black(sh.em)) {
+            if (shadow_light_hit(S, ld_s(&P.nhit[slot]), sh) && !is_black(sh.em)) {
                 Col lc = col(b.x, b.y, b.z) * sh.em * dr.w;
                 targetb = lum(lc);
                 float lpdf = pdf_emissive_hit(S, sh, mk3(dr.x, dr.y, dr.z));
@@ -2235,18 +2242,18 @@ DEV void resolve_entry(const DevScene& S, const DevPaths& P, const MptFrame& F, 
                 float c = dr.w;
                 if (c > 0.0f) ld = col(b.x, b.y, b.z) * ucw * emission_of(S.mats[S.mat_idx[trib]]) * c;
             } else if (!occ(0)) {
-                const float4 a = P.na[slot];
+                const float4 a = ld_s(&P.na[slot]);
                 float c = a.w;
                 if (c > 0.0f) ld = col(a.x, a.y, a.z) * ucw * emission_of(S.mats[S.mat_idx[__float_as_int(ris.w)]]) * c;
             }
         }
     } else if (lssb == MPT_LSS_MIS_LIGHT_BSDF) {
         Col lrad = col(0.0f), brad = col(0.0f);
-        if ((fl & NF_A) && !occ(0)) { const float4 a = P.na[slot]; lrad = col(a.x, a.y, a.z); }
+        if ((fl & NF_A) && !occ(0)) { const float4 a = ld_s(&P.na[slot]); lrad = col(a.x, a.y, a.z); }
         if (fl & NF_B) {
             ShadowLightHit sh;
-            if (shadow_light_hit(S, P.nhit[slot], sh) && !is_black(sh.em)) {
-                const float4 b = P.nb[slot], dr = P.ndir[slot];
+            if (shadow_light_hit(S, ld_s(&P.nhit[slot]), sh) && !is_black(sh.em)) {
+                const float4 b = ld_s(&P.nb[slot]), dr = ld_s(&P.ndir[slot]);
                 float lp2 = pdf_emissive_hit(S, sh, mk3(dr.x, dr.y, dr.z));
                 float w = balance(b.w, lp2);
                 brad = col(b.x, b.y, b.z) * dr.w * sh.em * w / b.w;
@@ -2254,12 +2261,12 @@ DEV void resolve_entry(const DevScene& S, const DevPaths& P, const MptFrame& F, 
         }
         ld = lrad + brad;
     } else if (lssb == MPT_LSS_UNIFORM_ONE_LIGHT) {
-        if ((fl & NF_A) && !occ(0)) { const float4 a = P.na[slot]; ld = col(a.x, a.y, a.z); }
+        if ((fl & NF_A) && !occ(0)) { const float4 a = ld_s(&P.na[slot]); ld = col(a.x, a.y, a.z); }
     } else if (lssb == MPT_LSS_BSDF) {
         if (fl & NF_B) {
             ShadowLightHit sh;
-            if (shadow_light_hit(S, P.nhit[slot], sh) && !is_black(sh.em)) {
-                const float4 b = P.nb[slot], dr = P.ndir[slot];
+            if (shadow_light_hit(S, ld_s(&P.nhit[slot]), sh) && !is_black(sh.em)) {
+                const float4 b = ld_s(&P.nb[slot]), dr = ld_s(&P.ndir[slot]);
                 ld = col(b.x, b.y, b.z) * dr.w * sh.em / b.w;
             }
         }
@@ -2270,16 +2277,16 @@ DEV void resolve_entry(const DevScene& S, const DevPaths& P, const MptFrame& F, 
         ld = ld / (float)rs.number_of_light_samples;
     {
         Col e2 = col(0.0f), e1 = col(0.0f);
-        if ((fl & NF_E2) && !occ(2)) { const float4 e = P.ne2[slot]; e2 = col(e.x, e.y, e.z); }
-        if ((fl & NF_E1) && !occ(1)) { const float4 e = P.ne1[slot]; e1 = col(e.x, e.y, e.z); }
+        if ((fl & NF_E2) && !occ(2)) { const float4 e = ld_s(&P.ne2[slot]); e2 = col(e.x, e.y, e.z); }
+        if ((fl & NF_E1) && !occ(1)) { const float4 e = ld_s(&P.ne1[slot]); e1 = col(e.x, e.y, e.z); }
         ed = e2 + e1;
     }
     ld = clamp_contrib(ld, rs.direct_contribution_clamp, bounce == 0);
     ed = clamp_contrib(ed, rs.envmap_contribution_clamp, bounce == 0);
     Col ind = (ld + ed) * col(t4.x, t4.y, t4.z);
-    float4 cv = P.col[slot];
+    float4 cv = ld_s(&P.col[slot]);
     Col rc = col(cv.x, cv.y, cv.z) + clamp_contrib(ind, rs.indirect_contribution_clamp, bounce > 0);
-    P.col[slot] = make_float4(rc.r, rc.g, rc.b, 0.0f);
+    st_s(&P.col[slot], make_float4(rc.r, rc.g, rc.b, 0.0f));
 #ifdef MPT_DEBUG_SLOT
     if (slot == MPT_DEBUG_SLOT) { Col t_ = col(t4.x, t4.y, t4.z); printf("GPU b%d ld %a %a %a ed %a %a %a thr %a %a %a rc %a %a %a\n", bounce, ld.r, ld.g, ld.b, ed.r, ed.g, ed.b, t_.r, t_.g, t_.b, rc.r, rc.g, rc.b); }
 #endif
