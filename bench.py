@@ -255,6 +255,7 @@ def main():
     W = a.width or (3840 if a.workload == "c5" else 256 if a.workload == "c1" else 1920)
     H = a.height or (2160 if a.workload == "c5" else 256 if a.workload == "c1" else 1080)
     default_bounces = a.bounces is None
+    default_bsdf = a.bsdf == "principled"   # (C1's Lambert override below is its configuration's own)
     a.bounces = a.bounces if a.bounces is not None else (16 if a.workload == "c5" else 3)
     if a.workload in ("c3", "c4"):
         from mpt import synthetic
@@ -450,7 +451,7 @@ def main():
     # the dominant KERNEL (the ReSTIR DI pass lines above span several kernels: reported, not candidates)
     dom = max(lines[:n_kernel_lines], key=lambda x: x["total_ms"])
 
-    default_cfg = a.strategy is None and default_bounces and a.bsdf == "principled" and a.scene is None
+    default_cfg = a.strategy is None and default_bounces and default_bsdf and a.scene is None
     pmc = load_traffic(a.workload, W, H) if default_cfg else None
 
     def pmc_entry(sym):

@@ -1,0 +1,3 @@
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
+bash tools/gpu_evidence.sh r04b c4 "--steps 16 --warmup 4" "--steps 64 --cpu-seconds 10 --parity-seconds 60" || exit $?
