@@ -1554,7 +1554,12 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_
             // per-vertex half of every BSDF evaluation below, one LDS record per lane (55
             // dwords: an odd stride, so lane-parallel accesses are bank-conflict free).  Held
             // in registers it pushed the kernel into ~140 spilled VGPRs; in LDS it costs one
-            // ds_read per field per evaluation (-23% k_shade time on C3)
+            // ds_read per field per evaluation (-23% k_shade time on C3).  The kernel's 80640 B
+            // of LDS per 256-lane block are these 56320 B plus 24320 B (95 B per lane) of private
+            // arrays that the compiler's promote-alloca pass moves into the LDS the 2-wave
+            // occupancy leaves free (-mllvm -disable-promote-alloca-to-lds: 160 B of scratch per
+            // lane instead); two blocks fill a CU's 160 KB, so LDS and VGPRs (238) both cap the
+            // kernel at 2 waves / SIMD
             __shared__ PEval pe_lds[TB];
             PEval& pe = pe_lds[threadIdx.x];
             // the first light sample's emissive record, loaded while the per-vertex BSDF terms are
