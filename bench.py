@@ -7,6 +7,10 @@ Workloads (BASELINE.json configs):
   sampling + BSDF MIS), 1920x1080, layered Principled BSDF, reference-default RIS light
   sampling, alpha testing on (C3 pins it for the foliage); K = 256.
 * c2: the Cornell box glTF at 1920x1080, Principled + NEE/MIS (LSS_MIS_LIGHT_BSDF); K = 64.
+* c3t: c3 on the texture-realistic city (synthetic.procedural_city_textured: 70 materials, 83 % of
+  the triangles with base-colour + normal-map + roughness-metallic textures, 193 MB of textures),
+  so that the shading roofline is measured where texture gathers and per-vertex resolved
+  materials cost something.
 * c4: c3 with ReSTIR DI (fused spatiotemporal + spatial reuse), GPURenderer seed schedule.
 * c5: the glass-dispersion stress scene (multi-dispersion.gltf; --scene
   nested-dielectrics-complex for the nested-dielectrics one) at 3840x2160, 16 bounces,
@@ -60,7 +64,7 @@ MAX_BATCH = 128    # MPT_MAX_BATCH
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--workload", default="c3", choices=["c1", "c2", "c3", "c4", "c5"])
+    ap.add_argument("--workload", default="c3", choices=["c1", "c2", "c3", "c3t", "c4", "c5"])
     ap.add_argument("--steps", type=int, default=None, help="default: the workload's spp (c3/c4 256, c2 64, c5 1024, c1 1)")
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--width", type=int, default=None, help="default 1920 (c5: 3840)")
@@ -257,15 +261,18 @@ def main():
     default_bounces = a.bounces is None
     default_bsdf = a.bsdf == "principled"   # (C1's Lambert override below is its configuration's own)
     a.bounces = a.bounces if a.bounces is not None else (16 if a.workload == "c5" else 3)
-    if a.workload in ("c3", "c4"):
+    if a.workload in ("c3", "c3t", "c4"):
         from mpt import synthetic
-        sd = synthetic.procedural_city(1234)
+        sd = synthetic.procedural_city_textured() if a.workload == "c3t" else synthetic.procedural_city(1234)
         env = mpt.build_envmap(scene.procedural_sky(2048, 1024, seed=7))
         wset = scene.envmap_world(1.0)
-        strategy = a.strategy or ("ris" if a.workload == "c3" else "restir")
+        strategy = a.strategy or ("restir" if a.workload == "c4" else "ris")
         K = a.steps or 256
         alpha = True      # C3 pins do_alpha_testing = true (the Bistro's foliage)
         desc = (f"{a.workload.upper()} stand-in: procedural city (2.86 M tris incl. alpha-tested leaf cards, seed 1234) + "
+                if a.workload != "c3t" else
+                "C3T (texture-realistic C3 variant): procedural city seed 1235, 2.77 M tris, 70 materials, 83 % of the "
+                "triangles textured (base colour + normal map + roughness-metallic, 44 textures / 193 MB RGBA8) + "
                 "procedural HDR sky 2048x1024, alpha testing on"
                 + (", ReSTIR DI fused spatiotemporal + 1 spatial pass, GPURenderer seed schedule" if a.workload == "c4" else ""))
     elif a.workload == "c5":
@@ -528,7 +535,7 @@ def main():
             "dtype": "f32",
             "data": ("synthetic (seeded procedural city + sky standing in for Bistro + its HDR, "
                      + ("GPURenderer seed schedule)" if a.workload == "c4" else "CPU seed schedule)")
-                     if a.workload in ("c3", "c4") else f"synthetic (reference glTF {sd.name}, seeded CPU seed schedule)"),
+                     if a.workload in ("c3", "c3t", "c4") else f"synthetic (reference glTF {sd.name}, seeded CPU seed schedule)"),
             "msample_per_s": round(W * H * K / elapsed / 1e6, 3),
             "samples_per_launch": round(st.frames / max(1, st.shade_launches / (a.bounces + 1)), 3),
             "rays_per_sample": round(rays_total / (W * H * K), 4),

@@ -586,3 +586,143 @@ def write_textured_gltf(dirpath: str, seed: int = 5, glb: bool = False) -> str:
     with open(path, "w") as f:
         json.dump(g, f)
     return path
+
+
+# ---- texture-realistic variant (VERDICT r03 "What's weak" 7) ------------------------------
+def _value_noise(rng, size, cells, octaves=3):
+    """Smooth periodic value noise in [0, 1), [size, size] float32 (bilinear upsampled lattices)."""
+    out = np.zeros((size, size), np.float32)
+    amp, tot = 1.0, 0.0
+    for o in range(octaves):
+        n = cells << o
+        lat = rng.random((n, n)).astype(np.float32)
+        t = (np.arange(size, dtype=np.float32) + 0.5) * n / size - 0.5
+        i0 = np.floor(t).astype(np.int64)
+        f = (t - i0).astype(np.float32)
+        i0 %= n
+        i1 = (i0 + 1) % n
+        rows = lat[i0][:, i0] * (1 - f)[None, :] + lat[i0][:, i1] * f[None, :]
+        rows1 = lat[i1][:, i0] * (1 - f)[None, :] + lat[i1][:, i1] * f[None, :]
+        out += amp * (rows * (1 - f)[:, None] + rows1 * f[:, None])
+        tot += amp
+        amp *= 0.5
+    return out / tot
+
+
+def _albedo_texture(rng, size, base, pattern):
+    """RGBA8 base-colour texture: a tinted noise field with bricks / planks / tiles / plaster."""
+    n = _value_noise(rng, size, 8)
+    y, x = np.mgrid[0:size, 0:size].astype(np.float32) / size
+    if pattern == 0:     # bricks
+        row = np.floor(y * 32)
+        mortar = ((y * 32) % 1 < 0.12) | (((x * 16 + 0.5 * (row % 2)) % 1) < 0.06)
+        shade = 0.75 + 0.5 * n
+        shade = np.where(mortar, 1.35, shade)
+    elif pattern == 1:   # planks
+        shade = 0.7 + 0.4 * n + 0.2 * np.sin(x * 60.0 + 6.0 * n)
+    elif pattern == 2:   # tiles
+        grout = ((x * 12) % 1 < 0.05) | ((y * 12) % 1 < 0.05)
+        shade = np.where(grout, 0.5, 0.85 + 0.3 * n)
+    else:                # plaster
+        shade = 0.8 + 0.35 * n
+    rgb = np.clip(np.asarray(base, np.float32)[None, None, :] * shade[..., None] * 255.0, 0, 255)
+    t = np.empty((size, size, 4), np.uint8)
+    t[..., :3] = rgb.astype(np.uint8)
+    t[..., 3] = 255
+    return t
+
+
+def _normal_texture(rng, size, strength):
+    """RGBA8 tangent-space normal map from the gradient of a noise height field."""
+    h = _value_noise(rng, size, 16) * strength
+    gx = np.roll(h, -1, 1) - np.roll(h, 1, 1)
+    gy = np.roll(h, -1, 0) - np.roll(h, 1, 0)
+    n = np.stack([-gx * size / 64.0, -gy * size / 64.0, np.ones_like(h)], -1)
+    n /= np.linalg.norm(n, axis=-1, keepdims=True)
+    t = np.empty((size, size, 4), np.uint8)
+    t[..., :3] = np.clip(np.round((n * 0.5 + 0.5) * 255.0), 0, 255).astype(np.uint8)
+    t[..., 3] = 255
+    return t
+
+
+def _rm_texture(rng, size, rough, metal):
+    """RGB roughness-metallic texture (G roughness, B metallic, Material.h: the packed slot)."""
+    n = _value_noise(rng, size, 8)
+    t = np.zeros((size, size, 4), np.uint8)
+    t[..., 1] = np.clip((rough + 0.3 * (n - 0.5)) * 255.0, 8, 255).astype(np.uint8)
+    t[..., 2] = np.clip(metal * 255.0 * (n > 0.35), 0, 255).astype(np.uint8)
+    t[..., 3] = 255
+    return t
+
+
+def procedural_city_textured(seed: int = 1235, tex_scale: float = 3.0) -> SceneData:
+    """The C3 city with the texture load of a production exterior (the Bistro's materials are
+    textured on most surfaces): 64 materials -- 48 facade materials (24 base-colour textures at
+    1024^2 in 4 patterns, 8 normal maps at 1024^2, 8 roughness-metallic textures at 512^2), 8
+    roof materials and textured asphalt / sidewalks at 2048^2 -- ~190 MB of RGBA8 textures,
+    world-space planar texture coordinates (tex_scale metres per repeat).  Glass, lamps,
+    foliage and the alpha-tested leaf cards keep the C3 materials."""
+    sd = procedural_city(seed)
+    rng = np.random.default_rng(seed + 101)
+    V = np.asarray(sd.vertices, np.float32)
+    I = np.asarray(sd.triangle_indices).reshape(-1, 3)
+    M = np.asarray(sd.material_indices).copy()
+    mats = list(sd.materials)
+    textures = list(sd.textures)          # texture 0: the leaf cards' alpha texture
+
+    def add_tex(t):
+        textures.append(t)
+        return len(textures) - 1
+
+    palettes = [(0.62, 0.55, 0.45), (0.55, 0.25, 0.2), (0.7, 0.7, 0.72), (0.3, 0.35, 0.4), (0.5, 0.42, 0.3), (0.68, 0.6, 0.52)]
+    albedo = [add_tex(_albedo_texture(rng, 1024, palettes[k % len(palettes)], k % 4)) for k in range(24)]
+    normals = [add_tex(_normal_texture(rng, 1024, 2.0 + k)) for k in range(8)]
+    rms = [add_tex(_rm_texture(rng, 512, 0.5 + 0.05 * k, 0.6 if k % 4 == 3 else 0.0)) for k in range(8)]
+
+    def textured(base_tex, normal_tex, rm_tex, specular=0.5):
+        m = _mat((1.0, 1.0, 1.0), rough=1.0, metallic=1.0, specular=specular)
+        m.base_color_texture_index = base_tex
+        m.normal_map_texture_index = normal_tex
+        m.roughness_metallic_texture_index = rm_tex
+        m.make_safe()
+        m.precompute_properties()
+        return m
+
+    facade0 = len(mats)
+    for k in range(48):
+        mats.append(textured(albedo[k % 24], normals[(k * 5) % 8], rms[(k * 3) % 8]))
+    roof0 = len(mats)
+    for k in range(8):
+        mats.append(textured(albedo[(3 * k + 1) % 24], normals[k], rms[(k + 2) % 8], specular=0.3))
+    asphalt = len(mats)
+    mats.append(textured(add_tex(_albedo_texture(rng, 2048, (0.09, 0.09, 0.095), 3)), add_tex(_normal_texture(rng, 2048, 4.0)),
+                         rms[0], specular=0.3))
+    sidewalk = len(mats)
+    mats.append(textured(add_tex(_albedo_texture(rng, 2048, (0.5, 0.49, 0.47), 2)), normals[1], rms[1], specular=0.4))
+    # reassign: each building's facade (C3 materials 2-5) one of the 48, roofs (7) one of 8
+    tri_bld = rng.integers(0, 1 << 30, len(M))
+    fac = np.isin(M, [2, 3, 4, 5])
+    # one facade material per original wall material and 12 variants by position (blocks of 64 m)
+    cen = V[I].mean(1)
+    cell = (np.floor(cen[:, 0] / 64.0).astype(np.int64) * 7 + np.floor(cen[:, 2] / 64.0).astype(np.int64) * 13) % 12
+    M[fac] = facade0 + (M[fac] - 2) * 12 + cell[fac]
+    roof = M == 7
+    M[roof] = roof0 + (tri_bld[roof] % 8) * 0 + (cell[roof] % 8)
+    M[M == 0] = asphalt
+    M[M == 1] = sidewalk
+    # world-space planar texture coordinates by the dominant axis of the triangle's normal
+    tn = np.cross(V[I[:, 1]] - V[I[:, 0]], V[I[:, 2]] - V[I[:, 0]])
+    ax = np.argmax(np.abs(tn), 1)
+    uv = np.asarray(sd.texcoords, np.float32).copy()
+    retex = M >= facade0
+    for a, (ui, vi) in enumerate([(2, 1), (0, 2), (0, 1)]):
+        sel = retex & (ax == a)
+        vid = np.unique(I[sel].reshape(-1))
+        uv[vid, 0] = V[vid, ui] / tex_scale
+        uv[vid, 1] = V[vid, vi] / tex_scale
+    sd.texcoords = uv.astype(np.float32)
+    sd.material_indices = M.astype(np.int32)
+    sd.materials = mats
+    sd.textures = textures
+    sd.name = f"procedural_city_textured_{seed}"
+    return sd.finalize()

@@ -231,3 +231,35 @@ def test_c4_city_restir_reset_in_used_context_bit_exact(city, luts, city_oracle,
     assert not np.array_equal(o.render(b), got)
     o.close()
     r.close()
+
+
+# ---- C3T: the texture-realistic city (bench --workload c3t) on an 8-row band ------------------
+
+@pytest.mark.gpu
+def test_c3t_textured_city_band_bit_exact(luts):
+    """70 materials, 83 % of the triangles with base-colour + normal-map + roughness-metallic
+    textures (193 MB): per-vertex resolved materials, normal mapping and texel gathers on most
+    hits, RIS + envmap MIS + alpha testing as C3, 4 spp on rows 536-543, against the oracle."""
+    import mpt
+    from mpt import synthetic
+    from oracle import oracle as orc
+    sd = synthetic.procedural_city_textured()
+    env = mpt.build_envmap(scene.procedural_sky(512, 256, seed=7))
+    cam = scene.make_camera(sd.camera_info, 1920, 1080)
+    opt = abi.KernelOptions.default()
+    opt.direct_light_sampling = abi.LSS_RIS_BSDF_AND_LIGHT
+    st = scene.parity_settings(3)
+    st.do_alpha_testing = True
+    band = (8, 67, 135)
+    frs = [scene.make_frame(cam, 1920, 1080, options=opt, settings=st, world=scene.envmap_world(1.0), sample_number=s,
+                            random_seed=seed, band=band) for s, seed in scene.cpu_seed_schedule(4)]
+    r = _gpu(sd, luts, env)
+    r.render_samples(frs)
+    r.synchronize_kernel()
+    got = r.framebuffer(abi.FB_COLOR)
+    r.close()
+    o = orc.Oracle(sd, luts, envmap=env)
+    ref = o.render(frs)
+    o.close()
+    _same(got, ref, "C3T band colour")
+    assert np.isfinite(got).all() and got.mean() > 0
