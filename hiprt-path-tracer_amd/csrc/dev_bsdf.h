@@ -75,8 +75,7 @@ DEV VState vs_default() {
     v.pos = 0; v.incident = -1; v.outgoing = -1; v.inside = false; v.dist = 0.0f; v.wl = 0.0f;
     return v;
 }
-DEV VState vs_load(const uint4* A, const uint4* B, int i) {
-    uint4 a = ld_s(A + i), b = ld_s(B + i);
+DEV VState vs_unpack(uint4 a, uint4 b) {
     VState v;
     v.st[0] = a.x; v.st[1] = a.y; v.st[2] = a.z;
     v.pos = (int)(a.w & 3u);
@@ -85,10 +84,15 @@ DEV VState vs_load(const uint4* A, const uint4* B, int i) {
     v.dist = __uint_as_float(b.z); v.wl = __uint_as_float(b.w);
     return v;
 }
-DEV void vs_store(uint4* A, uint4* B, int i, const VState& v) {
-    st_s(A + i, make_uint4(v.st[0], v.st[1], v.st[2], (uint32_t)v.pos | ((uint32_t)v.inside << 2)));
-    st_s(B + i, make_uint4((uint32_t)v.incident, (uint32_t)v.outgoing, __float_as_uint(v.dist), __float_as_uint(v.wl)));
+DEV uint4 vs_pack_a(const VState& v) { return make_uint4(v.st[0], v.st[1], v.st[2], (uint32_t)v.pos | ((uint32_t)v.inside << 2)); }
+DEV uint4 vs_pack_b(const VState& v) {
+    return make_uint4((uint32_t)v.incident, (uint32_t)v.outgoing, __float_as_uint(v.dist), __float_as_uint(v.wl));
 }
+// cached (G-buffer, re-read by neighbours) and streaming (path state, ld_s / st_s) accessors
+template <class PA, class PB> DEV VState vs_load(const PA& A, const PB& B, int i) { return vs_unpack(A[i], B[i]); }
+template <class PA, class PB> DEV void vs_store(const PA& A, const PB& B, int i, const VState& v) { A[i] = vs_pack_a(v); B[i] = vs_pack_b(v); }
+DEV VState vs_load_s(const uint4* A, const uint4* B, int i) { return vs_unpack(ld_s(A + i), ld_s(B + i)); }
+DEV void vs_store_s(uint4* A, uint4* B, int i, const VState& v) { st_s(A + i, vs_pack_a(v)); st_s(B + i, vs_pack_b(v)); }
 DEV uint32_t& vs_entry(VState& v, int i) {   // constant-index friendly access
     return i == 0 ? v.st[0] : (i == 1 ? v.st[1] : v.st[2]);
 }

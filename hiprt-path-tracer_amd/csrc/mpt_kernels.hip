@@ -500,7 +500,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MODE == TM_P
         const bool found = tr.bprim >= 0;
         if (MODE == TM_PATH) {
             // trace_ray's boundary-skipping loop (Intersect.h:117-206)
-            VState vs = vs_load(P.vsA, P.vsB, ray);
+            VState vs = vs_load_s(P.vsA, P.vsB, ray);
             bool again = false;
             if (found) {
                 was_inside = vs.pos > 0;
@@ -514,7 +514,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MODE == TM_P
                     again = true;
                 }
             }
-            vs_store(P.vsA, P.vsB, ray, vs);
+            vs_store_s(P.vsA, P.vsB, ray, vs);
             if (again) {
                 n_rays++;
                 tr.init(tr.o + tr.best * tr.d, tr.d, tr.last_hit, INFINITY, A.alpha != 0,
@@ -901,7 +901,7 @@ __global__ __launch_bounds__(TB) void k_camera(DevPaths P, const MptFrame* __res
     P.ray_o[slot] = make_float4(o.x, o.y, o.z, __uint_as_float(0xffffffffu));
     P.ray_d[slot] = make_float4(d.x, d.y, d.z, INFINITY);
     P.rng[slot] = rng.s;   // camera stream after the jitter draws (trace_ray's wavelength draw)
-    vs_store(P.vsA, P.vsB, slot, vs_default());
+    vs_store_s(P.vsA, P.vsB, slot, vs_default());
     P.thr[slot] = make_float4(1.0f, 1.0f, 1.0f, 0.0f);
     P.col[slot] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     P.alb[slot] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
@@ -1437,7 +1437,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_
         v3 o = mk3(ro.x, ro.y, ro.z), d = mk3(rdv.x, rdv.y, rdv.z);
         int prim = (int)__float_as_uint(hv.w);
         bool found = prim >= 0;
-        VState vs = vs_load(P.vsA, P.vsB, slot);
+        VState vs = vs_load_s(P.vsA, P.vsB, slot);
         Rng rng = make_rng(ld_s(&P.rng[slot]));
         const float4 thv = ld_s(&P.thr[slot]);
         Col thr = col(thv.x, thv.y, thv.z);
@@ -1858,7 +1858,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_
         st_s(&P.rng[slot], rng.s);
         st_s(&P.thr[slot], make_float4(thr.r, thr.g, thr.b, 0.0f));
         st_s(&P.col[slot], make_float4(rcol.r, rcol.g, rcol.b, 0.0f));
-        vs_store(P.vsA, P.vsB, slot, vs);
+        vs_store_s(P.vsA, P.vsB, slot, vs);
     }
     // queue appends (every lane of the wave takes part in the ballots)
     SECT(4);

@@ -423,7 +423,7 @@ __global__ __launch_bounds__(TB) void k_gbuffer(DevScene S, DevPaths P, const Mp
     int4 meta = P.gb_meta[gp];
     if (found) {
         // trace_ray hit processing (Intersect.h:150-216), as k_shade does at bounce 0
-        VState vs = vs_load(P.vsA, P.vsB, slot);
+        VState vs = vs_load_s(P.vsA, P.vsB, slot);
         Rng rng = make_rng(P.rng[slot]);
         float t = hv.x;
         v2 uv = mk2(hv.y, hv.z);
