@@ -136,6 +136,8 @@ struct MptContext {
     int restir_staged = 1;                // ReSTIR DI reuse passes staged around their rays (MPT_RESTIR_STAGED)
     int restir_batch = 1;                 // ReSTIR DI samples batched after bounce 0 (MPT_RESTIR_BATCH)
     int shade_glass = 1;                  // glass-class shading kernel (MPT_SHADE_GLASS)
+    int shade_split = 0;                  // plain-class shading stages (MPT_SHADE_SPLIT, LaunchCfg::shade_split)
+    int shade_texmetal = 1;               // MT_TEXMETAL materials through the plain list (MPT_SHADE_TEXMETAL)
     std::vector<MptMaterial> h_mats;
     std::vector<int32_t> h_mat_idx;       // per triangle (alpha flags of the triangle records)
     std::vector<uint8_t> h_tex_alpha;     // per texture: some texel has alpha < 255
@@ -153,7 +155,7 @@ struct MptContext {
     int res_x = 0, res_y = 0, band_h = 1, band_i = 0, band_c = 1, n_slots = 0;   // n_slots = pixels of the partition
     int batch_cap = 0;      // samples per pixel the path state is sized for (mpt_render_frames)
     int batch = 1;          // samples of the launch being set up
-    DBuf<float4> ray_o, ray_d, hit, thr, col, alb, nrmv, nq_o, nq_d, nhit;
+    DBuf<float4> ray_o, ray_d, hit, thr, col, alb, nrmv, nq_o, nq_d, nhit, s_gn;
     DBuf<uint8_t> hit_inside, hit_cls, occ, qmask;
     DBuf<uint32_t> rng, spill, spill2;
     DBuf<uint2> seeds;
@@ -304,6 +306,7 @@ DevPaths dev_paths(MptContext* c) {
     P.occ = c->occ.p;
     P.qmask = c->qmask.p;
     P.nhit = c->nhit.p;
+    P.s_gn = c->s_gn.p;
     P.mat_slot = c->mat_slot.p;
     P.fb_color = c->fb_color.p;
     P.fb_albedo = c->fb_albedo.p;
@@ -359,15 +362,15 @@ struct Allocs {
 };
 
 // Bytes of path state per path slot (ensure_batch): ray_o, ray_d, hit, thr, col, alb, nrmv,
-// nhit (8 x 16), vsA + vsB (32), the NEE record planes (7 x 16), 4 staged NEE query rays (2 x 64), the
+// nhit, s_gn (9 x 16), vsA + vsB (32), the NEE record planes (7 x 16), 4 staged NEE query rays (2 x 64), the
 // compacted query entries (16), occlusion bytes (4), 6 queues (24), rng (4), seeds (8), hit_inside,
 // qmask, active (3).  Textured scenes add a resolved material per slot.
-constexpr size_t PATH_BYTES = 8 * 16 + 32 + 7 * 16 + 128 + 16 + 4 + 24 + 4 + 8 + 3;
+constexpr size_t PATH_BYTES = 9 * 16 + 32 + 7 * 16 + 128 + 16 + 4 + 24 + 4 + 8 + 3;
 
 void release_batch(MptContext* c) {
     release_all(c->ray_o, c->ray_d, c->hit, c->hit_inside, c->hit_cls, c->rng, c->seeds, c->thr, c->col, c->vsA, c->vsB, c->alb, c->nrmv,
                 c->q0, c->q1, c->qh, c->qm, c->qf, c->nq_light, c->nthr, c->na, c->nb, c->ndir, c->nris, c->ne1, c->ne2, c->nq_o,
-                c->nq_d, c->nq_tgt, c->occ, c->nhit, c->qmask, c->active,
+                c->nq_d, c->nq_tgt, c->occ, c->nhit, c->s_gn, c->qmask, c->active,
                 c->mat_slot);
     c->batch_cap = 0;
 }
@@ -389,7 +392,7 @@ int ensure_batch(MptContext* c, int batch, bool mat_slot) {
         A(c->ray_o, N); A(c->ray_d, N); A(c->hit, N); A(c->hit_inside, N); A(c->hit_cls, N); A(c->rng, N); A(c->seeds, N); A(c->thr, N); A(c->col, N);
         A(c->vsA, N); A(c->vsB, N); A(c->alb, N); A(c->nrmv, N); A(c->q0, N); A(c->q1, N); A(c->qh, N); A(c->qm, N); A(c->qf, N); A(c->nq_light, N);
         A(c->nthr, N); A(c->na, N); A(c->nb, N); A(c->ndir, N); A(c->nris, N); A(c->ne1, N); A(c->ne2, N);
-        A(c->nq_o, 4 * N); A(c->nq_d, 4 * N); A(c->nq_tgt, 4 * N); A(c->occ, 4 * N); A(c->nhit, N);
+        A(c->nq_o, 4 * N); A(c->nq_d, 4 * N); A(c->nq_tgt, 4 * N); A(c->occ, 4 * N); A(c->nhit, N); A(c->s_gn, N);
         A(c->qmask, N); A(c->active, N);
         if (A.e == hipSuccess) A(hipMemsetAsync(c->active.p, 0, N, c->stream));
     }
@@ -661,7 +664,8 @@ int resolve_materials(MptContext* c) {
     for (TriRec& tr : c->bvh.tris) {
         int32_t prim;
         std::memcpy(&prim, &tr.prim_bits, 4);
-        const uint32_t cls = (prim >= 0 && (size_t)prim < c->h_mat_idx.size()) ? (uint32_t)(t[c->h_mat_idx[prim]] & 0x7f) : 0u;
+        const int32_t keep = 0x7f & ~(c->shade_texmetal ? 0 : MT_TEXMETAL);
+        const uint32_t cls = (prim >= 0 && (size_t)prim < c->h_mat_idx.size()) ? (uint32_t)(t[c->h_mat_idx[prim]] & keep) : 0u;
         uint32_t old;
         std::memcpy(&old, &tr.pad1, 4);
         if (old != cls) { std::memcpy(&tr.pad1, &cls, 4); changed = true; }
@@ -847,6 +851,8 @@ int mpt_create(int device, void* hip_stream, MptContext** out) {
     if (const char* e = std::getenv("MPT_RESTIR_STAGED")) c->restir_staged = std::atoi(e);
     if (const char* e = std::getenv("MPT_RESTIR_BATCH")) c->restir_batch = std::atoi(e);
     if (const char* e = std::getenv("MPT_SHADE_GLASS")) c->shade_glass = std::atoi(e);
+    if (const char* e = std::getenv("MPT_SHADE_SPLIT")) c->shade_split = std::atoi(e);
+    if (const char* e = std::getenv("MPT_SHADE_TEXMETAL")) c->shade_texmetal = std::atoi(e);
     if (const char* e = std::getenv("MPT_LIGHT_BVH")) c->light_bvh = std::atoi(e);
     if (const char* e = std::getenv("MPT_OVERLAP")) c->overlap = std::atoi(e);
     if (const char* e = std::getenv("MPT_LIGHT_BVH_MAX_STACK")) c->light_bvh_max_stack = std::atoi(e);
@@ -1234,6 +1240,7 @@ static int launch_batch(MptContext* c, const MptFrame* f, int batch) {
     cfg.shade_classes = c->shade_classes;
     cfg.restir_staged = c->restir_staged;
     cfg.shade_glass = c->shade_glass;
+    cfg.shade_split = c->shade_split;
     cfg.light_bvh = c->light_bvh && c->light_bvh_ok;
     cfg.light_static = !c->h_light_prims.empty() && 2 * c->bvh_light.depth + 2 <= TRAV_LDS_STACK;
     if (restir_part) {

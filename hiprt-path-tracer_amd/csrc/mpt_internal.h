@@ -149,7 +149,8 @@ struct DevPaths {
     int32_t* nq_tgt;          // compacted query lists: [0, 3n) any hit, [3n, 4n) closest; entries slot * 4 + kind
     uint8_t* qmask;           // per slot: staged queries (bits 0..3), continuation (QM_CONT)
     uint8_t* occ;             // any-hit results, kind-major like nq_o
-    float4* nhit;             // closest NEE result per slot
+    float4* nhit;             // closest NEE result per slot; between split shading stages: shading normal + material
+    float4* s_gn;             // between split shading stages: geometric normal (k_shade's ST)
     MptMaterial* mat_slot;    // per-slot resolved material (textured materials, white furnace)
     float* fb_color;          // 3 per slot (sum)
     float* fb_albedo;
@@ -233,6 +234,10 @@ constexpr uint32_t QM_CONT = 16u;
 // mat_tex bits: a texture feeds the resolved material; the material is outside the
 // plain-dielectric class (coat, sheen, metallic, transmission or thin film may be non-zero)
 constexpr int32_t MT_TEXTURED = 1, MT_FULL = 2, MT_GLASS = 4;   // MT_GLASS: k_resolve_materials
+// MT_TEXMETAL (with MT_FULL): outside the plain class only through its metallic texture; the
+// resolved material at the hit decides (k_split sends it to the plain list, k_shade<PLAIN>
+// defers the vertices whose texel is metallic)
+constexpr int32_t MT_TEXMETAL = 8;
 constexpr int STATS_STRIDE = 6;   // per mode: traversals, nodes, tris, (unused), node slots, tri slots
 constexpr int N_STATS = N_TRACE_MODES * STATS_STRIDE;
 
@@ -274,6 +279,8 @@ struct LaunchCfg {
     int light_static;         // the light BVH's traversal stack fits in LDS (one query per lane, no spill)
     int restir_staged;        // ReSTIR DI reuse passes staged around their rays (restir_di.h), when supported
     int shade_glass;          // k_split's glass class (MPT_SHADE_GLASS)
+    int shade_split;          // plain class in stages (MPT_SHADE_SPLIT): 0 one kernel, 1 light / env / cont,
+                              // 2 light / env + cont, 3 light + env / cont
     // overlapped batch halves (mpt_api.cpp launch_batch): recorded after the bounce-0 path
     // traversal / after k_accumulate; waited for before k_accumulate (all optional)
     hipEvent_t ev_first_trace;
@@ -291,7 +298,7 @@ inline void offset_slots(DevPaths& P, size_t off) {
     // NEE record planes, and the kind-major query / occlusion planes (stride = the allocation)
     P.nthr += off; P.na += off; P.nb += off; P.ndir += off; P.nris += off; P.ne1 += off; P.ne2 += off;
     P.nq_o += off; P.nq_d += off; P.occ += off; P.nq_tgt += 4 * off;
-    P.nhit += off; P.qmask += off; P.active += off;
+    P.nhit += off; P.s_gn += off; P.qmask += off; P.active += off;
     if (P.mat_slot) P.mat_slot += off;
 }
 

@@ -1380,6 +1380,26 @@ enum ShadeOp {
     OP_DONE = 0, OP_RIS_LIGHT, OP_RIS_BSDF, OP_RIS_WIN, OP_MIS_LIGHT, OP_MIS_BSDF, OP_UNI_LIGHT, OP_BSDF_LIGHT,
     OP_ENV_LIGHT, OP_ENV_BSDF, OP_CONT, OP_RESTIR
 };
+// Shading stages (k_shade's ST): the operations of a vertex fall into three groups that run
+// in this RNG order -- light sampling (NEE / MIS / RIS / ReSTIR DI final shading), envmap
+// sampling (alias-table light sample + its BSDF-sampled MIS partner), the BSDF-sampled
+// continuation with Russian roulette.  ST = SG_ALL shades a vertex in one kernel; a split
+// launches one kernel per group (or per pair), each continuing the vertex's RNG stream where
+// the previous one stored it.  The first stage (the one with SG_LIGHT) does the hit
+// processing and leaves the surface (shading / geometric normal, material) in a per-slot
+// record for the later ones.
+enum { SG_LIGHT = 1, SG_ENV = 2, SG_CONT = 4, SG_ALL = 7 };
+DEV constexpr int op_group(int op) {
+    return op == OP_DONE ? 0 : (op == OP_ENV_LIGHT || op == OP_ENV_BSDF) ? SG_ENV : op == OP_CONT ? SG_CONT : SG_LIGHT;
+}
+// the first operation at or after `op` (in the vertex's order) that stage ST runs
+template <int ST>
+DEV int stage_op(int op, bool do_env, bool do_cont) {
+    if (!(ST & SG_LIGHT) && op_group(op) == SG_LIGHT) op = do_env ? OP_ENV_LIGHT : (do_cont ? OP_CONT : OP_DONE);
+    if (!(ST & SG_ENV) && op_group(op) == SG_ENV) op = do_cont ? OP_CONT : OP_DONE;
+    if (!(ST & SG_CONT) && op == OP_CONT) op = OP_DONE;
+    return op;
+}
 
 struct ShadeArgs {
     DevScene S;
@@ -1408,9 +1428,23 @@ struct ShadeArgs {
 #ifndef MPT_SHADE_WAVES_PLAIN
 #define MPT_SHADE_WAVES_PLAIN MPT_SHADE_WAVES
 #endif
-template <int OVR, bool PLAIN, bool EXT = false, bool GLASS = false>
-__global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_SHADE_WAVES_PLAIN : MPT_SHADE_WAVES))) void k_shade(ShadeArgs A) {
+// an operation test that a stage without the operation's group compiles out
+#define OPIS(X) ((ST & op_group(X)) && op == (X))
+// the later stages (envmap, continuation: one or two BSDF evaluations per vertex) keep the
+// per-vertex BSDF terms in registers and run at more waves
+#ifndef MPT_SHADE_WAVES_LATE
+#define MPT_SHADE_WAVES_LATE 3
+#endif
+#ifndef MPT_SHADE_PE_LDS_LATE
+#define MPT_SHADE_PE_LDS_LATE 0
+#endif
+template <int OVR, bool PLAIN, bool EXT = false, bool GLASS = false, int ST = SG_ALL>
+__global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(
+    !(ST & SG_LIGHT) ? MPT_SHADE_WAVES_LATE : (PLAIN ? MPT_SHADE_WAVES_PLAIN : MPT_SHADE_WAVES)))) void k_shade(ShadeArgs A) {
     constexpr int CLS = PLAIN ? BC_PLAIN : (GLASS ? BC_GLASS : BC_FULL);   // the BSDF code's class (dev_bsdf.h)
+    constexpr bool FIRST = (ST & SG_LIGHT) != 0;   // hit processing, AOVs, deferral, emission
+    constexpr bool LAST = (ST & SG_CONT) != 0;
+    static_assert(!EXT || ST == SG_ALL, "extended light sampling shades in one stage");
     const DevScene& S = A.S;
     const DevPaths& P = A.P;
     const MptFrame& F = *A.F;
@@ -1423,6 +1457,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_
     int i = blockIdx.x * TB + threadIdx.x;
     bool valid = i < count;
     int slot = valid ? (A.rev ? A.q_cur[-1 - i] : A.q_cur[i]) : 0;
+    if (!FIRST && slot < 0) { valid = false; slot = 0; }   // deferred by the first stage
 
     BCtx bc;
     bc.mats = S.mats;
@@ -1449,7 +1484,17 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_
         // registers: untextured materials use the per-material resolved copy, textured ones
         // (and white-furnace mode) a per-slot resolved copy written here.
         const Mat* mp = S.mats_res;
-        if (found) {
+        bool mat_in_slot = false;   // mp is the per-slot resolved copy
+        if (!FIRST) {
+            // a later stage: the surface as the first stage left it (after every flip)
+            const float4 ra = ld_s(&P.nhit[slot]), rb = ld_s(&P.s_gn[slot]);
+            sn = mk3(ra.x, ra.y, ra.z);
+            gn = mk3(rb.x, rb.y, rb.z);
+            const int mref = __float_as_int(ra.w);
+            mp = mref < 0 ? &P.mat_slot[slot] : &S.mats_res[mref];
+            ip = o + hv.x * d;
+            if (bounce == 0) d = normalize(d);
+        } else if (found) {
             // trace_ray hit processing (Intersect.h:154-216)
             float t = hv.x;
             v2 uv = mk2(hv.y, hv.z);
@@ -1462,6 +1507,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_
             if (F.bsdf_flags.white_furnace_mode || (S.mat_tex[mi] & MT_TEXTURED)) {
                 P.mat_slot[slot] = intersection_material(S, mi, tc, F.bsdf_flags.white_furnace_mode);
                 mp = &P.mat_slot[slot];
+                mat_in_slot = true;
             } else {
                 mp = &S.mats_res[mi];
             }
@@ -1477,7 +1523,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_
                 vs.wl = -(rng() * (float)(830 - 360) + (float)360);
         }
         const Mat& m = *mp;
-        if (bounce == 0) {
+        if (FIRST && bounce == 0) {
             // CameraRays G-buffer hand-off (CameraRays.h:147-166) and FullPathTracer's
             // re-read of it (FullPathTracer.h:131-150): emissive flip, normalise, restart RNG
             if (found && is_emissive(m) && dot(-d, gn) < 0) { gn = -gn; sn = -sn; }
@@ -1486,10 +1532,11 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_
             d = normalize(d);
             rng = make_rng(P.seeds[slot].y);   // path_seed(F, P, slot, false), from k_camera
         }
-        if (PLAIN) {
+        if (PLAIN && FIRST) {
             // principled_eval_pre's 'outside' with the normal the vertex is shaded with
             const v3 sn_f = (is_emissive(m) && dot(-d, gn) < 0) ? -sn : sn;
-            if (!(dot(-d, sn_f) > 0 || m.thin_walled) || A.force_defer) {
+            // (a material of the MT_TEXMETAL class is shaded here where its texel is not metallic)
+            if (!(dot(-d, sn_f) > 0 || m.thin_walled) || m.metallic != 0.0f || A.force_defer) {
                 A.q_defer[atomicAdd(A.count_defer, 1)] = slot;
                 atomicAdd(&P.counters[CTR_DEFER], 1);
                 A.q_cur[i] = -1;    // k_compact / k_resolve skip the entry here
@@ -1499,14 +1546,14 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_
         uint32_t fl = 0;
         uint32_t qm = 0;            // staged NEE queries (bits 0..3) + continuation (bit 4)
         if (found) {
-            if (bounce == 0) {
+            if (FIRST && bounce == 0) {
                 float4 a = P.alb[slot], n4 = P.nrm[slot];
                 P.alb[slot] = make_float4(a.x + m.base_color.r, a.y + m.base_color.g, a.z + m.base_color.b, 0.0f);
                 P.nrm[slot] = make_float4(n4.x + sn.x, n4.y + sn.y, n4.z + sn.z, 0.0f);
             }
-            if (is_emissive(m) && dot(-d, gn) < 0) { gn = -gn; sn = -sn; }
+            if (FIRST && is_emissive(m) && dot(-d, gn) < 0) { gn = -gn; sn = -sn; }
             v3 view = -d;
-            fl |= NF_SHADED;
+            if (FIRST) fl |= NF_SHADED;
             const int lss = F.options.direct_light_sampling;
             const MptWorldSettings& ws = F.world_settings;
             // ---------------- which BSDF operations this vertex runs, in RNG order ----------------
@@ -1517,7 +1564,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_
                             !(F.bsdf_flags.white_furnace_mode && F.bsdf_flags.white_furnace_mode_turn_off_emissives);
             if (do_light && is_emissive(m)) {
                 do_light = false;
-                if (m.emissive_texture_used && bounce > 0) {
+                if (FIRST && m.emissive_texture_used && bounce > 0) {
                     fl |= NF_IMM;
                     const Col e = emission_of(m);
                     st_s(&P.na[slot], make_float4(e.r, e.g, e.b, 0.0f));
@@ -1527,7 +1574,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_
             const int lssb = bounce_lss(F, bounce);
             // sample_lights_RIS returns 0 without emissive triangles (RIS.h:292-302)
             if (restir && bounce > 0 && S.n_emissive == 0 && lssb == MPT_LSS_RIS_BSDF_AND_LIGHT) do_light = false;
-            if (do_light) fl |= NF_L;
+            if (FIRST && do_light) fl |= NF_L;
             const bool do_env = ws.ambient_light_type == MPT_AMBIENT_ENVMAP && !F.bsdf_flags.white_furnace_mode &&
                                 !is_emissive(m) && ws.envmap_intensity > 0.0f && F.options.envmap_sampling != MPT_ESS_NO_SAMPLING &&
                                 !(restir && bounce == 0);
@@ -1545,6 +1592,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_
                 else if (lssb == MPT_LSS_BSDF) op = OP_BSDF_LIGHT;
             }
             if (op == OP_DONE) op = do_env ? OP_ENV_LIGHT : (do_cont ? OP_CONT : OP_DONE);
+            op = stage_op<ST>(op, do_env, do_cont);
             // RIS reservoir (sample_bsdf_and_lights_RIS_reservoir, RIS.h:82-289)
             float wsum = 0.0f, targetW = 0.0f;
             v3 pointW = mk3(0, 0, 0);
@@ -1560,15 +1608,17 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_
             // occupancy leaves free (-mllvm -disable-promote-alloca-to-lds: 160 B of scratch per
             // lane instead); two blocks fill a CU's 160 KB, so LDS and VGPRs (238) both cap the
             // kernel at 2 waves / SIMD
-            __shared__ PEval pe_lds[TB];
-            PEval& pe = pe_lds[threadIdx.x];
+            constexpr bool PE_LDS = (ST & SG_LIGHT) || MPT_SHADE_PE_LDS_LATE;
+            __shared__ PEval pe_lds[PE_LDS ? TB : 1];
+            PEval pe_reg;
+            PEval& pe = PE_LDS ? pe_lds[threadIdx.x] : pe_reg;
             // the first light sample's emissive record, loaded while the per-vertex BSDF terms are
             // computed (its index is the vertex's next draw); each RIS light candidate then loads
             // the next one's record (the draws between them are fixed: two for the point, one for
             // the reservoir) while it is evaluated
             EmPrefetch pf;
             pf.valid = false;
-            if (MPT_EM_PREFETCH && (op == OP_RIS_LIGHT || op == OP_MIS_LIGHT || op == OP_UNI_LIGHT)) pf.issue(S, rng);
+            if (MPT_EM_PREFETCH && (ST & SG_LIGHT) && (op == OP_RIS_LIGHT || op == OP_MIS_LIGHT || op == OP_UNI_LIGHT)) pf.issue(S, rng);
             SECT(0);
             bsdf_eval_pre<OVR, CLS>(bc, m, vs, view, sn, pe);
             SECT(5);
@@ -1596,11 +1646,11 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_
                 Col ec = col(0.0f);
                 bool inner = false;
                 float4 etex = make_float4(0.0f, 0.0f, 0.0f, 0.0f);   // OP_ENV_BSDF: the envmap texel along L
-                if (op == OP_RIS_BSDF || op == OP_MIS_BSDF || op == OP_BSDF_LIGHT || op == OP_ENV_BSDF || op == OP_CONT) {
+                if (OPIS(OP_RIS_BSDF) || OPIS(OP_MIS_BSDF) || OPIS(OP_BSDF_LIGHT) || OPIS(OP_ENV_BSDF) || OPIS(OP_CONT)) {
                     do_eval = bsdf_sample_dir<OVR, CLS>(bc, m, tv, view, sn, gn, L, rng);
                     // the texel's load is issued here and waited for after the evaluation
-                    if (MPT_ENV_EARLY && op == OP_ENV_BSDF && do_eval) etex = env_fetch(S, F, L);
-                } else if (op == OP_RIS_LIGHT) {
+                    if (MPT_ENV_EARLY && OPIS(OP_ENV_BSDF) && do_eval) etex = env_fetch(S, F, L);
+                } else if (OPIS(OP_RIS_LIGHT)) {
                     lp = pf.sample(S, rng, lpdf, li);
                     if (MPT_EM_PREFETCH && ris_c + 1 < nl) {   // the next candidate's index draw follows this one's reservoir draw
                         Rng nx = rng;
@@ -1620,7 +1670,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_
                             if (min_contrib(rs.minimum_light_contribution, li.emission / lpdf)) { L = tl; do_eval = true; }
                         }
                     }
-                } else if (op == OP_RIS_WIN) {
+                } else if (OPIS(OP_RIS_WIN)) {
                     // evaluate_reservoir_sample for the light winner (RIS.h:18-80), speculatively
                     v3 ep2 = ip + sn * 1.0e-4f;
                     v3 sd = pointW - ep2;
@@ -1630,11 +1680,11 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_
                     // outside the surface the winner's direction is bit-identical to its
                     // candidate's (same origin), and so is the evaluation: reuse it
                     do_eval = hasW && ism != 1.0f;
-                } else if (op == OP_MIS_LIGHT || op == OP_UNI_LIGHT) {
+                } else if (OPIS(OP_MIS_LIGHT) || OPIS(OP_UNI_LIGHT)) {
                     // sample_one_light_MIS (Lights.h:115-220) / _no_MIS (Lights.h:22-65)
                     lp = pf.sample(S, rng, lpdf, li);
                     if (lpdf > 0.0f) {
-                        v3 so = op == OP_MIS_LIGHT ? ep : ip + sn * 1.0e-4f;
+                        v3 so = OPIS(OP_MIS_LIGHT) ? ep : ip + sn * 1.0e-4f;
                         v3 sd = lp - so;
                         dist = length(sd);
                         L = sd / dist;
@@ -1642,7 +1692,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_
                         lp = so;
                         do_eval = geo > 0.0f;
                     }
-                } else if (op == OP_RESTIR) {
+                } else if (OPIS(OP_RESTIR)) {
                     // sample_light_ReSTIR_DI + evaluate_ReSTIR_DI_reservoir (FinalShading.h:16-115);
                     // a batched ReSTIR DI launch reads the sample's kept final reservoirs
                     float4* rsb = P.rs_out;
@@ -1664,7 +1714,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_
                         else { L = rres.point - ip; dist = length(L); L = L / dist; }
                         do_eval = true;
                     }
-                } else if (op == OP_ENV_LIGHT) {
+                } else if (OPIS(OP_ENV_LIGHT)) {
                     ec = env_sample(S, F, L, lpdf, rng);
                     geo = dot(sn, L);
                     do_eval = lpdf > 0.0f && geo > 0.0f;
@@ -1678,7 +1728,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_
                 if (do_eval) f = bsdf_eval_post<OVR, CLS>(bc, m, tv, pe, sn, L, pdf);
                 SECT(2);
                 int next = OP_DONE;
-                if (op == OP_RIS_LIGHT) {
+                if (OPIS(OP_RIS_LIGHT)) {
                     float target = 0.0f, cw = 0.0f;
                     if (inner) {
                         float bp = 0.0f;
@@ -1693,7 +1743,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_
                     if (rng() < cw / wsum) { hasW = true; targetW = target; pointW = lp; triW = li.tri; fW = f; pdfW = pdf; }
                     ris_c++;
                     next = ris_c < nl ? OP_RIS_LIGHT : (nbc > 0 ? OP_RIS_BSDF : OP_RIS_WIN);
-                } else if (op == OP_RIS_BSDF) {
+                } else if (OPIS(OP_RIS_BSDF)) {
                     bool refr = dot(L, sn * ism) < 0;
                     v3 so = refr ? ip + sn * 1.0e-4f * ism * -1.0f : ep;
                     if (pdf > 0.0f) {
@@ -1704,7 +1754,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_
                     }
                     r_add = rng();
                     next = OP_RIS_WIN;
-                } else if (op == OP_RIS_WIN) {
+                } else if (OPIS(OP_RIS_WIN)) {
                     if (!do_eval) { f = fW; pdf = pdfW; }
                     st_s(&P.nris[slot], make_float4(wsum, targetW, r_add, __int_as_float(triW)));
                     if (hasW) {
@@ -1713,7 +1763,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_
                         st_s(&P.na[slot], make_float4(f.r, f.g, f.b, maxr(0.0f, dot(sn, L))));
                     }
                     next = OP_DONE;
-                } else if (op == OP_MIS_LIGHT) {
+                } else if (OPIS(OP_MIS_LIGHT)) {
                     if (do_eval && pdf != 0.0f) {
                         float lp2 = lpdf;
                         lp2 *= dist * dist;
@@ -1726,7 +1776,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_
                         stage_query(P, slot, 0, qm, lp, prim, L, dist - 1.0e-4f);
                     }
                     next = lpdf > 0.0f ? OP_MIS_BSDF : OP_DONE;
-                } else if (op == OP_MIS_BSDF) {
+                } else if (OPIS(OP_MIS_BSDF)) {
                     bool refr = dot(L, sn * ism) < 0;
                     v3 bo = refr ? ip + sn * 1.0e-4f * ism * -1.0f : ep;
                     if (pdf > 0) {
@@ -1735,7 +1785,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_
                         st_s(&P.nb[slot], make_float4(f.r, f.g, f.b, pdf));
                         st_s(&P.ndir[slot], make_float4(L.x, L.y, L.z, absr(dot(sn, L))));
                     }
-                } else if (op == OP_UNI_LIGHT) {
+                } else if (OPIS(OP_UNI_LIGHT)) {
                     if (do_eval && pdf != 0.0f) {
                         float lp2 = lpdf;
                         lp2 *= dist * dist;
@@ -1746,7 +1796,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_
                         fl |= NF_A;
                         stage_query(P, slot, 0, qm, lp, prim, L, dist - 1.0e-4f);
                     }
-                } else if (op == OP_BSDF_LIGHT) {
+                } else if (OPIS(OP_BSDF_LIGHT)) {
                     // sample_one_light_bsdf (Lights.h:67-113)
                     bool refr = dot(L, sn * ism) < 0;
                     if (pdf > 0.0f) {
@@ -1756,7 +1806,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_
                         st_s(&P.nb[slot], make_float4(f.r, f.g, f.b, pdf));
                         st_s(&P.ndir[slot], make_float4(L.x, L.y, L.z, maxr(0.0f, dot(sn, L))));
                     }
-                } else if (op == OP_RESTIR) {
+                } else if (OPIS(OP_RESTIR)) {
                     if (do_eval) {
                         float c = dot(sn, L);
                         if (rres.flags & RF_BSDF_REFRACTION) c = absr(c);
@@ -1773,7 +1823,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_
                             }
                         }
                     }
-                } else if (op == OP_ENV_LIGHT) {
+                } else if (OPIS(OP_ENV_LIGHT)) {
                     // Envmap.h:151-246
                     if (do_eval) {
                         float mw = F.options.envmap_bsdf_mis ? balance(lpdf, pdf) : 1.0f;
@@ -1788,7 +1838,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_
                         }
                     }
                     next = F.options.envmap_bsdf_mis ? OP_ENV_BSDF : OP_DONE;
-                } else if (op == OP_ENV_BSDF) {
+                } else if (OPIS(OP_ENV_BSDF)) {
                     float c2 = absr(dot(sn, L));
                     if (pdf > 0.0f) {
                         float epdf;
@@ -1801,7 +1851,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_
                             stage_query(P, slot, 2, qm, ip, prim, L, 1.0e35f - 1.0e-4f);
                         }
                     }
-                } else if (op == OP_CONT) {
+                } else if (OPIS(OP_CONT)) {
                     // continuation (FullPathTracer.h:221-247)
 #ifdef MPT_DEBUG_SLOT
                     if (slot == MPT_DEBUG_SLOT) printf("GPU b%d cont mi %d vs %d %d %d %d st %x %x %x L %a %a %a f %a %a %a pdf %a\n", bounce, (int)(mp - S.mats_res), tv.incident, tv.outgoing, (int)tv.inside, tv.pos, tv.st[0], tv.st[1], tv.st[2], L.x, L.y, L.z, f.r, f.g, f.b, pdf);
@@ -1838,27 +1888,42 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PLAIN ? MPT_
                 // after the light strategy: envmap, then the continuation
                 if (next == OP_DONE && op != OP_ENV_LIGHT && op != OP_ENV_BSDF && do_env) next = OP_ENV_LIGHT;
                 else if (next == OP_DONE && do_cont) next = OP_CONT;
-                op = next < 0 ? OP_DONE : next;
+                op = next < 0 ? OP_DONE : stage_op<ST>(next, do_env, do_cont);
                 SECT(3);
             }
-            // emission (FullPathTracer.h:192-214)
-            if (lss == MPT_LSS_NO_DIRECT_LIGHT_SAMPLING) {
+            // emission (FullPathTracer.h:192-214); without direct light sampling no later stage
+            // sets a NEE flag (env_use), so the first stage's clearing covers the vertex
+            if (FIRST && lss == MPT_LSS_NO_DIRECT_LIGHT_SAMPLING) {
                 Col he = clamp_contrib(emission_of(m), rs.indirect_contribution_clamp, bounce > 0);
                 rcol += he * thr_vertex;
                 fl &= ~(NF_A | NF_B | NF_E1 | NF_E2 | NF_RIS_W | NF_IMM | NF_L);
                 fl |= NF_NOADD;
-            } else if (bounce == 0) {
+            } else if (FIRST && bounce == 0) {
                 rcol += emission_of(m);
+            }
+            if (FIRST && !LAST) {   // the surface record of the later stages
+                const int mref = mat_in_slot ? -1 : (int)(mp - S.mats_res);
+                st_s(&P.nhit[slot], make_float4(sn.x, sn.y, sn.z, __int_as_float(mref)));
+                st_s(&P.s_gn[slot], make_float4(gn.x, gn.y, gn.z, 0.0f));
             }
         } else {
             rcol += miss_radiance(S, F, bounce, d, thr);   // not reached: k_split sends misses to k_miss
         }
-        st_s(&P.nthr[slot], make_float4(thr_vertex.r, thr_vertex.g, thr_vertex.b, __uint_as_float(fl)));
-        st_s(&P.qmask[slot], (uint8_t)(qm | (cont ? QM_CONT : 0u)));
+        const uint32_t qb = qm | (cont ? QM_CONT : 0u);
+        if (FIRST) {
+            st_s(&P.nthr[slot], make_float4(thr_vertex.r, thr_vertex.g, thr_vertex.b, __uint_as_float(fl)));
+            st_s(&P.qmask[slot], (uint8_t)qb);
+            st_s(&P.col[slot], make_float4(rcol.r, rcol.g, rcol.b, 0.0f));
+        } else {
+            if (fl) {
+                const float4 t4 = ld_s(&P.nthr[slot]);
+                st_s(&P.nthr[slot], make_float4(t4.x, t4.y, t4.z, __uint_as_float(__float_as_uint(t4.w) | fl)));
+            }
+            if (qb) st_s(&P.qmask[slot], (uint8_t)(ld_s(&P.qmask[slot]) | qb));
+        }
         st_s(&P.rng[slot], rng.s);
-        st_s(&P.thr[slot], make_float4(thr.r, thr.g, thr.b, 0.0f));
-        st_s(&P.col[slot], make_float4(rcol.r, rcol.g, rcol.b, 0.0f));
-        vs_store_s(P.vsA, P.vsB, slot, vs);
+        if (LAST) st_s(&P.thr[slot], make_float4(thr.r, thr.g, thr.b, 0.0f));
+        if (FIRST || LAST) vs_store_s(P.vsA, P.vsB, slot, vs);
     }
     // queue appends (every lane of the wave takes part in the ballots)
     SECT(4);
@@ -1964,7 +2029,7 @@ __global__ __launch_bounds__(CP_NT) void k_split(DevScene S, DevPaths P, const i
         if (hc != 0xffu) {
             const int32_t mt = classes ? (int32_t)hc : 0;
             if (classes == 2 && (mt & MT_GLASS)) { gm |= 1u << j; ng++; }
-            else if (mt & MT_FULL) { fm |= 1u << j; nf++; }
+            else if ((mt & MT_FULL) && !(mt & MT_TEXMETAL)) { fm |= 1u << j; nf++; }
             else { hm |= 1u << j; nh++; }
         }
     }
@@ -2398,6 +2463,7 @@ __global__ __launch_bounds__(TB) void k_accumulate(DevPaths P, const MptFrame* _
 void part_shade_generic(dim3 g, hipStream_t st, const ShadeArgs& a);          // k_shade<NONE, false>
 void part_shade_plain(dim3 g, hipStream_t st, const ShadeArgs& a);            // k_shade<NONE, true>
 void part_shade_glass(dim3 g, hipStream_t st, const ShadeArgs& a);            // k_shade<NONE, false, false, true>
+void part_shade_plain_stage(int stage, dim3 g, hipStream_t st, const ShadeArgs& a);   // k_shade<NONE, true, false, false, stage>
 void part_shade_ext(dim3 g, hipStream_t st, const ShadeArgs& a);              // k_shade<NONE, false, true>
 void part_shade_override(int ovr, bool ext, dim3 g, hipStream_t st, const ShadeArgs& a);   // Lambert, Oren-Nayar
 enum RestirKernel { RK_INITIAL, RK_SPATIOTEMPORAL, RK_SPATIOTEMPORAL_ANY, RK_SPATIAL, RK_SPATIAL_ANY, RK_TEMPORAL, RK_SP_SELECT,
@@ -2735,7 +2801,20 @@ static void frame_bounces(const DevScene& S, DevPaths& P, const MptFrame* d_fram
             if (hf.options.bsdf_override != MPT_BSDF_NONE) part_shade_override(hf.options.bsdf_override, ext, sg, st, sa);
             else if (ext) part_shade_ext(sg, st, sa);
             else if (!classes) part_shade_generic(sg, st, sa);
-            else part_shade_plain(sg, st, sa);
+            else if (cfg.shade_split) {
+                // the plain class in stages (k_shade's ST); a stage whose groups have no work
+                // in this bounce is not launched
+                static const int splits[3][3] = {{SG_LIGHT, SG_ENV, SG_CONT}, {SG_LIGHT, SG_ENV | SG_CONT, 0},
+                                                 {SG_LIGHT | SG_ENV, SG_CONT, 0}};
+                const MptWorldSettings& ws = hf.world_settings;
+                const bool env = ws.ambient_light_type == MPT_AMBIENT_ENVMAP && !hf.bsdf_flags.white_furnace_mode &&
+                                 ws.envmap_intensity > 0.0f && hf.options.envmap_sampling != MPT_ESS_NO_SAMPLING &&
+                                 !(hf.options.direct_light_sampling == MPT_LSS_RESTIR_DI && b == 0);
+                const int work = SG_LIGHT | (env ? SG_ENV : 0) | (b < nb ? SG_CONT : 0);
+                const int* sp = splits[std::min(std::max(cfg.shade_split, 1), 3) - 1];
+                for (int k = 0; k < 3 && sp[k]; k++)
+                    if (sp[k] & work) part_shade_plain_stage(sp[k], sg, st, sa);
+            } else part_shade_plain(sg, st, sa);
         }
         if (classes) {
             TimedScope ts(cfg, st, KT_SHADE_GENERIC);
@@ -2955,7 +3034,12 @@ __global__ void k_resolve_materials(DevScene S, MptMaterial* out, int32_t* tex, 
     const bool glass = !plain && r.coat == 0.0f && r.sheen == 0.0f && r.metallic == 0.0f && r.thin_film == 0.0f &&
                        m.coat_texture_index == MPT_NO_TEXTURE && m.sheen_texture_index == MPT_NO_TEXTURE &&
                        m.metallic_texture_index == MPT_NO_TEXTURE && m.roughness_metallic_texture_index == MPT_NO_TEXTURE;
-    tex[i] = (textured ? MT_TEXTURED : 0) | (plain ? 0 : MT_FULL) | (glass ? MT_GLASS : 0);
+    // plain but for a metallic texture: per hit, by the resolved metallic value
+    const bool texmetal = !plain && r.coat == 0.0f && r.sheen == 0.0f && r.specular_transmission == 0.0f && r.thin_film == 0.0f &&
+                          m.coat_texture_index == MPT_NO_TEXTURE && m.sheen_texture_index == MPT_NO_TEXTURE &&
+                          m.specular_transmission_texture_index == MPT_NO_TEXTURE &&
+                          (m.roughness_metallic_texture_index != MPT_NO_TEXTURE || m.metallic_texture_index != MPT_NO_TEXTURE);
+    tex[i] = (textured ? MT_TEXTURED : 0) | (plain ? 0 : MT_FULL) | (glass ? MT_GLASS : 0) | (texmetal ? MT_TEXMETAL : 0);
 }
 
 

@@ -3,7 +3,7 @@
 // so that the shading and ReSTIR DI kernels compile in parallel.  mpt_kernels.hip's host glue
 // launches them through these functions.
 #ifndef MPT_TU_PART
-#error "compile with -DMPT_TU_PART=<1..6>"
+#error "compile with -DMPT_TU_PART=<1..7>"
 #endif
 #include "mpt_kernels.hip"
 
@@ -24,6 +24,19 @@ extern "C" int mpt_debug_sections(unsigned long long* out, int reset) {   // k_s
     return 0;
 }
 #endif
+#elif MPT_TU_PART == 7
+// the plain class shaded in stages (k_shade's ST: SG_* groups; LaunchCfg::shade_split)
+void part_shade_plain_stage(int stage, dim3 g, hipStream_t st, const ShadeArgs& a) {
+    switch (stage) {
+    case SG_LIGHT: hipLaunchKernelGGL((k_shade<MPT_BSDF_NONE, true, false, false, SG_LIGHT>), g, dim3(TB), 0, st, a); break;
+    case SG_ENV: hipLaunchKernelGGL((k_shade<MPT_BSDF_NONE, true, false, false, SG_ENV>), g, dim3(TB), 0, st, a); break;
+    case SG_CONT: hipLaunchKernelGGL((k_shade<MPT_BSDF_NONE, true, false, false, SG_CONT>), g, dim3(TB), 0, st, a); break;
+    case SG_LIGHT | SG_ENV:
+        hipLaunchKernelGGL((k_shade<MPT_BSDF_NONE, true, false, false, SG_LIGHT | SG_ENV>), g, dim3(TB), 0, st, a);
+        break;
+    default: hipLaunchKernelGGL((k_shade<MPT_BSDF_NONE, true, false, false, SG_ENV | SG_CONT>), g, dim3(TB), 0, st, a); break;
+    }
+}
 #elif MPT_TU_PART == 3
 void part_shade_ext(dim3 g, hipStream_t st, const ShadeArgs& a) {
     hipLaunchKernelGGL((k_shade<MPT_BSDF_NONE, false, true>), g, dim3(TB), 0, st, a);

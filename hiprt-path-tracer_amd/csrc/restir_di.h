@@ -534,7 +534,10 @@ __global__ __launch_bounds__(TB) void k_restir_presample(DevScene S, DevPaths P,
 // condition k_shade<PLAIN> checks before it shades, principled_eval_pre's 'outside')
 DEV bool rs_plain(const DevScene& S, const DevPaths& P, int pix, const RSurf& g, bool prev = false) {
     const int mi = (prev ? P.pgb_meta[pix].y : P.gb_meta[pix].y) - 1;
-    return mi >= 0 && !(S.mat_tex[mi] & MT_FULL) && (dot(g.view, g.sn) > 0.0f || g.m->thin_walled);
+    if (mi < 0) return false;
+    const int32_t mt = S.mat_tex[mi];
+    // MT_TEXMETAL: plain where the resolved (per-pixel) material's texel is not metallic
+    return (!(mt & MT_FULL) || ((mt & MT_TEXMETAL) && g.m->metallic == 0.0f)) && (dot(g.view, g.sn) > 0.0f || g.m->thin_walled);
 }
 
 // ---- ReSTIR_DI_InitialCandidates (InitialCandidates.h:24-508) ------------------------

@@ -22,7 +22,7 @@ OBJ_DIR = CSRC / "build"
 SOURCES = ["bvh8.cpp", "mpt_kernels.hip", "bake.hip", "mpt_api.cpp", "image.cpp", "jpeg.cpp"]
 # mpt_part.hip is compiled once per part (-DMPT_TU_PART=k): the shading and ReSTIR DI kernel
 # instantiations, so that they compile in parallel with the rest
-PARTS = [1, 2, 3, 4, 5, 6]
+PARTS = [1, 2, 3, 4, 5, 6, 7]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 CXXFLAGS = [

@@ -82,3 +82,62 @@ def test_glass_class(monkeypatch, luts, name, strategy, bounces):
     frs = frames(sd, 40, 30, 2, lss=STRATEGIES[strategy], bounces=bounces)
     out = _render_modes(monkeypatch, sd, luts, frs, var="MPT_SHADE_GLASS", modes=(0, 1))
     _assert_modes_equal(out, oracle_for(sd, luts).render(frs, aov=True), f"{name} glass class")
+
+
+STAGE_STRATEGIES = ["mis", "ris", "uniform", "bsdf", "none"]
+
+
+@pytest.mark.parametrize("strategy", STAGE_STRATEGIES)
+def test_plain_stages_cornell_envmap(monkeypatch, luts, strategy):
+    """The plain class shaded in stages (MPT_SHADE_SPLIT: 1 light / envmap / continuation, 2
+    light / envmap + continuation, 3 light + envmap / continuation; k_shade's ST): each stage
+    continues the vertex's RNG stream and the later ones read the first one's surface record,
+    so every split equals the one-kernel shading (0) and the oracle -- under an envmap (the
+    envmap stage), with every light strategy, incl. no direct light sampling (the first stage
+    clears the NEE flags for all)."""
+    sd = scene.load_scene("cornell_pbr")
+    env = mpt.build_envmap(scene.procedural_sky(64, 32, seed=3))
+    frs = frames(sd, 40, 28, 2, lss=STRATEGIES[strategy], world=scene.envmap_world(0.7))
+    out = _render_modes(monkeypatch, sd, luts, frs, env=env, var="MPT_SHADE_SPLIT", modes=(0, 1, 2, 3))
+    _assert_modes_equal(out, oracle_for(sd, luts, env).render(frs, aov=True), f"cornell stages {strategy}")
+
+
+def test_plain_stages_city_band_batched(monkeypatch, luts):
+    """The bench workload on a band (textured alpha-tested leaf cards: per-slot resolved
+    materials in the surface record) under each split, as one batched wavefront."""
+    from mpt import synthetic
+    city = synthetic.procedural_city(1234)
+    env = mpt.build_envmap(scene.procedural_sky(512, 256, seed=7))
+    frs = frames(city, 1920, 1080, 2, lss=abi.LSS_RIS_BSDF_AND_LIGHT, world=scene.envmap_world(1.0), band=(8, 3, 64))
+    for f in frs:
+        f.render_settings.do_alpha_testing = True
+    out = _render_modes(monkeypatch, city, luts, frs, env=env, batch=2, var="MPT_SHADE_SPLIT", modes=(0, 1, 3))
+    _assert_modes_equal(out, oracle_for(city, luts, env).render(frs, aov=True), "city band stages")
+
+
+@pytest.mark.parametrize("strategy", ["mis", "ris"])
+def test_texture_decided_plain_class(monkeypatch, luts, strategy):
+    """MT_TEXMETAL (k_resolve_materials): a material outside the plain class only through its
+    metallic / roughness-metallic texture goes to the plain list (k_split), and k_shade<PLAIN>
+    defers the vertices whose resolved texel is metallic.  The textured-panel scene's panel 0
+    (roughness-metallic texture, metallic 0 / 0.5 / 1 texels) is such a material: with the
+    routing on (MPT_SHADE_TEXMETAL=1, the default) fewer vertices reach the generic kernel,
+    and the frames equal the routing off and the oracle, bit for bit."""
+    from mpt import synthetic
+    sd = synthetic.with_textured_panels(scene.load_scene("cornell_pbr"))
+    env = mpt.build_envmap(scene.procedural_sky(64, 32, seed=5))
+    frs = frames(sd, 48, 32, 2, lss=STRATEGIES[strategy], world=scene.envmap_world(0.6))
+    out, generic = {}, {}
+    for mode in (0, 1):
+        monkeypatch.setenv("MPT_SHADE_TEXMETAL", str(mode))
+        r = mpt.GPURenderer(0)
+        try:
+            r.set_scene(sd)
+            r.set_luts(luts)
+            r.set_envmap(env)
+            out[mode] = gpu_render(r, frs)
+            generic[mode] = r.stats().shade_generic_vertices
+        finally:
+            r.close()
+    _assert_modes_equal(out, oracle_for(sd, luts, env).render(frs, aov=True), f"panels texmetal {strategy}")
+    assert 0 < generic[1] < generic[0], generic

@@ -1,6 +1,7 @@
 """Runs bench.py once per libmpt variant (MPT_LIB_PATH) and prints the per-kernel times.
 Development tool for A/B experiments on the GPU box:
     python tools/bench_variants.py path/to/a/libmpt.so path/to/b/libmpt.so [-- bench args]
+A variant may carry environment settings: path/to/libmpt.so@MPT_SHADE_SPLIT=1,MPT_X=2
 """
 import json
 import os
@@ -16,16 +17,18 @@ def main():
     if "--" in args:
         i = args.index("--")
         args, extra = args[:i], args[i + 1:]
-    for lib in args:
+    for spec in args:
+        lib, _, sets = spec.partition("@")
         env = dict(os.environ, MPT_LIB_PATH=os.path.abspath(lib))
+        env.update(kv.split("=", 1) for kv in sets.split(",") if kv)
         cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "16", "--warmup", "2", "--no-cpu-baseline", *extra]
         r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
         if r.returncode != 0:
-            print(lib, "FAILED", r.returncode, r.stderr[-2000:], flush=True)
+            print(spec, "FAILED", r.returncode, r.stderr[-2000:], flush=True)
             sys.exit(r.returncode)
         line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
         j = json.loads(line)
-        print(json.dumps({"lib": lib, "ms_per_step": j["ms_per_step"], "value": j["value"],
+        print(json.dumps({"lib": spec, "ms_per_step": j["ms_per_step"], "value": j["value"],
                           "kernels": j["kernel_ms_per_step"], "trav": j.get("traversal_stages")}), flush=True)
 
 
