@@ -417,6 +417,17 @@ def main():
                   "total_ms": st.shade_ms, "avg_launch_ms": s_avg, "bytes_per_unit": b_vtx, "unit_of_work": "path vertex (hit)",
                   "units_per_launch": hits / sl, "launches": st.shade_launches,
                   "achieved": hits * b_vtx / sl / (s_avg * 1e-3) / 1e9 if s_avg > 0 else 0.0})
+    # the generic class (every other material, incl. the vertices the plain kernel deferred);
+    # launched once per bounce beside the plain kernel, same bytes per vertex
+    if st.shade_generic_vertices and st.shade_generic_ms > 0:
+        g_avg = st.shade_generic_ms / sl
+        lines.append({"kernel": "k_shade<BSDF_NONE, generic> (path vertex of any other material: coat, sheen, metal, "
+                                "thin film, transmission, metallic texels)",
+                      "symbol": "void mpt::k_shade<0, false, false, false",
+                      "total_ms": st.shade_generic_ms, "avg_launch_ms": g_avg, "bytes_per_unit": b_vtx,
+                      "unit_of_work": "path vertex (hit)", "units_per_launch": st.shade_generic_vertices / sl,
+                      "launches": st.shade_launches,
+                      "achieved": st.shade_generic_vertices * b_vtx / sl / (g_avg * 1e-3) / 1e9})
     # ReSTIR DI (C4): the staged reuse passes' plain-class target-function evaluations, timed on
     # their own (HIP events around every k_rsp_eval<OVR, true, *> launch, fused and spatial); per
     # evaluation item: item 4 + its record 16 read + 4 written + the evaluated

@@ -185,12 +185,13 @@ DEV v3 cosine_sample_z_up(Rng& rng) {
     const float2 sc = psincos(phi);
     return normalize(mk3(sc.y * st, sc.x * st, ct));
 }
-DEV Col lambert_eval(const Mat& m, float NoL, float& pdf) {
+DEV Col lambert_eval_c(Col base, float NoL, float& pdf) {
     pdf = 0.0f;
     if (NoL <= 0.0f) return col(0.0f);
     pdf = NoL * INV_PI;
-    return C3(m.base_color) * INV_PI;
+    return base * INV_PI;
 }
+DEV Col lambert_eval(const Mat& m, float NoL, float& pdf) { return lambert_eval_c(C3(m.base_color), NoL, pdf); }
 DEV Col lambert_sample(const Mat& m, v3 n, v3& dir, float& pdf, Rng& rng) {
     dir = cosine_sample_around(n, rng);
     return lambert_eval(m, dot(n, dir), pdf);
@@ -526,14 +527,17 @@ DEV float thin_walled_roughness(bool thin, float r, float eta) {
 enum : int { BC_PLAIN = 0, BC_FULL = 1, BC_GLASS = 2 };
 DEV constexpr bool bc_extra(int cls) { return cls == BC_FULL; }    // sheen, metal, thin film, coat / sheen sampling
 DEV constexpr bool bc_layers(int cls) { return cls != BC_PLAIN; }  // coat evaluation, glass lobe
+// (ior, tf: the material's ior and thin_film, from the PEval snapshot in the evaluations)
 template <int FULL = BC_FULL>
-DEV Col spec_fresnel(const Mat& m, float rel, float ci) {
-    float above = m.ior / rel;
+DEV Col spec_fresnel_v(const Mat& m, float ior, float tf, float rel, float ci) {
+    float above = ior / rel;
     Col Fs = col(0.0f), Ft = col(0.0f);
-    if (m.thin_film < 1.0f) Fs = col(fresnel_dielectric(ci, rel));
-    if (bc_extra(FULL) && m.thin_film > 0.0f) Ft = thin_film_fresnel(m, above, ci);
-    return lerpc(Fs, Ft, m.thin_film);
+    if (tf < 1.0f) Fs = col(fresnel_dielectric(ci, rel));
+    if (bc_extra(FULL) && tf > 0.0f) Ft = thin_film_fresnel(m, above, ci);
+    return lerpc(Fs, Ft, tf);
 }
+template <int FULL = BC_FULL>
+DEV Col spec_fresnel(const Mat& m, float rel, float ci) { return spec_fresnel_v<FULL>(m, m.ior, m.thin_film, rel, ci); }
 DEV float ior_or_air(const BCtx& c, int idx) { return idx == MAX_MAT ? 1.0f : c.mats[idx].ior; }
 
 template <int FULL = BC_FULL>
@@ -668,6 +672,11 @@ struct PEval {
     bool spec_ok;
     Col spec_tint, spec_vdf, spec_dark;
     float gbc, ccc;
+    // the material fields every class's glossy base reads per evaluation: a snapshot here, so
+    // that a per-slot resolved (textured) material is gathered once per vertex, not once per
+    // evaluation (63 dwords: an odd LDS stride)
+    float rough, aniso, ior, tfilm, spec;
+    Col base;
 };
 
 template <int FULL = BC_FULL>
@@ -676,6 +685,8 @@ DEV void principled_eval_pre(const BCtx& c, const Mat& m, const VState& vs, v3 v
     e.outside = dot(view, n) > 0 || m.thin_walled;
     if (dot(view, n) < 0.0f) n = -n;
     e.n = n;
+    e.rough = m.roughness; e.aniso = m.anisotropy; e.ior = m.ior; e.tfilm = m.thin_film; e.spec = m.specular;
+    e.base = C3(m.base_color);
     build_onb(n, e.T, e.B);
     e.lv = to_local(e.T, e.B, n, view);
     build_rotated_onb(n, e.TR, e.BR, m.anisotropy_rotation * PI);
@@ -791,16 +802,16 @@ DEV Col principled_eval_post(const BCtx& c, const Mat& m, VState& vs, const PEva
         float ws = e.w[4] * nr;
         if (ws > 0.0f) {
             float sp;
-            Col ct = ts_ggx0(c, m.roughness, m.anisotropy, spec_fresnel<FULL>(m, e.rel, dot(llr, lhr)), lvr, llr, lhr, sp);
+            Col ct = ts_ggx0(c, e.rough, e.aniso, spec_fresnel_v<FULL>(m, e.ior, e.tfilm, e.rel, dot(llr, lhr)), lvr, llr, lhr, sp);
             if (e.spec_ok) {
                 ct *= e.spec_tint;
                 ct *= ws;
                 ct *= thr;
                 Col att = col(1.0f);
-                att *= col(1.0f) - spec_fresnel<FULL>(m, e.rel, llr.z);
+                att *= col(1.0f) - spec_fresnel_v<FULL>(m, e.ior, e.tfilm, e.rel, llr.z);
                 att *= col(1.0f) - e.spec_vdf;
                 att *= e.spec_dark;
-                att = lerpc(col(1.0f), att, m.specular);
+                att = lerpc(col(1.0f), att, e.spec);
                 thr *= att;
             }
             pdf += sp * e.p[4];
@@ -809,7 +820,7 @@ DEV Col principled_eval_post(const BCtx& c, const Mat& m, VState& vs, const PEva
         float wd = e.w[5] * nr;
         if (wd > 0.0f) {
             float dp;
-            Col ct = lambert_eval(m, ll.z, dp);
+            Col ct = lambert_eval_c(e.base, ll.z, dp);
             ct *= wd;
             ct *= thr;
             pdf += dp * e.p[5];
