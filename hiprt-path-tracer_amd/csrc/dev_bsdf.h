@@ -343,13 +343,11 @@ DEV float lambda_smith(float ax, float ay, v3 d) {
     return (-1.0f + sqrtf(1.0f + (a * a + b * b) / (d.z * d.z))) * 0.5f;
 }
 DEV float G1(float ax, float ay, v3 d) { return 1.0f / (1.0f + lambda_smith(ax, ay, d)); }
-DEV Col ts_ggx0(const BCtx& c, float r, float an, Col F, v3 V, v3 L, v3 H, float& pdf) {
+// ts_ggx0 with the view-only terms given: alphas (ax, ay), lambda_smith(ax, ay, V) and
+// 1 / (1 + lV) -- the per-vertex part of the glossy base, computed once in principled_eval_pre
+DEV Col ts_ggx0_v(const BCtx& c, float ax, float ay, float lV, float G1V, Col F, v3 V, v3 L, v3 H, float& pdf) {
     pdf = 0.0f;
-    float ax, ay;
-    alphas(r, an, ax, ay);
     float D = ggx_D(ax, ay, H);
-    float lV = lambda_smith(ax, ay, V);
-    float G1V = 1.0f / (1.0f + lV);
     float HoL = maxr(1.0e-3f, dot(V, H));
     float Dv = G1V * D * HoL / V.z;
     float NoV = maxr(1.0e-3f, absr(V.z)), NoL = maxr(1.0e-3f, absr(L.z));
@@ -359,6 +357,12 @@ DEV Col ts_ggx0(const BCtx& c, float r, float an, Col F, v3 V, v3 L, v3 H, float
     if (c.masking == 1) return F * D * (G1V * (1.0f / (1.0f + lL))) / (4.0f * NoL * NoV);
     float G2 = 1.0f / (1.0f + lV + lL);
     return F * D * G2 / (4.0f * NoL * NoV);
+}
+DEV Col ts_ggx0(const BCtx& c, float r, float an, Col F, v3 V, v3 L, v3 H, float& pdf) {
+    float ax, ay;
+    alphas(r, an, ax, ay);
+    const float lV = lambda_smith(ax, ay, V);
+    return ts_ggx0_v(c, ax, ay, lV, 1.0f / (1.0f + lV), F, V, L, H, pdf);
 }
 DEV Col ts_ggx1(const BCtx& c, float r, float an, Col F, v3 V, v3 L, v3 H, float& pdf) {
     float Ess = lut2d(c.luts.conductor, 128, 128, maxr(0.0f, V.z), r);
@@ -381,12 +385,15 @@ DEV v3 ggx_vndf(v3 V, float ax, float ay, Rng& rng) {
     v3 Nh = t1 * T1 + t2 * T2 + sqrtf(maxr(0.0f, 1.0f - t1 * t1 - t2 * t2)) * Vh;
     return normalize(mk3(ax * Nh.x, ay * Nh.y, maxr(0.0f, Nh.z)));
 }
-DEV v3 ggx_sample_reflection(float r, float an, v3 V, Rng& rng) {
+DEV v3 ggx_sample_reflection_a(float ax, float ay, v3 V, Rng& rng) {
     float below = V.z < 0 ? -1.0f : 1.0f;
-    float ax, ay;
-    alphas(r, an, ax, ay);
     v3 m = ggx_vndf(V * below, ax, ay, rng);
     return normalize(reflect_ray(V, m * below));
+}
+DEV v3 ggx_sample_reflection(float r, float an, v3 V, Rng& rng) {
+    float ax, ay;
+    alphas(r, an, ax, ay);
+    return ggx_sample_reflection_a(ax, ay, V, rng);
 }
 
 // ----------------------------------------------------------------------------------
@@ -675,8 +682,11 @@ struct PEval {
     // the material fields every class's glossy base reads per evaluation: a snapshot here, so
     // that a per-slot resolved (textured) material is gathered once per vertex, not once per
     // evaluation (63 dwords: an odd LDS stride)
-    float rough, aniso, ior, tfilm, spec;
+    float ior, tfilm, spec;
     Col base;
+    // the glossy base's view-only GGX terms: alphas of (roughness, anisotropy), lambda_smith and
+    // G1 of the view direction lvr (65 dwords: an odd LDS stride)
+    float gax, gay, glv, gg1v;
 };
 
 template <int FULL = BC_FULL>
@@ -685,12 +695,15 @@ DEV void principled_eval_pre(const BCtx& c, const Mat& m, const VState& vs, v3 v
     e.outside = dot(view, n) > 0 || m.thin_walled;
     if (dot(view, n) < 0.0f) n = -n;
     e.n = n;
-    e.rough = m.roughness; e.aniso = m.anisotropy; e.ior = m.ior; e.tfilm = m.thin_film; e.spec = m.specular;
+    e.ior = m.ior; e.tfilm = m.thin_film; e.spec = m.specular;
     e.base = C3(m.base_color);
     build_onb(n, e.T, e.B);
     e.lv = to_local(e.T, e.B, n, view);
     build_rotated_onb(n, e.TR, e.BR, m.anisotropy_rotation * PI);
     e.lvr = to_local(e.TR, e.BR, n, view);
+    alphas(m.roughness, m.anisotropy, e.gax, e.gay);
+    e.glv = lambda_smith(e.gax, e.gay, e.lvr);
+    e.gg1v = 1.0f / (1.0f + e.glv);
     lobe_weights(m, e.outside, e.w);
     e.inc = ior_or_air(c, vs.incident);
     lobe_probas(e.w, e.p);
@@ -802,7 +815,8 @@ DEV Col principled_eval_post(const BCtx& c, const Mat& m, VState& vs, const PEva
         float ws = e.w[4] * nr;
         if (ws > 0.0f) {
             float sp;
-            Col ct = ts_ggx0(c, e.rough, e.aniso, spec_fresnel_v<FULL>(m, e.ior, e.tfilm, e.rel, dot(llr, lhr)), lvr, llr, lhr, sp);
+            Col ct = ts_ggx0_v(c, e.gax, e.gay, e.glv, e.gg1v, spec_fresnel_v<FULL>(m, e.ior, e.tfilm, e.rel, dot(llr, lhr)), lvr, llr,
+                               lhr, sp);
             if (e.spec_ok) {
                 ct *= e.spec_tint;
                 ct *= ws;
@@ -884,6 +898,40 @@ DEV bool principled_sample_dir(const BCtx& c, const Mat& m, VState& vs, v3 view,
         out = to_world(TR, BR, n, glass_sample<FULL>(c, m, vs, lvr, rng));
     }
     return !(dot(out, sn) < 0 && !glass);
+}
+
+// The plain class's direction sampling from the vertex's PEval (k_shade<PLAIN>).  Such a
+// vertex is shaded from outside (k_shade defers the others), so principled_sample_dir's
+// frame (n, TR, BR, lvr), lobe weights and probabilities are the ones principled_eval_pre
+// stored -- the same operations on the same inputs, done once per vertex instead of once per
+// sample (a rotated frame costs a sine / cosine pair).  The glass branch (reached only by
+// rounding, p[6] = 0) rebuilds its frame as principled_sample_dir does.
+DEV bool principled_sample_dir_plain(const BCtx& c, const Mat& m, VState& vs, const PEval& e, v3 view, v3 sn, v3 gn, v3& out,
+                                     Rng& rng) {
+    const float* p = e.p;
+    float c0 = p[0], c1 = c0 + p[1], c2 = c1 + p[2], c3 = c2 + p[3], c4 = c3 + p[4], c5 = c4 + p[5];
+    (void)c0;
+    float r1 = rng();
+    if (r1 > c5) {
+        v3 n = sn;
+        float ds = dot(view, sn), dg = dot(view, gn);
+        if (ds * dg < 0) n = reflect_ray(sn, gn);
+        if (dot(view, n) < 0) n = -n;
+        v3 TR, BR;
+        build_rotated_onb(n, TR, BR, m.anisotropy_rotation * PI);
+        out = to_world(TR, BR, n, glass_sample<BC_PLAIN>(c, m, vs, to_local(TR, BR, n, view), rng));
+        return true;
+    }
+    vs_pop(vs, false);
+    if (r1 < c4) {
+        out = to_world(e.TR, e.BR, e.n, (r1 >= c2 && r1 < c3) ? ggx_sample_reflection(m.second_roughness, m.anisotropy, e.lvr, rng)
+                                                              : ggx_sample_reflection_a(e.gax, e.gay, e.lvr, rng));
+    } else if (r1 < c5) {
+        out = cosine_sample_around(e.n, rng);
+    } else {
+        out = to_world(e.TR, e.BR, e.n, glass_sample<BC_PLAIN>(c, m, vs, e.lvr, rng));
+    }
+    return !(dot(out, sn) < 0);
 }
 
 DEV Col principled_sample(const BCtx& c, const Mat& m, VState& vs, v3 view, v3 sn, v3 gn, v3& out, float& pdf, Rng& rng) {

@@ -1415,6 +1415,10 @@ struct ShadeArgs {
     int rev;                   // the list grows downward from q_cur (the glass class, stored at the top of qf)
 };
 
+// the plain class samples directions from the vertex's PEval (principled_sample_dir_plain)
+#ifndef MPT_PLAIN_SAMPLE_PE
+#define MPT_PLAIN_SAMPLE_PE 1
+#endif
 #ifndef MPT_SHADE_WAVES
 #define MPT_SHADE_WAVES 2
 #endif
@@ -1647,7 +1651,9 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(
                 bool inner = false;
                 float4 etex = make_float4(0.0f, 0.0f, 0.0f, 0.0f);   // OP_ENV_BSDF: the envmap texel along L
                 if (OPIS(OP_RIS_BSDF) || OPIS(OP_MIS_BSDF) || OPIS(OP_BSDF_LIGHT) || OPIS(OP_ENV_BSDF) || OPIS(OP_CONT)) {
-                    do_eval = bsdf_sample_dir<OVR, CLS>(bc, m, tv, view, sn, gn, L, rng);
+                    do_eval = (MPT_PLAIN_SAMPLE_PE && CLS == BC_PLAIN && OVR == MPT_BSDF_NONE)
+                                  ? principled_sample_dir_plain(bc, m, tv, pe, view, sn, gn, L, rng)
+                                  : bsdf_sample_dir<OVR, CLS>(bc, m, tv, view, sn, gn, L, rng);
                     // the texel's load is issued here and waited for after the evaluation
                     if (MPT_ENV_EARLY && OPIS(OP_ENV_BSDF) && do_eval) etex = env_fetch(S, F, L);
                 } else if (OPIS(OP_RIS_LIGHT)) {
