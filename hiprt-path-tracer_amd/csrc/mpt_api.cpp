@@ -172,6 +172,7 @@ struct MptContext {
     DBuf<int4> gb_meta, pgb_meta;
     DBuf<uint4> gb_vsA, gb_vsB, pgb_vsA, pgb_vsB;
     DBuf<MptMaterial> gb_mat, pgb_mat;
+    DBuf<float4> gb_cs, pgb_cs;           // compact surface records (4 float4 per pixel)
     DBuf<float4> rs_init, rs_sp1, rs_sp2, rs_plights;
     DBuf<float4> rs_keep;                 // batched ReSTIR DI: the final reservoirs of each sample of a batch
     DBuf<int32_t> rs_conv;
@@ -323,6 +324,7 @@ DevPaths dev_paths(MptContext* c) {
     P.gb_vsA = c->gb_vsA.p; P.gb_vsB = c->gb_vsB.p; P.gb_mat = c->gb_mat.p;
     P.pgb_pos = c->pgb_pos.p; P.pgb_sn = c->pgb_sn.p; P.pgb_gn = c->pgb_gn.p; P.pgb_view = c->pgb_view.p; P.pgb_meta = c->pgb_meta.p;
     P.pgb_vsA = c->pgb_vsA.p; P.pgb_vsB = c->pgb_vsB.p; P.pgb_mat = c->pgb_mat.p;
+    P.gb_cs = c->gb_cs.p; P.pgb_cs = c->pgb_cs.p;
     P.rs_init = c->rs_init.p; P.rs_sp1 = c->rs_sp1.p; P.rs_sp2 = c->rs_sp2.p; P.rs_plights = c->rs_plights.p;
     P.rs_keep = c->rs_keep.p; P.rs_keep_n = (int64_t)c->rs_init.n / 3; P.rs_keep_on = 0;
     P.rs_out = c->restir_out_sp2 == 1 ? c->rs_sp2.p : c->restir_out_sp2 == 2 ? c->rs_init.p : c->rs_sp1.p;
@@ -588,7 +590,7 @@ int build_light_bvh(MptContext* c) {
 // Zero-filled G-buffers decode as "never written" (see restir_di.h gb_surface).
 void release_restir(MptContext* c) {
     release_all(c->gb_pos, c->gb_sn, c->gb_gn, c->gb_view, c->pgb_pos, c->pgb_sn, c->pgb_gn, c->pgb_view, c->gb_meta,
-                c->pgb_meta, c->gb_vsA, c->gb_vsB, c->pgb_vsA, c->pgb_vsB, c->gb_mat, c->pgb_mat, c->rs_init, c->rs_sp1,
+                c->pgb_meta, c->gb_vsA, c->gb_vsB, c->pgb_vsA, c->pgb_vsB, c->gb_mat, c->pgb_mat, c->gb_cs, c->pgb_cs, c->rs_init, c->rs_sp1,
                 c->rs_sp2, c->rs_plights, c->rs_keep, c->rs_conv, c->rq_o, c->rq_d, c->rq_rec, c->rq_key, c->rq_occ, c->rq_list, c->rq_items, c->rq_meta);
     c->restir_out_sp2 = 0;
 }
@@ -605,12 +607,15 @@ int ensure_restir(MptContext* c, const MptFrame* f) {
         A(c->pgb_pos, N); A(c->pgb_sn, N); A(c->pgb_gn, N); A(c->pgb_view, N);
         A(c->gb_meta, N); A(c->pgb_meta, N);
         A(c->gb_vsA, N); A(c->gb_vsB, N); A(c->pgb_vsA, N); A(c->pgb_vsB, N);
+        A(c->gb_cs, 4 * N); A(c->pgb_cs, 4 * N);
         A(c->rs_init, 3 * N); A(c->rs_sp1, 3 * N); A(c->rs_sp2, 3 * N);
         if (A.e == hipSuccess) {
             for (DBuf<float4>* b : {&c->gb_pos, &c->gb_sn, &c->gb_gn, &c->gb_view, &c->pgb_pos, &c->pgb_sn, &c->pgb_gn, &c->pgb_view})
                 A(hipMemsetAsync(b->p, 0, N * sizeof(float4), st));
             A(hipMemsetAsync(c->gb_meta.p, 0, N * sizeof(int4), st));
             A(hipMemsetAsync(c->pgb_meta.p, 0, N * sizeof(int4), st));
+            A(hipMemsetAsync(c->gb_cs.p, 0, 4 * N * sizeof(float4), st));
+            A(hipMemsetAsync(c->pgb_cs.p, 0, 4 * N * sizeof(float4), st));
             for (DBuf<uint4>* b : {&c->gb_vsA, &c->gb_vsB, &c->pgb_vsA, &c->pgb_vsB})
                 A(hipMemsetAsync(b->p, 0, N * sizeof(uint4), st));
             A(launch_restir_fill(c->rs_init.p, (int)N, st));

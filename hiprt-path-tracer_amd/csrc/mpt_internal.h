@@ -177,6 +177,11 @@ struct DevPaths {
     MptMaterial* gb_mat;      // per-pixel resolved material (textured materials / white furnace)
     float4* pgb_pos; float4* pgb_sn; float4* pgb_gn; float4* pgb_view; int4* pgb_meta;
     uint4* pgb_vsA; uint4* pgb_vsB; MptMaterial* pgb_mat;
+    // the same surfaces as one 64-B record per pixel (4 float4: position + material reference,
+    // shading normal + incident medium, view + last hit, geometric normal) for the plain-class
+    // target-function evaluations, which read neighbours' surfaces at random (restir_di.h
+    // gb_csurf): one line per neighbour instead of one per plane
+    float4* gb_cs; float4* pgb_cs;
     float4* rs_init;          // reservoirs (3 float4 each): initial candidates
     float4* rs_sp1;           // spatial outputs, ping-pong
     float4* rs_sp2;

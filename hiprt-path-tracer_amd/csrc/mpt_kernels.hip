@@ -2662,11 +2662,12 @@ static void launch_restir(const DevScene& S, DevPaths& P, const MptFrame* d_fram
         const int64_t MS = sizeof(MptMaterial);
         cfg.halo_rows = halo_exchange(hf, cfg, st, MPT_HALO_GBUFFER, 0, need,
                                       {{P.gb_pos, 16}, {P.gb_sn, 16}, {P.gb_gn, 16}, {P.gb_view, 16}, {P.gb_meta, 16},
-                                       {P.gb_vsA, 16}, {P.gb_vsB, 16}, {P.gb_mat, MS}, {as ? P.rs_conv : nullptr, 4}});
+                                       {P.gb_vsA, 16}, {P.gb_vsB, 16}, {P.gb_mat, MS}, {as ? P.rs_conv : nullptr, 4},
+                                       {MPT_RESTIR_CS ? P.gb_cs : nullptr, 64}});
         if (cfg.halo_rows > cfg.halo_prev)   // rows frame_begin did not maintain last frame
             halo_exchange(hf, cfg, st, MPT_HALO_PREV_GBUFFER, 0, cfg.halo_rows,
                           {{P.pgb_pos, 16}, {P.pgb_sn, 16}, {P.pgb_gn, 16}, {P.pgb_view, 16}, {P.pgb_meta, 16},
-                           {P.pgb_vsA, 16}, {P.pgb_vsB, 16}, {P.pgb_mat, MS}});
+                           {P.pgb_vsA, 16}, {P.pgb_vsB, 16}, {P.pgb_mat, MS}, {MPT_RESTIR_CS ? P.pgb_cs : nullptr, 64}});
     }
     if (hf.options.restir_di_do_lights_presampling) {   // ReSTIRDIRenderPass::launch (.cpp:241-242)
         TimedScope tk(cfg, st, KT_RS_PRESAMPLE);

@@ -16,6 +16,10 @@
 #ifndef MPT_RESTIR_WAVES
 #define MPT_RESTIR_WAVES 2
 #endif
+// the plain-class target-function evaluations read surfaces from the compact per-pixel record
+#ifndef MPT_RESTIR_CS
+#define MPT_RESTIR_CS 1
+#endif
 #define RESTIR_KERNEL __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MPT_RESTIR_WAVES)))
 
 // ---- surfaces (Surface.h:12-73) ----------------------------------------------------
@@ -38,6 +42,28 @@ DEV RSurf gb_surface(const DevScene& S, const DevPaths& P, int i, bool prev) {
     s.sn = mk3(sn.x, sn.y, sn.z);
     s.gn = mk3(gn.x, gn.y, gn.z);
     s.p = mk3(pos.x, pos.y, pos.z);
+    s.sp = s.p + s.sn * 1.0e-4f;
+    return s;
+}
+
+// gb_surface from the compact record (DevPaths::gb_cs), for the plain-class evaluations:
+// the same surface, with the nested-dielectric state reduced to the incident medium (all a
+// plain-dielectric evaluation reads of it: principled_eval_pre's incident IOR)
+DEV RSurf gb_csurf(const DevScene& S, const DevPaths& P, int i, bool prev) {
+    const float4* cs = (prev ? P.pgb_cs : P.gb_cs) + 4 * (size_t)i;
+    const float4 a = cs[0], b = cs[1], v = cs[2];
+    const int mref = __float_as_int(a.w);   // material index + 1, negative: the per-pixel copy, 0: never written
+    RSurf s;
+    if (mref == 0) s.m = &g_zero_mat;
+    else if (mref < 0) s.m = prev ? &P.pgb_mat[i] : &P.gb_mat[i];
+    else s.m = &S.mats_res[mref - 1];
+    s.vs = vs_default();
+    if (mref != 0) s.vs.incident = __float_as_int(b.w);
+    s.last = __float_as_int(v.w);
+    s.view = mk3(v.x, v.y, v.z);
+    s.sn = mk3(b.x, b.y, b.z);
+    s.gn = mk3(0.0f, 0.0f, 0.0f);   // (not read by a plain evaluation; cs[3])
+    s.p = mk3(a.x, a.y, a.z);
     s.sp = s.p + s.sn * 1.0e-4f;
     return s;
 }
@@ -469,11 +495,19 @@ __global__ __launch_bounds__(TB) void k_gbuffer(DevScene S, DevPaths P, const Mp
         vs_store(P.gb_vsA, P.gb_vsB, gp, vs);
         meta.y = mi + 1;
         meta.w = per_pixel;
+        if (MPT_RESTIR_CS) {
+            float4* cs = P.gb_cs + 4 * (size_t)gp;
+            cs[0] = make_float4(ip.x, ip.y, ip.z, __int_as_float(per_pixel ? -meta.y : meta.y));
+            cs[1] = make_float4(sn.x, sn.y, sn.z, __int_as_float(vs.incident));
+            cs[3] = make_float4(gn.x, gn.y, gn.z, 0.0f);
+        }
     }
     meta.x = found ? prim : -1;
     meta.z = found ? 1 : 0;
     P.gb_meta[gp] = meta;
     P.gb_view[gp] = make_float4(-d.x, -d.y, -d.z, 0.0f);
+    // (a miss keeps the record's surface, as it keeps the planes', and updates view + last hit)
+    if (MPT_RESTIR_CS) P.gb_cs[4 * (size_t)gp + 2] = make_float4(-d.x, -d.y, -d.z, __int_as_float(meta.x));
 }
 #endif
 
@@ -1489,7 +1523,8 @@ RESTIR_KERNEL void k_rsp_eval(DevScene S, DevPaths P, const MptFrame* __restrict
             const int center = s + P.pix_off;
             float* rec = reinterpret_cast<float*>(&P.rq_rec[rq_rec_at(P, s, k)]);
             const int ni = __float_as_int(rec[0]);
-            const RSurf g = gb_surface(S, P, which ? ni : center, which && prev);
+            const RSurf g = (PLAIN && MPT_RESTIR_CS) ? gb_csurf(S, P, which ? ni : center, which && prev)
+                                                     : gb_surface(S, P, which ? ni : center, which && prev);
             const RResv smp = which ? rr_load(FUSED ? P.rs_init : in, center) : rr_load(in, ni);
             TgtRay ray;
             float t;
@@ -1864,6 +1899,8 @@ __global__ __launch_bounds__(TB) void k_restir_frame_begin(DevPaths P, const Mpt
         P.pgb_meta[i] = meta;
         P.pgb_vsA[i] = P.gb_vsA[i]; P.pgb_vsB[i] = P.gb_vsB[i];
         if (meta.w) P.pgb_mat[i] = P.gb_mat[i];
+        if (MPT_RESTIR_CS)
+            for (int k = 0; k < 4; k++) P.pgb_cs[4 * (size_t)i + k] = P.gb_cs[4 * (size_t)i + k];
     }
     if ((rs.sample_number == 0 || rs.need_to_reset) && rs.accumulate) {
         rr_store(P.rs_init, i, rr_default());
