@@ -308,16 +308,24 @@ DEV float restir_jacobian(const DevScene& S, const RResv& nr, v3 csp, v3 nsp) {
 // check_neighbor_similarity_heuristics (Utils.h:214-263), incl. the inverted normal test
 DEV bool restir_similar(const DevScene& S, const DevPaths& P, const MptReSTIRDISettings& rd, int nb, const Mat& center_m,
                         v3 sp, v3 n, bool prev) {
+#if MPT_RESTIR_CS
+    // from the compact records: position + material of the neighbour's (current or previous)
+    // surface, the shading normal of its current one (as the planes' version reads gb_sn)
+    const float4 pos = ((prev ? P.pgb_cs : P.gb_cs) + 4 * (size_t)nb)[0];
+    const int mref = __float_as_int(pos.w);
+    const Mat* nm = mref == 0 ? &g_zero_mat : mref < 0 ? (prev ? &P.pgb_mat[nb] : &P.gb_mat[nb]) : &S.mats_res[mref - 1];
+#else
     float4 pos = prev ? P.pgb_pos[nb] : P.gb_pos[nb];
+    const Mat* nm = gb_surface(S, P, nb, prev).m;
+#endif
     bool plane = !rd.use_plane_distance_heuristic || absr(dot(mk3(pos.x, pos.y, pos.z) - sp, n)) < rd.plane_distance_threshold;
     bool normal = true;
     if (!rd.use_normal_similarity_heuristic) {
-        float4 ns = P.gb_sn[nb];
+        float4 ns = MPT_RESTIR_CS ? P.gb_cs[4 * (size_t)nb + 1] : P.gb_sn[nb];
         normal = dot(n, mk3(ns.x, ns.y, ns.z)) > rd.normal_similarity_angle_precomp;
     }
-    RSurf ns = gb_surface(S, P, nb, prev);
-    bool rough = !rd.use_roughness_similarity_heuristic || absr(ns.m->roughness - center_m.roughness) < rd.roughness_similarity_threshold;
-    return plane && normal && rough && !is_emissive(*ns.m);
+    bool rough = !rd.use_roughness_similarity_heuristic || absr(nm->roughness - center_m.roughness) < rd.roughness_similarity_threshold;
+    return plane && normal && rough && !is_emissive(*nm);
 }
 
 // get_spatial_neighbor_pixel_index (Utils.h:289-339)
