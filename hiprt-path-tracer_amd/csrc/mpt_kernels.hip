@@ -1603,15 +1603,14 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(
             int triW = -1, ris_c = 0;
             bool hasW = false;
             float r_add = 0.0f;                // the RIS BSDF candidate's random (add_one_candidate)
-            // per-vertex half of every BSDF evaluation below, one LDS record per lane (55
+            // per-vertex half of every BSDF evaluation below, one LDS record per lane (65
             // dwords: an odd stride, so lane-parallel accesses are bank-conflict free).  Held
             // in registers it pushed the kernel into ~140 spilled VGPRs; in LDS it costs one
             // ds_read per field per evaluation (-23% k_shade time on C3).  The kernel's 80640 B
-            // of LDS per 256-lane block are these 56320 B plus 24320 B (95 B per lane) of private
+            // of LDS per 256-lane block are these 66560 B plus 14080 B (55 B per lane) of private
             // arrays that the compiler's promote-alloca pass moves into the LDS the 2-wave
-            // occupancy leaves free (-mllvm -disable-promote-alloca-to-lds: 160 B of scratch per
-            // lane instead); two blocks fill a CU's 160 KB, so LDS and VGPRs (238) both cap the
-            // kernel at 2 waves / SIMD
+            // occupancy leaves free (the rest, 128 B per lane, in scratch); two blocks fill a
+            // CU's 160 KB, so LDS and VGPRs (249) both cap the kernel at 2 waves / SIMD
             constexpr bool PE_LDS = (ST & SG_LIGHT) || MPT_SHADE_PE_LDS_LATE;
             __shared__ PEval pe_lds[PE_LDS ? TB : 1];
             PEval pe_reg;
