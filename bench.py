@@ -236,6 +236,76 @@ def load_traffic(workload, W, H):
     return d
 
 
+def emulate_restir_ranks(a, r, cam, W, H, opt, wset, alpha, n_ranks, K, device):
+    """C4 scaling rehearsal on one GPU (--workload c4 --emulate-rank-of N): each rank of the
+    N-way split renders ONE contiguous band with the halo exchange, so the
+    ranks' work differs (sky rows against street rows) and the job's time is the slowest
+    rank's.  Every band k is timed in turn in this context: two whole-frame samples first (so
+    the frame-sized G-buffer / reservoir buffers hold a single-context render around every
+    band), then the band's own warmup + K timed samples, batched as the rank would batch them.
+    The halo callback stands in for the exchange: at each exchange point it copies the halo
+    rows the rank would receive (same bytes, device to device on the library's stream) and
+    synchronises the host once per sample at the G-buffer phase as the RCCL exchange's
+    all-reduce does; the rows keep the whole-frame render's content, so the images are not
+    the partitioned render's (tests/test_configs.py pins that bit-exact), only its timing."""
+    import torch
+    from mpt import partition
+    bh = partition.contiguous_band(H, n_ranks, 0)[0]
+    stats = {"calls": 0, "bytes": 0}
+
+    def halo(x):
+        st = torch.cuda.ExternalStream(x.stream, device=torch.device("cuda", device))
+        if x.phase == partition.HALO_GBUFFER:
+            st.synchronize()
+        _, recvs = partition.halo_plan(x.res_y, bh, n_ranks, cur[0], x.halo_rows)
+        with torch.cuda.stream(st):
+            for v in partition._row_views(x, torch, torch.device("cuda", device)):
+                for (_, y0, y1) in recvs:
+                    scratch = torch.empty_like(v[y0:y1])
+                    scratch.copy_(v[y0:y1])
+                    stats["bytes"] += scratch.numel()
+        stats["calls"] += 1
+
+    cur = [0]
+    r.set_halo_exchange(halo)
+    bands = []
+    for k in range(n_ranks):
+        cur[0] = k
+        band = (bh, k, n_ranks)
+        rows = mpt.partition_rows(H, *band)
+        if rows == 0:
+            continue
+        want = TARGET_PATHS / max(1, rows * W)
+        batch = min((d for d in range(1, min(MAX_BATCH, K) + 1) if K % d == 0), key=lambda d: (abs(d - want), -d))
+        r.enable_stats(timing=False, instrumented=False)
+        r.render_samples(frames_for(cam, W, H, opt, (1, 0, 1), 2, bounces=a.bounces, world=wset, alpha=alpha))
+        r.render_samples(frames_for(cam, W, H, opt, band, a.warmup, bounces=a.bounces, world=wset, alpha=alpha),
+                         max_batch=batch)
+        frames = frames_for(cam, W, H, opt, band, K, bounces=a.bounces, world=wset, alpha=alpha)
+        r.synchronize_kernel()
+        r.enable_stats(timing=True, instrumented=False)
+        c0, b0 = stats["calls"], stats["bytes"]
+        t0 = time.perf_counter()
+        r.render_samples(frames, max_batch=batch)
+        r.synchronize_kernel()
+        dt = time.perf_counter() - t0
+        st = r.stats()
+        bands.append({"band": k, "rows": f"{k * bh}-{min(H, (k + 1) * bh) - 1}", "ms_per_spp": round(dt * 1e3 / K, 4),
+                      "batch": batch, "mray_s": round((st.rays_closest + st.rays_any) / dt / 1e6, 2),
+                      "restir_ms_per_spp": round(st.restir_ms / K, 4), "shade_ms_per_spp": round(st.shade_ms / K, 4),
+                      "trace_path_ms_per_spp": round(st.stage_ms[0] / K, 4),
+                      "halo_calls_per_spp": round((stats["calls"] - c0) / K, 2),
+                      "halo_mb_per_spp": round((stats["bytes"] - b0) / K / 1e6, 3)})
+        print(json.dumps(bands[-1]), file=sys.stderr, flush=True)
+    worst = max(bands, key=lambda b: b["ms_per_spp"])
+    return {"rehearsal": f"C4 ReSTIR DI tile-parallel over {n_ranks} ranks on one GPU: every rank's contiguous band "
+                         "timed in turn (halo rows from a single-context render, exchange bytes copied locally)",
+            "emulated_rank_of": n_ranks, "steps": K, "warmup": a.warmup, "width": W, "height": H,
+            "ms_per_spp_slowest_rank": worst["ms_per_spp"], "slowest_band": worst["band"],
+            "ms_per_spp_mean_rank": round(sum(b["ms_per_spp"] for b in bands) / len(bands), 4),
+            "bands": bands, "device": {"libmpt_sha256_16": mpt.build_id()}}
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -334,6 +404,10 @@ def main():
     r.set_luts(luts)
     if env is not None:
         r.set_envmap(env)
+    if a.workload == "c4" and world == 1 and a.emulate_rank_of > 1:
+        print(json.dumps(emulate_restir_ranks(a, r, cam, W, H, opt, wset, alpha, a.emulate_rank_of, K, local)), flush=True)
+        r.close()
+        return
     halo = None
     if a.workload == "c4" and world > 1:
         halo = partition.TorchHaloExchange(dist, band_h)

@@ -326,7 +326,7 @@ DevPaths dev_paths(MptContext* c) {
     P.pgb_vsA = c->pgb_vsA.p; P.pgb_vsB = c->pgb_vsB.p; P.pgb_mat = c->pgb_mat.p;
     P.gb_cs = c->gb_cs.p; P.pgb_cs = c->pgb_cs.p;
     P.rs_init = c->rs_init.p; P.rs_sp1 = c->rs_sp1.p; P.rs_sp2 = c->rs_sp2.p; P.rs_plights = c->rs_plights.p;
-    P.rs_keep = c->rs_keep.p; P.rs_keep_n = (int64_t)c->rs_init.n / 3; P.rs_keep_on = 0;
+    P.rs_keep = c->rs_keep.p; P.rs_keep_n = (int64_t)std::max(c->n_slots, 1); P.rs_keep_on = 0;   // band pixels per sample
     P.rs_out = c->restir_out_sp2 == 1 ? c->rs_sp2.p : c->restir_out_sp2 == 2 ? c->rs_init.p : c->rs_sp1.p;
     P.rs_tin = P.rs_out;
     // contiguous band (ReSTIR DI across a partition) or the whole frame: slot s = pixel s + pix_off
@@ -717,8 +717,9 @@ int validate_frame(const MptFrame* f) {
     if ((int64_t)f->res_x * f->res_y > MPT_MAX_WAVEFRONT_PATHS)
         return fail(MPT_ERR_UNSUPPORTED, "more than MPT_MAX_WAVEFRONT_PATHS pixels per frame");
     if (rs.nb_bounces < 0 || rs.nb_bounces > 64) return fail(MPT_ERR_INVALID_ARGUMENT, "nb_bounces out of range");
-    if (rs.wants_render_low_resolution && rs.allow_render_low_resolution && rs.accumulate)
-        return fail(MPT_ERR_UNSUPPORTED, "low-resolution interactive mode not implemented");
+    if (rs.wants_render_low_resolution && rs.allow_render_low_resolution && rs.accumulate &&
+        (rs.render_low_resolution_scaling < 1 || rs.render_low_resolution_scaling > 64))
+        return fail(MPT_ERR_INVALID_ARGUMENT, "render_low_resolution_scaling must be in [1, 64]");
     // sample_many_lights / RIS (Lights.h:222-241, RIS.h:82-289); the UI ranges are 1-8 light
     // samples and 0-16 candidates (ImGuiSettingsWindow.cpp:787, 833), the bounds here 64
     if (rs.number_of_light_samples < 1 || rs.number_of_light_samples > 64)
@@ -747,8 +748,6 @@ int validate_frame(const MptFrame* f) {
             return fail(MPT_ERR_INVALID_ARGUMENT, "ReSTIR DI: bad light presampling settings");
         if (rd.reuse_neighbor_count > 32 || rd.disocclusion_reuse_count > 32)
             return fail(MPT_ERR_UNSUPPORTED, "ReSTIR DI: at most 32 spatial neighbours");
-        if (rs.wants_render_low_resolution && rs.allow_render_low_resolution)
-            return fail(MPT_ERR_UNSUPPORTED, "ReSTIR DI with low-resolution rendering");
     }
     if (f->options.bsdf_override != MPT_BSDF_NONE && f->options.bsdf_override != MPT_BSDF_LAMBERTIAN &&
         f->options.bsdf_override != MPT_BSDF_OREN_NAYAR)
@@ -1195,9 +1194,10 @@ static int prepare_batch(MptContext* c, const MptFrame* f, int batch) {
     const bool keep = f->options.direct_light_sampling == MPT_LSS_RESTIR_DI &&
                       f->world_settings.ambient_light_type == MPT_AMBIENT_ENVMAP;
     if (!keep) c->rs_keep.release();
-    if (keep && batch > 1 && c->rs_keep.n < c->rs_init.n * (size_t)batch) {
+    const size_t keep_n = 3 * (size_t)std::max(c->n_slots, 1) * (size_t)batch;   // the band's pixels only
+    if (keep && batch > 1 && c->rs_keep.n < keep_n) {
         c->rs_keep.release();
-        if (c->rs_keep.alloc(c->rs_init.n * (size_t)batch) != hipSuccess) {
+        if (c->rs_keep.alloc(keep_n) != hipSuccess) {
             (void)hipGetLastError();
             return fail(MPT_ERR_OUT_OF_MEMORY, "ReSTIR DI batch reservoirs");
         }
@@ -1321,10 +1321,36 @@ static int launch_batch(MptContext* c, const MptFrame* f, int batch) {
     return MPT_OK;
 }
 
+// do_render_low_resolution (RenderSettings.h:195-198): the settings the launches of a
+// low-resolution frame see -- at most 3 bounces (FullPathTracer.h:117-122), RIS with one light
+// and one BSDF candidate and no visibility in its target function (RIS.h:93-94, 162), ReSTIR DI
+// initial candidates capped at one of each (InitialCandidates.h:420-421); these fields are read
+// nowhere else.  (The initial candidates' visibility test, InitialCandidates.h:248-249, is
+// skipped in the kernel: its option also feeds the spatial passes.)  The pixels a low-resolution
+// frame renders are k_camera's (low_res_region).
+static MptFrame low_res_frame(const MptFrame& f) {
+    MptFrame e = f;
+    MptRenderSettings& rs = e.render_settings;
+    if (!(rs.wants_render_low_resolution && rs.allow_render_low_resolution && rs.accumulate)) return e;
+    rs.nb_bounces = std::min(3, rs.nb_bounces);
+    rs.ris_number_of_light_candidates = 1;
+    rs.ris_number_of_bsdf_candidates = 1;
+    e.options.ris_use_visibility = 0;
+    MptReSTIRDISettings& rd = rs.restir_di_settings;
+    rd.number_of_initial_light_candidates = std::min(1, rd.number_of_initial_light_candidates);
+    rd.number_of_initial_bsdf_candidates = std::min(1, rd.number_of_initial_bsdf_candidates);
+    return e;
+}
+static bool is_low_res(const MptFrame& f) {
+    const MptRenderSettings& rs = f.render_settings;
+    return rs.wants_render_low_resolution && rs.allow_render_low_resolution && rs.accumulate;
+}
+
 int mpt_render_frame(MptContext* c, const MptFrame* f) {
     if (!c || !f) return fail(MPT_ERR_INVALID_ARGUMENT, "NULL argument");
-    int r = prepare_batch(c, f, 1);
-    return r != MPT_OK ? r : launch_batch(c, f, 1);
+    const MptFrame e = low_res_frame(*f);
+    int r = prepare_batch(c, &e, 1);
+    return r != MPT_OK ? r : launch_batch(c, &e, 1);
 }
 
 // Frames that differ only in what GPURenderer::render changes between the samples of one
@@ -1334,10 +1360,12 @@ int mpt_render_frame(MptContext* c, const MptFrame* f) {
 // threshold gate each sample's camera rays on the previous ones) are rendered as one
 // wavefront.  ReSTIR DI samples, whose reuse passes read the previous sample's reservoirs,
 // run their first bounce one sample after the other (launch_frames_restir) and share the
-// later bounces' wavefront; not across a partition (the halo exchange is per sample).
+// later bounces' wavefront; across a partition each sample's reuse passes exchange their halo
+// in turn (the exchange callback fires per sample inside the batch, launch_frames_restir).
 static bool batchable(const MptContext* c, const MptFrame& a, const MptFrame& b) {
     const bool restir = a.options.direct_light_sampling == MPT_LSS_RESTIR_DI;
-    if (restir && (!c->restir_batch || a.band_count > 1)) return false;
+    if (restir && !c->restir_batch) return false;
+    if (is_low_res(a)) return false;   // interactive frames: one sample each (RenderWindow.cpp:798-802)
     const MptRenderSettings& rs = a.render_settings;
     if ((rs.stop_pixel_noise_threshold > 0.0f || rs.enable_adaptive_sampling) && rs.accumulate) return false;
     MptFrame t = b;
@@ -1365,6 +1393,14 @@ int mpt_render_frames(MptContext* c, const MptFrame* frames, int32_t count, int3
     max_batch = std::min<int32_t>(max_batch, MPT_MAX_BATCH);
     // batched ReSTIR DI runs each sample's first bounce in turn (its timing events per sample)
     if (frames[0].options.direct_light_sampling == MPT_LSS_RESTIR_DI) max_batch = std::min(max_batch, RESTIR_MAX_BATCH);
+    // the launches' view of low-resolution frames (low_res_frame), copied only when there is one
+    std::vector<MptFrame> eff;
+    for (int k = 0; k < count && eff.empty(); k++)
+        if (is_low_res(frames[k])) {
+            eff.reserve((size_t)count);
+            for (int j = 0; j < count; j++) eff.push_back(low_res_frame(frames[j]));
+        }
+    if (!eff.empty()) frames = eff.data();
     int i = 0;
     while (i < count) {
         int b = 1;

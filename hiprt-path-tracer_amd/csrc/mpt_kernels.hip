@@ -801,6 +801,20 @@ DEV uint32_t path_seed(const MptFrame* Fp, const DevPaths& P, int slot, bool cam
 DEV bool has_adaptive_buffers(const MptRenderSettings& rs) {   // RenderSettings.h:207-218
     return (rs.stop_pixel_noise_threshold > 0.0f || rs.enable_adaptive_sampling) && rs.accumulate;
 }
+// Low-resolution interactive mode (do_render_low_resolution, RenderSettings.h:195-198;
+// CameraRays.h:63-76): CameraRays renders one pixel out of s x s, the representative (x, y)
+// with x, y multiples of s, at pixel_index / s = (x / s, y / s) -- the frame's top-left
+// ceil(W / s) x ceil(H / s) pixels, row stride W, hold the low-resolution image.  A pixel of
+// that region is active and traces the camera ray through its representative; every other
+// pixel is inactive (the reference's racy pixel_active writes resolved as DESIGN.md §2 states).
+DEV bool low_res(const MptRenderSettings& rs) {
+    return rs.wants_render_low_resolution && rs.allow_render_low_resolution && rs.accumulate;
+}
+DEV bool low_res_region(const MptFrame& F, int x, int y) {
+    const MptRenderSettings& rs = F.render_settings;
+    const int s = rs.render_low_resolution_scaling;
+    return x < (F.res_x + s - 1) / s && y < (F.res_y + s - 1) / s;
+}
 // get_pixel_confidence_interval (AdaptiveSampling.h:11-20)
 DEV float pixel_confidence(const DevPaths& P, int slot, int count, float& avg) {
     const float* px = P.fb_color + 3 * (size_t)slot;
@@ -844,8 +858,15 @@ __global__ __launch_bounds__(TB) void k_camera(DevPaths P, const MptFrame* __res
     const MptFrame& F = Fp[sub];
     const MptRenderSettings& rs = F.render_settings;
     const bool as = has_adaptive_buffers(rs);
+    const bool lr = low_res(rs);
     bool act = slot < P.n;
-    if (act) {
+    int x = 0, y = 0;
+    uint32_t pix = 0;
+    if (act) pix = slot_pixel(F, pslot, x, y);
+    if (act && lr && !low_res_region(F, x, y)) {
+        act = false;                      // CameraRays.h:68-72: no reset, no adaptive gate
+        P.active[slot] = 0;
+    } else if (act) {
         // reset_render + adaptive gate (CameraRays.h:19-43, 88-125)
         if (as && (rs.sample_number == 0 || rs.need_to_reset)) {
             P.as_count[slot] = 0;
@@ -867,7 +888,7 @@ __global__ __launch_bounds__(TB) void k_camera(DevPaths P, const MptFrame* __res
         }
         P.active[slot] = act ? 1 : 0;
     }
-    if (as) {
+    if (as || lr) {
         // camera-ray queue of the active pixels (wave64 ballot, one atomic per wave)
         uint64_t m = __ballot(act);
         int lane = threadIdx.x & 63;
@@ -883,14 +904,15 @@ __global__ __launch_bounds__(TB) void k_camera(DevPaths P, const MptFrame* __res
     }
     if (!act) return;
     if (rs.do_update_status_buffers) P.status[1] = 1u;
-    int x, y;
-    uint32_t pix = slot_pixel(F, pslot, x, y);
     const uint32_t cseed = camera_seed(F, pix);
     // the path's seeds for the later stages (path_seed of the camera launch / of the path
     // tracing launch), computed once here instead of per traversal query
     P.seeds[slot] = make_uint2(cseed, pixel_seed(F, pix));
     Rng rng = make_rng(cseed);
-    float xd = (float)x + 0.5f, yd = (float)y + 0.5f;
+    // low resolution: the ray through the representative pixel (CameraRays.h:127-131 with the
+    // thread's own x, y), seeded with the low-resolution index (pixel_index / s)
+    const int ls = lr ? rs.render_low_resolution_scaling : 1;
+    float xd = (float)(x * ls) + 0.5f, yd = (float)(y * ls) + 0.5f;
     if (F.current_camera.do_jittering) { xd += rng() - 0.5f; yd += rng() - 0.5f; }
     float xn = xd / (float)F.res_x * 2.0f - 1.0f;
     float yn = yd / (float)F.res_y * 2.0f - 1.0f;
@@ -1706,7 +1728,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(
                         int kpix, ksub;
                         batch_split(P, slot, kpix, ksub);
                         rsb = P.rs_keep + (size_t)ksub * 3 * (size_t)P.rs_keep_n;
-                        rpix = (size_t)kpix + P.pix_off;
+                        rpix = (size_t)kpix;   // rs_keep holds the band's pixels
                     }
                     rres = rr_load(rsb, (int)rpix);
                     if ((rres.flags & RF_ENVMAP) && ws.ambient_light_type != MPT_AMBIENT_ENVMAP) {
@@ -2634,6 +2656,41 @@ static void launch_fused_pass(int ovr, bool def_bias, const MptFrame& hf, Launch
     hipLaunchKernelGGL(k_rs_visapply, gp, dim3(TB), 0, st, P, P.rs_out);
 }
 
+// The G-buffer halo exchange of a partitioned context (and, when the agreed halo grew, the
+// previous frame's rows frame_begin did not maintain); sets cfg.halo_rows.
+static void exchange_gbuffers(const MptFrame& hf, LaunchCfg& cfg, hipStream_t st, const DevPaths& P, int need) {
+    const bool as = hf.render_settings.enable_adaptive_sampling;
+    const int64_t MS = sizeof(MptMaterial);
+    cfg.halo_rows = halo_exchange(hf, cfg, st, MPT_HALO_GBUFFER, 0, need,
+                                  {{P.gb_pos, 16}, {P.gb_sn, 16}, {P.gb_gn, 16}, {P.gb_view, 16}, {P.gb_meta, 16},
+                                   {P.gb_vsA, 16}, {P.gb_vsB, 16}, {P.gb_mat, MS}, {as ? P.rs_conv : nullptr, 4},
+                                   {MPT_RESTIR_CS ? P.gb_cs : nullptr, 64}});
+    if (cfg.halo_rows > cfg.halo_prev)   // rows frame_begin did not maintain last frame
+        halo_exchange(hf, cfg, st, MPT_HALO_PREV_GBUFFER, 0, cfg.halo_rows,
+                      {{P.pgb_pos, 16}, {P.pgb_sn, 16}, {P.pgb_gn, 16}, {P.pgb_view, 16}, {P.pgb_meta, 16},
+                       {P.pgb_vsA, 16}, {P.pgb_vsB, 16}, {P.pgb_mat, MS}, {MPT_RESTIR_CS ? P.pgb_cs : nullptr, 64}});
+}
+
+// A partitioned context whose band holds no row (more contexts than rows): nothing to render,
+// but the other bands' exchanges pair with its own, so it makes the calls launch_restir makes,
+// in the same order (G-buffer, then the reservoirs each reuse pass reads), with its buffers.
+static void restir_empty_band(const MptFrame& hf, LaunchCfg& cfg, hipStream_t st, const DevPaths& P) {
+    if (!cfg.halo_fn) return;
+    const MptReSTIRDISettings& rd = hf.render_settings.restir_di_settings;
+    const int64_t RB = 3 * sizeof(float4);
+    exchange_gbuffers(hf, cfg, st, P, 0);
+    if (rd.do_fused_spatiotemporal) {
+        for (int pass = 0; pass < rd.number_of_passes; pass++)
+            halo_exchange(hf, cfg, st, MPT_HALO_RESERVOIRS, pass, cfg.halo_rows, {{P.rs_sp1, RB}});
+    } else {
+        if (rd.do_temporal_reuse_pass) halo_exchange(hf, cfg, st, MPT_HALO_RESERVOIRS, 0, cfg.halo_rows, {{P.rs_sp1, RB}});
+        if (rd.do_spatial_reuse_pass)
+            for (int pass = 0; pass < rd.number_of_passes; pass++)
+                halo_exchange(hf, cfg, st, MPT_HALO_RESERVOIRS, pass + 1, cfg.halo_rows, {{P.rs_sp1, RB}});
+    }
+    cfg.halo_prev = cfg.halo_rows;
+}
+
 // ReSTIRDIRenderPass::launch (ReSTIRDIRenderPass.cpp:233-264) for the fused configuration:
 // presampling, initial candidates, fused spatiotemporal, (number_of_passes - 1) spatial
 // passes ping-ponging between the two spatial buffers; returns the output buffer in P.rs_out.
@@ -2656,17 +2713,9 @@ static void launch_restir(const DevScene& S, DevPaths& P, const MptFrame* d_fram
         hipStreamSynchronize(st);
         const int need = std::min(hf.res_y, *cfg.h_reproj + std::max(0, rd.reuse_radius) +
                                                 std::max(0, rd.neighbor_search_radius) + 8);
-        const bool as = hf.render_settings.enable_adaptive_sampling;
-        if (as) hipLaunchKernelGGL(k_restir_conv, dim3(blocks_for(P.n)), dim3(TB), 0, st, P);
-        const int64_t MS = sizeof(MptMaterial);
-        cfg.halo_rows = halo_exchange(hf, cfg, st, MPT_HALO_GBUFFER, 0, need,
-                                      {{P.gb_pos, 16}, {P.gb_sn, 16}, {P.gb_gn, 16}, {P.gb_view, 16}, {P.gb_meta, 16},
-                                       {P.gb_vsA, 16}, {P.gb_vsB, 16}, {P.gb_mat, MS}, {as ? P.rs_conv : nullptr, 4},
-                                       {MPT_RESTIR_CS ? P.gb_cs : nullptr, 64}});
-        if (cfg.halo_rows > cfg.halo_prev)   // rows frame_begin did not maintain last frame
-            halo_exchange(hf, cfg, st, MPT_HALO_PREV_GBUFFER, 0, cfg.halo_rows,
-                          {{P.pgb_pos, 16}, {P.pgb_sn, 16}, {P.pgb_gn, 16}, {P.pgb_view, 16}, {P.pgb_meta, 16},
-                           {P.pgb_vsA, 16}, {P.pgb_vsB, 16}, {P.pgb_mat, MS}, {MPT_RESTIR_CS ? P.pgb_cs : nullptr, 64}});
+        if (hf.render_settings.enable_adaptive_sampling)
+            hipLaunchKernelGGL(k_restir_conv, dim3(blocks_for(P.n)), dim3(TB), 0, st, P);
+        exchange_gbuffers(hf, cfg, st, P, need);
     }
     if (hf.options.restir_di_do_lights_presampling) {   // ReSTIRDIRenderPass::launch (.cpp:241-242)
         TimedScope tk(cfg, st, KT_RS_PRESAMPLE);
@@ -2898,9 +2947,14 @@ hipError_t launch_frame(const DevScene& S, const DevPaths& P0, const MptFrame* d
                         hipStream_t st) {
     DevPaths P = P0;
     const int n = P.n;
-    if (n == 0) return hipSuccess;
+    if (n == 0) {
+        if (hf.options.direct_light_sampling == MPT_LSS_RESTIR_DI) restir_empty_band(hf, cfg, st, P);
+        return hipGetLastError();
+    }
     const MptRenderSettings& hrs = hf.render_settings;
-    const bool as = (hrs.stop_pixel_noise_threshold > 0.0f || hrs.enable_adaptive_sampling) && hrs.accumulate;
+    // the camera queue is compacted by k_camera under adaptive sampling and at low resolution
+    const bool as = ((hrs.stop_pixel_noise_threshold > 0.0f || hrs.enable_adaptive_sampling) && hrs.accumulate) ||
+                    (hrs.wants_render_low_resolution && hrs.allow_render_low_resolution && hrs.accumulate);
     if (hf.options.direct_light_sampling == MPT_LSS_RESTIR_DI) {
         hipLaunchKernelGGL(k_restir_frame_begin, dim3(blocks_for(P.rs_hi - P.rs_lo)), dim3(TB), 0, st, P, d_frame);
         P.rs_out = restir_buffer(P, cfg.restir_out_sp2);
@@ -2942,7 +2996,11 @@ __global__ __launch_bounds__(TB) void k_iota(int32_t* q, int n) {
 hipError_t launch_frames_restir(const DevScene& S, const DevPaths& PF, const MptFrame* d_frames, const MptFrame* hf,
                                 int batch, LaunchCfg& cfg, hipStream_t st) {
     const int n = PF.n_pix;
-    if (n == 0 || batch <= 0) return hipSuccess;
+    if (batch <= 0) return hipSuccess;
+    if (n == 0) {   // an empty band of a partition: only its side of every sample's exchanges
+        for (int s = 0; s < batch; s++) restir_empty_band(hf[s], cfg, st, PF);
+        return hipGetLastError();
+    }
     const int nb = hf[0].render_settings.nb_bounces;
     // the camera rays of every sample over its own slots [s * n, (s + 1) * n) (their seeds,
     // jitter and alpha keys are the sample's; nothing of the ReSTIR DI state is read), then
@@ -2976,16 +3034,26 @@ hipError_t launch_frames_restir(const DevScene& S, const DevPaths& PF, const Mpt
         DevPaths P = PF;
         offset_slots(P, (size_t)s * n);
         P.n = n; P.batch = 1; P.group = 1;
+        if (cfg.halo_fn) {
+            // a partitioned context: frame_begin maintains the band and the halo the previous
+            // sample agreed on (launch_batch does the same for a batch's first sample)
+            P.rs_lo = std::max(0, cfg.own_y0 - cfg.halo_prev) * hf[s].res_x;
+            P.rs_hi = std::min(hf[s].res_y, cfg.own_y1 + cfg.halo_prev) * hf[s].res_x;
+        }
         hipLaunchKernelGGL(k_restir_frame_begin, dim3(blocks_for(P.rs_hi - P.rs_lo)), dim3(TB), 0, st, P, d_frames + s);
         P.rs_out = restir_buffer(P, cfg.restir_out_sp2);
         hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(&P.counters[CTR_Q0]), n, 1, st);   // the camera queue
         if (defer) {
             restir_first_bounce(S, P, d_frames + s, hf[s], cfg, st);
+            if (cfg.halo_fn) cfg.halo_prev = cfg.halo_rows;
+            // the band's reservoirs (rs_keep_n = the band's pixels, read by k_shade at the pixel's slot)
             const size_t rn = 3 * (size_t)PF.rs_keep_n;
-            hipMemcpyAsync(PF.rs_keep + (size_t)s * rn, P.rs_out, rn * sizeof(float4), hipMemcpyDeviceToDevice, st);
+            hipMemcpyAsync(PF.rs_keep + (size_t)s * rn, P.rs_out + 3 * (size_t)PF.pix_off, rn * sizeof(float4),
+                           hipMemcpyDeviceToDevice, st);
             continue;
         }
         frame_bounces(S, P, d_frames + s, hf[s], cfg, st, 0, 0, P.q0, CTR_Q0, P.q1, CTR_Q1, true);
+        if (cfg.halo_fn) cfg.halo_prev = cfg.halo_rows;
         if (nb > 0) {
             // the global queue's first entries never reach the next sample's slots: after
             // sample s it holds at most (s + 1) * n entries

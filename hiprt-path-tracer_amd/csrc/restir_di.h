@@ -747,7 +747,8 @@ RESTIR_KERNEL void k_restir_initial(DevScene S, DevPaths P, const MptFrame* __re
                 }
             }
             // ReSTIR_DI_InitialTargetFunctionVisibility (InitialCandidates.h:248-264)
-            if (F.options.restir_di_initial_target_visibility && target > 0.0f) {
+            // InitialCandidates.h:248-249: no visibility in the target function at low resolution
+            if (F.options.restir_di_initial_target_visibility && !low_res(F.render_settings) && target > 0.0f) {
                 if (rr.at(RP_LIGHT(i)).any(ep, tl, dist, g.last)) { r.M++; continue; }
                 flags |= RF_UNOCCLUDED;
             }
@@ -1901,6 +1902,8 @@ __global__ __launch_bounds__(TB) void k_restir_frame_begin(DevPaths P, const Mpt
     const MptRenderSettings& rs = F.render_settings;
     int i = P.rs_lo + blockIdx.x * TB + threadIdx.x;   // the band and its halo rows
     if (i >= P.rs_hi) return;
+    // low resolution: only the representatives' entries (pixel_index / s) are copied and reset
+    if (low_res(rs) && !low_res_region(F, i % F.res_x, i / F.res_x)) return;
     if (rs.restir_di_settings.do_temporal_reuse_pass) {
         P.pgb_pos[i] = P.gb_pos[i]; P.pgb_sn[i] = P.gb_sn[i]; P.pgb_gn[i] = P.gb_gn[i]; P.pgb_view[i] = P.gb_view[i];
         int4 meta = P.gb_meta[i];

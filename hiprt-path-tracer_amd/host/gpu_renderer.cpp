@@ -14,30 +14,65 @@ namespace mpt_host {
 LocalHaloGroup::LocalHaloGroup(int band_count, int band_height, std::vector<int> devices)
     : m_n(band_count), m_bh(band_height), m_devices(std::move(devices)), m_members(band_count),
       m_published(band_count), m_need(band_count, 0) {
-    for (int k = 0; k < m_n; k++) m_members[k] = Member{this, k};
+    for (int k = 0; k < m_n; k++) m_members[k] = Member{this, k, 0};
 }
 
-void LocalHaloGroup::wait() {
+bool LocalHaloGroup::wait() {
     std::unique_lock<std::mutex> lk(m_mu);
+    if (m_aborted) return false;
     const unsigned gen = m_generation;
     if (++m_arrived == m_n) {
         m_arrived = 0;
         m_generation++;
         m_cv.notify_all();
     } else {
-        m_cv.wait(lk, [&] { return m_generation != gen; });
+        m_cv.wait(lk, [&] { return m_generation != gen || m_aborted; });
     }
+    return m_generation != gen;   // an abort after the last arrival still completes this barrier
+}
+
+void LocalHaloGroup::abort(int rank) {
+    std::lock_guard<std::mutex> lk(m_mu);
+    if (!m_aborted) m_origin = rank;
+    m_aborted = true;
+    m_cv.notify_all();
+}
+
+int LocalHaloGroup::abort_origin() {
+    std::lock_guard<std::mutex> lk(m_mu);
+    return m_aborted ? m_origin : -1;
+}
+
+void LocalHaloGroup::reset() {
+    std::lock_guard<std::mutex> lk(m_mu);
+    m_aborted = false;
+    m_origin = -1;
+    m_arrived = 0;
+    m_generation++;
+    for (Member& m : m_members) m.calls = 0;
+}
+
+bool LocalHaloGroup::aborted() {
+    std::lock_guard<std::mutex> lk(m_mu);
+    return m_aborted;
 }
 
 int LocalHaloGroup::exchange(void* user, MptHaloExchange* x) {
     Member* me = (Member*)user;
     LocalHaloGroup& g = *me->group;
     const int k = me->rank;
+    const bool inject = k == g.m_fail_rank && me->calls == g.m_fail_call;
+    me->calls++;
     hipStream_t st = (hipStream_t)x->stream;
     int rc = hipSetDevice(g.m_devices[k]) == hipSuccess && hipStreamSynchronize(st) == hipSuccess ? 0 : 1;   // own rows final
+    if (inject) rc = 1;
+    if (rc != 0) {   // the others must not wait for this member's rows
+        g.abort(k);
+        return rc;
+    }
     g.m_published[k] = *x;
     g.m_need[k] = x->halo_rows;
-    g.wait();
+    if (!g.wait()) return 1;
     if (x->phase == MPT_HALO_GBUFFER) x->halo_rows = *std::max_element(g.m_need.begin(), g.m_need.end());
     // rows [y0 - halo, y0) and [y1, y1 + halo) of every buffer, from the bands that own them
     const int h = x->halo_rows;
@@ -56,7 +91,8 @@ int LocalHaloGroup::exchange(void* user, MptHaloExchange* x) {
         }
     }
     if (hipStreamSynchronize(st) != hipSuccess) rc = 1;
-    g.wait();   // nobody overwrites rows another member is still copying
+    if (rc != 0) g.abort(k);
+    if (!g.wait()) return 1;   // nobody overwrites rows another member is still copying
     return rc;
 }
 
@@ -218,6 +254,10 @@ void GPURenderer::flush() {
         m_halo_bh = bh;
         for (int k = 0; k < n; k++) check(mpt_set_halo_exchange(m_ctxs[k], &LocalHaloGroup::exchange, m_halo->member(k)));
     }
+    if (restir) {
+        m_halo->reset();
+        m_halo->inject_failure(m_fail_band, m_fail_call);
+    }
     std::vector<int> rcs(n, MPT_OK);
     std::vector<std::string> errs(n);
     std::vector<std::thread> th;
@@ -226,11 +266,26 @@ void GPURenderer::flush() {
             std::vector<MptFrame> fr = m_last_frames;
             for (MptFrame& f : fr) band_fields(f, k);
             rcs[k] = mpt_render_frames(m_ctxs[k], fr.data(), (int32_t)fr.size(), 0);
-            if (rcs[k] != MPT_OK) errs[k] = mpt_last_error();   // the error text is per thread
+            if (rcs[k] != MPT_OK) {
+                errs[k] = mpt_last_error();   // the error text is per thread
+                // a band that stops before its next exchange point must not leave the others waiting
+                if (restir) m_halo->abort(k);
+            }
         });
     for (auto& t : th) t.join();
-    for (int k = 0; k < n; k++)
-        if (rcs[k] != MPT_OK) throw std::runtime_error("libmpt (band " + std::to_string(k) + "): " + errs[k]);
+    // the band that failed first names the cause (the others report the aborted exchange)
+    int first = restir ? m_halo->abort_origin() : -1;
+    if (first < 0 || rcs[first] == MPT_OK) {
+        first = -1;
+        for (int k = 0; k < n && first < 0; k++)
+            if (rcs[k] != MPT_OK) first = k;
+    }
+    if (first >= 0) {
+        std::string all;
+        for (int k = 0; k < n; k++)
+            if (rcs[k] != MPT_OK) all += "; band " + std::to_string(k) + ": " + errs[k];
+        throw std::runtime_error("libmpt (band " + std::to_string(first) + "): " + errs[first] + " [" + all.substr(2) + "]");
+    }
 }
 
 void GPURenderer::render() {
@@ -259,6 +314,8 @@ void GPURenderer::render() {
     }
     m_in_render = false;
     flush();
+    // GPURenderer.cpp:458: do_render_low_resolution (RenderSettings.h:195-198)
+    m_was_last_frame_low_resolution = rs.wants_render_low_resolution && rs.allow_render_low_resolution && rs.accumulate;
 }
 
 void GPURenderer::synchronize_kernel() {
@@ -306,8 +363,23 @@ void GPURenderer::get_framebuffer(int kind, float* dst_rgb) {
 }
 
 void GPURenderer::get_aux_buffer(int kind, void* dst) {
-    if (kind >= MPT_AUX_RESTIR_OUTPUT) {   // frame-sized reservoirs: the first context's copy
-        check(mpt_get_aux_buffer(m_ctxs[0], kind, dst, 0));
+    if (kind >= MPT_AUX_RESTIR_OUTPUT) {
+        // frame-sized reservoirs (48 B per pixel): a context keeps only its own contiguous band (plus
+        // halo rows) current, so each band's rows come from the context that owns it
+        const int n = (int)m_ctxs.size();
+        if (n == 1) {
+            check(mpt_get_aux_buffer(m_ctxs[0], kind, dst, 0));
+            return;
+        }
+        const size_t row = (size_t)m_width * 48;
+        const int bh = (m_height + n - 1) / n;   // band_fields' ReSTIR DI partition
+        std::vector<char> tmp((size_t)m_height * row);
+        for (int k = 0; k < n; k++) {
+            const int y0 = std::min(m_height, k * bh), y1 = std::min(m_height, y0 + bh);
+            if (y0 >= y1) continue;
+            check(mpt_get_aux_buffer(m_ctxs[k], kind, tmp.data(), 0));
+            std::memcpy((char*)dst + (size_t)y0 * row, tmp.data() + (size_t)y0 * row, (size_t)(y1 - y0) * row);
+        }
         return;
     }
     check(mpt_gather(m_ctxs.data(), (int32_t)m_ctxs.size(), 0, MPT_GATHER_AUX + kind, dst, 0));

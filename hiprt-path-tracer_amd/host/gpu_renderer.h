@@ -47,16 +47,25 @@ struct DisplayBuffers {
 // publishes its buffers, waits for the others, copies its halo rows from the owners (peer
 // copies between GPUs) on its own stream and waits again, so that no owner overwrites rows
 // still being read.  (mpt.partition.LocalHaloGroup is the same protocol in Python.)
+// A member that fails (its copies, or its context's render returning an error before the
+// next exchange point) aborts the group: every waiting and every later exchange returns
+// non-zero at once, so all band threads unwind and the renderer throws instead of hanging.
 class LocalHaloGroup {
 public:
     LocalHaloGroup(int band_count, int band_height, std::vector<int> devices);
     // the MptHaloExchangeFn of member `rank` (user = the Member)
-    struct Member { LocalHaloGroup* group; int rank; };
+    struct Member { LocalHaloGroup* group; int rank; int calls; };
     Member* member(int rank) { return &m_members[rank]; }
     static int exchange(void* user, MptHaloExchange* x);
+    void abort(int rank);   // wakes every member; exchanges fail until reset(); records the first rank
+    int abort_origin();     // the member that aborted first (-1: none)
+    void reset();    // a new render: no member waiting, not aborted
+    bool aborted();
+    // test hook: member `rank`'s callback fails at its `call`-th exchange (0-based) of a render
+    void inject_failure(int rank, int call) { m_fail_rank = rank; m_fail_call = call; }
 
 private:
-    void wait();   // generation barrier over the band_count members
+    bool wait();   // generation barrier over the band_count members; false once aborted
     int m_n, m_bh;
     std::vector<int> m_devices;
     std::vector<Member> m_members;
@@ -66,6 +75,9 @@ private:
     std::condition_variable m_cv;
     int m_arrived = 0;
     unsigned m_generation = 0;
+    bool m_aborted = false;
+    int m_origin = -1;
+    int m_fail_rank = -1, m_fail_call = -1;
 };
 
 class GPURenderer {
@@ -123,6 +135,9 @@ public:
     void launch_path_tracing();
     // reset (GPURenderer.cpp:953-973): restart the accumulation, m_rng re-seeded 42
     void reset();
+    // was_last_frame_low_resolution (GPURenderer.cpp:458, 512-515): the last render() ran in the
+    // low-resolution interactive mode (RenderWindow displays its top-left block scaled up)
+    bool was_last_frame_low_resolution() const { return m_was_last_frame_low_resolution; }
     void synchronize_kernel();
     bool frame_render_done();
 
@@ -146,7 +161,8 @@ public:
     // the 'pixels' sum buffer and the denoiser AOVs (RenderData.h:32-36), host copy
     void get_framebuffer(int kind, float* dst_rgb);
     // pixel_sample_count / pixel_converged_sample_count / pixel_squared_luminance
-    // (RenderData.h:62-84; get_pixels_converged_sample_count_buffer, GPURenderer.h:193), host copy
+    // (RenderData.h:62-84; get_pixels_converged_sample_count_buffer, GPURenderer.h:193), host copy;
+    // the ReSTIR DI reservoir kinds (frame-sized): each band's rows from the context that owns them
     void get_aux_buffer(int kind, void* dst);
     int render_width() const { return m_width; }
     int render_height() const { return m_height; }
@@ -154,6 +170,9 @@ public:
     // the whole frame)
     const std::vector<MptFrame>& last_frames() const { return m_last_frames; }
     int device_count() const { return (int)m_ctxs.size(); }
+    // test hook (tests/test_host_cpp.py): band `band`'s halo exchange fails at its `call`-th
+    // exchange of a render -- the render must throw, not hang
+    void inject_halo_failure(int band, int call) { m_fail_band = band; m_fail_call = call; }
 
 private:
     void check(int rc) const;
@@ -165,6 +184,7 @@ private:
     std::vector<int> m_devices;
     std::unique_ptr<LocalHaloGroup> m_halo;   // ReSTIR DI over several contexts
     int m_halo_bh = 0;
+    int m_fail_band = -1, m_fail_call = -1;
     Xorshift32 m_rng{42};
     int m_width = 0, m_height = 0;
     MptFrame m_render_data{};
@@ -174,6 +194,7 @@ private:
     bool m_in_render = false;
     bool m_has_envmap = false;
     bool m_mapped = false;
+    bool m_was_last_frame_low_resolution = false;
     std::string m_envmap_path;
     DisplayBuffers m_display;
     MptStatus m_status{};

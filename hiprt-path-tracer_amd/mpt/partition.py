@@ -227,6 +227,13 @@ class LocalHaloGroup:
 
     def member(self, rank: int):
         def exchange(x):
+            try:
+                _exchange(x)
+            except BaseException:
+                self.barrier.abort()     # no other member waits for this one's rows
+                raise
+
+        def _exchange(x):
             torch = self.torch
             dev = self.devices[rank]
             views = _row_views(x, torch, dev)

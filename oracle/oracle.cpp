@@ -32,7 +32,9 @@
  *     csrc/tmath.h with the product; pinned against double libm by tests/test_tmath.py);
  *   * alpha testing draws the candidate's uniform from a hash of (query, primitive)
  *     instead of the path's RNG inside HIPRT's traversal (same accept probability);
- *   * the low-resolution interactive mode is rejected (a data race in the reference);
+ *   * the low-resolution interactive mode renders the reference's evident intent where its
+ *     pixel_active writes race (CameraRays.h:63-76): the top-left ceil(W/s) x ceil(H/s)
+ *     pixels are active, every other pixel inactive;
  *   * undefined behaviour of the reference (uninitialised locals) is given a fixed value.
  *
  * PARITY STATUS: "parity unpinned" against the reference itself -- the reference's
@@ -659,6 +661,11 @@ struct RISReservoir {
     void end() { if (wsum == 0.0f) UCW = 0.0f; else UCW = 1.0f / sample.target * wsum; }
 };
 
+// do_render_low_resolution (RenderSettings.h:195-198)
+inline bool low_res(const MptRenderSettings& rs) {
+    return rs.wants_render_low_resolution && rs.allow_render_low_resolution && rs.accumulate;
+}
+
 Col sample_lights_ris(Ctx& c, const Payload& pl, const HitInfo& hi, f3 view, Rng& rng) {
     const OScene& s = *c.s;
     const MptRenderSettings& rs = c.f->render_settings;
@@ -666,7 +673,8 @@ Col sample_lights_ris(Ctx& c, const Payload& pl, const HitInfo& hi, f3 view, Rng
     bool inside = dot(view, hi.geometric_normal) < 0;
     float ism = inside ? -1.0f : 1.0f;
     f3 ep = hi.inter_point + hi.shading_normal * 1.0e-4f * ism;
-    int nl = rs.ris_number_of_light_candidates, nb = rs.ris_number_of_bsdf_candidates;
+    // RIS.h:93-94: one candidate of each at low resolution
+    int nl = low_res(rs) ? 1 : rs.ris_number_of_light_candidates, nb = low_res(rs) ? 1 : rs.ris_number_of_bsdf_candidates;
     RISReservoir res;
     for (int i = 0; i < nl; i++) {
         float lpdf, dist, cl, ce;
@@ -693,7 +701,7 @@ Col sample_lights_ris(Ctx& c, const Payload& pl, const HitInfo& hi, f3 view, Rng
                     enough = min_contrib(rs.minimum_light_contribution, lc / bp / lpdf);
                     target = enough ? lc.luminance() : 0.0f;
                 }
-                if (c.f->options.ris_use_visibility && target > 0.0f) {
+                if (c.f->options.ris_use_visibility && !low_res(rs) && target > 0.0f) {   // RIS.h:162
                     bool vis = !shadow_ray(c, ep, tl, dist, hi.prim, 1);
                     target *= vis ? 1.0f : 0.0f;
                 }
@@ -978,6 +986,14 @@ inline uint32_t frame_pixel_seed(const MptFrame& f, uint32_t pix, uint32_t rando
     return rs.freeze_random ? wang_hash(pix + 1u) : wang_hash((pix + 1u) * (uint32_t)(rs.sample_number + 1) * random_seed);
 }
 
+// CameraRays.h:63-76 at low resolution: representative (x, y) (multiples of s) renders at
+// pixel_index / s = (x / s, y / s); so pixel (x, y) of the frame is rendered iff it lies in the
+// top-left ceil(W / s) x ceil(H / s) block, through the representative's ray (s x, s y)
+inline bool low_res_rendered(const MptFrame& f, int x, int y) {
+    const int s = f.render_settings.render_low_resolution_scaling;
+    return x < (f.res_x + s - 1) / s && y < (f.res_y + s - 1) / s;
+}
+
 // CameraRays (CameraRays.h:127-179): primary ray + G-buffer write.  The seed is the
 // camera launch's (GPURenderer::launch_camera_rays) when the frame carries one, else
 // the frame seed (CPURenderer: one seed per sample).
@@ -991,7 +1007,10 @@ void camera_pixel(Ctx& c, int x, int y, GB& gb) {
     c.bounce = 0;
     {   // ---- CameraRays
         Rng rng(seed);
-        float xd = (float)x + 0.5f, yd = (float)y + 0.5f;
+        // low resolution: this pixel is pixel_index / s of its representative (s x, s y), whose
+        // thread computes the ray (CameraRays.h:127-131) with the divided index's seed
+        const int ls = low_res(rs) ? rs.render_low_resolution_scaling : 1;
+        float xd = (float)(x * ls) + 0.5f, yd = (float)(y * ls) + 0.5f;
         if (f.current_camera.do_jittering) { xd += rng() - 0.5f; yd += rng() - 0.5f; }
         f3 o, d;
         camera_ray(f.current_camera, xd, yd, f.res_x, f.res_y, o, d);
@@ -1037,7 +1056,9 @@ PixelOut path_pixel(Ctx& c, int x, int y, GB& gb) {
     pl.material = gb.mat;
     pl.vs = gb.vs;
     const MptWorldSettings& w = f.world_settings;
-    for (int bounce = 0; bounce < rs.nb_bounces + 1; bounce++) {
+    // FullPathTracer.h:117-122: at most 3 bounces at low resolution
+    const int nb_bounces = low_res(rs) ? std::min(3, rs.nb_bounces) : rs.nb_bounces;
+    for (int bounce = 0; bounce < nb_bounces + 1; bounce++) {
         if (pl.missed) break;
         c.bounce = bounce;
         if (bounce > 0) found = trace_ray(c, ro, rd, pl, hi, hi.prim, rng);
@@ -1247,7 +1268,7 @@ int oracle_render(OracleScene* sc, const MptFrame* frames, int nframes, float* s
     const MptFrame& f0 = frames[0];
     const bool restir = f0.options.direct_light_sampling == MPT_LSS_RESTIR_DI;
     if ((has_adaptive_buffers(f0.render_settings) && !(as_count && as_sqlum && as_conv && status)) ||
-        f0.render_settings.wants_render_low_resolution ||
+        (low_res(f0.render_settings) && (f0.render_settings.render_low_resolution_scaling < 1)) ||
         (restir && (f0.band_count != 1 || f0.render_settings.restir_di_settings.number_of_passes > 4)) ||
         (f0.options.envmap_sampling == MPT_ESS_BINARY_SEARCH && s.env_rgba && !s.env_cdf))
         return -4;
@@ -1300,6 +1321,10 @@ int oracle_render(OracleScene* sc, const MptFrame* frames, int nframes, float* s
             for (int x = 0; x < W; x++) {
                 size_t o = (size_t)r * W + x;
                 float* p = sum_rgb + 3 * o;
+                if (low_res(rs) && !low_res_rendered(f, x, y)) {   // CameraRays.h:68-72
+                    active[o] = 0;
+                    continue;
+                }
                 if (use_prev) gprev[o] = gbuf[o];
                 if ((rs.sample_number == 0 || rs.need_to_reset) && restir && rs.accumulate) {
                     B.init[o] = OResv(); B.sp1[o] = OResv(); B.sp2[o] = OResv();   // reset_render (CameraRays.h:19-34)
@@ -1391,7 +1416,16 @@ int oracle_render(OracleScene* sc, const MptFrame* frames, int nframes, float* s
                 float* p = sum_rgb + 3 * o;
                 if (restir) c.restir_out = &(*B.output)[o];
                 PixelOut po = path_pixel(c, x, y, gbuf[o]);
-                if (!po.valid) continue;   // sanity_check fails -> no buffer write (FullPathTracer.h:293-294)
+                if (!po.valid) {
+                    // sanity_check fails -> no buffer write (FullPathTracer.h:293-294), except the
+                    // debug colour of display_NaNs (debug_set_final_color, FullPathTracer.h:29-35, 88-91)
+                    if (rs.display_NaNs) {
+                        Col dc(1.0e30f, 0.0f, 1.0e30f);
+                        if (rs.sample_number != 0) dc = dc * (float)rs.sample_number;
+                        p[0] = dc.r; p[1] = dc.g; p[2] = dc.b;
+                    }
+                    continue;
+                }
                 if (status) status[1] = 1u;
                 if (as) { float l = po.color.luminance(); as_sqlum[o] += l * l; }
                 if (rs.sample_number == 0) { p[0] = po.color.r; p[1] = po.color.g; p[2] = po.color.b; }

@@ -272,6 +272,7 @@ void restir_initial(Ctx& c, RestirPassCtx& R, int x, int y) {
     c.pseed = seed;
     RestirRays rr{c, 5};
     int nl = rd.number_of_initial_light_candidates, nb = rd.number_of_initial_bsdf_candidates;
+    if (low_res(f.render_settings)) { nl = std::min(1, nl); nb = std::min(1, nb); }   // InitialCandidates.h:420-421
     float env_p = 0.0f;
     if (w.ambient_light_type == MPT_AMBIENT_ENVMAP) env_p = s.n_emissive == 0 ? 1.0f : rd.envmap_candidate_probability;
     OResv r;
@@ -349,7 +350,7 @@ void restir_initial(Ctx& c, RestirPassCtx& R, int x, int y) {
             }
         }
         // ReSTIR_DI_InitialTargetFunctionVisibility (InitialCandidates.h:248-264)
-        if (f.options.restir_di_initial_target_visibility && target > 0.0f) {
+        if (f.options.restir_di_initial_target_visibility && !low_res(f.render_settings) && target > 0.0f) {
             if (rr.at(RP_LIGHT(i)).any(ep, tl, dist, g.prim)) { r.M++; continue; }
             flags |= RF_UNOCCLUDED;
         }

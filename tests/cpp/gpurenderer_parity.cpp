@@ -14,6 +14,8 @@
 #include <hip/hip_runtime_api.h>
 
 #include <cstdio>
+#include <cstdlib>
+#include <algorithm>
 #include <cstring>
 #include <stdexcept>
 #include <vector>
@@ -64,6 +66,13 @@ int main(int argc, char** argv) {
         // n_split > 1: the frame tiled across n_split contexts (here all on device 0), gathered
         // with mpt_gather
         mpt_host::GPURenderer gr(std::vector<int>(n_split > 1 ? n_split : 1, 0));
+        // test hooks: GPURENDERER_HALO_FAIL="band,call" makes that band's halo exchange fail (the
+        // render must throw, not hang); GPURENDERER_RESTIR_AUX=<path> writes the ReSTIR DI output
+        // reservoirs (get_aux_buffer, each band's rows from its owner) after the render
+        if (const char* hf = getenv("GPURENDERER_HALO_FAIL")) {
+            int band = -1, call = -1;
+            if (sscanf(hf, "%d,%d", &band, &call) == 2) gr.inject_halo_failure(band, call);
+        }
         MptScene s{};
         s.triangle_indices = idx.data(); s.num_triangles = T;
         s.vertices = pos.data(); s.vertex_normals = nrm.data(); s.has_vertex_normals = has_n.data();
@@ -94,7 +103,25 @@ int main(int argc, char** argv) {
         db.color = display;
         gr.set_display_buffers(db);
         std::vector<MptFrame> frames;
+        // GPURENDERER_INTERACT="u0,u1,...": the displayed frames during which the user moves the
+        // camera -- RenderWindow.cpp:797-802 sets wants_render_low_resolution = is_interacting() and,
+        // with auto_sample_per_frame, one sample per frame while rendering at low resolution
+        std::vector<int> interact;
+        if (const char* it = getenv("GPURENDERER_INTERACT"))
+            for (const char* p = it; *p;) {
+                interact.push_back(atoi(p));
+                while (*p && *p != ',') p++;
+                if (*p == ',') p++;
+            }
+        const int spf0 = gr.get_render_settings().samples_per_frame;
+        int low_frames = 0;
         for (int u = 0; u < n_updates; u++) {   // RenderWindow::render: update() then render() per displayed frame
+            if (!interact.empty()) {
+                MptRenderSettings& rs = gr.get_render_settings();
+                rs.wants_render_low_resolution = std::find(interact.begin(), interact.end(), u) != interact.end();
+                const bool low = rs.wants_render_low_resolution && rs.allow_render_low_resolution && rs.accumulate;
+                rs.samples_per_frame = (low || gr.was_last_frame_low_resolution()) ? 1 : spf0;
+            }
             gr.update();
             if (mode == 0) {
                 gr.render();
@@ -116,7 +143,9 @@ int main(int argc, char** argv) {
                 }
             }
             gr.unmap_buffers();
+            low_frames += gr.was_last_frame_low_resolution() ? 1 : 0;
         }
+        if (!interact.empty() && low_frames != (int)interact.size()) throw std::runtime_error("was_last_frame_low_resolution");
         gr.synchronize_kernel();
         if (gr.get_render_data().render_settings.sample_number != (int)frames.size())
             throw std::runtime_error("render data sample_number");
@@ -131,6 +160,14 @@ int main(int argc, char** argv) {
         gr.get_aux_buffer(MPT_AUX_SAMPLE_COUNT, cnt.data());
         gr.copy_status_buffers();
         MptStatus st = gr.get_status_buffer_values();
+        if (const char* ap = getenv("GPURENDERER_RESTIR_AUX")) {
+            std::vector<float> res(px * 12);
+            gr.get_aux_buffer(MPT_AUX_RESTIR_OUTPUT, res.data());
+            FILE* fa = fopen(ap, "wb");
+            if (!fa) throw std::runtime_error("cannot open aux output");
+            fwrite(res.data(), sizeof(float), res.size(), fa);
+            fclose(fa);
+        }
         FILE* fo = fopen(argv[2], "wb");
         if (!fo) throw std::runtime_error("cannot open output");
         int32_t nf = (int32_t)frames.size();

@@ -133,6 +133,38 @@ def test_c4_city_restir_full_frame_bit_exact(city, luts, city_oracle, fused):
     assert np.isfinite(got).all() and got.mean() > 0
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("nb", [2, 4])
+def test_c4_city_partitioned_batched_bit_exact(city, luts, city_oracle, nb):
+    """C4 tile-parallel: the 1920x1080 city frame split into nb contiguous bands
+    (contexts on cuda:0, one host thread each, the in-process halo exchange), each context's
+    samples BATCHED through mpt_render_frames (per-sample reuse passes with their halo exchange
+    inside the batch, shared later bounces) -- the same sums as the single-context batched render,
+    which test_c4_city_restir_full_frame_bit_exact pins to the oracle."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from test_restir import render_partitioned_local
+    _, env = city_oracle
+    n = 4
+
+    def make(band):
+        frs = c4_frames(city, n)
+        for f in frs:
+            f.band_height, f.band_index, f.band_count = band
+        return frs
+
+    r = _gpu(city, luts, env)
+    r.render_samples(c4_frames(city, n))
+    r.synchronize_kernel()
+    ref = r.framebuffer(abi.FB_COLOR)
+    r.close()
+    st = []
+    got = render_partitioned_local(city, luts, make, 1920, 1080, nb, env=env, batch=n, stats=st)
+    _same(got, ref, f"C4 city over {nb} bands, batched")
+    # one wavefront per batch for bounces 0..3 (the envmap defers bounce 0): 4 shading launches
+    assert all(0 < x.shade_launches <= 4 for x in st), [x.shade_launches for x in st]
+
+
 # ---- C5: glass dispersion + nested dielectrics at 16 bounces, 4K camera crop ---------------------
 
 @pytest.mark.gpu

@@ -127,3 +127,73 @@ def test_cpp_gpurenderer_matches_oracle(cornell, luts, tmp_path, case):
     assert np.array_equal(img, ref), f"{case}: {(img != ref).sum()} values differ"
     assert np.array_equal(cnt, o.last_aux["sample_count"]), f"{case}: pixel_sample_count differs"
     assert img.mean() > 0
+
+
+def _restir_blob(cornell, luts, path, split, spf=2, updates=2):
+    st = scene.parity_settings(3)
+    st.samples_per_frame = spf
+    opt = abi.KernelOptions.default()
+    opt.direct_light_sampling = abi.LSS_RESTIR_DI
+    cam = scene.make_camera(cornell.camera_info, W, H)
+    _blob(path, cornell, luts, st, abi.WorldSettings.default(), opt, cam, updates, 0, [], split)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("split", [2, 3])
+def test_cpp_restir_aux_reservoirs_assembled_from_owners(cornell, luts, tmp_path, split):
+    """get_aux_buffer(MPT_AUX_RESTIR_OUTPUT) of the tiled renderer: each band's rows come from
+    the context that owns them, so the frame equals the single-context reservoirs byte for byte."""
+    outs = {}
+    for sp in (1, split):
+        blob, out, aux = tmp_path / f"in{sp}.blob", tmp_path / f"out{sp}.bin", tmp_path / f"aux{sp}.bin"
+        _restir_blob(cornell, luts, blob, sp)
+        env = dict(os.environ, GPURENDERER_RESTIR_AUX=str(aux))
+        r = subprocess.run([str(_build.HOST_TEST), str(blob), str(out)], capture_output=True, text=True, timeout=120, env=env)
+        assert r.returncode == 0, r.stderr
+        outs[sp] = (_read_out(out)[1], np.fromfile(aux, np.float32).reshape(H, W, 12))
+    assert np.array_equal(outs[1][0], outs[split][0])
+    assert np.array_equal(outs[1][1], outs[split][1]), f"{(outs[1][1] != outs[split][1]).sum()} reservoir values differ"
+    assert (outs[1][1][..., 0] > 0).any()    # M > 0 somewhere: the buffers hold reservoirs
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("band,call", [(0, 0), (1, 0), (1, 3), (2, 5)])
+def test_cpp_restir_halo_failure_throws_not_hangs(cornell, luts, tmp_path, band, call):
+    """A band whose halo exchange fails aborts the LocalHaloGroup: every band thread unwinds
+    and render() throws the failing band's error instead of leaving the others waiting."""
+    blob, out = tmp_path / "in.blob", tmp_path / "out.bin"
+    _restir_blob(cornell, luts, blob, 3)
+    env = dict(os.environ, GPURENDERER_HALO_FAIL=f"{band},{call}")
+    r = subprocess.run([str(_build.HOST_TEST), str(blob), str(out)], capture_output=True, text=True, timeout=60, env=env)
+    assert r.returncode == 1, (r.returncode, r.stdout, r.stderr)
+    assert f"band {band}" in r.stderr and "halo exchange" in r.stderr, r.stderr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("lss", [abi.LSS_RIS_BSDF_AND_LIGHT, abi.LSS_RESTIR_DI], ids=["ris", "restir"])
+@pytest.mark.parametrize("split", [1, 2])
+def test_cpp_interaction_low_resolution_matches_oracle(cornell, luts, tmp_path, lss, split):
+    """RenderWindow's interaction: while the camera moves (displayed frames 1 and 2 here) it sets
+    wants_render_low_resolution = is_interacting() (RenderWindow.cpp:797) with one sample per
+    frame (:798-802); allow_render_low_resolution is on by default (RenderSettings.h:115).  The
+    C++ mirror renders those frames at low resolution, reports was_last_frame_low_resolution,
+    and the image equals the oracle's on the frames it enqueued."""
+    from oracle import oracle as orc
+    st = scene.parity_settings(5)
+    st.samples_per_frame = 2
+    st.render_low_resolution_scaling = 2
+    opt = abi.KernelOptions.default()
+    opt.direct_light_sampling = lss
+    cam = scene.make_camera(cornell.camera_info, W, H)
+    blob, out = tmp_path / "in.blob", tmp_path / "out.bin"
+    _blob(blob, cornell, luts, st, abi.WorldSettings.default(), opt, cam, 4, 0, [], split)
+    env = dict(os.environ, GPURENDERER_INTERACT="1,2")
+    r = subprocess.run([str(_build.HOST_TEST), str(blob), str(out)], capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 0, r.stderr
+    frames, img, cnt = _read_out(out)
+    low = [f.render_settings.wants_render_low_resolution for f in frames]
+    assert low == [False, False, True, True, False], low      # 2 spp, then 1 + 1 at low resolution, then 1
+    o = orc.Oracle(cornell, luts)
+    ref = o.render(frames)
+    o.close()
+    assert np.array_equal(img, ref), f"{(img != ref).sum()} values differ"

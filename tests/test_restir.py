@@ -373,9 +373,12 @@ def _renderer(sd, luts, env=None):
     return r
 
 
-def render_partitioned_local(sd, luts, make_frames, w, h, nb, env=None):
+def render_partitioned_local(sd, luts, make_frames, w, h, nb, env=None, batch=None, stats=None):
     """nb contexts on cuda:0, one contiguous band each, rendered from nb threads with the
-    in-process halo exchange; returns the assembled frame (sums) and the bytes exchanged."""
+    in-process halo exchange; returns the assembled frame (sums).  batch: the frames go through
+    mpt_render_frames with that max_batch (batched ReSTIR DI samples, the halo exchanged per
+    sample inside the batch) instead of one mpt_render_frame each; stats: a list that receives
+    each context's abi.Stats."""
     import threading
     from mpt import partition
     bh = partition.contiguous_band(h, nb, 0)[0]
@@ -383,12 +386,18 @@ def render_partitioned_local(sd, luts, make_frames, w, h, nb, env=None):
     rs = [_renderer(sd, luts, env) for _ in range(nb)]
     for k, r in enumerate(rs):
         r.set_halo_exchange(group.member(k))
+        if stats is not None:
+            r.enable_stats(timing=True)
     errs = []
 
     def run(k):
         try:
-            for f in make_frames(partition.contiguous_band(h, nb, k)):
-                rs[k].render(f)
+            frs = make_frames(partition.contiguous_band(h, nb, k))
+            if batch is not None:
+                rs[k].render_samples(frs, max_batch=batch)
+            else:
+                for f in frs:
+                    rs[k].render(f)
             rs[k].synchronize_kernel()
         except BaseException as e:
             errs.append(e)
@@ -402,6 +411,8 @@ def render_partitioned_local(sd, luts, make_frames, w, h, nb, env=None):
     if errs:
         raise errs[0]
     out = np.concatenate([r.framebuffer(abi.FB_COLOR) for r in rs])
+    if stats is not None:
+        stats.extend(r.stats() for r in rs)
     for r in rs:
         r.close()
     return out
@@ -431,6 +442,53 @@ def test_gpu_restir_partitioned_bit_exact(cornell, luts, case):
         c = o.render(frames(cornell, abi.LSS_RESTIR_DI, n, w=w, h=h, **kw))
         o.close()
         assert np.array_equal(got, c)
+
+
+PART_BATCH_CASES = {
+    # name: (W, H, bands, max_batch, frames kwargs); 6 frames: batches of 4 + 2 or one of 6
+    "radius4_3bands_b4": (32, 48, 3, 4, dict(reuse_radius=4)),
+    "default_radius_4bands_b6": (24, 96, 4, 6, dict()),
+    "three_passes_b3": (24, 64, 2, 3, dict(passes=3, reuse_radius=6)),
+    "camera_moves_b4": (24, 64, 3, 4, dict(move_at=2, reuse_radius=5)),
+    "unfused_b4": (24, 64, 3, 4, dict(do_fused_spatiotemporal=False, reuse_radius=5)),
+    "envmap_deferred_b4": (24, 64, 3, 4, dict(reuse_radius=5, envmap=True)),
+    "empty_last_band_b4": (24, 9, 4, 4, dict(reuse_radius=2)),    # bands of 3 rows: the 4th is empty
+}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", list(PART_BATCH_CASES))
+def test_gpu_restir_partitioned_batched_bit_exact(cornell, luts, case):
+    """Batched ReSTIR DI samples across a partition (mpt_render_frames: each sample's reuse
+    passes exchange their halo in turn inside the batch) render exactly the single-context
+    frame sample by sample, and the oracle's."""
+    import mpt
+    from oracle import oracle as orc
+    w, h, nb, mb, kw = PART_BATCH_CASES[case]
+    kw = dict(kw)
+    env = None
+    if kw.pop("envmap", False):
+        env = mpt.build_envmap(scene.procedural_sky(128, 64, seed=7))
+        kw["world"] = scene.envmap_world(1.0)
+    n = 6
+    r = _renderer(cornell, luts, env)
+    for f in frames(cornell, abi.LSS_RESTIR_DI, n, w=w, h=h, **kw):
+        r.render(f)
+    r.synchronize_kernel()
+    ref = r.framebuffer(abi.FB_COLOR)
+    r.close()
+    st = []
+    got = render_partitioned_local(cornell, luts, lambda band: frames(cornell, abi.LSS_RESTIR_DI, n, w=w, h=h, band=band, **kw),
+                                   w, h, nb, env=env, batch=mb, stats=st)
+    assert got.shape == ref.shape
+    assert np.array_equal(got, ref), f"{case}: {(got != ref).sum()} values differ"
+    assert got.mean() > 0
+    # batched: fewer shading launches than one wavefront per sample would take
+    assert 0 < st[0].shade_launches < n * 4, st[0].shade_launches
+    o = orc.Oracle(cornell, luts, envmap=env)
+    c = o.render(frames(cornell, abi.LSS_RESTIR_DI, n, w=w, h=h, **kw))
+    o.close()
+    assert np.array_equal(got, c)
 
 
 @pytest.mark.gpu
