@@ -82,6 +82,12 @@ def parse():
     ap.add_argument("--batch", type=int, default=0,
                     help="samples per pixel traced as one wavefront (mpt_render_frames); 0 = auto: "
                          "TARGET_PATHS / the rank's pixels, so a rank's launches keep the same size")
+    ap.add_argument("--configs", default="all",
+                    help="after the headline workload, the other BASELINE configs at reduced budgets in the same "
+                         "line ('all' = c1,c2,c4,c5; a comma list; 'none')")
+    ap.add_argument("--config-steps", type=int, default=8, help="timed steps of each extra config")
+    ap.add_argument("--batch1-steps", type=int, default=8,
+                    help="C3: steps also timed with one sample per wavefront (mpt_render_frame's launch set; 0 = skip)")
     ap.add_argument("--emulate-rank-of", type=int, default=1,
                     help="scaling rehearsal on one GPU: render only rank 0's share of an N-way row split "
                          "(the line then reports that rank's rate; not a bench line)")
@@ -306,6 +312,16 @@ def emulate_restir_ranks(a, r, cam, W, H, opt, wset, alpha, n_ranks, K, device):
             "bands": bands, "device": {"libmpt_sha256_16": mpt.build_id()}}
 
 
+_SCENES = {}
+
+
+def _cached(key, make):
+    """Scenes / envmaps shared by the workloads of one process (C3 and C4 use the same city)."""
+    if key not in _SCENES:
+        _SCENES[key] = make()
+    return _SCENES[key]
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -326,6 +342,45 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
+    out = run_workload(a, world, rank, local, dist, coll_dev)
+    if out is not None and world == 1 and a.emulate_rank_of == 1 and a.configs != "none":
+        # the other BASELINE configurations in the same line, each at a reduced budget (their
+        # own spp would take minutes; a step is still one sample per pixel of the full frame)
+        import copy
+        extra = ["c1", "c2", "c4", "c5"] if a.configs == "all" else [w for w in a.configs.split(",") if w]
+        out["configs"] = []
+        for w in extra:
+            if w == a.workload:
+                continue
+            b = copy.copy(a)
+            b.workload, b.steps, b.warmup = w, a.config_steps, 2
+            b.width = b.height = b.scene = b.strategy = b.bounces = None
+            b.bsdf, b.batch = "principled", 0
+            b.cpu_seconds, b.parity_seconds = 5.0, 15.0
+            b.batch1_steps = 0
+            t0 = time.perf_counter()
+            try:
+                o = run_workload(b, world, rank, local, dist, coll_dev, quiet=True)
+                rf = o["roofline"]
+                out["configs"].append({
+                    "workload": o["config"]["workload"], "value": o["value"], "unit": o["unit"],
+                    "ms_per_step": o["ms_per_step"], "steps": o["steps"], "msample_per_s": o["msample_per_s"],
+                    "roofline": {"kernel": rf["kernel"].split(" (")[0], "frac": rf["frac"], "achieved": rf["achieved"],
+                                 "pmc_hbm_frac": rf.get("pmc_hbm_frac"), "traffic_per_unit": rf.get("traffic_per_unit"),
+                                 "bytes_per_unit": rf["bytes_per_unit"]},
+                    "kernel_ms_per_step": {k: v for k, v in o["kernel_ms_per_step"].items() if k != "restir_kernels"},
+                    "cpu_baseline": o["cpu_baseline"], "parity_vs_oracle": o["parity_vs_oracle"],
+                    "wall_s": round(time.perf_counter() - t0, 1)})
+            except Exception as e:   # one config failing must not lose the headline line
+                out["configs"].append({"workload": w, "error": f"{type(e).__name__}: {e}"})
+    if out is not None:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def run_workload(a, world, rank, local, dist, coll_dev, quiet=False):
+    """One workload through the timed region; returns rank 0's line (None on other ranks)."""
     W = a.width or (3840 if a.workload == "c5" else 256 if a.workload == "c1" else 1920)
     H = a.height or (2160 if a.workload == "c5" else 256 if a.workload == "c1" else 1080)
     default_bounces = a.bounces is None
@@ -333,18 +388,21 @@ def main():
     a.bounces = a.bounces if a.bounces is not None else (16 if a.workload == "c5" else 3)
     if a.workload in ("c3", "c3t", "c4"):
         from mpt import synthetic
-        sd = synthetic.procedural_city_textured() if a.workload == "c3t" else synthetic.procedural_city(1234)
-        env = mpt.build_envmap(scene.procedural_sky(2048, 1024, seed=7))
+        sd = (_cached("city_tex", synthetic.procedural_city_textured) if a.workload == "c3t" else
+              _cached("city", lambda: synthetic.procedural_city(1234)))
+        env = _cached("sky", lambda: mpt.build_envmap(scene.procedural_sky(2048, 1024, seed=7)))
         wset = scene.envmap_world(1.0)
         strategy = a.strategy or ("restir" if a.workload == "c4" else "ris")
         K = a.steps or 256
         alpha = True      # C3 pins do_alpha_testing = true (the Bistro's foliage)
-        desc = (f"{a.workload.upper()} stand-in: procedural city (2.86 M tris incl. alpha-tested leaf cards, seed 1234) + "
-                if a.workload != "c3t" else
-                "C3T (texture-realistic C3 variant): procedural city seed 1235, 2.77 M tris, 70 materials, 83 % of the "
-                "triangles textured (base colour + normal map + roughness-metallic, 44 textures / 193 MB RGBA8) + "
-                "procedural HDR sky 2048x1024, alpha testing on"
-                + (", ReSTIR DI fused spatiotemporal + 1 spatial pass, GPURenderer seed schedule" if a.workload == "c4" else ""))
+        if a.workload == "c3t":
+            desc = ("C3T (texture-realistic C3 variant): procedural city seed 1235, 2.77 M tris, 70 materials, 83 % of the "
+                    "triangles textured (base colour + normal map + roughness-metallic, 44 textures / 193 MB RGBA8)")
+        else:
+            desc = f"{a.workload.upper()} stand-in: procedural city (2.86 M tris incl. alpha-tested leaf cards, seed 1234)"
+        desc += " + procedural HDR sky 2048x1024 (alias-table sampling + BSDF MIS), alpha testing on"
+        if a.workload == "c4":
+            desc += ", ReSTIR DI fused spatiotemporal + 1 spatial pass, GPURenderer seed schedule"
     elif a.workload == "c5":
         # glass dispersion + nested dielectrics stress: ISS_WITH_PRIORITIES,
         # stack 3, nb_bounces raised to 16; uniform ambient world
@@ -405,9 +463,9 @@ def main():
     if env is not None:
         r.set_envmap(env)
     if a.workload == "c4" and world == 1 and a.emulate_rank_of > 1:
-        print(json.dumps(emulate_restir_ranks(a, r, cam, W, H, opt, wset, alpha, a.emulate_rank_of, K, local)), flush=True)
+        out = emulate_restir_ranks(a, r, cam, W, H, opt, wset, alpha, a.emulate_rank_of, K, local)
         r.close()
-        return
+        return out
     halo = None
     if a.workload == "c4" and world > 1:
         halo = partition.TorchHaloExchange(dist, band_h)
@@ -458,6 +516,22 @@ def main():
     else:
         rays_total = float(rays_local)
 
+    # launch latency: the same frames with one sample per wavefront (the launch set of
+    # mpt_render_frame, ~50 launches per sample) against the batched wavefronts timed above
+    batch1 = None
+    if a.workload == "c3" and world == 1 and band[2] == 1 and getattr(a, "batch1_steps", 0) > 0:
+        n1 = a.batch1_steps
+        fr1 = frames_for(cam, W, H, opt, band, n1, bounces=a.bounces, world=wset, alpha=alpha)
+        r.enable_stats(timing=False, instrumented=False)
+        r.render_samples(fr1[:2], max_batch=1)
+        r.synchronize_kernel()
+        t1 = time.perf_counter()
+        r.render_samples(fr1, max_batch=1)
+        r.synchronize_kernel()
+        dt1 = time.perf_counter() - t1
+        batch1 = {"steps": n1, "ms_per_step": round(dt1 * 1e3 / n1, 4),
+                  "vs_batched": round((dt1 / n1) / (elapsed / K), 3), "batched_samples_per_launch": batch}
+
     # rooflines (SURVEY.md §8d algorithmic bytes): every traversal stage and the shade
     # kernel; "roofline" is the one with the largest summed time in the timed region
     names = ["k_trace<TM_PATH> (camera/continuation rays, closest hit)", "k_trace<TM_NEE_ANY> (NEE shadow rays, any hit)",
@@ -505,9 +579,10 @@ def main():
     # ReSTIR DI (C4): the staged reuse passes' plain-class target-function evaluations, timed on
     # their own (HIP events around every k_rsp_eval<OVR, true, *> launch, fused and spatial); per
     # evaluation item: item 4 + its record 16 read + 4 written + the evaluated
-    # surface's G-buffer entry 7 x 16 + the sample's reservoir 48 + the material 256 + the
-    # light's emissive-table record 80 + the staged ray 36 = 556 B
-    B_EVAL = 4 + 16 + 4 + 112 + 48 + 256 + 80 + 36
+    # surface's compact 64-B record (gb_cs) + the sample's reservoir 48 + the light's
+    # emissive-table record 80 + the staged ray 36 = 252 B (an untextured surface's material is
+    # the per-material resolved copy, L2-resident: not per-evaluation traffic; PMC r04: 244 B)
+    B_EVAL = 4 + 16 + 4 + 64 + 48 + 80 + 36
     if st.restir_eval_launches:
         el = st.restir_eval_launches
         e_avg = st.restir_eval_ms / el
@@ -661,6 +736,8 @@ def main():
             "cpu_baseline": cpu,
             "parity_vs_oracle": parity,
         }
+        if batch1 is not None:
+            out["batch1"] = batch1
         if band[2] > world:
             out["emulated_rank_of"] = band[2]
             out["msample_per_s"] = round(rows * W * K / elapsed / 1e6, 3)
@@ -668,10 +745,8 @@ def main():
             nfr = 2 + a.warmup + K
             out["halo_exchange"] = {"calls_per_frame": round(halo.calls / nfr, 2),
                                     "mb_received_per_frame_rank0": round(halo.bytes_moved / nfr / 1e6, 3)}
-        print(json.dumps(out), flush=True)
     r.close()
-    if dist is not None:
-        dist.destroy_process_group()
+    return out if rank == 0 else None
 
 
 if __name__ == "__main__":

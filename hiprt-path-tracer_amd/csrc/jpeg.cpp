@@ -20,6 +20,7 @@
 // A vertical flip (stbi_set_flip_vertically_on_load) is the caller's (mpt/image.py).
 #include <cstdint>
 #include <cstdlib>
+#include <climits>
 #include <cstring>
 #include <cmath>
 #include <string>
@@ -187,6 +188,21 @@ struct Jpeg {
         return true;
     }
 
+    // corrupt-stream guards of stb_image 2.28 (stbi__addints_valid / stbi__mul2shorts_valid,
+    // stb_image.h:1068-1083): a DC prediction that would overflow int, or a dequantised DC
+    // beyond int16 (of the int16-truncated operands, as stb computes it), ends the decode
+    static bool addints_valid(int a, int b) {
+        if ((a >= 0) != (b >= 0)) return true;
+        if (a < 0 && b < 0) return a >= INT_MIN - b;
+        return a <= INT_MAX - b;
+    }
+    static bool mul2shorts_valid(int16_t a, int16_t b) {
+        if (b == 0 || b == -1) return true;
+        if ((a >= 0) == (b >= 0)) return a <= SHRT_MAX / b;
+        if (b < 0) return a <= SHRT_MIN / b;
+        return a >= SHRT_MIN / b;
+    }
+
     // ---- one 8x8 block ----
     bool decode_block(int16_t data[64], int b) {
         Comp& c = comp[b];
@@ -195,8 +211,10 @@ struct Jpeg {
         if (t < 0 || t > 15) return fail("bad huffman code");
         std::memset(data, 0, 64 * sizeof(int16_t));
         const int diff = t ? receive_extend(t) : 0;
+        if (!addints_valid(c.dc_pred, diff)) return fail("bad delta");
         const int dc = c.dc_pred + diff;
         c.dc_pred = dc;
+        if (!mul2shorts_valid((int16_t)dc, (int16_t)dq[0])) return fail("can't merge dc and ac");
         data[0] = (int16_t)(dc * dq[0]);
         int k = 1;
         do {
@@ -221,8 +239,10 @@ struct Jpeg {
             const int t = decode(hdc[comp[b].hd]);
             if (t < 0 || t > 15) return fail("bad huffman code");
             const int diff = t ? receive_extend(t) : 0;
+            if (!addints_valid(comp[b].dc_pred, diff)) return fail("bad delta");
             const int dc = comp[b].dc_pred + diff;
             comp[b].dc_pred = dc;
+            if (!mul2shorts_valid((int16_t)dc, (int16_t)(1 << succ_low))) return fail("can't merge dc and ac");
             data[0] = (int16_t)(dc * (1 << succ_low));
         } else if (get_bit()) {
             data[0] = (int16_t)(data[0] + (1 << succ_low));
@@ -298,7 +318,7 @@ struct Jpeg {
 
     bool parse_scan_data();
     bool process_marker(int m);
-    bool frame_header();
+    bool frame_header(bool alloc = true);
     bool scan_header();
     bool decode_image();
 };
@@ -455,7 +475,8 @@ bool Jpeg::process_marker(int m) {
     return fail("unknown marker");
 }
 
-bool Jpeg::frame_header() {
+// alloc = false: the checks only (mpt_jpeg_decode's header query), no sample planes
+bool Jpeg::frame_header(bool alloc) {
     const int Lf = get16();
     if (Lf < 11) return fail("bad SOF len");
     if (get8() != 8) return fail("only 8-bit JPEG");
@@ -489,6 +510,7 @@ bool Jpeg::frame_header() {
         if (h_max % comp[i].h || v_max % comp[i].v) return fail("non-integer sampling ratio");
     mcu_x = (img_x + h_max * 8 - 1) / (h_max * 8);
     mcu_y = (img_y + v_max * 8 - 1) / (v_max * 8);
+    if (!alloc) return true;
     for (int i = 0; i < c; i++) {
         Comp& k = comp[i];
         k.x = (img_x * k.h + h_max - 1) / h_max;
@@ -789,7 +811,7 @@ extern "C" int mpt_jpeg_decode(const uint8_t* data, int64_t size, int32_t req_co
                                int32_t* out_w, int32_t* out_h, int32_t* out_comp) {
     if (!data || size <= 0 || !out_w || !out_h) return mpt::api_fail(MPT_ERR_INVALID_ARGUMENT, "jpeg: NULL argument");
     if (req_comp < 0 || req_comp > 4) return mpt::api_fail(MPT_ERR_INVALID_ARGUMENT, "jpeg: req_comp must be 0..4");
-    Jpeg z;
+    Jpeg z{};   // stb memsets its decoder (stb_image.h:4031): undefined tables decode from zeros
     z.p = data;
     z.end = data + size;
     if (!out) {   // header only: the size of the decoded image
@@ -806,14 +828,12 @@ extern "C" int mpt_jpeg_decode(const uint8_t* data, int64_t size, int32_t req_co
             }
         }
         z.progressive = m == 0xc2;
-        // the frame header without allocating planes
-        const uint8_t* save = z.p;
-        z.p += 3;
-        *out_h = z.get16();
-        *out_w = z.get16();
-        const int c = z.get8();
-        z.p = save;
-        if (out_comp) *out_comp = c;
+        // the frame header's checks (Lf, precision, zero / oversized dimensions, components,
+        // sampling factors, the 2^31-byte limit) without allocating planes
+        if (!z.frame_header(false)) return mpt::api_fail(MPT_ERR_INVALID_ARGUMENT, ("jpeg: " + z.err).c_str());
+        *out_h = z.img_y;
+        *out_w = z.img_x;
+        if (out_comp) *out_comp = z.img_n;
         return MPT_OK;
     }
     if (!z.decode_image()) return mpt::api_fail(MPT_ERR_INVALID_ARGUMENT, ("jpeg: " + z.err).c_str());

@@ -80,7 +80,10 @@ constexpr int FRAME_RING = 256;   // >= 2 x MPT_MAX_BATCH
 // light-hit traversals, split, plain and generic shade, miss, compact, resolve) for up to 65
 // bounces (validate_frame), + camera, ReSTIR, accumulate
 // + the ReSTIR DI kernels (G-buffer, presampling, initial, temporal / spatiotemporal, 4 spatial)
-constexpr int RESTIR_MAX_BATCH = 32;                    // <= 50 timed scopes per batched ReSTIR DI sample
+// samples per batched ReSTIR DI wavefront (<= 50 timed scopes each): a partitioned context's
+// band is 1/N of the frame, so its later bounces need up to 128 samples to reach the
+// single-GPU wavefront size (MPT_RESTIR_MAX_BATCH lowers it, A/B)
+constexpr int RESTIR_MAX_BATCH = 128;
 // x2: the two halves of an overlapped batch
 constexpr int EV_POOL = 2 * 2 * ((10 * 65 + 3 + 8) > 50 * RESTIR_MAX_BATCH ? (10 * 65 + 3 + 8) : 50 * RESTIR_MAX_BATCH);
 #ifndef MPT_TRACE_BLOCKS_PER_CU
@@ -135,6 +138,8 @@ struct MptContext {
     int shade_classes = 1;
     int restir_staged = 1;                // ReSTIR DI reuse passes staged around their rays (MPT_RESTIR_STAGED)
     int restir_batch = 1;                 // ReSTIR DI samples batched after bounce 0 (MPT_RESTIR_BATCH)
+    int adaptive_batch = 1;               // adaptive samples batched, gated in k_accumulate (MPT_ADAPTIVE_BATCH)
+    int restir_max_batch = RESTIR_MAX_BATCH;   // MPT_RESTIR_MAX_BATCH
     int shade_glass = 1;                  // glass-class shading kernel (MPT_SHADE_GLASS)
     int shade_split = 0;                  // plain-class shading stages (MPT_SHADE_SPLIT, LaunchCfg::shade_split)
     int shade_texmetal = 1;               // MT_TEXMETAL materials through the plain list (MPT_SHADE_TEXMETAL)
@@ -854,6 +859,9 @@ int mpt_create(int device, void* hip_stream, MptContext** out) {
     if (const char* e = std::getenv("MPT_SHADE_CLASSES")) c->shade_classes = std::atoi(e);
     if (const char* e = std::getenv("MPT_RESTIR_STAGED")) c->restir_staged = std::atoi(e);
     if (const char* e = std::getenv("MPT_RESTIR_BATCH")) c->restir_batch = std::atoi(e);
+    if (const char* e = std::getenv("MPT_ADAPTIVE_BATCH")) c->adaptive_batch = std::atoi(e);
+    if (const char* e = std::getenv("MPT_RESTIR_MAX_BATCH"))
+        c->restir_max_batch = std::max(1, std::min(RESTIR_MAX_BATCH, std::atoi(e)));
     if (const char* e = std::getenv("MPT_SHADE_GLASS")) c->shade_glass = std::atoi(e);
     if (const char* e = std::getenv("MPT_SHADE_SPLIT")) c->shade_split = std::atoi(e);
     if (const char* e = std::getenv("MPT_SHADE_TEXMETAL")) c->shade_texmetal = std::atoi(e);
@@ -1262,11 +1270,16 @@ static int launch_batch(MptContext* c, const MptFrame* f, int batch) {
     c->batch = batch;
     DevPaths P = dev_paths(c);
     c->batch = 1;
+    {
+        const MptRenderSettings& rs = f->render_settings;
+        P.spec_as = batch > 1 && (rs.stop_pixel_noise_threshold > 0.0f || rs.enable_adaptive_sampling) && rs.accumulate;
+    }
     if (restir_part) {   // frame_begin maintains the band and the previous frame's halo rows
         P.rs_lo = std::max(0, cfg.own_y0 - cfg.halo_prev) * f->res_x;
         P.rs_hi = std::min(f->res_y, cfg.own_y1 + cfg.halo_prev) * f->res_x;
     }
-    const bool ovl = c->overlap && batch >= 2 && f->options.direct_light_sampling != MPT_LSS_RESTIR_DI && c->x_per == 0;
+    const bool ovl = c->overlap && batch >= 2 && f->options.direct_light_sampling != MPT_LSS_RESTIR_DI && c->x_per == 0 &&
+                     !P.spec_as;
     hipError_t e = hipSuccess;
     if (ovl) {
         int rr = ensure_overlap(c);
@@ -1367,7 +1380,11 @@ static bool batchable(const MptContext* c, const MptFrame& a, const MptFrame& b)
     if (restir && !c->restir_batch) return false;
     if (is_low_res(a)) return false;   // interactive frames: one sample each (RenderWindow.cpp:798-802)
     const MptRenderSettings& rs = a.render_settings;
-    if ((rs.stop_pixel_noise_threshold > 0.0f || rs.enable_adaptive_sampling) && rs.accumulate) return false;
+    // adaptive sampling / the stop-noise threshold: traced speculatively and gated in sample order
+    // by k_accumulate (not under ReSTIR DI, whose reuse passes read neighbours' converged counts)
+    if ((rs.stop_pixel_noise_threshold > 0.0f || rs.enable_adaptive_sampling) && rs.accumulate &&
+        (restir || !c->adaptive_batch))
+        return false;
     MptFrame t = b;
     t.render_settings.sample_number = a.render_settings.sample_number;
     t.render_settings.denoiser_AOV_accumulation_counter = a.render_settings.denoiser_AOV_accumulation_counter;
@@ -1392,7 +1409,7 @@ int mpt_render_frames(MptContext* c, const MptFrame* frames, int32_t count, int3
     if (max_batch <= 0) max_batch = default_batch(c, frames[0]);
     max_batch = std::min<int32_t>(max_batch, MPT_MAX_BATCH);
     // batched ReSTIR DI runs each sample's first bounce in turn (its timing events per sample)
-    if (frames[0].options.direct_light_sampling == MPT_LSS_RESTIR_DI) max_batch = std::min(max_batch, RESTIR_MAX_BATCH);
+    if (frames[0].options.direct_light_sampling == MPT_LSS_RESTIR_DI) max_batch = std::min(max_batch, c->restir_max_batch);
     // the launches' view of low-resolution frames (low_res_frame), copied only when there is one
     std::vector<MptFrame> eff;
     for (int k = 0; k < count && eff.empty(); k++)

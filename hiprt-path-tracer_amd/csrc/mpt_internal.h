@@ -164,6 +164,7 @@ struct DevPaths {
     float* as_sqlum;          // pixel_squared_luminance
     int32_t* as_conv;         // pixel_converged_sample_count (-1 = not converged)
     uint8_t* active;          // pixel_active
+    int32_t spec_as;          // a batch of adaptive samples: traced speculatively, gated in k_accumulate
     uint32_t* status;         // [0] stop_noise_threshold_converged_count, [1] still_one_ray_active
     // ReSTIR DI (LSS_RESTIR_DI only; NULL otherwise).  G-buffer of the camera hits as
     // CameraRays writes it (CameraRays.h:144-166, GBuffer.h:17-34), current + previous frame:

@@ -815,39 +815,46 @@ DEV bool low_res_region(const MptFrame& F, int x, int y) {
     const int s = rs.render_low_resolution_scaling;
     return x < (F.res_x + s - 1) / s && y < (F.res_y + s - 1) / s;
 }
-// get_pixel_confidence_interval (AdaptiveSampling.h:11-20)
-DEV float pixel_confidence(const DevPaths& P, int slot, int count, float& avg) {
-    const float* px = P.fb_color + 3 * (size_t)slot;
-    float l = lum(col(px[0], px[1], px[2]));
+// get_pixel_confidence_interval (AdaptiveSampling.h:11-20) of a pixel's sum c, squared
+// luminance sum sq and sample count
+DEV float pixel_confidence(Col c, float sq, int count, float& avg) {
+    float l = lum(c);
     avg = l / (float)(count + 1);
-    float var = (P.as_sqlum[slot] - l * avg) / (float)(count + 1);
+    float var = (sq - l * avg) / (float)(count + 1);
     return 1.96f * sqrtf(var) / sqrtf((float)(count + 1));
 }
-// adaptive_sampling (AdaptiveSampling.h:30-104): true if the pixel needs this sample
-DEV bool adaptive_sampling(const DevPaths& P, const MptRenderSettings& rs, int slot, bool& converged) {
+// adaptive_sampling (AdaptiveSampling.h:30-104) on a pixel's values: true if the pixel needs
+// this sample; updates the converged sample count `conv`
+DEV bool adaptive_gate(const MptRenderSettings& rs, Col c, float sq, int cnt, int& conv, bool& converged) {
     if (!has_adaptive_buffers(rs)) return true;
     if (rs.enable_adaptive_sampling) {
-        if (P.as_conv[slot] != -1) return false;
-        int cnt = P.as_count[slot];
+        if (conv != -1) return false;
         if (cnt > rs.adaptive_sampling_min_samples) {
             float avg;
-            float ci = pixel_confidence(P, slot, cnt, avg);
+            float ci = pixel_confidence(c, sq, cnt, avg);
             if (!(ci > rs.adaptive_sampling_noise_threshold * avg)) {
-                if (P.as_conv[slot] == -1) P.as_conv[slot] = cnt;
+                if (conv == -1) conv = cnt;
                 return false;
             }
         }
         return true;
     } else if (rs.stop_pixel_noise_threshold > 0.0f && rs.enable_pixel_stop_noise_threshold) {
-        int cnt = P.as_count[slot];
         float avg;
-        float ci = pixel_confidence(P, slot, cnt, avg);
+        float ci = pixel_confidence(c, sq, cnt, avg);
         converged = (ci <= rs.stop_pixel_noise_threshold * avg) && (rs.sample_number > 1);
-        int cur = P.as_conv[slot];
-        if (converged && cur == -1) P.as_conv[slot] = cnt;
-        else if (!converged) P.as_conv[slot] = -1;
+        if (converged && conv == -1) conv = cnt;
+        else if (!converged) conv = -1;
     }
     return true;
+}
+// the same on the pixel's buffers (CameraRays' gate, one sample per launch)
+DEV bool adaptive_sampling(const DevPaths& P, const MptRenderSettings& rs, int slot, bool& converged) {
+    if (!has_adaptive_buffers(rs)) return true;
+    const float* px = P.fb_color + 3 * (size_t)slot;
+    int conv = P.as_conv[slot];
+    const bool needed = adaptive_gate(rs, col(px[0], px[1], px[2]), P.as_sqlum[slot], P.as_count[slot], conv, converged);
+    P.as_conv[slot] = conv;
+    return needed;
 }
 
 #ifndef MPT_TU_PART   // k_camera
@@ -857,7 +864,9 @@ __global__ __launch_bounds__(TB) void k_camera(DevPaths P, const MptFrame* __res
     if (slot < P.n) batch_split(P, slot, pslot, sub);   // batched launches never use the adaptive buffers
     const MptFrame& F = Fp[sub];
     const MptRenderSettings& rs = F.render_settings;
-    const bool as = has_adaptive_buffers(rs);
+    // a batch of adaptive samples is traced speculatively: every slot gets its camera ray and
+    // k_accumulate replays the gate in sample order (P.spec_as)
+    const bool as = has_adaptive_buffers(rs) && !P.spec_as;
     const bool lr = low_res(rs);
     bool act = slot < P.n;
     int x = 0, y = 0;
@@ -874,7 +883,8 @@ __global__ __launch_bounds__(TB) void k_camera(DevPaths P, const MptFrame* __res
             P.as_conv[slot] = -1;
         }
         bool converged = false;
-        bool needed = adaptive_sampling(P, rs, slot, converged);
+        // (speculative batches: the gate runs in k_accumulate, on the pixel's values)
+        bool needed = as ? adaptive_sampling(P, rs, slot, converged) : true;
         if ((converged || !needed) && rs.do_update_status_buffers) atomicAdd(&P.status[0], 1u);
         if (as) {
             if (!needed) {
@@ -903,7 +913,7 @@ __global__ __launch_bounds__(TB) void k_camera(DevPaths P, const MptFrame* __res
         P.q0[slot] = slot;
     }
     if (!act) return;
-    if (rs.do_update_status_buffers) P.status[1] = 1u;
+    if (rs.do_update_status_buffers && !P.spec_as) P.status[1] = 1u;   // (speculative: k_accumulate)
     const uint32_t cseed = camera_seed(F, pix);
     // the path's seeds for the later stages (path_seed of the camera launch / of the path
     // tracing launch), computed once here instead of per traversal query
@@ -2460,9 +2470,16 @@ DEV void accumulate_sample(const DevPaths& P, const MptRenderSettings& rs, int s
 // framebuffer values (read once, written once per launch); the still-active flag is
 // written once per wave instead of once per path
 #ifndef MPT_TU_PART   // k_accumulate
+// Speculative batched adaptive sampling (P.spec_as): every sample of the batch was traced, and
+// here each sample meets CameraRays' reset and gate (CameraRays.h:78-125) on the pixel's
+// running values -- those of the samples before it -- exactly when the sequential frames
+// would: a sample the gate refuses rescales the sum and is dropped, a needed one is counted
+// and added.  The gate reads nothing a later sample changes, so the sums, counts and status
+// values equal one frame per sample.
 __global__ __launch_bounds__(TB) void k_accumulate(DevPaths P, const MptFrame* __restrict__ Fp) {
     const int pixel = blockIdx.x * TB + threadIdx.x;
     bool any = false;
+    uint32_t n_conv = 0u;
     if (pixel < P.n_pix) {
         float* fb = P.fb_color + 3 * (size_t)pixel;
         float* fa = P.fb_albedo + 3 * (size_t)pixel;
@@ -2474,13 +2491,40 @@ __global__ __launch_bounds__(TB) void k_accumulate(DevPaths P, const MptFrame* _
         bool adaptive = false;
         for (int sub = 0; sub < P.batch; sub++) adaptive |= has_adaptive_buffers(Fp[sub].render_settings);
         f.sq = adaptive ? P.as_sqlum[pixel] : 0.0f;
-        for (int sub = 0; sub < P.batch; sub++) accumulate_sample(P, Fp[sub].render_settings, batch_slot(P, pixel, sub), f, any);
+        if (P.spec_as) {
+            int cnt = P.as_count[pixel], conv = P.as_conv[pixel];
+            for (int sub = 0; sub < P.batch; sub++) {
+                const MptRenderSettings& rs = Fp[sub].render_settings;
+                if (has_adaptive_buffers(rs)) {
+                    if (rs.sample_number == 0 || rs.need_to_reset) { cnt = 0; f.sq = 0.0f; conv = -1; }
+                    bool converged = false;
+                    const bool needed = adaptive_gate(rs, f.c, f.sq, cnt, conv, converged);
+                    if ((converged || !needed) && rs.do_update_status_buffers) n_conv++;
+                    if (!needed) {
+                        f.c = f.c / (float)rs.sample_number * (float)(rs.sample_number + 1);
+                        continue;
+                    }
+                    cnt++;
+                }
+                if (rs.do_update_status_buffers) any = true;   // CameraRays.h:171-177
+                accumulate_sample(P, rs, batch_slot(P, pixel, sub), f, any);
+            }
+            P.as_count[pixel] = cnt;
+            P.as_conv[pixel] = conv;
+        } else {
+            for (int sub = 0; sub < P.batch; sub++) accumulate_sample(P, Fp[sub].render_settings, batch_slot(P, pixel, sub), f, any);
+        }
         fb[0] = f.c.r; fb[1] = f.c.g; fb[2] = f.c.b;
         fa[0] = f.a.x; fa[1] = f.a.y; fa[2] = f.a.z;
         fn[0] = f.n.x; fn[1] = f.n.y; fn[2] = f.n.z;
         if (adaptive) P.as_sqlum[pixel] = f.sq;
     }
     if (__ballot(any) != 0ull && lane_id() == 0) P.status[1] = 1u;
+    if (P.spec_as) {
+        // the converged-pixel counter: one atomic per wave
+        for (int off = 32; off > 0; off >>= 1) n_conv += __shfl_xor(n_conv, off);
+        if (lane_id() == 0 && n_conv) atomicAdd(&P.status[0], n_conv);
+    }
 }
 
 #endif
@@ -2952,8 +2996,9 @@ hipError_t launch_frame(const DevScene& S, const DevPaths& P0, const MptFrame* d
         return hipGetLastError();
     }
     const MptRenderSettings& hrs = hf.render_settings;
-    // the camera queue is compacted by k_camera under adaptive sampling and at low resolution
-    const bool as = ((hrs.stop_pixel_noise_threshold > 0.0f || hrs.enable_adaptive_sampling) && hrs.accumulate) ||
+    // the camera queue is compacted by k_camera under adaptive sampling (unless speculative) and at
+    // low resolution
+    const bool as = ((hrs.stop_pixel_noise_threshold > 0.0f || hrs.enable_adaptive_sampling) && hrs.accumulate && !P.spec_as) ||
                     (hrs.wants_render_low_resolution && hrs.allow_render_low_resolution && hrs.accumulate);
     if (hf.options.direct_light_sampling == MPT_LSS_RESTIR_DI) {
         hipLaunchKernelGGL(k_restir_frame_begin, dim3(blocks_for(P.rs_hi - P.rs_lo)), dim3(TB), 0, st, P, d_frame);

@@ -101,3 +101,46 @@ def test_gpu_adaptive_sampling_bit_exact(cornell, luts, mode):
     assert 0 < s["pixel_converged_count"]
     o.close()
     r.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("max_batch", [3, 12])
+@pytest.mark.parametrize("mode", ["adaptive", "adaptive_min5", "stop_noise", "adaptive_band", "adaptive_reset"])
+def test_gpu_adaptive_batched_speculative_bit_exact(cornell, luts, mode, max_batch):
+    """Adaptive sampling at the reference defaults through batched wavefronts
+    (mpt_render_frames): every sample traced, k_accumulate replays CameraRays' reset and gate in
+    sample order -- sums, per-pixel counts, converged counts, squared luminance and the status
+    values equal the oracle's sequential frames, with the min-samples threshold crossed inside a
+    batch, status updates at the end of every 4-sample render() call and a reset mid-run."""
+    import mpt
+    from oracle import oracle as orc
+    band = (4, 1, 3) if mode == "adaptive_band" else (1, 0, 1)
+    st = stop_noise_settings() if mode == "stop_noise" else adaptive_settings(min_samples=5 if mode == "adaptive_min5" else 3)
+    frs = frames(cornell, st, band=band, last_status=False)
+    for k, f in enumerate(frs):
+        f.render_settings.do_update_status_buffers = k % 4 == 3
+    if mode == "adaptive_reset":
+        frs[6].render_settings.need_to_reset = True
+    r = mpt.GPURenderer(0)
+    r.set_scene(cornell)
+    r.set_luts(luts)
+    r.enable_stats(timing=True)
+    r.clear_status_buffers()
+    r.render_samples(frs, max_batch=max_batch)
+    r.synchronize_kernel()
+    launches = r.stats().shade_launches
+    o = orc.Oracle(cornell, luts)
+    c = o.render(frs)
+    g = r.framebuffer(abi.FB_COLOR)
+    assert np.array_equal(g, c), f"{(g != c).sum()} values differ"
+    assert np.array_equal(r.aux_buffer(abi.AUX_SAMPLE_COUNT), o.last_aux["sample_count"])
+    assert np.array_equal(r.aux_buffer(abi.AUX_CONVERGED_SAMPLE_COUNT), o.last_aux["converged_sample_count"])
+    assert np.array_equal(r.aux_buffer(abi.AUX_SQUARED_LUMINANCE), o.last_aux["squared_luminance"])
+    s = r.get_status_buffer_values()
+    assert s == {"one_ray_active": o.last_aux["one_ray_active"], "pixel_converged_count": o.last_aux["pixel_converged_count"]}
+    if mode != "stop_noise":
+        assert (o.last_aux["converged_sample_count"] >= 0).any()
+    # batched: one shading launch per bounce per wavefront, not per sample
+    assert 0 < launches <= (N // max_batch + (1 if mode == "adaptive_reset" else 0)) * 4 * 2, launches
+    o.close()
+    r.close()

@@ -397,3 +397,34 @@ def test_traversal_bvh_variants_bit_exact(scenes, luts, monkeypatch, mode):
         assert_same(gt[op >= 0], ot[op >= 0], f"{mode}: t")
     finally:
         r.close()
+
+
+@pytest.mark.parametrize("display", [False, True], ids=["dropped", "display_nans"])
+def test_display_nans_bit_exact(cornell, luts, display):
+    """A sample that fails the sanity check (negative colour: a wall given negative emission) is
+    dropped, or with display_NaNs painted (1e30, 0, 1e30) x sample_number into the sum
+    (FullPathTracer.h:29-35, 80-95) -- GPU equals the oracle, both ways."""
+    import copy
+    from oracle import oracle as orc
+    sd = copy.copy(cornell)
+    mats = [abi.Material.from_buffer_copy(m) for m in cornell.materials]
+    wall = int(cornell.material_indices[0])
+    mats[wall].emission = abi.Color(-3.0, -3.0, -3.0)
+    mats[wall].emission_strength = 1.0
+    sd.materials = mats
+    frs = frames(sd, 40, 30, 3)
+    for f in frs:
+        f.render_settings.display_NaNs = display
+    r = mpt.GPURenderer(0)
+    r.set_scene(sd)
+    r.set_luts(luts)
+    r.render_samples(frs)
+    r.synchronize_kernel()
+    got = r.framebuffer(abi.FB_COLOR)
+    r.close()
+    o = orc.Oracle(sd, luts)
+    ref = o.render(frs)
+    o.close()
+    assert np.array_equal(got, ref), f"{(got != ref).sum()} values differ"
+    painted = got[..., 0] >= 1.0e30
+    assert painted.any() == display

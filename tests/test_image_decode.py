@@ -93,3 +93,43 @@ def test_unsupported_and_corrupt_inputs_raise():
         image.decode_jpeg(jpg[:2] + b"\xff\xc4\x00\x03\x20")   # a DHT naming table class 2
     with pytest.raises(mpt.MptError, match="hdr"):
         image.decode_hdr(b"#?RADIANCE\nFORMAT=32-bit_rle_xyze\n\n-Y 1 +X 1\n\x00\x00\x00\x00")
+
+
+def _patch_sof(jpg, h, w):
+    """The JPEG with its SOF0 frame size replaced (marker FFC0: Lf, P, Y, X)."""
+    i = jpg.index(b"\xff\xc0")
+    return jpg[:i + 5] + h.to_bytes(2, "big") + w.to_bytes(2, "big") + jpg[i + 9:]
+
+
+def test_jpeg_header_query_validates_before_allocating():
+    """mpt_jpeg_decode's header-only call (out == NULL, what decode_jpeg sizes its array by) runs the
+    frame header's checks: an oversized (65535 x 65535 x 3 > 2^31 bytes) or zero frame is an error
+    there, not an allocation; a file cut inside the SOF reads zeros and fails the same way."""
+    import mpt
+    from mpt import image
+    jpg = open(os.path.join(IMG, "pil_q75_444.jpg"), "rb").read()
+    with pytest.raises(mpt.MptError, match="too large"):
+        image.decode_jpeg(_patch_sof(jpg, 65535, 65535))
+    with pytest.raises(mpt.MptError, match="height"):
+        image.decode_jpeg(_patch_sof(jpg, 0, 64))
+    with pytest.raises(mpt.MptError, match="jpeg"):
+        image.decode_jpeg(jpg[:jpg.index(b"\xff\xc0") + 6])
+
+
+def test_jpeg_undefined_tables_are_deterministic():
+    """A scan that names Huffman tables no DHT defined decodes from zeroed tables (stb memsets its
+    decoder, stb_image.h:4031): the outcome -- here an error -- is the same on every call."""
+    import mpt
+    from mpt import image
+    jpg = bytearray(open(os.path.join(IMG, "pil_q75_444.jpg"), "rb").read())
+    i = jpg.index(b"\xff\xda")
+    n = jpg[i + 4]
+    for c in range(n):
+        jpg[i + 6 + 2 * c] = 0x33          # Td = Ta = 3: never defined in this file
+    outcomes = []
+    for _ in range(3):
+        try:
+            outcomes.append(image.decode_jpeg(bytes(jpg)).tobytes())
+        except mpt.MptError as e:
+            outcomes.append(str(e))
+    assert outcomes[0] == outcomes[1] == outcomes[2]

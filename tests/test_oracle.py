@@ -208,8 +208,9 @@ def test_oracle_golden_image(cornell, luts, oracle_lib):
 def test_oracle_rejects_unsupported_options(cornell, luts, oracle_lib):
     o = oracle_lib.Oracle(cornell, luts)
     fr = _frames(cornell, 8, 8, 1)
-    fr[0].render_settings.wants_render_low_resolution = True
+    fr[0].render_settings.wants_render_low_resolution = True     # low resolution with no valid scaling
     fr[0].render_settings.allow_render_low_resolution = True
+    fr[0].render_settings.render_low_resolution_scaling = 0
     with pytest.raises(RuntimeError):
         o.render(fr)
     o.close()

@@ -12,6 +12,6 @@ bash tools/profile_round.sh ${tag}_$w --workload $w $pargs || exit $?
 python tools/pmc_traffic.py gpurun_out/prof_${tag}_$w $o/${tag}_${w}_pmc_traffic.json > $o/${tag}_${w}_pmc.txt || exit 1
 cp $o/${tag}_${w}_pmc_traffic.json profiles/
 python tools/prof_summary.py gpurun_out/prof_${tag}_$w/trace > $o/${tag}_${w}_kernel_stats.txt 2>/dev/null || true
-timeout -k 10 600 python bench.py --workload $w $bargs > $o/${tag}_${w}_bench.json 2> $o/${tag}_${w}_bench.err || { tail -n 20 $o/${tag}_${w}_bench.err; exit 1; }
+timeout -k 10 600 python bench.py --workload $w --configs none $bargs > $o/${tag}_${w}_bench.json 2> $o/${tag}_${w}_bench.err || { tail -n 20 $o/${tag}_${w}_bench.err; exit 1; }
 tail -c 400 $o/${tag}_${w}_bench.json
 echo
