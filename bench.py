@@ -250,10 +250,11 @@ def emulate_restir_ranks(a, r, cam, W, H, opt, wset, alpha, n_ranks, K, device):
     the frame-sized G-buffer / reservoir buffers hold a single-context render around every
     band), then the band's own warmup + K timed samples, batched as the rank would batch them.
     The halo callback stands in for the exchange: at each exchange point it copies the halo
-    rows the rank would receive (same bytes, device to device on the library's stream) and
-    synchronises the host once per sample at the G-buffer phase as the RCCL exchange's
-    all-reduce does; the rows keep the whole-frame render's content, so the images are not
-    the partitioned render's (tests/test_configs.py pins that bit-exact), only its timing."""
+    rows the rank would receive (same bytes, device to device on the library's stream) and,
+    when the library could not derive the halo from the frame alone (a moving camera), waits
+    for the G-buffer as the RCCL exchange's agreement does; the rows keep the whole-frame
+    render's content, so the images are not the partitioned render's (tests/test_configs.py
+    pins that bit-exact), only its timing."""
     import torch
     from mpt import partition
     bh = partition.contiguous_band(H, n_ranks, 0)[0]
@@ -261,8 +262,8 @@ def emulate_restir_ranks(a, r, cam, W, H, opt, wset, alpha, n_ranks, K, device):
 
     def halo(x):
         st = torch.cuda.ExternalStream(x.stream, device=torch.device("cuda", device))
-        if x.phase == partition.HALO_GBUFFER:
-            st.synchronize()
+        if x.phase == partition.HALO_GBUFFER and not x.halo_agreed:
+            st.synchronize()      # the agreement's all-reduce (TorchHaloExchange.agree) waits for the G-buffer
         _, recvs = partition.halo_plan(x.res_y, bh, n_ranks, cur[0], x.halo_rows)
         with torch.cuda.stream(st):
             for v in partition._row_views(x, torch, torch.device("cuda", device)):

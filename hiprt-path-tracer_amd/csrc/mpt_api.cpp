@@ -133,6 +133,8 @@ struct MptContext {
     DBuf<int32_t> mat_tex;
     DBuf<float4> em_tab;
     bool any_tex = false;
+    double tex_tri_frac = 0.0;            // triangles with a textured material / all (resolve_materials)
+    int mat_private = -1;                 // MPT_MAT_PRIVATE: 1 / 0 force k_shade's MATP, -1 by tex_tri_frac
     // material-class shading (k_split / k_shade): 1 on (default), 0 off, 2 on with every
     // plain vertex deferred to the generic kernel (test hook); MPT_SHADE_CLASSES at mpt_create
     int shade_classes = 1;
@@ -668,6 +670,11 @@ int resolve_materials(MptContext* c) {
     HIPCHK(hipStreamSynchronize(c->stream));
     c->any_tex = false;
     for (int32_t v : t) c->any_tex |= (v & MT_TEXTURED) != 0;
+    // the share of triangles with a textured material: above 1/4 the shading kernels hold a
+    // textured vertex's resolved material in private memory (k_shade's MATP)
+    size_t n_tex_tris = 0;
+    for (int32_t mi : c->h_mat_idx) n_tex_tris += (mi >= 0 && (size_t)mi < n && (t[mi] & MT_TEXTURED)) ? 1 : 0;
+    c->tex_tri_frac = c->h_mat_idx.empty() ? 0.0 : (double)n_tex_tris / (double)c->h_mat_idx.size();
     // each triangle's material class in its BVH record (TriRec::pad1): the path traversal
     // reports it with the hit (DevPaths::hit_cls), so k_split needs no material lookups
     bool changed = false;
@@ -860,6 +867,7 @@ int mpt_create(int device, void* hip_stream, MptContext** out) {
     if (const char* e = std::getenv("MPT_RESTIR_STAGED")) c->restir_staged = std::atoi(e);
     if (const char* e = std::getenv("MPT_RESTIR_BATCH")) c->restir_batch = std::atoi(e);
     if (const char* e = std::getenv("MPT_ADAPTIVE_BATCH")) c->adaptive_batch = std::atoi(e);
+    if (const char* e = std::getenv("MPT_MAT_PRIVATE")) c->mat_private = std::atoi(e);
     if (const char* e = std::getenv("MPT_RESTIR_MAX_BATCH"))
         c->restir_max_batch = std::max(1, std::min(RESTIR_MAX_BATCH, std::atoi(e)));
     if (const char* e = std::getenv("MPT_SHADE_GLASS")) c->shade_glass = std::atoi(e);
@@ -1254,6 +1262,7 @@ static int launch_batch(MptContext* c, const MptFrame* f, int batch) {
     cfg.restir_staged = c->restir_staged;
     cfg.shade_glass = c->shade_glass;
     cfg.shade_split = c->shade_split;
+    cfg.mat_private = c->mat_private >= 0 ? (c->mat_private != 0) : (c->tex_tri_frac >= 0.25);
     cfg.light_bvh = c->light_bvh && c->light_bvh_ok;
     cfg.light_static = !c->h_light_prims.empty() && 2 * c->bvh_light.depth + 2 <= TRAV_LDS_STACK;
     if (restir_part) {

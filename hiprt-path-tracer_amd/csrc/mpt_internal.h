@@ -248,19 +248,25 @@ constexpr int STATS_STRIDE = 6;   // per mode: traversals, nodes, tris, (unused)
 constexpr int N_STATS = N_TRACE_MODES * STATS_STRIDE;
 
 enum {
-    CTR_Q0 = 0, CTR_Q1 = 1, CTR_ANY = 2, CTR_CL = 3, CTR_FETCH = 4,
-    CTR_REPROJ = 5,           // max |reprojected row - row| of the frame's G-buffer (partitioned ReSTIR DI)
-    CTR_HIT = 6, CTR_MISS = 7,  // lengths of the hit / miss queues of the bounce (k_split)
-    CTR_FULL = 8,             // length of the generic-material hit queue (k_split + k_shade deferrals)
-    CTR_DEFER = 9,            // plain-class hits deferred to the generic queue (tombstones in qh)
-    CTR_LIGHT = 10,           // length of nq_light (k_trace TM_NEE_LIGHT)
-    CTR_XANY = 11, CTR_XCL = 12, CTR_XLIGHT = 13,   // ext query lists (extended light sampling)
-    CTR_RQ = 14, CTR_RQV = 15,                      // staged ReSTIR DI rays / visibility-reuse rays
-    CTR_RQE0 = 16, CTR_RQE1 = 17,                   // staged ReSTIR DI target evaluations: plain / generic class
-    CTR_QG = 18,                                    // batched ReSTIR DI: the later bounces' path queue
+    CTR_Q0 = 0, CTR_Q1 = 1,                         // path queues (ping-pong)
+    CTR_QG = 2,                                     // batched ReSTIR DI: the later bounces' path queue
+    // from CTR_ANY on: zeroed by ONE memset at the top of every bounce (frame_bounces)
+    CTR_ANY = 3, CTR_CL = 4,                        // NEE query lists: any hit, closest
+    CTR_FETCH = 5,                                  // work counter of the list traversals outside the bounce loop
+    CTR_REPROJ = 6,           // max |reprojected row - row| of the frame's G-buffer (partitioned ReSTIR DI)
+    CTR_HIT = 7, CTR_MISS = 8,  // lengths of the hit / miss queues of the bounce (k_split)
+    CTR_FULL = 9,             // length of the generic-material hit queue (k_split + k_shade deferrals)
+    CTR_DEFER = 10,           // plain-class hits deferred to the generic queue (tombstones in qh)
+    CTR_LIGHT = 11,           // length of nq_light (k_trace TM_NEE_LIGHT)
+    CTR_XANY = 12, CTR_XCL = 13, CTR_XLIGHT = 14,   // ext query lists (extended light sampling)
+    CTR_RQ = 15, CTR_RQV = 16,                      // staged ReSTIR DI rays / visibility-reuse rays
+    CTR_RQE0 = 17, CTR_RQE1 = 18,                   // staged ReSTIR DI target evaluations: plain / generic class
     CTR_GLASS = 19,                                 // length of the glass-class list (top of qf, k_split)
-    CTR_COUNT = 20
+    // the persistent traversals' work counters of a bounce, one per launch (no reset between them)
+    CTR_F_PATH = 20, CTR_F_ANY = 21, CTR_F_CL = 22, CTR_F_OCC = 23, CTR_F_XANY = 24, CTR_F_XCL = 25, CTR_F_XOCC = 26,
+    CTR_COUNT = 27
 };
+constexpr int CTR_BOUNCE_FIRST = CTR_ANY;           // [CTR_BOUNCE_FIRST, CTR_COUNT): reset per bounce
 
 // launch glue (mpt_kernels.hip)
 struct LaunchCfg {
@@ -285,6 +291,7 @@ struct LaunchCfg {
     int light_static;         // the light BVH's traversal stack fits in LDS (one query per lane, no spill)
     int restir_staged;        // ReSTIR DI reuse passes staged around their rays (restir_di.h), when supported
     int shade_glass;          // k_split's glass class (MPT_SHADE_GLASS)
+    int mat_private;          // k_shade<..., MATP>: textured vertices' resolved material in private memory
     int shade_split;          // plain class in stages (MPT_SHADE_SPLIT): 0 one kernel, 1 light / env / cont,
                               // 2 light / env + cont, 3 light + env / cont
     // overlapped batch halves (mpt_api.cpp launch_batch): recorded after the bounce-0 path

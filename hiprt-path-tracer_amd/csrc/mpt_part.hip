@@ -11,11 +11,13 @@ namespace mpt {
 
 #if MPT_TU_PART == 1
 void part_shade_generic(dim3 g, hipStream_t st, const ShadeArgs& a) {
-    hipLaunchKernelGGL((k_shade<MPT_BSDF_NONE, false>), g, dim3(TB), 0, st, a);
+    if (a.mat_private) hipLaunchKernelGGL((k_shade<MPT_BSDF_NONE, false, false, false, SG_ALL, true>), g, dim3(TB), 0, st, a);
+    else hipLaunchKernelGGL((k_shade<MPT_BSDF_NONE, false>), g, dim3(TB), 0, st, a);
 }
 #elif MPT_TU_PART == 2
 void part_shade_plain(dim3 g, hipStream_t st, const ShadeArgs& a) {
-    hipLaunchKernelGGL((k_shade<MPT_BSDF_NONE, true>), g, dim3(TB), 0, st, a);
+    if (a.mat_private) hipLaunchKernelGGL((k_shade<MPT_BSDF_NONE, true, false, false, SG_ALL, true>), g, dim3(TB), 0, st, a);
+    else hipLaunchKernelGGL((k_shade<MPT_BSDF_NONE, true>), g, dim3(TB), 0, st, a);
 }
 #ifdef MPT_SECTION_TIMING
 extern "C" int mpt_debug_sections(unsigned long long* out, int reset) {   // k_shade<NONE, true>'s section clocks

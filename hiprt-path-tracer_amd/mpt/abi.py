@@ -399,7 +399,7 @@ class HaloExchange(C.Structure):
     _fields_ = [("phase", C.c_int32), ("pass_index", C.c_int32), ("res_x", C.c_int32), ("res_y", C.c_int32),
                 ("own_y0", C.c_int32), ("own_y1", C.c_int32), ("halo_rows", C.c_int32), ("n_buffers", C.c_int32),
                 ("buffers", C.c_void_p * HALO_MAX_BUFFERS), ("bytes_per_pixel", C.c_int64 * HALO_MAX_BUFFERS),
-                ("stream", C.c_void_p)]
+                ("stream", C.c_void_p), ("halo_agreed", C.c_int32)]
 
 
 HaloExchangeFn = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(HaloExchange))

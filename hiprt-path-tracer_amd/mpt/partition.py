@@ -158,7 +158,7 @@ class TorchHaloExchange:
 
     def __call__(self, x):
         torch = self.torch
-        if x.phase == HALO_GBUFFER:
+        if x.phase == HALO_GBUFFER and not x.halo_agreed:   # (agreed: a still camera, same halo everywhere)
             x.halo_rows = self.agree(x.halo_rows)
         stream = torch.cuda.ExternalStream(x.stream, device=self.device) if x.stream else torch.cuda.current_stream(self.device)
         self.exchange_views(_row_views(x, torch, self.device), x.res_y, x.halo_rows, stream)

@@ -490,7 +490,11 @@ typedef struct MptContext MptContext;
  *                         plus the reuse radius and temporal search extent -- the
  *                         reference's reprojection is not confined to a pixel's
  *                         neighbourhood).  The callback agrees on the maximum over all
- *                         contexts, exchanges with it and stores it back in halo_rows.
+ *                         contexts, exchanges with it and stores it back in halo_rows --
+ *                         unless halo_agreed is set: the frame's camera did not move, so every
+ *                         context derived the same halo from the frame alone (a pixel
+ *                         reprojects onto itself) without waiting for its G-buffer, and the
+ *                         callback may skip the agreement (and any host synchronisation).
  *  MPT_HALO_PREV_GBUFFER  only when the agreed halo grew since the previous frame: the
  *                         previous frame's G-buffer rows the context did not maintain.
  *  MPT_HALO_RESERVOIRS    the temporal input before the fused pass (pass 0), then the
@@ -509,6 +513,7 @@ typedef struct MptHaloExchange {
     void* buffers[MPT_HALO_MAX_BUFFERS];
     int64_t bytes_per_pixel[MPT_HALO_MAX_BUFFERS];
     void* stream;         /* hipStream_t */
+    int32_t halo_agreed;  /* MPT_HALO_GBUFFER: halo_rows is already the same in every context */
 } MptHaloExchange;
 typedef int (*MptHaloExchangeFn)(void* user, MptHaloExchange* x);
 

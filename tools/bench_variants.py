@@ -21,7 +21,8 @@ def main():
         lib, _, sets = spec.partition("@")
         env = dict(os.environ, MPT_LIB_PATH=os.path.abspath(lib))
         env.update(kv.split("=", 1) for kv in sets.split(",") if kv)
-        cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "16", "--warmup", "2", "--no-cpu-baseline", *extra]
+        cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "16", "--warmup", "2", "--no-cpu-baseline",
+               "--no-parity", "--configs", "none", "--batch1-steps", "0", *extra]
         r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
         if r.returncode != 0:
             print(spec, "FAILED", r.returncode, r.stderr[-2000:], flush=True)
