@@ -88,6 +88,8 @@ def parse():
     ap.add_argument("--config-steps", type=int, default=8, help="timed steps of each extra config")
     ap.add_argument("--batch1-steps", type=int, default=8,
                     help="C3: steps also timed with one sample per wavefront (mpt_render_frame's launch set; 0 = skip)")
+    ap.add_argument("--emulate-band", type=int, default=-1,
+                    help="C4 rehearsal: time only this rank's band (default: every band in turn)")
     ap.add_argument("--emulate-rank-of", type=int, default=1,
                     help="scaling rehearsal on one GPU: render only rank 0's share of an N-way row split "
                          "(the line then reports that rank's rate; not a bench line)")
@@ -277,6 +279,8 @@ def emulate_restir_ranks(a, r, cam, W, H, opt, wset, alpha, n_ranks, K, device):
     r.set_halo_exchange(halo)
     bands = []
     for k in range(n_ranks):
+        if a.emulate_band >= 0 and k != a.emulate_band:
+            continue
         cur[0] = k
         band = (bh, k, n_ranks)
         rows = mpt.partition_rows(H, *band)

@@ -1,0 +1,41 @@
+"""GPU idle time between kernels in a rocprofv3 --kernel-trace run (development tool).
+
+Reads the run's kernel_trace.csv, takes the dispatches of the last `window_ms` of the trace
+(the bench's timed region sits at its end), and prints the busy fraction of the GPU over that
+window (union of kernel intervals), the number of dispatches, their mean duration and the
+mean gap between consecutive dispatches -- the cost of a launch chain of small kernels.
+usage: python tools/trace_gaps.py <rocprofv3 output dir> [window_ms]
+"""
+import csv
+import glob
+import os
+import sys
+
+
+def main():
+    d = sys.argv[1]
+    window = float(sys.argv[2]) if len(sys.argv) > 2 else 50.0
+    f = sorted(glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True))[0]
+    rows = list(csv.DictReader(open(f)))
+    iv = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in rows)
+    t_end = max(e for _, e, _ in iv)
+    t0 = t_end - window * 1e6
+    iv = [x for x in iv if x[0] >= t0]
+    busy, cur_s, cur_e = 0, None, None
+    for s, e, _ in iv:
+        if cur_e is None or s > cur_e:
+            if cur_e is not None:
+                busy += cur_e - cur_s
+            cur_s, cur_e = s, e
+        else:
+            cur_e = max(cur_e, e)
+    busy += cur_e - cur_s
+    span = iv[-1][1] - iv[0][0]
+    gaps = [max(0, iv[i + 1][0] - iv[i][1]) for i in range(len(iv) - 1)]
+    print(f"window {span / 1e6:.3f} ms, {len(iv)} dispatches, busy {busy / span:.3f}, "
+          f"mean kernel {sum(e - s for s, e, _ in iv) / len(iv) / 1e3:.1f} us, mean gap {sum(gaps) / max(1, len(gaps)) / 1e3:.1f} us, "
+          f"gaps > 20 us: {sum(1 for g in gaps if g > 20000)}")
+
+
+if __name__ == "__main__":
+    main()
