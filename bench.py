@@ -88,6 +88,9 @@ def parse():
     ap.add_argument("--config-steps", type=int, default=8, help="timed steps of each extra config")
     ap.add_argument("--batch1-steps", type=int, default=8,
                     help="C3: steps also timed with one sample per wavefront (mpt_render_frame's launch set; 0 = skip)")
+    ap.add_argument("--halo", default="native", choices=["native", "python"],
+                    help="C4 across ranks: the library's RCCL halo exchange (mpt_set_halo_native; the one-GPU "
+                         "rehearsal: its local stand-in) or the Python callback (mpt.partition.TorchHaloExchange)")
     ap.add_argument("--emulate-band", type=int, default=-1,
                     help="C4 rehearsal: time only this rank's band (default: every band in turn)")
     ap.add_argument("--emulate-rank-of", type=int, default=1,
@@ -251,8 +254,8 @@ def emulate_restir_ranks(a, r, cam, W, H, opt, wset, alpha, n_ranks, K, device):
     rank's.  Every band k is timed in turn in this context: two whole-frame samples first (so
     the frame-sized G-buffer / reservoir buffers hold a single-context render around every
     band), then the band's own warmup + K timed samples, batched as the rank would batch them.
-    The halo callback stands in for the exchange: at each exchange point it copies the halo
-    rows the rank would receive (same bytes, device to device on the library's stream) and,
+    The halo callback stands in for the exchange: at each exchange point it moves the bytes of
+    the halo rows the rank would receive (one device-to-device copy on the library's stream) and,
     when the library could not derive the halo from the frame alone (a moving camera), waits
     for the G-buffer as the RCCL exchange's agreement does; the rows keep the whole-frame
     render's content, so the images are not the partitioned render's (tests/test_configs.py
@@ -267,16 +270,23 @@ def emulate_restir_ranks(a, r, cam, W, H, opt, wset, alpha, n_ranks, K, device):
         if x.phase == partition.HALO_GBUFFER and not x.halo_agreed:
             st.synchronize()      # the agreement's all-reduce (TorchHaloExchange.agree) waits for the G-buffer
         _, recvs = partition.halo_plan(x.res_y, bh, n_ranks, cur[0], x.halo_rows)
-        with torch.cuda.stream(st):
-            for v in partition._row_views(x, torch, torch.device("cuda", device)):
-                for (_, y0, y1) in recvs:
-                    scratch = torch.empty_like(v[y0:y1])
-                    scratch.copy_(v[y0:y1])
-                    stats["bytes"] += scratch.numel()
+        # the bytes this rank would receive, moved by ONE device copy (an RCCL exchange is one
+        # grouped send / receive kernel per exchange point, not a copy per buffer and range)
+        nbytes = sum(x.res_x * x.bytes_per_pixel[i] * (y1 - y0) for i in range(x.n_buffers) for (_, y0, y1) in recvs)
+        if nbytes:
+            if scratch[0] is None or scratch[0].numel() < 2 * nbytes:
+                scratch[0] = torch.empty(2 * nbytes, dtype=torch.uint8, device=torch.device("cuda", device))
+            with torch.cuda.stream(st):
+                scratch[0][nbytes:2 * nbytes].copy_(scratch[0][:nbytes])
+        stats["bytes"] += nbytes
         stats["calls"] += 1
 
     cur = [0]
-    r.set_halo_exchange(halo)
+    scratch = [None]
+    if a.halo == "native":
+        r.set_halo_native(2)      # the library's exchange, rehearsal mode: the received bytes moved locally
+    else:
+        r.set_halo_exchange(halo)
     bands = []
     for k in range(n_ranks):
         if a.emulate_band >= 0 and k != a.emulate_band:
@@ -305,12 +315,15 @@ def emulate_restir_ranks(a, r, cam, W, H, opt, wset, alpha, n_ranks, K, device):
                       "batch": batch, "mray_s": round((st.rays_closest + st.rays_any) / dt / 1e6, 2),
                       "restir_ms_per_spp": round(st.restir_ms / K, 4), "shade_ms_per_spp": round(st.shade_ms / K, 4),
                       "trace_path_ms_per_spp": round(st.stage_ms[0] / K, 4),
-                      "halo_calls_per_spp": round((stats["calls"] - c0) / K, 2),
-                      "halo_mb_per_spp": round((stats["bytes"] - b0) / K / 1e6, 3)})
+                      "halo_calls_per_spp": round((stats["calls"] - c0) / K, 2) if a.halo == "python" else None,
+                      "halo_mb_per_spp": round((stats["bytes"] - b0) / K / 1e6, 3) if a.halo == "python" else None})
         print(json.dumps(bands[-1]), file=sys.stderr, flush=True)
     worst = max(bands, key=lambda b: b["ms_per_spp"])
     return {"rehearsal": f"C4 ReSTIR DI tile-parallel over {n_ranks} ranks on one GPU: every rank's contiguous band "
                          "timed in turn (halo rows from a single-context render, exchange bytes copied locally)",
+            "halo": ("libmpt's native exchange in rehearsal mode (mpt_set_halo_native(2): one device copy of the "
+                     "received bytes per exchange point, no host callback)" if a.halo == "native" else
+                     "Python callback (one device copy of the received bytes per exchange point)"),
             "emulated_rank_of": n_ranks, "steps": K, "warmup": a.warmup, "width": W, "height": H,
             "ms_per_spp_slowest_rank": worst["ms_per_spp"], "slowest_band": worst["band"],
             "ms_per_spp_mean_rank": round(sum(b["ms_per_spp"] for b in bands) / len(bands), 4),
@@ -473,8 +486,16 @@ def run_workload(a, world, rank, local, dist, coll_dev, quiet=False):
         return out
     halo = None
     if a.workload == "c4" and world > 1:
-        halo = partition.TorchHaloExchange(dist, band_h)
-        r.set_halo_exchange(halo)
+        if a.halo == "native":
+            # the library's RCCL communicator: rank k renders band k, the halo rows go peer to
+            # peer in one ncclSend / ncclRecv group per exchange point on the library's stream
+            uid = [mpt.comm_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(uid, src=0)
+            r.comm_init(world, rank, uid[0])
+            r.set_halo_native(1)
+        else:
+            halo = partition.TorchHaloExchange(dist, band_h)
+            r.set_halo_exchange(halo)
 
     # calibration: instrumented traversal -> nodes / triangles per query per stage
     r.enable_stats(timing=False, instrumented=True)
@@ -710,8 +731,9 @@ def run_workload(a, world, rank, local, dist, coll_dev, quiet=False):
                                    f"({strategy.upper()}), {a.bounces} bounces, 1 step = 1 spp",
                        "scene": sd.name, "triangles": int(sd.num_triangles), "width": W, "height": H, "spp": K,
                        "strategy": strategy,
-                       "partition": (f"contiguous {band_h}-row bands over {world} rank(s), halo exchange by RCCL send/recv, "
-                                     "RCCL all_gather" if a.workload == "c4" and world > 1 else
+                       "partition": (f"contiguous {band_h}-row bands over {world} rank(s), halo exchange by RCCL send/recv "
+                                     f"({'libmpt native' if a.halo == 'native' else 'torch.distributed'}), RCCL all_gather"
+                                     if a.workload == "c4" and world > 1 else
                                      f"interleaved {BAND_H}-row bands over {world} rank(s), RCCL all_gather")},
             "roofline": roof(dom),
             "roofline_traversal": roof(max(lines[:3], key=lambda x: x["total_ms"])),

@@ -104,6 +104,17 @@ struct MptContext {
     int overlap = 0;   // opt-in: +1.2 % on C3, but per-kernel times then overlap
     hipStream_t stream2 = nullptr;
     hipEvent_t ev_fork = nullptr, ev_first = nullptr, ev_acc = nullptr, ev_join = nullptr;
+    // Overlapped ReSTIR DI batches (MPT_RESTIR_OVERLAP, default on): a batch's per-sample chain
+    // (G-buffer, reuse passes, halo exchanges: many small dependent launches) runs on the
+    // context's stream while the previous batch's shared later-bounce wavefront runs on stream2.
+    // The two batches in flight use the two halves of the path state (restir_half), each with its
+    // own counters; ev_half[h] marks the end of the last wavefront that used half h.
+    int restir_overlap = 1;
+    bool restir_overlap_ok = false;       // prepare_batch found room for both halves
+    int restir_half = 0;
+    hipEvent_t ev_chain = nullptr, ev_half[2] = {nullptr, nullptr}, ev_wave_join = nullptr;
+    bool ev_half_used[2] = {false, false};
+    bool wave_pending = false;            // a wavefront on stream2 not yet joined into the stream
     int num_cus = 256;
     int grid = 1024;
     // scene
@@ -229,6 +240,11 @@ struct MptContext {
     // padded staging rows of mpt_comm_gather (send: this rank's rows, recv: every rank's, root)
     void* comm = nullptr;
     int comm_rank = 0, comm_size = 1;
+    // the library's own halo exchange (mpt_set_halo_native): 1 RCCL send / receive over the
+    // communicator, 2 the one-GPU rehearsal (the bytes moved locally, no peers)
+    int halo_native = 0;
+    DBuf<uint8_t> halo_scratch;           // rehearsal: where the bytes go
+    DBuf<int32_t> halo_agree;             // device word of the halo agreement (ncclAllReduce max)
     DBuf<uint8_t> comm_send, comm_recv;
 };
 
@@ -388,11 +404,19 @@ void release_batch(MptContext* c) {
 // partition (+ the per-slot resolved materials when `mat_slot`); grows on demand.  On a
 // failure every path-state buffer is released (batch_cap = 0), so that the next call
 // allocates again instead of launching on a half-allocated state.
+// Both of the context's streams drained (before buffers an overlapped ReSTIR DI wavefront on
+// stream2 may still read are released or reallocated)
+static hipError_t drain(MptContext* c) {
+    hipError_t e = hipStreamSynchronize(c->stream);
+    if (e == hipSuccess && c->stream2) e = hipStreamSynchronize(c->stream2);
+    return e;
+}
+
 int ensure_batch(MptContext* c, int batch, bool mat_slot) {
     const size_t pix = (size_t)std::max(c->n_slots, 1);
     const bool have = batch <= c->batch_cap && c->ray_o.p;
     if (have && (!mat_slot || c->mat_slot.n >= pix * (size_t)c->batch_cap)) return MPT_OK;
-    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(drain(c));
     const int cap = have ? c->batch_cap : batch;
     const size_t N = pix * (size_t)cap;
     Allocs A;
@@ -430,7 +454,7 @@ int ensure_ext(MptContext* c, int batch, int per, int iter) {
     const size_t E = (size_t)std::max(c->n_slots, 1) * (size_t)batch * (size_t)per;
     if (E >= ((size_t)1 << 31)) return fail(MPT_ERR_OUT_OF_MEMORY, "extended light sampling: more than 2^31 entries");
     if (c->xq_o.n < E) {
-        HIPCHK(hipStreamSynchronize(c->stream));
+        HIPCHK(drain(c));
         Allocs A;
         A(c->xq_o, E); A(c->xq_d, E); A(c->xq_hit, E); A(c->xrec, 2 * E); A(c->xq_occ, E); A(c->xq_flag, E);
         A(c->xl_any, E); A(c->xl_cl, E); A(c->xl_light, E);
@@ -453,7 +477,7 @@ int ensure_paths(MptContext* c, int rx, int ry, int bh, int bi, int bc) {
     const bool same = c->res_x == rx && c->res_y == ry && c->band_h == bh && c->band_i == bi && c->band_c == bc &&
                       c->n_slots == n && c->fb_color.p;
     if (same) return MPT_OK;
-    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(drain(c));
     release_batch(c);                       // sized for the previous partition
     c->res_x = c->res_y = c->n_slots = 0;   // no partition until the group below is complete
     const size_t N = (size_t)std::max(n, 1);
@@ -868,6 +892,7 @@ int mpt_create(int device, void* hip_stream, MptContext** out) {
     if (const char* e = std::getenv("MPT_RESTIR_BATCH")) c->restir_batch = std::atoi(e);
     if (const char* e = std::getenv("MPT_ADAPTIVE_BATCH")) c->adaptive_batch = std::atoi(e);
     if (const char* e = std::getenv("MPT_MAT_PRIVATE")) c->mat_private = std::atoi(e);
+    if (const char* e = std::getenv("MPT_RESTIR_OVERLAP")) c->restir_overlap = std::atoi(e);
     if (const char* e = std::getenv("MPT_RESTIR_MAX_BATCH"))
         c->restir_max_batch = std::max(1, std::min(RESTIR_MAX_BATCH, std::atoi(e)));
     if (const char* e = std::getenv("MPT_SHADE_GLASS")) c->shade_glass = std::atoi(e);
@@ -909,7 +934,8 @@ int mpt_destroy(MptContext* c) {
     if (c->d_frames) (void)hipFree(c->d_frames);
     if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
     if (c->stream2) (void)hipStreamDestroy(c->stream2);
-    for (hipEvent_t e : {c->ev_fork, c->ev_first, c->ev_acc, c->ev_join})
+    for (hipEvent_t e : {c->ev_fork, c->ev_first, c->ev_acc, c->ev_join, c->ev_chain, c->ev_half[0], c->ev_half[1],
+                         c->ev_wave_join})
         if (e) (void)hipEventDestroy(e);
     delete c;
     (void)hipGetLastError();
@@ -1203,15 +1229,34 @@ static int prepare_batch(MptContext* c, const MptFrame* f, int batch) {
                                          "triangles picks from an empty list in the reference (Lights.h:22-220)");
     if ((int64_t)std::max(c->n_slots, 1) * batch > MPT_MAX_WAVEFRONT_PATHS)
         return fail(MPT_ERR_OUT_OF_MEMORY, "wavefront above MPT_MAX_WAVEFRONT_PATHS paths");
-    r = ensure_batch(c, batch, c->any_tex || f->bsdf_flags.white_furnace_mode);
-    if (r != MPT_OK) return r;
+    // overlapped ReSTIR DI batches need both halves of the path state (2 x the batch); without
+    // the room they run one after the other
+    const bool want_overlap = f->options.direct_light_sampling == MPT_LSS_RESTIR_DI && batch > 1 && c->restir_overlap &&
+                              ext_layout(*f, nullptr) == 0 && (int64_t)std::max(c->n_slots, 1) * 2 * batch <= MPT_MAX_WAVEFRONT_PATHS;
+    c->restir_overlap_ok = false;
+    if (want_overlap) {
+        // the second half sits at half the capacity
+        const int cap = 2 * batch;
+        r = ensure_batch(c, cap, c->any_tex || f->bsdf_flags.white_furnace_mode);
+        if (r == MPT_OK) c->restir_overlap_ok = c->batch_cap / 2 >= batch;
+        else { (void)hipGetLastError(); g_err.clear(); }
+    }
+    if (!c->restir_overlap_ok) {
+        r = ensure_batch(c, batch, c->any_tex || f->bsdf_flags.white_furnace_mode);
+        if (r != MPT_OK) return r;
+    }
     // each sample's final reservoirs, for the batch's bounce-0 shading (launch_frames_restir):
     // only read when the envmap is the ambient light (the deferred first bounce), so only held then
     const bool keep = f->options.direct_light_sampling == MPT_LSS_RESTIR_DI &&
                       f->world_settings.ambient_light_type == MPT_AMBIENT_ENVMAP;
-    if (!keep) c->rs_keep.release();
-    const size_t keep_n = 3 * (size_t)std::max(c->n_slots, 1) * (size_t)batch;   // the band's pixels only
+    if (!keep && c->rs_keep.p) {
+        HIPCHK(drain(c));
+        c->rs_keep.release();
+    }
+    // the band's pixels only; both halves' when overlapped (half 1 at half the capacity)
+    const size_t keep_n = 3 * (size_t)std::max(c->n_slots, 1) * (size_t)(c->restir_overlap_ok ? c->batch_cap : batch);
     if (keep && batch > 1 && c->rs_keep.n < keep_n) {
+        HIPCHK(drain(c));
         c->rs_keep.release();
         if (c->rs_keep.alloc(keep_n) != hipSuccess) {
             (void)hipGetLastError();
@@ -1227,7 +1272,8 @@ static int prepare_batch(MptContext* c, const MptFrame* f, int batch) {
 static int ensure_overlap(MptContext* c) {
     if (c->stream2) return MPT_OK;
     if (c->spill2.n != c->spill.n) HIPCHK(c->spill2.alloc(c->spill.n));
-    for (hipEvent_t* e : {&c->ev_fork, &c->ev_first, &c->ev_acc, &c->ev_join})
+    for (hipEvent_t* e : {&c->ev_fork, &c->ev_first, &c->ev_acc, &c->ev_join, &c->ev_chain, &c->ev_half[0], &c->ev_half[1],
+                          &c->ev_wave_join})
         if (!*e) HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));   // kept across a failed attempt
     HIPCHK(hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking));
     return MPT_OK;
@@ -1241,7 +1287,10 @@ static int launch_batch(MptContext* c, const MptFrame* f, int batch) {
     if (c->frame_slot + batch > FRAME_RING) c->frame_slot = 0;
     int slot = c->frame_slot;
     c->frame_slot = (c->frame_slot + batch) % FRAME_RING;
-    if (slot == 0) HIPCHK(hipStreamSynchronize(c->stream));
+    if (slot == 0) {
+        HIPCHK(hipStreamSynchronize(c->stream));
+        if (c->stream2) HIPCHK(hipStreamSynchronize(c->stream2));   // an overlapped wavefront reads its frames
+    }
     for (int k = 0; k < batch; k++) c->h_frames[slot + k] = f[k];
     HIPCHK(hipMemcpyAsync(c->d_frames + slot, c->h_frames + slot, batch * sizeof(MptFrame), hipMemcpyHostToDevice,
                           c->stream));
@@ -1324,7 +1373,29 @@ static int launch_batch(MptContext* c, const MptFrame* f, int batch) {
         cfg.launches = cfg0.launches + cfg1.launches;
     } else if (f->options.direct_light_sampling == MPT_LSS_RESTIR_DI && batch > 1) {
         P.group = std::max(c->n_slots, 1);   // slot = sample * pixels + pixel
-        e = launch_frames_restir(dev_scene(c), P, c->d_frames + slot, c->h_frames + slot, batch, cfg, c->stream);
+        if (c->restir_overlap_ok) {
+            int rr = ensure_overlap(c);
+            if (rr != MPT_OK) return rr;
+            const int h = c->restir_half;
+            c->restir_half ^= 1;
+            if (h) {   // the second half of the path state, counters and kept reservoirs
+                const size_t off = (size_t)(c->batch_cap / 2) * (size_t)std::max(c->n_slots, 1);
+                offset_slots(P, off);
+                P.counters += CTR_COUNT;
+                if (P.rs_keep) P.rs_keep += 3 * off;
+            }
+            // this half's previous wavefront must be done before the chain rewrites its slots
+            if (c->ev_half_used[h]) HIPCHK(hipStreamWaitEvent(c->stream, c->ev_half[h], 0));
+            cfg.wave_stream = c->stream2;
+            cfg.wave_spill = c->spill2.p;
+            cfg.ev_chain = c->ev_chain;
+            e = launch_frames_restir(dev_scene(c), P, c->d_frames + slot, c->h_frames + slot, batch, cfg, c->stream);
+            HIPCHK(hipEventRecord(c->ev_half[h], c->stream2));
+            c->ev_half_used[h] = true;
+            c->wave_pending = true;
+        } else {
+            e = launch_frames_restir(dev_scene(c), P, c->d_frames + slot, c->h_frames + slot, batch, cfg, c->stream);
+        }
     } else {
         e = launch_frame(dev_scene(c), P, c->d_frames + slot, *f, cfg, c->stream);
     }
@@ -1333,7 +1404,8 @@ static int launch_batch(MptContext* c, const MptFrame* f, int batch) {
     if (e != hipSuccess) return fail(MPT_ERR_HIP, std::string("kernel launch: ") + hipGetErrorString(e));
     if (cfg.halo_rc != 0) return fail(MPT_ERR_HIP, "halo exchange callback failed (" + std::to_string(cfg.halo_rc) + ")");
     if (c->timing) {
-        HIPCHK(hipEventRecord(c->ev_frame[pool][1], c->stream));
+        // (an overlapped ReSTIR DI batch ends with its wavefront on stream2)
+        HIPCHK(hipEventRecord(c->ev_frame[pool][1], cfg.wave_stream ? cfg.wave_stream : c->stream));
         c->ev_used[pool] = cfg.ev_used;
         c->ev_pending[pool] = true;
     }
@@ -1411,6 +1483,16 @@ static bool batchable(const MptContext* c, const MptFrame& a, const MptFrame& b)
     return std::memcmp(&t, &a, sizeof(MptFrame)) == 0;
 }
 
+// The overlapped ReSTIR DI wavefronts of the call joined into the context's stream: everything
+// later enqueued there (the next call, framebuffer reads, synchronisation) follows them.
+static int join_waves(MptContext* c) {
+    if (!c->wave_pending) return MPT_OK;
+    c->wave_pending = false;
+    HIPCHK(hipEventRecord(c->ev_wave_join, c->stream2));
+    HIPCHK(hipStreamWaitEvent(c->stream, c->ev_wave_join, 0));
+    return MPT_OK;
+}
+
 int mpt_render_frames(MptContext* c, const MptFrame* frames, int32_t count, int32_t max_batch) {
     if (!c || !frames || count < 0) return fail(MPT_ERR_INVALID_ARGUMENT, "NULL argument or negative count");
     if (count == 0) return MPT_OK;
@@ -1441,14 +1523,15 @@ int mpt_render_frames(MptContext* c, const MptFrame* frames, int32_t count, int3
         }
         if (r != MPT_OK) return r;
         r = launch_batch(c, frames + i, b);
-        if (r != MPT_OK) return r;
+        if (r != MPT_OK) { join_waves(c); return r; }
         i += b;
     }
-    return MPT_OK;
+    return join_waves(c);
 }
 
 int mpt_set_halo_exchange(MptContext* c, MptHaloExchangeFn fn, void* user) {
     if (!c) return fail(MPT_ERR_INVALID_ARGUMENT, "NULL context");
+    c->halo_native = 0;
     c->halo_fn = fn;
     c->halo_user = fn ? user : nullptr;
     return MPT_OK;
@@ -1587,6 +1670,12 @@ struct Rccl {
     int (*comm_destroy)(void*) = nullptr;
     int (*gather)(const void*, void*, size_t, int, int, void*, hipStream_t) = nullptr;
     const char* (*error_string)(int) = nullptr;
+    // the ReSTIR DI halo exchange (native_halo)
+    int (*group_start)() = nullptr;
+    int (*group_end)() = nullptr;
+    int (*send)(const void*, size_t, int, int, void*, hipStream_t) = nullptr;
+    int (*recv)(void*, size_t, int, int, void*, hipStream_t) = nullptr;
+    int (*all_reduce)(const void*, void*, size_t, int, int, void*, hipStream_t) = nullptr;
 };
 
 Rccl* rccl_lib() {
@@ -1603,6 +1692,11 @@ Rccl* rccl_lib() {
     r.gather = (int (*)(const void*, void*, size_t, int, int, void*, hipStream_t))dlsym(h, "ncclGather");
     r.error_string = (const char* (*)(int))dlsym(h, "ncclGetErrorString");
     r.comm_init_rank = (int (*)(void**, int, const void*, int))dlsym(h, "ncclCommInitRank");
+    r.group_start = (int (*)())dlsym(h, "ncclGroupStart");
+    r.group_end = (int (*)())dlsym(h, "ncclGroupEnd");
+    r.send = (int (*)(const void*, size_t, int, int, void*, hipStream_t))dlsym(h, "ncclSend");
+    r.recv = (int (*)(void*, size_t, int, int, void*, hipStream_t))dlsym(h, "ncclRecv");
+    r.all_reduce = (int (*)(const void*, void*, size_t, int, int, void*, hipStream_t))dlsym(h, "ncclAllReduce");
     r.ok = r.get_unique_id && r.comm_destroy && r.gather && r.error_string && r.comm_init_rank;
     if (!r.ok) r.why = "librccl.so.1 lacks ncclGetUniqueId / ncclCommInitRank / ncclGather / ncclCommDestroy";
     return &r;
@@ -1611,6 +1705,8 @@ Rccl* rccl_lib() {
 constexpr int NCCL_ID_BYTES = 128;   // NCCL_UNIQUE_ID_BYTES
 struct NcclId { char internal[NCCL_ID_BYTES]; };
 constexpr int NCCL_UINT8 = 1;        // ncclUint8
+constexpr int NCCL_INT32 = 2;        // ncclInt32
+constexpr int NCCL_MAX = 2;          // ncclMax
 
 void rccl_comm_destroy(void* comm) {
     if (rccl_lib()->ok) (void)rccl_lib()->comm_destroy(comm);
@@ -1687,6 +1783,104 @@ int mpt_comm_gather(MptContext* c, int32_t root, int kind, void* dst, int dst_is
                                      dst_is_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, false, c->device,
                                      c->device, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
+    return MPT_OK;
+}
+
+// ---- the ReSTIR DI halo exchange in the library (mpt_set_halo_native) --------------------------
+// Rank k of the communicator owns contiguous band k of the frame (band_height rows).  At each
+// exchange point (mpt.h MptHaloExchange) the rows of every buffer that lie in a peer's halo go to
+// it and the peers' rows in this band's halo come in: one ncclGroupStart / ncclSend / ncclRecv
+// group on the context's stream (peer-to-peer over xGMI; the host does not wait).  The halo
+// agreement is an ncclAllReduce (max) of one int read back by the host -- skipped when the
+// library derived the halo from the frame alone (halo_agreed, a still camera).  Sends and
+// receives with one peer are issued in buffer order on both sides, so they pair up.
+namespace {
+int band_overlap(int a0, int a1, int b0, int b1, int& lo, int& hi) {
+    lo = std::max(a0, b0);
+    hi = std::min(a1, b1);
+    return lo < hi;
+}
+int native_halo(void* user, MptHaloExchange* x) {
+    MptContext* c = (MptContext*)user;
+    hipStream_t st = (hipStream_t)x->stream;
+    const int h0 = x->halo_rows;
+    if (c->halo_native == 2) {
+        // rehearsal on one GPU: the bytes this rank would receive, moved by one device copy (an
+        // exchange is one grouped send / receive); a moving camera's agreement waits as the
+        // all-reduce's read-back would
+        if (x->phase == MPT_HALO_GBUFFER && !x->halo_agreed && hipStreamSynchronize(st) != hipSuccess) return 1;
+        const int n = std::max(1, c->band_c), bh = c->band_h, k = c->band_i;
+        size_t bytes = 0;
+        for (int p = 0; p < n; p++) {
+            if (p == k) continue;
+            const int p0 = std::min(x->res_y, p * bh), p1 = std::min(x->res_y, p0 + bh);
+            int lo, hi;
+            for (int i = 0; i < x->n_buffers; i++) {
+                const size_t row = (size_t)x->res_x * (size_t)x->bytes_per_pixel[i];
+                if (band_overlap(std::max(0, x->own_y0 - h0), x->own_y0, p0, p1, lo, hi)) bytes += (size_t)(hi - lo) * row;
+                if (band_overlap(x->own_y1, std::min(x->res_y, x->own_y1 + h0), p0, p1, lo, hi)) bytes += (size_t)(hi - lo) * row;
+            }
+        }
+        if (bytes == 0) return 0;
+        if (c->halo_scratch.n < 2 * bytes && c->halo_scratch.alloc(2 * bytes) != hipSuccess) return 1;
+        return hipMemcpyAsync(c->halo_scratch.p + bytes, c->halo_scratch.p, bytes, hipMemcpyDeviceToDevice, st) == hipSuccess ? 0 : 1;
+    }
+    Rccl& r = *rccl_lib();
+    if (!c->comm || !r.send || !r.recv || !r.group_start || !r.group_end || !r.all_reduce) return 2;
+    const int n = c->comm_size, k = c->comm_rank, bh = c->band_h;
+    if (c->band_c != n || c->band_i != k) return 4;   // rank k must render band k of ranks
+    if (x->phase == MPT_HALO_GBUFFER && !x->halo_agreed) {
+        if (c->halo_agree.n < 1 && c->halo_agree.alloc(1) != hipSuccess) return 1;
+        int32_t v = x->halo_rows;
+        if (hipMemcpyAsync(c->halo_agree.p, &v, sizeof(v), hipMemcpyHostToDevice, st) != hipSuccess) return 1;
+        if (r.all_reduce(c->halo_agree.p, c->halo_agree.p, 1, NCCL_INT32, NCCL_MAX, c->comm, st) != 0) return 3;
+        if (hipMemcpyAsync(&v, c->halo_agree.p, sizeof(v), hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess) return 1;
+        x->halo_rows = v;
+    }
+    const int h = x->halo_rows;
+    auto need = [&](int q, int& a0, int& a1, int& b0, int& b1) {   // band q's halo ranges
+        const int q0 = std::min(x->res_y, q * bh), q1 = std::min(x->res_y, q0 + bh);
+        a0 = std::max(0, q0 - h); a1 = q0; b0 = q1; b1 = std::min(x->res_y, q1 + h);
+        return q0 < q1;
+    };
+    const int m0 = std::min(x->res_y, k * bh), m1 = std::min(x->res_y, m0 + bh);
+    int rc = r.group_start();
+    for (int p = 0; p < n && rc == 0; p++) {
+        if (p == k) continue;
+        const int p0 = std::min(x->res_y, p * bh), p1 = std::min(x->res_y, p0 + bh);
+        int a0, a1, b0, b1, lo, hi;
+        const bool mine = need(k, a0, a1, b0, b1);
+        int c0, c1, d0, d1;
+        const bool theirs = need(p, c0, c1, d0, d1);
+        for (int i = 0; i < x->n_buffers && rc == 0; i++) {
+            uint8_t* buf = (uint8_t*)x->buffers[i];
+            const size_t row = (size_t)x->res_x * (size_t)x->bytes_per_pixel[i];
+            // this band's rows in peer p's halo
+            if (theirs && band_overlap(c0, c1, m0, m1, lo, hi)) rc = r.send(buf + lo * row, (hi - lo) * row, NCCL_UINT8, p, c->comm, st);
+            if (rc == 0 && theirs && band_overlap(d0, d1, m0, m1, lo, hi)) rc = r.send(buf + lo * row, (hi - lo) * row, NCCL_UINT8, p, c->comm, st);
+            // peer p's rows in this band's halo
+            if (rc == 0 && mine && band_overlap(a0, a1, p0, p1, lo, hi)) rc = r.recv(buf + lo * row, (hi - lo) * row, NCCL_UINT8, p, c->comm, st);
+            if (rc == 0 && mine && band_overlap(b0, b1, p0, p1, lo, hi)) rc = r.recv(buf + lo * row, (hi - lo) * row, NCCL_UINT8, p, c->comm, st);
+        }
+    }
+    const int re = r.group_end();
+    return rc != 0 ? 3 : (re != 0 ? 3 : 0);
+}
+}  // namespace
+
+int mpt_set_halo_native(MptContext* c, int32_t mode) {
+    if (!c) return fail(MPT_ERR_INVALID_ARGUMENT, "NULL context");
+    if (mode < 0 || mode > 2) return fail(MPT_ERR_INVALID_ARGUMENT, "mode must be 0 (off), 1 (RCCL) or 2 (rehearsal)");
+    if (mode == 1) {
+        if (!c->comm) return fail(MPT_ERR_INVALID_ARGUMENT, "no communicator (mpt_comm_init)");
+        Rccl& r = *rccl_lib();
+        if (!r.send || !r.recv || !r.group_start || !r.group_end || !r.all_reduce)
+            return fail(MPT_ERR_UNSUPPORTED, "librccl.so.1 lacks ncclSend / ncclRecv / ncclGroupStart / ncclAllReduce");
+    }
+    c->halo_native = mode;
+    c->halo_fn = mode ? &native_halo : nullptr;
+    c->halo_user = mode ? (void*)c : nullptr;
     return MPT_OK;
 }
 

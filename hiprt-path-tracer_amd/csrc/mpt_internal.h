@@ -261,10 +261,12 @@ enum {
     CTR_XANY = 12, CTR_XCL = 13, CTR_XLIGHT = 14,   // ext query lists (extended light sampling)
     CTR_RQ = 15, CTR_RQV = 16,                      // staged ReSTIR DI rays / visibility-reuse rays
     CTR_RQE0 = 17, CTR_RQE1 = 18,                   // staged ReSTIR DI target evaluations: plain / generic class
-    CTR_GLASS = 19,                                 // length of the glass-class list (top of qf, k_split)
+    CTR_F_RQA = 19, CTR_F_RQB = 20,                 // the work counters of a staged pass's two list traversals
+    CTR_RQ_GROUP = 6,                               // CTR_RQ .. CTR_F_RQB: zeroed by one memset per staged pass
+    CTR_GLASS = 21,                                 // length of the glass-class list (top of qf, k_split)
     // the persistent traversals' work counters of a bounce, one per launch (no reset between them)
-    CTR_F_PATH = 20, CTR_F_ANY = 21, CTR_F_CL = 22, CTR_F_OCC = 23, CTR_F_XANY = 24, CTR_F_XCL = 25, CTR_F_XOCC = 26,
-    CTR_COUNT = 27
+    CTR_F_PATH = 22, CTR_F_ANY = 23, CTR_F_CL = 24, CTR_F_OCC = 25, CTR_F_XANY = 26, CTR_F_XCL = 27, CTR_F_XOCC = 28,
+    CTR_COUNT = 29
 };
 constexpr int CTR_BOUNCE_FIRST = CTR_ANY;           // [CTR_BOUNCE_FIRST, CTR_COUNT): reset per bounce
 
@@ -299,6 +301,12 @@ struct LaunchCfg {
     hipEvent_t ev_first_trace;
     hipEvent_t ev_acc_done;
     hipEvent_t ev_acc_wait;
+    // overlapped ReSTIR DI batches (launch_frames_restir): the shared later-bounce wavefront runs
+    // on wave_stream (after ev_chain, recorded at the end of the per-sample chain) with its own
+    // traversal spill area
+    hipStream_t wave_stream;
+    uint32_t* wave_spill;
+    hipEvent_t ev_chain;
 };
 
 // Moves every per-slot pointer of P by `off` slots: a view of slots [off, off + P.n) of the

@@ -2663,7 +2663,7 @@ static void launch_spatial_pass(int ovr, bool def_bias, const MptFrame& hf, Laun
         return;
     }
     const dim3 gp(blocks_for(P.n));
-    hipMemsetAsync(&P.counters[CTR_RQ], 0, 4 * sizeof(int32_t), st);   // CTR_RQ, CTR_RQV, CTR_RQE0, CTR_RQE1
+    hipMemsetAsync(&P.counters[CTR_RQ], 0, CTR_RQ_GROUP * sizeof(int32_t), st);   // the lists + their work counters
     launch_restir_kernel(ovr, RK_SP_SELECT, gp, st, S, P, d_frame, pass, in, out);
     hipLaunchKernelGGL(k_count_add64, dim3(1), dim3(64), 0, st, P.ray_counts + 5, &P.counters[CTR_RQE0]);
     {
@@ -2672,14 +2672,13 @@ static void launch_spatial_pass(int ovr, bool def_bias, const MptFrame& hf, Laun
     }
     launch_restir_kernel(ovr, RK_SP_EVAL_GENERIC, g, st, S, P, d_frame, pass, in, out);
     TraceArgs ta{};
-    ta.S = S; ta.P = P; ta.queue = P.rq_list; ta.count_ptr = &P.counters[CTR_RQ]; ta.fetch = &P.counters[CTR_FETCH];
+    ta.S = S; ta.P = P; ta.queue = P.rq_list; ta.count_ptr = &P.counters[CTR_RQ]; ta.fetch = &P.counters[CTR_F_RQA];
     ta.raw_o = P.rq_o; ta.raw_d = P.rq_d; ta.raw_key = P.rq_key; ta.raw_occ = P.rq_occ;
     ta.F = d_frame; ta.alpha = hf.render_settings.do_alpha_testing ? 1 : 0;
-    hipMemsetAsync(&P.counters[CTR_FETCH], 0, sizeof(int32_t), st);
     launch_trace_mode<TM_LIST_ANY>(ta, cfg.grid_persistent, cfg.stats, st);
     launch_restir_kernel(ovr, RK_SP_COMBINE, gp, st, S, P, d_frame, pass, in, out);
     ta.count_ptr = &P.counters[CTR_RQV];
-    hipMemsetAsync(&P.counters[CTR_FETCH], 0, sizeof(int32_t), st);
+    ta.fetch = &P.counters[CTR_F_RQB];
     launch_trace_mode<TM_LIST_ANY>(ta, cfg.grid_persistent, cfg.stats, st);
     hipLaunchKernelGGL(k_rs_visapply, gp, dim3(TB), 0, st, P, out);
 }
@@ -2698,7 +2697,7 @@ static void launch_fused_pass(int ovr, bool def_bias, const MptFrame& hf, Launch
         return;
     }
     const dim3 gp(blocks_for(P.n));
-    hipMemsetAsync(&P.counters[CTR_RQ], 0, 4 * sizeof(int32_t), st);   // CTR_RQ, CTR_RQV, CTR_RQE0, CTR_RQE1
+    hipMemsetAsync(&P.counters[CTR_RQ], 0, CTR_RQ_GROUP * sizeof(int32_t), st);   // the lists + their work counters
     launch_restir_kernel(ovr, RK_ST_SELECT, gp, st, S, P, d_frame);
     hipLaunchKernelGGL(k_count_add64, dim3(1), dim3(64), 0, st, P.ray_counts + 5, &P.counters[CTR_RQE0]);
     {
@@ -2707,14 +2706,13 @@ static void launch_fused_pass(int ovr, bool def_bias, const MptFrame& hf, Launch
     }
     launch_restir_kernel(ovr, RK_ST_EVAL_GENERIC, g, st, S, P, d_frame);
     TraceArgs ta{};
-    ta.S = S; ta.P = P; ta.queue = P.rq_list; ta.count_ptr = &P.counters[CTR_RQ]; ta.fetch = &P.counters[CTR_FETCH];
+    ta.S = S; ta.P = P; ta.queue = P.rq_list; ta.count_ptr = &P.counters[CTR_RQ]; ta.fetch = &P.counters[CTR_F_RQA];
     ta.raw_o = P.rq_o; ta.raw_d = P.rq_d; ta.raw_key = P.rq_key; ta.raw_occ = P.rq_occ;
     ta.F = d_frame; ta.alpha = hf.render_settings.do_alpha_testing ? 1 : 0;
-    hipMemsetAsync(&P.counters[CTR_FETCH], 0, sizeof(int32_t), st);
     launch_trace_mode<TM_LIST_ANY>(ta, cfg.grid_persistent, cfg.stats, st);
     launch_restir_kernel(ovr, RK_ST_COMBINE, gp, st, S, P, d_frame);
     ta.count_ptr = &P.counters[CTR_RQV];
-    hipMemsetAsync(&P.counters[CTR_FETCH], 0, sizeof(int32_t), st);
+    ta.fetch = &P.counters[CTR_F_RQB];
     launch_trace_mode<TM_LIST_ANY>(ta, cfg.grid_persistent, cfg.stats, st);
     hipLaunchKernelGGL(k_rs_visapply, gp, dim3(TB), 0, st, P, P.rs_out);
 }
@@ -2805,21 +2803,20 @@ static void launch_restir(const DevScene& S, DevPaths& P, const MptFrame* d_fram
         if (!staged) launch_restir_kernel(ovr, RK_INITIAL, g, st, S, P, d_frame);
         else {
             const dim3 gp(blocks_for(P.n));
-            hipMemsetAsync(&P.counters[CTR_RQ], 0, 4 * sizeof(int32_t), st);   // CTR_RQ, CTR_RQV, CTR_RQE0, CTR_RQE1
+            hipMemsetAsync(&P.counters[CTR_RQ], 0, CTR_RQ_GROUP * sizeof(int32_t), st);   // the lists + their work counters
             hipLaunchKernelGGL(k_rsi_classify, dim3((P.n + TB * RSI_PPT - 1) / (TB * RSI_PPT)), dim3(TB), 0, st, S, P, d_frame,
                                ovr == MPT_BSDF_NONE ? 1 : 0);
             launch_restir_kernel(ovr, RK_INITIAL_STAGED_PLAIN, g, st, S, P, d_frame);
             launch_restir_kernel(ovr, RK_INITIAL_STAGED_GENERIC, g, st, S, P, d_frame);
             TraceArgs ta{};
-            ta.S = S; ta.P = P; ta.queue = P.rq_list; ta.count_ptr = &P.counters[CTR_RQ]; ta.fetch = &P.counters[CTR_FETCH];
+            ta.S = S; ta.P = P; ta.queue = P.rq_list; ta.count_ptr = &P.counters[CTR_RQ]; ta.fetch = &P.counters[CTR_F_RQA];
             ta.raw_o = P.rq_o; ta.raw_d = P.rq_d; ta.raw_key = P.rq_key; ta.raw_occ = P.rq_occ;
             ta.raw_hit = P.rq_o;   // each hit written over its own (already read) ray origin
             ta.F = d_frame; ta.alpha = hf.render_settings.do_alpha_testing ? 1 : 0;
-            hipMemsetAsync(&P.counters[CTR_FETCH], 0, sizeof(int32_t), st);
             launch_trace_mode<TM_LIST_CLOSEST>(ta, cfg.grid_persistent, cfg.stats, st);
             hipLaunchKernelGGL(k_rsi_finish, dim3((P.n + TB * RSI_PPT - 1) / (TB * RSI_PPT)), dim3(TB), 0, st, S, P, d_frame);
             ta.count_ptr = &P.counters[CTR_RQV];
-            hipMemsetAsync(&P.counters[CTR_FETCH], 0, sizeof(int32_t), st);
+            ta.fetch = &P.counters[CTR_F_RQB];
             launch_trace_mode<TM_LIST_ANY>(ta, cfg.grid_persistent, cfg.stats, st);
             hipLaunchKernelGGL(k_rs_visapply, gp, dim3(TB), 0, st, P, P.rs_init);
         }
@@ -2911,11 +2908,8 @@ static void frame_bounces(const DevScene& S, DevPaths& P, const MptFrame* d_fram
             timed_trace<TM_PATH>(ta, cfg, st);
         }
         if (b == 0 && cfg.ev_first_trace) hipEventRecord(cfg.ev_first_trace, st);
-        if (restir && b == 0 && !restir_done) {
-            restir_first_bounce(S, P, d_frame, hf, cfg, st);
-            // the ReSTIR DI passes use some of the per-bounce counters (their lists and staged rays)
-            hipMemsetAsync(&P.counters[CTR_BOUNCE_FIRST], 0, (CTR_COUNT - CTR_BOUNCE_FIRST) * sizeof(int32_t), st);
-        }
+        // (the ReSTIR DI passes use only CTR_REPROJ and their own CTR_RQ group of the per-bounce counters)
+        if (restir && b == 0 && !restir_done) restir_first_bounce(S, P, d_frame, hf, cfg, st);
         const dim3 cp_grid((n + CP_NT * CP_ITEMS - 1) / (CP_NT * CP_ITEMS));
         {
             TimedScope ts(cfg, st, KT_SPLIT);
@@ -3139,9 +3133,16 @@ hipError_t launch_frames_restir(const DevScene& S, const DevPaths& PF, const Mpt
         }
     }
     // bounces 1..nb (deferred: 0..nb) of every sample as one wavefront (slot = sample * n + pixel:
-    // group = n)
+    // group = n); overlapped batches: on the wave stream, once the chain above is done, so that
+    // the next batch's chain runs beside it
     DevPaths G = PF;
     G.group = n;
+    if (cfg.wave_stream) {
+        hipEventRecord(cfg.ev_chain, st);
+        hipStreamWaitEvent(cfg.wave_stream, cfg.ev_chain, 0);
+        st = cfg.wave_stream;
+        G.stack_spill = cfg.wave_spill;
+    }
     if (defer) {
         G.rs_keep_on = 1;
         hipLaunchKernelGGL(k_iota, dim3(blocks_for(batch * n)), dim3(TB), 0, st, G.q0, batch * n);

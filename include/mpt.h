@@ -598,6 +598,15 @@ int mpt_gather(MptContext* const* ctxs, int32_t n, int32_t root, int kind, void*
 int mpt_comm_unique_id(uint8_t* out_id, int32_t cap);
 int mpt_comm_init(MptContext* ctx, int32_t nranks, int32_t rank, const uint8_t* id);
 int mpt_comm_gather(MptContext* ctx, int32_t root, int kind, void* dst, int dst_is_device);
+/* ReSTIR DI across the ranks of the communicator without a host callback: rank k's frames carry
+ * the contiguous band (band_height = ceil(res_y / ranks), band_index = k, band_count = ranks) and
+ * the library exchanges the halo rows itself -- one ncclGroupStart / ncclSend / ncclRecv group per
+ * exchange point on the context's stream, the halo agreement an ncclAllReduce (max), skipped when
+ * the camera did not move (MptHaloExchange.halo_agreed).  mode: 1 RCCL (after mpt_comm_init),
+ * 2 the one-GPU rehearsal (the bytes a rank would receive moved by one local device copy; the
+ * rows keep what the buffers held -- timing only), 0 off.  Replaces mpt_set_halo_exchange's
+ * callback. */
+int mpt_set_halo_native(MptContext* ctx, int32_t mode);
 /* Status buffers: mpt_clear_status <- GPURenderer::internal_update_clear_device_status_buffers
  * (GPURenderer.cpp:275-283, once per displayed frame); the last sample of the frame sets
  * render_settings.do_update_status_buffers; mpt_query_status <- copy_status_buffers (.cpp:269-273). */

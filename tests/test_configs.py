@@ -236,6 +236,28 @@ def test_c4_restir_batched_equals_unbatched(city, luts, city_oracle, monkeypatch
 
 
 @pytest.mark.gpu
+def test_c4_restir_overlapped_batches_equal_sequential(city, luts, city_oracle, monkeypatch):
+    """Overlapped ReSTIR DI batches (a batch's later-bounce wavefront on a second stream beside the
+    next batch's per-sample chain, the two batches on the two halves of the path state) against
+    MPT_RESTIR_OVERLAP=0, on the C4 city frame with three batches per call: the same sums and ray
+    counts."""
+    _, env = city_oracle
+    frs = c4_frames(city, 6)
+    out = {}
+    for mode in ("sequential", "overlapped"):
+        monkeypatch.setenv("MPT_RESTIR_OVERLAP", "0" if mode == "sequential" else "1")
+        r = _gpu(city, luts, env)
+        r.render_samples(frs, max_batch=2)
+        r.synchronize_kernel()
+        out[mode] = r.framebuffer(abi.FB_COLOR)
+        st = r.stats()
+        out[mode + "_rays"] = (st.rays_any, st.rays_closest)
+        r.close()
+    _same(out["overlapped"], out["sequential"], "C4 overlapped vs sequential batches")
+    assert out["overlapped_rays"] == out["sequential_rays"]
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("fused", [True, False], ids=["fused", "unfused"])
 def test_c4_city_restir_reset_in_used_context_bit_exact(city, luts, city_oracle, fused):
     """The C4 timed path: frames rendered, then GPURenderer::reset (sample 0, need_to_reset, the
