@@ -296,12 +296,13 @@ def emulate_restir_ranks(a, r, cam, W, H, opt, wset, alpha, n_ranks, K, device):
         rows = mpt.partition_rows(H, *band)
         if rows == 0:
             continue
-        want = TARGET_PATHS / max(1, rows * W)
+        want = a.batch or TARGET_PATHS / max(1, rows * W)
         batch = min((d for d in range(1, min(MAX_BATCH, K) + 1) if K % d == 0), key=lambda d: (abs(d - want), -d))
         r.enable_stats(timing=False, instrumented=False)
         r.render_samples(frames_for(cam, W, H, opt, (1, 0, 1), 2, bounces=a.bounces, world=wset, alpha=alpha))
-        r.render_samples(frames_for(cam, W, H, opt, band, a.warmup, bounces=a.bounces, world=wset, alpha=alpha),
-                         max_batch=batch)
+        # the band's warmup: one whole batch, so that the path state is allocated before the timing
+        r.render_samples(frames_for(cam, W, H, opt, band, max(a.warmup, 2 * batch), bounces=a.bounces, world=wset,
+                                    alpha=alpha), max_batch=batch)
         frames = frames_for(cam, W, H, opt, band, K, bounces=a.bounces, world=wset, alpha=alpha)
         r.synchronize_kernel()
         r.enable_stats(timing=True, instrumented=False)

@@ -1279,9 +1279,17 @@ static int ensure_overlap(MptContext* c) {
     return MPT_OK;
 }
 
+static int join_waves(MptContext* c);
+
 // Enqueues a prepared wavefront (prepare_batch).
 static int launch_batch(MptContext* c, const MptFrame* f, int batch) {
     const bool restir_part = f->options.direct_light_sampling == MPT_LSS_RESTIR_DI && f->band_count > 1;
+    // anything but the next overlapped ReSTIR DI batch uses the first half of the path state and
+    // counter set: a wavefront still running on stream2 is joined first
+    if (!(f->options.direct_light_sampling == MPT_LSS_RESTIR_DI && batch > 1 && c->restir_overlap_ok)) {
+        int jr = join_waves(c);
+        if (jr != MPT_OK) return jr;
+    }
     // stage the frame constants through a pinned ring (the previous use of the slot
     // has completed once 64 frames later are enqueued; synchronise defensively)
     if (c->frame_slot + batch > FRAME_RING) c->frame_slot = 0;

@@ -233,12 +233,12 @@ def test_unsupported_options_fail_loudly(scenes, luts):
     sd = scenes["cornell_pbr"]
     r = renderer(sd, luts)
     f = frames(sd, 16, 16, 1)[0]
-    f.render_settings.wants_render_low_resolution = True
-    f.render_settings.allow_render_low_resolution = True
+    f.render_settings.restir_di_settings.number_of_passes = 5   # more spatial passes than restir_di_seeds holds
+    f.options.direct_light_sampling = abi.LSS_RESTIR_DI
     with pytest.raises(mpt.MptError) as e:
         r.render(f)
     assert e.value.code == -4
-    f = frames(sd, 16, 16, 1, lss=abi.LSS_RESTIR_DI, band=(8, 0, 2))[0]   # ReSTIR DI needs the whole frame
+    f = frames(sd, 16, 16, 1, lss=abi.LSS_RESTIR_DI, band=(8, 0, 2))[0]   # interleaved bands under ReSTIR DI
     with pytest.raises(mpt.MptError):
         r.render(f)
 
