@@ -2,7 +2,7 @@
 # rank-of-8 rehearsal at 128 and 32 samples per batch
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 o=gpurun_out/r05d; mkdir -p $o
-timeout -k 10 600 python -u -m pytest -q -x --timeout 300 --timeout-method thread -m gpu tests/test_low_res.py tests/test_restir.py tests > $o/pytest.log 2>&1 || { tail -30 $o/pytest.log; exit 1; }
+timeout -k 10 600 python -u -m pytest -q -x --timeout 300 --timeout-method thread -m gpu tests > $o/pytest.log 2>&1 || { tail -30 $o/pytest.log; exit 1; }
 tail -3 $o/pytest.log
 timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > $o/smoke.log 2>&1 || { tail -5 $o/smoke.log; exit 1; }
 cat $o/smoke.log
