@@ -115,6 +115,15 @@ struct MptContext {
     hipEvent_t ev_chain = nullptr, ev_half[2] = {nullptr, nullptr}, ev_wave_join = nullptr;
     bool ev_half_used[2] = {false, false};
     bool wave_pending = false;            // a wavefront on stream2 not yet joined into the stream
+    // One-sample launch sets as a HIP graph (MPT_GRAPHS, default on): mpt_render_frame's ~50
+    // launches of a path-tracing sample captured once and replayed while the frame differs only in
+    // what the kernels read from it (seeds, sample number, cameras, status flags); the graph reads
+    // its frame from the extra ring slot d_frames[FRAME_RING].  Keyed by those frame fields that
+    // steer the host's launch sequence and by the kernels' by-value arguments (buffer pointers).
+    int graphs = 1;
+    hipGraphExec_t graph_exec = nullptr;
+    std::vector<uint8_t> graph_key;
+    uint32_t graph_launches = 0;
     int num_cus = 256;
     int grid = 1024;
     // scene
@@ -851,8 +860,8 @@ static int create_context(MptContext* c, int device, void* hip_stream) {
     c->grid = c->num_cus * MPT_TRACE_BLOCKS_PER_CU;   // persistent traversal / ReSTIR grids
     if (hip_stream) c->stream = (hipStream_t)hip_stream;
     else { HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)); c->own_stream = true; }
-    HIPCHK(hipHostMalloc((void**)&c->h_frames, sizeof(MptFrame) * FRAME_RING));
-    HIPCHK(hipMalloc((void**)&c->d_frames, sizeof(MptFrame) * FRAME_RING));
+    HIPCHK(hipHostMalloc((void**)&c->h_frames, sizeof(MptFrame) * (FRAME_RING + 1)));
+    HIPCHK(hipMalloc((void**)&c->d_frames, sizeof(MptFrame) * (FRAME_RING + 1)));   // + the graph's frame
     HIPCHK(c->counters.alloc(2 * CTR_COUNT));   // second set: the second half of an overlapped batch
     HIPCHK(hipMemsetAsync(c->counters.p, 0, 2 * CTR_COUNT * sizeof(int32_t), c->stream));
     HIPCHK(c->fetch_raw.alloc(4));
@@ -893,6 +902,7 @@ int mpt_create(int device, void* hip_stream, MptContext** out) {
     if (const char* e = std::getenv("MPT_ADAPTIVE_BATCH")) c->adaptive_batch = std::atoi(e);
     if (const char* e = std::getenv("MPT_MAT_PRIVATE")) c->mat_private = std::atoi(e);
     if (const char* e = std::getenv("MPT_RESTIR_OVERLAP")) c->restir_overlap = std::atoi(e);
+    if (const char* e = std::getenv("MPT_GRAPHS")) c->graphs = std::atoi(e);
     if (const char* e = std::getenv("MPT_RESTIR_MAX_BATCH"))
         c->restir_max_batch = std::max(1, std::min(RESTIR_MAX_BATCH, std::atoi(e)));
     if (const char* e = std::getenv("MPT_SHADE_GLASS")) c->shade_glass = std::atoi(e);
@@ -929,6 +939,7 @@ int mpt_destroy(MptContext* c) {
         for (int k = 0; k < 2; k++)
             if (c->ev_frame[p][k]) (void)hipEventDestroy(c->ev_frame[p][k]);
     }
+    if (c->graph_exec) (void)hipGraphExecDestroy(c->graph_exec);
     if (c->h_frames) (void)hipHostFree(c->h_frames);
     if (c->h_reproj) (void)hipHostFree(c->h_reproj);
     if (c->d_frames) (void)hipFree(c->d_frames);
@@ -1281,6 +1292,61 @@ static int ensure_overlap(MptContext* c) {
 
 static int join_waves(MptContext* c);
 
+// The graph path of a one-sample path-tracing launch set (MptContext::graphs): (re)captured when
+// the key changes, then replayed with the frame copied into the graph's fixed slot.
+static hipError_t launch_frame_graph(MptContext* c, const DevPaths& P, const MptFrame* f, int slot, LaunchCfg& cfg) {
+    const DevScene S = dev_scene(c);
+    MptFrame k = *f;   // the fields the kernels read from the frame, not the host
+    k.random_seed = 0;
+    k.camera_random_seed = 0;
+    std::memset(k.restir_di_seeds, 0, sizeof(k.restir_di_seeds));
+    std::memset(&k.current_camera, 0, sizeof(MptCamera));
+    std::memset(&k.prev_camera, 0, sizeof(MptCamera));
+    k.render_settings.sample_number = 0;
+    k.render_settings.denoiser_AOV_accumulation_counter = 0;
+    k.render_settings.need_to_reset = false;
+    k.render_settings.do_update_status_buffers = false;
+    const int flags[9] = {cfg.grid_persistent, cfg.stats, cfg.shade_classes, cfg.light_bvh, cfg.light_static,
+                          cfg.restir_staged, cfg.shade_glass, cfg.shade_split, cfg.mat_private};
+    std::vector<uint8_t> key(sizeof(k) + sizeof(S) + sizeof(P) + sizeof(flags));
+    uint8_t* q = key.data();
+    std::memcpy(q, &k, sizeof(k)); q += sizeof(k);
+    std::memcpy(q, &S, sizeof(S)); q += sizeof(S);
+    std::memcpy(q, &P, sizeof(P)); q += sizeof(P);
+    std::memcpy(q, flags, sizeof(flags));
+    MptFrame* d_fixed = c->d_frames + FRAME_RING;
+    hipError_t e = hipMemcpyAsync(d_fixed, c->h_frames + slot, sizeof(MptFrame), hipMemcpyHostToDevice, c->stream);
+    if (e != hipSuccess) return e;
+    if (!c->graph_exec || key != c->graph_key) {
+        if (c->graph_exec) { (void)hipGraphExecDestroy(c->graph_exec); c->graph_exec = nullptr; }
+        hipGraph_t g = nullptr;
+        e = hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal);
+        if (e != hipSuccess) return e;
+        LaunchCfg gc = cfg;
+        gc.launches = 0;
+        const hipError_t le = launch_frame(S, P, d_fixed, *f, gc, c->stream);
+        e = hipStreamEndCapture(c->stream, &g);
+        if (le != hipSuccess || e != hipSuccess) {
+            if (g) (void)hipGraphDestroy(g);
+            (void)hipGetLastError();
+            c->graphs = 0;   // not capturable here: launch directly from now on
+            return launch_frame(S, P, c->d_frames + slot, *f, cfg, c->stream);
+        }
+        e = hipGraphInstantiate(&c->graph_exec, g, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(g);
+        if (e != hipSuccess) {
+            c->graph_exec = nullptr;
+            (void)hipGetLastError();
+            c->graphs = 0;
+            return launch_frame(S, P, c->d_frames + slot, *f, cfg, c->stream);
+        }
+        c->graph_key = std::move(key);
+        c->graph_launches = gc.launches;
+    }
+    cfg.launches += c->graph_launches;
+    return hipGraphLaunch(c->graph_exec, c->stream);
+}
+
 // Enqueues a prepared wavefront (prepare_batch).
 static int launch_batch(MptContext* c, const MptFrame* f, int batch) {
     const bool restir_part = f->options.direct_light_sampling == MPT_LSS_RESTIR_DI && f->band_count > 1;
@@ -1404,6 +1470,8 @@ static int launch_batch(MptContext* c, const MptFrame* f, int batch) {
         } else {
             e = launch_frames_restir(dev_scene(c), P, c->d_frames + slot, c->h_frames + slot, batch, cfg, c->stream);
         }
+    } else if (batch == 1 && c->graphs && !c->timing && f->options.direct_light_sampling != MPT_LSS_RESTIR_DI) {
+        e = launch_frame_graph(c, P, f, slot, cfg);
     } else {
         e = launch_frame(dev_scene(c), P, c->d_frames + slot, *f, cfg, c->stream);
     }
