@@ -556,8 +556,10 @@ def run_workload(a, world, rank, local, dist, coll_dev, quiet=False):
         r.render_samples(fr1, max_batch=1)
         r.synchronize_kernel()
         dt1 = time.perf_counter() - t1
+        st1 = r.stats()
         batch1 = {"steps": n1, "ms_per_step": round(dt1 * 1e3 / n1, 4),
-                  "vs_batched": round((dt1 / n1) / (elapsed / K), 3), "batched_samples_per_launch": batch}
+                  "vs_batched": round((dt1 / n1) / (elapsed / K), 3), "batched_samples_per_launch": batch,
+                  "graph_replays": int(st1.graph_replays), "graph_captures": int(st1.graph_captures)}
 
     # rooflines (SURVEY.md §8d algorithmic bytes): every traversal stage and the shade
     # kernel; "roofline" is the one with the largest summed time in the timed region

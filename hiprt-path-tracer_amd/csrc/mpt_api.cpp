@@ -124,6 +124,7 @@ struct MptContext {
     hipGraphExec_t graph_exec = nullptr;
     std::vector<uint8_t> graph_key;
     uint32_t graph_launches = 0;
+    uint32_t graph_captures = 0, graph_replays = 0;   // since mpt_enable_stats (MptStats)
     int num_cus = 256;
     int grid = 1024;
     // scene
@@ -1342,8 +1343,10 @@ static hipError_t launch_frame_graph(MptContext* c, const DevPaths& P, const Mpt
         }
         c->graph_key = std::move(key);
         c->graph_launches = gc.launches;
+        c->graph_captures++;
     }
     cfg.launches += c->graph_launches;
+    c->graph_replays++;
     return hipGraphLaunch(c->graph_exec, c->stream);
 }
 
@@ -2015,6 +2018,7 @@ int mpt_enable_stats(MptContext* c, int enable, int instrumented) {
     c->trace_launches = 0;
     c->frames = 0;
     c->frame_ms = 0.0;
+    c->graph_captures = c->graph_replays = 0;
     for (int m = 0; m < KT_COUNT; m++) { c->stage_ms[m] = 0.0; c->stage_launches[m] = 0; }
     HIPCHK(hipMemsetAsync(c->stats.p, 0, N_STATS * sizeof(uint64_t), c->stream));
     HIPCHK(hipMemsetAsync(c->ray_counts.p, 0, N_RAY_COUNTS * sizeof(uint64_t), c->stream));
@@ -2072,6 +2076,8 @@ int mpt_get_stats(MptContext* c, MptStats* out) {
     out->trace_launches = c->trace_launches;
     out->frames = c->frames;
     out->frame_ms = c->frame_ms;
+    out->graph_captures = c->graph_captures;
+    out->graph_replays = c->graph_replays;
     return MPT_OK;
 }
 

@@ -226,6 +226,44 @@ struct Trav {
                 uint32_t meta0 = __float_as_uint(n1.z), meta1 = __float_as_uint(n1.w);
                 uint32_t hit_internal = 0u;   // k-ordered
                 uint32_t hit_tris = 0u;       // triangle offsets from the node's tri_base
+#ifdef MPT_TRAV_PK
+                // children in pairs: the near/far plane distances through packed fp32 FMA and the
+                // far-distance widening through packed multiply (v_pk_fma_f32 / v_pk_mul_f32: two
+                // IEEE operations per instruction, the same bits as the scalar forms)
+                typedef float pf2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+                for (int c2 = 0; c2 < 8; c2 += 2) {
+                    float tn2[2], tf2[2];
+#pragma unroll
+                    for (int j = 0; j < 2; j++) {
+                        const int c = c2 + j;
+                        const pf2 qx = {(float)qbyte(nx0, nx1, c), (float)qbyte(fx0, fx1, c)};
+                        const pf2 qy = {(float)qbyte(ny0, ny1, c), (float)qbyte(fy0, fy1, c)};
+                        const pf2 qz = {(float)qbyte(nz0, nz1, c), (float)qbyte(fz0, fz1, c)};
+                        const pf2 px = __builtin_elementwise_fma(qx, (pf2){cx, cx}, (pf2){ax, ax});
+                        const pf2 py = __builtin_elementwise_fma(qy, (pf2){cy, cy}, (pf2){ay, ay});
+                        const pf2 pz = __builtin_elementwise_fma(qz, (pf2){cz, cz}, (pf2){az, az});
+                        tn2[j] = fmaxf(fmaxf(px.x, py.x), fmaxf(pz.x, 0.0f));
+                        tf2[j] = fminf(fminf(px.y, py.y), fminf(pz.y, best));
+                    }
+                    const pf2 tfw = (pf2){tf2[0], tf2[1]} * (pf2){1.0000009f, 1.0000009f};
+#pragma unroll
+                    for (int j = 0; j < 2; j++) {
+                        const int c = c2 + j;
+                        bool h = tn2[j] <= tfw[j];
+                        bool internal = (imask >> c) & 1u;
+                        if (h && internal) hit_internal |= 1u << (c ^ xr);
+                        // leaf: count (meta >> 5) triangles from offset (meta & 31).  Internal slots
+                        // hold their rank (< 8) and empty slots 0, so their count field is 0 and
+                        // the mask is empty without testing the internal bit: one v_bfm_b32
+                        // (offset from the low 5 bits of its operand) builds the range
+                        const uint32_t mw = c < 4 ? meta0 : meta1, msh = 8u * (c & 3);
+                        uint32_t lm;
+                        asm("v_bfm_b32 %0, %1, %2" : "=v"(lm) : "v"((mw >> (msh + 5u)) & 7u), "v"(mw >> msh));
+                        if (h) hit_tris |= lm;
+                    }
+                }
+#else
 #pragma unroll
                 for (int c = 0; c < 8; c++) {
                     float tnx = fmaf((float)qbyte(nx0, nx1, c), cx, ax), tfx = fmaf((float)qbyte(fx0, fx1, c), cx, ax);
@@ -240,6 +278,7 @@ struct Trav {
                     // leaf: count (meta >> 5) triangles from offset (meta & 31); empty slots have meta 0
                     if (h && !internal) hit_tris |= ((1u << (meta >> 5)) - 1u) << (meta & 31u);
                 }
+#endif
                 if (hit_tris) {
                     // the current triangle group is empty here (popped groups go straight to the loop)
                     tbase = __float_as_uint(n1.y);

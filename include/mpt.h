@@ -442,6 +442,9 @@ typedef struct MptStats {
     double restir_eval_ms;
     uint32_t restir_eval_launches;
     uint64_t restir_eval_items;
+    /* one-sample launch sets (MPT_GRAPHS): captured HIP graphs and replays of them */
+    uint32_t graph_captures;
+    uint32_t graph_replays;
 } MptStats;
 
 #define MPT_FB_COLOR 0        /* 'pixels': running SUM of samples (RenderData.h:34-36) */

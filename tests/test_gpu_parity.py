@@ -457,6 +457,12 @@ def test_graph_replay_equals_direct_launches(scenes, luts, monkeypatch):
             r.render(f)
         r.synchronize_kernel()
         out[mode] = [r.framebuffer(k) for k in (abi.FB_COLOR, abi.FB_ALBEDO, abi.FB_NORMALS)]
+        st = r.stats()
+        if mode == "graph":   # the graph path really ran: re-captured per launch-set change only
+            assert st.graph_replays == len(frs) and 1 <= st.graph_captures < len(frs), \
+                (st.graph_captures, st.graph_replays)
+        else:
+            assert st.graph_replays == 0
         r.close()
     for g, d in zip(out["graph"], out["direct"]):
         assert np.array_equal(g, d), f"{(g != d).sum()} values differ"

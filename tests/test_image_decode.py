@@ -133,3 +133,19 @@ def test_jpeg_undefined_tables_are_deterministic():
         except mpt.MptError as e:
             outcomes.append(str(e))
     assert outcomes[0] == outcomes[1] == outcomes[2]
+
+
+@pytest.mark.gpu
+def test_every_stb_fixture_on_the_gpu_box():
+    """The decode fixtures again inside the GPU run (the driver records that run): every committed
+    input decodes byte for byte as the reference's stb_image did (host code of libmpt)."""
+    bad = []
+    for key in sorted(DECODES):
+        name, mode, req, flip = key.split("|")
+        got = _decode(name, mode, int(req), int(flip))
+        want = DECODES[key]
+        same = got.shape == want.shape and (np.array_equal(got.view(np.uint32), want.view(np.uint32)) if mode == "f32"
+                                            else np.array_equal(got, want))
+        if not same:
+            bad.append(key)
+    assert not bad and len(DECODES) > 300, bad[:5]
