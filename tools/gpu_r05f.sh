@@ -17,3 +17,4 @@ for l in open('$o/$w.jsonl'):
     j = json.loads(l); k = j['kernels']
     print('$w', j['lib'].split('/')[-2], j['ms_per_step'], 'trace', k['trace_path'], k['trace_nee_any'], k['trace_nee_closest'])"; done
 python -c "import json; print(json.load(open('$o/c3_batch1.json'))['batch1'])"
+bash tools/gpu_r05g.sh
