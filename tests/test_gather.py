@@ -82,3 +82,77 @@ def test_comm_gather_one_rank(cornell, luts):
     assert np.array_equal(got, want)
     got_alb = r.comm_gather(root=0, kind=abi.FB_ALBEDO)
     assert np.array_equal(got_alb, r.framebuffer(abi.FB_ALBEDO))
+
+
+def _n_devices():
+    import torch
+    return torch.cuda.device_count()
+
+
+@pytest.mark.gpu
+def test_gather_across_devices(cornell, luts):
+    """mpt_gather with the bands on different GPUs (peer copies after hipDeviceEnablePeerAccess);
+    needs two GPUs -- skipped on a one-GPU box, where the tests above put every band on device 0."""
+    import mpt
+    from mpt import abi
+    nd = _n_devices()
+    if nd < 2:
+        pytest.skip("one GPU")
+    lss = abi.LSS_MIS_LIGHT_BSDF
+    ref = _renderer(cornell, luts)
+    ref.render_samples(_frames(cornell, (1, 0, 1), lss))
+    ref.synchronize_kernel()
+    want = ref.framebuffer(abi.FB_COLOR)
+    parts = []
+    for k in range(3):
+        r = mpt.GPURenderer(k % nd)
+        r.set_scene(cornell)
+        r.set_luts(luts)
+        r.render_samples(_frames(cornell, (8, k, 3), lss))
+        parts.append(r)
+    got = mpt.gather(parts, root=1, kind=abi.FB_COLOR)
+    assert np.array_equal(got, want)
+
+
+def _comm_rank(rank, n, uid_q, out_q):
+    import mpt
+    from mpt import abi, scene
+    sd = scene.load_scene("cornell_pbr")
+    r = mpt.GPURenderer(rank)
+    r.set_scene(sd)
+    r.set_luts(scene.load_luts())
+    r.render_samples(_frames(sd, (8, rank, n), abi.LSS_MIS_LIGHT_BSDF))
+    r.synchronize_kernel()
+    if rank == 0:
+        uid = mpt.comm_unique_id()
+        for _ in range(n - 1):
+            uid_q.put(uid)
+    else:
+        uid = uid_q.get(timeout=60)
+    r.comm_init(n, rank, uid)
+    got = r.comm_gather(root=0, kind=abi.FB_COLOR)
+    out_q.put((rank, got if rank == 0 else None))
+
+
+@pytest.mark.gpu
+def test_comm_gather_two_processes(cornell, luts):
+    """mpt_comm_gather over a two-rank RCCL communicator, one process per GPU (the process-per-GPU
+    host's output path); needs two GPUs -- skipped on a one-GPU box."""
+    import multiprocessing as mp
+    from mpt import abi
+    if _n_devices() < 2:
+        pytest.skip("one GPU")
+    ref = _renderer(cornell, luts)
+    ref.render_samples(_frames(cornell, (1, 0, 1), abi.LSS_MIS_LIGHT_BSDF))
+    ref.synchronize_kernel()
+    want = ref.framebuffer(abi.FB_COLOR)
+    ctx = mp.get_context("spawn")
+    uid_q, out_q = ctx.Queue(), ctx.Queue()
+    ps = [ctx.Process(target=_comm_rank, args=(k, 2, uid_q, out_q)) for k in range(2)]
+    for p in ps:
+        p.start()
+    res = dict(out_q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert np.array_equal(res[0], want)
