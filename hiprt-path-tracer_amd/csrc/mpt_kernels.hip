@@ -109,6 +109,12 @@ DEV float alpha_uniform(uint32_t key, int prim) {
 }
 DEV bool alpha_rejects(const DevScene& S, int prim, float u, float v, uint32_t key);
 
+// The node test's children in pairs through packed fp32 arithmetic and v_bfm leaf ranges (264 -> 220
+// VALU per 8-child node; C3 path rays -1.5 %, shadow rays -2.3 %, C5 path rays -1.8 %:
+// profiles/r05f_*_trav_pk_ab.jsonl); 0: the scalar loop
+#ifndef MPT_TRAV_PK
+#define MPT_TRAV_PK 1
+#endif
 DEV uint32_t qbyte(uint32_t w0, uint32_t w1, int s) { return ((s < 4 ? w0 : w1) >> ((s & 3) * 8)) & 0xffu; }
 
 // Resumable BVH8 traversal of one ray: init() sets it up, run() opens nodes until the
@@ -226,7 +232,7 @@ struct Trav {
                 uint32_t meta0 = __float_as_uint(n1.z), meta1 = __float_as_uint(n1.w);
                 uint32_t hit_internal = 0u;   // k-ordered
                 uint32_t hit_tris = 0u;       // triangle offsets from the node's tri_base
-#ifdef MPT_TRAV_PK
+#if MPT_TRAV_PK
                 // children in pairs: the near/far plane distances through packed fp32 FMA and the
                 // far-distance widening through packed multiply (v_pk_fma_f32 / v_pk_mul_f32: two
                 // IEEE operations per instruction, the same bits as the scalar forms)

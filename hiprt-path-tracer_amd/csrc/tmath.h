@@ -4,19 +4,23 @@
 //
 // The reference calls float libm (sinf, cosf, expf, logf, powf, atan2f, asinf, acosf via
 // hippt::, HostDeviceCommon/Math.h:141-229) on the CPU and the device library's float
-// functions on the GPU; neither is reproducible on the other.  Here each function
-// evaluates a short double-precision approximation of the float argument (relative error
-// below 1e-14: Cody-Waite reduction + truncated series whose tail is < 1e-16) and rounds
-// it once to float, so the result is the correctly rounded float except within ~1e-14 of
-// a rounding tie -- at most 1 ulp from glibc's functions, which are correctly rounded in
-// nearly all cases too.  Only IEEE double +, -, *, /, sqrt, rint, frexp and ldexp are used
-// (exact or correctly rounded on x86-64 and gfx950 alike; compile both sides with
-// -ffp-contract=off).  Arguments outside the reduced ranges (huge, infinite, NaN, zero,
-// non-positive for log / pow, results beyond the float range) go to the platform's double
-// libm, whose special values are exact.
-//
-// On the GPU this replaces out-of-line calls of the device library's double functions
-// (function-call register saves, scratch spills, ~3x the f64 operations).
+// functions on the GPU; neither is reproducible on the other.  Here every function is one
+// fixed sequence of IEEE operations (+, -, *, /, sqrt, fma, rint, frexp, ldexp: exact or
+// correctly rounded on x86-64 and gfx950 alike; both sides compiled with -ffp-contract=off),
+// so the oracle and the kernels agree bit for bit:
+// * sin / cos / exp / log / atan2 / asin / acos (MPT_TMATH_F32, the default): single
+//   precision -- Cody-Waite reductions (sin / cos: in double) and the Cephes single-precision minimax
+//   polynomials (Horner in fmaf) -- within 2 ulp of the correctly rounded float for sin /
+//   cos, 1 for exp / log, 3 for atan2, 4 for asin / acos (tests/test_tmath.py), the accuracy
+//   class of the device library's float functions the reference's GPU build calls;
+// * pow, and every function with MPT_TMATH_F32=0: a short double-precision approximation of
+//   the float argument (relative error below 1e-14: Cody-Waite reduction + truncated series
+//   whose tail is < 1e-16) rounded once to float -- the correctly rounded float except within
+//   ~1e-14 of a rounding tie.
+// Arguments outside the reduced ranges (huge, infinite, NaN, zero, non-positive for log /
+// pow, results beyond or below the normal float range) go to the platform's double libm,
+// whose special values are exact.  The single-precision functions cut C3's shading time by
+// 4.5 % against the double ones (profiles/r05g_c3_tmath_f32_ab.jsonl).
 #ifndef MPT_TMATH_H
 #define MPT_TMATH_H
 
@@ -26,6 +30,13 @@
 #define TM_FN __host__ __device__ static inline
 #else
 #define TM_FN static inline
+#endif
+
+// MPT_TMATH_F32 (default 1): sin / cos / exp / log / atan2 / asin / acos in single precision
+// (below); 0: every function through the double-precision approximations.  pow stays double
+// either way (y ln x needs more than float's precision for large exponents).
+#ifndef MPT_TMATH_F32
+#define MPT_TMATH_F32 1
 #endif
 
 namespace tmath {
@@ -89,14 +100,11 @@ TM_FN double log_d(double x) {
     const double lm = 2.0 * s + 2.0 * s * p;
     return (double)e * LN2_HI + ((double)e * LN2_LO + lm);
 }
-#ifdef MPT_TMATH_F32
-// ---- single precision: Cody-Waite reduction in three parts + the Cephes single-precision
-// minimax polynomials, fmaf Horner (one IEEE fma per step on x86-64 libm and gfx950 alike).
+#if MPT_TMATH_F32
+// ---- single precision: Cody-Waite reductions + the Cephes single-precision minimax
+// polynomials, fmaf Horner (one IEEE fma per step on x86-64 libm and gfx950 alike).
 // Results within 1-2 ulp of the correctly rounded float; the ranges outside the reductions go
 // to the platform's double libm as above.
-constexpr float F_PIO2_1 = 1.5703125f;                  // 8 bits: k F_PIO2_1 exact for |k| < 2^16
-constexpr float F_PIO2_2 = 4.837512969970703125e-4f;
-constexpr float F_PIO2_3 = 7.54978995489188216e-8f;
 constexpr float F_INV_PIO2 = 0.636619772367581343f;
 constexpr float F_LN2_HI = 0.693359375f;
 constexpr float F_LN2_LO = -2.12194440e-4f;
@@ -112,27 +120,31 @@ TM_FN float cos_kernel_f(float r) {
     return fmaf(fmaf(fmaf(2.443315711809948e-5f, z, -1.388731625493765e-3f), z, 4.166664568298827e-2f) * z, z,
                 fmaf(-0.5f, z, 1.0f));
 }
+// x = k pi/2 + r: k from float, the reduction itself in double (two products and two
+// differences, as reduce_pio2) so that r keeps its relative accuracy next to the zeros of sin /
+// cos, where a float Cody-Waite reduction loses up to 3 digits
 TM_FN int reduce_pio2_f(float x, float& r) {
     const float k = rintf(x * F_INV_PIO2);
-    r = fmaf(-k, F_PIO2_3, fmaf(-k, F_PIO2_2, fmaf(-k, F_PIO2_1, x)));
+    const double kd = (double)k;
+    r = (float)(((double)x - kd * PIO2_HI) - kd * PIO2_LO);
     return (int)k;
 }
 TM_FN float sinf_(float x) {
-    if (!(fabsf(x) <= 256.0f) || x == 0.0f) return (float)sin((double)x);
+    if (!(fabsf(x) <= 1.0e5f) || x == 0.0f) return (float)sin((double)x);
     float r;
     const int q = reduce_pio2_f(x, r) & 3;
     const float s = (q & 1) ? cos_kernel_f(r) : sin_kernel_f(r);
     return (q & 2) ? -s : s;
 }
 TM_FN float cosf_(float x) {
-    if (!(fabsf(x) <= 256.0f)) return (float)cos((double)x);
+    if (!(fabsf(x) <= 1.0e5f)) return (float)cos((double)x);
     float r;
     const int q = reduce_pio2_f(x, r) & 3;
     const float c = (q & 1) ? sin_kernel_f(r) : cos_kernel_f(r);
     return (q == 1 || q == 2) ? -c : c;
 }
 TM_FN void sincosf_(float x, float& sf, float& cf) {
-    if (!(fabsf(x) <= 256.0f)) { sf = (float)sin((double)x); cf = (float)cos((double)x); return; }
+    if (!(fabsf(x) <= 1.0e5f)) { sf = (float)sin((double)x); cf = (float)cos((double)x); return; }
     float r;
     const int q = reduce_pio2_f(x, r) & 3;
     const float sk = sin_kernel_f(r), ck = cos_kernel_f(r);
@@ -220,7 +232,7 @@ TM_FN float powf_(float xf, float yf) {
     return (float)exp_d(t);
 }
 
-#ifdef MPT_TMATH_F32
+#if MPT_TMATH_F32
 // atan t, t in [0, inf) finite: Cephes atanf's reduction by tan(3pi/8) / tan(pi/8)
 TM_FN float atan_f(float t) {
     float y = 0.0f, u = t;

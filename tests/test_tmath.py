@@ -1,9 +1,11 @@
 """The transcendental layer shared by the HIP kernels and the oracle (csrc/tmath.h).
 
-CPU: every function equals the correctly rounded float of the platform's double libm
+CPU: every function against the correctly rounded float of the platform's double libm
 (numpy's float64 ufuncs call it) on random arguments over the ranges the path tracer uses
-and beyond, within 1 ulp everywhere incl. the special values -- the reference's own CPU
-build calls glibc's float functions, which are correctly rounded in nearly all cases.
+and beyond, incl. the special values: the single-precision functions (sin, cos, exp, log,
+atan2, asin, acos) within their stated ulp bounds -- the accuracy class of the device library's
+float functions the reference's GPU build calls -- and pow, still evaluated in double, within 1
+ulp and off by one essentially never.
 GPU: libmpt's device build of the same code equals the oracle's bit for bit."""
 import math
 
@@ -11,6 +13,8 @@ import numpy as np
 import pytest
 
 FNS = ["sin", "cos", "exp", "log", "pow", "atan2", "asin", "acos"]
+# max ulps from the correctly rounded float (tmath.h: single precision but for pow)
+ULP_BOUND = {"sin": 2, "cos": 2, "exp": 1, "log": 1, "pow": 1, "atan2": 3, "asin": 4, "acos": 4}
 REF = {"sin": lambda a, b: np.sin(a), "cos": lambda a, b: np.cos(a), "exp": lambda a, b: np.exp(a),
        "log": lambda a, b: np.log(a), "pow": lambda a, b: np.power(a, b), "atan2": lambda a, b: np.arctan2(a, b),
        "asin": lambda a, b: np.arcsin(a), "acos": lambda a, b: np.arccos(a)}
@@ -64,9 +68,13 @@ def test_tmath_correctly_rounded(oracle_lib, fn, name):
     nan = np.isnan(exp)
     assert np.array_equal(np.isnan(got), nan), name
     d = ulps(got[~nan], exp[~nan])
-    assert d.max() <= 1, (name, int(d.max()))
-    # off by one only within ~1e-14 of a rounding tie: essentially never
-    assert np.count_nonzero(d) <= 5, (name, int(np.count_nonzero(d)))
+    assert d.max() <= ULP_BOUND[name], (name, int(d.max()))
+    if name == "pow":
+        # double precision: off by one only within ~1e-14 of a rounding tie, essentially never
+        assert np.count_nonzero(d) <= 5, (name, int(np.count_nonzero(d)))
+    else:
+        # single precision: most results still correctly rounded
+        assert np.count_nonzero(d) <= 0.5 * len(d), (name, int(np.count_nonzero(d)))
 
 
 @pytest.mark.gpu
