@@ -210,6 +210,15 @@ struct MptContext {
     DBuf<uint8_t> rq_occ;
     DBuf<int32_t> rq_list, rq_items;
     DBuf<int4> rq_meta;
+    // chunked ReSTIR DI initial candidates (launch_frames_restir, LaunchCfg::ci_planes): the
+    // G-buffer, initial reservoirs and presampled lights of up to restir_chunk samples
+    int restir_chunk = 1;                 // MPT_RESTIR_CHUNK: samples per chunk (-1: by the band's pixels)
+    int ci_chunk = 1;                     // the chunk the planes below are sized for
+    DBuf<float4> ci_pos, ci_sn, ci_gn, ci_view, ci_cs, ci_rs, ci_pl;
+    DBuf<int4> ci_meta;
+    DBuf<uint4> ci_vsA, ci_vsB;
+    DBuf<MptMaterial> ci_mat;
+    DevPaths ci_dp{};
     int restir_out_sp2 = 0;
     MptHaloExchangeFn halo_fn = nullptr;   // ReSTIR DI across a row partition
     void* halo_user = nullptr;
@@ -632,7 +641,9 @@ int build_light_bvh(MptContext* c) {
 void release_restir(MptContext* c) {
     release_all(c->gb_pos, c->gb_sn, c->gb_gn, c->gb_view, c->pgb_pos, c->pgb_sn, c->pgb_gn, c->pgb_view, c->gb_meta,
                 c->pgb_meta, c->gb_vsA, c->gb_vsB, c->pgb_vsA, c->pgb_vsB, c->gb_mat, c->pgb_mat, c->gb_cs, c->pgb_cs, c->rs_init, c->rs_sp1,
-                c->rs_sp2, c->rs_plights, c->rs_keep, c->rs_conv, c->rq_o, c->rq_d, c->rq_rec, c->rq_key, c->rq_occ, c->rq_list, c->rq_items, c->rq_meta);
+                c->rs_sp2, c->rs_plights, c->rs_keep, c->rs_conv, c->rq_o, c->rq_d, c->rq_rec, c->rq_key, c->rq_occ, c->rq_list, c->rq_items, c->rq_meta,
+                c->ci_pos, c->ci_sn, c->ci_gn, c->ci_view, c->ci_cs, c->ci_rs, c->ci_pl, c->ci_meta, c->ci_vsA, c->ci_vsB, c->ci_mat);
+    c->ci_chunk = 1;
     c->restir_out_sp2 = 0;
 }
 
@@ -674,13 +685,35 @@ int ensure_restir(MptContext* c, const MptFrame* f) {
         if (A.e == hipSuccess) A(hipMemsetAsync(c->rs_conv.p, 0xff, N * sizeof(int32_t), st));
     }
     if (c->restir_staged) {
-        // staged reuse passes: per pixel slot of the partition (ReSTIR frames trace one sample)
+        // staged reuse passes: per pixel slot of the partition (ReSTIR frames trace one sample).
+        // A chunk of samples' initial candidates (launch_frames_restir) stages one ray position
+        // per (sample, pixel) item -- up to RS_RPP samples -- and two records and a metadata entry
+        // per item; its G-buffer / reservoir / light planes are the ci_* buffers.  The chunk
+        // follows the band's size: ~4 M items, so that a small band's launches fill the GPU and a
+        // whole frame's stay as they are (1080p: 2 samples)
         const size_t ns = (size_t)std::max(c->n_slots, 1);
-        if (c->rq_meta.n != ns) {
+        int ck = c->restir_chunk >= 0 ? c->restir_chunk : (int)std::max<size_t>(1, ((size_t)4 << 20) / ns);
+        ck = std::max(1, std::min(ck, RS_RPP_HOST));
+        if (c->rq_o.n != ns * RS_RPP_HOST) {
             A(c->rq_o, ns * RS_RPP_HOST); A(c->rq_d, ns * RS_RPP_HOST); A(c->rq_key, ns * RS_RPP_HOST);
             A(c->rq_occ, ns * RS_RPP_HOST); A(c->rq_list, ns * RS_RPP_HOST); A(c->rq_items, 2 * ns * RS_RPP_HOST);
-            A(c->rq_meta, ns); A(c->rq_rec, ns * RS_REC_HOST);
         }
+        if (c->rq_meta.n != ns * ck) {
+            A(c->rq_meta, ns * ck); A(c->rq_rec, ns * std::max(RS_REC_HOST, 2 * ck));
+        }
+        const bool mat = c->any_tex || f->bsdf_flags.white_furnace_mode;
+        if (ck > 1 && (c->ci_chunk != ck || c->ci_pos.n != ns * ck || (mat && c->ci_mat.n != ns * ck))) {
+            const size_t m = ns * ck;
+            A(c->ci_pos, m); A(c->ci_sn, m); A(c->ci_gn, m); A(c->ci_view, m); A(c->ci_meta, m);
+            A(c->ci_vsA, m); A(c->ci_vsB, m); A(c->ci_cs, 4 * m); A(c->ci_rs, 3 * m);
+            if (mat) A(c->ci_mat, m);
+        }
+        if (ck > 1 && c->ci_pl.n != 4 * npl * ck) A(c->ci_pl, 4 * npl * ck);
+        c->ci_chunk = ck;
+        DevPaths& d = c->ci_dp;
+        d.gb_pos = c->ci_pos.p; d.gb_sn = c->ci_sn.p; d.gb_gn = c->ci_gn.p; d.gb_view = c->ci_view.p; d.gb_meta = c->ci_meta.p;
+        d.gb_vsA = c->ci_vsA.p; d.gb_vsB = c->ci_vsB.p; d.gb_mat = c->ci_mat.p; d.gb_cs = c->ci_cs.p;
+        d.rs_init = c->ci_rs.p; d.rs_plights = c->ci_pl.p;
     }
     if (c->rs_plights.n != 4 * npl) {
         A(c->rs_plights, 4 * npl);
@@ -906,6 +939,7 @@ int mpt_create(int device, void* hip_stream, MptContext** out) {
     if (const char* e = std::getenv("MPT_GRAPHS")) c->graphs = std::atoi(e);
     if (const char* e = std::getenv("MPT_RESTIR_MAX_BATCH"))
         c->restir_max_batch = std::max(1, std::min(RESTIR_MAX_BATCH, std::atoi(e)));
+    if (const char* e = std::getenv("MPT_RESTIR_CHUNK")) c->restir_chunk = std::atoi(e);
     if (const char* e = std::getenv("MPT_SHADE_GLASS")) c->shade_glass = std::atoi(e);
     if (const char* e = std::getenv("MPT_SHADE_SPLIT")) c->shade_split = std::atoi(e);
     if (const char* e = std::getenv("MPT_SHADE_TEXMETAL")) c->shade_texmetal = std::atoi(e);
@@ -1386,6 +1420,11 @@ static int launch_batch(MptContext* c, const MptFrame* f, int batch) {
     cfg.restir_out_sp2 = c->restir_out_sp2;
     cfg.shade_classes = c->shade_classes;
     cfg.restir_staged = c->restir_staged;
+    if (c->ci_chunk > 1 && c->ci_pos.p && c->ci_pl.n >= 4 * (size_t)std::max(1, f->render_settings.restir_di_settings.number_of_subsets *
+                                                                                     f->render_settings.restir_di_settings.subset_size) * c->ci_chunk) {
+        cfg.ci_chunk = c->ci_chunk;
+        cfg.ci_planes = &c->ci_dp;
+    }
     cfg.shade_glass = c->shade_glass;
     cfg.shade_split = c->shade_split;
     cfg.mat_private = c->mat_private >= 0 ? (c->mat_private != 0) : (c->tex_tri_frac >= 0.25);

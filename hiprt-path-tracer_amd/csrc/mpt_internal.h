@@ -197,6 +197,13 @@ struct DevPaths {
     // [rs_lo, rs_hi) = the pixels of the band plus its halo rows (what frame_begin maintains).
     int32_t pix_off;
     int32_t rs_lo, rs_hi;
+    // ReSTIR DI initial candidates of a chunk of samples in one launch set (launch_frames_restir):
+    // ci_n > 0 = the band's pixels per sample; item s of the launch is pixel s % ci_n of the
+    // chunk's sample s / ci_n, its frame Fp[s / ci_n]; the G-buffer / rs_init / rs_plights
+    // pointers are the chunk's planes, indexed by item (pix_off 0), and ci_pix_off is the band's
+    // first pixel (seeds, coordinates)
+    int32_t ci_n;
+    int32_t ci_pix_off;
     int32_t* rs_conv;         // pixel_converged_sample_count by pixel (== as_conv when unpartitioned)
     // extended light sampling (NF_EXT), sized by the frame's options; NULL / 0 otherwise
     int32_t x_per;            // entries per slot
@@ -307,6 +314,11 @@ struct LaunchCfg {
     hipStream_t wave_stream;
     uint32_t* wave_spill;
     hipEvent_t ev_chain;
+    // chunked ReSTIR DI initial candidates (launch_frames_restir): up to ci_chunk samples per
+    // chunk; ci_planes' G-buffer / rs_init / rs_plights pointers are the chunk's planes (NULL
+    // ci_planes or ci_chunk < 2: one sample's chain at a time)
+    int ci_chunk;
+    const DevPaths* ci_planes;
 };
 
 // Moves every per-slot pointer of P by `off` slots: a view of slots [off, off + P.n) of the

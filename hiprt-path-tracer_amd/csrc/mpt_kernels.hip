@@ -2801,42 +2801,18 @@ static void restir_empty_band(const MptFrame& hf, LaunchCfg& cfg, hipStream_t st
     cfg.halo_prev = cfg.halo_rows;
 }
 
-// ReSTIRDIRenderPass::launch (ReSTIRDIRenderPass.cpp:233-264) for the fused configuration:
-// presampling, initial candidates, fused spatiotemporal, (number_of_passes - 1) spatial
-// passes ping-ponging between the two spatial buffers; returns the output buffer in P.rs_out.
-// A partitioned context exchanges the halo of the G-buffer (after k_gbuffer) and of every
-// reservoir buffer a reuse pass reads at neighbours: the temporal input right before the
-// fused pass (so the final-shading write-through of the previous frame is included), then
-// each pass's output before the next pass.
-static void launch_restir(const DevScene& S, DevPaths& P, const MptFrame* d_frame, const MptFrame& hf, LaunchCfg& cfg,
+// Lights presampling and initial candidates (ReSTIRDIRenderPass.cpp:241-247) into P.rs_init: one
+// sample's, or a chunk's (DevPaths::ci_n: the chunk's planes, every item of every sample in each
+// launch)
+static void restir_initial(const DevScene& S, const DevPaths& P, const MptFrame* d_frame, const MptFrame& hf, LaunchCfg& cfg,
                           hipStream_t st) {
-    TimedScope ts(cfg, st, KT_RESTIR);
     const MptReSTIRDISettings& rd = hf.render_settings.restir_di_settings;
     const int ovr = hf.options.bsdf_override;
     const int n_pl = rd.number_of_subsets * rd.subset_size;
-    const int64_t RB = 3 * sizeof(float4);
-    if (cfg.halo_fn) {
-        // halo this context needs: its pixels' largest reprojection offset (measured by
-        // k_gbuffer) + the reuse radius + the temporal search / permutation extent
-        // (Utils.h:371-421); agreed over all contexts by the host's G-buffer exchange.  A frame
-        // whose camera did not move reprojects every hit onto its own (jittered) pixel, an offset
-        // of at most one row: every context then derives the same halo from the frame alone,
-        // without reading the measure back (no host synchronisation per sample)
-        const bool still = std::memcmp(&hf.current_camera, &hf.prev_camera, sizeof(MptCamera)) == 0;
-        int reproj = 2;
-        if (!still) {
-            hipMemcpyAsync(cfg.h_reproj, &P.counters[CTR_REPROJ], sizeof(int32_t), hipMemcpyDeviceToHost, st);
-            hipStreamSynchronize(st);
-            reproj = *cfg.h_reproj;
-        }
-        const int need = std::min(hf.res_y, reproj + std::max(0, rd.reuse_radius) + std::max(0, rd.neighbor_search_radius) + 8);
-        if (hf.render_settings.enable_adaptive_sampling)
-            hipLaunchKernelGGL(k_restir_conv, dim3(blocks_for(P.n)), dim3(TB), 0, st, P);
-        exchange_gbuffers(hf, cfg, st, P, need, still);
-    }
+    const int n_smp = P.ci_n ? P.n / P.ci_n : 1;
     if (hf.options.restir_di_do_lights_presampling) {   // ReSTIRDIRenderPass::launch (.cpp:241-242)
         TimedScope tk(cfg, st, KT_RS_PRESAMPLE);
-        hipLaunchKernelGGL(k_restir_presample, dim3((n_pl + TB - 1) / TB), dim3(TB), 0, st, S, P, d_frame);
+        hipLaunchKernelGGL(k_restir_presample, dim3((n_smp * n_pl + TB - 1) / TB), dim3(TB), 0, st, S, P, d_frame);
     }
     const dim3 g(cfg.grid_persistent);
     {
@@ -2866,6 +2842,42 @@ static void launch_restir(const DevScene& S, DevPaths& P, const MptFrame* d_fram
             hipLaunchKernelGGL(k_rs_visapply, gp, dim3(TB), 0, st, P, P.rs_init);
         }
     }
+}
+
+// ReSTIRDIRenderPass::launch (ReSTIRDIRenderPass.cpp:233-264) for the fused configuration:
+// presampling, initial candidates, fused spatiotemporal, (number_of_passes - 1) spatial
+// passes ping-ponging between the two spatial buffers; returns the output buffer in P.rs_out.
+// A partitioned context exchanges the halo of the G-buffer (after k_gbuffer) and of every
+// reservoir buffer a reuse pass reads at neighbours: the temporal input right before the
+// fused pass (so the final-shading write-through of the previous frame is included), then
+// each pass's output before the next pass.
+static void launch_restir(const DevScene& S, DevPaths& P, const MptFrame* d_frame, const MptFrame& hf, LaunchCfg& cfg,
+                          hipStream_t st, bool initial_done = false) {
+    TimedScope ts(cfg, st, KT_RESTIR);
+    const MptReSTIRDISettings& rd = hf.render_settings.restir_di_settings;
+    const int ovr = hf.options.bsdf_override;
+    const int64_t RB = 3 * sizeof(float4);
+    if (cfg.halo_fn) {
+        // halo this context needs: its pixels' largest reprojection offset (measured by
+        // k_gbuffer) + the reuse radius + the temporal search / permutation extent
+        // (Utils.h:371-421); agreed over all contexts by the host's G-buffer exchange.  A frame
+        // whose camera did not move reprojects every hit onto its own (jittered) pixel, an offset
+        // of at most one row: every context then derives the same halo from the frame alone,
+        // without reading the measure back (no host synchronisation per sample)
+        const bool still = std::memcmp(&hf.current_camera, &hf.prev_camera, sizeof(MptCamera)) == 0;
+        int reproj = 2;
+        if (!still) {
+            hipMemcpyAsync(cfg.h_reproj, &P.counters[CTR_REPROJ], sizeof(int32_t), hipMemcpyDeviceToHost, st);
+            hipStreamSynchronize(st);
+            reproj = *cfg.h_reproj;
+        }
+        const int need = std::min(hf.res_y, reproj + std::max(0, rd.reuse_radius) + std::max(0, rd.neighbor_search_radius) + 8);
+        if (hf.render_settings.enable_adaptive_sampling)
+            hipLaunchKernelGGL(k_restir_conv, dim3(blocks_for(P.n)), dim3(TB), 0, st, P);
+        exchange_gbuffers(hf, cfg, st, P, need, still);
+    }
+    if (!initial_done) restir_initial(S, P, d_frame, hf, cfg, st);
+    const dim3 g(cfg.grid_persistent);
     float4* last_out = restir_buffer(P, cfg.restir_out_sp2);
     // the reference-default weights run a kernel variant with the mode compiled in
     const bool def_bias = hf.options.restir_di_bias_correction_weights == MPT_RESTIR_DI_BIAS_PAIRWISE_MIS_DEFENSIVE &&
@@ -3143,7 +3155,33 @@ hipError_t launch_frames_restir(const DevScene& S, const DevPaths& PF, const Mpt
     // sample's shading: each sample's final reservoirs are kept (rs_keep) and bounce 0 runs
     // once over the batch, like the later bounces
     const bool defer = PF.rs_keep && hf[0].world_settings.ambient_light_type == MPT_AMBIENT_ENVMAP;
+    // Chunked initial candidates (deferred first bounce, staged initial pass): the G-buffer,
+    // lights presampling and initial candidates of up to ci_chunk samples -- which read no earlier
+    // sample's state -- as one launch set into the chunk's planes (cfg.ci_planes); each sample then
+    // merges its G-buffer and initial reservoirs into the context's planes (k_gb_merge /
+    // k_rs_merge: the stores the per-sample kernels make) before its reuse passes, in order.
+    const MptReSTIRDISettings& rd0 = hf[0].render_settings.restir_di_settings;
+    const int chunk = (defer && cfg.ci_planes && cfg.ci_chunk > 1 && cfg.restir_staged && PF.rq_o &&
+                       rd0.number_of_initial_bsdf_candidates <= 1 && !hf[0].options.restir_di_initial_target_visibility)
+                          ? std::min(cfg.ci_chunk, batch) : 1;
     for (int s = 0; s < batch; s++) {
+        if (chunk > 1 && s % chunk == 0) {
+            const int cn = std::min(chunk, batch - s);
+            DevPaths G = PF;
+            offset_slots(G, (size_t)s * n);
+            G.n = cn * n; G.batch = 1; G.group = 1;
+            G.pix_off = 0; G.ci_n = n; G.ci_pix_off = PF.pix_off;
+            const DevPaths& C = *cfg.ci_planes;
+            G.gb_pos = C.gb_pos; G.gb_sn = C.gb_sn; G.gb_gn = C.gb_gn; G.gb_view = C.gb_view; G.gb_meta = C.gb_meta;
+            G.gb_vsA = C.gb_vsA; G.gb_vsB = C.gb_vsB; G.gb_mat = C.gb_mat; G.gb_cs = C.gb_cs;
+            G.rs_init = C.rs_init; G.rs_plights = C.rs_plights;
+            {
+                TimedScope tk(cfg, st, KT_GBUFFER);
+                hipLaunchKernelGGL(k_gbuffer, dim3(blocks_for(G.n)), dim3(TB), 0, st, S, G, d_frames + s);
+            }
+            TimedScope ts(cfg, st, KT_RESTIR);
+            restir_initial(S, G, d_frames + s, hf[s], cfg, st);
+        }
         // sample s: frame_begin, G-buffer, the ReSTIR DI passes (which read sample s - 1's
         // reservoirs and G-buffer) and, unless deferred, the rest of bounce 0 over its own slots
         DevPaths P = PF;
@@ -3158,6 +3196,21 @@ hipError_t launch_frames_restir(const DevScene& S, const DevPaths& PF, const Mpt
         hipLaunchKernelGGL(k_restir_frame_begin, dim3(blocks_for(P.rs_hi - P.rs_lo)), dim3(TB), 0, st, P, d_frames + s);
         P.rs_out = restir_buffer(P, cfg.restir_out_sp2);
         hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(&P.counters[CTR_Q0]), n, 1, st);   // the camera queue
+        if (defer && chunk > 1) {
+            const int k = s % chunk;
+            if (cfg.halo_fn) hipMemsetAsync(&P.counters[CTR_REPROJ], 0, sizeof(int32_t), st);
+            {
+                TimedScope tk(cfg, st, KT_GBUFFER);
+                hipLaunchKernelGGL(k_gb_merge, dim3(blocks_for(n)), dim3(TB), 0, st, P, *cfg.ci_planes, k, d_frames + s);
+            }
+            hipLaunchKernelGGL(k_rs_merge, dim3(blocks_for(n)), dim3(TB), 0, st, P, cfg.ci_planes->rs_init, PF.rq_meta, k);
+            launch_restir(S, P, d_frames + s, hf[s], cfg, st, true);
+            if (cfg.halo_fn) cfg.halo_prev = cfg.halo_rows;
+            const size_t rn = 3 * (size_t)PF.rs_keep_n;
+            hipMemcpyAsync(PF.rs_keep + (size_t)s * rn, P.rs_out + 3 * (size_t)PF.pix_off, rn * sizeof(float4),
+                           hipMemcpyDeviceToDevice, st);
+            continue;
+        }
         if (defer) {
             restir_first_bounce(S, P, d_frames + s, hf[s], cfg, st);
             if (cfg.halo_fn) cfg.halo_prev = cfg.halo_rows;

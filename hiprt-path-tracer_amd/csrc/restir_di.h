@@ -445,16 +445,21 @@ DEV void restir_reproject(const MptFrame& F, v3 p, float& fx, float& fy) {
 // ---- G-buffer write: CameraRays (CameraRays.h:144-166) over the camera queue ----------
 #ifndef MPT_TU_PART   // k_gbuffer
 __global__ __launch_bounds__(TB) void k_gbuffer(DevScene S, DevPaths P, const MptFrame* __restrict__ Fp) {
-    const MptFrame& F = *Fp;
     int i = blockIdx.x * TB + threadIdx.x;
-    if (i >= P.counters[CTR_Q0]) return;
-    int slot = P.q0[i];
+    // a chunk of samples (DevPaths::ci_n): every slot of the chunk's samples (their camera
+    // queues are whole: no adaptive sampling, no low resolution), written to the chunk's planes
+    // at the slot; a miss's record starts empty instead of keeping the pixel's last surface
+    // (the chunk's consumers skip misses; k_gb_merge keeps it in the context's planes)
+    const bool chunk = P.ci_n > 0;
+    if (i >= (chunk ? P.n : P.counters[CTR_Q0])) return;
+    const MptFrame& F = chunk ? Fp[i / P.ci_n] : *Fp;
+    int slot = chunk ? i : P.q0[i];
     const int gp = slot + P.pix_off;   // G-buffer entry of the slot's pixel
     float4 ro = P.ray_o[slot], rdv = P.ray_d[slot], hv = P.hit[slot];
     v3 o = mk3(ro.x, ro.y, ro.z), d = mk3(rdv.x, rdv.y, rdv.z);
     int prim = (int)__float_as_uint(hv.w);
     bool found = prim >= 0;
-    int4 meta = P.gb_meta[gp];
+    int4 meta = chunk ? make_int4(0, 0, 0, 0) : P.gb_meta[gp];
     if (found) {
         // trace_ray hit processing (Intersect.h:150-216), as k_shade does at bounce 0
         VState vs = vs_load_s(P.vsA, P.vsB, slot);
@@ -487,7 +492,7 @@ __global__ __launch_bounds__(TB) void k_gbuffer(DevScene S, DevPaths P, const Mp
         if (m.dispersion_scale > 0.0f && m.specular_transmission > 0.0f && vs.wl == 0.0f)
             vs.wl = -(rng() * (float)(830 - 360) + (float)360);
         if (is_emissive(m) && dot(-d, gn) < 0) { gn = -gn; sn = -sn; }
-        if (F.band_count > 1) {
+        if (F.band_count > 1 && !chunk) {   // (a chunk: measured by k_gb_merge)
             // rows between this pixel and its reprojection (restir_temporal_neighbor's base
             // position): the halo a partitioned context needs for the temporal reuse
             float fx, fy;
@@ -522,13 +527,16 @@ __global__ __launch_bounds__(TB) void k_gbuffer(DevScene S, DevPaths P, const Mp
 // ---- ReSTIR_DI_LightsPresampling (LightsPresampling.h:22-130) ------------------------
 #ifndef MPT_TU_PART   // k_restir_presample
 __global__ __launch_bounds__(TB) void k_restir_presample(DevScene S, DevPaths P, const MptFrame* __restrict__ Fp) {
-    const MptFrame& F = *Fp;
-    const MptReSTIRDISettings& rd = F.render_settings.restir_di_settings;
-    const MptWorldSettings& w = F.world_settings;
+    const MptReSTIRDISettings& rd = Fp->render_settings.restir_di_settings;
+    const MptWorldSettings& w = Fp->world_settings;
     if (S.n_emissive == 0 && w.ambient_light_type != MPT_AMBIENT_ENVMAP) return;
+    const int n_pl = rd.number_of_subsets * rd.subset_size;
     int x = blockIdx.x * TB + threadIdx.x;
-    if (x >= rd.number_of_subsets * rd.subset_size) return;
-    Rng rng = make_rng(pass_seed(F, (uint32_t)x, F.restir_di_seeds[0]));
+    // a chunk of samples (DevPaths::ci_n): sample x / n_pl's lights, sample-major
+    const int smp = P.ci_n ? x / n_pl : 0;
+    if (x >= (P.ci_n ? P.n / P.ci_n : 1) * n_pl) return;
+    const MptFrame& F = Fp[smp];
+    Rng rng = make_rng(pass_seed(F, (uint32_t)(x - smp * n_pl), F.restir_di_seeds[0]));
     float env_p = 0.0f;
     if (w.ambient_light_type == MPT_AMBIENT_ENVMAP) env_p = S.n_emissive == 0 ? 1.0f : rd.envmap_candidate_probability;
     int tri = -1;
@@ -659,14 +667,18 @@ RESTIR_KERNEL void k_restir_initial(DevScene S, DevPaths P, const MptFrame* __re
         const int s = STAGED ? list[t] : t;
         s_lane = s;
         const int pix = s + P.pix_off;
+        // the frame pixel and the sample's frame: a chunk's item s is pixel s % ci_n of its
+        // sample s / ci_n (DevPaths::ci_n; the planes are indexed by item)
+        const int fpix = P.ci_n ? s % P.ci_n + P.ci_pix_off : pix;
+        const MptFrame& Fs = P.ci_n ? Fp[s / P.ci_n] : F;
         RSurf g = gb_surface(S, P, pix, false);
         if (is_emissive(*g.m)) continue;
-        uint32_t seed = pass_seed(F, (uint32_t)pix, F.restir_di_seeds[1]);
+        uint32_t seed = pass_seed(Fs, (uint32_t)fpix, Fs.restir_di_seeds[1]);
         Rng rng = make_rng(seed);
         if (!P.active[s] || !P.gb_meta[pix].z) continue;
         rr.pseed = seed;
         rr.n = 0;
-        const int x = pix % W, y = pix / W;
+        const int x = fpix % W, y = fpix / W;
         int nl = rd.number_of_initial_light_candidates, nb = rd.number_of_initial_bsdf_candidates;
         float env_p = 0.0f;
         if (w.ambient_light_type == MPT_AMBIENT_ENVMAP) env_p = S.n_emissive == 0 ? 1.0f : rd.envmap_candidate_probability;
@@ -683,10 +695,11 @@ RESTIR_KERNEL void k_restir_initial(DevScene S, DevPaths P, const MptFrame* __re
             if (F.options.restir_di_do_lights_presampling) {
                 // use_presampled_light_candidate (InitialCandidates.h:30-90)
                 int tcs = (x / rd.tile_size + y / rd.tile_size + 1) * (x / rd.tile_size + y / rd.tile_size) / 2 + y / rd.tile_size;
-                Rng subset_rng = make_rng(F.restir_di_seeds[1] * (uint32_t)(tcs + 1));
+                Rng subset_rng = make_rng(Fs.restir_di_seeds[1] * (uint32_t)(tcs + 1));
                 int subset = subset_rng.random_index(rd.number_of_subsets);
                 int li = rng.random_index(rd.subset_size);
-                const float4* pl = P.rs_plights + 4 * (size_t)(subset * rd.subset_size + li);
+                const size_t pl0 = P.ci_n ? (size_t)(s / P.ci_n) * (size_t)(rd.number_of_subsets * rd.subset_size) : 0;
+                const float4* pl = P.rs_plights + 4 * (pl0 + (size_t)(subset * rd.subset_size + li));
                 float4 p0 = pl[0], p1 = pl[1], p2 = pl[2];
                 tri = __float_as_int(p0.x);
                 point = mk3(p0.y, p0.z, p0.w);
@@ -873,8 +886,11 @@ RESTIR_KERNEL void k_rsi_finish(DevScene S, DevPaths P, const MptFrame* __restri
             ray.o = sp;
             if (r.flags & RF_ENVMAP) { ray.d = mat_x_vec(w.envmap_to_world_matrix.m, r.point); ray.dist = 1.0e35f; }
             else { v3 dir = r.point - sp; ray.dist = length(dir); ray.d = dir / ray.dist; }
+            // (a chunk's item: its sample's frame and the frame pixel, as k_restir_initial)
+            const MptFrame& Fs = P.ci_n ? Fp[s / P.ci_n] : F;
+            const uint32_t fpix = (uint32_t)(P.ci_n ? s % P.ci_n + P.ci_pix_off : pix);
             rs_stage_ray(P, id, ray, P.gb_meta[pix].x,
-                         F.render_settings.do_alpha_testing ? alpha_key(pass_seed(F, (uint32_t)pix, F.restir_di_seeds[1]), 0, 5,
+                         F.render_settings.do_alpha_testing ? alpha_key(pass_seed(Fs, fpix, Fs.restir_di_seeds[1]), 0, 5,
                                                                         RP_VISREUSE)
                                                             : 0u);
             vbits |= 1u << kk;
@@ -1892,6 +1908,67 @@ __global__ __launch_bounds__(TB) void k_rs_visapply(DevPaths P, float4* out) {
     const size_t c = (size_t)(id / RS_RPP + P.pix_off);
     if (P.rq_occ[rq_phys(P, id)]) out[3 * c].z = -1.0f;
     else out[3 * c + 2].x = __uint_as_float(__float_as_uint(out[3 * c + 2].x) | RF_UNOCCLUDED);
+}
+#endif
+
+// Chunked initial candidates (launch_frames_restir): sample k of the chunk C -- its G-buffer
+// into the context's planes with exactly the stores k_gbuffer makes for the pixel (a miss keeps
+// the pixel's surface, material and per-pixel flag), plus the halo measure of a partitioned
+// context; the camera queue is every slot (q0[i] = i)
+#ifndef MPT_TU_PART   // k_gb_merge
+__global__ __launch_bounds__(TB) void k_gb_merge(DevPaths P, DevPaths C, int k, const MptFrame* __restrict__ Fp) {
+    const MptFrame& F = *Fp;
+    const int i = blockIdx.x * TB + threadIdx.x;
+    if (i >= P.n) return;
+    const size_t c = (size_t)k * (size_t)P.n + (size_t)i;
+    const int gp = i + P.pix_off;
+    const int4 cm = C.gb_meta[c];
+    int4 meta = P.gb_meta[gp];
+    if (cm.z) {
+        if (cm.w) P.gb_mat[gp] = C.gb_mat[c];
+        const float4 pos = C.gb_pos[c];
+        if (F.band_count > 1) {   // k_gbuffer's halo measure
+            float fx, fy;
+            restir_reproject(F, mk3(pos.x, pos.y, pos.z), fx, fy);
+            const float H = (float)F.res_y;
+            int off = F.res_y;
+            if (fy > -H && fy < 2.0f * H) off = min(F.res_y, abs((int)roundf(fy) - gp / F.res_x));
+            atomicMax(&P.counters[CTR_REPROJ], off);
+        }
+        P.gb_pos[gp] = pos;
+        P.gb_sn[gp] = C.gb_sn[c];
+        P.gb_gn[gp] = C.gb_gn[c];
+        P.gb_vsA[gp] = C.gb_vsA[c];
+        P.gb_vsB[gp] = C.gb_vsB[c];
+        meta.y = cm.y;
+        meta.w = cm.w;
+        if (MPT_RESTIR_CS) {
+            P.gb_cs[4 * (size_t)gp + 0] = C.gb_cs[4 * c + 0];
+            P.gb_cs[4 * (size_t)gp + 1] = C.gb_cs[4 * c + 1];
+            P.gb_cs[4 * (size_t)gp + 3] = C.gb_cs[4 * c + 3];
+        }
+    }
+    meta.x = cm.x;
+    meta.z = cm.z;
+    P.gb_meta[gp] = meta;
+    P.gb_view[gp] = C.gb_view[c];
+    if (MPT_RESTIR_CS) P.gb_cs[4 * (size_t)gp + 2] = C.gb_cs[4 * c + 2];
+}
+#endif
+
+// Chunked initial candidates: sample k's initial reservoirs into rs_init where the pass wrote
+// one (every pixel k_rsi_classify listed: not RSM_SKIP); the others keep theirs, as they do
+// when the pass runs per sample
+#ifndef MPT_TU_PART   // k_rs_merge
+__global__ __launch_bounds__(TB) void k_rs_merge(DevPaths P, const float4* __restrict__ cr, const int4* __restrict__ cmeta, int k) {
+    const int i = blockIdx.x * TB + threadIdx.x;
+    if (i >= P.n) return;
+    const size_t c = (size_t)k * (size_t)P.n + (size_t)i;
+    if (cmeta[c].x & RSM_SKIP) return;
+    const size_t p = (size_t)(i + P.pix_off);
+    P.rs_init[3 * p + 0] = cr[3 * c + 0];
+    P.rs_init[3 * p + 1] = cr[3 * c + 1];
+    P.rs_init[3 * p + 2] = cr[3 * c + 2];
 }
 #endif
 

@@ -269,7 +269,12 @@ BATCH_CASES = ["principled", "lambert", "three_passes", "permutation_sampling", 
 @pytest.mark.gpu
 @pytest.mark.parametrize("max_batch", [2, 7])
 @pytest.mark.parametrize("case", BATCH_CASES + ["zero_bounces", "alpha_cards", "envmap", "envmap_alpha_cards",
-                                               "envmap_unfused", "envmap_zero_bounces", "envmap_moving"])
+                                               "envmap_unfused", "envmap_zero_bounces", "envmap_moving"] +
+                         # under an envmap the initial candidates run in chunks of samples (restir_di.h
+                         # k_gb_merge / k_rs_merge), except with the options the staged pass excludes
+                         ["envmap_" + c for c in ("lambert", "three_passes", "permutation_sampling", "bias_gbh",
+                                                  "no_presampling", "seven_neighbours", "unfused_temporal_only",
+                                                  "initial_target_visibility", "two_bsdf_candidates")])
 def test_gpu_restir_batched_bit_exact(cornell, luts, case, max_batch):
     """mpt_render_frames over ReSTIR DI frames: each sample's camera rays, reuse passes and
     first bounce in turn, the later bounces of the batch as one wavefront (slot = sample *
@@ -308,6 +313,36 @@ def test_gpu_restir_batched_bit_exact(cornell, luts, case, max_batch):
     assert np.isfinite(g).all() and g.mean() > 0
     o.close()
     r.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["principled", "unfused", "three_passes"])
+def test_gpu_restir_chunked_initial_equals_per_sample(cornell, luts, case, monkeypatch):
+    """The chunked initial candidates (a chunk of samples' G-buffers, presampled lights and
+    initial reservoirs in one launch set, merged per sample before its reuse passes) leave every
+    buffer the per-sample chain leaves: the image and AOVs, and the three reservoir buffers bit
+    for bit -- incl. rs_init at the pixels the initial pass skips (misses, emissive hits), which
+    keep an earlier sample's reservoir in both."""
+    import mpt
+    env = mpt.build_envmap(scene.procedural_sky(128, 64, seed=7))
+    kw = dict(CASES[case])
+    kw["world"] = scene.envmap_world(1.0)
+    frs = frames(cornell, abi.LSS_RESTIR_DI, 9, **kw)
+    out = {}
+    for chunk in ("1", "4"):
+        monkeypatch.setenv("MPT_RESTIR_CHUNK", chunk)
+        r = mpt.GPURenderer(0)
+        r.set_scene(cornell)
+        r.set_luts(luts)
+        r.set_envmap(env)
+        r.render_samples(frs, max_batch=9)
+        r.synchronize_kernel()
+        out[chunk] = [r.framebuffer(k) for k in (abi.FB_COLOR, abi.FB_ALBEDO, abi.FB_NORMALS)] + \
+                     [r.aux_buffer(k).view(np.uint32) for k in (abi.AUX_RESTIR_OUTPUT, abi.AUX_RESTIR_OTHER,
+                                                                abi.AUX_RESTIR_INITIAL)]
+        r.close()
+    for k, (a, b) in enumerate(zip(out["4"], out["1"])):
+        assert np.array_equal(a, b), f"buffer {k}: {(a != b).sum()} values differ"
 
 
 @pytest.mark.gpu

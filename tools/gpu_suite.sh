@@ -1,7 +1,7 @@
-# the whole GPU suite and smoke at the packed-traversal / single-precision-transcendental build,
-# then the driver's default bench command and the C4 rank-of-8 rehearsal
+# The GPU suite and smoke, then the driver's default bench command and the C4 rank-of-8 rehearsal
+# (gpurun: bash tools/gpu_suite.sh [tag]; outputs under gpurun_out/<tag>)
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
-o=gpurun_out/r05h; mkdir -p $o
+o=gpurun_out/${1:-suite}; mkdir -p $o
 timeout -k 10 600 python -u -m pytest -q -x --timeout 300 --timeout-method thread -m gpu tests > $o/pytest.log 2>&1 || { tail -30 $o/pytest.log; exit 1; }
 tail -3 $o/pytest.log
 timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > $o/smoke.log 2>&1 || { tail -5 $o/smoke.log; exit 1; }
