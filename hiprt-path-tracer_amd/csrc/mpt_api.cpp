@@ -212,7 +212,7 @@ struct MptContext {
     DBuf<int4> rq_meta;
     // chunked ReSTIR DI initial candidates (launch_frames_restir, LaunchCfg::ci_planes): the
     // G-buffer, initial reservoirs and presampled lights of up to restir_chunk samples
-    int restir_chunk = 1;                 // MPT_RESTIR_CHUNK: samples per chunk (-1: by the band's pixels)
+    int restir_chunk = -1;                // MPT_RESTIR_CHUNK: samples per chunk (-1: by the band's pixels)
     int ci_chunk = 1;                     // the chunk the planes below are sized for
     DBuf<float4> ci_pos, ci_sn, ci_gn, ci_view, ci_cs, ci_rs, ci_pl;
     DBuf<int4> ci_meta;
@@ -689,10 +689,13 @@ int ensure_restir(MptContext* c, const MptFrame* f) {
         // A chunk of samples' initial candidates (launch_frames_restir) stages one ray position
         // per (sample, pixel) item -- up to RS_RPP samples -- and two records and a metadata entry
         // per item; its G-buffer / reservoir / light planes are the ci_* buffers.  The chunk
-        // follows the band's size: ~4 M items, so that a small band's launches fill the GPU and a
-        // whole frame's stay as they are (1080p: 2 samples)
+        // follows the band's size: ~4 M items, so that a small band's launches fill the GPU; a
+        // band of more than 1 M pixels keeps one sample's chain at a time (a 1080p frame in chunks
+        // of 2 measured no faster: the merges cost what the shared launches save,
+        // profiles/r05i_c4_chunk_ab.jsonl)
         const size_t ns = (size_t)std::max(c->n_slots, 1);
-        int ck = c->restir_chunk >= 0 ? c->restir_chunk : (int)std::max<size_t>(1, ((size_t)4 << 20) / ns);
+        int ck = c->restir_chunk >= 0 ? c->restir_chunk : (int)(((size_t)4 << 20) / ns);
+        if (c->restir_chunk < 0 && ck < 4) ck = 1;
         ck = std::max(1, std::min(ck, RS_RPP_HOST));
         if (c->rq_o.n != ns * RS_RPP_HOST) {
             A(c->rq_o, ns * RS_RPP_HOST); A(c->rq_d, ns * RS_RPP_HOST); A(c->rq_key, ns * RS_RPP_HOST);
