@@ -1,0 +1,2 @@
+# round-5 evidence at the final build: rocprofv3 kernel tables + PMC passes + bench lines, C3 and C4
+bash tools/gpu_evidence.sh r05k c3 "--steps 32" "--steps 64" && bash tools/gpu_evidence.sh r05k c4 "--steps 32" "--steps 32"
