@@ -487,6 +487,10 @@ PART_BATCH_CASES = {
     "camera_moves_b4": (24, 64, 3, 4, dict(move_at=2, reuse_radius=5)),
     "unfused_b4": (24, 64, 3, 4, dict(do_fused_spatiotemporal=False, reuse_radius=5)),
     "envmap_deferred_b4": (24, 64, 3, 4, dict(reuse_radius=5, envmap=True)),
+    # under the envmap the initial candidates run in chunks (k_gb_merge measures the halo of a
+    # moving camera instead of k_gbuffer)
+    "envmap_camera_moves_b6": (24, 64, 3, 6, dict(move_at=2, reuse_radius=5, envmap=True)),
+    "envmap_unfused_4bands_b6": (24, 96, 4, 6, dict(do_fused_spatiotemporal=False, reuse_radius=4, envmap=True)),
     "empty_last_band_b4": (24, 9, 4, 4, dict(reuse_radius=2)),    # bands of 3 rows: the 4th is empty
 }
 
