@@ -4,3 +4,9 @@ bash tools/gpu_evidence.sh r05k c3 "--steps 32" "--steps 64" && bash tools/gpu_e
 o=gpurun_out/ev_r05k
 timeout -k 10 300 python -u bench.py --emulate-rank-of 8 --steps 64 > $o/c3_rank8.json 2> $o/c3_rank8.err || { tail -20 $o/c3_rank8.err; exit 1; }
 tail -c 300 $o/c3_rank8.json
+timeout -k 10 300 python -u bench.py --emulate-rank-of 8 --steps 20 > $o/c3_rank8_s20.json 2> $o/c3_rank8_s20.err || { tail -20 $o/c3_rank8_s20.err; exit 1; }
+timeout -k 10 300 python -u bench.py --steps 20 --configs none --no-parity --no-cpu-baseline > $o/c3_s20.json 2> $o/c3_s20.err || { tail -20 $o/c3_s20.err; exit 1; }
+python -c "
+import json
+a = json.load(open('$o/c3_rank8_s20.json')); b = json.load(open('$o/c3_s20.json'))
+print('c3 steps 20: whole', b['ms_per_step'], 'rank-of-8', a['ms_per_step'], 'ratio', b['ms_per_step'] / a['ms_per_step'])"
