@@ -160,6 +160,7 @@ struct MptContext {
     // plain vertex deferred to the generic kernel (test hook); MPT_SHADE_CLASSES at mpt_create
     int shade_classes = 1;
     int restir_staged = 1;                // ReSTIR DI reuse passes staged around their rays (MPT_RESTIR_STAGED)
+    int restir_mono_reuse = 0;            // MPT_RESTIR_MONO_REUSE: the reuse passes monolithic, the initial pass staged
     int restir_batch = 1;                 // ReSTIR DI samples batched after bounce 0 (MPT_RESTIR_BATCH)
     int adaptive_batch = 1;               // adaptive samples batched, gated in k_accumulate (MPT_ADAPTIVE_BATCH)
     int restir_max_batch = RESTIR_MAX_BATCH;   // MPT_RESTIR_MAX_BATCH
@@ -935,6 +936,7 @@ int mpt_create(int device, void* hip_stream, MptContext** out) {
     MptContext* c = new MptContext();   // value-initialised: every handle starts null
     if (const char* e = std::getenv("MPT_SHADE_CLASSES")) c->shade_classes = std::atoi(e);
     if (const char* e = std::getenv("MPT_RESTIR_STAGED")) c->restir_staged = std::atoi(e);
+    if (const char* e = std::getenv("MPT_RESTIR_MONO_REUSE")) c->restir_mono_reuse = std::atoi(e);
     if (const char* e = std::getenv("MPT_RESTIR_BATCH")) c->restir_batch = std::atoi(e);
     if (const char* e = std::getenv("MPT_ADAPTIVE_BATCH")) c->adaptive_batch = std::atoi(e);
     if (const char* e = std::getenv("MPT_MAT_PRIVATE")) c->mat_private = std::atoi(e);
@@ -1423,6 +1425,7 @@ static int launch_batch(MptContext* c, const MptFrame* f, int batch) {
     cfg.restir_out_sp2 = c->restir_out_sp2;
     cfg.shade_classes = c->shade_classes;
     cfg.restir_staged = c->restir_staged;
+    cfg.restir_mono_reuse = c->restir_mono_reuse;
     if (c->ci_chunk > 1 && c->ci_pos.p && c->ci_pl.n >= 4 * (size_t)std::max(1, f->render_settings.restir_di_settings.number_of_subsets *
                                                                                      f->render_settings.restir_di_settings.subset_size) * c->ci_chunk) {
         cfg.ci_chunk = c->ci_chunk;

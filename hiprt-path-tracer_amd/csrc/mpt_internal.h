@@ -299,6 +299,7 @@ struct LaunchCfg {
     int light_bvh;            // light-hit queries through the light BVH (1) or one closest-hit traversal (0)
     int light_static;         // the light BVH's traversal stack fits in LDS (one query per lane, no spill)
     int restir_staged;        // ReSTIR DI reuse passes staged around their rays (restir_di.h), when supported
+    int restir_mono_reuse;    // the reuse passes as the monolithic kernels (the initial pass staged)
     int shade_glass;          // k_split's glass class (MPT_SHADE_GLASS)
     int mat_private;          // k_shade<..., MATP>: textured vertices' resolved material in private memory
     int shade_split;          // plain class in stages (MPT_SHADE_SPLIT): 0 one kernel, 1 light / env / cont,

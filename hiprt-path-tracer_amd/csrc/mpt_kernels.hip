@@ -2701,7 +2701,7 @@ static void launch_spatial_pass(int ovr, bool def_bias, const MptFrame& hf, Laun
                                 const DevScene& S, const DevPaths& P, const MptFrame* d_frame, int pass, const float4* in,
                                 float4* out) {
     const MptReSTIRDISettings& rd = hf.render_settings.restir_di_settings;
-    const bool staged = def_bias && cfg.restir_staged && P.rq_o && rd.reuse_neighbor_count <= RS_KMAX &&
+    const bool staged = def_bias && cfg.restir_staged && !cfg.restir_mono_reuse && P.rq_o && rd.reuse_neighbor_count <= RS_KMAX &&
                         (!rd.do_disocclusion_reuse_boost || rd.disocclusion_reuse_count <= RS_KMAX);
     if (!staged) {
         launch_restir_kernel(ovr, def_bias ? RK_SPATIAL : RK_SPATIAL_ANY, g, st, S, P, d_frame, pass, in, out);
@@ -2734,7 +2734,7 @@ static void launch_spatial_pass(int ovr, bool def_bias, const MptFrame& hf, Laun
 static void launch_fused_pass(int ovr, bool def_bias, const MptFrame& hf, LaunchCfg& cfg, dim3 g, hipStream_t st,
                               const DevScene& S, const DevPaths& P, const MptFrame* d_frame) {
     const MptReSTIRDISettings& rd = hf.render_settings.restir_di_settings;
-    const bool staged = def_bias && cfg.restir_staged && P.rq_o && rd.reuse_neighbor_count <= RS_KMAX &&
+    const bool staged = def_bias && cfg.restir_staged && !cfg.restir_mono_reuse && P.rq_o && rd.reuse_neighbor_count <= RS_KMAX &&
                         (!rd.do_disocclusion_reuse_boost || rd.disocclusion_reuse_count <= RS_KMAX) &&
                         !rd.temporal_buffer_clear_requested;
     if (!staged) {

@@ -10,3 +10,8 @@ python -c "
 import json
 a = json.load(open('$o/c3_rank8_s20.json')); b = json.load(open('$o/c3_s20.json'))
 print('c3 steps 20: whole', b['ms_per_step'], 'rank-of-8', a['ms_per_step'], 'ratio', b['ms_per_step'] / a['ms_per_step'])"
+# the reuse passes monolithic on a small band (the initial pass staged and chunked)
+for m in 0 1; do
+  MPT_RESTIR_MONO_REUSE=$m timeout -k 10 300 python -u bench.py --workload c4 --emulate-rank-of 8 --steps 128 > $o/c4_rank8_mono$m.json 2> $o/c4_rank8_mono$m.err || { tail -20 $o/c4_rank8_mono$m.err; exit 1; }
+  python -c "import json; d=json.load(open('$o/c4_rank8_mono$m.json')); print('c4 rank8 mono_reuse=$m slowest', d['ms_per_spp_slowest_rank'], 'mean', d['ms_per_spp_mean_rank'])"
+done
