@@ -1,17 +1,3 @@
 # round-5 evidence at the final build: rocprofv3 kernel tables + PMC passes + bench lines (C3, C4),
 # then the C3 rank-of-8 rehearsal
 bash tools/gpu_evidence.sh r05k c3 "--steps 32" "--steps 64" && bash tools/gpu_evidence.sh r05k c4 "--steps 32" "--steps 32" || exit 1
-o=gpurun_out/ev_r05k
-timeout -k 10 300 python -u bench.py --emulate-rank-of 8 --steps 64 > $o/c3_rank8.json 2> $o/c3_rank8.err || { tail -20 $o/c3_rank8.err; exit 1; }
-tail -c 300 $o/c3_rank8.json
-timeout -k 10 300 python -u bench.py --emulate-rank-of 8 --steps 20 > $o/c3_rank8_s20.json 2> $o/c3_rank8_s20.err || { tail -20 $o/c3_rank8_s20.err; exit 1; }
-timeout -k 10 300 python -u bench.py --steps 20 --configs none --no-parity --no-cpu-baseline > $o/c3_s20.json 2> $o/c3_s20.err || { tail -20 $o/c3_s20.err; exit 1; }
-python -c "
-import json
-a = json.load(open('$o/c3_rank8_s20.json')); b = json.load(open('$o/c3_s20.json'))
-print('c3 steps 20: whole', b['ms_per_step'], 'rank-of-8', a['ms_per_step'], 'ratio', b['ms_per_step'] / a['ms_per_step'])"
-# the reuse passes monolithic on a small band (the initial pass staged and chunked)
-for m in 0 1; do
-  MPT_RESTIR_MONO_REUSE=$m timeout -k 10 300 python -u bench.py --workload c4 --emulate-rank-of 8 --steps 128 > $o/c4_rank8_mono$m.json 2> $o/c4_rank8_mono$m.err || { tail -20 $o/c4_rank8_mono$m.err; exit 1; }
-  python -c "import json; d=json.load(open('$o/c4_rank8_mono$m.json')); print('c4 rank8 mono_reuse=$m slowest', d['ms_per_spp_slowest_rank'], 'mean', d['ms_per_spp_mean_rank'])"
-done
