@@ -198,3 +198,40 @@ def test_cpp_interaction_low_resolution_matches_oracle(cornell, luts, tmp_path, 
     ref = o.render(frames)
     o.close()
     assert np.array_equal(img, ref), f"{(img != ref).sum()} values differ"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("split", [2, 4])
+def test_cpp_restir_city_tiled_equals_one_context(luts, tmp_path, split, monkeypatch):
+    """The C4 frame size through the C++ GPURenderer tiled over 2 / 4 contexts on device 0
+    (contiguous bands, LocalHaloGroup exchanging the halo at every reuse pass, batched samples):
+    the 1920x1080 city (2.86 M triangles; its leaf cards untextured here: the blob carries no
+    textures) renders bit for bit what one context renders."""
+    import copy
+    import sys
+    from mpt import synthetic
+    mod = sys.modules[__name__]
+    monkeypatch.setattr(mod, "W", 1920)
+    monkeypatch.setattr(mod, "H", 1080)
+    sd = copy.copy(synthetic.procedural_city(1234))
+    mats = [abi.Material.from_buffer_copy(m) for m in sd.materials]
+    for m in mats:
+        if m.base_color_texture_index >= 0:
+            m.base_color_texture_index = -1   # MPT_NO_TEXTURE
+    sd.materials = mats
+    sd.textures = []
+    st = scene.parity_settings(3)
+    st.samples_per_frame = 2
+    opt = abi.KernelOptions.default()
+    opt.direct_light_sampling = abi.LSS_RESTIR_DI
+    cam = scene.make_camera(sd.camera_info, 1920, 1080)
+    imgs = {}
+    for sp in (1, split):
+        blob, out = tmp_path / f"in{sp}.blob", tmp_path / f"out{sp}.bin"
+        _blob(blob, sd, luts, st, abi.WorldSettings.default(), opt, cam, 2, 0, [], sp)
+        r = subprocess.run([str(_build.HOST_TEST), str(blob), str(out)], capture_output=True, text=True, timeout=240)
+        assert r.returncode == 0, r.stderr
+        imgs[sp] = _read_out(out)[1]
+        blob.unlink()
+    assert imgs[1].mean() > 0
+    assert np.array_equal(imgs[split], imgs[1]), f"{(imgs[split] != imgs[1]).sum()} values differ"
