@@ -15,3 +15,4 @@ for m in 0 1; do
   MPT_RESTIR_MONO_REUSE=$m timeout -k 10 300 python -u bench.py --workload c4 --emulate-rank-of 8 --steps 128 > $o/c4_rank8_mono$m.json 2> $o/c4_rank8_mono$m.err || { tail -20 $o/c4_rank8_mono$m.err; exit 1; }
   python -c "import json; d=json.load(open('$o/c4_rank8_mono$m.json')); print('c4 rank8 mono_reuse=$m slowest', d['ms_per_spp_slowest_rank'], 'mean', d['ms_per_spp_mean_rank'])"
 done
+bash tools/gpu_r05m.sh
