@@ -101,7 +101,12 @@ struct MptContext {
     // overlapped batches (MPT_OVERLAP at mpt_create): the second half of a sample batch runs
     // on stream2, one pipeline stage behind the first, so that shading waves of one half and
     // traversal waves of the other share the CUs
-    int overlap = 0;   // opt-in: +1.2 % on C3, but per-kernel times then overlap
+    // MPT_OVERLAP: a path-tracing batch's two halves on two streams: 1 always, 0
+    // never, -1 (default) for wavefronts of at most OVERLAP_AUTO_PATHS paths -- a rank's share of
+    // a split frame, where the launch tails are a larger part of each launch (one rank of 8 at
+    // 20 samples: -3.8 %); a whole 1080p frame keeps one stream (+1.2 % only, and its per-kernel
+    // times stay unshared)
+    int overlap = -1;
     hipStream_t stream2 = nullptr;
     hipEvent_t ev_fork = nullptr, ev_first = nullptr, ev_acc = nullptr, ev_join = nullptr;
     // Overlapped ReSTIR DI batches (MPT_RESTIR_OVERLAP, default on): a batch's per-sample chain
@@ -410,6 +415,7 @@ struct Allocs {
 // nhit, s_gn (9 x 16), vsA + vsB (32), the NEE record planes (7 x 16), 4 staged NEE query rays (2 x 64), the
 // compacted query entries (16), occlusion bytes (4), 6 queues (24), rng (4), seeds (8), hit_inside,
 // qmask, active (3).  Textured scenes add a resolved material per slot.
+constexpr size_t OVERLAP_AUTO_PATHS = (size_t)8 << 20;   // MPT_OVERLAP=-1: overlapped halves up to this many paths
 constexpr size_t PATH_BYTES = 9 * 16 + 32 + 7 * 16 + 128 + 16 + 4 + 24 + 4 + 8 + 3;
 
 void release_batch(MptContext* c) {
@@ -1458,8 +1464,8 @@ static int launch_batch(MptContext* c, const MptFrame* f, int batch) {
         P.rs_lo = std::max(0, cfg.own_y0 - cfg.halo_prev) * f->res_x;
         P.rs_hi = std::min(f->res_y, cfg.own_y1 + cfg.halo_prev) * f->res_x;
     }
-    const bool ovl = c->overlap && batch >= 2 && f->options.direct_light_sampling != MPT_LSS_RESTIR_DI && c->x_per == 0 &&
-                     !P.spec_as;
+    const bool ovl = (c->overlap > 0 || (c->overlap < 0 && (size_t)batch * (size_t)std::max(c->n_slots, 1) <= OVERLAP_AUTO_PATHS)) &&
+                     batch >= 2 && f->options.direct_light_sampling != MPT_LSS_RESTIR_DI && c->x_per == 0 && !P.spec_as;
     hipError_t e = hipSuccess;
     if (ovl) {
         int rr = ensure_overlap(c);
