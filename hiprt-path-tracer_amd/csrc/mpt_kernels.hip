@@ -3158,8 +3158,8 @@ hipError_t launch_frames_restir(const DevScene& S, const DevPaths& PF, const Mpt
     // Chunked initial candidates (deferred first bounce, staged initial pass): the G-buffer,
     // lights presampling and initial candidates of up to ci_chunk samples -- which read no earlier
     // sample's state -- as one launch set into the chunk's planes (cfg.ci_planes); each sample then
-    // merges its G-buffer and initial reservoirs into the context's planes (k_gb_merge /
-    // k_rs_merge: the stores the per-sample kernels make) before its reuse passes, in order.
+    // merges its G-buffer and initial reservoirs into the context's planes (k_chunk_join: the
+    // stores the per-sample kernels make) before its reuse passes, in order.
     const MptReSTIRDISettings& rd0 = hf[0].render_settings.restir_di_settings;
     const int chunk = (defer && cfg.ci_planes && cfg.ci_chunk > 1 && cfg.restir_staged && PF.rq_o &&
                        rd0.number_of_initial_bsdf_candidates <= 1 && !hf[0].options.restir_di_initial_target_visibility)
@@ -3193,17 +3193,16 @@ hipError_t launch_frames_restir(const DevScene& S, const DevPaths& PF, const Mpt
             P.rs_lo = std::max(0, cfg.own_y0 - cfg.halo_prev) * hf[s].res_x;
             P.rs_hi = std::min(hf[s].res_y, cfg.own_y1 + cfg.halo_prev) * hf[s].res_x;
         }
-        hipLaunchKernelGGL(k_restir_frame_begin, dim3(blocks_for(P.rs_hi - P.rs_lo)), dim3(TB), 0, st, P, d_frames + s);
         P.rs_out = restir_buffer(P, cfg.restir_out_sp2);
-        hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(&P.counters[CTR_Q0]), n, 1, st);   // the camera queue
         if (defer && chunk > 1) {
-            const int k = s % chunk;
+            // frame_begin, the G-buffer and the initial reservoirs of the chunk's sample k in one
+            // pass (k_chunk_join); the camera queue counter is not read on this path
             if (cfg.halo_fn) hipMemsetAsync(&P.counters[CTR_REPROJ], 0, sizeof(int32_t), st);
             {
                 TimedScope tk(cfg, st, KT_GBUFFER);
-                hipLaunchKernelGGL(k_gb_merge, dim3(blocks_for(n)), dim3(TB), 0, st, P, *cfg.ci_planes, k, d_frames + s);
+                hipLaunchKernelGGL(k_chunk_join, dim3(blocks_for(P.rs_hi - P.rs_lo)), dim3(TB), 0, st, P, *cfg.ci_planes, PF.rq_meta,
+                                   s % chunk, d_frames + s);
             }
-            hipLaunchKernelGGL(k_rs_merge, dim3(blocks_for(n)), dim3(TB), 0, st, P, cfg.ci_planes->rs_init, PF.rq_meta, k);
             launch_restir(S, P, d_frames + s, hf[s], cfg, st, true);
             if (cfg.halo_fn) cfg.halo_prev = cfg.halo_rows;
             const size_t rn = 3 * (size_t)PF.rs_keep_n;
@@ -3211,6 +3210,8 @@ hipError_t launch_frames_restir(const DevScene& S, const DevPaths& PF, const Mpt
                            hipMemcpyDeviceToDevice, st);
             continue;
         }
+        hipLaunchKernelGGL(k_restir_frame_begin, dim3(blocks_for(P.rs_hi - P.rs_lo)), dim3(TB), 0, st, P, d_frames + s);
+        hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(&P.counters[CTR_Q0]), n, 1, st);   // the camera queue
         if (defer) {
             restir_first_bounce(S, P, d_frames + s, hf[s], cfg, st);
             if (cfg.halo_fn) cfg.halo_prev = cfg.halo_rows;

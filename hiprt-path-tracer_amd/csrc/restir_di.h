@@ -449,7 +449,7 @@ __global__ __launch_bounds__(TB) void k_gbuffer(DevScene S, DevPaths P, const Mp
     // a chunk of samples (DevPaths::ci_n): every slot of the chunk's samples (their camera
     // queues are whole: no adaptive sampling, no low resolution), written to the chunk's planes
     // at the slot; a miss's record starts empty instead of keeping the pixel's last surface
-    // (the chunk's consumers skip misses; k_gb_merge keeps it in the context's planes)
+    // (the chunk's consumers skip misses; k_chunk_join keeps it in the context's planes)
     const bool chunk = P.ci_n > 0;
     if (i >= (chunk ? P.n : P.counters[CTR_Q0])) return;
     const MptFrame& F = chunk ? Fp[i / P.ci_n] : *Fp;
@@ -492,7 +492,7 @@ __global__ __launch_bounds__(TB) void k_gbuffer(DevScene S, DevPaths P, const Mp
         if (m.dispersion_scale > 0.0f && m.specular_transmission > 0.0f && vs.wl == 0.0f)
             vs.wl = -(rng() * (float)(830 - 360) + (float)360);
         if (is_emissive(m) && dot(-d, gn) < 0) { gn = -gn; sn = -sn; }
-        if (F.band_count > 1 && !chunk) {   // (a chunk: measured by k_gb_merge)
+        if (F.band_count > 1 && !chunk) {   // (a chunk: measured by k_chunk_join)
             // rows between this pixel and its reprojection (restir_temporal_neighbor's base
             // position): the halo a partitioned context needs for the temporal reuse
             float fx, fy;
@@ -1911,17 +1911,38 @@ __global__ __launch_bounds__(TB) void k_rs_visapply(DevPaths P, float4* out) {
 }
 #endif
 
-// Chunked initial candidates (launch_frames_restir): sample k of the chunk C -- its G-buffer
-// into the context's planes with exactly the stores k_gbuffer makes for the pixel (a miss keeps
-// the pixel's surface, material and per-pixel flag), plus the halo measure of a partitioned
-// context; the camera queue is every slot (q0[i] = i)
-#ifndef MPT_TU_PART   // k_gb_merge
-__global__ __launch_bounds__(TB) void k_gb_merge(DevPaths P, DevPaths C, int k, const MptFrame* __restrict__ Fp) {
+// Chunked initial candidates (launch_frames_restir): sample k of the chunk C joins the context
+// in one pass over the band and its halo rows, per pixel in the order of the per-sample chain:
+// k_restir_frame_begin's previous-frame copy and reservoir reset (band + halo), then, on the band,
+// the stores k_gbuffer would have made (a miss keeps the pixel's surface, material and per-pixel
+// flag; the halo measure of a partitioned context) and the initial reservoirs the chunk's pass
+// wrote (every pixel k_rsi_classify listed: not RSM_SKIP -- the others keep theirs).  The camera
+// queue is every slot (q0[i] = i).
+#ifndef MPT_TU_PART   // k_chunk_join
+__global__ __launch_bounds__(TB) void k_chunk_join(DevPaths P, DevPaths C, const int4* __restrict__ cmeta, int k,
+                                                   const MptFrame* __restrict__ Fp) {
     const MptFrame& F = *Fp;
-    const int i = blockIdx.x * TB + threadIdx.x;
-    if (i >= P.n) return;
+    const MptRenderSettings& rs = F.render_settings;
+    const int gp = P.rs_lo + blockIdx.x * TB + threadIdx.x;
+    if (gp >= P.rs_hi) return;
+    if (rs.restir_di_settings.do_temporal_reuse_pass) {   // k_restir_frame_begin
+        P.pgb_pos[gp] = P.gb_pos[gp]; P.pgb_sn[gp] = P.gb_sn[gp]; P.pgb_gn[gp] = P.gb_gn[gp]; P.pgb_view[gp] = P.gb_view[gp];
+        const int4 m = P.gb_meta[gp];
+        P.pgb_meta[gp] = m;
+        P.pgb_vsA[gp] = P.gb_vsA[gp]; P.pgb_vsB[gp] = P.gb_vsB[gp];
+        if (m.w) P.pgb_mat[gp] = P.gb_mat[gp];
+        if (MPT_RESTIR_CS)
+            for (int q = 0; q < 4; q++) P.pgb_cs[4 * (size_t)gp + q] = P.gb_cs[4 * (size_t)gp + q];
+    }
+    const bool reset = (rs.sample_number == 0 || rs.need_to_reset) && rs.accumulate;
+    if (reset) {
+        rr_store(P.rs_init, gp, rr_default());
+        rr_store(P.rs_sp1, gp, rr_default());
+        rr_store(P.rs_sp2, gp, rr_default());
+    }
+    const int i = gp - P.pix_off;   // the band's pixel (slot)
+    if (i < 0 || i >= P.n) return;
     const size_t c = (size_t)k * (size_t)P.n + (size_t)i;
-    const int gp = i + P.pix_off;
     const int4 cm = C.gb_meta[c];
     int4 meta = P.gb_meta[gp];
     if (cm.z) {
@@ -1953,22 +1974,11 @@ __global__ __launch_bounds__(TB) void k_gb_merge(DevPaths P, DevPaths C, int k, 
     P.gb_meta[gp] = meta;
     P.gb_view[gp] = C.gb_view[c];
     if (MPT_RESTIR_CS) P.gb_cs[4 * (size_t)gp + 2] = C.gb_cs[4 * c + 2];
-}
-#endif
-
-// Chunked initial candidates: sample k's initial reservoirs into rs_init where the pass wrote
-// one (every pixel k_rsi_classify listed: not RSM_SKIP); the others keep theirs, as they do
-// when the pass runs per sample
-#ifndef MPT_TU_PART   // k_rs_merge
-__global__ __launch_bounds__(TB) void k_rs_merge(DevPaths P, const float4* __restrict__ cr, const int4* __restrict__ cmeta, int k) {
-    const int i = blockIdx.x * TB + threadIdx.x;
-    if (i >= P.n) return;
-    const size_t c = (size_t)k * (size_t)P.n + (size_t)i;
-    if (cmeta[c].x & RSM_SKIP) return;
-    const size_t p = (size_t)(i + P.pix_off);
-    P.rs_init[3 * p + 0] = cr[3 * c + 0];
-    P.rs_init[3 * p + 1] = cr[3 * c + 1];
-    P.rs_init[3 * p + 2] = cr[3 * c + 2];
+    if (!(cmeta[c].x & RSM_SKIP)) {
+        P.rs_init[3 * (size_t)gp + 0] = C.rs_init[3 * c + 0];
+        P.rs_init[3 * (size_t)gp + 1] = C.rs_init[3 * c + 1];
+        P.rs_init[3 * (size_t)gp + 2] = C.rs_init[3 * c + 2];
+    }
 }
 #endif
 
