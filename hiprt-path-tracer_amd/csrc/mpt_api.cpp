@@ -696,12 +696,12 @@ int ensure_restir(MptContext* c, const MptFrame* f) {
         // A chunk of samples' initial candidates (launch_frames_restir) stages one ray position
         // per (sample, pixel) item -- up to RS_RPP samples -- and two records and a metadata entry
         // per item; its G-buffer / reservoir / light planes are the ci_* buffers.  The chunk
-        // follows the band's size: ~4 M items, so that a small band's launches fill the GPU; a
-        // band of more than 1 M pixels keeps one sample's chain at a time (a 1080p frame in chunks
-        // of 2 measured no faster: the merges cost what the shared launches save,
-        // profiles/r05i_c4_chunk_ab.jsonl)
+        // follows the band's size: ~8 M items, so that a small band's launches fill the GPU (1/8
+        // of 1080p: 12 samples) and a 1080p frame runs chunks of 4 (8.19 -> 8.05 ms/spp,
+        // profiles/r05p_c4_whole_frame_chunk_ab.jsonl; chunks of 2 measured no faster); a band
+        // of more than ~2 M pixels keeps one sample's chain at a time
         const size_t ns = (size_t)std::max(c->n_slots, 1);
-        int ck = c->restir_chunk >= 0 ? c->restir_chunk : (int)(((size_t)4 << 20) / ns);
+        int ck = c->restir_chunk >= 0 ? c->restir_chunk : (int)(((size_t)8 << 20) / ns);
         if (c->restir_chunk < 0 && ck < 4) ck = 1;
         ck = std::max(1, std::min(ck, RS_RPP_HOST));
         if (c->rq_o.n != ns * RS_RPP_HOST) {
