@@ -915,7 +915,8 @@ static int create_context(MptContext* c, int device, void* hip_stream) {
     HIPCHK(c->status.alloc(4));
     HIPCHK(hipMemsetAsync(c->status.p, 0, 4 * sizeof(uint32_t), c->stream));
     HIPCHK(hipMemsetAsync(c->ray_counts.p, 0, N_RAY_COUNTS * sizeof(uint64_t), c->stream));
-    HIPCHK(c->spill.alloc((size_t)c->grid * TRAV_BLOCK * SPILL_WORDS));
+    // traversal spill stacks per lane of a persistent grid: up to 8 blocks per CU (launch_trace_mode)
+    HIPCHK(c->spill.alloc((size_t)c->num_cus * 8 * TRAV_BLOCK * SPILL_WORDS));
     HIPCHK(c->srgb.alloc(256));
     HIPCHK(launch_srgb_table(c->srgb.p, c->stream));
     return MPT_OK;

@@ -405,11 +405,16 @@ DEV uint32_t path_seed(const MptFrame* Fp, const DevPaths& P, int slot, bool cam
 #ifndef MPT_TRACE_WAVES
 #define MPT_TRACE_WAVES 5   // 5 waves / SIMD (<= 96 VGPRs): C3 traversal -4 % vs 4 (VGPR-capped), 6 and 8 no better (r02 A/B)
 #endif
+#ifndef MPT_TRACE_WAVES_LIST
+#define MPT_TRACE_WAVES_LIST MPT_TRACE_WAVES   // the ReSTIR DI staged lists (TM_LIST_ANY / TM_LIST_CLOSEST)
+#endif
 #ifndef MPT_TRACE_WAVES_PATH
 #define MPT_TRACE_WAVES_PATH MPT_TRACE_WAVES
 #endif
 template <int MODE, bool STATS>
-__global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MODE == TM_PATH ? MPT_TRACE_WAVES_PATH : MPT_TRACE_WAVES))) void k_trace(TraceArgs A) {
+__global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(
+    MODE == TM_PATH ? MPT_TRACE_WAVES_PATH : (MODE == TM_LIST_ANY || MODE == TM_LIST_CLOSEST) ? MPT_TRACE_WAVES_LIST : MPT_TRACE_WAVES)))
+    void k_trace(TraceArgs A) {
     __shared__ uint2 lds[LDS_STACK * TB];
     const DevScene& S = A.S;
     const DevPaths& P = A.P;
@@ -2627,6 +2632,10 @@ static void launch_restir_kernel(int ovr, int kind, dim3 g, hipStream_t st, cons
 template <int MODE>
 static void launch_trace_mode(const TraceArgs& a, int grid, bool stats, hipStream_t st) {
     if (MODE == TM_NEE_LIGHT && a.static_grid && !stats) grid = blocks_for(a.P.n);   // the query list holds at most n entries
+    // the persistent grid is MPT_TRACE_WAVES blocks per CU (one 4-wave block per SIMD and wave);
+    // the list modes fill their own occupancy (the spill area holds 8 blocks per CU)
+    static_assert(MPT_TRACE_WAVES_LIST <= 8 && MPT_TRACE_WAVES <= 8, "the traversal spill area holds 8 blocks per CU");
+    if (MODE == TM_LIST_ANY || MODE == TM_LIST_CLOSEST) grid = grid / MPT_TRACE_WAVES * MPT_TRACE_WAVES_LIST;
     if (stats) {
         // instrumented (calibration) launches stay persistent: their per-wave counter atomics
         // over a static grid of ~500 k waves would serialise the launch
