@@ -103,9 +103,9 @@ struct MptContext {
     // traversal waves of the other share the CUs
     // MPT_OVERLAP: a path-tracing batch's two halves on two streams: 1 always, 0
     // never, -1 (default) for wavefronts of at most OVERLAP_AUTO_PATHS paths -- a rank's share of
-    // a split frame, where the launch tails are a larger part of each launch (one rank of 8 at
-    // 20 samples: -3.8 %); a whole 1080p frame keeps one stream (+1.2 % only, and its per-kernel
-    // times stay unshared)
+    // a split frame at the driver's 20 samples, where the launch tails are a larger part of each
+    // launch (one rank of 2 / 4 / 8: -2.3 / -2.7 / -3.8 %); a whole 1080p frame's 33-41 M paths
+    // keep one stream (+1.2 % only, and its per-kernel times stay unshared)
     int overlap = -1;
     hipStream_t stream2 = nullptr;
     hipEvent_t ev_fork = nullptr, ev_first = nullptr, ev_acc = nullptr, ev_join = nullptr;
@@ -415,7 +415,7 @@ struct Allocs {
 // nhit, s_gn (9 x 16), vsA + vsB (32), the NEE record planes (7 x 16), 4 staged NEE query rays (2 x 64), the
 // compacted query entries (16), occlusion bytes (4), 6 queues (24), rng (4), seeds (8), hit_inside,
 // qmask, active (3).  Textured scenes add a resolved material per slot.
-constexpr size_t OVERLAP_AUTO_PATHS = (size_t)8 << 20;   // MPT_OVERLAP=-1: overlapped halves up to this many paths
+constexpr size_t OVERLAP_AUTO_PATHS = (size_t)24 << 20;   // MPT_OVERLAP=-1: overlapped halves up to this many paths
 constexpr size_t PATH_BYTES = 9 * 16 + 32 + 7 * 16 + 128 + 16 + 4 + 24 + 4 + 8 + 3;
 
 void release_batch(MptContext* c) {
