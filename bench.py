@@ -386,7 +386,7 @@ def main():
                     "ms_per_step": o["ms_per_step"], "steps": o["steps"], "msample_per_s": o["msample_per_s"],
                     "roofline": {"kernel": rf["kernel"].split(" (")[0], "frac": rf["frac"], "achieved": rf["achieved"],
                                  "pmc_hbm_frac": rf.get("pmc_hbm_frac"), "traffic_per_unit": rf.get("traffic_per_unit"),
-                                 "bytes_per_unit": rf["bytes_per_unit"]},
+                                 "bytes_per_unit": rf["bytes_per_unit"], "shared_gpu": rf.get("shared_gpu")},
                     "kernel_ms_per_step": {k: v for k, v in o["kernel_ms_per_step"].items() if k != "restir_kernels"},
                     "cpu_baseline": o["cpu_baseline"], "parity_vs_oracle": o["parity_vs_oracle"],
                     "wall_s": round(time.perf_counter() - t0, 1)})
@@ -690,6 +690,11 @@ def run_workload(a, world, rank, local, dist, coll_dev, quiet=False):
         if "nodes_per_ray" in x:
             r.update(nodes_per_ray=round(x["nodes_per_ray"], 3), tris_per_ray=round(x["tris_per_ray"], 3),
                      node_simd_util=round(x["node_simd_util"], 3), tri_simd_util=round(x["tri_simd_util"], 3))
+        if getattr(st, "overlapped_batches", 0):
+            # MPT_OVERLAP (the library's default for wavefronts of <= 24 M paths): each batch ran as
+            # two halves on two streams, so this kernel's launches shared the GPU with the other
+            # half's kernels -- its launch time, and with it `achieved`, is not the kernel's alone
+            r["shared_gpu"] = f"{st.overlapped_batches} overlapped batch(es): launch times shared with the other half"
         return r
 
     dname, darch, dcus = mpt.device_info(local)

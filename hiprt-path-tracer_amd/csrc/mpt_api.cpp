@@ -130,6 +130,7 @@ struct MptContext {
     std::vector<uint8_t> graph_key;
     uint32_t graph_launches = 0;
     uint32_t graph_captures = 0, graph_replays = 0;   // since mpt_enable_stats (MptStats)
+    uint32_t overlapped_batches = 0;
     int num_cus = 256;
     int grid = 1024;
     // scene
@@ -1498,6 +1499,7 @@ static int launch_batch(MptContext* c, const MptFrame* f, int batch) {
         if (e == hipSuccess) e = launch_frame(dev_scene(c), P1, c->d_frames + slot + b0, f[b0], cfg1, c->stream2);
         HIPCHK(hipEventRecord(c->ev_join, c->stream2));
         HIPCHK(hipStreamWaitEvent(c->stream, c->ev_join, 0));
+        c->overlapped_batches++;
         cfg.ev_used = cfg1.ev_used;
         cfg.launches = cfg0.launches + cfg1.launches;
     } else if (f->options.direct_light_sampling == MPT_LSS_RESTIR_DI && batch > 1) {
@@ -2071,6 +2073,7 @@ int mpt_enable_stats(MptContext* c, int enable, int instrumented) {
     c->frames = 0;
     c->frame_ms = 0.0;
     c->graph_captures = c->graph_replays = 0;
+    c->overlapped_batches = 0;
     for (int m = 0; m < KT_COUNT; m++) { c->stage_ms[m] = 0.0; c->stage_launches[m] = 0; }
     HIPCHK(hipMemsetAsync(c->stats.p, 0, N_STATS * sizeof(uint64_t), c->stream));
     HIPCHK(hipMemsetAsync(c->ray_counts.p, 0, N_RAY_COUNTS * sizeof(uint64_t), c->stream));
@@ -2130,6 +2133,7 @@ int mpt_get_stats(MptContext* c, MptStats* out) {
     out->frame_ms = c->frame_ms;
     out->graph_captures = c->graph_captures;
     out->graph_replays = c->graph_replays;
+    out->overlapped_batches = c->overlapped_batches;
     return MPT_OK;
 }
 

@@ -368,7 +368,7 @@ class Stats(C.Structure):
                 ("shade_generic_ms", C.c_double), ("shade_generic_vertices", C.c_uint64),
                 ("restir_kernel_ms", C.c_double * 5), ("restir_kernel_launches", C.c_uint32 * 5),
                 ("restir_eval_ms", C.c_double), ("restir_eval_launches", C.c_uint32), ("restir_eval_items", C.c_uint64),
-                ("graph_captures", C.c_uint32), ("graph_replays", C.c_uint32)]
+                ("graph_captures", C.c_uint32), ("graph_replays", C.c_uint32), ("overlapped_batches", C.c_uint32)]
 
 
 OK, ERR_INVALID_ARGUMENT, ERR_HIP, ERR_NO_SCENE, ERR_UNSUPPORTED, ERR_OUT_OF_MEMORY = 0, -1, -2, -3, -4, -5

@@ -445,6 +445,9 @@ typedef struct MptStats {
     /* one-sample launch sets (MPT_GRAPHS): captured HIP graphs and replays of them */
     uint32_t graph_captures;
     uint32_t graph_replays;
+    /* path-tracing batches launched as two overlapped halves on two streams (MPT_OVERLAP): their
+     * kernels share the GPU, so the per-kernel times above overlap */
+    uint32_t overlapped_batches;
 } MptStats;
 
 #define MPT_FB_COLOR 0        /* 'pixels': running SUM of samples (RenderData.h:34-36) */
