@@ -1466,8 +1466,12 @@ static int launch_batch(MptContext* c, const MptFrame* f, int batch) {
         P.rs_lo = std::max(0, cfg.own_y0 - cfg.halo_prev) * f->res_x;
         P.rs_hi = std::min(f->res_y, cfg.own_y1 + cfg.halo_prev) * f->res_x;
     }
-    const bool ovl = (c->overlap > 0 || (c->overlap < 0 && (size_t)batch * (size_t)std::max(c->n_slots, 1) <= OVERLAP_AUTO_PATHS)) &&
-                     batch >= 2 && f->options.direct_light_sampling != MPT_LSS_RESTIR_DI && c->x_per == 0 && !P.spec_as;
+    // (auto: small wavefronts, or many bounces -- the later bounces' short lists are tails too:
+    // C5 at 4K and 16 bounces 8.93 -> 8.67 ms/spp, profiles/r05v_c5_overlap_ab.jsonl)
+    const bool ovl_auto = (size_t)batch * (size_t)std::max(c->n_slots, 1) <= OVERLAP_AUTO_PATHS ||
+                          f->render_settings.nb_bounces >= 8;
+    const bool ovl = (c->overlap > 0 || (c->overlap < 0 && ovl_auto)) && batch >= 2 &&
+                     f->options.direct_light_sampling != MPT_LSS_RESTIR_DI && c->x_per == 0 && !P.spec_as;
     hipError_t e = hipSuccess;
     if (ovl) {
         int rr = ensure_overlap(c);
