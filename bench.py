@@ -88,9 +88,12 @@ def parse():
     ap.add_argument("--config-steps", type=int, default=8, help="timed steps of each extra config")
     ap.add_argument("--batch1-steps", type=int, default=8,
                     help="C3: steps also timed with one sample per wavefront (mpt_render_frame's launch set; 0 = skip)")
-    ap.add_argument("--halo", default="native", choices=["native", "python"],
+    ap.add_argument("--halo", default="auto", choices=["auto", "native", "python"],
                     help="C4 across ranks: the library's RCCL halo exchange (mpt_set_halo_native; the one-GPU "
-                         "rehearsal: its local stand-in) or the Python callback (mpt.partition.TorchHaloExchange)")
+                         "rehearsal: its local stand-in) or the Python callback (mpt.partition.TorchHaloExchange); "
+                         "auto: the Python callback over torch.distributed for world > 1 (the library's RCCL exchange "
+                         "needs the 2-GPU test tests/test_halo_native.py, which a one-GPU box skips), the native "
+                         "rehearsal for --emulate-rank-of")
     ap.add_argument("--emulate-band", type=int, default=-1,
                     help="C4 rehearsal: time only this rank's band (default: every band in turn)")
     ap.add_argument("--emulate-rank-of", type=int, default=1,
@@ -346,6 +349,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.halo == "auto":
+        a.halo = "python" if world > 1 else "native"
     dist = None
     # rehearsal of the N-rank path on a one-GPU box: MPT_BENCH_BACKEND=gloo (host-staged
     # collectives) + MPT_BENCH_SHARE_GPU=1 (every rank on device 0); not a bench line
@@ -695,6 +700,11 @@ def run_workload(a, world, rank, local, dist, coll_dev, quiet=False):
             # two halves on two streams, so this kernel's launches shared the GPU with the other
             # half's kernels -- its launch time, and with it `achieved`, is not the kernel's alone
             r["shared_gpu"] = f"{st.overlapped_batches} overlapped batch(es): launch times shared with the other half"
+        elif getattr(st, "restir_overlapped_batches", 0):
+            # MPT_RESTIR_OVERLAP: a ReSTIR DI batch's later bounces ran on the second stream beside
+            # the next batch's per-sample chain
+            r["shared_gpu"] = (f"{st.restir_overlapped_batches} overlapped ReSTIR DI batch(es): launch times shared "
+                               "with the next batch's reuse chain")
         return r
 
     dname, darch, dcus = mpt.device_info(local)

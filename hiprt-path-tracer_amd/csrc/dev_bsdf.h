@@ -934,6 +934,135 @@ DEV bool principled_sample_dir_plain(const BCtx& c, const Mat& m, VState& vs, co
     return !(dot(out, sn) < 0);
 }
 
+// The plain class's per-vertex record (k_shade<PLAIN>, Principled BSDF).  k_shade shades a plain
+// vertex only when the resolved material has zero coat, sheen, metallic, transmission and thin
+// film and the vertex is seen from outside (any other vertex is deferred to the generic kernel
+// before it writes anything), so of PEval the evaluation reads only the glossy base: the frame
+// (n, TR, BR, lvr), the specular layer's view-side terms, the diffuse colour and the GGX
+// view-only terms.  The other terms are exact constants there -- lobe weights w[4] = specular,
+// w[5] = 1 and the rest 0, so probabilities p[0..3] = p[6] = 0; the coat's clearcoat
+// compensation 1; the unrotated frame (T, B) is build_onb(n), recomputed per evaluation -- and the
+// operations on the terms kept are principled_eval_pre / _post<BC_PLAIN>'s, so the values are
+// bit-identical to PEval's.  35 dwords (an odd LDS stride, conflict-free) instead of 65: with
+// the 55 B per lane of promoted private arrays a 256-lane block needs 49.9 KB of LDS, so three
+// blocks fit a CU.
+struct PEvalP {
+    v3 n, TR, BR, lvr;
+    float p4, p5;
+    float rel;
+    uint32_t spec_ok;
+    Col spec_tint, spec_vdf, spec_dark;
+    float gbc, spec;
+    Col base;
+    float gax, gay, glv, gg1v;
+    float pad_;
+};
+DEV bool plain_vertex_ok(const Mat& m) {   // k_shade<PLAIN>: the material terms PEvalP takes as zero
+    return m.metallic == 0.0f && m.specular_transmission == 0.0f && m.thin_film == 0.0f && m.coat == 0.0f && m.sheen == 0.0f;
+}
+DEV void principled_eval_pre_plain(const BCtx& c, const Mat& m, const VState& vs, v3 view, v3 sn, PEvalP& e) {
+    v3 n = sn;
+    const bool outside = dot(view, n) > 0 || m.thin_walled;
+    if (dot(view, n) < 0.0f) n = -n;
+    e.n = n;
+    e.spec = m.specular;
+    e.base = C3(m.base_color);
+    v3 T, B;
+    build_onb(n, T, B);
+    const v3 lv = to_local(T, B, n, view);
+    build_rotated_onb(n, e.TR, e.BR, m.anisotropy_rotation * PI);
+    e.lvr = to_local(e.TR, e.BR, n, view);
+    alphas(m.roughness, m.anisotropy, e.gax, e.gay);
+    e.glv = lambda_smith(e.gax, e.gay, e.lvr);
+    e.gg1v = 1.0f / (1.0f + e.glv);
+    float w[7], p[7];
+    lobe_weights(m, outside, w);
+    const float inc = ior_or_air(c, vs.incident);
+    lobe_probas(w, p);
+    e.p4 = p[4];
+    e.p5 = p[5];
+    e.rel = 1.0f;
+    e.spec_ok = 0u;
+    e.spec_tint = col(1.0f); e.spec_vdf = col(0.0f); e.spec_dark = col(1.0f);
+    if (w[4] > 0.0f) {
+        e.rel = spec_rel_ior(m, inc);
+        const bool ok = absr(e.rel - 1.0f) > 1.0e-3f;
+        e.spec_ok = ok ? 1u : 0u;
+        if (ok) {
+            e.spec_tint = lerpc(col(1.0f), m.specular_tint * C3(m.specular_color), m.specular);
+            e.spec_vdf = spec_fresnel_v<BC_PLAIN>(m, 0.0f, 0.0f, e.rel, e.lvr.z);
+            e.spec_dark = spec_darkening(m, e.rel);
+        }
+    }
+    e.gbc = glossy_base_comp(c, m, inc, lv.z);
+    e.pad_ = 0.0f;
+}
+DEV Col principled_eval_post_plain(const BCtx& c, const Mat& m, const PEvalP& e, v3 sn, v3 L, float& pdf) {
+    pdf = 0.0f;
+    const bool refracting = dot(sn, L) < 0.0f;   // (seen from outside)
+    const v3 n = e.n;
+    v3 T, B;
+    build_onb(n, T, B);
+    const v3 ll = to_local(T, B, n, L);
+    const v3 llr = to_local(e.TR, e.BR, n, L);
+    const v3 lhr = normalize(e.lvr + llr);
+    Col thr = col(1.0f), fc = col(0.0f);
+    const float nr = refracting ? 0.0f : 1.0f;
+    Col g = col(0.0f);
+    const float ws = e.spec * nr;
+    if (ws > 0.0f) {
+        float sp;
+        Col ct = ts_ggx0_v(c, e.gax, e.gay, e.glv, e.gg1v, spec_fresnel_v<BC_PLAIN>(m, 0.0f, 0.0f, e.rel, dot(llr, lhr)), e.lvr, llr,
+                           lhr, sp);
+        if (e.spec_ok) {
+            ct *= e.spec_tint;
+            ct *= ws;
+            ct *= thr;
+            Col att = col(1.0f);
+            att *= col(1.0f) - spec_fresnel_v<BC_PLAIN>(m, 0.0f, 0.0f, e.rel, llr.z);
+            att *= col(1.0f) - e.spec_vdf;
+            att *= e.spec_dark;
+            att = lerpc(col(1.0f), att, e.spec);
+            thr *= att;
+        }
+        pdf += sp * e.p4;
+        g += ct;
+    }
+    const float wd = 1.0f * nr;
+    if (wd > 0.0f) {
+        float dp;
+        Col ct = lambert_eval_c(e.base, ll.z, dp);
+        ct *= wd;
+        ct *= thr;
+        pdf += dp * e.p5;
+        g += ct;
+    }
+    fc += g / e.gbc;
+    return fc;   // (the clearcoat compensation of a coat-less material divides by 1)
+}
+// principled_sample_dir_plain from the plain record: c0 .. c3 are 0 (p[0..3] = 0), so the
+// second-roughness metal branch is never taken
+DEV bool principled_sample_dir_plain(const BCtx& c, const Mat& m, VState& vs, const PEvalP& e, v3 view, v3 sn, v3 gn, v3& out,
+                                      Rng& rng) {
+    const float c4 = 0.0f + e.p4, c5 = c4 + e.p5;
+    float r1 = rng();
+    if (r1 > c5) {
+        v3 n = sn;
+        float ds = dot(view, sn), dg = dot(view, gn);
+        if (ds * dg < 0) n = reflect_ray(sn, gn);
+        if (dot(view, n) < 0) n = -n;
+        v3 TR, BR;
+        build_rotated_onb(n, TR, BR, m.anisotropy_rotation * PI);
+        out = to_world(TR, BR, n, glass_sample<BC_PLAIN>(c, m, vs, to_local(TR, BR, n, view), rng));
+        return true;
+    }
+    vs_pop(vs, false);
+    if (r1 < c4) out = to_world(e.TR, e.BR, e.n, ggx_sample_reflection_a(e.gax, e.gay, e.lvr, rng));
+    else if (r1 < c5) out = cosine_sample_around(e.n, rng);
+    else out = to_world(e.TR, e.BR, e.n, glass_sample<BC_PLAIN>(c, m, vs, e.lvr, rng));
+    return !(dot(out, sn) < 0);
+}
+
 DEV Col principled_sample(const BCtx& c, const Mat& m, VState& vs, v3 view, v3 sn, v3 gn, v3& out, float& pdf, Rng& rng) {
     pdf = 0.0f;
     if (!principled_sample_dir(c, m, vs, view, sn, gn, out, rng)) return col(0.0f);
@@ -968,6 +1097,17 @@ DEV Col bsdf_eval_post(const BCtx& c, const Mat& m, VState& vs, const PEval& e, 
     if (OVERRIDE == MPT_BSDF_LAMBERTIAN) return lambert_eval(m, dot(L, sn), pdf);
     if (OVERRIDE == MPT_BSDF_OREN_NAYAR) return oren_nayar_eval(m, e.lv, to_local(e.T, e.B, sn, L), pdf);
     return principled_eval_post<FULL>(c, m, vs, e, sn, L, pdf);
+}
+// the plain record (k_shade<PLAIN>, Principled only)
+template <int OVERRIDE, int FULL = BC_FULL>
+DEV void bsdf_eval_pre(const BCtx& c, const Mat& m, const VState& vs, v3 view, v3 sn, PEvalP& e) {
+    static_assert(OVERRIDE == MPT_BSDF_NONE && FULL == BC_PLAIN, "PEvalP: the plain class of the Principled BSDF");
+    principled_eval_pre_plain(c, m, vs, view, sn, e);
+}
+template <int OVERRIDE, int FULL = BC_FULL>
+DEV Col bsdf_eval_post(const BCtx& c, const Mat& m, VState&, const PEvalP& e, v3 sn, v3 L, float& pdf) {
+    static_assert(OVERRIDE == MPT_BSDF_NONE && FULL == BC_PLAIN, "PEvalP: the plain class of the Principled BSDF");
+    return principled_eval_post_plain(c, m, e, sn, L, pdf);
 }
 // sample = sample_dir + bsdf_eval on the updated state (eval skipped when sample_dir is false)
 template <int OVERRIDE, int FULL = BC_FULL>

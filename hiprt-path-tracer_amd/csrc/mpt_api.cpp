@@ -86,9 +86,6 @@ constexpr int FRAME_RING = 256;   // >= 2 x MPT_MAX_BATCH
 constexpr int RESTIR_MAX_BATCH = 128;
 // x2: the two halves of an overlapped batch
 constexpr int EV_POOL = 2 * 2 * ((10 * 65 + 3 + 8) > 50 * RESTIR_MAX_BATCH ? (10 * 65 + 3 + 8) : 50 * RESTIR_MAX_BATCH);
-#ifndef MPT_TRACE_BLOCKS_PER_CU
-#define MPT_TRACE_BLOCKS_PER_CU 5
-#endif
 constexpr int SPILL_WORDS = 2 * TRAV_SPILL_DEPTH;
 constexpr int MAX_STACK = TRAV_LDS_STACK + TRAV_SPILL_DEPTH;
 
@@ -271,6 +268,13 @@ struct MptContext {
     int halo_native = 0;
     DBuf<uint8_t> halo_scratch;           // rehearsal: where the bytes go
     DBuf<int32_t> halo_agree;             // device word of the halo agreement (ncclAllReduce max)
+    std::vector<MptHaloOp> halo_plan_ops; // the exchange point's operations (native_halo)
+    uint64_t halo_exchanges = 0, halo_agreements = 0, halo_bytes_sent = 0, halo_bytes_recv = 0;   // MptStats
+    uint32_t restir_overlapped_batches = 0;
+    // upper bound of pixel_sample_count over the partition's pixels (restir_gate_static): a reset
+    // frame restarts it, every frame with the adaptive buffers adds at most one sample; unknown
+    // (large) until a reset frame has been launched
+    int as_bound = 1 << 30;
     DBuf<uint8_t> comm_send, comm_recv;
 };
 
@@ -507,6 +511,7 @@ int ensure_paths(MptContext* c, int rx, int ry, int bh, int bi, int bc) {
     HIPCHK(drain(c));
     release_batch(c);                       // sized for the previous partition
     c->res_x = c->res_y = c->n_slots = 0;   // no partition until the group below is complete
+    c->as_bound = 1 << 30;
     const size_t N = (size_t)std::max(n, 1);
     hipStream_t st = c->stream;
     Allocs A;
@@ -662,7 +667,12 @@ int ensure_restir(MptContext* c, const MptFrame* f) {
     size_t npl = (size_t)std::max(1, rd.number_of_subsets * rd.subset_size);
     hipStream_t st = c->stream;
     Allocs A;
+    // every reallocating branch first drains both streams: an overlapped ReSTIR DI wavefront on
+    // stream2 may still read the G-buffer, reservoir and staged-ray planes (as in ensure_batch)
+    bool drained = false;
+    auto D = [&] { if (!drained) { A(drain(c)); drained = true; } };
     if (c->rs_init.n != 3 * N) {
+        D();
         A(c->gb_pos, N); A(c->gb_sn, N); A(c->gb_gn, N); A(c->gb_view, N);
         A(c->pgb_pos, N); A(c->pgb_sn, N); A(c->pgb_gn, N); A(c->pgb_view, N);
         A(c->gb_meta, N); A(c->pgb_meta, N);
@@ -685,10 +695,12 @@ int ensure_restir(MptContext* c, const MptFrame* f) {
         c->restir_out_sp2 = 0;
     }
     if ((c->any_tex || f->bsdf_flags.white_furnace_mode) && c->gb_mat.n < N) {
+        D();
         A(c->gb_mat, N);
         A(c->pgb_mat, N);
     }
     if (c->band_c > 1 && c->rs_conv.n != N) {
+        D();
         A(c->rs_conv, N);
         if (A.e == hipSuccess) A(hipMemsetAsync(c->rs_conv.p, 0xff, N * sizeof(int32_t), st));
     }
@@ -706,20 +718,23 @@ int ensure_restir(MptContext* c, const MptFrame* f) {
         if (c->restir_chunk < 0 && ck < 4) ck = 1;
         ck = std::max(1, std::min(ck, RS_RPP_HOST));
         if (c->rq_o.n != ns * RS_RPP_HOST) {
+            D();
             A(c->rq_o, ns * RS_RPP_HOST); A(c->rq_d, ns * RS_RPP_HOST); A(c->rq_key, ns * RS_RPP_HOST);
             A(c->rq_occ, ns * RS_RPP_HOST); A(c->rq_list, ns * RS_RPP_HOST); A(c->rq_items, 2 * ns * RS_RPP_HOST);
         }
         if (c->rq_meta.n != ns * ck) {
+            D();
             A(c->rq_meta, ns * ck); A(c->rq_rec, ns * std::max(RS_REC_HOST, 2 * ck));
         }
         const bool mat = c->any_tex || f->bsdf_flags.white_furnace_mode;
         if (ck > 1 && (c->ci_chunk != ck || c->ci_pos.n != ns * ck || (mat && c->ci_mat.n != ns * ck))) {
+            D();
             const size_t m = ns * ck;
             A(c->ci_pos, m); A(c->ci_sn, m); A(c->ci_gn, m); A(c->ci_view, m); A(c->ci_meta, m);
             A(c->ci_vsA, m); A(c->ci_vsB, m); A(c->ci_cs, 4 * m); A(c->ci_rs, 3 * m);
             if (mat) A(c->ci_mat, m);
         }
-        if (ck > 1 && c->ci_pl.n != 4 * npl * ck) A(c->ci_pl, 4 * npl * ck);
+        if (ck > 1 && c->ci_pl.n != 4 * npl * ck) { D(); A(c->ci_pl, 4 * npl * ck); }
         c->ci_chunk = ck;
         DevPaths& d = c->ci_dp;
         d.gb_pos = c->ci_pos.p; d.gb_sn = c->ci_sn.p; d.gb_gn = c->ci_gn.p; d.gb_view = c->ci_view.p; d.gb_meta = c->ci_meta.p;
@@ -727,6 +742,7 @@ int ensure_restir(MptContext* c, const MptFrame* f) {
         d.rs_init = c->ci_rs.p; d.rs_plights = c->ci_pl.p;
     }
     if (c->rs_plights.n != 4 * npl) {
+        D();
         A(c->rs_plights, 4 * npl);
         if (A.e == hipSuccess) A(launch_restir_fill_lights(c->rs_plights.p, (int)npl, st));
     }
@@ -916,8 +932,9 @@ static int create_context(MptContext* c, int device, void* hip_stream) {
     HIPCHK(c->status.alloc(4));
     HIPCHK(hipMemsetAsync(c->status.p, 0, 4 * sizeof(uint32_t), c->stream));
     HIPCHK(hipMemsetAsync(c->ray_counts.p, 0, N_RAY_COUNTS * sizeof(uint64_t), c->stream));
-    // traversal spill stacks per lane of a persistent grid: up to 8 blocks per CU (launch_trace_mode)
-    HIPCHK(c->spill.alloc((size_t)c->num_cus * 8 * TRAV_BLOCK * SPILL_WORDS));
+    // traversal spill stacks per lane of the largest persistent grid (path or list mode,
+    // launch_trace_mode): TRACE_SPILL_BLOCKS_PER_CU blocks per CU
+    HIPCHK(c->spill.alloc((size_t)c->num_cus * TRACE_SPILL_BLOCKS_PER_CU * TRAV_BLOCK * SPILL_WORDS));
     HIPCHK(c->srgb.alloc(256));
     HIPCHK(launch_srgb_table(c->srgb.p, c->stream));
     return MPT_OK;
@@ -1290,7 +1307,11 @@ static int prepare_batch(MptContext* c, const MptFrame* f, int batch) {
         return fail(MPT_ERR_OUT_OF_MEMORY, "wavefront above MPT_MAX_WAVEFRONT_PATHS paths");
     // overlapped ReSTIR DI batches need both halves of the path state (2 x the batch); without
     // the room they run one after the other
-    const bool want_overlap = f->options.direct_light_sampling == MPT_LSS_RESTIR_DI && batch > 1 && c->restir_overlap &&
+    // (not under adaptive sampling: the next batch's camera gate reads the converged counts this
+    // batch's k_accumulate writes at its end)
+    const MptRenderSettings& frs = f->render_settings;
+    const bool adaptive = (frs.stop_pixel_noise_threshold > 0.0f || frs.enable_adaptive_sampling) && frs.accumulate;
+    const bool want_overlap = f->options.direct_light_sampling == MPT_LSS_RESTIR_DI && batch > 1 && c->restir_overlap && !adaptive &&
                               ext_layout(*f, nullptr) == 0 && (int64_t)std::max(c->n_slots, 1) * 2 * batch <= MPT_MAX_WAVEFRONT_PATHS;
     c->restir_overlap_ok = false;
     if (want_overlap) {
@@ -1397,6 +1418,16 @@ static hipError_t launch_frame_graph(MptContext* c, const DevPaths& P, const Mpt
     return hipGraphLaunch(c->graph_exec, c->stream);
 }
 
+static bool is_reset(const MptFrame& f) { return f.render_settings.sample_number == 0 || f.render_settings.need_to_reset; }
+static bool has_adaptive(const MptFrame& f) {   // RenderSettings.h:207-218 (has_adaptive_buffers)
+    const MptRenderSettings& rs = f.render_settings;
+    return (rs.stop_pixel_noise_threshold > 0.0f || rs.enable_adaptive_sampling) && rs.accumulate;
+}
+static int next_as_bound(int b, const MptFrame& f) {
+    if (!has_adaptive(f)) return b;
+    if (is_reset(f)) b = 0;
+    return b < (1 << 30) ? b + 1 : b;
+}
 // Enqueues a prepared wavefront (prepare_batch).
 static int launch_batch(MptContext* c, const MptFrame* f, int batch) {
     const bool restir_part = f->options.direct_light_sampling == MPT_LSS_RESTIR_DI && f->band_count > 1;
@@ -1528,6 +1559,7 @@ static int launch_batch(MptContext* c, const MptFrame* f, int batch) {
             HIPCHK(hipEventRecord(c->ev_half[h], c->stream2));
             c->ev_half_used[h] = true;
             c->wave_pending = true;
+            c->restir_overlapped_batches++;
         } else {
             e = launch_frames_restir(dev_scene(c), P, c->d_frames + slot, c->h_frames + slot, batch, cfg, c->stream);
         }
@@ -1548,6 +1580,7 @@ static int launch_batch(MptContext* c, const MptFrame* f, int batch) {
     }
     c->frames_submitted++;
     c->frames += batch;
+    for (int k = 0; k < batch; k++) c->as_bound = next_as_bound(c->as_bound, f[k]);
     c->trace_launches += cfg.launches;
     return MPT_OK;
 }
@@ -1599,9 +1632,8 @@ static bool batchable(const MptContext* c, const MptFrame& a, const MptFrame& b)
     if (is_low_res(a)) return false;   // interactive frames: one sample each (RenderWindow.cpp:798-802)
     const MptRenderSettings& rs = a.render_settings;
     // adaptive sampling / the stop-noise threshold: traced speculatively and gated in sample order
-    // by k_accumulate (not under ReSTIR DI, whose reuse passes read neighbours' converged counts)
-    if ((rs.stop_pixel_noise_threshold > 0.0f || rs.enable_adaptive_sampling) && rs.accumulate &&
-        (restir || !c->adaptive_batch))
+    // by k_accumulate (under ReSTIR DI only while the gate is static: restir_gate_static)
+    if ((rs.stop_pixel_noise_threshold > 0.0f || rs.enable_adaptive_sampling) && rs.accumulate && !c->adaptive_batch)
         return false;
     MptFrame t = b;
     t.render_settings.sample_number = a.render_settings.sample_number;
@@ -1618,6 +1650,24 @@ static bool batchable(const MptContext* c, const MptFrame& a, const MptFrame& b)
         std::memcpy(t.restir_di_seeds, a.restir_di_seeds, sizeof(t.restir_di_seeds));
     }
     return std::memcmp(&t, &a, sizeof(MptFrame)) == 0;
+}
+
+// Batched ReSTIR DI under adaptive sampling (CameraRays.h:93-125, AdaptiveSampling.h:11-104): the
+// reuse passes of sample s read which pixels are active at s and the neighbours' converged counts
+// (Utils.h:289-339), i.e. the gate of sample s, which needs the radiance of every earlier sample --
+// known only after the batch's later bounces.  The gate is static while no pixel can reach its
+// noise test (pixel_sample_count > adaptive_sampling_min_samples): it then refuses exactly the
+// pixels that had converged before the batch (sticky) and passes the others, and the converged
+// counts do not change.  So frame i + k may join a run starting at frame i when neither is a reset
+// frame (a reset clears the converged counts the passes read) and the host's bound on
+// pixel_sample_count before it, as_bound + k, is at most the minimum.  The stop-noise threshold
+// alone never refuses a sample and the passes do not read its counts: always static.
+static bool restir_gate_static(const MptContext* c, const MptFrame* run, int k) {
+    const MptFrame& a = run[0];
+    const MptRenderSettings& rs = a.render_settings;
+    if (a.options.direct_light_sampling != MPT_LSS_RESTIR_DI || !rs.enable_adaptive_sampling || !rs.accumulate) return true;
+    if (is_reset(a) || is_reset(run[k])) return false;
+    return (int64_t)c->as_bound + k <= (int64_t)rs.adaptive_sampling_min_samples;
 }
 
 // The overlapped ReSTIR DI wavefronts of the call joined into the context's stream: everything
@@ -1649,7 +1699,7 @@ int mpt_render_frames(MptContext* c, const MptFrame* frames, int32_t count, int3
     int i = 0;
     while (i < count) {
         int b = 1;
-        while (i + b < count && b < max_batch && batchable(c, frames[i], frames[i + b])) b++;
+        while (i + b < count && b < max_batch && batchable(c, frames[i], frames[i + b]) && restir_gate_static(c, frames + i, b)) b++;
         int r = prepare_batch(c, frames + i, b);
         // a wavefront that does not fit in device memory is halved (bit-identical result),
         // and the smaller size is kept for the rest of the call
@@ -1937,34 +1987,62 @@ int band_overlap(int a0, int a1, int b0, int b1, int& lo, int& hi) {
     hi = std::min(a1, b1);
     return lo < hi;
 }
+// The point-to-point operations of one exchange point for band k of n (band_height rows, the
+// agreed halo h), in the order they are issued: per peer p != k in increasing order, per buffer
+// i, this band's rows in p's upper then lower halo (sends), then p's rows in this band's upper
+// then lower halo (receives).  Peer p derives its receives from k and sends to k in the same
+// order, so the operations pair up (ncclSend / ncclRecv match in issue order per peer); the
+// receive ranges are mpt.partition.halo_plan's (tests/test_halo_plan.py).
+void halo_ops(int res_y, int bh, int n, int k, int h, int n_buffers, std::vector<MptHaloOp>& ops) {
+    ops.clear();
+    auto need = [&](int q, int& a0, int& a1, int& b0, int& b1) {   // band q's halo ranges
+        const int q0 = std::min(res_y, q * bh), q1 = std::min(res_y, q0 + bh);
+        a0 = std::max(0, q0 - h); a1 = q0; b0 = q1; b1 = std::min(res_y, q1 + h);
+        return q0 < q1;
+    };
+    const int m0 = std::min(res_y, k * bh), m1 = std::min(res_y, m0 + bh);
+    int a0, a1, b0, b1;
+    const bool mine = need(k, a0, a1, b0, b1);
+    for (int p = 0; p < n; p++) {
+        if (p == k) continue;
+        const int p0 = std::min(res_y, p * bh), p1 = std::min(res_y, p0 + bh);
+        int c0, c1, d0, d1, lo, hi;
+        const bool theirs = need(p, c0, c1, d0, d1);
+        for (int i = 0; i < n_buffers; i++) {
+            if (theirs && band_overlap(c0, c1, m0, m1, lo, hi)) ops.push_back({p, 0, i, lo, hi});
+            if (theirs && band_overlap(d0, d1, m0, m1, lo, hi)) ops.push_back({p, 0, i, lo, hi});
+            if (mine && band_overlap(a0, a1, p0, p1, lo, hi)) ops.push_back({p, 1, i, lo, hi});
+            if (mine && band_overlap(b0, b1, p0, p1, lo, hi)) ops.push_back({p, 1, i, lo, hi});
+        }
+    }
+}
 int native_halo(void* user, MptHaloExchange* x) {
     MptContext* c = (MptContext*)user;
     hipStream_t st = (hipStream_t)x->stream;
-    const int h0 = x->halo_rows;
+    std::vector<MptHaloOp>& ops = c->halo_plan_ops;
+    auto count = [&](int recv) {
+        size_t bytes = 0;
+        for (const MptHaloOp& o : ops)
+            if (o.recv == recv) bytes += (size_t)(o.row_hi - o.row_lo) * (size_t)x->res_x * (size_t)x->bytes_per_pixel[o.buffer];
+        return bytes;
+    };
     if (c->halo_native == 2) {
         // rehearsal on one GPU: the bytes this rank would receive, moved by one device copy (an
         // exchange is one grouped send / receive); a moving camera's agreement waits as the
         // all-reduce's read-back would
         if (x->phase == MPT_HALO_GBUFFER && !x->halo_agreed && hipStreamSynchronize(st) != hipSuccess) return 1;
-        const int n = std::max(1, c->band_c), bh = c->band_h, k = c->band_i;
-        size_t bytes = 0;
-        for (int p = 0; p < n; p++) {
-            if (p == k) continue;
-            const int p0 = std::min(x->res_y, p * bh), p1 = std::min(x->res_y, p0 + bh);
-            int lo, hi;
-            for (int i = 0; i < x->n_buffers; i++) {
-                const size_t row = (size_t)x->res_x * (size_t)x->bytes_per_pixel[i];
-                if (band_overlap(std::max(0, x->own_y0 - h0), x->own_y0, p0, p1, lo, hi)) bytes += (size_t)(hi - lo) * row;
-                if (band_overlap(x->own_y1, std::min(x->res_y, x->own_y1 + h0), p0, p1, lo, hi)) bytes += (size_t)(hi - lo) * row;
-            }
-        }
+        halo_ops(x->res_y, c->band_h, std::max(1, c->band_c), c->band_i, x->halo_rows, x->n_buffers, ops);
+        const size_t bytes = count(1);
+        c->halo_exchanges++;
+        c->halo_bytes_recv += bytes;
+        c->halo_bytes_sent += count(0);
         if (bytes == 0) return 0;
         if (c->halo_scratch.n < 2 * bytes && c->halo_scratch.alloc(2 * bytes) != hipSuccess) return 1;
         return hipMemcpyAsync(c->halo_scratch.p + bytes, c->halo_scratch.p, bytes, hipMemcpyDeviceToDevice, st) == hipSuccess ? 0 : 1;
     }
     Rccl& r = *rccl_lib();
     if (!c->comm || !r.send || !r.recv || !r.group_start || !r.group_end || !r.all_reduce) return 2;
-    const int n = c->comm_size, k = c->comm_rank, bh = c->band_h;
+    const int n = c->comm_size, k = c->comm_rank;
     if (c->band_c != n || c->band_i != k) return 4;   // rank k must render band k of ranks
     if (x->phase == MPT_HALO_GBUFFER && !x->halo_agreed) {
         if (c->halo_agree.n < 1 && c->halo_agree.alloc(1) != hipSuccess) return 1;
@@ -1974,37 +2052,37 @@ int native_halo(void* user, MptHaloExchange* x) {
         if (hipMemcpyAsync(&v, c->halo_agree.p, sizeof(v), hipMemcpyDeviceToHost, st) != hipSuccess ||
             hipStreamSynchronize(st) != hipSuccess) return 1;
         x->halo_rows = v;
+        c->halo_agreements++;
     }
-    const int h = x->halo_rows;
-    auto need = [&](int q, int& a0, int& a1, int& b0, int& b1) {   // band q's halo ranges
-        const int q0 = std::min(x->res_y, q * bh), q1 = std::min(x->res_y, q0 + bh);
-        a0 = std::max(0, q0 - h); a1 = q0; b0 = q1; b1 = std::min(x->res_y, q1 + h);
-        return q0 < q1;
-    };
-    const int m0 = std::min(x->res_y, k * bh), m1 = std::min(x->res_y, m0 + bh);
+    halo_ops(x->res_y, c->band_h, n, k, x->halo_rows, x->n_buffers, ops);
+    c->halo_exchanges++;
+    c->halo_bytes_recv += count(1);
+    c->halo_bytes_sent += count(0);
+    if (ops.empty()) return 0;
     int rc = r.group_start();
-    for (int p = 0; p < n && rc == 0; p++) {
-        if (p == k) continue;
-        const int p0 = std::min(x->res_y, p * bh), p1 = std::min(x->res_y, p0 + bh);
-        int a0, a1, b0, b1, lo, hi;
-        const bool mine = need(k, a0, a1, b0, b1);
-        int c0, c1, d0, d1;
-        const bool theirs = need(p, c0, c1, d0, d1);
-        for (int i = 0; i < x->n_buffers && rc == 0; i++) {
-            uint8_t* buf = (uint8_t*)x->buffers[i];
-            const size_t row = (size_t)x->res_x * (size_t)x->bytes_per_pixel[i];
-            // this band's rows in peer p's halo
-            if (theirs && band_overlap(c0, c1, m0, m1, lo, hi)) rc = r.send(buf + lo * row, (hi - lo) * row, NCCL_UINT8, p, c->comm, st);
-            if (rc == 0 && theirs && band_overlap(d0, d1, m0, m1, lo, hi)) rc = r.send(buf + lo * row, (hi - lo) * row, NCCL_UINT8, p, c->comm, st);
-            // peer p's rows in this band's halo
-            if (rc == 0 && mine && band_overlap(a0, a1, p0, p1, lo, hi)) rc = r.recv(buf + lo * row, (hi - lo) * row, NCCL_UINT8, p, c->comm, st);
-            if (rc == 0 && mine && band_overlap(b0, b1, p0, p1, lo, hi)) rc = r.recv(buf + lo * row, (hi - lo) * row, NCCL_UINT8, p, c->comm, st);
-        }
+    for (size_t j = 0; j < ops.size() && rc == 0; j++) {
+        const MptHaloOp& o = ops[j];
+        uint8_t* buf = (uint8_t*)x->buffers[o.buffer];
+        const size_t row = (size_t)x->res_x * (size_t)x->bytes_per_pixel[o.buffer];
+        uint8_t* at = buf + (size_t)o.row_lo * row;
+        const size_t len = (size_t)(o.row_hi - o.row_lo) * row;
+        rc = o.recv ? r.recv(at, len, NCCL_UINT8, o.peer, c->comm, st) : r.send(at, len, NCCL_UINT8, o.peer, c->comm, st);
     }
     const int re = r.group_end();
     return rc != 0 ? 3 : (re != 0 ? 3 : 0);
 }
 }  // namespace
+
+int mpt_halo_plan(int32_t res_y, int32_t band_height, int32_t band_count, int32_t band_index, int32_t halo_rows,
+                  int32_t n_buffers, MptHaloOp* out, int32_t cap) {
+    if (res_y <= 0 || band_height <= 0 || band_count <= 0 || band_index < 0 || band_index >= band_count || halo_rows < 0 ||
+        n_buffers < 0 || n_buffers > MPT_HALO_MAX_BUFFERS || cap < 0 || (cap > 0 && !out))
+        return fail(MPT_ERR_INVALID_ARGUMENT, "mpt_halo_plan: bad partition, halo or output");
+    std::vector<MptHaloOp> ops;
+    halo_ops(res_y, band_height, band_count, band_index, halo_rows, n_buffers, ops);
+    for (size_t j = 0; j < ops.size() && (int32_t)j < cap; j++) out[j] = ops[j];
+    return (int)ops.size();
+}
 
 int mpt_set_halo_native(MptContext* c, int32_t mode) {
     if (!c) return fail(MPT_ERR_INVALID_ARGUMENT, "NULL context");
@@ -2078,6 +2156,8 @@ int mpt_enable_stats(MptContext* c, int enable, int instrumented) {
     c->frame_ms = 0.0;
     c->graph_captures = c->graph_replays = 0;
     c->overlapped_batches = 0;
+    c->halo_exchanges = c->halo_agreements = c->halo_bytes_sent = c->halo_bytes_recv = 0;
+    c->restir_overlapped_batches = 0;
     for (int m = 0; m < KT_COUNT; m++) { c->stage_ms[m] = 0.0; c->stage_launches[m] = 0; }
     HIPCHK(hipMemsetAsync(c->stats.p, 0, N_STATS * sizeof(uint64_t), c->stream));
     HIPCHK(hipMemsetAsync(c->ray_counts.p, 0, N_RAY_COUNTS * sizeof(uint64_t), c->stream));
@@ -2138,6 +2218,11 @@ int mpt_get_stats(MptContext* c, MptStats* out) {
     out->graph_captures = c->graph_captures;
     out->graph_replays = c->graph_replays;
     out->overlapped_batches = c->overlapped_batches;
+    out->halo_exchanges = c->halo_exchanges;
+    out->halo_agreements = c->halo_agreements;
+    out->halo_bytes_sent = c->halo_bytes_sent;
+    out->halo_bytes_received = c->halo_bytes_recv;
+    out->restir_overlapped_batches = c->restir_overlapped_batches;
     return MPT_OK;
 }
 

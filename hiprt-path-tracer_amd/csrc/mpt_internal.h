@@ -23,6 +23,28 @@ constexpr int TRAV_BLOCK = 256;
 constexpr int TRAV_LDS_STACK = MPT_LDS_STACK;
 constexpr int TRAV_SPILL_DEPTH = 64 - TRAV_LDS_STACK;
 
+// persistent traversal grid: MPT_TRACE_BLOCKS_PER_CU blocks of TRAV_BLOCK lanes per CU for the
+// path / NEE modes (MPT_TRACE_WAVES waves per SIMD), the staged ReSTIR DI list modes scaled to
+// MPT_TRACE_WAVES_LIST; every lane of such a grid owns TRAV_SPILL_DEPTH spill entries in HBM,
+// indexed by its global thread id, so the spill area is sized for the larger of the two grids
+#ifndef MPT_TRACE_BLOCKS_PER_CU
+#define MPT_TRACE_BLOCKS_PER_CU 5
+#endif
+#ifndef MPT_TRACE_WAVES
+#define MPT_TRACE_WAVES 5   // 5 waves / SIMD (<= 96 VGPRs): C3 traversal -4 % vs 4 (VGPR-capped), 6 and 8 no better (r02 A/B)
+#endif
+#ifndef MPT_TRACE_WAVES_LIST
+#define MPT_TRACE_WAVES_LIST MPT_TRACE_WAVES   // the ReSTIR DI staged lists (TM_LIST_ANY / TM_LIST_CLOSEST)
+#endif
+#ifndef MPT_TRACE_WAVES_PATH
+#define MPT_TRACE_WAVES_PATH MPT_TRACE_WAVES
+#endif
+// blocks per CU of the list-mode grid (launch_trace_mode: grid / MPT_TRACE_WAVES * MPT_TRACE_WAVES_LIST)
+constexpr int TRACE_LIST_BLOCKS_PER_CU = MPT_TRACE_BLOCKS_PER_CU * MPT_TRACE_WAVES_LIST / MPT_TRACE_WAVES;
+constexpr int TRACE_SPILL_BLOCKS_PER_CU =
+    MPT_TRACE_BLOCKS_PER_CU > TRACE_LIST_BLOCKS_PER_CU ? MPT_TRACE_BLOCKS_PER_CU : TRACE_LIST_BLOCKS_PER_CU;
+static_assert(MPT_TRACE_BLOCKS_PER_CU >= 1 && MPT_TRACE_WAVES >= 1 && MPT_TRACE_WAVES_LIST >= 1, "traversal grid");
+
 struct DevScene {
     const Node8* nodes;
     const TriRec* tris;
@@ -165,6 +187,7 @@ struct DevPaths {
     int32_t* as_conv;         // pixel_converged_sample_count (-1 = not converged)
     uint8_t* active;          // pixel_active
     int32_t spec_as;          // a batch of adaptive samples: traced speculatively, gated in k_accumulate
+    int32_t spec_reset;       // (k_camera, one sample of a batch) an earlier sample of the batch resets the buffers
     uint32_t* status;         // [0] stop_noise_threshold_converged_count, [1] still_one_ray_active
     // ReSTIR DI (LSS_RESTIR_DI only; NULL otherwise).  G-buffer of the camera hits as
     // CameraRays writes it (CameraRays.h:144-166, GBuffer.h:17-34), current + previous frame:
@@ -191,6 +214,7 @@ struct DevPaths {
     float4* rs_keep;          // batched ReSTIR DI: each sample's final reservoirs (sample-major, rs_keep_n pixels each)
     int64_t rs_keep_n;
     int rs_keep_on;           // k_shade's final shading reads rs_keep by (sample, pixel) instead of rs_out
+    int32_t cam_noqueue;      // k_camera writes no camera queue (batched ReSTIR DI builds it from `active`)
     float4* rs_plights;       // presampled lights (4 float4 each)
     // The G-buffer / reservoir / rs_conv arrays are frame-sized and indexed by the global
     // pixel index; path-state slot s of this context is pixel s + pix_off (contiguous band).

@@ -30,6 +30,7 @@
 #include <cfloat>
 #include <cstring>
 #include <initializer_list>
+#include <type_traits>
 #include <utility>
 
 #include "dev_bsdf.h"
@@ -402,15 +403,6 @@ DEV uint32_t pixel_seed(const MptFrame& F, uint32_t pix);
 DEV uint32_t camera_seed(const MptFrame& F, uint32_t pix);
 DEV uint32_t path_seed(const MptFrame* Fp, const DevPaths& P, int slot, bool camera);
 
-#ifndef MPT_TRACE_WAVES
-#define MPT_TRACE_WAVES 5   // 5 waves / SIMD (<= 96 VGPRs): C3 traversal -4 % vs 4 (VGPR-capped), 6 and 8 no better (r02 A/B)
-#endif
-#ifndef MPT_TRACE_WAVES_LIST
-#define MPT_TRACE_WAVES_LIST MPT_TRACE_WAVES   // the ReSTIR DI staged lists (TM_LIST_ANY / TM_LIST_CLOSEST)
-#endif
-#ifndef MPT_TRACE_WAVES_PATH
-#define MPT_TRACE_WAVES_PATH MPT_TRACE_WAVES
-#endif
 template <int MODE, bool STATS>
 __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(
     MODE == TM_PATH ? MPT_TRACE_WAVES_PATH : (MODE == TM_LIST_ANY || MODE == TM_LIST_CLOSEST) ? MPT_TRACE_WAVES_LIST : MPT_TRACE_WAVES)))
@@ -915,15 +907,29 @@ __global__ __launch_bounds__(TB) void k_camera(DevPaths P, const MptFrame* __res
     if (slot < P.n) batch_split(P, slot, pslot, sub);   // batched launches never use the adaptive buffers
     const MptFrame& F = Fp[sub];
     const MptRenderSettings& rs = F.render_settings;
-    // a batch of adaptive samples is traced speculatively: every slot gets its camera ray and
-    // k_accumulate replays the gate in sample order (P.spec_as)
+    // a batch of adaptive samples is traced speculatively: k_accumulate replays the gate in sample
+    // order (P.spec_as).  Under enable_adaptive_sampling a converged pixel stays converged
+    // (AdaptiveSampling.h:45-48: the gate refuses it while pixel_converged_sample_count != -1) until
+    // a reset, so a pixel that had converged before the batch began -- with no reset frame among
+    // the batch's samples up to this one -- gets no camera ray: the gate will refuse that sample.
+    // The camera queue is then compacted (spec_skip).
     const bool as = has_adaptive_buffers(rs) && !P.spec_as;
+    const bool spec_skip = P.spec_as && rs.enable_adaptive_sampling && rs.accumulate;
     const bool lr = low_res(rs);
     bool act = slot < P.n;
     int x = 0, y = 0;
     uint32_t pix = 0;
     if (act) pix = slot_pixel(F, pslot, x, y);
-    if (act && lr && !low_res_region(F, x, y)) {
+    if (act && spec_skip && P.as_conv[pslot] != -1) {
+        bool reset = P.spec_reset != 0;
+        for (int k = 0; k <= sub; k++) reset |= Fp[k].render_settings.sample_number == 0 || Fp[k].render_settings.need_to_reset;
+        if (!reset) {
+            act = false;
+            P.active[slot] = 0;
+        }
+    }
+    if (!act) {
+    } else if (lr && !low_res_region(F, x, y)) {
         act = false;                      // CameraRays.h:68-72: no reset, no adaptive gate
         P.active[slot] = 0;
     } else if (act) {
@@ -949,7 +955,9 @@ __global__ __launch_bounds__(TB) void k_camera(DevPaths P, const MptFrame* __res
         }
         P.active[slot] = act ? 1 : 0;
     }
-    if (as || lr) {
+    if (P.cam_noqueue) {
+        // (batched ReSTIR DI: k_queue_active lists the active slots per sample and for the trace)
+    } else if (as || lr || spec_skip) {
         // camera-ray queue of the active pixels (wave64 ballot, one atomic per wave)
         uint64_t m = __ballot(act);
         int lane = threadIdx.x & 63;
@@ -1506,6 +1514,9 @@ struct ShadeArgs {
 #ifndef MPT_SHADE_WAVES
 #define MPT_SHADE_WAVES 2
 #endif
+#ifndef MPT_SHADE_PEP
+#define MPT_SHADE_PEP 1   // the plain kernel's per-vertex terms as the plain record (dev_bsdf.h PEvalP)
+#endif
 // Material classes (mat_tex bit MT_FULL, k_resolve_materials): k_split sorts the hit
 // vertices into the plain-dielectric list (no coat, sheen, metal, transmission or thin film:
 // the diffuse + specular base of the Principled BSDF, most of a city) and the list of every
@@ -1538,6 +1549,7 @@ template <int OVR, bool PLAIN, bool EXT = false, bool GLASS = false, int ST = SG
 __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(
     !(ST & SG_LIGHT) ? MPT_SHADE_WAVES_LATE : (PLAIN ? MPT_SHADE_WAVES_PLAIN : MPT_SHADE_WAVES)))) void k_shade(ShadeArgs A) {
     constexpr int CLS = PLAIN ? BC_PLAIN : (GLASS ? BC_GLASS : BC_FULL);   // the BSDF code's class (dev_bsdf.h)
+    constexpr bool PE_PLAIN = MPT_SHADE_PEP && PLAIN && OVR == MPT_BSDF_NONE && !EXT;   // the plain record (PEvalP)
     constexpr bool FIRST = (ST & SG_LIGHT) != 0;   // hit processing, AOVs, deferral, emission
     constexpr bool LAST = (ST & SG_CONT) != 0;
     static_assert(!EXT || ST == SG_ALL, "extended light sampling shades in one stage");
@@ -1639,7 +1651,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(
             // principled_eval_pre's 'outside' with the normal the vertex is shaded with
             const v3 sn_f = (is_emissive(m) && dot(-d, gn) < 0) ? -sn : sn;
             // (a material of the MT_TEXMETAL class is shaded here where its texel is not metallic)
-            if (!(dot(-d, sn_f) > 0 || m.thin_walled) || m.metallic != 0.0f || A.force_defer) {
+            if (!(dot(-d, sn_f) > 0 || m.thin_walled) || m.metallic != 0.0f || A.force_defer || (PE_PLAIN && !plain_vertex_ok(m))) {
                 A.q_defer[atomicAdd(A.count_defer, 1)] = slot;
                 atomicAdd(&P.counters[CTR_DEFER], 1);
                 A.q_cur[i] = -1;    // k_compact / k_resolve skip the entry here
@@ -1710,10 +1722,12 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(
             // arrays that the compiler's promote-alloca pass moves into the LDS the 2-wave
             // occupancy leaves free (the rest, 128 B per lane, in scratch); two blocks fill a
             // CU's 160 KB, so LDS and VGPRs (249) both cap the kernel at 2 waves / SIMD
+            // The plain kernel keeps the plain record instead (dev_bsdf.h PEvalP: 35 dwords)
             constexpr bool PE_LDS = (ST & SG_LIGHT) || MPT_SHADE_PE_LDS_LATE;
-            __shared__ PEval pe_lds[PE_LDS ? TB : 1];
-            PEval pe_reg;
-            PEval& pe = PE_LDS ? pe_lds[threadIdx.x] : pe_reg;
+            using PE = typename std::conditional<PE_PLAIN, PEvalP, PEval>::type;
+            __shared__ PE pe_lds[PE_LDS ? TB : 1];
+            PE pe_reg;
+            PE& pe = PE_LDS ? pe_lds[threadIdx.x] : pe_reg;
             // the first light sample's emissive record, loaded while the per-vertex BSDF terms are
             // computed (its index is the vertex's next draw); each RIS light candidate then loads
             // the next one's record (the draws between them are fixed: two for the point, one for
@@ -1724,11 +1738,13 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(
             SECT(0);
             bsdf_eval_pre<OVR, CLS>(bc, m, vs, view, sn, pe);
             SECT(5);
-            if (EXT && do_light && !(restir && bounce == 0)) {
-                // extended light sampling: every light sample's draws, records and queries
-                ext_light<OVR, CLS>(S, P, F, bc, m, vs, pe, slot, prim, ip, sn, gn, view, ism, ep, lssb, rng);
-                fl |= NF_EXT;
-                op = do_env ? OP_ENV_LIGHT : (do_cont ? OP_CONT : OP_DONE);
+            if constexpr (EXT) {
+                if (do_light && !(restir && bounce == 0)) {
+                    // extended light sampling: every light sample's draws, records and queries
+                    ext_light<OVR, CLS>(S, P, F, bc, m, vs, pe, slot, prim, ip, sn, gn, view, ism, ep, lssb, rng);
+                    fl |= NF_EXT;
+                    op = do_env ? OP_ENV_LIGHT : (do_cont ? OP_CONT : OP_DONE);
+                }
             }
             Col fW = col(0.0f);                // BSDF value / pdf at the RIS light winner
             float pdfW = 0.0f;
@@ -2632,9 +2648,9 @@ static void launch_restir_kernel(int ovr, int kind, dim3 g, hipStream_t st, cons
 template <int MODE>
 static void launch_trace_mode(const TraceArgs& a, int grid, bool stats, hipStream_t st) {
     if (MODE == TM_NEE_LIGHT && a.static_grid && !stats) grid = blocks_for(a.P.n);   // the query list holds at most n entries
-    // the persistent grid is MPT_TRACE_WAVES blocks per CU (one 4-wave block per SIMD and wave);
-    // the list modes fill their own occupancy (the spill area holds 8 blocks per CU)
-    static_assert(MPT_TRACE_WAVES_LIST <= 8 && MPT_TRACE_WAVES <= 8, "the traversal spill area holds 8 blocks per CU");
+    // the persistent grid is MPT_TRACE_BLOCKS_PER_CU blocks per CU (one 4-wave block per SIMD and
+    // wave); the list modes fill their own occupancy.  The spill area holds
+    // TRACE_SPILL_BLOCKS_PER_CU blocks per CU (mpt_internal.h), which covers both grids
     if (MODE == TM_LIST_ANY || MODE == TM_LIST_CLOSEST) grid = grid / MPT_TRACE_WAVES * MPT_TRACE_WAVES_LIST;
     if (stats) {
         // instrumented (calibration) launches stay persistent: their per-wave counter atomics
@@ -3090,7 +3106,8 @@ hipError_t launch_frame(const DevScene& S, const DevPaths& P0, const MptFrame* d
     // the camera queue is compacted by k_camera under adaptive sampling (unless speculative) and at
     // low resolution
     const bool as = ((hrs.stop_pixel_noise_threshold > 0.0f || hrs.enable_adaptive_sampling) && hrs.accumulate && !P.spec_as) ||
-                    (hrs.wants_render_low_resolution && hrs.allow_render_low_resolution && hrs.accumulate);
+                    (hrs.wants_render_low_resolution && hrs.allow_render_low_resolution && hrs.accumulate) ||
+                    (P.spec_as && hrs.enable_adaptive_sampling && hrs.accumulate);   // (k_camera's spec_skip)
     if (hf.options.direct_light_sampling == MPT_LSS_RESTIR_DI) {
         hipLaunchKernelGGL(k_restir_frame_begin, dim3(blocks_for(P.rs_hi - P.rs_lo)), dim3(TB), 0, st, P, d_frame);
         P.rs_out = restir_buffer(P, cfg.restir_out_sp2);
@@ -3128,6 +3145,22 @@ __global__ __launch_bounds__(TB) void k_iota(int32_t* q, int n) {
     const int i = blockIdx.x * TB + threadIdx.x;
     if (i < n) q[i] = i;
 }
+// batched ReSTIR DI under adaptive sampling: the slots [0, n) of `active` that are set, listed
+// in q (wave64 ballot, one atomic per wave on *count, which starts at 0)
+__global__ __launch_bounds__(TB) void k_queue_active(int32_t* __restrict__ q, int32_t* count, const uint8_t* __restrict__ active,
+                                                     int n) {
+    const int i = blockIdx.x * TB + threadIdx.x;
+    const bool act = i < n && active[i] != 0;
+    const uint64_t m = __ballot(act);
+    const int lane = threadIdx.x & 63;
+    int base = 0;
+    if (m) {
+        const int first = __ffsll((unsigned long long)m) - 1;
+        if (lane == first) base = atomicAdd(count, __popcll(m));
+        base = __shfl(base, first);
+    }
+    if (act) q[base + __popcll(m & ((1ull << lane) - 1ull))] = i;
+}
 
 hipError_t launch_frames_restir(const DevScene& S, const DevPaths& PF, const MptFrame* d_frames, const MptFrame* hf,
                                 int batch, LaunchCfg& cfg, hipStream_t st) {
@@ -3141,20 +3174,38 @@ hipError_t launch_frames_restir(const DevScene& S, const DevPaths& PF, const Mpt
     // the camera rays of every sample over its own slots [s * n, (s + 1) * n) (their seeds,
     // jitter and alpha keys are the sample's; nothing of the ReSTIR DI state is read), then
     // one traversal of all of them: a launch of batch x n rays instead of `batch` of n
+    //
+    // Adaptive sampling (PF.spec_as; mpt_render_frames batches such samples only while no pixel
+    // can reach the gate's noise test, see restir_gate_static): a pixel converged before the batch
+    // gets no camera ray (k_camera's spec_skip, `active` cleared), so the camera queues are built
+    // from `active` -- all samples' for the one traversal, then each sample's own before its
+    // G-buffer -- and k_accumulate replays the gate in sample order
+    const bool skip = PF.spec_as && hf[0].render_settings.enable_adaptive_sampling && hf[0].render_settings.accumulate;
+    bool reset_before = false;
     for (int s = 0; s < batch; s++) {
         DevPaths P = PF;
         offset_slots(P, (size_t)s * n);
         P.n = n; P.batch = 1; P.group = 1;
+        const MptRenderSettings& rs = hf[s].render_settings;
+        P.spec_reset = reset_before ? 1 : 0;
+        P.cam_noqueue = skip ? 1 : 0;
+        reset_before |= rs.sample_number == 0 || rs.need_to_reset;
         TimedScope ts(cfg, st, KT_CAMERA);
         hipLaunchKernelGGL(k_camera, dim3(blocks_for(n)), dim3(TB), 0, st, P, d_frames + s);
     }
     {
         DevPaths G = PF;
         G.group = n;
-        hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(&PF.counters[CTR_QG]), batch * n, 1, st);
+        if (skip) {
+            hipMemsetAsync(&PF.counters[CTR_QG], 0, sizeof(int32_t), st);
+            hipLaunchKernelGGL(k_queue_active, dim3(blocks_for(batch * n)), dim3(TB), 0, st, PF.q0, &PF.counters[CTR_QG],
+                               PF.active, batch * n);
+        } else {
+            hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(&PF.counters[CTR_QG]), batch * n, 1, st);
+        }
         hipMemsetAsync(&PF.counters[CTR_FETCH], 0, sizeof(int32_t), st);
         TraceArgs ta{};
-        ta.S = S; ta.P = G; ta.queue = nullptr; ta.count_ptr = &PF.counters[CTR_QG]; ta.fetch = &PF.counters[CTR_FETCH];
+        ta.S = S; ta.P = G; ta.queue = skip ? PF.q0 : nullptr; ta.count_ptr = &PF.counters[CTR_QG]; ta.fetch = &PF.counters[CTR_FETCH];
         ta.F = d_frames; ta.bounce = 0; ta.alpha = hf[0].render_settings.do_alpha_testing ? 1 : 0;
         timed_trace<TM_PATH>(ta, cfg, st);
     }
@@ -3170,7 +3221,7 @@ hipError_t launch_frames_restir(const DevScene& S, const DevPaths& PF, const Mpt
     // merges its G-buffer and initial reservoirs into the context's planes (k_chunk_join: the
     // stores the per-sample kernels make) before its reuse passes, in order.
     const MptReSTIRDISettings& rd0 = hf[0].render_settings.restir_di_settings;
-    const int chunk = (defer && cfg.ci_planes && cfg.ci_chunk > 1 && cfg.restir_staged && PF.rq_o &&
+    const int chunk = (defer && !skip && cfg.ci_planes && cfg.ci_chunk > 1 && cfg.restir_staged && PF.rq_o &&
                        rd0.number_of_initial_bsdf_candidates <= 1 && !hf[0].options.restir_di_initial_target_visibility)
                           ? std::min(cfg.ci_chunk, batch) : 1;
     for (int s = 0; s < batch; s++) {
@@ -3220,7 +3271,12 @@ hipError_t launch_frames_restir(const DevScene& S, const DevPaths& PF, const Mpt
             continue;
         }
         hipLaunchKernelGGL(k_restir_frame_begin, dim3(blocks_for(P.rs_hi - P.rs_lo)), dim3(TB), 0, st, P, d_frames + s);
-        hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(&P.counters[CTR_Q0]), n, 1, st);   // the camera queue
+        if (skip) {   // the sample's camera queue: its active slots
+            hipMemsetAsync(&P.counters[CTR_Q0], 0, sizeof(int32_t), st);
+            hipLaunchKernelGGL(k_queue_active, dim3(blocks_for(n)), dim3(TB), 0, st, P.q0, &P.counters[CTR_Q0], P.active, n);
+        } else {
+            hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(&P.counters[CTR_Q0]), n, 1, st);   // the camera queue (k_camera's iota)
+        }
         if (defer) {
             restir_first_bounce(S, P, d_frames + s, hf[s], cfg, st);
             if (cfg.halo_fn) cfg.halo_prev = cfg.halo_rows;
@@ -3253,8 +3309,14 @@ hipError_t launch_frames_restir(const DevScene& S, const DevPaths& PF, const Mpt
     }
     if (defer) {
         G.rs_keep_on = 1;
-        hipLaunchKernelGGL(k_iota, dim3(blocks_for(batch * n)), dim3(TB), 0, st, G.q0, batch * n);
-        hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(&G.counters[CTR_Q0]), batch * n, 1, st);
+        if (skip) {   // the batch's active slots
+            hipMemsetAsync(&G.counters[CTR_Q0], 0, sizeof(int32_t), st);
+            hipLaunchKernelGGL(k_queue_active, dim3(blocks_for(batch * n)), dim3(TB), 0, st, G.q0, &G.counters[CTR_Q0], G.active,
+                               batch * n);
+        } else {
+            hipLaunchKernelGGL(k_iota, dim3(blocks_for(batch * n)), dim3(TB), 0, st, G.q0, batch * n);
+            hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(&G.counters[CTR_Q0]), batch * n, 1, st);
+        }
         frame_bounces(S, G, d_frames, hf[0], cfg, st, 0, nb, G.q0, CTR_Q0, G.q1, CTR_Q1, true, true);
     } else if (nb > 0) {
         frame_bounces(S, G, d_frames, hf[0], cfg, st, 1, nb, G.q0, CTR_QG, G.q1, CTR_Q1);

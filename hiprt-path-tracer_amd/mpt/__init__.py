@@ -29,7 +29,7 @@ SYMBOLS = [
     "mpt_render_frame", "mpt_render_frames", "mpt_synchronize", "mpt_query_done", "mpt_get_framebuffer", "mpt_partition_rows",
     "mpt_enable_stats", "mpt_get_stats", "mpt_trace_closest", "mpt_trace_any", "mpt_clear_status",
     "mpt_query_status", "mpt_get_aux_buffer", "mpt_build_envmap_cdf", "mpt_set_envmap_cdf", "mpt_set_halo_exchange",
-    "mpt_set_halo_native",
+    "mpt_set_halo_native", "mpt_halo_plan",
     "mpt_bake_lut", "mpt_png_unfilter", "mpt_device_info", "mpt_gather", "mpt_comm_unique_id", "mpt_comm_init",
     "mpt_comm_gather", "mpt_jpeg_decode", "mpt_hdr_decode",
 ]
@@ -92,6 +92,7 @@ def lib() -> C.CDLL:
     L.mpt_get_aux_buffer.argtypes = [vp, C.c_int, vp, C.c_int]
     L.mpt_set_halo_exchange.argtypes = [vp, abi.HaloExchangeFn, vp]
     L.mpt_set_halo_native.argtypes = [vp, C.c_int32]
+    L.mpt_halo_plan.argtypes = [i32, i32, i32, i32, i32, i32, C.POINTER(abi.HaloOp), i32]
     L.mpt_bake_lut.argtypes = [vp, C.c_int, i32, i32, i32, i32, vp, C.c_int]
     L.mpt_gather.argtypes = [C.POINTER(vp), i32, i32, C.c_int, vp, C.c_int]
     L.mpt_comm_unique_id.argtypes = [vp, i32]
@@ -133,6 +134,18 @@ def build_id():
 
 def partition_rows(res_y, band_height, band_index, band_count):
     return lib().mpt_partition_rows(res_y, band_height, band_index, band_count)
+
+
+def halo_plan(res_y, band_height, band_count, band_index, halo_rows, n_buffers=1):
+    """mpt_halo_plan: the library's halo-exchange operations for one band, in issue order, as
+    (peer, 'send' | 'recv', buffer, row_lo, row_hi) tuples (host only, no device needed)."""
+    args = (res_y, band_height, band_count, band_index, halo_rows, n_buffers)
+    n = lib().mpt_halo_plan(*args, None, 0)
+    _check(min(n, 0))
+    ops = (abi.HaloOp * max(n, 1))()
+    m = lib().mpt_halo_plan(*args, ops, n)
+    _check(min(m, 0))
+    return [(o.peer, "recv" if o.recv else "send", o.buffer, o.row_lo, o.row_hi) for o in ops[:m]]
 
 
 GATHER_AUX = 16   # mpt.h MPT_GATHER_AUX: gather kind of an MPT_AUX_* buffer

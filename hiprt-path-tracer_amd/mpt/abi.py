@@ -368,7 +368,9 @@ class Stats(C.Structure):
                 ("shade_generic_ms", C.c_double), ("shade_generic_vertices", C.c_uint64),
                 ("restir_kernel_ms", C.c_double * 5), ("restir_kernel_launches", C.c_uint32 * 5),
                 ("restir_eval_ms", C.c_double), ("restir_eval_launches", C.c_uint32), ("restir_eval_items", C.c_uint64),
-                ("graph_captures", C.c_uint32), ("graph_replays", C.c_uint32), ("overlapped_batches", C.c_uint32)]
+                ("graph_captures", C.c_uint32), ("graph_replays", C.c_uint32), ("overlapped_batches", C.c_uint32),
+                ("halo_exchanges", C.c_uint64), ("halo_agreements", C.c_uint64), ("halo_bytes_sent", C.c_uint64),
+                ("halo_bytes_received", C.c_uint64), ("restir_overlapped_batches", C.c_uint32)]
 
 
 OK, ERR_INVALID_ARGUMENT, ERR_HIP, ERR_NO_SCENE, ERR_UNSUPPORTED, ERR_OUT_OF_MEMORY = 0, -1, -2, -3, -4, -5
@@ -404,6 +406,12 @@ class HaloExchange(C.Structure):
 
 
 HaloExchangeFn = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(HaloExchange))
+
+
+class HaloOp(C.Structure):
+    """MptHaloOp: one send (recv 0) or receive (recv 1) of buffer rows [row_lo, row_hi) with a peer band."""
+    _fields_ = [("peer", C.c_int32), ("recv", C.c_int32), ("buffer", C.c_int32), ("row_lo", C.c_int32),
+                ("row_hi", C.c_int32)]
 
 ABI_SIZES = {"Material": 332, "RenderSettings": 304, "WorldSettings": 200, "Camera": 196}
 

@@ -448,6 +448,16 @@ typedef struct MptStats {
     /* path-tracing batches launched as two overlapped halves on two streams (MPT_OVERLAP): their
      * kernels share the GPU, so the per-kernel times above overlap */
     uint32_t overlapped_batches;
+    /* the library's halo exchange (mpt_set_halo_native): exchange points served, halo
+     * agreements run (the all-reduce of a moving camera), bytes sent to / received from peers
+     * (mode 2: the bytes a rank would move; mpt_halo_plan's operations) */
+    uint64_t halo_exchanges;
+    uint64_t halo_agreements;
+    uint64_t halo_bytes_sent;
+    uint64_t halo_bytes_received;
+    /* batched ReSTIR DI wavefronts whose later bounces ran on the second stream beside the next
+     * batch's per-sample chain (MPT_RESTIR_OVERLAP) */
+    uint32_t restir_overlapped_batches;
 } MptStats;
 
 #define MPT_FB_COLOR 0        /* 'pixels': running SUM of samples (RenderData.h:34-36) */
@@ -613,6 +623,21 @@ int mpt_comm_gather(MptContext* ctx, int32_t root, int kind, void* dst, int dst_
  * rows keep what the buffers held -- timing only), 0 off.  Replaces mpt_set_halo_exchange's
  * callback. */
 int mpt_set_halo_native(MptContext* ctx, int32_t mode);
+/* One point-to-point operation of a halo exchange point: `buffer`'s rows [row_lo, row_hi)
+ * sent to (recv = 0) or received from (recv = 1) band `peer`. */
+typedef struct MptHaloOp {
+    int32_t peer;
+    int32_t recv;
+    int32_t buffer;
+    int32_t row_lo, row_hi;
+} MptHaloOp;
+/* The operations mpt_set_halo_native's exchange issues, in issue order, for band band_index of
+ * band_count contiguous bands of band_height rows (res_y rows in all), the agreed halo_rows and
+ * n_buffers buffers: per peer in increasing order, per buffer, the sends of this band's rows in
+ * the peer's upper and lower halo, then the receives of the peer's rows in this band's upper and
+ * lower halo.  Writes at most cap entries to out, returns the count (< 0: error).  Host only. */
+int mpt_halo_plan(int32_t res_y, int32_t band_height, int32_t band_count, int32_t band_index, int32_t halo_rows,
+                  int32_t n_buffers, MptHaloOp* out, int32_t cap);
 /* Status buffers: mpt_clear_status <- GPURenderer::internal_update_clear_device_status_buffers
  * (GPURenderer.cpp:275-283, once per displayed frame); the last sample of the frame sets
  * render_settings.do_update_status_buffers; mpt_query_status <- copy_status_buffers (.cpp:269-273). */

@@ -144,3 +144,42 @@ def test_gpu_adaptive_batched_speculative_bit_exact(cornell, luts, mode, max_bat
     assert 0 < launches <= (N // max_batch + (1 if mode == "adaptive_reset" else 0)) * 4 * 2, launches
     o.close()
     r.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("max_batch", [2, 4])
+def test_gpu_adaptive_batched_skips_converged_pixels(cornell, luts, max_batch):
+    """A speculative batch traces no camera ray for a pixel that converged before the batch began
+    (pixel_converged_sample_count != -1 is sticky under enable_adaptive_sampling,
+    AdaptiveSampling.h:45-48; CameraRays.h:107-121 rescales it instead): with 0 bounces the path
+    queries are exactly the camera rays, so their count is, per batch [j, j + L), L for every pixel
+    that had not converged before sample j -- derived from the oracle's converged sample counts (a
+    pixel with count c is refused from sample c on) -- and the image still equals the oracle's."""
+    import mpt
+    from oracle import oracle as orc
+    st = adaptive_settings(min_samples=2, threshold=0.8)
+    st.nb_bounces = 0
+    frs = frames(cornell, st)
+    r = mpt.GPURenderer(0)
+    r.set_scene(cornell)
+    r.set_luts(luts)
+    r.enable_stats(timing=False)
+    r.render_samples(frs, max_batch=max_batch)
+    r.synchronize_kernel()
+    rays = r.stats().stage_rays[0]
+    o = orc.Oracle(cornell, luts)
+    c = o.render(frs)
+    conv = o.last_aux["converged_sample_count"].reshape(-1).astype(np.int64)
+    o.close()
+    g = r.framebuffer(abi.FB_COLOR)
+    assert np.array_equal(g, c), f"{(g != c).sum()} values differ"
+    assert np.array_equal(r.aux_buffer(abi.AUX_CONVERGED_SAMPLE_COUNT).reshape(-1), conv)
+    want = 0
+    for j in range(0, N, max_batch):
+        L = min(max_batch, N - j)
+        live = (conv < 0) | (conv >= j)
+        want += L * int(live.sum())
+    assert (conv >= 0).sum() > conv.size // 4, "the test needs pixels converging early"
+    assert rays == want, (rays, want, N * W * H)
+    assert rays < N * W * H
+    r.close()

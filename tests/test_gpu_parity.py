@@ -2,8 +2,9 @@
 
 Bar: bit-exact.  Traversal results (prim, t, u, v) and rendered sums / AOVs must equal
 the oracle's float32 values exactly -- the device code is compiled without
-contraction, transcendentals are rounded from double on both sides and the RNG stream
-of every path is consumed in the reference's order (DESIGN.md "Parity").
+contraction, both sides evaluate every transcendental with the same single-precision
+sequence of IEEE operations (csrc/tmath.h, pinned against libm by tests/test_tmath.py) and
+the RNG stream of every path is consumed in the reference's order (DESIGN.md "Parity").
 At the bench size (1920x1080) the properties checked are size-independent: run-to-run
 determinism, partition invariance and finite output.
 """
@@ -342,8 +343,10 @@ def test_batched_samples_city_alpha_bit_exact(city, luts):
 
 
 def test_batched_samples_fall_back_for_adaptive(scenes, luts):
-    """Adaptive sampling reads each sample's result before the next: such frames are
-    rendered one by one and equal the sequential render."""
+    """Adaptive sampling gates each sample's camera rays on the previous samples: batched
+    frames are traced speculatively (pixels that converged before the batch began are left out
+    of its camera queue) and k_accumulate replays the gate in sample order, so the batched render
+    equals the sequential one."""
     sd = scenes["cornell_pbr"]
     r = renderer(sd, luts)
     frs = frames(sd, 32, 16, 6)
@@ -470,3 +473,20 @@ def test_graph_replay_equals_direct_launches(scenes, luts, monkeypatch):
     ref = o.render(frs)
     o.close()
     assert np.array_equal(out["graph"][0], ref)
+
+
+def test_graph_captured_once_over_identical_launch_sets(scenes, luts, monkeypatch):
+    """Frames that differ only in seeds and sample number share one captured graph: the cache key
+    (the frame with its per-sample fields cleared, the scene and path-state views, the launch
+    flags) must not pick up stray bytes (struct padding) that would re-capture every frame."""
+    sd = scenes["cornell_pbr"]
+    monkeypatch.setenv("MPT_GRAPHS", "1")
+    frs = frames(sd, 32, 24, 6)
+    with mpt.GPURenderer(0) as r:
+        r.set_scene(sd)
+        r.set_luts(luts)
+        for f in frs:
+            r.render(f)
+        r.synchronize_kernel()
+        st = r.stats()
+    assert st.graph_replays == len(frs) and st.graph_captures == 1, (st.graph_captures, st.graph_replays)

@@ -17,7 +17,8 @@ W, H = 32, 24
 
 
 def frames(sd, lss, n, passes=2, ovr=abi.BSDF_NONE, bounces=3, world=None, alpha=False, w=W, h=H, adaptive=False,
-           band=(1, 0, 1), move_at=None, bias=abi.RESTIR_DI_BIAS_PAIRWISE_MIS_DEFENSIVE, bias_vis=1, kopt=None, **rd):
+           band=(1, 0, 1), move_at=None, bias=abi.RESTIR_DI_BIAS_PAIRWISE_MIS_DEFENSIVE, bias_vis=1, kopt=None,
+           adaptive_min=2, adaptive_threshold=0.8, **rd):
     """move_at: from that frame on the camera is moved (prev_camera = the old one for one frame)."""
     cam = scene.make_camera(sd.camera_info, w, h)
     cam2 = None
@@ -42,8 +43,8 @@ def frames(sd, lss, n, passes=2, ovr=abi.BSDF_NONE, bounces=3, world=None, alpha
         st.do_alpha_testing = alpha
         if adaptive:
             st.enable_adaptive_sampling = True
-            st.adaptive_sampling_min_samples = 2
-            st.adaptive_sampling_noise_threshold = 0.8
+            st.adaptive_sampling_min_samples = adaptive_min
+            st.adaptive_sampling_noise_threshold = adaptive_threshold
         st.restir_di_settings.number_of_passes = passes
         for k, v in rd.items():
             setattr(st.restir_di_settings, k, v)
@@ -636,4 +637,91 @@ def test_gpu_restir_reset_in_used_context_bit_exact(cornell, luts, case, batched
         assert np.array_equal(r.framebuffer(abi.FB_NORMALS), cn)
     assert np.isfinite(g).all() and g.mean() > 0
     o.close()
+    r.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("envmap", [False, True], ids=["no_envmap", "envmap"])
+def test_gpu_restir_overlapped_batch_then_unbatched_frame(cornell, luts, monkeypatch, envmap):
+    """Regression for the race behind the r05d GPU fault: in ONE mpt_render_frames call, overlapped
+    ReSTIR DI batches (a batch's later bounces still running on the second stream) followed by
+    frames that cannot overlap -- the odd one-sample tail of 4 + 4 + 1, a low-resolution frame,
+    then another overlapped batch -- reuse the first half's path state and counters; launch_batch
+    must join the second stream first.  Against MPT_RESTIR_OVERLAP=0 and the oracle."""
+    import mpt
+    from oracle import oracle as orc
+    env = mpt.build_envmap(scene.procedural_sky(128, 64, seed=7)) if envmap else None
+    kw = dict(world=scene.envmap_world(1.0)) if envmap else {}
+    frs = frames(cornell, abi.LSS_RESTIR_DI, 13, **kw)
+    frs[9].render_settings.wants_render_low_resolution = True
+    frs[9].render_settings.render_low_resolution_scaling = 2
+    out = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("MPT_RESTIR_OVERLAP", mode)
+        r = _renderer(cornell, luts, env)
+        r.enable_stats(timing=False)
+        r.render_samples(frs, max_batch=4)
+        r.synchronize_kernel()
+        out[mode] = [r.framebuffer(k) for k in (abi.FB_COLOR, abi.FB_ALBEDO, abi.FB_NORMALS)]
+        st = r.stats()
+        out[mode + "_ovl"] = st.restir_overlapped_batches
+        r.close()
+    assert out["0_ovl"] == 0 and out["1_ovl"] >= 2, (out["0_ovl"], out["1_ovl"])
+    for a, b in zip(out["1"], out["0"]):
+        assert np.array_equal(a, b), f"{(a != b).sum()} values differ"
+    o = orc.Oracle(cornell, luts, envmap=env)
+    c = o.render(frs)
+    o.close()
+    assert np.array_equal(out["1"][0], c), f"{(out['1'][0] != c).sum()} values differ from the oracle"
+
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["fused", "unfused", "envmap", "partitioned"])
+def test_gpu_restir_adaptive_batched_bit_exact(cornell, luts, case):
+    """ReSTIR DI under adaptive sampling through mpt_render_frames: the samples whose gate is static
+    (no pixel can reach the noise test before adaptive_sampling_min_samples) run as batched
+    wavefronts, the rest one by one, and the pixels converge after the minimum -- sums, AOVs, sample
+    counts, converged counts and status values equal the oracle's sample-by-sample render."""
+    import mpt
+    from oracle import oracle as orc
+    env = mpt.build_envmap(scene.procedural_sky(128, 64, seed=7)) if case == "envmap" else None
+    kw = dict(adaptive=True, adaptive_min=5, adaptive_threshold=0.9)
+    if case == "unfused":
+        kw["do_fused_spatiotemporal"] = False
+    if env is not None:
+        kw["world"] = scene.envmap_world(1.0)
+    n = 12
+    w, h, nb = (24, 64, 3) if case == "partitioned" else (W, H, 1)
+    frs = frames(cornell, abi.LSS_RESTIR_DI, n, w=w, h=h, reuse_radius=5, **kw)
+    for f in frs:
+        f.render_settings.do_update_status_buffers = True
+    o = orc.Oracle(cornell, luts, envmap=env)
+    c, ca, cn = o.render(frs, aov=True)
+    aux = o.last_aux
+    o.close()
+    assert (aux["converged_sample_count"] >= 0).any(), "the test needs pixels converging"
+    if case == "partitioned":
+        st = []
+        got = render_partitioned_local(cornell, luts, lambda band: frames(cornell, abi.LSS_RESTIR_DI, n, w=w, h=h, band=band,
+                                                                          reuse_radius=5, **kw),
+                                       w, h, nb, env=env, batch=8, stats=st)
+        assert np.array_equal(got, c), f"{(got != c).sum()} values differ"
+        assert 0 < st[0].shade_launches < n * 4, st[0].shade_launches
+        return
+    r = _renderer(cornell, luts, env)
+    r.enable_stats(timing=True)
+    r.clear_status_buffers()
+    r.render_samples(frs, max_batch=8)
+    r.synchronize_kernel()
+    g = r.framebuffer(abi.FB_COLOR)
+    assert np.array_equal(g, c), f"{case}: {(g != c).sum()} values differ"
+    assert np.array_equal(r.framebuffer(abi.FB_ALBEDO), ca)
+    assert np.array_equal(r.framebuffer(abi.FB_NORMALS), cn)
+    assert np.array_equal(r.aux_buffer(abi.AUX_SAMPLE_COUNT), aux["sample_count"])
+    assert np.array_equal(r.aux_buffer(abi.AUX_CONVERGED_SAMPLE_COUNT), aux["converged_sample_count"])
+    s = r.get_status_buffer_values()
+    assert s == {"one_ray_active": aux["one_ray_active"], "pixel_converged_count": aux["pixel_converged_count"]}
+    # sample 0 (a reset) alone, samples 1..5 as one wavefront, then one by one: 1 + 1 + 6 wavefronts
+    assert r.stats().shade_launches < n * 4, r.stats().shade_launches
     r.close()
