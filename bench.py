@@ -391,7 +391,8 @@ def main():
                     "ms_per_step": o["ms_per_step"], "steps": o["steps"], "msample_per_s": o["msample_per_s"],
                     "roofline": {"kernel": rf["kernel"].split(" (")[0], "frac": rf["frac"], "achieved": rf["achieved"],
                                  "pmc_hbm_frac": rf.get("pmc_hbm_frac"), "traffic_per_unit": rf.get("traffic_per_unit"),
-                                 "bytes_per_unit": rf["bytes_per_unit"], "shared_gpu": rf.get("shared_gpu")},
+                                 "bytes_per_unit": rf["bytes_per_unit"], "shared_gpu": rf.get("shared_gpu"),
+                                 "frac_kind": rf.get("frac_kind")},
                     "kernel_ms_per_step": {k: v for k, v in o["kernel_ms_per_step"].items() if k != "restir_kernels"},
                     "cpu_baseline": o["cpu_baseline"], "parity_vs_oracle": o["parity_vs_oracle"],
                     "wall_s": round(time.perf_counter() - t0, 1)})
@@ -681,6 +682,9 @@ def run_workload(a, world, rank, local, dist, coll_dev, quiet=False):
                      traffic_per_unit=round(tr["traffic_per_unit"], 1),
                      traffic_read_per_unit=round(tr["read_per_unit"], 1), traffic_write_per_unit=round(tr["write_per_unit"], 1),
                      traffic_source=pmc["file"],
+                     # the profiled library against this run's: counters of another build are flagged
+                     traffic_libmpt_sha256_16=pmc.get("libmpt_sha256_16"),
+                     traffic_same_library=(pmc.get("libmpt_sha256_16") == mpt.build_id()) if pmc.get("libmpt_sha256_16") else None,
                      profiled={"units_per_launch": round(tr["units_per_launch"], 1), "launches": tr["launches"],
                                "avg_launch_ms": round(tr["avg_ns"] / 1e6, 5), "traffic_per_launch": round(tr["traffic_bytes"])},
                      # the kernel's measured HBM bytes over its own profiled launch time
@@ -692,6 +696,10 @@ def run_workload(a, world, rank, local, dist, coll_dev, quiet=False):
             r["valu"] = {"insts_per_launch": round(tr["valu_insts"]), "achieved_tinst_s": round(tr["valu_rate"] / 1e12, 4),
                          "peak_tinst_s": VALU_PEAK / 1e12, "frac": round(tr["valu_rate"] / VALU_PEAK, 4),
                          "per_unit": round(tr["valu_insts"] / max(1.0, tr["units_per_launch"]), 2)}
+        if x["unit_of_work"] == "ray":
+            # a traversal's algorithmic bytes count every node and triangle record it fetches, most of
+            # them L2 hits: frac is an accounting figure, pmc_hbm_frac the HBM bandwidth it draws
+            r["frac_kind"] = "algorithmic node/triangle bytes (mostly L2 hits; HBM drawn: pmc_hbm_frac)"
         if "nodes_per_ray" in x:
             r.update(nodes_per_ray=round(x["nodes_per_ray"], 3), tris_per_ray=round(x["tris_per_ray"], 3),
                      node_simd_util=round(x["node_simd_util"], 3), tri_simd_util=round(x["tri_simd_util"], 3))

@@ -76,6 +76,7 @@ struct DBuf {
 };
 
 constexpr int FRAME_RING = 256;   // >= 2 x MPT_MAX_BATCH
+constexpr int PIX_PARTS_MAX = 4;  // row parts of a one-sample frame (MptContext::pix_parts)
 // timing events per frame: one pair per timed launch, 10 per bounce (path, any-hit and two
 // light-hit traversals, split, plain and generic shade, miss, compact, resolve) for up to 65
 // bounces (validate_frame), + camera, ReSTIR, accumulate
@@ -105,6 +106,10 @@ struct MptContext {
     // keep one stream (+1.2 % only, and its per-kernel times stay unshared)
     int overlap = -1;
     hipStream_t stream2 = nullptr;
+    // the third and fourth row parts of a one-sample frame (MptContext::pix_parts): streams,
+    // traversal spill areas, join events
+    hipStream_t streamx[2] = {nullptr, nullptr};
+    hipEvent_t ev_joinx[2] = {nullptr, nullptr};
     hipEvent_t ev_fork = nullptr, ev_first = nullptr, ev_acc = nullptr, ev_join = nullptr;
     // Overlapped ReSTIR DI batches (MPT_RESTIR_OVERLAP, default on): a batch's per-sample chain
     // (G-buffer, reuse passes, halo exchanges: many small dependent launches) runs on the
@@ -122,7 +127,14 @@ struct MptContext {
     // what the kernels read from it (seeds, sample number, cameras, status flags); the graph reads
     // its frame from the extra ring slot d_frames[FRAME_RING].  Keyed by those frame fields that
     // steer the host's launch sequence and by the kernels' by-value arguments (buffer pointers).
-    int graphs = 1;
+    int graphs = 0;   // MPT_GRAPHS=1: one-sample launch sets replayed from a captured HIP graph (no gain measured, r05e)
+    // one-sample frames of a whole-frame context as row parts on their own streams (MPT_PIX_PARTS:
+    // 0 / 1 off, 2 .. PIX_PARTS_MAX parts)
+    int pix_parts = 3;   // batch-1 C3 6.09 -> 5.44 (2 parts) -> 5.29 ms/spp (3); 4 parts 6.76 (past GPU_MAX_HW_QUEUES), r06d
+    // staged ReSTIR DI stages: the generic-class kernel on a side stream beside the plain one
+    // (MPT_RESTIR_SIDE)
+    int restir_side = 1;
+    hipEvent_t ev_side[2] = {nullptr, nullptr};
     hipGraphExec_t graph_exec = nullptr;
     std::vector<uint8_t> graph_key;
     uint32_t graph_launches = 0;
@@ -189,7 +201,7 @@ struct MptContext {
     int batch = 1;          // samples of the launch being set up
     DBuf<float4> ray_o, ray_d, hit, thr, col, alb, nrmv, nq_o, nq_d, nhit, s_gn;
     DBuf<uint8_t> hit_inside, hit_cls, occ, qmask;
-    DBuf<uint32_t> rng, spill, spill2;
+    DBuf<uint32_t> rng, spill, spill2, spillx[2];
     DBuf<uint2> seeds;
     DBuf<uint4> vsA, vsB;
     DBuf<int32_t> q0, q1, qh, qm, qf, nq_light, counters, nq_tgt, fetch_raw;
@@ -440,6 +452,8 @@ void release_batch(MptContext* c) {
 static hipError_t drain(MptContext* c) {
     hipError_t e = hipStreamSynchronize(c->stream);
     if (e == hipSuccess && c->stream2) e = hipStreamSynchronize(c->stream2);
+    for (hipStream_t x : c->streamx)
+        if (e == hipSuccess && x) e = hipStreamSynchronize(x);
     return e;
 }
 
@@ -923,8 +937,10 @@ static int create_context(MptContext* c, int device, void* hip_stream) {
     else { HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)); c->own_stream = true; }
     HIPCHK(hipHostMalloc((void**)&c->h_frames, sizeof(MptFrame) * (FRAME_RING + 1)));
     HIPCHK(hipMalloc((void**)&c->d_frames, sizeof(MptFrame) * (FRAME_RING + 1)));   // + the graph's frame
-    HIPCHK(c->counters.alloc(2 * CTR_COUNT));   // second set: the second half of an overlapped batch
-    HIPCHK(hipMemsetAsync(c->counters.p, 0, 2 * CTR_COUNT * sizeof(int32_t), c->stream));
+    // second set: the second half of an overlapped batch; up to PIX_PARTS_MAX: the row parts of a
+    // one-sample frame
+    HIPCHK(c->counters.alloc(PIX_PARTS_MAX * CTR_COUNT));
+    HIPCHK(hipMemsetAsync(c->counters.p, 0, PIX_PARTS_MAX * CTR_COUNT * sizeof(int32_t), c->stream));
     HIPCHK(c->fetch_raw.alloc(4));
     HIPCHK(c->stats.alloc(N_STATS));
     HIPCHK(hipMemsetAsync(c->stats.p, 0, N_STATS * sizeof(uint64_t), c->stream));
@@ -967,6 +983,8 @@ int mpt_create(int device, void* hip_stream, MptContext** out) {
     if (const char* e = std::getenv("MPT_MAT_PRIVATE")) c->mat_private = std::atoi(e);
     if (const char* e = std::getenv("MPT_RESTIR_OVERLAP")) c->restir_overlap = std::atoi(e);
     if (const char* e = std::getenv("MPT_GRAPHS")) c->graphs = std::atoi(e);
+    if (const char* e = std::getenv("MPT_PIX_PARTS")) c->pix_parts = std::atoi(e);
+    if (const char* e = std::getenv("MPT_RESTIR_SIDE")) c->restir_side = std::atoi(e);
     if (const char* e = std::getenv("MPT_RESTIR_MAX_BATCH"))
         c->restir_max_batch = std::max(1, std::min(RESTIR_MAX_BATCH, std::atoi(e)));
     if (const char* e = std::getenv("MPT_RESTIR_CHUNK")) c->restir_chunk = std::atoi(e);
@@ -1010,6 +1028,11 @@ int mpt_destroy(MptContext* c) {
     if (c->d_frames) (void)hipFree(c->d_frames);
     if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
     if (c->stream2) (void)hipStreamDestroy(c->stream2);
+    for (int k = 0; k < 2; k++) {
+        if (c->streamx[k]) (void)hipStreamDestroy(c->streamx[k]);
+        if (c->ev_joinx[k]) (void)hipEventDestroy(c->ev_joinx[k]);
+        if (c->ev_side[k]) (void)hipEventDestroy(c->ev_side[k]);
+    }
     for (hipEvent_t e : {c->ev_fork, c->ev_first, c->ev_acc, c->ev_join, c->ev_chain, c->ev_half[0], c->ev_half[1],
                          c->ev_wave_join})
         if (e) (void)hipEventDestroy(e);
@@ -1361,6 +1384,18 @@ static int ensure_overlap(MptContext* c) {
 
 static int join_waves(MptContext* c);
 
+// The streams, spill areas and join events of row parts 3 and 4 (pix_parts), on first use.
+static int ensure_pix_parts(MptContext* c, int parts) {
+    int r = ensure_overlap(c);
+    if (r != MPT_OK) return r;
+    for (int k = 0; k + 2 < parts; k++) {
+        if (c->spillx[k].n != c->spill.n) HIPCHK(c->spillx[k].alloc(c->spill.n));
+        if (!c->ev_joinx[k]) HIPCHK(hipEventCreateWithFlags(&c->ev_joinx[k], hipEventDisableTiming));
+        if (!c->streamx[k]) HIPCHK(hipStreamCreateWithFlags(&c->streamx[k], hipStreamNonBlocking));
+    }
+    return MPT_OK;
+}
+
 // The graph path of a one-sample path-tracing launch set (MptContext::graphs): (re)captured when
 // the key changes, then replayed with the frame copied into the graph's fixed slot.
 static hipError_t launch_frame_graph(MptContext* c, const DevPaths& P, const MptFrame* f, int slot, LaunchCfg& cfg) {
@@ -1437,17 +1472,39 @@ static int launch_batch(MptContext* c, const MptFrame* f, int batch) {
         int jr = join_waves(c);
         if (jr != MPT_OK) return jr;
     }
+    // One-sample frames of a whole-frame context (the interactive launch set: the reference's
+    // samples_per_frame = 1, low-resolution frames, a moving camera) run as two row halves on two
+    // streams: every pixel's path is independent and its accumulation touches only its own pixel,
+    // so the halves need no ordering, and one half's kernels fill the other's launch tails (each
+    // of the ~50 dependent launches of a sample otherwise drains the GPU before the next starts)
+    const int parts = std::min(std::max(c->pix_parts, 1), std::min(PIX_PARTS_MAX, f->res_y));
+    const bool pix_ovl = parts > 1 && batch == 1 && f->band_count == 1 && c->n_slots >= (1 << 16) &&
+                         f->options.direct_light_sampling != MPT_LSS_RESTIR_DI && c->x_per == 0 &&
+                         !(c->graphs && !c->timing);
+    const int nfr = batch + (pix_ovl ? parts - 1 : 0);
     // stage the frame constants through a pinned ring (the previous use of the slot
     // has completed once 64 frames later are enqueued; synchronise defensively)
-    if (c->frame_slot + batch > FRAME_RING) c->frame_slot = 0;
+    if (c->frame_slot + nfr > FRAME_RING) c->frame_slot = 0;
     int slot = c->frame_slot;
-    c->frame_slot = (c->frame_slot + batch) % FRAME_RING;
+    c->frame_slot = (c->frame_slot + nfr) % FRAME_RING;
     if (slot == 0) {
         HIPCHK(hipStreamSynchronize(c->stream));
         if (c->stream2) HIPCHK(hipStreamSynchronize(c->stream2));   // an overlapped wavefront reads its frames
     }
     for (int k = 0; k < batch; k++) c->h_frames[slot + k] = f[k];
-    HIPCHK(hipMemcpyAsync(c->d_frames + slot, c->h_frames + slot, batch * sizeof(MptFrame), hipMemcpyHostToDevice,
+    // row part k's frame: rows [k hp, (k + 1) hp) as band k of `parts` bands of hp rows, so that
+    // its slot s is pixel k hp W + s (slot_pixel); part 0 keeps the whole frame's (same mapping)
+    const int hp = (f->res_y + parts - 1) / parts;
+    if (pix_ovl) {
+        for (int k = 1; k < parts; k++) {
+            MptFrame& g = c->h_frames[slot + k];
+            g = f[0];
+            g.band_height = hp;
+            g.band_index = k;
+            g.band_count = parts;
+        }
+    }
+    HIPCHK(hipMemcpyAsync(c->d_frames + slot, c->h_frames + slot, nfr * sizeof(MptFrame), hipMemcpyHostToDevice,
                           c->stream));
     int pool = (int)(c->frames_submitted & 1u);
     if (c->timing) {
@@ -1469,6 +1526,16 @@ static int launch_batch(MptContext* c, const MptFrame* f, int batch) {
                                                                                      f->render_settings.restir_di_settings.subset_size) * c->ci_chunk) {
         cfg.ci_chunk = c->ci_chunk;
         cfg.ci_planes = &c->ci_dp;
+    }
+    if (f->options.direct_light_sampling == MPT_LSS_RESTIR_DI && c->restir_side && c->restir_staged) {
+        int rr = ensure_pix_parts(c, 3);   // (streamx[0] and its spill area)
+        if (rr != MPT_OK) return rr;
+        for (hipEvent_t& ev : c->ev_side)
+            if (!ev) HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        cfg.side_stream = c->streamx[0];
+        cfg.side_spill = c->spillx[0].p;
+        cfg.ev_side_fork = c->ev_side[0];
+        cfg.ev_side_join = c->ev_side[1];
     }
     cfg.shade_glass = c->shade_glass;
     cfg.shade_split = c->shade_split;
@@ -1504,7 +1571,43 @@ static int launch_batch(MptContext* c, const MptFrame* f, int batch) {
     const bool ovl = (c->overlap > 0 || (c->overlap < 0 && ovl_auto)) && batch >= 2 &&
                      f->options.direct_light_sampling != MPT_LSS_RESTIR_DI && c->x_per == 0 && !P.spec_as;
     hipError_t e = hipSuccess;
-    if (ovl) {
+    if (pix_ovl) {
+        int rr = ensure_pix_parts(c, parts);
+        if (rr != MPT_OK) return rr;
+        // part 0 on the context's stream, part k on its own stream over its own slots (and
+        // per-pixel buffers: slot == pixel at one sample), counters and traversal spill area
+        HIPCHK(hipEventRecord(c->ev_fork, c->stream));
+        LaunchCfg cur = cfg;
+        int launches = 0;
+        for (int k = 0; k < parts && e == hipSuccess; k++) {
+            const size_t r0 = std::min((size_t)f->res_y, (size_t)k * hp), r1 = std::min((size_t)f->res_y, (size_t)(k + 1) * hp);
+            const size_t off = r0 * (size_t)f->res_x, n = (r1 - r0) * (size_t)f->res_x;
+            if (n == 0) continue;
+            DevPaths Pk = P;
+            Pk.n = Pk.n_pix = (int)n;
+            if (k > 0) {
+                offset_slots(Pk, off);
+                Pk.fb_color += 3 * off; Pk.fb_albedo += 3 * off; Pk.fb_normal += 3 * off;
+                Pk.as_count += off; Pk.as_sqlum += off; Pk.as_conv += off;
+                Pk.counters += k * CTR_COUNT;
+                Pk.stack_spill = k == 1 ? c->spill2.p : c->spillx[k - 2].p;
+            }
+            hipStream_t sk = k == 0 ? c->stream : k == 1 ? c->stream2 : c->streamx[k - 2];
+            if (k > 0) HIPCHK(hipStreamWaitEvent(sk, c->ev_fork, 0));
+            cur.launches = 0;
+            e = launch_frame(dev_scene(c), Pk, c->d_frames + slot + k, k == 0 ? f[0] : c->h_frames[slot + k], cur, sk);
+            launches += cur.launches;
+        }
+        for (int k = 1; k < parts; k++) {
+            hipStream_t sk = k == 1 ? c->stream2 : c->streamx[k - 2];
+            hipEvent_t ej = k == 1 ? c->ev_join : c->ev_joinx[k - 2];
+            HIPCHK(hipEventRecord(ej, sk));
+            HIPCHK(hipStreamWaitEvent(c->stream, ej, 0));
+        }
+        c->overlapped_batches++;
+        cfg.ev_used = cur.ev_used;
+        cfg.launches = launches;
+    } else if (ovl) {
         int rr = ensure_overlap(c);
         if (rr != MPT_OK) return rr;
         // samples [0, b0) on the context's stream, [b0, batch) on stream2 over their own

@@ -339,6 +339,12 @@ struct LaunchCfg {
     hipStream_t wave_stream;
     uint32_t* wave_spill;
     hipEvent_t ev_chain;
+    // staged ReSTIR DI stages: the generic-class kernel on side_stream beside the plain-class one
+    // (they read and write disjoint items; forked after the selection, joined before the trace),
+    // with its own spill area (NULL side_stream: one stream)
+    hipStream_t side_stream;
+    uint32_t* side_spill;
+    hipEvent_t ev_side_fork, ev_side_join;
     // chunked ReSTIR DI initial candidates (launch_frames_restir): up to ci_chunk samples per
     // chunk; ci_planes' G-buffer / rs_init / rs_plights pointers are the chunk's planes (NULL
     // ci_planes or ci_chunk < 2: one sample's chain at a time)

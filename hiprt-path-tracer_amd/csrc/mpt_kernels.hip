@@ -1515,7 +1515,7 @@ struct ShadeArgs {
 #define MPT_SHADE_WAVES 2
 #endif
 #ifndef MPT_SHADE_PEP
-#define MPT_SHADE_PEP 1   // the plain kernel's per-vertex terms as the plain record (dev_bsdf.h PEvalP)
+#define MPT_SHADE_PEP 0   // 1: the plain kernel keeps the per-vertex terms as the plain record (dev_bsdf.h PEvalP): measured +0.7 % at 2 waves, +2.8 % at 3 (77 spilled VGPRs), r06c
 #endif
 // Material classes (mat_tex bit MT_FULL, k_resolve_materials): k_split sorts the hit
 // vertices into the plain-dielectric list (no coat, sheen, metal, transmission or thin film:
@@ -2719,6 +2719,21 @@ static int halo_exchange(const MptFrame& hf, LaunchCfg& cfg, hipStream_t st, int
     return x.halo_rows;
 }
 
+// The generic-class kernel of a staged stage on the side stream (LaunchCfg::side_stream), forked
+// from `st` here and joined by side_end; the side kernels take their own traversal spill area
+static hipStream_t side_begin(LaunchCfg& cfg, hipStream_t st, DevPaths& PS) {
+    if (!cfg.side_stream) return st;
+    hipEventRecord(cfg.ev_side_fork, st);
+    hipStreamWaitEvent(cfg.side_stream, cfg.ev_side_fork, 0);
+    PS.stack_spill = cfg.side_spill;
+    return cfg.side_stream;
+}
+static void side_end(LaunchCfg& cfg, hipStream_t st) {
+    if (!cfg.side_stream) return;
+    hipEventRecord(cfg.ev_side_join, cfg.side_stream);
+    hipStreamWaitEvent(st, cfg.ev_side_join, 0);
+}
+
 // One spatial reuse pass: staged (selection, class-sorted target evaluations, traced rays,
 // combine, visibility reuse; restir_di.h) when the reference-default weights are selected and the neighbour counts fit
 // RS_KMAX, else the monolithic kernel.
@@ -2737,10 +2752,15 @@ static void launch_spatial_pass(int ovr, bool def_bias, const MptFrame& hf, Laun
     launch_restir_kernel(ovr, RK_SP_SELECT, gp, st, S, P, d_frame, pass, in, out);
     hipLaunchKernelGGL(k_count_add64, dim3(1), dim3(64), 0, st, P.ray_counts + 5, &P.counters[CTR_RQE0]);
     {
-        TimedScope te(cfg, st, KT_RS_EVAL);
-        launch_restir_kernel(ovr, RK_SP_EVAL_PLAIN, g, st, S, P, d_frame, pass, in, out);
+        DevPaths PS = P;
+        const hipStream_t ss = side_begin(cfg, st, PS);
+        launch_restir_kernel(ovr, RK_SP_EVAL_GENERIC, g, ss, S, PS, d_frame, pass, in, out);
+        {
+            TimedScope te(cfg, st, KT_RS_EVAL);
+            launch_restir_kernel(ovr, RK_SP_EVAL_PLAIN, g, st, S, P, d_frame, pass, in, out);
+        }
+        side_end(cfg, st);
     }
-    launch_restir_kernel(ovr, RK_SP_EVAL_GENERIC, g, st, S, P, d_frame, pass, in, out);
     TraceArgs ta{};
     ta.S = S; ta.P = P; ta.queue = P.rq_list; ta.count_ptr = &P.counters[CTR_RQ]; ta.fetch = &P.counters[CTR_F_RQA];
     ta.raw_o = P.rq_o; ta.raw_d = P.rq_d; ta.raw_key = P.rq_key; ta.raw_occ = P.rq_occ;
@@ -2771,10 +2791,15 @@ static void launch_fused_pass(int ovr, bool def_bias, const MptFrame& hf, Launch
     launch_restir_kernel(ovr, RK_ST_SELECT, gp, st, S, P, d_frame);
     hipLaunchKernelGGL(k_count_add64, dim3(1), dim3(64), 0, st, P.ray_counts + 5, &P.counters[CTR_RQE0]);
     {
-        TimedScope te(cfg, st, KT_RS_EVAL);
-        launch_restir_kernel(ovr, RK_ST_EVAL_PLAIN, g, st, S, P, d_frame);
+        DevPaths PS = P;
+        const hipStream_t ss = side_begin(cfg, st, PS);
+        launch_restir_kernel(ovr, RK_ST_EVAL_GENERIC, g, ss, S, PS, d_frame);
+        {
+            TimedScope te(cfg, st, KT_RS_EVAL);
+            launch_restir_kernel(ovr, RK_ST_EVAL_PLAIN, g, st, S, P, d_frame);
+        }
+        side_end(cfg, st);
     }
-    launch_restir_kernel(ovr, RK_ST_EVAL_GENERIC, g, st, S, P, d_frame);
     TraceArgs ta{};
     ta.S = S; ta.P = P; ta.queue = P.rq_list; ta.count_ptr = &P.counters[CTR_RQ]; ta.fetch = &P.counters[CTR_F_RQA];
     ta.raw_o = P.rq_o; ta.raw_d = P.rq_d; ta.raw_key = P.rq_key; ta.raw_occ = P.rq_occ;
@@ -2852,8 +2877,13 @@ static void restir_initial(const DevScene& S, const DevPaths& P, const MptFrame*
             hipMemsetAsync(&P.counters[CTR_RQ], 0, CTR_RQ_GROUP * sizeof(int32_t), st);   // the lists + their work counters
             hipLaunchKernelGGL(k_rsi_classify, dim3((P.n + TB * RSI_PPT - 1) / (TB * RSI_PPT)), dim3(TB), 0, st, S, P, d_frame,
                                ovr == MPT_BSDF_NONE ? 1 : 0);
-            launch_restir_kernel(ovr, RK_INITIAL_STAGED_PLAIN, g, st, S, P, d_frame);
-            launch_restir_kernel(ovr, RK_INITIAL_STAGED_GENERIC, g, st, S, P, d_frame);
+            {
+                DevPaths PS = P;
+                const hipStream_t ss = side_begin(cfg, st, PS);
+                launch_restir_kernel(ovr, RK_INITIAL_STAGED_GENERIC, g, ss, S, PS, d_frame);
+                launch_restir_kernel(ovr, RK_INITIAL_STAGED_PLAIN, g, st, S, P, d_frame);
+                side_end(cfg, st);
+            }
             TraceArgs ta{};
             ta.S = S; ta.P = P; ta.queue = P.rq_list; ta.count_ptr = &P.counters[CTR_RQ]; ta.fetch = &P.counters[CTR_F_RQA];
             ta.raw_o = P.rq_o; ta.raw_d = P.rq_d; ta.raw_key = P.rq_key; ta.raw_occ = P.rq_occ;

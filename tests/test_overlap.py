@@ -33,3 +33,27 @@ def test_overlap_city_band(monkeypatch, luts):
         f.render_settings.do_alpha_testing = True
     out = _render_modes(monkeypatch, city, luts, frs, env=env, batch=4, var="MPT_OVERLAP", modes=(0, 1))
     _assert_modes_equal(out, oracle_for(city, luts, env).render(frs, aov=True), "city band overlapped")
+
+
+@pytest.mark.parametrize("case", ["mis", "ris_adaptive", "low_res", "envmap_odd_rows"])
+def test_pixel_parts_one_sample_frames(monkeypatch, luts, case):
+    """One-sample frames of a whole-frame context as 2 / 3 / 4 row parts on their own streams
+    (MPT_PIX_PARTS, frames of at least 65536 pixels; part k renders its rows as band k of the
+    parts): bit-exact against one stream and the oracle -- an odd row count, adaptive sampling
+    past its minimum, a low-resolution frame (all of its pixels in the first part)."""
+    import mpt
+    sd = scene.load_scene("cornell_pbr")
+    lss = STRATEGIES["ris"] if case == "ris_adaptive" else STRATEGIES["mis"]
+    env = mpt.build_envmap(scene.procedural_sky(128, 64, seed=7)) if case.startswith("envmap") else None
+    w, h = (256, 257) if case == "envmap_odd_rows" else (320, 206)
+    frs = frames(sd, w, h, 4, lss=lss, world=scene.envmap_world(1.0) if env is not None else None)
+    if case == "ris_adaptive":
+        for f in frs:
+            f.render_settings.enable_adaptive_sampling = True
+            f.render_settings.adaptive_sampling_min_samples = 1
+            f.render_settings.adaptive_sampling_noise_threshold = 0.9
+    if case == "low_res":
+        frs[2].render_settings.wants_render_low_resolution = True
+        frs[2].render_settings.render_low_resolution_scaling = 2
+    out = _render_modes(monkeypatch, sd, luts, frs, env=env, var="MPT_PIX_PARTS", modes=(0, 2, 3, 4))
+    _assert_modes_equal(out, oracle_for(sd, luts, env).render(frs, aov=True), f"pixel parts {case}")

@@ -139,6 +139,8 @@ def main(src, dst):
                 out[k]["timed"] = e
     meta = {"source": src, "note": __doc__.strip().splitlines()[0],
             "bench_command_line": {kk: line.get(kk) for kk in ("steps", "warmup", "config", "ms_per_step", "value")} if line else None,
+            # the library the profiled command ran (bench.py compares it with the one it runs)
+            "libmpt_sha256_16": ((line or {}).get("device") or {}).get("libmpt_sha256_16"),
             "kernels": out}
     json.dump(meta, open(dst, "w"), indent=1)
     for k, v in sorted(out.items(), key=lambda kv: -(kv[1]["traffic_bytes"] or 0)):
