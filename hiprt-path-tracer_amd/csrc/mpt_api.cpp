@@ -132,7 +132,7 @@ struct MptContext {
     // 0 / 1 off, 2 .. PIX_PARTS_MAX parts)
     int pix_parts = 3;   // batch-1 C3 6.09 -> 5.44 (2 parts) -> 5.29 ms/spp (3); 4 parts 6.76 (past GPU_MAX_HW_QUEUES), r06d
     // staged ReSTIR DI stages: the generic-class kernel on a side stream beside the plain one
-    // (MPT_RESTIR_SIDE)
+    // (MPT_RESTIR_SIDE: 1 for partitions of at most 2^20 pixels, 2 always, 0 never)
     int restir_side = 1;
     hipEvent_t ev_side[2] = {nullptr, nullptr};
     hipGraphExec_t graph_exec = nullptr;
@@ -287,6 +287,9 @@ struct MptContext {
     // frame restarts it, every frame with the adaptive buffers adds at most one sample; unknown
     // (large) until a reset frame has been launched
     int as_bound = 1 << 30;
+    // the last batch reset the adaptive buffers in its k_accumulate (which an overlapped next batch
+    // would run beside): the next ReSTIR DI batch does not overlap it
+    bool as_reset_pending = false;
     DBuf<uint8_t> comm_send, comm_recv;
 };
 
@@ -1330,11 +1333,13 @@ static int prepare_batch(MptContext* c, const MptFrame* f, int batch) {
         return fail(MPT_ERR_OUT_OF_MEMORY, "wavefront above MPT_MAX_WAVEFRONT_PATHS paths");
     // overlapped ReSTIR DI batches need both halves of the path state (2 x the batch); without
     // the room they run one after the other
-    // (not under adaptive sampling: the next batch's camera gate reads the converged counts this
-    // batch's k_accumulate writes at its end)
+    // (under adaptive sampling such batches run only while the gate is static, restir_gate_static:
+    // the converged counts the next batch's chain reads are the ones the running batch's
+    // k_accumulate rewrites unchanged -- unless that batch reset them)
     const MptRenderSettings& frs = f->render_settings;
     const bool adaptive = (frs.stop_pixel_noise_threshold > 0.0f || frs.enable_adaptive_sampling) && frs.accumulate;
-    const bool want_overlap = f->options.direct_light_sampling == MPT_LSS_RESTIR_DI && batch > 1 && c->restir_overlap && !adaptive &&
+    const bool want_overlap = f->options.direct_light_sampling == MPT_LSS_RESTIR_DI && batch > 1 && c->restir_overlap &&
+                              !(adaptive && c->as_reset_pending) &&
                               ext_layout(*f, nullptr) == 0 && (int64_t)std::max(c->n_slots, 1) * 2 * batch <= MPT_MAX_WAVEFRONT_PATHS;
     c->restir_overlap_ok = false;
     if (want_overlap) {
@@ -1527,7 +1532,10 @@ static int launch_batch(MptContext* c, const MptFrame* f, int batch) {
         cfg.ci_chunk = c->ci_chunk;
         cfg.ci_planes = &c->ci_dp;
     }
-    if (f->options.direct_light_sampling == MPT_LSS_RESTIR_DI && c->restir_side && c->restir_staged) {
+    // (a band of a split frame: its kernels are tail-bound -- 8-way 1080p C4 at 20 steps, slowest band
+    // 1.734 -> 1.705 ms/spp; the whole 1080p frame measured 8.12 -> 8.17, so not there, r06e)
+    if (f->options.direct_light_sampling == MPT_LSS_RESTIR_DI && c->restir_staged &&
+        (c->restir_side > 1 || (c->restir_side == 1 && c->n_slots <= (1 << 20)))) {
         int rr = ensure_pix_parts(c, 3);   // (streamx[0] and its spill area)
         if (rr != MPT_OK) return rr;
         for (hipEvent_t& ev : c->ev_side)
@@ -1559,6 +1567,9 @@ static int launch_batch(MptContext* c, const MptFrame* f, int batch) {
     {
         const MptRenderSettings& rs = f->render_settings;
         P.spec_as = batch > 1 && (rs.stop_pixel_noise_threshold > 0.0f || rs.enable_adaptive_sampling) && rs.accumulate;
+        // a pixel converges only at a gate with its count above the minimum, so while the bound on
+        // the counts is at most the minimum no pixel has converged and none is left out
+        P.spec_skip = P.spec_as && rs.enable_adaptive_sampling && c->as_bound > rs.adaptive_sampling_min_samples;
     }
     if (restir_part) {   // frame_begin maintains the band and the previous frame's halo rows
         P.rs_lo = std::max(0, cfg.own_y0 - cfg.halo_prev) * f->res_x;
@@ -1683,7 +1694,11 @@ static int launch_batch(MptContext* c, const MptFrame* f, int batch) {
     }
     c->frames_submitted++;
     c->frames += batch;
-    for (int k = 0; k < batch; k++) c->as_bound = next_as_bound(c->as_bound, f[k]);
+    c->as_reset_pending = false;
+    for (int k = 0; k < batch; k++) {
+        c->as_bound = next_as_bound(c->as_bound, f[k]);
+        c->as_reset_pending |= batch > 1 && has_adaptive(f[k]) && is_reset(f[k]);
+    }
     c->trace_launches += cfg.launches;
     return MPT_OK;
 }
@@ -1765,12 +1780,17 @@ static bool batchable(const MptContext* c, const MptFrame& a, const MptFrame& b)
 // frame (a reset clears the converged counts the passes read) and the host's bound on
 // pixel_sample_count before it, as_bound + k, is at most the minimum.  The stop-noise threshold
 // alone never refuses a sample and the passes do not read its counts: always static.
+// A run may also start with a reset frame: the passes read the converged counts -- which the
+// batch's k_accumulate resets only at its end -- only at sample numbers of at least the minimum
+// (restir_spatial_neighbor), so the run's sample numbers stay below it.
 static bool restir_gate_static(const MptContext* c, const MptFrame* run, int k) {
     const MptFrame& a = run[0];
     const MptRenderSettings& rs = a.render_settings;
     if (a.options.direct_light_sampling != MPT_LSS_RESTIR_DI || !rs.enable_adaptive_sampling || !rs.accumulate) return true;
-    if (is_reset(a) || is_reset(run[k])) return false;
-    return (int64_t)c->as_bound + k <= (int64_t)rs.adaptive_sampling_min_samples;
+    if (is_reset(run[k])) return false;
+    const int mn = rs.adaptive_sampling_min_samples;
+    if (is_reset(a)) return k <= mn && a.render_settings.sample_number < mn && run[k].render_settings.sample_number < mn;
+    return (int64_t)c->as_bound + k <= (int64_t)mn;
 }
 
 // The overlapped ReSTIR DI wavefronts of the call joined into the context's stream: everything

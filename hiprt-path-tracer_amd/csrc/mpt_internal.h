@@ -188,6 +188,8 @@ struct DevPaths {
     uint8_t* active;          // pixel_active
     int32_t spec_as;          // a batch of adaptive samples: traced speculatively, gated in k_accumulate
     int32_t spec_reset;       // (k_camera, one sample of a batch) an earlier sample of the batch resets the buffers
+    int32_t spec_skip;        // spec_as under enable_adaptive_sampling with pixels possibly converged before the
+                              // batch: k_camera leaves them out of the camera queue (host: MptContext::as_bound)
     uint32_t* status;         // [0] stop_noise_threshold_converged_count, [1] still_one_ray_active
     // ReSTIR DI (LSS_RESTIR_DI only; NULL otherwise).  G-buffer of the camera hits as
     // CameraRays writes it (CameraRays.h:144-166, GBuffer.h:17-34), current + previous frame:

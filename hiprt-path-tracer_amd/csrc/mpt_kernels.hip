@@ -912,9 +912,10 @@ __global__ __launch_bounds__(TB) void k_camera(DevPaths P, const MptFrame* __res
     // (AdaptiveSampling.h:45-48: the gate refuses it while pixel_converged_sample_count != -1) until
     // a reset, so a pixel that had converged before the batch began -- with no reset frame among
     // the batch's samples up to this one -- gets no camera ray: the gate will refuse that sample.
-    // The camera queue is then compacted (spec_skip).
+    // The camera queue is then compacted (P.spec_skip: set by the host unless no pixel can have
+    // converged yet -- every pixel's count still at most the minimum since the last reset).
     const bool as = has_adaptive_buffers(rs) && !P.spec_as;
-    const bool spec_skip = P.spec_as && rs.enable_adaptive_sampling && rs.accumulate;
+    const bool spec_skip = P.spec_skip != 0;
     const bool lr = low_res(rs);
     bool act = slot < P.n;
     int x = 0, y = 0;
@@ -2750,7 +2751,6 @@ static void launch_spatial_pass(int ovr, bool def_bias, const MptFrame& hf, Laun
     const dim3 gp(blocks_for(P.n));
     hipMemsetAsync(&P.counters[CTR_RQ], 0, CTR_RQ_GROUP * sizeof(int32_t), st);   // the lists + their work counters
     launch_restir_kernel(ovr, RK_SP_SELECT, gp, st, S, P, d_frame, pass, in, out);
-    hipLaunchKernelGGL(k_count_add64, dim3(1), dim3(64), 0, st, P.ray_counts + 5, &P.counters[CTR_RQE0]);
     {
         DevPaths PS = P;
         const hipStream_t ss = side_begin(cfg, st, PS);
@@ -2789,7 +2789,6 @@ static void launch_fused_pass(int ovr, bool def_bias, const MptFrame& hf, Launch
     const dim3 gp(blocks_for(P.n));
     hipMemsetAsync(&P.counters[CTR_RQ], 0, CTR_RQ_GROUP * sizeof(int32_t), st);   // the lists + their work counters
     launch_restir_kernel(ovr, RK_ST_SELECT, gp, st, S, P, d_frame);
-    hipLaunchKernelGGL(k_count_add64, dim3(1), dim3(64), 0, st, P.ray_counts + 5, &P.counters[CTR_RQE0]);
     {
         DevPaths PS = P;
         const hipStream_t ss = side_begin(cfg, st, PS);
@@ -2983,9 +2982,9 @@ static void launch_restir(const DevScene& S, DevPaths& P, const MptFrame* d_fram
 }
 
 // CameraRays' G-buffer write and the ReSTIR DI passes of a frame (P.rs_out: their output)
+// (k_restir_frame_begin, right before in the stream, zeroed the halo measure CTR_REPROJ)
 static void restir_first_bounce(const DevScene& S, DevPaths& P, const MptFrame* d_frame, const MptFrame& hf, LaunchCfg& cfg,
                                 hipStream_t st) {
-    if (cfg.halo_fn) hipMemsetAsync(&P.counters[CTR_REPROJ], 0, sizeof(int32_t), st);
     {
         TimedScope tk(cfg, st, KT_GBUFFER);
         hipLaunchKernelGGL(k_gbuffer, dim3(blocks_for(P.n)), dim3(TB), 0, st, S, P, d_frame);
@@ -3137,13 +3136,16 @@ hipError_t launch_frame(const DevScene& S, const DevPaths& P0, const MptFrame* d
     // low resolution
     const bool as = ((hrs.stop_pixel_noise_threshold > 0.0f || hrs.enable_adaptive_sampling) && hrs.accumulate && !P.spec_as) ||
                     (hrs.wants_render_low_resolution && hrs.allow_render_low_resolution && hrs.accumulate) ||
-                    (P.spec_as && hrs.enable_adaptive_sampling && hrs.accumulate);   // (k_camera's spec_skip)
+                    P.spec_skip;   // (k_camera's spec_skip)
+    // all pixels start a path, unless adaptive sampling compacts the camera queue (the counter set
+    // by k_restir_frame_begin under ReSTIR DI, with the halo measure zeroed)
     if (hf.options.direct_light_sampling == MPT_LSS_RESTIR_DI) {
-        hipLaunchKernelGGL(k_restir_frame_begin, dim3(blocks_for(P.rs_hi - P.rs_lo)), dim3(TB), 0, st, P, d_frame);
+        hipLaunchKernelGGL(k_restir_frame_begin, dim3(std::max(1, blocks_for(P.rs_hi - P.rs_lo))), dim3(TB), 0, st, P, d_frame, as ? 0 : n,
+                           cfg.halo_fn ? 1 : 0);
         P.rs_out = restir_buffer(P, cfg.restir_out_sp2);
+    } else {
+        hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(&P.counters[CTR_Q0]), as ? 0 : n, 1, st);
     }
-    // all pixels start a path, unless adaptive sampling compacts the camera queue
-    hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(&P.counters[CTR_Q0]), as ? 0 : n, 1, st);
     {
         TimedScope ts(cfg, st, KT_CAMERA);
         hipLaunchKernelGGL(k_camera, dim3(blocks_for(n)), dim3(TB), 0, st, P, d_frame);
@@ -3210,7 +3212,7 @@ hipError_t launch_frames_restir(const DevScene& S, const DevPaths& PF, const Mpt
     // gets no camera ray (k_camera's spec_skip, `active` cleared), so the camera queues are built
     // from `active` -- all samples' for the one traversal, then each sample's own before its
     // G-buffer -- and k_accumulate replays the gate in sample order
-    const bool skip = PF.spec_as && hf[0].render_settings.enable_adaptive_sampling && hf[0].render_settings.accumulate;
+    const bool skip = PF.spec_skip != 0;
     bool reset_before = false;
     for (int s = 0; s < batch; s++) {
         DevPaths P = PF;
@@ -3300,13 +3302,11 @@ hipError_t launch_frames_restir(const DevScene& S, const DevPaths& PF, const Mpt
                            hipMemcpyDeviceToDevice, st);
             continue;
         }
-        hipLaunchKernelGGL(k_restir_frame_begin, dim3(blocks_for(P.rs_hi - P.rs_lo)), dim3(TB), 0, st, P, d_frames + s);
-        if (skip) {   // the sample's camera queue: its active slots
-            hipMemsetAsync(&P.counters[CTR_Q0], 0, sizeof(int32_t), st);
-            hipLaunchKernelGGL(k_queue_active, dim3(blocks_for(n)), dim3(TB), 0, st, P.q0, &P.counters[CTR_Q0], P.active, n);
-        } else {
-            hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(&P.counters[CTR_Q0]), n, 1, st);   // the camera queue (k_camera's iota)
-        }
+        // (the camera queue's length: n, k_camera's iota, or 0 for k_queue_active's list of the
+        // sample's active slots; the halo measure zeroed)
+        hipLaunchKernelGGL(k_restir_frame_begin, dim3(std::max(1, blocks_for(P.rs_hi - P.rs_lo))), dim3(TB), 0, st, P, d_frames + s,
+                           skip ? 0 : n, cfg.halo_fn ? 1 : 0);
+        if (skip) hipLaunchKernelGGL(k_queue_active, dim3(blocks_for(n)), dim3(TB), 0, st, P.q0, &P.counters[CTR_Q0], P.active, n);
         if (defer) {
             restir_first_bounce(S, P, d_frames + s, hf[s], cfg, st);
             if (cfg.halo_fn) cfg.halo_prev = cfg.halo_rows;

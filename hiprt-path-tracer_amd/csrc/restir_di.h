@@ -1532,6 +1532,9 @@ RESTIR_KERNEL void k_rsp_eval(DevScene S, DevPaths P, const MptFrame* __restrict
     const uint32_t pass_rs = FUSED ? F.restir_di_seeds[2] : F.restir_di_seeds[4 + pass];
     const bool alpha = F.render_settings.do_alpha_testing;
     const int count = *count_ptr;
+    // the plain-class evaluation counter (ray_counts[5]: MptStats::restir_eval_items), added here
+    // instead of by a launch of its own
+    if (PLAIN && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd((unsigned long long*)(P.ray_counts + 5), (unsigned long long)(uint32_t)count);
     for (int b0 = blockIdx.x * TB; b0 < count; b0 += gridDim.x * TB) {
         const int i = b0 + (int)threadIdx.x;
         uint32_t rmask = 0u;
@@ -1984,9 +1987,16 @@ __global__ __launch_bounds__(TB) void k_chunk_join(DevPaths P, DevPaths C, const
 
 // CameraRays' reset / previous-frame G-buffer copy for LSS_RESTIR_DI (CameraRays.h:19-34, 78-91)
 #ifndef MPT_TU_PART   // k_restir_frame_begin
-__global__ __launch_bounds__(TB) void k_restir_frame_begin(DevPaths P, const MptFrame* __restrict__ Fp) {
+__global__ __launch_bounds__(TB) void k_restir_frame_begin(DevPaths P, const MptFrame* __restrict__ Fp, int32_t q0_count,
+                                                           int32_t zero_reproj) {
     const MptFrame& F = *Fp;
     const MptRenderSettings& rs = F.render_settings;
+    // the frame's counters, set here instead of by launches of their own (the kernels that read
+    // them follow in the stream): the camera queue's length, and the halo measure k_gbuffer raises
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        if (q0_count >= 0) P.counters[CTR_Q0] = q0_count;
+        if (zero_reproj) P.counters[CTR_REPROJ] = 0;
+    }
     int i = P.rs_lo + blockIdx.x * TB + threadIdx.x;   // the band and its halo rows
     if (i >= P.rs_hi) return;
     // low resolution: only the representatives' entries (pixel_index / s) are copied and reset

@@ -677,7 +677,7 @@ def test_gpu_restir_overlapped_batch_then_unbatched_frame(cornell, luts, monkeyp
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("case", ["fused", "unfused", "envmap", "partitioned"])
+@pytest.mark.parametrize("case", ["fused", "unfused", "envmap", "partitioned", "restart"])
 def test_gpu_restir_adaptive_batched_bit_exact(cornell, luts, case):
     """ReSTIR DI under adaptive sampling through mpt_render_frames: the samples whose gate is static
     (no pixel can reach the noise test before adaptive_sampling_min_samples) run as batched
@@ -696,11 +696,19 @@ def test_gpu_restir_adaptive_batched_bit_exact(cornell, luts, case):
     frs = frames(cornell, abi.LSS_RESTIR_DI, n, w=w, h=h, reuse_radius=5, **kw)
     for f in frs:
         f.render_settings.do_update_status_buffers = True
+    if case == "restart":
+        # a restart at sample 0 after pixels converged (GPURenderer::reset): the run starting with
+        # the reset frame is batched (sample numbers below the minimum), its k_accumulate resets the
+        # converged counts the earlier frames left
+        for k, f in enumerate(frs[8:]):
+            f.render_settings.sample_number = k
+            f.render_settings.need_to_reset = k == 0
     o = orc.Oracle(cornell, luts, envmap=env)
     c, ca, cn = o.render(frs, aov=True)
     aux = o.last_aux
     o.close()
-    assert (aux["converged_sample_count"] >= 0).any(), "the test needs pixels converging"
+    if case != "restart":   # (the restart's four samples stay below the minimum)
+        assert (aux["converged_sample_count"] >= 0).any(), "the test needs pixels converging"
     if case == "partitioned":
         st = []
         got = render_partitioned_local(cornell, luts, lambda band: frames(cornell, abi.LSS_RESTIR_DI, n, w=w, h=h, band=band,
