@@ -708,6 +708,11 @@ def run_workload(a, world, rank, local, dist, coll_dev, quiet=False):
             # two halves on two streams, so this kernel's launches shared the GPU with the other
             # half's kernels -- its launch time, and with it `achieved`, is not the kernel's alone
             r["shared_gpu"] = f"{st.overlapped_batches} overlapped batch(es): launch times shared with the other half"
+        elif x["unit_of_work"] == "ray" and getattr(st, "trace_ahead_launches", 0):
+            # MPT_TRACE_AHEAD: a bounce's path traversal ran beside the previous bounce's NEE
+            # traversals, so the traversal stages' launch times overlap
+            r["shared_gpu"] = (f"{st.trace_ahead_launches} path traversal(s) launched ahead: launch times shared with "
+                               "the previous bounce's NEE traversals")
         elif getattr(st, "restir_overlapped_batches", 0):
             # MPT_RESTIR_OVERLAP: a ReSTIR DI batch's later bounces ran on the second stream beside
             # the next batch's per-sample chain

@@ -135,6 +135,11 @@ struct MptContext {
     // (MPT_RESTIR_SIDE: 1 for partitions of at most 2^20 pixels, 2 always, 0 never)
     int restir_side = 1;
     hipEvent_t ev_side[2] = {nullptr, nullptr};
+    // trace-ahead (MPT_TRACE_AHEAD): the next bounce's path traversal beside this bounce's NEE
+    // traversals and resolve, on streamx[1]
+    int trace_ahead = 1;
+    hipEvent_t ev_ahead[2] = {nullptr, nullptr};
+    uint32_t ahead_launches = 0;   // MptStats::trace_ahead_launches
     hipGraphExec_t graph_exec = nullptr;
     std::vector<uint8_t> graph_key;
     uint32_t graph_launches = 0;
@@ -169,6 +174,7 @@ struct MptContext {
     DBuf<int32_t> mat_tex;
     DBuf<float4> em_tab;
     bool any_tex = false;
+    bool any_glass = false;   // a material of the glass class (MT_GLASS): k_shade<GLASS> is launched
     double tex_tri_frac = 0.0;            // triangles with a textured material / all (resolve_materials)
     int mat_private = -1;                 // MPT_MAT_PRIVATE: 1 / 0 force k_shade's MATP, -1 by tex_tri_frac
     // material-class shading (k_split / k_shade): 1 on (default), 0 off, 2 on with every
@@ -779,8 +785,11 @@ int resolve_materials(MptContext* c) {
     std::vector<int32_t> t(n);
     HIPCHK(hipMemcpyAsync(t.data(), c->mat_tex.p, n * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
-    c->any_tex = false;
-    for (int32_t v : t) c->any_tex |= (v & MT_TEXTURED) != 0;
+    c->any_tex = c->any_glass = false;
+    for (int32_t v : t) {
+        c->any_tex |= (v & MT_TEXTURED) != 0;
+        c->any_glass |= (v & MT_GLASS) != 0;
+    }
     // the share of triangles with a textured material: above 1/4 the shading kernels hold a
     // textured vertex's resolved material in private memory (k_shade's MATP)
     size_t n_tex_tris = 0;
@@ -988,6 +997,7 @@ int mpt_create(int device, void* hip_stream, MptContext** out) {
     if (const char* e = std::getenv("MPT_GRAPHS")) c->graphs = std::atoi(e);
     if (const char* e = std::getenv("MPT_PIX_PARTS")) c->pix_parts = std::atoi(e);
     if (const char* e = std::getenv("MPT_RESTIR_SIDE")) c->restir_side = std::atoi(e);
+    if (const char* e = std::getenv("MPT_TRACE_AHEAD")) c->trace_ahead = std::atoi(e);
     if (const char* e = std::getenv("MPT_RESTIR_MAX_BATCH"))
         c->restir_max_batch = std::max(1, std::min(RESTIR_MAX_BATCH, std::atoi(e)));
     if (const char* e = std::getenv("MPT_RESTIR_CHUNK")) c->restir_chunk = std::atoi(e);
@@ -1035,6 +1045,7 @@ int mpt_destroy(MptContext* c) {
         if (c->streamx[k]) (void)hipStreamDestroy(c->streamx[k]);
         if (c->ev_joinx[k]) (void)hipEventDestroy(c->ev_joinx[k]);
         if (c->ev_side[k]) (void)hipEventDestroy(c->ev_side[k]);
+        if (c->ev_ahead[k]) (void)hipEventDestroy(c->ev_ahead[k]);
     }
     for (hipEvent_t e : {c->ev_fork, c->ev_first, c->ev_acc, c->ev_join, c->ev_chain, c->ev_half[0], c->ev_half[1],
                          c->ev_wave_join})
@@ -1545,7 +1556,8 @@ static int launch_batch(MptContext* c, const MptFrame* f, int batch) {
         cfg.ev_side_fork = c->ev_side[0];
         cfg.ev_side_join = c->ev_side[1];
     }
-    cfg.shade_glass = c->shade_glass;
+    // (no glass-class material: k_split's glass list stays empty, so the kernel is not launched)
+    cfg.shade_glass = c->shade_glass && c->any_glass;
     cfg.shade_split = c->shade_split;
     cfg.mat_private = c->mat_private >= 0 ? (c->mat_private != 0) : (c->tex_tri_frac >= 0.25);
     cfg.light_bvh = c->light_bvh && c->light_bvh_ok;
@@ -1680,7 +1692,18 @@ static int launch_batch(MptContext* c, const MptFrame* f, int batch) {
     } else if (batch == 1 && c->graphs && !c->timing && f->options.direct_light_sampling != MPT_LSS_RESTIR_DI) {
         e = launch_frame_graph(c, P, f, slot, cfg);
     } else {
+        if (c->trace_ahead && f->options.direct_light_sampling != MPT_LSS_RESTIR_DI && f->render_settings.nb_bounces > 0) {
+            int rr = ensure_pix_parts(c, 4);   // (streamx[1] and its spill area)
+            if (rr != MPT_OK) return rr;
+            for (hipEvent_t& ev : c->ev_ahead)
+                if (!ev) HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+            cfg.ahead_stream = c->streamx[1];
+            cfg.ahead_spill = c->spillx[1].p;
+            cfg.ev_ahead_fork = c->ev_ahead[0];
+            cfg.ev_ahead_join = c->ev_ahead[1];
+        }
         e = launch_frame(dev_scene(c), P, c->d_frames + slot, *f, cfg, c->stream);
+        c->ahead_launches += cfg.ahead_launches;
     }
     c->restir_out_sp2 = cfg.restir_out_sp2;
     if (restir_part) c->halo_prev = cfg.halo_rows;
@@ -2281,6 +2304,7 @@ int mpt_enable_stats(MptContext* c, int enable, int instrumented) {
     c->overlapped_batches = 0;
     c->halo_exchanges = c->halo_agreements = c->halo_bytes_sent = c->halo_bytes_recv = 0;
     c->restir_overlapped_batches = 0;
+    c->ahead_launches = 0;
     for (int m = 0; m < KT_COUNT; m++) { c->stage_ms[m] = 0.0; c->stage_launches[m] = 0; }
     HIPCHK(hipMemsetAsync(c->stats.p, 0, N_STATS * sizeof(uint64_t), c->stream));
     HIPCHK(hipMemsetAsync(c->ray_counts.p, 0, N_RAY_COUNTS * sizeof(uint64_t), c->stream));
@@ -2346,6 +2370,7 @@ int mpt_get_stats(MptContext* c, MptStats* out) {
     out->halo_bytes_sent = c->halo_bytes_sent;
     out->halo_bytes_received = c->halo_bytes_recv;
     out->restir_overlapped_batches = c->restir_overlapped_batches;
+    out->trace_ahead_launches = c->ahead_launches;
     return MPT_OK;
 }
 

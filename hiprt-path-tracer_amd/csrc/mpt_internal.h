@@ -347,6 +347,12 @@ struct LaunchCfg {
     hipStream_t side_stream;
     uint32_t* side_spill;
     hipEvent_t ev_side_fork, ev_side_join;
+    // trace-ahead (frame_bounces): bounce b + 1's path traversal on ahead_stream beside bounce b's
+    // NEE traversals and resolve, with its own spill area (NULL ahead_stream: one stream)
+    hipStream_t ahead_stream;
+    uint32_t* ahead_spill;
+    hipEvent_t ev_ahead_fork, ev_ahead_join;
+    uint32_t ahead_launches;   // out: path traversals launched ahead
     // chunked ReSTIR DI initial candidates (launch_frames_restir): up to ci_chunk samples per
     // chunk; ci_planes' G-buffer / rs_init / rs_plights pointers are the chunk's planes (NULL
     // ci_planes or ci_chunk < 2: one sample's chain at a time)

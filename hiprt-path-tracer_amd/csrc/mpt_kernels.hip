@@ -2195,9 +2195,12 @@ DEV int shaded_entry(const DevPaths& P, int nh, int i) {
 
 // k_compact: next path queue + NEE query lists from the per-path masks of the shaded paths
 #ifndef MPT_TU_PART   // k_compact
-__global__ __launch_bounds__(CP_NT) void k_compact(DevPaths P, int32_t* q_next, int32_t* count_next) {
+__global__ __launch_bounds__(CP_NT) void k_compact(DevPaths P, int32_t* q_next, int32_t* count_next, int32_t* zero_fetch) {
     __shared__ int tmp[CP_NT / 64 + 1];
     __shared__ int base[5];
+    // the next bounce's path traversal, launched right after on the trace-ahead stream, takes its
+    // work counter zeroed (frame_bounces)
+    if (zero_fetch && blockIdx.x == 0 && threadIdx.x == 0) *zero_fetch = 0;
     const int nh = P.counters[CTR_HIT];
     const int count = shaded_count(P);
     const int b0 = blockIdx.x * CP_NT * CP_ITEMS;
@@ -3006,13 +3009,16 @@ static void frame_bounces(const DevScene& S, DevPaths& P, const MptFrame* d_fram
     // extended light sampling (DevPaths::x_per > 0): the EXT shading / resolve kernels, one class
     const bool ext = P.x_per > 0;
     const int classes = (hf.options.bsdf_override != MPT_BSDF_NONE || ext) ? 0 : (cfg.shade_classes != 0 ? (cfg.shade_glass ? 2 : 1) : 0);
+    // the next bounce's path rays on the trace-ahead stream (below); not with ReSTIR DI (its first
+    // bounce's G-buffer and reuse passes sit between the trace and the split)
+    const bool ahead = cfg.ahead_stream != nullptr && !restir;
     for (int b = b_first; b <= b_last; b++) {
         // every per-bounce counter (lists, class queues, the traversals' work counters) in one
         // memset; the next path queue's counter is zeroed by k_split
         hipMemsetAsync(&P.counters[CTR_BOUNCE_FIRST], 0, (CTR_COUNT - CTR_BOUNCE_FIRST) * sizeof(int32_t), st);
         // continuation / camera rays (first_traced: the first bounce's rays were traced already)
         const int alpha = hf.render_settings.do_alpha_testing ? 1 : 0;
-        if (!(first_traced && b == b_first)) {
+        if (!(first_traced && b == b_first) && !(ahead && b > b_first)) {
             TraceArgs ta{};
             ta.S = S; ta.P = P; ta.queue = q_cur; ta.count_ptr = &P.counters[c_cur]; ta.fetch = &P.counters[CTR_F_PATH];
             ta.F = d_frame; ta.bounce = b; ta.alpha = alpha;
@@ -3072,7 +3078,27 @@ static void frame_bounces(const DevScene& S, DevPaths& P, const MptFrame* d_fram
             TimedScope ts(cfg, st, KT_COMPACT);
             // the shaded list (qh ++ qf) holds up to 2n entries: deferred vertices appear in both
             const dim3 cp_grid2((2 * n + CP_NT * CP_ITEMS - 1) / (CP_NT * CP_ITEMS));
-            hipLaunchKernelGGL(k_compact, classes ? cp_grid2 : cp_grid, dim3(CP_NT), 0, st, P, q_next, &P.counters[c_next]);
+            hipLaunchKernelGGL(k_compact, classes ? cp_grid2 : cp_grid, dim3(CP_NT), 0, st, P, q_next, &P.counters[c_next],
+                               ahead && b < b_last ? &P.counters[CTR_F_PATH] : nullptr);
+        }
+        // Trace-ahead: the next bounce's path rays depend only on the continuation list k_compact
+        // just wrote, not on this bounce's NEE queries or k_resolve (which read the NEE planes,
+        // occlusion bytes and light hits, none of which the path traversal writes: it writes the
+        // hits, hit classes and retrace origins of the continuation slots), so they are traced on
+        // the trace-ahead stream beside this bounce's NEE traversals and resolve, with their own
+        // traversal spill area; joined before the next bounce's split
+        const bool fork = ahead && b < b_last;
+        if (fork) {
+            hipEventRecord(cfg.ev_ahead_fork, st);
+            hipStreamWaitEvent(cfg.ahead_stream, cfg.ev_ahead_fork, 0);
+            DevPaths PA = P;
+            PA.stack_spill = cfg.ahead_spill;
+            TraceArgs ta{};
+            ta.S = S; ta.P = PA; ta.queue = q_next; ta.count_ptr = &P.counters[c_next]; ta.fetch = &P.counters[CTR_F_PATH];
+            ta.F = d_frame; ta.bounce = b + 1; ta.alpha = hf.render_settings.do_alpha_testing ? 1 : 0;
+            timed_trace<TM_PATH>(ta, cfg, cfg.ahead_stream);
+            hipEventRecord(cfg.ev_ahead_join, cfg.ahead_stream);
+            cfg.ahead_launches++;
         }
         // NEE queries (each traversal with its own work counter, zeroed at the top of the bounce)
         TraceArgs tn{};
@@ -3117,6 +3143,7 @@ static void frame_bounces(const DevScene& S, DevPaths& P, const MptFrame* d_fram
             if (ext) hipLaunchKernelGGL(k_resolve<true>, rg, dim3(TB), 0, st, S, P, d_frame, b, &P.counters[c_cur]);
             else hipLaunchKernelGGL(k_resolve<false>, rg, dim3(TB), 0, st, S, P, d_frame, b, &P.counters[c_cur]);
         }
+        if (fork) hipStreamWaitEvent(st, cfg.ev_ahead_join, 0);
         // swap queues
         int32_t* tq = q_cur; q_cur = q_next; q_next = tq;
         int tc = c_cur; c_cur = c_next; c_next = tc;

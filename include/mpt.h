@@ -458,6 +458,9 @@ typedef struct MptStats {
     /* batched ReSTIR DI wavefronts whose later bounces ran on the second stream beside the next
      * batch's per-sample chain (MPT_RESTIR_OVERLAP) */
     uint32_t restir_overlapped_batches;
+    /* path traversals launched ahead, beside the previous bounce's NEE traversals and resolve
+     * (MPT_TRACE_AHEAD): their times and those of the NEE traversals overlap */
+    uint32_t trace_ahead_launches;
 } MptStats;
 
 #define MPT_FB_COLOR 0        /* 'pixels': running SUM of samples (RenderData.h:34-36) */
