@@ -1479,6 +1479,21 @@ static int next_as_bound(int b, const MptFrame& f) {
     if (is_reset(f)) b = 0;
     return b < (1 << 30) ? b + 1 : b;
 }
+// The trace-ahead stream of a single-stream wavefront (frame_bounces): streamx[1], its spill area
+// and events, on first use
+static int set_ahead(MptContext* c, LaunchCfg& cfg, const MptFrame& f) {
+    if (!c->trace_ahead || f.render_settings.nb_bounces <= 0) return MPT_OK;
+    int rr = ensure_pix_parts(c, 4);   // (streamx[1] and its spill area)
+    if (rr != MPT_OK) return rr;
+    for (hipEvent_t& ev : c->ev_ahead)
+        if (!ev) HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    cfg.ahead_stream = c->streamx[1];
+    cfg.ahead_spill = c->spillx[1].p;
+    cfg.ev_ahead_fork = c->ev_ahead[0];
+    cfg.ev_ahead_join = c->ev_ahead[1];
+    return MPT_OK;
+}
+
 // Enqueues a prepared wavefront (prepare_batch).
 static int launch_batch(MptContext* c, const MptFrame* f, int batch) {
     const bool restir_part = f->options.direct_light_sampling == MPT_LSS_RESTIR_DI && f->band_count > 1;
@@ -1664,6 +1679,8 @@ static int launch_batch(MptContext* c, const MptFrame* f, int batch) {
         cfg.ev_used = cfg1.ev_used;
         cfg.launches = cfg0.launches + cfg1.launches;
     } else if (f->options.direct_light_sampling == MPT_LSS_RESTIR_DI && batch > 1) {
+        int ra = set_ahead(c, cfg, *f);   // (the batch's later-bounce wavefront)
+        if (ra != MPT_OK) return ra;
         P.group = std::max(c->n_slots, 1);   // slot = sample * pixels + pixel
         if (c->restir_overlap_ok) {
             int rr = ensure_overlap(c);
@@ -1692,19 +1709,11 @@ static int launch_batch(MptContext* c, const MptFrame* f, int batch) {
     } else if (batch == 1 && c->graphs && !c->timing && f->options.direct_light_sampling != MPT_LSS_RESTIR_DI) {
         e = launch_frame_graph(c, P, f, slot, cfg);
     } else {
-        if (c->trace_ahead && f->options.direct_light_sampling != MPT_LSS_RESTIR_DI && f->render_settings.nb_bounces > 0) {
-            int rr = ensure_pix_parts(c, 4);   // (streamx[1] and its spill area)
-            if (rr != MPT_OK) return rr;
-            for (hipEvent_t& ev : c->ev_ahead)
-                if (!ev) HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-            cfg.ahead_stream = c->streamx[1];
-            cfg.ahead_spill = c->spillx[1].p;
-            cfg.ev_ahead_fork = c->ev_ahead[0];
-            cfg.ev_ahead_join = c->ev_ahead[1];
-        }
+        int rr = set_ahead(c, cfg, *f);
+        if (rr != MPT_OK) return rr;
         e = launch_frame(dev_scene(c), P, c->d_frames + slot, *f, cfg, c->stream);
-        c->ahead_launches += cfg.ahead_launches;
     }
+    c->ahead_launches += cfg.ahead_launches;
     c->restir_out_sp2 = cfg.restir_out_sp2;
     if (restir_part) c->halo_prev = cfg.halo_rows;
     if (e != hipSuccess) return fail(MPT_ERR_HIP, std::string("kernel launch: ") + hipGetErrorString(e));

@@ -3009,9 +3009,10 @@ static void frame_bounces(const DevScene& S, DevPaths& P, const MptFrame* d_fram
     // extended light sampling (DevPaths::x_per > 0): the EXT shading / resolve kernels, one class
     const bool ext = P.x_per > 0;
     const int classes = (hf.options.bsdf_override != MPT_BSDF_NONE || ext) ? 0 : (cfg.shade_classes != 0 ? (cfg.shade_glass ? 2 : 1) : 0);
-    // the next bounce's path rays on the trace-ahead stream (below); not with ReSTIR DI (its first
-    // bounce's G-buffer and reuse passes sit between the trace and the split)
-    const bool ahead = cfg.ahead_stream != nullptr && !restir;
+    // the next bounce's path rays on the trace-ahead stream (below); not while a ReSTIR DI first
+    // bounce runs its G-buffer and reuse passes between the trace and the split (a batched ReSTIR
+    // DI wavefront's later bounces, or its deferred first bounce after the passes, can)
+    const bool ahead = cfg.ahead_stream != nullptr && (!restir || restir_done || b_first > 0);
     for (int b = b_first; b <= b_last; b++) {
         // every per-bounce counter (lists, class queues, the traversals' work counters) in one
         // memset; the next path queue's counter is zeroed by k_split
