@@ -138,7 +138,9 @@ struct MptContext {
     // trace-ahead (MPT_TRACE_AHEAD): the next bounce's path traversal beside this bounce's NEE
     // traversals and resolve, on streamx[1]
     int trace_ahead = 1;
+    int ovl_ahead = 1;   // MPT_OVERLAP_AHEAD: trace-ahead in both halves of an overlapped batch
     hipEvent_t ev_ahead[2] = {nullptr, nullptr};
+    hipEvent_t ev_ahead2[2] = {nullptr, nullptr};   // (the second half of an overlapped batch)
     uint32_t ahead_launches = 0;   // MptStats::trace_ahead_launches
     hipGraphExec_t graph_exec = nullptr;
     std::vector<uint8_t> graph_key;
@@ -998,6 +1000,7 @@ int mpt_create(int device, void* hip_stream, MptContext** out) {
     if (const char* e = std::getenv("MPT_PIX_PARTS")) c->pix_parts = std::atoi(e);
     if (const char* e = std::getenv("MPT_RESTIR_SIDE")) c->restir_side = std::atoi(e);
     if (const char* e = std::getenv("MPT_TRACE_AHEAD")) c->trace_ahead = std::atoi(e);
+    if (const char* e = std::getenv("MPT_OVERLAP_AHEAD")) c->ovl_ahead = std::atoi(e);
     if (const char* e = std::getenv("MPT_RESTIR_MAX_BATCH"))
         c->restir_max_batch = std::max(1, std::min(RESTIR_MAX_BATCH, std::atoi(e)));
     if (const char* e = std::getenv("MPT_RESTIR_CHUNK")) c->restir_chunk = std::atoi(e);
@@ -1046,6 +1049,7 @@ int mpt_destroy(MptContext* c) {
         if (c->ev_joinx[k]) (void)hipEventDestroy(c->ev_joinx[k]);
         if (c->ev_side[k]) (void)hipEventDestroy(c->ev_side[k]);
         if (c->ev_ahead[k]) (void)hipEventDestroy(c->ev_ahead[k]);
+        if (c->ev_ahead2[k]) (void)hipEventDestroy(c->ev_ahead2[k]);
     }
     for (hipEvent_t e : {c->ev_fork, c->ev_first, c->ev_acc, c->ev_join, c->ev_chain, c->ev_half[0], c->ev_half[1],
                          c->ev_wave_join})
@@ -1481,16 +1485,19 @@ static int next_as_bound(int b, const MptFrame& f) {
 }
 // The trace-ahead stream of a single-stream wavefront (frame_bounces): streamx[1], its spill area
 // and events, on first use
-static int set_ahead(MptContext* c, LaunchCfg& cfg, const MptFrame& f) {
+// (which = 1: streamx[0] with its own events, for the first half of an overlapped batch, whose
+// second half takes streamx[1])
+static int set_ahead(MptContext* c, LaunchCfg& cfg, const MptFrame& f, int which = 0) {
     if (!c->trace_ahead || f.render_settings.nb_bounces <= 0) return MPT_OK;
-    int rr = ensure_pix_parts(c, 4);   // (streamx[1] and its spill area)
+    int rr = ensure_pix_parts(c, 4);   // (streamx[0..1] and their spill areas)
     if (rr != MPT_OK) return rr;
-    for (hipEvent_t& ev : c->ev_ahead)
-        if (!ev) HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-    cfg.ahead_stream = c->streamx[1];
-    cfg.ahead_spill = c->spillx[1].p;
-    cfg.ev_ahead_fork = c->ev_ahead[0];
-    cfg.ev_ahead_join = c->ev_ahead[1];
+    hipEvent_t* evs = which ? c->ev_ahead2 : c->ev_ahead;
+    for (int k = 0; k < 2; k++)
+        if (!evs[k]) HIPCHK(hipEventCreateWithFlags(&evs[k], hipEventDisableTiming));
+    cfg.ahead_stream = which ? c->streamx[0] : c->streamx[1];
+    cfg.ahead_spill = which ? c->spillx[0].p : c->spillx[1].p;
+    cfg.ev_ahead_fork = evs[0];
+    cfg.ev_ahead_join = evs[1];
     return MPT_OK;
 }
 
@@ -1665,12 +1672,22 @@ static int launch_batch(MptContext* c, const MptFrame* f, int batch) {
         LaunchCfg cfg0 = cfg;
         cfg0.ev_first_trace = c->ev_first;
         cfg0.ev_acc_done = c->ev_acc;
+        if (c->ovl_ahead) {   // each half with a trace-ahead stream of its own (MPT_OVERLAP_AHEAD)
+            int ra = set_ahead(c, cfg0, f[0], 1);
+            if (ra != MPT_OK) return ra;
+        }
         e = launch_frame(dev_scene(c), P0, c->d_frames + slot, f[0], cfg0, c->stream);
         LaunchCfg cfg1 = cfg0;
         cfg1.ev_first_trace = nullptr;
         cfg1.ev_acc_done = nullptr;
         cfg1.ev_acc_wait = c->ev_acc;
         cfg1.launches = 0;
+        cfg1.ahead_launches = 0;
+        cfg1.ahead_stream = nullptr;
+        if (c->ovl_ahead) {
+            int ra = set_ahead(c, cfg1, f[b0], 0);
+            if (ra != MPT_OK) return ra;
+        }
         HIPCHK(hipStreamWaitEvent(c->stream2, c->ev_first, 0));
         if (e == hipSuccess) e = launch_frame(dev_scene(c), P1, c->d_frames + slot + b0, f[b0], cfg1, c->stream2);
         HIPCHK(hipEventRecord(c->ev_join, c->stream2));
@@ -1678,6 +1695,7 @@ static int launch_batch(MptContext* c, const MptFrame* f, int batch) {
         c->overlapped_batches++;
         cfg.ev_used = cfg1.ev_used;
         cfg.launches = cfg0.launches + cfg1.launches;
+        cfg.ahead_launches = cfg0.ahead_launches + cfg1.ahead_launches;
     } else if (f->options.direct_light_sampling == MPT_LSS_RESTIR_DI && batch > 1) {
         int ra = set_ahead(c, cfg, *f);   // (the batch's later-bounce wavefront)
         if (ra != MPT_OK) return ra;

@@ -17,27 +17,28 @@ sys.path.insert(0, os.path.join(ROOT, "hiprt-path-tracer_amd"))
 from mpt import abi, scene as mscene  # noqa: E402
 
 LIB_PATH = os.path.join(HERE, "liboracle.so")
+# the same restatement with the C library's float transcendentals (sinf, powf, ...: what the
+# reference's CPU build calls) instead of the tmath.h layer it shares with the product
+LIBM_PATH = os.path.join(HERE, "liboracle_libm.so")
 
 
-def build(force=False):
+def build(force=False, variant=None):
     srcs = [os.path.join(HERE, f) for f in ("oracle.cpp", "oracle_math.h", "oracle_bsdf.h", "oracle_restir.h", "Makefile",
                                             os.path.join("..", "include", "mpt.h"),
                                             os.path.join("..", "hiprt-path-tracer_amd", "csrc", "tmath.h"))]
-    stale = os.path.exists(LIB_PATH) and any(os.path.getmtime(f) > os.path.getmtime(LIB_PATH) for f in srcs
-                                             if os.path.exists(f))
-    if force or stale or not os.path.exists(LIB_PATH):
-        subprocess.check_call(["make", "-s", "-C", HERE])
-    return LIB_PATH
+    path = LIBM_PATH if variant == "libm" else LIB_PATH
+    stale = os.path.exists(path) and any(os.path.getmtime(f) > os.path.getmtime(path) for f in srcs if os.path.exists(f))
+    if force or stale or not os.path.exists(path):
+        subprocess.check_call(["make", "-s", "-C", HERE, os.path.basename(path)])
+    return path
 
 
-_lib = None
+_libs = {}
 
 
-def lib():
-    global _lib
-    if _lib is None:
-        build()
-        L = C.CDLL(LIB_PATH)
+def lib(variant=None):
+    if variant not in _libs:
+        L = C.CDLL(build(variant=variant))
         L.oracle_create.restype = C.c_void_p
         L.oracle_create.argtypes = [C.POINTER(abi.Scene), C.POINTER(abi.Luts), C.c_void_p, C.c_int, C.c_int,
                                     C.c_void_p, C.c_void_p, C.c_float]
@@ -61,8 +62,8 @@ def lib():
         L.oracle_xorshift.argtypes = [C.c_uint32, C.c_int, C.c_void_p, C.c_void_p]
         L.oracle_tmath.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
         L.oracle_bake.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p]
-        _lib = L
-    return _lib
+        _libs[variant] = L
+    return _libs[variant]
 
 
 def _p(a):
@@ -72,7 +73,9 @@ def _p(a):
 class Oracle:
     """CPU oracle bound to one scene (+ LUTs, + optional envmap)."""
 
-    def __init__(self, scene_data, luts=None, envmap=None, keep_state=False):
+    def __init__(self, scene_data, luts=None, envmap=None, keep_state=False, variant=None):
+        """variant "libm": the restatement with the C library's float transcendentals."""
+        self.L = lib(variant)
         self.sd = scene_data
         self.luts = luts if luts is not None else mscene.load_luts()
         self._abi_scene = scene_data.to_abi()
@@ -85,27 +88,27 @@ class Oracle:
             ptrs = (_p(self._env[0]), ew, eh, _p(self._env[1]), _p(self._env[2]), es)
         else:
             ptrs = (None, 0, 0, None, None, 0.0)
-        self.h = lib().oracle_create(C.byref(self._abi_scene), C.byref(self._abi_luts), *ptrs)
+        self.h = self.L.oracle_create(C.byref(self._abi_scene), C.byref(self._abi_luts), *ptrs)
         if envmap is not None and envmap.get("cdf") is not None:
             self._cdf = np.ascontiguousarray(envmap["cdf"], np.float32)
-            lib().oracle_set_envmap_cdf(self.h, _p(self._cdf), envmap["cdf_sum"])
+            self.L.oracle_set_envmap_cdf(self.h, _p(self._cdf), envmap["cdf_sum"])
         if keep_state:
-            lib().oracle_keep_state(self.h, 1)
+            self.L.oracle_keep_state(self.h, 1)
 
     def gbuffer_history(self, frames, nthreads=0):
         """Sets the kept ReSTIR DI state to what rendering `frames` leaves for a later
         reset-to-sample-0 run: their G-buffer (oracle_gbuffer_history), without rendering them."""
         arr = (abi.Frame * len(frames))(*frames)
-        if lib().oracle_gbuffer_history(self.h, arr, len(frames), nthreads) != 0:
+        if self.L.oracle_gbuffer_history(self.h, arr, len(frames), nthreads) != 0:
             raise RuntimeError("oracle_gbuffer_history: needs keep_state and whole-frame ReSTIR DI frames without adaptive sampling")
 
     def reset_state(self, keep=True):
         """Drops the kept ReSTIR DI state (a fresh renderer); keeps state from then on if keep."""
-        lib().oracle_keep_state(self.h, 1 if keep else 0)
+        self.L.oracle_keep_state(self.h, 1 if keep else 0)
 
     def close(self):
         if self.h:
-            lib().oracle_destroy(self.h)
+            self.L.oracle_destroy(self.h)
             self.h = None
 
     def __del__(self):
@@ -122,7 +125,7 @@ class Oracle:
         u = np.empty(n, np.float32)
         v = np.empty(n, np.float32)
         lh = np.ascontiguousarray(last_hit, np.int32) if last_hit is not None else None
-        lib().oracle_trace_closest(self.h, _p(rays), _p(lh), n, _p(prim), _p(t), _p(u), _p(v))
+        self.L.oracle_trace_closest(self.h, _p(rays), _p(lh), n, _p(prim), _p(t), _p(u), _p(v))
         return prim, t, u, v
 
     def render(self, frames, nthreads=0, aov=False):
@@ -141,7 +144,7 @@ class Oracle:
         sql = np.zeros(n, np.float32)
         conv = np.full(n, -1, np.int32)
         status = np.zeros(4, np.uint32)
-        rc = lib().oracle_render(self.h, arr, len(frames), _p(out), _p(alb), _p(nrm), _p(rays), nthreads,
+        rc = self.L.oracle_render(self.h, arr, len(frames), _p(out), _p(alb), _p(nrm), _p(rays), nthreads,
                                  _p(cnt), _p(sql), _p(conv), _p(status))
         if rc != 0:
             raise RuntimeError("oracle_render failed: %d (unsupported option)" % rc)

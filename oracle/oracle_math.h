@@ -15,11 +15,13 @@
  * determinant form, normalize(v) = v / sqrt(dot(v, v)).
  *
  * Transcendentals: the reference calls float libm (sinf, cosf, powf ...).  The
- * oracle and the HIP product share hiprt-path-tracer_amd/csrc/tmath.h: double-precision
- * kernels (relative error < 1e-14) rounded once to float, i.e. the correctly rounded
- * float except within ~1e-14 of a rounding tie -- within 1 ulp of glibc's float
- * functions, and equal to (float)libm((double)x) on 2e7 random arguments per function
- * (tests/test_tmath.py).  Only IEEE double arithmetic, so both sides agree bit for bit.
+ * oracle and the HIP product share hiprt-path-tracer_amd/csrc/tmath.h: sin / cos / exp /
+ * log / atan2 / asin / acos as single-precision minimax polynomials within 1-4 ulp of the
+ * correctly rounded float, pow in double precision rounded once (tests/test_tmath.py pins
+ * both against libm) -- one sequence of IEEE operations, so both sides agree bit for bit.
+ * Built with -DORACLE_LIBM (liboracle_libm.so) the oracle calls libm's float functions
+ * instead, as the reference's CPU build does: tests/test_libm_oracle.py bounds the image
+ * difference that sharing the layer could hide by the north_star tolerance.
  * Compile with -ffp-contract=off (no fused multiply-add), like the reference's
  * x86-64 CPU build.
  */
@@ -71,6 +73,7 @@ inline float pow4(float x) { float x2 = x * x; return x2 * x2; }
 inline float pow5(float x) { float x2 = x * x; float x4 = x2 * x2; return x4 * x; }
 inline float pow6(float x) { float x2 = x * x; float x4 = x2 * x2; return x4 * x2; }
 
+#ifndef ORACLE_LIBM
 // parity transcendentals (see header comment): the product's tmath.h, verbatim
 inline float psin(float x) { return tmath::sinf_(x); }
 inline float pcos(float x) { return tmath::cosf_(x); }
@@ -80,6 +83,17 @@ inline float ppow(float x, float y) { return tmath::powf_(x, y); }
 inline float patan2(float y, float x) { return tmath::atan2f_(y, x); }
 inline float pasin(float x) { return tmath::asinf_(x); }
 inline float pacos(float x) { return tmath::acosf_(x); }
+#else
+// the reference CPU build's float libm calls (Math.h:141-229: sinf, cosf, expf, logf, powf, ...)
+inline float psin(float x) { return std::sin(x); }
+inline float pcos(float x) { return std::cos(x); }
+inline float pexp(float x) { return std::exp(x); }
+inline float plog(float x) { return std::log(x); }
+inline float ppow(float x, float y) { return std::pow(x, y); }
+inline float patan2(float y, float x) { return std::atan2(y, x); }
+inline float pasin(float x) { return std::asin(x); }
+inline float pacos(float x) { return std::acos(x); }
+#endif
 inline float psqrt(float x) { return std::sqrt(x); }
 
 constexpr float PI = 3.14159265358979323846f;      // Math.h:144
