@@ -713,6 +713,11 @@ def run_workload(a, world, rank, local, dist, coll_dev, quiet=False):
             # traversals, so the traversal stages' launch times overlap
             r["shared_gpu"] = (f"{st.trace_ahead_launches} path traversal(s) launched ahead: launch times shared with "
                                "the previous bounce's NEE traversals")
+            if getattr(st, "pipelined_batches", 0):
+                # MPT_PIPELINE: a bounce's NEE traversals and resolve also ran beside the next
+                # bounce's split and shading
+                r["shared_gpu"] += (f"; {st.pipelined_batches} pipelined batch(es): NEE traversals beside the next "
+                                    "bounce's split and shading")
         elif getattr(st, "restir_overlapped_batches", 0):
             # MPT_RESTIR_OVERLAP: a ReSTIR DI batch's later bounces ran on the second stream beside
             # the next batch's per-sample chain

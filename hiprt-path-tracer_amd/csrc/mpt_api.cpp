@@ -142,6 +142,7 @@ struct MptContext {
     hipEvent_t ev_ahead[2] = {nullptr, nullptr};
     hipEvent_t ev_ahead2[2] = {nullptr, nullptr};   // (the second half of an overlapped batch)
     uint32_t ahead_launches = 0;   // MptStats::trace_ahead_launches
+    uint32_t pipelined_batches = 0;   // MptStats::pipelined_batches
     hipGraphExec_t graph_exec = nullptr;
     std::vector<uint8_t> graph_key;
     uint32_t graph_launches = 0;
@@ -214,6 +215,13 @@ struct MptContext {
     DBuf<uint4> vsA, vsB;
     DBuf<int32_t> q0, q1, qh, qm, qf, nq_light, counters, nq_tgt, fetch_raw;
     DBuf<float4> nthr, na, nb, ndir, nris, ne1, ne2;   // NEE record planes (mpt_internal.h)
+    // bounce pipeline (LaunchCfg::pipe_alt): the odd bounces' NEE planes, staged queries and their
+    // lists, shaded lists, and both parities' col additions (MPT_PIPELINE)
+    DBuf<float4> nthr2, na2, nb2, ndir2, nris2, ne12, ne22, nq_o2, nq_d2, ce, ce2;
+    DBuf<int32_t> nq_tgt2, qh2, qf2;
+    int pipeline = 1;
+    size_t pipe_n = 0;
+    hipEvent_t ev_nee[2] = {nullptr, nullptr};
     DBuf<float> fb_color, fb_albedo, fb_normal;
     DBuf<int32_t> as_count, as_conv;
     DBuf<float> as_sqlum;
@@ -445,12 +453,18 @@ struct Allocs {
 // qmask, active (3).  Textured scenes add a resolved material per slot.
 constexpr size_t OVERLAP_AUTO_PATHS = (size_t)24 << 20;   // MPT_OVERLAP=-1: overlapped halves up to this many paths
 constexpr size_t PATH_BYTES = 9 * 16 + 32 + 7 * 16 + 128 + 16 + 4 + 24 + 4 + 8 + 3;
+// + the bounce pipeline's alternate set per slot (set_pipe): 7 NEE planes, 4 staged query rays,
+// 2 col additions (16 B each ... 64 B), 4 query list entries, 2 shaded-list entries
+constexpr size_t PIPE_BYTES = 7 * 16 + 2 * 64 + 2 * 16 + 16 + 8;
 
 void release_batch(MptContext* c) {
     release_all(c->ray_o, c->ray_d, c->hit, c->hit_inside, c->hit_cls, c->rng, c->seeds, c->thr, c->col, c->vsA, c->vsB, c->alb, c->nrmv,
                 c->q0, c->q1, c->qh, c->qm, c->qf, c->nq_light, c->nthr, c->na, c->nb, c->ndir, c->nris, c->ne1, c->ne2, c->nq_o,
                 c->nq_d, c->nq_tgt, c->occ, c->nhit, c->s_gn, c->qmask, c->active,
                 c->mat_slot);
+    release_all(c->nthr2, c->na2, c->nb2, c->ndir2, c->nris2, c->ne12, c->ne22, c->nq_o2, c->nq_d2, c->ce, c->ce2, c->nq_tgt2,
+                c->qh2, c->qf2);
+    c->pipe_n = 0;
     c->batch_cap = 0;
 }
 
@@ -1000,6 +1014,7 @@ int mpt_create(int device, void* hip_stream, MptContext** out) {
     if (const char* e = std::getenv("MPT_PIX_PARTS")) c->pix_parts = std::atoi(e);
     if (const char* e = std::getenv("MPT_RESTIR_SIDE")) c->restir_side = std::atoi(e);
     if (const char* e = std::getenv("MPT_TRACE_AHEAD")) c->trace_ahead = std::atoi(e);
+    if (const char* e = std::getenv("MPT_PIPELINE")) c->pipeline = std::atoi(e);
     if (const char* e = std::getenv("MPT_OVERLAP_AHEAD")) c->ovl_ahead = std::atoi(e);
     if (const char* e = std::getenv("MPT_RESTIR_MAX_BATCH"))
         c->restir_max_batch = std::max(1, std::min(RESTIR_MAX_BATCH, std::atoi(e)));
@@ -1050,6 +1065,7 @@ int mpt_destroy(MptContext* c) {
         if (c->ev_side[k]) (void)hipEventDestroy(c->ev_side[k]);
         if (c->ev_ahead[k]) (void)hipEventDestroy(c->ev_ahead[k]);
         if (c->ev_ahead2[k]) (void)hipEventDestroy(c->ev_ahead2[k]);
+        if (c->ev_nee[k]) (void)hipEventDestroy(c->ev_nee[k]);
     }
     for (hipEvent_t e : {c->ev_fork, c->ev_first, c->ev_acc, c->ev_join, c->ev_chain, c->ev_half[0], c->ev_half[1],
                          c->ev_wave_join})
@@ -1305,7 +1321,7 @@ static int default_batch(MptContext* c, const MptFrame& f) {
     // per pixel and sample, see prepare_batch)
     const bool keep = f.options.direct_light_sampling == MPT_LSS_RESTIR_DI &&
                       f.world_settings.ambient_light_type == MPT_AMBIENT_ENVMAP;
-    const size_t per = PATH_BYTES + ((c->any_tex || f.bsdf_flags.white_furnace_mode) ? sizeof(MptMaterial) : 0) +
+    const size_t per = PATH_BYTES + (c->pipeline ? PIPE_BYTES : 0) + ((c->any_tex || f.bsdf_flags.white_furnace_mode) ? sizeof(MptMaterial) : 0) +
                        EXT_ENTRY_BYTES * (size_t)ext_layout(f, nullptr) + (keep ? 3 * sizeof(float4) : 0);
     size_t fr = 0, tot = 0;
     if (hipMemGetInfo(&fr, &tot) != hipSuccess) { (void)hipGetLastError(); fr = 0; }
@@ -1498,6 +1514,48 @@ static int set_ahead(MptContext* c, LaunchCfg& cfg, const MptFrame& f, int which
     cfg.ahead_spill = which ? c->spillx[0].p : c->spillx[1].p;
     cfg.ev_ahead_fork = evs[0];
     cfg.ev_ahead_join = evs[1];
+    return MPT_OK;
+}
+
+// The bounce pipeline of a single-stream wavefront (LaunchCfg::pipe_alt, frame_bounces): the
+// alternate plane set for the path slots the context holds (allocated on first use; a failure to
+// allocate leaves the wavefront in line), its view `alt` of P, the NEE stream (streamx[0]), its
+// spill area and events.  P.ce is set: the shading hands its col additions to k_resolve.
+static int set_pipe(MptContext* c, LaunchCfg& cfg, const MptFrame& f, DevPaths& P, DevPaths& alt) {
+    if (!c->pipeline || f.options.direct_light_sampling == MPT_LSS_RESTIR_DI || c->x_per != 0 || c->shade_split ||
+        f.render_settings.nb_bounces <= 0)
+        return MPT_OK;
+    const size_t N = (size_t)std::max(c->n_slots, 1) * (size_t)c->batch_cap;
+    if (c->pipe_n != N) {
+        HIPCHK(drain(c));
+        Allocs A;
+        A(c->nthr2, N); A(c->na2, N); A(c->nb2, N); A(c->ndir2, N); A(c->nris2, N); A(c->ne12, N); A(c->ne22, N);
+        A(c->nq_o2, 4 * N); A(c->nq_d2, 4 * N); A(c->ce, N); A(c->ce2, N);
+        A(c->nq_tgt2, 4 * N); A(c->qh2, N); A(c->qf2, N);
+        if (A.e != hipSuccess) {   // no room: this wavefront (and the next ones) in line
+            (void)hipGetLastError();
+            release_all(c->nthr2, c->na2, c->nb2, c->ndir2, c->nris2, c->ne12, c->ne22, c->nq_o2, c->nq_d2, c->ce, c->ce2,
+                        c->nq_tgt2, c->qh2, c->qf2);
+            c->pipe_n = 0;
+            return MPT_OK;
+        }
+        c->pipe_n = N;
+    }
+    int rr = ensure_pix_parts(c, 4);   // (streamx[0] and its spill area)
+    if (rr != MPT_OK) return rr;
+    for (hipEvent_t& ev : c->ev_nee)
+        if (!ev) HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    P.ce = c->ce.p;
+    alt = P;
+    alt.nthr = c->nthr2.p; alt.na = c->na2.p; alt.nb = c->nb2.p; alt.ndir = c->ndir2.p; alt.nris = c->nris2.p;
+    alt.ne1 = c->ne12.p; alt.ne2 = c->ne22.p; alt.nq_o = c->nq_o2.p; alt.nq_d = c->nq_d2.p; alt.nq_tgt = c->nq_tgt2.p;
+    alt.qh = c->qh2.p; alt.qf = c->qf2.p; alt.ce = c->ce2.p;
+    alt.counters = P.counters + CTR_COUNT;   // (the queue counters are always taken from P)
+    cfg.pipe_alt = &alt;
+    cfg.nee_stream = c->streamx[0];
+    cfg.nee_spill = c->spillx[0].p;
+    cfg.ev_nee_fork = c->ev_nee[0];
+    cfg.ev_nee_join = c->ev_nee[1];
     return MPT_OK;
 }
 
@@ -1729,6 +1787,10 @@ static int launch_batch(MptContext* c, const MptFrame* f, int batch) {
     } else {
         int rr = set_ahead(c, cfg, *f);
         if (rr != MPT_OK) return rr;
+        DevPaths alt{};
+        rr = set_pipe(c, cfg, *f, P, alt);
+        if (rr != MPT_OK) return rr;
+        if (cfg.pipe_alt) c->pipelined_batches++;
         e = launch_frame(dev_scene(c), P, c->d_frames + slot, *f, cfg, c->stream);
     }
     c->ahead_launches += cfg.ahead_launches;
@@ -2332,6 +2394,7 @@ int mpt_enable_stats(MptContext* c, int enable, int instrumented) {
     c->halo_exchanges = c->halo_agreements = c->halo_bytes_sent = c->halo_bytes_recv = 0;
     c->restir_overlapped_batches = 0;
     c->ahead_launches = 0;
+    c->pipelined_batches = 0;
     for (int m = 0; m < KT_COUNT; m++) { c->stage_ms[m] = 0.0; c->stage_launches[m] = 0; }
     HIPCHK(hipMemsetAsync(c->stats.p, 0, N_STATS * sizeof(uint64_t), c->stream));
     HIPCHK(hipMemsetAsync(c->ray_counts.p, 0, N_RAY_COUNTS * sizeof(uint64_t), c->stream));
@@ -2398,6 +2461,7 @@ int mpt_get_stats(MptContext* c, MptStats* out) {
     out->halo_bytes_received = c->halo_bytes_recv;
     out->restir_overlapped_batches = c->restir_overlapped_batches;
     out->trace_ahead_launches = c->ahead_launches;
+    out->pipelined_batches = c->pipelined_batches;
     return MPT_OK;
 }
 

@@ -174,6 +174,8 @@ struct DevPaths {
     float4* nhit;             // closest NEE result per slot; between split shading stages: shading normal + material
     float4* s_gn;             // between split shading stages: geometric normal (k_shade's ST)
     MptMaterial* mat_slot;    // per-slot resolved material (textured materials, white furnace)
+    float4* ce;               // bounce pipeline (frame_bounces): the shading's addition to col, added by k_resolve
+                              // (NULL: k_shade adds it to col itself)
     float* fb_color;          // 3 per slot (sum)
     float* fb_albedo;
     float* fb_normal;
@@ -353,6 +355,14 @@ struct LaunchCfg {
     uint32_t* ahead_spill;
     hipEvent_t ev_ahead_fork, ev_ahead_join;
     uint32_t ahead_launches;   // out: path traversals launched ahead
+    // bounce pipeline (frame_bounces): bounce b's NEE traversals and resolve on nee_stream beside
+    // bounce b + 1's split and shading, over the alternate plane set pipe_alt (odd bounces: NEE
+    // planes, staged queries and lists, shaded lists, per-bounce counters, col additions); NULL
+    // nee_stream: in line
+    hipStream_t nee_stream;
+    uint32_t* nee_spill;
+    hipEvent_t ev_nee_fork, ev_nee_join;
+    const DevPaths* pipe_alt;
     // chunked ReSTIR DI initial candidates (launch_frames_restir): up to ci_chunk samples per
     // chunk; ci_planes' G-buffer / rs_init / rs_plights pointers are the chunk's planes (NULL
     // ci_planes or ci_chunk < 2: one sample's chain at a time)

@@ -1586,8 +1586,13 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(
         const float4 thv = ld_s(&P.thr[slot]);
         Col thr = col(thv.x, thv.y, thv.z);
         const Col thr_vertex = thr;        // the NEE terms' throughput (k_resolve)
-        float4 cv = ld_s(&P.col[slot]);
-        Col rcol = col(cv.x, cv.y, cv.z);
+        // (bounce pipeline, P.ce: this vertex's addition to col, handed to k_resolve, which adds it
+        // after the previous bounce's resolve -- the sum keeps its order)
+        Col rcol = col(0.0f);
+        if (!P.ce) {
+            const float4 cv = ld_s(&P.col[slot]);
+            rcol = col(cv.x, cv.y, cv.z);
+        }
         v3 ip = mk3(0, 0, 0), gn = mk3(0, 0, 0), sn = mk3(0, 0, 0);
         // The material is read through a pointer (L1/L2-resident) instead of being held in
         // registers: untextured materials use the per-material resolved copy, textured ones
@@ -2034,7 +2039,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(
         if (FIRST) {
             st_s(&P.nthr[slot], make_float4(thr_vertex.r, thr_vertex.g, thr_vertex.b, __uint_as_float(fl)));
             st_s(&P.qmask[slot], (uint8_t)qb);
-            st_s(&P.col[slot], make_float4(rcol.r, rcol.g, rcol.b, 0.0f));
+            st_s(P.ce ? &P.ce[slot] : &P.col[slot], make_float4(rcol.r, rcol.g, rcol.b, 0.0f));
         } else {
             if (fl) {
                 const float4 t4 = ld_s(&P.nthr[slot]);
@@ -2136,8 +2141,11 @@ __global__ __launch_bounds__(CP_NT) void k_split(DevScene S, DevPaths P, const i
                                                  int classes, int32_t* zero_next) {
     __shared__ int tmp[CP_NT / 64 + 1];
     __shared__ int base[4];
-    if (blockIdx.x == 0 && threadIdx.x == 0) *zero_next = 0;   // the next path queue (filled by k_compact)
     const int count = *count_q;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        *zero_next = 0;   // the next path queue (filled by k_compact)
+        atomicAdd((unsigned long long*)P.ray_counts, (unsigned long long)count);   // the bounce's path rays
+    }
     const int b0 = blockIdx.x * CP_NT * CP_ITEMS;
     if (b0 >= count) return;
     int slots[CP_ITEMS];
@@ -2393,7 +2401,17 @@ DEV void resolve_entry(const DevScene& S, const DevPaths& P, const MptFrame& F, 
     // the NEE record planes the vertex wrote (flags in nthr.w), each read whole
     const float4 t4 = ld_s(&P.nthr[slot]);
     const uint32_t fl = __float_as_uint(t4.w);
-    if (!(fl & NF_SHADED) || (fl & NF_NOADD)) return;
+    // the bounce pipeline's col addition of the shading (P.ce), made here in the shading's place
+    float4 cv = ld_s(&P.col[slot]);
+    if (P.ce) {
+        const float4 e = ld_s(&P.ce[slot]);
+        const Col s = col(cv.x, cv.y, cv.z) + col(e.x, e.y, e.z);
+        cv = make_float4(s.r, s.g, s.b, 0.0f);
+    }
+    if (!(fl & NF_SHADED) || (fl & NF_NOADD)) {
+        if (P.ce) st_s(&P.col[slot], cv);
+        return;
+    }
     const int lss = F.options.direct_light_sampling;
     const int lssb = bounce_lss(F, bounce);
     Col ld = col(0.0f), ed = col(0.0f);
@@ -2479,7 +2497,6 @@ DEV void resolve_entry(const DevScene& S, const DevPaths& P, const MptFrame& F, 
     ld = clamp_contrib(ld, rs.direct_contribution_clamp, bounce == 0);
     ed = clamp_contrib(ed, rs.envmap_contribution_clamp, bounce == 0);
     Col ind = (ld + ed) * col(t4.x, t4.y, t4.z);
-    float4 cv = ld_s(&P.col[slot]);
     Col rc = col(cv.x, cv.y, cv.z) + clamp_contrib(ind, rs.indirect_contribution_clamp, bounce > 0);
     st_s(&P.col[slot], make_float4(rc.r, rc.g, rc.b, 0.0f));
 #ifdef MPT_DEBUG_SLOT
@@ -2495,8 +2512,10 @@ __global__ __launch_bounds__(TB) void k_resolve(DevScene S, DevPaths P, const Mp
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         // always-on ray accounting: path rays + NEE any-hit + NEE closest of this bounce, path hits
         // (atomic: the two halves of an overlapped batch resolve concurrently)
+        // (the path rays, *count_paths, are counted by k_split: a pipelined bounce's split zeroes
+        // the previous bounce's queue counter while this resolve may still run)
         unsigned long long* rc = (unsigned long long*)P.ray_counts;
-        atomicAdd(rc + 0, (unsigned long long)*count_paths);
+        (void)count_paths;
         atomicAdd(rc + 1, (unsigned long long)P.counters[CTR_ANY] + (EXT ? (unsigned long long)P.counters[CTR_XANY] : 0ull));
         atomicAdd(rc + 2, (unsigned long long)P.counters[CTR_CL] + (EXT ? (unsigned long long)P.counters[CTR_XCL] : 0ull));
         atomicAdd(rc + 3, (unsigned long long)(shaded_count(P) - P.counters[CTR_DEFER]));
@@ -3013,7 +3032,23 @@ static void frame_bounces(const DevScene& S, DevPaths& P, const MptFrame* d_fram
     // bounce runs its G-buffer and reuse passes between the trace and the split (a batched ReSTIR
     // DI wavefront's later bounces, or its deferred first bounce after the passes, can)
     const bool ahead = cfg.ahead_stream != nullptr && (!restir || restir_done || b_first > 0);
+    // Bounce pipeline (cfg.nee_stream): bounce b's NEE traversals and resolve run on the NEE stream
+    // beside bounce b + 1's split and shading.  Odd bounces use the alternate plane set (NEE
+    // records, staged queries and their lists, shaded lists, per-bounce counters, the shading's col
+    // additions), so the two bounces in flight touch disjoint buffers; the path queues and their
+    // counters (c_cur / c_next) are the base set's.  Bounce b + 1's k_miss (which adds to col)
+    // waits for bounce b's resolve.  Not under ReSTIR DI, extended light sampling or split shading.
+    const bool pipe = cfg.nee_stream != nullptr && cfg.pipe_alt != nullptr && !restir && !ext && !cfg.shade_split;
+    DevPaths PB = P;   // the base set (even bounces)
+    DevPaths* const Pout = &P;
+    bool nee_pending = false;
     for (int b = b_first; b <= b_last; b++) {
+        // this bounce's plane set; queue counters always from the base set
+        DevPaths Pv = (pipe && (b & 1)) ? *cfg.pipe_alt : PB;
+        if (pipe) Pv.ce = (b & 1) ? cfg.pipe_alt->ce : PB.ce;
+        DevPaths& P = Pv;
+        int32_t* const cnt_cur = &PB.counters[c_cur];
+        int32_t* const cnt_next = &PB.counters[c_next];
         // every per-bounce counter (lists, class queues, the traversals' work counters) in one
         // memset; the next path queue's counter is zeroed by k_split
         hipMemsetAsync(&P.counters[CTR_BOUNCE_FIRST], 0, (CTR_COUNT - CTR_BOUNCE_FIRST) * sizeof(int32_t), st);
@@ -3021,18 +3056,20 @@ static void frame_bounces(const DevScene& S, DevPaths& P, const MptFrame* d_fram
         const int alpha = hf.render_settings.do_alpha_testing ? 1 : 0;
         if (!(first_traced && b == b_first) && !(ahead && b > b_first)) {
             TraceArgs ta{};
-            ta.S = S; ta.P = P; ta.queue = q_cur; ta.count_ptr = &P.counters[c_cur]; ta.fetch = &P.counters[CTR_F_PATH];
+            ta.S = S; ta.P = P; ta.queue = q_cur; ta.count_ptr = cnt_cur; ta.fetch = &P.counters[CTR_F_PATH];
             ta.F = d_frame; ta.bounce = b; ta.alpha = alpha;
             timed_trace<TM_PATH>(ta, cfg, st);
         }
         if (b == 0 && cfg.ev_first_trace) hipEventRecord(cfg.ev_first_trace, st);
         // (the ReSTIR DI passes use only CTR_REPROJ and their own CTR_RQ group of the per-bounce counters)
-        if (restir && b == 0 && !restir_done) restir_first_bounce(S, P, d_frame, hf, cfg, st);
+        if (restir && b == 0 && !restir_done) {
+            restir_first_bounce(S, P, d_frame, hf, cfg, st);
+            PB.rs_out = Pout->rs_out = P.rs_out;   // (the passes' output buffer, as the caller sees it)
+        }
         const dim3 cp_grid((n + CP_NT * CP_ITEMS - 1) / (CP_NT * CP_ITEMS));
         {
             TimedScope ts(cfg, st, KT_SPLIT);
-            hipLaunchKernelGGL(k_split, cp_grid, dim3(CP_NT), 0, st, S, P, q_cur, &P.counters[c_cur], classes,
-                               &P.counters[c_next]);
+            hipLaunchKernelGGL(k_split, cp_grid, dim3(CP_NT), 0, st, S, P, q_cur, cnt_cur, classes, cnt_next);
         }
         ShadeArgs sa{};
         sa.S = S; sa.P = P; sa.F = d_frame; sa.bounce = b; sa.last_bounce = nb;
@@ -3071,6 +3108,8 @@ static void frame_bounces(const DevScene& S, DevPaths& P, const MptFrame* d_fram
                 part_shade_glass(dim3(blocks_for(n)), st, sg2);
             }
         }
+        // (the previous bounce's resolve adds to col first)
+        if (nee_pending) { hipStreamWaitEvent(st, cfg.ev_nee_join, 0); nee_pending = false; }
         {
             TimedScope ts(cfg, st, KT_MISS);
             hipLaunchKernelGGL(k_miss, dim3(std::min(blocks_for(n), 8 * cfg.grid_persistent)), dim3(TB), 0, st, S, P, d_frame, b);
@@ -3079,8 +3118,10 @@ static void frame_bounces(const DevScene& S, DevPaths& P, const MptFrame* d_fram
             TimedScope ts(cfg, st, KT_COMPACT);
             // the shaded list (qh ++ qf) holds up to 2n entries: deferred vertices appear in both
             const dim3 cp_grid2((2 * n + CP_NT * CP_ITEMS - 1) / (CP_NT * CP_ITEMS));
-            hipLaunchKernelGGL(k_compact, classes ? cp_grid2 : cp_grid, dim3(CP_NT), 0, st, P, q_next, &P.counters[c_next],
-                               ahead && b < b_last ? &P.counters[CTR_F_PATH] : nullptr);
+            // (the next bounce's plane set takes the next bounce's path-traversal work counter)
+            int32_t* const next_fetch = (pipe && !(b & 1)) ? &cfg.pipe_alt->counters[CTR_F_PATH] : &PB.counters[CTR_F_PATH];
+            hipLaunchKernelGGL(k_compact, classes ? cp_grid2 : cp_grid, dim3(CP_NT), 0, st, P, q_next, cnt_next,
+                               ahead && b < b_last ? next_fetch : nullptr);
         }
         // Trace-ahead: the next bounce's path rays depend only on the continuation list k_compact
         // just wrote, not on this bounce's NEE queries or k_resolve (which read the NEE planes,
@@ -3092,16 +3133,24 @@ static void frame_bounces(const DevScene& S, DevPaths& P, const MptFrame* d_fram
         if (fork) {
             hipEventRecord(cfg.ev_ahead_fork, st);
             hipStreamWaitEvent(cfg.ahead_stream, cfg.ev_ahead_fork, 0);
-            DevPaths PA = P;
+            DevPaths PA = (pipe && !(b & 1)) ? *cfg.pipe_alt : PB;   // the next bounce's plane set
             PA.stack_spill = cfg.ahead_spill;
             TraceArgs ta{};
-            ta.S = S; ta.P = PA; ta.queue = q_next; ta.count_ptr = &P.counters[c_next]; ta.fetch = &P.counters[CTR_F_PATH];
+            ta.S = S; ta.P = PA; ta.queue = q_next; ta.count_ptr = cnt_next; ta.fetch = &PA.counters[CTR_F_PATH];
             ta.F = d_frame; ta.bounce = b + 1; ta.alpha = hf.render_settings.do_alpha_testing ? 1 : 0;
             timed_trace<TM_PATH>(ta, cfg, cfg.ahead_stream);
             hipEventRecord(cfg.ev_ahead_join, cfg.ahead_stream);
             cfg.ahead_launches++;
         }
-        // NEE queries (each traversal with its own work counter, zeroed at the top of the bounce)
+        // NEE queries (each traversal with its own work counter, zeroed at the top of the bounce);
+        // pipelined: on the NEE stream, with its own spill area
+        const hipStream_t main_st = st;
+        if (pipe) {
+            hipEventRecord(cfg.ev_nee_fork, main_st);
+            hipStreamWaitEvent(cfg.nee_stream, cfg.ev_nee_fork, 0);
+            st = cfg.nee_stream;
+            P.stack_spill = cfg.nee_spill;
+        }
         TraceArgs tn{};
         tn.S = S; tn.P = P; tn.count_ptr = &P.counters[CTR_ANY]; tn.fetch = &P.counters[CTR_F_ANY];
         tn.F = d_frame; tn.bounce = b; tn.alpha = alpha;
@@ -3141,14 +3190,20 @@ static void frame_bounces(const DevScene& S, DevPaths& P, const MptFrame* d_fram
             TimedScope ts(cfg, st, KT_RESOLVE);
             // grid-stride over the shaded list (up to 2n entries with classes: deferred vertices appear twice)
             const dim3 rg(std::min(blocks_for(classes ? 2 * n : n), 8 * cfg.grid_persistent));
-            if (ext) hipLaunchKernelGGL(k_resolve<true>, rg, dim3(TB), 0, st, S, P, d_frame, b, &P.counters[c_cur]);
-            else hipLaunchKernelGGL(k_resolve<false>, rg, dim3(TB), 0, st, S, P, d_frame, b, &P.counters[c_cur]);
+            if (ext) hipLaunchKernelGGL(k_resolve<true>, rg, dim3(TB), 0, st, S, P, d_frame, b, cnt_cur);
+            else hipLaunchKernelGGL(k_resolve<false>, rg, dim3(TB), 0, st, S, P, d_frame, b, cnt_cur);
+        }
+        if (pipe) {
+            hipEventRecord(cfg.ev_nee_join, st);
+            nee_pending = true;
+            st = main_st;
         }
         if (fork) hipStreamWaitEvent(st, cfg.ev_ahead_join, 0);
         // swap queues
         int32_t* tq = q_cur; q_cur = q_next; q_next = tq;
         int tc = c_cur; c_cur = c_next; c_next = tc;
     }
+    if (nee_pending) hipStreamWaitEvent(st, cfg.ev_nee_join, 0);   // the last bounce's resolve
 }
 
 hipError_t launch_frame(const DevScene& S, const DevPaths& P0, const MptFrame* d_frame, const MptFrame& hf, LaunchCfg& cfg,

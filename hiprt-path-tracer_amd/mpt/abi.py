@@ -371,7 +371,7 @@ class Stats(C.Structure):
                 ("graph_captures", C.c_uint32), ("graph_replays", C.c_uint32), ("overlapped_batches", C.c_uint32),
                 ("halo_exchanges", C.c_uint64), ("halo_agreements", C.c_uint64), ("halo_bytes_sent", C.c_uint64),
                 ("halo_bytes_received", C.c_uint64), ("restir_overlapped_batches", C.c_uint32),
-                ("trace_ahead_launches", C.c_uint32)]
+                ("trace_ahead_launches", C.c_uint32), ("pipelined_batches", C.c_uint32)]
 
 
 OK, ERR_INVALID_ARGUMENT, ERR_HIP, ERR_NO_SCENE, ERR_UNSUPPORTED, ERR_OUT_OF_MEMORY = 0, -1, -2, -3, -4, -5

@@ -461,6 +461,9 @@ typedef struct MptStats {
     /* path traversals launched ahead, beside the previous bounce's NEE traversals and resolve
      * (MPT_TRACE_AHEAD): their times and those of the NEE traversals overlap */
     uint32_t trace_ahead_launches;
+    /* wavefronts whose bounces ran pipelined (MPT_PIPELINE: a bounce's NEE traversals and resolve
+     * beside the next bounce's split and shading): their kernels' times overlap */
+    uint32_t pipelined_batches;
 } MptStats;
 
 #define MPT_FB_COLOR 0        /* 'pixels': running SUM of samples (RenderData.h:34-36) */
