@@ -4,7 +4,9 @@ Reads the run's kernel_trace.csv, takes the dispatches of the last `window_ms` o
 (the bench's timed region sits at its end), and prints the busy fraction of the GPU over that
 window (union of kernel intervals), the number of dispatches, their mean duration and the
 mean gap between consecutive dispatches -- the cost of a launch chain of small kernels.
-usage: python tools/trace_gaps.py <rocprofv3 output dir> [window_ms]
+With a third argument, also the window's dispatches per kernel (count, total and mean
+duration; the busy time they overlap with other kernels is counted in each).
+usage: python tools/trace_gaps.py <rocprofv3 output dir> [window_ms] [per-kernel: 1]
 """
 import csv
 import glob
@@ -40,6 +42,14 @@ def main():
           f"({busy / max(1, span - top):.3f} without the largest gap, {top / 1e3:.1f} us), "
           f"mean kernel {sum(e - s for s, e, _ in iv) / len(iv) / 1e3:.1f} us, "
           f"mean gap {sum(rest) / max(1, len(rest)) / 1e3:.1f} us without it, gaps > 20 us: {sum(1 for g in rest if g > 20000)}")
+    if len(sys.argv) > 3:
+        per = {}
+        for s, e, n in iv:
+            k = n.split("(")[0][:90]
+            c, t = per.get(k, (0, 0))
+            per[k] = (c + 1, t + e - s)
+        for k, (c, t) in sorted(per.items(), key=lambda x: -x[1][1]):
+            print(f"{c:6d} {t / 1e3:10.1f} us {t / c / 1e3:8.2f} us/call  {k}")
 
 
 if __name__ == "__main__":
