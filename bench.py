@@ -79,6 +79,8 @@ def parse():
     ap.add_argument("--parity-seconds", type=float, default=90.0, help="oracle budget of the parity leg")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true", help="skip the RMSE-vs-oracle band check")
+    ap.add_argument("--no-solo", action="store_true",
+                    help="skip the pipelined shading kernel's solo timing after the timed region")
     ap.add_argument("--batch", type=int, default=0,
                     help="samples per pixel traced as one wavefront (mpt_render_frames); 0 = auto: "
                          "TARGET_PATHS / the rank's pixels, so a rank's launches keep the same size")
@@ -567,6 +569,24 @@ def run_workload(a, world, rank, local, dist, coll_dev, quiet=False):
                   "vs_batched": round((dt1 / n1) / (elapsed / K), 3), "batched_samples_per_launch": batch,
                   "graph_replays": int(st1.graph_replays), "graph_captures": int(st1.graph_captures)}
 
+    # the shading kernel alone: a pipelined wavefront (MPT_PIPELINE) runs a bounce's NEE
+    # traversals beside the next bounce's shading, so the timed region's shading launches share
+    # the GPU; one more batch of the same frames with the bounces in line (untimed for `value`,
+    # same images) gives the kernel's own launch time (the roofline's `solo`)
+    solo = None
+    if st.pipelined_batches and not a.no_solo:
+        r.set_pipeline(0)
+        fr_s = frames_for(cam, W, H, opt, band, batch, bounces=a.bounces, world=wset, alpha=alpha)
+        r.synchronize_kernel()
+        r.enable_stats(timing=True, instrumented=False)
+        r.render_samples(fr_s, max_batch=batch)
+        r.synchronize_kernel()
+        sts = r.stats()
+        r.set_pipeline(1)
+        hits_s = (sts.path_hits or sts.stage_rays[0]) - sts.shade_generic_vertices
+        solo = {"shade_avg_launch_ms": sts.shade_ms / max(1, sts.shade_launches),
+                "shade_units_per_launch": hits_s / max(1, sts.shade_launches), "steps": batch}
+
     # rooflines (SURVEY.md §8d algorithmic bytes): every traversal stage and the shade
     # kernel; "roofline" is the one with the largest summed time in the timed region
     names = ["k_trace<TM_PATH> (camera/continuation rays, closest hit)", "k_trace<TM_NEE_ANY> (NEE shadow rays, any hit)",
@@ -599,7 +619,7 @@ def run_workload(a, world, rank, local, dist, coll_dev, quiet=False):
                   "symbol": "void mpt::k_shade<0, true",   # k_shade<OVR, plain, RIS visibility>
                   "total_ms": st.shade_ms, "avg_launch_ms": s_avg, "bytes_per_unit": b_vtx, "unit_of_work": "path vertex (hit)",
                   "units_per_launch": hits / sl, "launches": st.shade_launches,
-                  "achieved": hits * b_vtx / sl / (s_avg * 1e-3) / 1e9 if s_avg > 0 else 0.0})
+                  "achieved": hits * b_vtx / sl / (s_avg * 1e-3) / 1e9 if s_avg > 0 else 0.0, "solo": solo})
     # the generic class (every other material, incl. the vertices the plain kernel deferred);
     # launched once per bounce beside the plain kernel, same bytes per vertex
     if st.shade_generic_vertices and st.shade_generic_ms > 0:
@@ -703,11 +723,22 @@ def run_workload(a, world, rank, local, dist, coll_dev, quiet=False):
         if "nodes_per_ray" in x:
             r.update(nodes_per_ray=round(x["nodes_per_ray"], 3), tris_per_ray=round(x["tris_per_ray"], 3),
                      node_simd_util=round(x["node_simd_util"], 3), tri_simd_util=round(x["tri_simd_util"], 3))
+        if x.get("solo") and x["solo"]["shade_avg_launch_ms"] > 0:
+            so = x["solo"]
+            ach = so["shade_units_per_launch"] * x["bytes_per_unit"] / (so["shade_avg_launch_ms"] * 1e-3) / 1e9
+            r["solo"] = {"what": "the same kernel with the bounces in line (mpt_set_pipeline 0), one more batch of the "
+                                 "frames after the timed region",
+                         "avg_launch_ms": round(so["shade_avg_launch_ms"], 5), "units_per_launch": round(so["shade_units_per_launch"], 1),
+                         "achieved": round(ach, 2), "frac": round(ach / HBM_PEAK_GBS, 5)}
         if getattr(st, "overlapped_batches", 0):
             # MPT_OVERLAP (the library's default for wavefronts of <= 24 M paths): each batch ran as
             # two halves on two streams, so this kernel's launches shared the GPU with the other
             # half's kernels -- its launch time, and with it `achieved`, is not the kernel's alone
             r["shared_gpu"] = f"{st.overlapped_batches} overlapped batch(es): launch times shared with the other half"
+        elif getattr(st, "pipelined_batches", 0) and x["unit_of_work"] != "ray":
+            # MPT_PIPELINE: the shading launches ran beside the previous bounce's NEE traversals
+            r["shared_gpu"] = (f"{st.pipelined_batches} pipelined batch(es): the shading launches shared the GPU with "
+                               "the previous bounce's NEE traversals (the kernel alone: `solo`)")
         elif x["unit_of_work"] == "ray" and getattr(st, "trace_ahead_launches", 0):
             # MPT_TRACE_AHEAD: a bounce's path traversal ran beside the previous bounce's NEE
             # traversals, so the traversal stages' launch times overlap

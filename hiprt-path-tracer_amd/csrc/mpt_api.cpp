@@ -2319,6 +2319,13 @@ int mpt_halo_plan(int32_t res_y, int32_t band_height, int32_t band_count, int32_
     return (int)ops.size();
 }
 
+int mpt_set_pipeline(MptContext* c, int32_t mode) {
+    if (!c) return fail(MPT_ERR_INVALID_ARGUMENT, "NULL context");
+    if (mode < 0 || mode > 1) return fail(MPT_ERR_INVALID_ARGUMENT, "mode must be 0 (in line) or 1 (pipelined)");
+    c->pipeline = mode;
+    return MPT_OK;
+}
+
 int mpt_set_halo_native(MptContext* c, int32_t mode) {
     if (!c) return fail(MPT_ERR_INVALID_ARGUMENT, "NULL context");
     if (mode < 0 || mode > 2) return fail(MPT_ERR_INVALID_ARGUMENT, "mode must be 0 (off), 1 (RCCL) or 2 (rehearsal)");

@@ -29,7 +29,7 @@ SYMBOLS = [
     "mpt_render_frame", "mpt_render_frames", "mpt_synchronize", "mpt_query_done", "mpt_get_framebuffer", "mpt_partition_rows",
     "mpt_enable_stats", "mpt_get_stats", "mpt_trace_closest", "mpt_trace_any", "mpt_clear_status",
     "mpt_query_status", "mpt_get_aux_buffer", "mpt_build_envmap_cdf", "mpt_set_envmap_cdf", "mpt_set_halo_exchange",
-    "mpt_set_halo_native", "mpt_halo_plan",
+    "mpt_set_halo_native", "mpt_halo_plan", "mpt_set_pipeline",
     "mpt_bake_lut", "mpt_png_unfilter", "mpt_device_info", "mpt_gather", "mpt_comm_unique_id", "mpt_comm_init",
     "mpt_comm_gather", "mpt_jpeg_decode", "mpt_hdr_decode",
 ]
@@ -92,6 +92,7 @@ def lib() -> C.CDLL:
     L.mpt_get_aux_buffer.argtypes = [vp, C.c_int, vp, C.c_int]
     L.mpt_set_halo_exchange.argtypes = [vp, abi.HaloExchangeFn, vp]
     L.mpt_set_halo_native.argtypes = [vp, C.c_int32]
+    L.mpt_set_pipeline.argtypes = [vp, C.c_int32]
     L.mpt_halo_plan.argtypes = [i32, i32, i32, i32, i32, i32, C.POINTER(abi.HaloOp), i32]
     L.mpt_bake_lut.argtypes = [vp, C.c_int, i32, i32, i32, i32, vp, C.c_int]
     L.mpt_gather.argtypes = [C.POINTER(vp), i32, i32, C.c_int, vp, C.c_int]
@@ -261,6 +262,10 @@ class GPURenderer:
         rehearsal (timing only), 0 off."""
         self._halo_cb = None
         _check(lib().mpt_set_halo_native(self.h, int(mode)))
+
+    def set_pipeline(self, mode: int):
+        """mpt_set_pipeline: 1 the bounce pipeline of single-stream wavefronts, 0 in line."""
+        _check(lib().mpt_set_pipeline(self.h, int(mode)))
 
     # --- frames --------------------------------------------------------------------
     def render(self, frame: "abi.Frame"):

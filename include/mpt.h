@@ -629,6 +629,11 @@ int mpt_comm_gather(MptContext* ctx, int32_t root, int kind, void* dst, int dst_
  * rows keep what the buffers held -- timing only), 0 off.  Replaces mpt_set_halo_exchange's
  * callback. */
 int mpt_set_halo_native(MptContext* ctx, int32_t mode);
+/* The bounce pipeline of single-stream path-tracing wavefronts (default 1, or MPT_PIPELINE at
+ * mpt_create): 1 a bounce's NEE traversals and resolve beside the next bounce's split and shading,
+ * 0 in line.  Images are identical either way; 0 gives every kernel the GPU to itself (the bench's
+ * solo roofline).  Takes effect at the next launch; no reference counterpart (a launch schedule). */
+int mpt_set_pipeline(MptContext* ctx, int32_t mode);
 /* One point-to-point operation of a halo exchange point: `buffer`'s rows [row_lo, row_hi)
  * sent to (recv = 0) or received from (recv = 1) band `peer`. */
 typedef struct MptHaloOp {

@@ -78,3 +78,27 @@ def test_pipeline_city_band(monkeypatch, luts):
         f.render_settings.do_alpha_testing = True
     out = _render(monkeypatch, city, luts, frs, 4, env=env, modes=((0, 1), (1, 1)))
     _assert_modes_equal(out, oracle_for(city, luts, env).render(frs, aov=True), "pipeline city band")
+
+
+def test_set_pipeline_switches_between_launches(monkeypatch, luts):
+    """mpt_set_pipeline (the bench's solo timing): in line after 0, pipelined after 1, the same
+    image either way; other modes are refused."""
+    monkeypatch.setenv("MPT_OVERLAP", "0")
+    monkeypatch.delenv("MPT_PIPELINE", raising=False)
+    sd = scene.load_scene("cornell_pbr")
+    frs = frames(sd, 40, 24, 4, lss=STRATEGIES["ris"])
+    r = mpt.GPURenderer(0)
+    try:
+        r.set_scene(sd)
+        r.set_luts(luts)
+        with pytest.raises(Exception):
+            r.set_pipeline(2)
+        out = {}
+        for mode in (0, 1):
+            r.set_pipeline(mode)
+            r.enable_stats(timing=False, instrumented=False)   # (resets the counters)
+            out[mode] = gpu_render_batched(r, frs, 4)
+            assert (r.stats().pipelined_batches > 0) == bool(mode), mode
+    finally:
+        r.close()
+    _assert_modes_equal(out, oracle_for(sd, luts).render(frs, aov=True), "set_pipeline")

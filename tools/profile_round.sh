@@ -7,7 +7,7 @@ tag=$1; shift
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 out=gpurun_out/prof_$tag
 mkdir -p $out
-args="$* --no-cpu-baseline --no-parity --configs none --batch1-steps 0"
+args="$* --no-cpu-baseline --no-parity --no-solo --configs none --batch1-steps 0"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/trace -o run --output-format csv -- python3 bench.py $args > $out/trace.log 2>&1 || exit $?
 i=0
 for pmc in "FETCH_SIZE" "WRITE_SIZE" "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum" "TCC_HIT_sum TCC_MISS_sum" "SQ_INSTS_VALU SQ_WAVES GRBM_GUI_ACTIVE"; do
