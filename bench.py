@@ -252,6 +252,16 @@ def load_traffic(workload, W, H):
     return d
 
 
+def restir_band_want(a, K, want, band_count):
+    """Samples per wavefront of a ReSTIR DI band: at most half the samples, so that the run has two
+    batches and the second one's per-sample reuse chain overlaps the first one's later bounces
+    (MPT_RESTIR_OVERLAP; one band of the 8-way 1080p split at the driver's 20 steps: 1.700 ms/spp
+    in one batch of 20, 1.677 in two of 10, 1.77 in four of 5, `profiles/r06v_c4_band_batch_ab.json`)"""
+    if a.workload != "c4" or band_count <= 1 or K < 4:
+        return want
+    return min(want, K // 2)
+
+
 def emulate_restir_ranks(a, r, cam, W, H, opt, wset, alpha, n_ranks, K, device):
     """C4 scaling rehearsal on one GPU (--workload c4 --emulate-rank-of N): each rank of the
     N-way split renders ONE contiguous band with the halo exchange, so the
@@ -301,7 +311,7 @@ def emulate_restir_ranks(a, r, cam, W, H, opt, wset, alpha, n_ranks, K, device):
         rows = mpt.partition_rows(H, *band)
         if rows == 0:
             continue
-        want = a.batch or TARGET_PATHS / max(1, rows * W)
+        want = a.batch or restir_band_want(a, K, TARGET_PATHS / max(1, rows * W), n_ranks)
         batch = min((d for d in range(1, min(MAX_BATCH, K) + 1) if K % d == 0), key=lambda d: (abs(d - want), -d))
         r.enable_stats(timing=False, instrumented=False)
         r.render_samples(frames_for(cam, W, H, opt, (1, 0, 1), 2, bounces=a.bounces, world=wset, alpha=alpha))
@@ -481,7 +491,7 @@ def run_workload(a, world, rank, local, dist, coll_dev, quiet=False):
         while K % batch:                                 # whole batches in the timed region
             batch -= 1
     else:   # the divisor of K nearest to TARGET_PATHS / the rank's pixels
-        want = TARGET_PATHS / max(1, rows_rank * W)
+        want = restir_band_want(a, K, TARGET_PATHS / max(1, rows_rank * W), band[2])
         batch = min((d for d in range(1, min(MAX_BATCH, K) + 1) if K % d == 0), key=lambda d: (abs(d - want), -d))
 
     r = mpt.GPURenderer(local)
