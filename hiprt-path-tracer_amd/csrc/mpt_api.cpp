@@ -452,6 +452,7 @@ struct Allocs {
 // compacted query entries (16), occlusion bytes (4), 6 queues (24), rng (4), seeds (8), hit_inside,
 // qmask, active (3).  Textured scenes add a resolved material per slot.
 constexpr size_t OVERLAP_AUTO_PATHS = (size_t)24 << 20;   // MPT_OVERLAP=-1: overlapped halves up to this many paths
+constexpr size_t PIPELINE_PREFER_TRIS = (size_t)1 << 20;   // ... unless the scene has this many triangles (launch_batch)
 constexpr size_t PATH_BYTES = 9 * 16 + 32 + 7 * 16 + 128 + 16 + 4 + 24 + 4 + 8 + 3;
 // + the bounce pipeline's alternate set per slot (set_pipe): 7 NEE planes, 4 staged query rays,
 // 2 col additions (16 B each ... 64 B), 4 query list entries, 2 shaded-list entries
@@ -1668,8 +1669,14 @@ static int launch_batch(MptContext* c, const MptFrame* f, int batch) {
         P.rs_hi = std::min(f->res_y, cfg.own_y1 + cfg.halo_prev) * f->res_x;
     }
     // (auto: small wavefronts, or many bounces -- the later bounces' short lists are tails too:
-    // C5 at 4K and 16 bounces 8.93 -> 8.67 ms/spp, profiles/r05v_c5_overlap_ab.jsonl)
-    const bool ovl_auto = (size_t)batch * (size_t)std::max(c->n_slots, 1) <= OVERLAP_AUTO_PATHS ||
+    // C5 at 4K and 16 bounces 8.93 -> 8.67 ms/spp, profiles/r05v_c5_overlap_ab.jsonl; but a
+    // traversal-heavy scene's small wavefront gains more from the bounce pipeline, which needs the
+    // single stream: one rank of the 8 / 4 / 2-way C3 split at 20 steps 0.597 / 1.083 / 2.033 ->
+    // 0.584 / 1.065 / 2.016 ms/spp, while Cornell C1 / C2 and C5 keep the halves, 0.5-1.2 % better
+    // there, profiles/r06x_rank_share_pipeline_ab.json, r06y_configs_halves_vs_pipeline_ab.json)
+    const bool pipe_first = c->pipeline && !c->shade_split && c->mat_idx.n >= PIPELINE_PREFER_TRIS &&
+                            f->render_settings.nb_bounces > 0;
+    const bool ovl_auto = ((size_t)batch * (size_t)std::max(c->n_slots, 1) <= OVERLAP_AUTO_PATHS && !pipe_first) ||
                           f->render_settings.nb_bounces >= 8;
     const bool ovl = (c->overlap > 0 || (c->overlap < 0 && ovl_auto)) && batch >= 2 &&
                      f->options.direct_light_sampling != MPT_LSS_RESTIR_DI && c->x_per == 0 && !P.spec_as;
