@@ -57,7 +57,7 @@ HBM_PEAK_GBS = 8000.0
 VALU_PEAK = 256 * 4 * 2.4e9 / 2    # wave64 VALU instructions / s (MI355X_MICROARCH.md: 2 cycles per wave instruction)
 S_NODE, S_TRI = 80, 48
 BAND_H = 8
-TARGET_PATHS = 16 * 1920 * 1080  # paths per wavefront launch (mpt_render_frames batch x rank pixels)
+TARGET_PATHS = 64 * 1920 * 1080  # paths per wavefront launch (mpt_render_frames batch x rank pixels)
 MAX_BATCH = 128    # MPT_MAX_BATCH
 
 
