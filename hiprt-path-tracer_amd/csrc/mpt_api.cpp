@@ -221,7 +221,8 @@ struct MptContext {
     DBuf<int32_t> nq_tgt2, qh2, qf2;
     int pipeline = 1;
     size_t pipe_n = 0;
-    hipEvent_t ev_nee[2] = {nullptr, nullptr};
+    hipEvent_t ev_nee[4] = {nullptr, nullptr, nullptr, nullptr};   // fork / join per NEE stream
+    int pix_pipe = 1;   // MPT_PIX_PIPE: a one-sample frame as 2 row parts, each pipelined
     DBuf<float> fb_color, fb_albedo, fb_normal;
     DBuf<int32_t> as_count, as_conv;
     DBuf<float> as_sqlum;
@@ -1016,6 +1017,7 @@ int mpt_create(int device, void* hip_stream, MptContext** out) {
     if (const char* e = std::getenv("MPT_RESTIR_SIDE")) c->restir_side = std::atoi(e);
     if (const char* e = std::getenv("MPT_TRACE_AHEAD")) c->trace_ahead = std::atoi(e);
     if (const char* e = std::getenv("MPT_PIPELINE")) c->pipeline = std::atoi(e);
+    if (const char* e = std::getenv("MPT_PIX_PIPE")) c->pix_pipe = std::atoi(e);
     if (const char* e = std::getenv("MPT_OVERLAP_AHEAD")) c->ovl_ahead = std::atoi(e);
     if (const char* e = std::getenv("MPT_RESTIR_MAX_BATCH"))
         c->restir_max_batch = std::max(1, std::min(RESTIR_MAX_BATCH, std::atoi(e)));
@@ -1066,8 +1068,9 @@ int mpt_destroy(MptContext* c) {
         if (c->ev_side[k]) (void)hipEventDestroy(c->ev_side[k]);
         if (c->ev_ahead[k]) (void)hipEventDestroy(c->ev_ahead[k]);
         if (c->ev_ahead2[k]) (void)hipEventDestroy(c->ev_ahead2[k]);
-        if (c->ev_nee[k]) (void)hipEventDestroy(c->ev_nee[k]);
     }
+    for (hipEvent_t e : c->ev_nee)
+        if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : {c->ev_fork, c->ev_first, c->ev_acc, c->ev_join, c->ev_chain, c->ev_half[0], c->ev_half[1],
                          c->ev_wave_join})
         if (e) (void)hipEventDestroy(e);
@@ -1520,12 +1523,18 @@ static int set_ahead(MptContext* c, LaunchCfg& cfg, const MptFrame& f, int which
 
 // The bounce pipeline of a single-stream wavefront (LaunchCfg::pipe_alt, frame_bounces): the
 // alternate plane set for the path slots the context holds (allocated on first use; a failure to
-// allocate leaves the wavefront in line), its view `alt` of P, the NEE stream (streamx[0]), its
-// spill area and events.  P.ce is set: the shading hands its col additions to k_resolve.
-static int set_pipe(MptContext* c, LaunchCfg& cfg, const MptFrame& f, DevPaths& P, DevPaths& alt) {
-    if (!c->pipeline || f.options.direct_light_sampling == MPT_LSS_RESTIR_DI || c->x_per != 0 || c->shade_split ||
-        f.render_settings.nb_bounces <= 0)
-        return MPT_OK;
+// allocate leaves the wavefront in line), its view `alt` of P, the NEE stream, its spill area and
+// events.  P.ce is set: the shading hands its col additions to k_resolve.  `part` k of a
+// pipelined one-sample frame in row parts (launch_batch, MPT_PIX_PIPE) takes NEE stream streamx[k]
+// and the alternate counter set part + 2 (P: the part's slots, counters part; alt from the
+// context's planes at the same slot offset `off`).
+static bool pipe_applies(const MptContext* c, const MptFrame& f) {
+    return c->pipeline && f.options.direct_light_sampling != MPT_LSS_RESTIR_DI && c->x_per == 0 && !c->shade_split &&
+           f.render_settings.nb_bounces > 0;
+}
+static int set_pipe(MptContext* c, LaunchCfg& cfg, const MptFrame& f, DevPaths& P, DevPaths& alt, int part = -1,
+                    size_t off = 0) {
+    if (!pipe_applies(c, f)) return MPT_OK;
     const size_t N = (size_t)std::max(c->n_slots, 1) * (size_t)c->batch_cap;
     if (c->pipe_n != N) {
         HIPCHK(drain(c));
@@ -1542,21 +1551,27 @@ static int set_pipe(MptContext* c, LaunchCfg& cfg, const MptFrame& f, DevPaths& 
         }
         c->pipe_n = N;
     }
-    int rr = ensure_pix_parts(c, 4);   // (streamx[0] and its spill area)
+    int rr = ensure_pix_parts(c, 4);   // (streamx[0], streamx[1] and their spill areas)
     if (rr != MPT_OK) return rr;
     for (hipEvent_t& ev : c->ev_nee)
         if (!ev) HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-    P.ce = c->ce.p;
+    const int k = std::max(part, 0);
+    P.ce = c->ce.p + off;
     alt = P;
     alt.nthr = c->nthr2.p; alt.na = c->na2.p; alt.nb = c->nb2.p; alt.ndir = c->ndir2.p; alt.nris = c->nris2.p;
     alt.ne1 = c->ne12.p; alt.ne2 = c->ne22.p; alt.nq_o = c->nq_o2.p; alt.nq_d = c->nq_d2.p; alt.nq_tgt = c->nq_tgt2.p;
     alt.qh = c->qh2.p; alt.qf = c->qf2.p; alt.ce = c->ce2.p;
-    alt.counters = P.counters + CTR_COUNT;   // (the queue counters are always taken from P)
+    if (off) {   // the part's slots of the alternate planes (as offset_slots does for P's)
+        alt.nthr += off; alt.na += off; alt.nb += off; alt.ndir += off; alt.nris += off; alt.ne1 += off; alt.ne2 += off;
+        alt.nq_o += off; alt.nq_d += off; alt.nq_tgt += 4 * off; alt.qh += off; alt.qf += off; alt.ce += off;
+    }
+    // (the queue counters are always taken from P)
+    alt.counters = part < 0 ? P.counters + CTR_COUNT : P.counters + 2 * CTR_COUNT;
     cfg.pipe_alt = &alt;
-    cfg.nee_stream = c->streamx[0];
-    cfg.nee_spill = c->spillx[0].p;
-    cfg.ev_nee_fork = c->ev_nee[0];
-    cfg.ev_nee_join = c->ev_nee[1];
+    cfg.nee_stream = c->streamx[k];
+    cfg.nee_spill = c->spillx[k].p;
+    cfg.ev_nee_fork = c->ev_nee[2 * k];
+    cfg.ev_nee_join = c->ev_nee[2 * k + 1];
     return MPT_OK;
 }
 
@@ -1574,7 +1589,10 @@ static int launch_batch(MptContext* c, const MptFrame* f, int batch) {
     // streams: every pixel's path is independent and its accumulation touches only its own pixel,
     // so the halves need no ordering, and one half's kernels fill the other's launch tails (each
     // of the ~50 dependent launches of a sample otherwise drains the GPU before the next starts)
-    const int parts = std::min(std::max(c->pix_parts, 1), std::min(PIX_PARTS_MAX, f->res_y));
+    // (MPT_PIX_PIPE: two parts, each pipelined, where the bounce pipeline applies -- batch-1 C3 5.24 ->
+    // 5.15 ms/spp against three parts in line, profiles/r06an_batch1_pix_pipe_ab.json)
+    const int parts_set = c->pix_pipe && pipe_applies(c, *f) ? std::min(c->pix_parts, 2) : c->pix_parts;
+    const int parts = std::min(std::max(parts_set, 1), std::min(PIX_PARTS_MAX, f->res_y));
     const bool pix_ovl = parts > 1 && batch == 1 && f->band_count == 1 && c->n_slots >= (1 << 16) &&
                          f->options.direct_light_sampling != MPT_LSS_RESTIR_DI && c->x_per == 0 &&
                          !(c->graphs && !c->timing);
@@ -1689,6 +1707,9 @@ static int launch_batch(MptContext* c, const MptFrame* f, int batch) {
         HIPCHK(hipEventRecord(c->ev_fork, c->stream));
         LaunchCfg cur = cfg;
         int launches = 0;
+        // MPT_PIX_PIPE: two parts, each with the bounce pipeline (its NEE work on streamx[k])
+        const bool part_pipe = c->pix_pipe && parts == 2 && pipe_applies(c, *f);
+        DevPaths alts[2];
         for (int k = 0; k < parts && e == hipSuccess; k++) {
             const size_t r0 = std::min((size_t)f->res_y, (size_t)k * hp), r1 = std::min((size_t)f->res_y, (size_t)(k + 1) * hp);
             const size_t off = r0 * (size_t)f->res_x, n = (r1 - r0) * (size_t)f->res_x;
@@ -1704,6 +1725,13 @@ static int launch_batch(MptContext* c, const MptFrame* f, int batch) {
             }
             hipStream_t sk = k == 0 ? c->stream : k == 1 ? c->stream2 : c->streamx[k - 2];
             if (k > 0) HIPCHK(hipStreamWaitEvent(sk, c->ev_fork, 0));
+            cur.pipe_alt = nullptr;
+            cur.nee_stream = nullptr;
+            if (part_pipe) {
+                int rr2 = set_pipe(c, cur, *f, Pk, alts[k], k, k > 0 ? off : 0);
+                if (rr2 != MPT_OK) return rr2;
+                if (cur.pipe_alt) c->pipelined_batches++;
+            }
             cur.launches = 0;
             e = launch_frame(dev_scene(c), Pk, c->d_frames + slot + k, k == 0 ? f[0] : c->h_frames[slot + k], cur, sk);
             launches += cur.launches;

@@ -382,6 +382,7 @@ inline void offset_slots(DevPaths& P, size_t off) {
     P.nq_o += off; P.nq_d += off; P.occ += off; P.nq_tgt += 4 * off;
     P.nhit += off; P.s_gn += off; P.qmask += off; P.active += off;
     if (P.mat_slot) P.mat_slot += off;
+    if (P.ce) P.ce += off;
 }
 
 hipError_t launch_frame(const DevScene& S, const DevPaths& P, const MptFrame* d_frame, const MptFrame& h_frame,

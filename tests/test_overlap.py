@@ -55,5 +55,6 @@ def test_pixel_parts_one_sample_frames(monkeypatch, luts, case):
     if case == "low_res":
         frs[2].render_settings.wants_render_low_resolution = True
         frs[2].render_settings.render_low_resolution_scaling = 2
+    monkeypatch.setenv("MPT_PIX_PIPE", "0")   # (the parts in line; pipelined parts: tests/test_pipeline.py)
     out = _render_modes(monkeypatch, sd, luts, frs, env=env, var="MPT_PIX_PARTS", modes=(0, 2, 3, 4))
     _assert_modes_equal(out, oracle_for(sd, luts, env).render(frs, aov=True), f"pixel parts {case}")

@@ -14,7 +14,7 @@ import pytest
 import mpt
 from mpt import abi, scene
 
-from test_gpu_parity import STRATEGIES, frames, gpu_render_batched, oracle_for
+from test_gpu_parity import STRATEGIES, frames, gpu_render, gpu_render_batched, oracle_for
 from test_shade_classes import _assert_modes_equal
 
 pytestmark = pytest.mark.gpu
@@ -102,3 +102,40 @@ def test_set_pipeline_switches_between_launches(monkeypatch, luts):
     finally:
         r.close()
     _assert_modes_equal(out, oracle_for(sd, luts).render(frs, aov=True), "set_pipeline")
+
+
+@pytest.mark.parametrize("case", ["mis", "ris_adaptive", "low_res", "envmap_odd_rows"])
+def test_pipelined_pixel_parts(monkeypatch, luts, case):
+    """One-sample frames as 2 row parts, each with the bounce pipeline (MPT_PIX_PIPE: part k's NEE
+    work on its own stream, over its rows of the alternate planes and counter set k + 2):
+    bit-exact against one stream and the oracle."""
+    sd = scene.load_scene("cornell_pbr")
+    lss = STRATEGIES["ris"] if case == "ris_adaptive" else STRATEGIES["mis"]
+    env = mpt.build_envmap(scene.procedural_sky(128, 64, seed=7)) if case.startswith("envmap") else None
+    w, h = (256, 257) if case == "envmap_odd_rows" else (320, 206)
+    frs = frames(sd, w, h, 4, lss=lss, world=scene.envmap_world(1.0) if env is not None else None)
+    if case == "ris_adaptive":
+        for f in frs:
+            f.render_settings.enable_adaptive_sampling = True
+            f.render_settings.adaptive_sampling_min_samples = 1
+            f.render_settings.adaptive_sampling_noise_threshold = 0.9
+    if case == "low_res":
+        frs[2].render_settings.wants_render_low_resolution = True
+        frs[2].render_settings.render_low_resolution_scaling = 2
+    out = {}
+    for parts, pipe in ((0, 0), (2, 1)):
+        monkeypatch.setenv("MPT_PIX_PARTS", str(parts))
+        monkeypatch.setenv("MPT_PIX_PIPE", str(pipe))
+        monkeypatch.setenv("MPT_PIPELINE", str(pipe))
+        r = mpt.GPURenderer(0)
+        try:
+            r.set_scene(sd)
+            r.set_luts(luts)
+            if env is not None:
+                r.set_envmap(env)
+            r.enable_stats(timing=False, instrumented=False)
+            out[(parts, pipe)] = gpu_render(r, frs)
+            assert (r.stats().pipelined_batches > 0) == bool(pipe), (parts, pipe)
+        finally:
+            r.close()
+    _assert_modes_equal(out, oracle_for(sd, luts, env).render(frs, aov=True), f"pipelined pixel parts {case}")
