@@ -60,9 +60,10 @@ BAND_H = 8
 TARGET_PATHS = 64 * 1920 * 1080  # paths per wavefront launch (mpt_render_frames batch x rank pixels)
 # ReSTIR DI (C4): smaller wavefronts, so that each batch's later bounces overlap the next batch's
 # per-sample reuse chain (C4 at 64 steps: batch 16 / 32 / 64 -> 8.09-8.12 / 8.17 / 8.33 ms/spp,
-# profiles/r06ae_c4_batch_ab.json; the path-tracing configs gain from larger ones: C3 16 / 32 / 64 ->
+# profiles/r06ae_c4_batch_ab.json; at 32 steps 8 / 16 -> 8.10 / 8.22, at 8 steps 4 / 8 -> 8.44 / 8.56,
+# r06as_c4_batch_ab.json; the path-tracing configs gain from larger ones: C3 16 / 32 / 64 ->
 # 3.92 / 3.86 / 3.77, profiles/r06ab_c3_batch_ab.json)
-TARGET_PATHS_RESTIR = 16 * 1920 * 1080
+TARGET_PATHS_RESTIR = 8 * 1920 * 1080
 MAX_BATCH = 128    # MPT_MAX_BATCH
 
 
@@ -258,15 +259,15 @@ def load_traffic(workload, W, H):
 
 
 def restir_band_want(a, K, want, band_count):
-    """Samples per wavefront under ReSTIR DI: TARGET_PATHS_RESTIR paths, and on a band at most half
-    the samples, so that the run has two
+    """Samples per wavefront under ReSTIR DI: TARGET_PATHS_RESTIR paths and at most half the
+    samples, so that the run has at least two
     batches and the second one's per-sample reuse chain overlaps the first one's later bounces
     (MPT_RESTIR_OVERLAP; one band of the 8-way 1080p split at the driver's 20 steps: 1.700 ms/spp
     in one batch of 20, 1.677 in two of 10, 1.77 in four of 5, `profiles/r06v_c4_band_batch_ab.json`)"""
     if a.workload != "c4":
         return want
     want = want * TARGET_PATHS_RESTIR / TARGET_PATHS
-    if band_count <= 1 or K < 4:
+    if K < 4:
         return want
     return min(want, K // 2)
 
