@@ -139,3 +139,14 @@ def test_pipelined_pixel_parts(monkeypatch, luts, case):
         finally:
             r.close()
     _assert_modes_equal(out, oracle_for(sd, luts, env).render(frs, aov=True), f"pipelined pixel parts {case}")
+
+
+@pytest.mark.parametrize("strategy,ovr", [("none", abi.BSDF_NONE), ("uniform", abi.BSDF_NONE), ("bsdf", abi.BSDF_NONE),
+                                          ("mis", abi.BSDF_LAMBERTIAN), ("ris", abi.BSDF_OREN_NAYAR)])
+def test_pipeline_strategies_and_overrides(monkeypatch, luts, strategy, ovr):
+    """Every light-sampling strategy (no direct light sampling: the emission handed to the resolve
+    with nothing else to add) and the Lambert / Oren-Nayar override kernels, pipelined vs in line."""
+    sd = scene.load_scene("cornell_pbr")
+    frs = frames(sd, 40, 24, 4, ovr=ovr, lss=STRATEGIES[strategy], bounces=4)
+    out = _render(monkeypatch, sd, luts, frs, 2, modes=((0, 1), (1, 1)))
+    _assert_modes_equal(out, oracle_for(sd, luts).render(frs, aov=True), f"pipeline {strategy} override {ovr}")
