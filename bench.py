@@ -852,6 +852,12 @@ def run_workload(a, world, rank, local, dist, coll_dev, quiet=False):
         }
         if batch1 is not None:
             out["batch1"] = batch1
+        if st.pipelined_batches or st.trace_ahead_launches:
+            # kernels on several streams: an event pair spans the wait for CUs held by the other
+            # stream's kernels (k_split starts beside the persistent NEE traversal), so the entries
+            # overlap and their sum exceeds frame_gpu
+            out["kernel_ms_note"] = ("pipelined / trace-ahead frames: per-kernel event spans overlap and include the "
+                                     "wait for CUs held by the other streams' kernels; frame_gpu is the frame's own span")
         if band[2] > world:
             out["emulated_rank_of"] = band[2]
             out["msample_per_s"] = round(rows * W * K / elapsed / 1e6, 3)
