@@ -1692,10 +1692,13 @@ static int launch_batch(MptContext* c, const MptFrame* f, int batch) {
     // single stream: one rank of the 8 / 4 / 2-way C3 split at 20 steps 0.597 / 1.083 / 2.033 ->
     // 0.584 / 1.065 / 2.016 ms/spp, while Cornell C1 / C2 and C5 keep the halves, 0.5-1.2 % better
     // there, profiles/r06x_rank_share_pipeline_ab.json, r06y_configs_halves_vs_pipeline_ab.json)
-    const bool pipe_first = c->pipeline && !c->shade_split && c->mat_idx.n >= PIPELINE_PREFER_TRIS &&
-                            f->render_settings.nb_bounces > 0;
+    // A large many-bounce wavefront, too, is faster in one stream with the pipeline: C5 (4K, 16
+    // bounces) in 8 / 16-sample wavefronts 8.21-8.37 / 7.88-7.94 ms/spp as halves, 8.14-8.19 /
+    // 7.81-7.84 pipelined (profiles/r06az_c5_halves_vs_pipeline_ab.json, r06al_*)
+    const bool pipe_ok = c->pipeline && !c->shade_split && f->render_settings.nb_bounces > 0;
+    const bool pipe_first = pipe_ok && c->mat_idx.n >= PIPELINE_PREFER_TRIS;
     const bool ovl_auto = ((size_t)batch * (size_t)std::max(c->n_slots, 1) <= OVERLAP_AUTO_PATHS && !pipe_first) ||
-                          f->render_settings.nb_bounces >= 8;
+                          (f->render_settings.nb_bounces >= 8 && !pipe_ok);
     const bool ovl = (c->overlap > 0 || (c->overlap < 0 && ovl_auto)) && batch >= 2 &&
                      f->options.direct_light_sampling != MPT_LSS_RESTIR_DI && c->x_per == 0 && !P.spec_as;
     hipError_t e = hipSuccess;
